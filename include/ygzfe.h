@@ -1,0 +1,226 @@
+/*
+ * ygzfe.h — C ABI of the MI355X (gfx950) front-end for ORB-YGZ-SLAM.
+ *
+ * The drop-in boundary of the per-frame hot path: ORB extraction
+ * (ORBextractor), Hamming matching (ORBmatcher) and direct alignment
+ * (SparseImgAlign, Align2D / FindDirectProjection).  Plain C types only; every
+ * entry point names the reference interface it replaces (paths relative to the
+ * Ewenwan/ORB-YGZ-SLAM checkout).  INTEGRATION.md shows the C++ adapter
+ * (orb-ygz-slam_amd/compat/) that keeps the reference's class signatures so
+ * Tracking.cc compiles unchanged.
+ *
+ * Conventions
+ *  - Return value: YGZFE_OK (0) or a negative YGZFE_E* code; ygzfe_last_error()
+ *    gives a thread-local message.  The reference never throws; the adapter maps
+ *    codes to its "empty result / 0 / false" conventions.
+ *  - Host pointers unless the name says `d_` (device pointer, HIP memory of the
+ *    handle's device).  `stream` is a hipStream_t passed as void* (NULL = the
+ *    handle's own stream).
+ *  - Handles are thread-safe across handles, not re-entrant per handle
+ *    (the reference extractor is stateful: mvImagePyramid, mnGridSize).
+ *  - Results are bit-exact with oracle/ (the CPU restatement) for keypoints and
+ *    descriptors; SparseImgAlign poses agree within 1e-4.
+ */
+#ifndef YGZFE_H_
+#define YGZFE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YGZFE_OK 0
+#define YGZFE_EINVAL (-1)   /* bad argument / shape */
+#define YGZFE_EHIP (-2)     /* HIP runtime failure (no device, launch error) */
+#define YGZFE_ECAP (-3)     /* caller buffer too small; *n_out holds the size needed */
+#define YGZFE_ENOMEM (-4)
+#define YGZFE_ESTATE (-5)   /* call order violated (e.g. extract before pyramid) */
+
+#define YGZFE_MAX_LEVELS 16
+
+/* Same 28-byte layout as cv::KeyPoint {Point2f pt; float size, angle, response;
+ * int octave, class_id} so std::vector<cv::KeyPoint>::data() passes straight. */
+typedef struct ygzfe_kp {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} ygzfe_kp;
+
+/* ORBextractor::KeyPointMethod (ORBextractor.h:49-51). */
+enum ygzfe_method { YGZFE_ORBSLAM_KEYPOINT = 0, YGZFE_FAST_KEYPOINT = 1, YGZFE_DSO_KEYPOINT = 2 };
+
+/* GaussianBlur 7x7 sigma 2 kernel variant: OpenCV >= 3.4.2
+ * bit-exact fixed point [18,34,48,56,...] or OpenCV 2.4/3.x cvRound [18,34,49,55,...]. */
+enum ygzfe_blur { YGZFE_BLUR_CV4 = 0, YGZFE_BLUR_CV3 = 1 };
+
+/* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST,
+ * int minThFAST) (ORBextractor.h:53-57, Tracking.cc:255-261). */
+typedef struct ygzfe_orb_params {
+    int32_t nfeatures;
+    float scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+    int32_t blur_variant;
+} ygzfe_orb_params;
+
+typedef struct ygzfe_camera { float fx, fy, cx, cy; } ygzfe_camera;   /* Frame::fx.. (Frame.h:178-183) */
+typedef struct ygzfe_se3 { float q[4]; float t[3]; } ygzfe_se3;        /* Sophus SE3f: quat (x,y,z,w) + t */
+
+const char *ygzfe_last_error(void);
+int ygzfe_device_count(void);
+
+/* ------------------------------------------------------------------------ */
+/* ORBextractor (ORBextractor.h:37-192)                                     */
+typedef struct ygzfe_extractor ygzfe_extractor;
+/* A device-resident frame pyramid: Frame::mvImagePyramid (Frame.h, Frame.cc:807-813). */
+typedef struct ygzfe_frame ygzfe_frame;
+
+/* ORBextractor::ORBextractor (ORBextractor.cc:412-470). */
+int ygzfe_extractor_create(const ygzfe_orb_params *p, int device, ygzfe_extractor **out);
+void ygzfe_extractor_destroy(ygzfe_extractor *ex);
+/* GetLevels / GetScaleFactor / GetScaleFactors / GetInverseScaleFactors /
+ * GetScaleSigmaSquares / GetInverseScaleSigmaSquares (ORBextractor.h:87-109).
+ * Any output pointer may be NULL; arrays hold nlevels floats. */
+int ygzfe_extractor_levels(const ygzfe_extractor *ex, int *nlevels, float *scale,
+                           float *inv_scale, float *sigma2, float *inv_sigma2);
+/* mnFeaturesPerLevel (ORBextractor.cc:434-445). */
+int ygzfe_extractor_features_per_level(const ygzfe_extractor *ex, int32_t *out);
+/* DSO grid state mnGridSize (ORBextractor.h:191): get / set (-1 = recompute). */
+int ygzfe_extractor_dso_grid(ygzfe_extractor *ex, int32_t *get, const int32_t *set);
+
+int ygzfe_frame_create(ygzfe_extractor *ex, int width, int height, ygzfe_frame **out);
+void ygzfe_frame_destroy(ygzfe_frame *f);
+/* Frame::ComputeImagePyramid -> ORBextractor::ComputePyramid
+ * (Frame.cc:807-813, ORBextractor.cc:1129-1150): H2D of the image + pyramid. */
+int ygzfe_compute_pyramid(ygzfe_extractor *ex, ygzfe_frame *f, const uint8_t *img, int stride);
+/* Same from an image already in device memory. */
+int ygzfe_compute_pyramid_device(ygzfe_extractor *ex, ygzfe_frame *f, const uint8_t *d_img,
+                                 int stride, void *stream);
+/* Host mirror of mvImagePyramid[level] (read at Frame.cc:515,604,618). */
+int ygzfe_frame_level(const ygzfe_frame *f, int level, int *w, int *h, uint8_t *dst, int dst_stride);
+/* Upload a whole host pyramid (e.g. a Frame deep-copied from elsewhere). */
+int ygzfe_frame_set_level(ygzfe_frame *f, int level, const uint8_t *src, int src_stride);
+
+/* ORBextractor::operator()(Frame*, keypoints, descriptors, method, leftEye=true)
+ * (ORBextractor.cc:1031-1127, called from Frame::ExtractORB Frame.cc:332-348).
+ * `kps_io` holds n_existing keypoints (Frame::mvKeys, level-0 coordinates) on
+ * entry; on return it holds existing + new keypoints (*n_out rows) and
+ * `desc` holds *n_out x 32 descriptor bytes (rows 0..n_existing-1 = existing).
+ * DSO mode recomputes the existing keypoints' angles (ORBextractor.cc:1383-1385).
+ * cap = capacity of kps_io / desc in rows. */
+int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps_io,
+                  int n_existing, int cap, uint8_t *desc, int *n_out);
+/* ORBextractor::operator()(InputArray image, mask, keypoints, descriptors)
+ * (ORBextractor.cc:970-1028): pyramid + octree extraction of one image. */
+int ygzfe_detect_and_compute(ygzfe_extractor *ex, ygzfe_frame *f, const uint8_t *img, int stride,
+                             ygzfe_kp *kps, int cap, uint8_t *desc, int *n_out);
+
+/* ------------------------------------------------------------------------ */
+/* Batched extraction: many frames resident in HBM, one launch per stage.    */
+typedef struct ygzfe_batch ygzfe_batch;
+int ygzfe_batch_create(const ygzfe_orb_params *p, int device, int width, int height,
+                       int max_frames, ygzfe_batch **out);
+void ygzfe_batch_destroy(ygzfe_batch *b);
+/* Geometry: frame_pitch = bytes of one frame pyramid (frame i level 0 starts at
+ * d_frames + i * frame_pitch, stride width), kp_cap = keypoint rows per frame. */
+int ygzfe_batch_info(ygzfe_batch *b, size_t *frame_pitch, int *kp_cap, int *nlevels);
+/* Device buffer the frame pyramids live in (max_frames x frame_pitch bytes). */
+int ygzfe_batch_frames(ygzfe_batch *b, uint8_t **d_frames);
+/* Use caller-owned device buffers instead (any may be NULL = keep): pyramids
+ * [max_frames * frame_pitch], kps [max_frames * kp_cap], desc
+ * [max_frames * kp_cap * 32], counts [max_frames]. */
+int ygzfe_batch_bind_buffers(ygzfe_batch *b, uint8_t *d_pyramids, ygzfe_kp *d_kps, uint8_t *d_desc,
+                             int32_t *d_counts);
+/* H2D of n_frames tight width x height images into the level-0 slots. */
+int ygzfe_batch_upload(ygzfe_batch *b, const uint8_t *frames, int n_frames);
+/* Pyramid + FAST + octree + orientation + blur + rBRIEF on frames [0, n). */
+int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream);
+/* Synchronise and report kernel-side errors (octree pool overflow). */
+int ygzfe_batch_check(ygzfe_batch *b);
+/* Dense best/second-best Hamming of frame qframe[p] against tframe[p] for each
+ * pair p; outputs [n_pairs][kp_cap] (device pointers). */
+int ygzfe_batch_match(ygzfe_batch *b, int n_pairs, const int32_t *d_qframe, const int32_t *d_tframe,
+                      int32_t *d_best_idx, int32_t *d_best_dist, int32_t *d_second_dist, void *stream);
+/* Results of frame i (same rows as ygzfe_extract with no existing keypoints). */
+int ygzfe_batch_result(ygzfe_batch *b, int frame, ygzfe_kp *kps, int cap, uint8_t *desc, int *n_out);
+/* Device views: kps [max_frames][kp_cap], desc [max_frames][kp_cap][32], counts [max_frames]. */
+int ygzfe_batch_device_results(ygzfe_batch *b, ygzfe_kp **d_kps, uint8_t **d_desc,
+                               int32_t **d_counts, int *kp_cap);
+/* Per-frame pyramid level view of the batch (device pointer + stride). */
+int ygzfe_batch_level(ygzfe_batch *b, int frame, int level, const uint8_t **d_level, int *w,
+                      int *h, int *stride);
+/* Kernel timing (hipEvents around each stage launch on the batch stream).
+ * enable != 0 turns it on; ms[] receives per-stage milliseconds of the last
+ * ygzfe_batch_extract; names[] the stage names. Returns stage count. */
+int ygzfe_batch_timing(ygzfe_batch *b, int enable, float *ms, const char **names, int cap);
+void *ygzfe_batch_stream(ygzfe_batch *b);
+
+/* ------------------------------------------------------------------------ */
+/* ORBmatcher (ORBmatcher.h:38-178)                                          */
+/* ORBmatcher::DescriptorDistance (ORBmatcher.cc:1507-1523), host scalar. */
+int ygzfe_descriptor_distance(const uint8_t *a, const uint8_t *b);
+/* Dense best / second-best Hamming search (the inner loops of
+ * ORBmatcher::SearchByProjection / SearchForInitialization /
+ * SearchByBoW, ORBmatcher.cc:43-126,375-478,1218-1350): for each query, the
+ * smallest distance (strict <, first train index wins), its index and the
+ * second-smallest distance (257 when absent).  Device pointers. */
+int ygzfe_hamming_best2_device(const uint8_t *d_query, int nq, const uint8_t *d_train, int nt,
+                               int32_t *d_best_idx, int32_t *d_best_dist, int32_t *d_second_dist,
+                               void *stream);
+/* Same on host buffers (H2D / D2H on an internal stream of `device`). */
+int ygzfe_hamming_best2(int device, const uint8_t *query, int nq, const uint8_t *train, int nt,
+                        int32_t *best_idx, int32_t *best_dist, int32_t *second_dist);
+/* Windowed search (Frame::GetFeaturesInArea candidate lists, Frame.cc:424-481):
+ * CSR candidates; writes the distance of every (query, candidate) pair so the
+ * caller replays the reference's sequential assignment rules exactly. */
+int ygzfe_hamming_csr(int device, const uint8_t *query, int nq, const uint8_t *train, int nt,
+                      const int32_t *row_ptr, const int32_t *cand, int32_t *dist_out);
+
+/* ------------------------------------------------------------------------ */
+/* SparseImgAlign (SparseImageAlign.h:37-60)                                 */
+typedef struct ygzfe_align_result {
+    ygzfe_se3 T_cur_ref;   /* TCR */
+    int32_t n_visible;     /* run() return value: n_meas_/16 */
+    float chi2;            /* chi2_ at exit */
+    float H[36];           /* H_ of the last linearisation (getFisherInformation() = H/(5e-4*255^2)) */
+} ygzfe_align_result;
+/* SparseImgAlign(n_levels=max_level, min_level, n_iter=10).run(ref, cur, TCR)
+ * (SparseImageAlign.cc:20-49, Tracking.cc:2145-2189).  kps = ref Frame::mvKeys
+ * (level-0 px), xyz_ref[3n] = T_ref * MapPoint::GetWorldPos(), usable[n] = map
+ * point present && !isBad && !outlier.  T_io: in = T_cur * T_ref^-1 guess,
+ * out = TCR.  Returns YGZFE_OK; result->n_visible = run()'s return. */
+int ygzfe_sparse_align(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam,
+                       const ygzfe_kp *kps, const float *xyz_ref, const uint8_t *usable, int n,
+                       int max_level, int min_level, const ygzfe_se3 *T_init,
+                       ygzfe_align_result *result);
+
+/* Batched: pair p aligns frame ref_idx[p] -> cur_idx[p] of a batch, with the
+ * ref frame's batch keypoints (level-0 px); d_xyz_ref [n_pairs][kp_cap][3] and
+ * d_usable [n_pairs][kp_cap] per ref keypoint row, d_T_init / d_out [n_pairs]. */
+int ygzfe_batch_sparse_align(ygzfe_batch *b, int n_pairs, const int32_t *d_ref_idx,
+                             const int32_t *d_cur_idx, const float *d_xyz_ref, const uint8_t *d_usable,
+                             const ygzfe_camera *cam, int max_level, int min_level,
+                             const ygzfe_se3 *d_T_init, ygzfe_align_result *d_out, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* Align2D / FindDirectProjection (Align.h:20-26, ORBmatcher.cc:1573-1602)   */
+/* Align2D(cur_img, ref_patch_with_border 10x10, ref_patch 8x8, n_iter, px)
+ * for n independent patches on one level of `cur`; px_io in/out (level px). */
+int ygzfe_align2d_batch(const ygzfe_frame *cur, int level, int n, const uint8_t *patches_with_border,
+                        const uint8_t *patches, int n_iter, float *px_io, uint8_t *converged);
+/* FindDirectProjection for n (map point, keyframe) items against `cur`:
+ * item i uses keyframe frame ref[ref_index[i]], its keypoint kp_ref[i],
+ * pt_ref[3i] = T_ref * P_w, T_cr[i] = T_cur * T_ref^-1, px_io[2i] (level-0 px,
+ * in: projection guess, out: aligned); writes search_level[i], ok[i]. */
+int ygzfe_find_direct_projection_batch(const ygzfe_frame *const *ref, const ygzfe_frame *cur,
+                                       const ygzfe_camera *cam, int n, const int32_t *ref_index,
+                                       const ygzfe_kp *kp_ref, const float *pt_ref,
+                                       const ygzfe_se3 *T_cr, float *px_io, int32_t *search_level,
+                                       uint8_t *ok);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,905 @@
+// api.cpp — the C ABI of include/ygzfe.h over the gfx950 kernels.
+//
+// Host-side responsibilities only: planning (plan.cpp), device buffers,
+// stream ordering and H2D/D2H of the host-pointer entry points.  No compute
+// happens on the host; there is no CPU fallback.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+#include "plan.hpp"
+
+namespace ygzfe {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+static const int kPatternHost[1024] = {
+#include "../../include/ygzfe_pattern.inc"
+};
+
+static int ensure_device(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        set_error("no HIP device available (the ygzfe product path has no CPU fallback)");
+        return YGZFE_EHIP;
+    }
+    if (device < 0 || device >= n) {
+        set_error("device %d out of range (%d devices)", device, n);
+        return YGZFE_EINVAL;
+    }
+    YGZ_HIP(hipSetDevice(device));
+    static std::mutex mu;
+    static bool uploaded[64] = {false};
+    std::lock_guard<std::mutex> lk(mu);
+    if (device < 64 && !uploaded[device]) {
+        YGZ_HIP(upload_pattern(kPatternHost));
+        uploaded[device] = true;
+    }
+    return YGZFE_OK;
+}
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    bool owned = true;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p && owned) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        owned = true;
+    }
+    int ensure(size_t bytes) {
+        if (owned && p && n >= bytes) return YGZFE_OK;
+        if (!owned && p && n >= bytes) return YGZFE_OK;
+        release();
+        if (bytes == 0) bytes = 16;
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            p = nullptr;
+            set_error("hipMalloc(%zu) failed", bytes);
+            return YGZFE_ENOMEM;
+        }
+        n = bytes;
+        return YGZFE_OK;
+    }
+    void bind(void *ext, size_t bytes) {
+        release();
+        p = ext;
+        n = bytes;
+        owned = false;
+    }
+    template <class T>
+    T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+#define YGZ_TRY(x)                          \
+    do {                                    \
+        int r_ = (x);                       \
+        if (r_ != YGZFE_OK) return r_;      \
+    } while (0)
+
+struct PlanDev {
+    PlanHost host;
+    DevBuf plan, cells, tabs;
+    int upload() {
+        YGZ_TRY(plan.ensure(sizeof(Plan)));
+        YGZ_TRY(cells.ensure(sizeof(CellDesc) * (host.cells.size() + 1)));
+        YGZ_TRY(tabs.ensure(sizeof(int) * host.tabs.size()));
+        YGZ_HIP(hipMemcpy(plan.p, &host.plan, sizeof(Plan), hipMemcpyHostToDevice));
+        if (!host.cells.empty())
+            YGZ_HIP(hipMemcpy(cells.p, host.cells.data(), sizeof(CellDesc) * host.cells.size(), hipMemcpyHostToDevice));
+        YGZ_HIP(hipMemcpy(tabs.p, host.tabs.data(), sizeof(int) * host.tabs.size(), hipMemcpyHostToDevice));
+        return YGZFE_OK;
+    }
+    const Plan &hp() const { return host.plan; }
+    const Plan *dp() const { return plan.as<Plan>(); }
+};
+
+static int make_plan(const ygzfe_orb_params &p, int W, int H, std::unique_ptr<PlanDev> *out) {
+    std::unique_ptr<PlanDev> pd(new PlanDev());
+    char err[256];
+    if (build_plan(p, W, H, &pd->host, err, sizeof(err)) != 0) {
+        set_error("%s", err);
+        return YGZFE_EINVAL;
+    }
+    YGZ_TRY(pd->upload());
+    *out = std::move(pd);
+    return YGZFE_OK;
+}
+
+// extraction scratch for F frames of one plan
+struct Workspace {
+    int F = 0, rows = 0;
+    DevBuf blur, cellbuf, cellcnt, candA, candB, sel, selcnt, kps, desc, counts, nexist, err;
+    DevBuf occ, dso_keys, dso_cnt, dso_total;
+    int ensure(const Plan &P, int frames, int rows_needed) {
+        F = frames;
+        rows = rows_needed;
+        YGZ_TRY(blur.ensure((size_t)F * P.pyr_bytes));
+        YGZ_TRY(cellbuf.ensure((size_t)F * P.ncells * P.cell_cap * 4 + 16));
+        YGZ_TRY(cellcnt.ensure((size_t)F * P.ncells * 4 + 16));
+        YGZ_TRY(candA.ensure((size_t)F * P.cand_total * 4 + 16));
+        YGZ_TRY(candB.ensure((size_t)F * P.cand_total * 4 + 16));
+        YGZ_TRY(sel.ensure((size_t)F * P.sel_total * 4 + 16));
+        YGZ_TRY(selcnt.ensure((size_t)F * P.nlevels * 4 + 16));
+        YGZ_TRY(kps.ensure((size_t)F * rows * sizeof(ygzfe_kp) + 16));
+        YGZ_TRY(desc.ensure((size_t)F * rows * 32 + 16));
+        YGZ_TRY(counts.ensure((size_t)F * 4 + 16));
+        YGZ_TRY(nexist.ensure((size_t)F * 4 + 16));
+        YGZ_TRY(err.ensure(16));
+        return YGZFE_OK;
+    }
+};
+
+}  // namespace ygzfe
+
+using namespace ygzfe;
+
+// --------------------------------------------------------------------------- handles
+struct ygzfe_extractor {
+    ygzfe_orb_params p;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    ScaleInfo scales;
+    std::map<std::pair<int, int>, std::unique_ptr<PlanDev>> plans;
+    Workspace ws;
+    int dso_grid = -1;
+    std::mutex mu;
+};
+
+struct ygzfe_frame {
+    ygzfe_extractor *ex = nullptr;
+    PlanDev *plan = nullptr;
+    int W = 0, H = 0;
+    DevBuf pyr;
+};
+
+struct ygzfe_batch {
+    ygzfe_orb_params p;
+    int device = 0;
+    int maxF = 0;
+    hipStream_t stream = nullptr;
+    std::unique_ptr<PlanDev> plan;
+    DevBuf pyr;
+    Workspace ws;
+    // align scratch
+    DevBuf jobs, ascratch, pairs_tmp;
+    size_t ascratch_per_job = 0;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev;
+    std::vector<float> stage_ms;
+};
+
+static const char *kStageNames[] = {"pyramid", "blur7", "fast9_cells", "octree", "orient_rbrief"};
+constexpr int kNumStages = 5;
+
+extern "C" {
+
+const char *ygzfe_last_error(void) { return g_err; }
+
+int ygzfe_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int ygzfe_descriptor_distance(const uint8_t *a, const uint8_t *b) {
+    // ORBmatcher::DescriptorDistance (ORBmatcher.cc:1507-1523): host scalar helper.
+    int d = 0;
+    for (int i = 0; i < 32; i += 4) {
+        uint32_t x, y;
+        memcpy(&x, a + i, 4);
+        memcpy(&y, b + i, 4);
+        d += __builtin_popcount(x ^ y);
+    }
+    return d;
+}
+
+// ------------------------------------------------------------------ extractor
+int ygzfe_extractor_create(const ygzfe_orb_params *p, int device, ygzfe_extractor **out) {
+    if (!p || !out) { set_error("null argument"); return YGZFE_EINVAL; }
+    if (p->nlevels < 1 || p->nlevels > YGZFE_MAX_LEVELS || !(p->scale_factor > 1.0f) || p->nfeatures < 0) {
+        set_error("invalid ORB parameters");
+        return YGZFE_EINVAL;
+    }
+    YGZ_TRY(ensure_device(device));
+    std::unique_ptr<ygzfe_extractor> ex(new ygzfe_extractor());
+    ex->p = *p;
+    ex->device = device;
+    orb_scales(*p, &ex->scales);
+    YGZ_HIP(hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking));
+    *out = ex.release();
+    return YGZFE_OK;
+}
+
+void ygzfe_extractor_destroy(ygzfe_extractor *ex) {
+    if (!ex) return;
+    (void)hipSetDevice(ex->device);
+    if (ex->stream) (void)hipStreamSynchronize(ex->stream);
+    ex->plans.clear();
+    if (ex->stream) (void)hipStreamDestroy(ex->stream);
+    delete ex;
+}
+
+int ygzfe_extractor_levels(const ygzfe_extractor *ex, int *nlevels, float *scale, float *inv_scale,
+                           float *sigma2, float *inv_sigma2) {
+    if (!ex) { set_error("null extractor"); return YGZFE_EINVAL; }
+    const int L = ex->p.nlevels;
+    if (nlevels) *nlevels = L;
+    for (int i = 0; i < L; i++) {
+        if (scale) scale[i] = ex->scales.scale[i];
+        if (inv_scale) inv_scale[i] = ex->scales.inv_scale[i];
+        if (sigma2) sigma2[i] = ex->scales.sigma2[i];
+        if (inv_sigma2) inv_sigma2[i] = ex->scales.inv_sigma2[i];
+    }
+    return YGZFE_OK;
+}
+
+int ygzfe_extractor_features_per_level(const ygzfe_extractor *ex, int32_t *out) {
+    if (!ex || !out) { set_error("null argument"); return YGZFE_EINVAL; }
+    for (int i = 0; i < ex->p.nlevels; i++) out[i] = ex->scales.budget[i];
+    return YGZFE_OK;
+}
+
+int ygzfe_extractor_dso_grid(ygzfe_extractor *ex, int32_t *get, const int32_t *set) {
+    if (!ex) { set_error("null extractor"); return YGZFE_EINVAL; }
+    if (get) *get = ex->dso_grid;
+    if (set) ex->dso_grid = *set;
+    return YGZFE_OK;
+}
+
+static int extractor_plan(ygzfe_extractor *ex, int W, int H, PlanDev **out) {
+    auto key = std::make_pair(W, H);
+    auto it = ex->plans.find(key);
+    if (it == ex->plans.end()) {
+        std::unique_ptr<PlanDev> pd;
+        YGZ_TRY(make_plan(ex->p, W, H, &pd));
+        it = ex->plans.emplace(key, std::move(pd)).first;
+    }
+    *out = it->second.get();
+    return YGZFE_OK;
+}
+
+int ygzfe_frame_create(ygzfe_extractor *ex, int width, int height, ygzfe_frame **out) {
+    if (!ex || !out) { set_error("null argument"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    std::unique_ptr<ygzfe_frame> f(new ygzfe_frame());
+    f->ex = ex;
+    f->W = width;
+    f->H = height;
+    YGZ_TRY(extractor_plan(ex, width, height, &f->plan));
+    YGZ_TRY(f->pyr.ensure(f->plan->hp().pyr_bytes));
+    *out = f.release();
+    return YGZFE_OK;
+}
+
+void ygzfe_frame_destroy(ygzfe_frame *f) {
+    if (!f) return;
+    (void)hipSetDevice(f->ex->device);
+    (void)hipStreamSynchronize(f->ex->stream);
+    delete f;
+}
+
+static int pyramid_from_level0(ygzfe_frame *f, hipStream_t st) {
+    const PlanDev &pd = *f->plan;
+    YGZ_HIP(launch_pyramid(f->pyr.as<uint8_t>(), pd.hp().pyr_bytes, pd.hp(), pd.dp(), pd.tabs.as<int>(), 1, st));
+    return YGZFE_OK;
+}
+
+int ygzfe_compute_pyramid(ygzfe_extractor *ex, ygzfe_frame *f, const uint8_t *img, int stride) {
+    if (!ex || !f || !img || stride < f->W) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    YGZ_HIP(hipMemcpy2DAsync(f->pyr.p, f->W, img, stride, f->W, f->H, hipMemcpyHostToDevice, ex->stream));
+    YGZ_TRY(pyramid_from_level0(f, ex->stream));
+    YGZ_HIP(hipStreamSynchronize(ex->stream));
+    return YGZFE_OK;
+}
+
+int ygzfe_compute_pyramid_device(ygzfe_extractor *ex, ygzfe_frame *f, const uint8_t *d_img, int stride,
+                                 void *stream) {
+    if (!ex || !f || !d_img || stride < f->W) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(ex->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ex->stream;
+    YGZ_HIP(hipMemcpy2DAsync(f->pyr.p, f->W, d_img, stride, f->W, f->H, hipMemcpyDeviceToDevice, st));
+    YGZ_TRY(pyramid_from_level0(f, st));
+    if (!stream) YGZ_HIP(hipStreamSynchronize(st));
+    return YGZFE_OK;
+}
+
+int ygzfe_frame_level(const ygzfe_frame *f, int level, int *w, int *h, uint8_t *dst, int dst_stride) {
+    if (!f) { set_error("null frame"); return YGZFE_EINVAL; }
+    const Plan &P = f->plan->hp();
+    if (level < 0 || level >= P.nlevels) { set_error("level %d out of range", level); return YGZFE_EINVAL; }
+    const LevelDesc &L = P.lv[level];
+    if (w) *w = L.w;
+    if (h) *h = L.h;
+    if (dst) {
+        if (dst_stride < L.w) { set_error("dst_stride < level width"); return YGZFE_EINVAL; }
+        YGZ_TRY(ensure_device(f->ex->device));
+        YGZ_HIP(hipStreamSynchronize(f->ex->stream));
+        YGZ_HIP(hipMemcpy2D(dst, dst_stride, f->pyr.as<uint8_t>() + L.off, L.w, L.w, L.h, hipMemcpyDeviceToHost));
+    }
+    return YGZFE_OK;
+}
+
+int ygzfe_frame_set_level(ygzfe_frame *f, int level, const uint8_t *src, int src_stride) {
+    if (!f || !src) { set_error("null argument"); return YGZFE_EINVAL; }
+    const Plan &P = f->plan->hp();
+    if (level < 0 || level >= P.nlevels) { set_error("level %d out of range", level); return YGZFE_EINVAL; }
+    const LevelDesc &L = P.lv[level];
+    if (src_stride < L.w) { set_error("src_stride < level width"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(f->ex->device));
+    YGZ_HIP(hipStreamSynchronize(f->ex->stream));
+    YGZ_HIP(hipMemcpy2D(f->pyr.as<uint8_t>() + L.off, L.w, src, src_stride, L.w, L.h, hipMemcpyHostToDevice));
+    return YGZFE_OK;
+}
+
+static int dso_max_rows(const Plan &P) {
+    const int g = 7;
+    return 3 * (P.lv[0].w / g) * (P.lv[0].h / g);
+}
+
+int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps_io, int n_existing, int cap,
+                  uint8_t *desc, int *n_out) {
+    if (!ex || !f || !n_out || n_existing < 0 || (n_existing > 0 && !kps_io)) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (method == YGZFE_FAST_KEYPOINT) {
+        set_error("FAST_KEYPOINT is flagged buggy and never called by the reference (ORBextractor.cc:1191)");
+        return YGZFE_EINVAL;
+    }
+    if (method != YGZFE_ORBSLAM_KEYPOINT && method != YGZFE_DSO_KEYPOINT) {
+        set_error("unknown method %d", method);
+        return YGZFE_EINVAL;
+    }
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    const PlanDev &pd = *f->plan;
+    const Plan &P = pd.hp();
+    hipStream_t st = ex->stream;
+    const int rows = n_existing + (method == YGZFE_DSO_KEYPOINT ? std::max(P.kp_cap, dso_max_rows(P)) : P.kp_cap);
+    Workspace &ws = ex->ws;
+    YGZ_TRY(ws.ensure(P, 1, rows));
+    if (n_existing > 0)
+        YGZ_HIP(hipMemcpyAsync(ws.kps.p, kps_io, sizeof(ygzfe_kp) * n_existing, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(ws.nexist.p, &n_existing, sizeof(int), hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemsetAsync(ws.err.p, 0, 16, st));
+    const uint8_t *pyr = f->pyr.as<uint8_t>();
+    YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), 1, st));
+    int total = 0;
+    if (method == YGZFE_ORBSLAM_KEYPOINT) {
+        YGZ_HIP(launch_fast(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(), ws.cellbuf.as<uint32_t>(),
+                            ws.cellcnt.as<int>(), 1, st));
+        YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
+                              ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.err.as<int>(), 1,
+                              st));
+        YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.sel.as<uint32_t>(),
+                                   ws.selcnt.as<int>(), ws.nexist.as<int>(), ws.kps.as<ygzfe_kp>(),
+                                   ws.desc.as<uint8_t>(), ws.counts.as<int>(), rows, 1, st));
+        YGZ_HIP(launch_desc_existing(pyr, ws.blur.as<uint8_t>(), pd.dp(), ws.kps.as<ygzfe_kp>(),
+                                     ws.desc.as<uint8_t>(), n_existing, 0, st));
+        int herr = 0;
+        YGZ_HIP(hipMemcpyAsync(&total, ws.counts.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        YGZ_HIP(hipMemcpyAsync(&herr, ws.err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        YGZ_HIP(hipStreamSynchronize(st));
+        if (herr) {
+            set_error("octree node pool overflow");
+            return YGZFE_EINVAL;
+        }
+    } else {
+        // DSO_KEYPOINT: ComputeKeyPointsDSOSingleLevel (ORBextractor.cc:1275-1386)
+        const LevelDesc &L0 = P.lv[0];
+        const int w = L0.w, h = L0.h, n = ex->p.nfeatures;
+        YGZ_TRY(ws.occ.ensure((size_t)w * h));
+        YGZ_HIP(launch_dso_occupancy(ws.kps.as<ygzfe_kp>(), n_existing, ws.occ.as<uint8_t>(), w, h, st));
+        int g = ex->dso_grid;
+        if (g < 0) g = (int)sqrt(1.0 * h * w / (n > 0 ? n : 1));
+        int cnt = 0;
+        for (;;) {
+            if (cnt >= n) break;
+            if (cnt > 0) {
+                g -= 5;
+                if (g < 7) { g = 7; break; }
+            }
+            if (g > kDsoMaxGridHost) {
+                set_error("DSO grid %d exceeds the supported %d", g, kDsoMaxGridHost);
+                return YGZFE_EINVAL;
+            }
+            const int ncells = (h / g) * (w / g);
+            YGZ_TRY(ws.dso_keys.ensure((size_t)ncells * 3 * 4 + 16));
+            YGZ_TRY(ws.dso_cnt.ensure((size_t)ncells * 4 + 16));
+            YGZ_TRY(ws.dso_total.ensure(16));
+            YGZ_HIP(launch_dso_pass(pyr, w, h, g, ws.occ.as<uint8_t>(), ws.dso_keys.as<uint32_t>(),
+                                    ws.dso_cnt.as<int>(), st));
+            YGZ_HIP(launch_dso_finish2(ws.dso_keys.as<uint32_t>(), ws.dso_cnt.as<int>(), ncells,
+                                       ws.kps.as<ygzfe_kp>(), n_existing, ws.dso_total.as<int>(), st));
+            YGZ_HIP(hipMemcpyAsync(&cnt, ws.dso_total.p, sizeof(int), hipMemcpyDeviceToHost, st));
+            YGZ_HIP(hipStreamSynchronize(st));
+            if (cnt == 0) break;  // the reference loops forever on a corner-free image
+        }
+        if (cnt > n) g += 5;
+        ex->dso_grid = g;
+        total = n_existing + cnt;
+        YGZ_HIP(launch_desc_existing(pyr, ws.blur.as<uint8_t>(), pd.dp(), ws.kps.as<ygzfe_kp>(),
+                                     ws.desc.as<uint8_t>(), total, 1, st));
+        YGZ_HIP(hipStreamSynchronize(st));
+    }
+    *n_out = total;
+    if (total > cap) {
+        set_error("capacity %d < %d keypoints", cap, total);
+        return YGZFE_ECAP;
+    }
+    if (total > 0) {
+        YGZ_HIP(hipMemcpyAsync(kps_io, ws.kps.p, sizeof(ygzfe_kp) * total, hipMemcpyDeviceToHost, st));
+        if (desc) YGZ_HIP(hipMemcpyAsync(desc, ws.desc.p, (size_t)32 * total, hipMemcpyDeviceToHost, st));
+        YGZ_HIP(hipStreamSynchronize(st));
+    }
+    return YGZFE_OK;
+}
+
+int ygzfe_detect_and_compute(ygzfe_extractor *ex, ygzfe_frame *f, const uint8_t *img, int stride, ygzfe_kp *kps,
+                             int cap, uint8_t *desc, int *n_out) {
+    if (!img) { set_error("empty image"); return YGZFE_EINVAL; }  // reference returns silently (:972-973)
+    YGZ_TRY(ygzfe_compute_pyramid(ex, f, img, stride));
+    return ygzfe_extract(ex, f, YGZFE_ORBSLAM_KEYPOINT, kps, 0, cap, desc, n_out);
+}
+
+// ------------------------------------------------------------------ batch
+int ygzfe_batch_create(const ygzfe_orb_params *p, int device, int width, int height, int max_frames,
+                       ygzfe_batch **out) {
+    if (!p || !out || max_frames <= 0) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(device));
+    std::unique_ptr<ygzfe_batch> b(new ygzfe_batch());
+    b->p = *p;
+    b->device = device;
+    b->maxF = max_frames;
+    YGZ_TRY(make_plan(*p, width, height, &b->plan));
+    const Plan &P = b->plan->hp();
+    YGZ_TRY(b->pyr.ensure((size_t)max_frames * P.pyr_bytes));
+    YGZ_TRY(b->ws.ensure(P, max_frames, P.kp_cap));
+    YGZ_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    b->ev.resize(kNumStages + 1);
+    for (auto &e : b->ev) YGZ_HIP(hipEventCreate(&e));
+    b->stage_ms.assign(kNumStages, 0.f);
+    *out = b.release();
+    return YGZFE_OK;
+}
+
+void ygzfe_batch_destroy(ygzfe_batch *b) {
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    (void)hipStreamSynchronize(b->stream);
+    for (auto &e : b->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(b->stream);
+    delete b;
+}
+
+int ygzfe_batch_info(ygzfe_batch *b, size_t *frame_pitch, int *kp_cap, int *nlevels) {
+    if (!b) { set_error("null batch"); return YGZFE_EINVAL; }
+    const Plan &P = b->plan->hp();
+    if (frame_pitch) *frame_pitch = P.pyr_bytes;
+    if (kp_cap) *kp_cap = P.kp_cap;
+    if (nlevels) *nlevels = P.nlevels;
+    return YGZFE_OK;
+}
+
+int ygzfe_batch_frames(ygzfe_batch *b, uint8_t **d_frames) {
+    if (!b || !d_frames) { set_error("null argument"); return YGZFE_EINVAL; }
+    *d_frames = b->pyr.as<uint8_t>();
+    return YGZFE_OK;
+}
+
+int ygzfe_batch_bind_buffers(ygzfe_batch *b, uint8_t *d_pyramids, ygzfe_kp *d_kps, uint8_t *d_desc,
+                             int32_t *d_counts) {
+    if (!b) { set_error("null batch"); return YGZFE_EINVAL; }
+    const Plan &P = b->plan->hp();
+    YGZ_TRY(ensure_device(b->device));
+    YGZ_HIP(hipStreamSynchronize(b->stream));
+    if (d_pyramids) b->pyr.bind(d_pyramids, (size_t)b->maxF * P.pyr_bytes);
+    if (d_kps) b->ws.kps.bind(d_kps, (size_t)b->maxF * P.kp_cap * sizeof(ygzfe_kp));
+    if (d_desc) b->ws.desc.bind(d_desc, (size_t)b->maxF * P.kp_cap * 32);
+    if (d_counts) b->ws.counts.bind(d_counts, (size_t)b->maxF * 4);
+    return YGZFE_OK;
+}
+
+int ygzfe_batch_upload(ygzfe_batch *b, const uint8_t *frames, int n_frames) {
+    if (!b || !frames || n_frames < 0 || n_frames > b->maxF) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(b->device));
+    const Plan &P = b->plan->hp();
+    // frame i -> level-0 slot of pyramid i (pitch P.pyr_bytes)
+    YGZ_HIP(hipMemcpy2DAsync(b->pyr.p, P.pyr_bytes, frames, (size_t)P.W * P.H, (size_t)P.W * P.H, n_frames,
+                             hipMemcpyHostToDevice, b->stream));
+    YGZ_HIP(hipStreamSynchronize(b->stream));
+    return YGZFE_OK;
+}
+
+int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream) {
+    if (!b || n_frames < 0 || n_frames > b->maxF) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    if (n_frames == 0) return YGZFE_OK;
+    YGZ_TRY(ensure_device(b->device));
+    hipStream_t st = stream ? (hipStream_t)stream : b->stream;
+    const PlanDev &pd = *b->plan;
+    const Plan &P = pd.hp();
+    Workspace &ws = b->ws;
+    uint8_t *pyr = b->pyr.as<uint8_t>();
+    const bool tm = b->timing;
+    YGZ_HIP(hipMemsetAsync(ws.err.p, 0, 16, st));
+    if (tm) YGZ_HIP(hipEventRecord(b->ev[0], st));
+    YGZ_HIP(launch_pyramid(pyr, P.pyr_bytes, P, pd.dp(), pd.tabs.as<int>(), n_frames, st));
+    if (tm) YGZ_HIP(hipEventRecord(b->ev[1], st));
+    YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), n_frames, st));
+    if (tm) YGZ_HIP(hipEventRecord(b->ev[2], st));
+    YGZ_HIP(launch_fast(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(), ws.cellbuf.as<uint32_t>(),
+                        ws.cellcnt.as<int>(), n_frames, st));
+    if (tm) YGZ_HIP(hipEventRecord(b->ev[3], st));
+    YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
+                          ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.err.as<int>(),
+                          n_frames, st));
+    if (tm) YGZ_HIP(hipEventRecord(b->ev[4], st));
+    YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.sel.as<uint32_t>(),
+                               ws.selcnt.as<int>(), nullptr, ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(),
+                               ws.counts.as<int>(), P.kp_cap, n_frames, st));
+    if (tm) {
+        YGZ_HIP(hipEventRecord(b->ev[5], st));
+        YGZ_HIP(hipEventSynchronize(b->ev[5]));
+        for (int s = 0; s < kNumStages; s++) YGZ_HIP(hipEventElapsedTime(&b->stage_ms[s], b->ev[s], b->ev[s + 1]));
+    }
+    return YGZFE_OK;
+}
+
+int ygzfe_batch_check(ygzfe_batch *b) {
+    if (!b) { set_error("null batch"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(b->device));
+    int herr = 0;
+    YGZ_HIP(hipStreamSynchronize(b->stream));
+    YGZ_HIP(hipDeviceSynchronize());
+    YGZ_HIP(hipMemcpy(&herr, b->ws.err.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (herr) { set_error("octree node pool overflow"); return YGZFE_EINVAL; }
+    return YGZFE_OK;
+}
+
+int ygzfe_batch_result(ygzfe_batch *b, int frame, ygzfe_kp *kps, int cap, uint8_t *desc, int *n_out) {
+    if (!b || frame < 0 || frame >= b->maxF || !n_out) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(b->device));
+    YGZ_HIP(hipDeviceSynchronize());
+    const Plan &P = b->plan->hp();
+    int n = 0;
+    YGZ_HIP(hipMemcpy(&n, b->ws.counts.as<int>() + frame, sizeof(int), hipMemcpyDeviceToHost));
+    *n_out = n;
+    if (n > cap) { set_error("capacity %d < %d", cap, n); return YGZFE_ECAP; }
+    if (kps && n) YGZ_HIP(hipMemcpy(kps, b->ws.kps.as<ygzfe_kp>() + (size_t)frame * P.kp_cap, sizeof(ygzfe_kp) * n,
+                                    hipMemcpyDeviceToHost));
+    if (desc && n) YGZ_HIP(hipMemcpy(desc, b->ws.desc.as<uint8_t>() + (size_t)frame * P.kp_cap * 32, (size_t)32 * n,
+                                     hipMemcpyDeviceToHost));
+    return YGZFE_OK;
+}
+
+int ygzfe_batch_device_results(ygzfe_batch *b, ygzfe_kp **d_kps, uint8_t **d_desc, int32_t **d_counts,
+                               int *kp_cap) {
+    if (!b) { set_error("null batch"); return YGZFE_EINVAL; }
+    if (d_kps) *d_kps = b->ws.kps.as<ygzfe_kp>();
+    if (d_desc) *d_desc = b->ws.desc.as<uint8_t>();
+    if (d_counts) *d_counts = b->ws.counts.as<int32_t>();
+    if (kp_cap) *kp_cap = b->plan->hp().kp_cap;
+    return YGZFE_OK;
+}
+
+int ygzfe_batch_level(ygzfe_batch *b, int frame, int level, const uint8_t **d_level, int *w, int *h, int *stride) {
+    if (!b || frame < 0 || frame >= b->maxF) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    const Plan &P = b->plan->hp();
+    if (level < 0 || level >= P.nlevels) { set_error("level out of range"); return YGZFE_EINVAL; }
+    if (d_level) *d_level = b->pyr.as<uint8_t>() + (size_t)frame * P.pyr_bytes + P.lv[level].off;
+    if (w) *w = P.lv[level].w;
+    if (h) *h = P.lv[level].h;
+    if (stride) *stride = P.lv[level].w;
+    return YGZFE_OK;
+}
+
+int ygzfe_batch_timing(ygzfe_batch *b, int enable, float *ms, const char **names, int cap) {
+    if (!b) { set_error("null batch"); return YGZFE_EINVAL; }
+    b->timing = enable != 0;
+    for (int s = 0; s < kNumStages && s < cap; s++) {
+        if (ms) ms[s] = b->stage_ms[s];
+        if (names) names[s] = kStageNames[s];
+    }
+    return kNumStages;
+}
+
+void *ygzfe_batch_stream(ygzfe_batch *b) { return b ? (void *)b->stream : nullptr; }
+
+// ------------------------------------------------------------------ hamming
+int ygzfe_hamming_best2_device(const uint8_t *d_query, int nq, const uint8_t *d_train, int nt, int32_t *d_best_idx,
+                               int32_t *d_best_dist, int32_t *d_second_dist, void *stream) {
+    if (nq < 0 || nt < 0 || (nq > 0 && (!d_query || !d_best_idx || !d_best_dist || !d_second_dist)) ||
+        (nt > 0 && !d_train)) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    YGZ_HIP(launch_hamming_best2(d_query, nq, d_train, nt, d_best_idx, d_best_dist, d_second_dist,
+                                 (hipStream_t)stream));
+    return YGZFE_OK;
+}
+
+int ygzfe_hamming_best2(int device, const uint8_t *query, int nq, const uint8_t *train, int nt, int32_t *best_idx,
+                        int32_t *best_dist, int32_t *second_dist) {
+    if (nq < 0 || nt < 0) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    if (nq == 0) return YGZFE_OK;
+    YGZ_TRY(ensure_device(device));
+    DevBuf q, t, o;
+    YGZ_TRY(q.ensure((size_t)nq * 32));
+    YGZ_TRY(t.ensure((size_t)(nt > 0 ? nt : 1) * 32));
+    YGZ_TRY(o.ensure((size_t)nq * 12));
+    YGZ_HIP(hipMemcpy(q.p, query, (size_t)nq * 32, hipMemcpyHostToDevice));
+    if (nt > 0) YGZ_HIP(hipMemcpy(t.p, train, (size_t)nt * 32, hipMemcpyHostToDevice));
+    int32_t *bi = o.as<int32_t>(), *bd = bi + nq, *sd = bd + nq;
+    YGZ_HIP(launch_hamming_best2(q.as<uint8_t>(), nq, t.as<uint8_t>(), nt, bi, bd, sd, nullptr));
+    YGZ_HIP(hipDeviceSynchronize());
+    YGZ_HIP(hipMemcpy(best_idx, bi, (size_t)nq * 4, hipMemcpyDeviceToHost));
+    YGZ_HIP(hipMemcpy(best_dist, bd, (size_t)nq * 4, hipMemcpyDeviceToHost));
+    YGZ_HIP(hipMemcpy(second_dist, sd, (size_t)nq * 4, hipMemcpyDeviceToHost));
+    return YGZFE_OK;
+}
+
+int ygzfe_hamming_csr(int device, const uint8_t *query, int nq, const uint8_t *train, int nt, const int32_t *row_ptr,
+                      const int32_t *cand, int32_t *dist_out) {
+    if (nq < 0 || nt < 0 || !row_ptr) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    if (nq == 0) return YGZFE_OK;
+    const int nc = row_ptr[nq];
+    if (nc == 0) return YGZFE_OK;
+    for (int k = 0; k < nc; k++)
+        if (cand[k] < 0 || cand[k] >= nt) { set_error("candidate index %d out of range", cand[k]); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(device));
+    DevBuf q, t, rp, cd, ds;
+    YGZ_TRY(q.ensure((size_t)nq * 32));
+    YGZ_TRY(t.ensure((size_t)nt * 32));
+    YGZ_TRY(rp.ensure((size_t)(nq + 1) * 4));
+    YGZ_TRY(cd.ensure((size_t)nc * 4));
+    YGZ_TRY(ds.ensure((size_t)nc * 4));
+    YGZ_HIP(hipMemcpy(q.p, query, (size_t)nq * 32, hipMemcpyHostToDevice));
+    YGZ_HIP(hipMemcpy(t.p, train, (size_t)nt * 32, hipMemcpyHostToDevice));
+    YGZ_HIP(hipMemcpy(rp.p, row_ptr, (size_t)(nq + 1) * 4, hipMemcpyHostToDevice));
+    YGZ_HIP(hipMemcpy(cd.p, cand, (size_t)nc * 4, hipMemcpyHostToDevice));
+    YGZ_HIP(launch_hamming_csr(q.as<uint8_t>(), nq, t.as<uint8_t>(), rp.as<int32_t>(), cd.as<int32_t>(),
+                               ds.as<int32_t>(), nullptr));
+    YGZ_HIP(hipDeviceSynchronize());
+    YGZ_HIP(hipMemcpy(dist_out, ds.p, (size_t)nc * 4, hipMemcpyDeviceToHost));
+    return YGZFE_OK;
+}
+
+int ygzfe_batch_match(ygzfe_batch *b, int n_pairs, const int32_t *d_qframe, const int32_t *d_tframe,
+                      int32_t *d_best_idx, int32_t *d_best_dist, int32_t *d_second_dist, void *stream) {
+    if (!b || n_pairs < 0) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(b->device));
+    hipStream_t st = stream ? (hipStream_t)stream : b->stream;
+    const Plan &P = b->plan->hp();
+    YGZ_HIP(launch_hamming_best2_pairs(b->ws.desc.as<uint8_t>(), b->ws.counts.as<int32_t>(), P.kp_cap, n_pairs,
+                                       d_qframe, d_tframe, d_best_idx, d_best_dist, d_second_dist, st));
+    return YGZFE_OK;
+}
+
+// ------------------------------------------------------------------ sparse align
+static AlignLevels levels_of(const Plan &P) {
+    AlignLevels lv;
+    memset(&lv, 0, sizeof(lv));
+    for (int l = 0; l < P.nlevels; l++) {
+        lv.w[l] = P.lv[l].w;
+        lv.h[l] = P.lv[l].h;
+        lv.off[l] = P.lv[l].off;
+        lv.inv_scale[l] = P.lv[l].inv_scale;
+    }
+    return lv;
+}
+
+int ygzfe_sparse_align(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam, const ygzfe_kp *kps,
+                       const float *xyz_ref, const uint8_t *usable, int n, int max_level, int min_level,
+                       const ygzfe_se3 *T_init, ygzfe_align_result *result) {
+    if (!ref || !cur || !cam || !T_init || !result || n < 0 || (n > 0 && (!kps || !xyz_ref || !usable))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (ref->plan != cur->plan) { set_error("ref and cur frames must share size and extractor"); return YGZFE_EINVAL; }
+    const Plan &P = ref->plan->hp();
+    if (min_level < 0 || max_level >= P.nlevels || min_level > max_level) {
+        set_error("levels [%d,%d] outside the %d-level pyramid", min_level, max_level, P.nlevels);
+        return YGZFE_EINVAL;
+    }
+    if (n == 0) {  // SparseImageAlign.cc:24-27
+        memset(result, 0, sizeof(*result));
+        result->T_cur_ref = *T_init;
+        result->chi2 = 1e10f;
+        return YGZFE_OK;
+    }
+    ygzfe_extractor *ex = ref->ex;
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    hipStream_t st = ex->stream;
+    DevBuf dk, dx, du, dj, ds, dout;
+    YGZ_TRY(dk.ensure(sizeof(ygzfe_kp) * n));
+    YGZ_TRY(dx.ensure(sizeof(float) * 3 * n));
+    YGZ_TRY(du.ensure(n));
+    YGZ_TRY(dj.ensure(sizeof(AlignJob)));
+    const size_t spj = sparse_align_scratch_floats(n);
+    YGZ_TRY(ds.ensure(sizeof(float) * spj));
+    YGZ_TRY(dout.ensure(sizeof(ygzfe_align_result)));
+    YGZ_HIP(hipMemcpyAsync(dk.p, kps, sizeof(ygzfe_kp) * n, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(dx.p, xyz_ref, sizeof(float) * 3 * n, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(du.p, usable, n, hipMemcpyHostToDevice, st));
+    AlignJob job;
+    job.ref_pyr = ref->pyr.as<uint8_t>();
+    job.cur_pyr = cur->pyr.as<uint8_t>();
+    job.kps = dk.as<ygzfe_kp>();
+    job.xyz = dx.as<float>();
+    job.usable = du.as<uint8_t>();
+    job.n = n;
+    job.max_level = max_level;
+    job.min_level = min_level;
+    job.T_init = *T_init;
+    YGZ_HIP(hipMemcpyAsync(dj.p, &job, sizeof(job), hipMemcpyHostToDevice, st));
+    YGZ_HIP(launch_sparse_align(levels_of(P), *cam, dj.as<AlignJob>(), 1, ds.as<float>(), spj,
+                                dout.as<ygzfe_align_result>(), st));
+    YGZ_HIP(hipMemcpyAsync(result, dout.p, sizeof(*result), hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipStreamSynchronize(st));
+    return YGZFE_OK;
+}
+
+}  // extern "C"
+
+namespace ygzfe {
+__global__ void k_build_align_jobs(AlignJob *jobs, int n_pairs, const int32_t *ref_idx, const int32_t *cur_idx,
+                                   const uint8_t *pyr, uint32_t pitch, const ygzfe_kp *kps, const int32_t *counts,
+                                   int kp_cap, const float *xyz, const uint8_t *usable, int max_level, int min_level,
+                                   const ygzfe_se3 *T_init) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_pairs) return;
+    const int r = ref_idx[p], c = cur_idx[p];
+    AlignJob j;
+    j.ref_pyr = pyr + (size_t)r * pitch;
+    j.cur_pyr = pyr + (size_t)c * pitch;
+    j.kps = kps + (size_t)r * kp_cap;
+    j.xyz = xyz + (size_t)p * kp_cap * 3;
+    j.usable = usable + (size_t)p * kp_cap;
+    j.n = counts[r];
+    j.max_level = max_level;
+    j.min_level = min_level;
+    j.T_init = T_init[p];
+    jobs[p] = j;
+}
+}  // namespace ygzfe
+
+extern "C" int ygzfe_batch_sparse_align(ygzfe_batch *b, int n_pairs, const int32_t *d_ref_idx,
+                                        const int32_t *d_cur_idx, const float *d_xyz_ref, const uint8_t *d_usable,
+                                        const ygzfe_camera *cam, int max_level, int min_level,
+                                        const ygzfe_se3 *d_T_init, ygzfe_align_result *d_out, void *stream) {
+    if (!b || !cam || n_pairs < 0 || !d_ref_idx || !d_cur_idx || !d_xyz_ref || !d_usable || !d_T_init || !d_out) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    const Plan &P = b->plan->hp();
+    if (min_level < 0 || max_level >= P.nlevels || min_level > max_level) {
+        set_error("levels [%d,%d] outside the %d-level pyramid", min_level, max_level, P.nlevels);
+        return YGZFE_EINVAL;
+    }
+    if (n_pairs == 0) return YGZFE_OK;
+    YGZ_TRY(ensure_device(b->device));
+    hipStream_t st = stream ? (hipStream_t)stream : b->stream;
+    const size_t spj = sparse_align_scratch_floats(P.kp_cap);
+    YGZ_TRY(b->jobs.ensure(sizeof(AlignJob) * n_pairs));
+    YGZ_TRY(b->ascratch.ensure(sizeof(float) * spj * n_pairs));
+    hipLaunchKernelGGL(k_build_align_jobs, dim3((n_pairs + 63) / 64), dim3(64), 0, st, b->jobs.as<AlignJob>(), n_pairs,
+                       d_ref_idx, d_cur_idx, b->pyr.as<uint8_t>(), P.pyr_bytes, b->ws.kps.as<ygzfe_kp>(),
+                       b->ws.counts.as<int32_t>(), P.kp_cap, d_xyz_ref, d_usable, max_level, min_level, d_T_init);
+    YGZ_HIP(hipGetLastError());
+    YGZ_HIP(launch_sparse_align(levels_of(P), *cam, b->jobs.as<AlignJob>(), n_pairs, b->ascratch.as<float>(), spj,
+                                d_out, st));
+    return YGZFE_OK;
+}
+
+// ------------------------------------------------------------------ Align2D / direct projection
+extern "C" int ygzfe_align2d_batch(const ygzfe_frame *cur, int level, int n, const uint8_t *patches_with_border,
+                                   const uint8_t *patches, int n_iter, float *px_io, uint8_t *converged) {
+    if (!cur || n < 0 || (n > 0 && (!patches_with_border || !patches || !px_io || !converged))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    const Plan &P = cur->plan->hp();
+    if (level < 0 || level >= P.nlevels) { set_error("level out of range"); return YGZFE_EINVAL; }
+    if (n == 0) return YGZFE_OK;
+    ygzfe_extractor *ex = cur->ex;
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    hipStream_t st = ex->stream;
+    DevBuf a, b, c, d;
+    YGZ_TRY(a.ensure((size_t)n * 100));
+    YGZ_TRY(b.ensure((size_t)n * 64));
+    YGZ_TRY(c.ensure((size_t)n * 8));
+    YGZ_TRY(d.ensure((size_t)n));
+    YGZ_HIP(hipMemcpyAsync(a.p, patches_with_border, (size_t)n * 100, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(b.p, patches, (size_t)n * 64, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(c.p, px_io, (size_t)n * 8, hipMemcpyHostToDevice, st));
+    const LevelDesc &L = P.lv[level];
+    YGZ_HIP(launch_align2d(cur->pyr.as<uint8_t>() + L.off, L.w, L.h, n, a.as<uint8_t>(), b.as<uint8_t>(), n_iter,
+                           c.as<float>(), d.as<uint8_t>(), st));
+    YGZ_HIP(hipMemcpyAsync(px_io, c.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipMemcpyAsync(converged, d.p, (size_t)n, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipStreamSynchronize(st));
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_find_direct_projection_batch(const ygzfe_frame *const *ref, const ygzfe_frame *cur,
+                                                  const ygzfe_camera *cam, int n, const int32_t *ref_index,
+                                                  const ygzfe_kp *kp_ref, const float *pt_ref, const ygzfe_se3 *T_cr,
+                                                  float *px_io, int32_t *search_level, uint8_t *ok) {
+    if (!ref || !cur || !cam || n < 0 ||
+        (n > 0 && (!ref_index || !kp_ref || !pt_ref || !T_cr || !px_io || !search_level || !ok))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (n == 0) return YGZFE_OK;
+    int nref = 0;
+    for (int i = 0; i < n; i++) nref = std::max(nref, ref_index[i] + 1);
+    for (int i = 0; i < n; i++)
+        if (ref_index[i] < 0) { set_error("negative ref_index"); return YGZFE_EINVAL; }
+    for (int r = 0; r < nref; r++)
+        if (!ref[r] || ref[r]->plan != cur->plan) {
+            set_error("reference keyframe %d missing or of a different size", r);
+            return YGZFE_EINVAL;
+        }
+    ygzfe_extractor *ex = cur->ex;
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    hipStream_t st = ex->stream;
+    const Plan &P = cur->plan->hp();
+    std::vector<const uint8_t *> ptrs(nref);
+    for (int r = 0; r < nref; r++) ptrs[r] = ref[r]->pyr.as<uint8_t>();
+    std::vector<float> scale(P.nlevels);
+    for (int l = 0; l < P.nlevels; l++) scale[l] = P.lv[l].scale;
+    DevBuf dptr, dsc, dri, dkp, dpt, dT, dpx, dlv, dok;
+    YGZ_TRY(dptr.ensure(sizeof(void *) * nref));
+    YGZ_TRY(dsc.ensure(sizeof(float) * P.nlevels));
+    YGZ_TRY(dri.ensure(4 * (size_t)n));
+    YGZ_TRY(dkp.ensure(sizeof(ygzfe_kp) * n));
+    YGZ_TRY(dpt.ensure(12 * (size_t)n));
+    YGZ_TRY(dT.ensure(sizeof(ygzfe_se3) * n));
+    YGZ_TRY(dpx.ensure(8 * (size_t)n));
+    YGZ_TRY(dlv.ensure(4 * (size_t)n));
+    YGZ_TRY(dok.ensure((size_t)n));
+    YGZ_HIP(hipMemcpyAsync(dptr.p, ptrs.data(), sizeof(void *) * nref, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(dsc.p, scale.data(), sizeof(float) * P.nlevels, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(dri.p, ref_index, 4 * (size_t)n, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(dkp.p, kp_ref, sizeof(ygzfe_kp) * n, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(dpt.p, pt_ref, 12 * (size_t)n, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(dT.p, T_cr, sizeof(ygzfe_se3) * n, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(dpx.p, px_io, 8 * (size_t)n, hipMemcpyHostToDevice, st));
+    const AlignLevels lv = levels_of(P);
+    YGZ_HIP(launch_find_direct(dptr.as<const uint8_t *>(), lv, cur->pyr.as<uint8_t>(), lv, P.nlevels,
+                               dsc.as<float>(), ex->scales.inv_sigma2[1 < P.nlevels ? 1 : 0], *cam, n,
+                               dri.as<int32_t>(), dkp.as<ygzfe_kp>(), dpt.as<float>(), dT.as<ygzfe_se3>(),
+                               dpx.as<float>(), dlv.as<int32_t>(), dok.as<uint8_t>(), st));
+    YGZ_HIP(hipMemcpyAsync(px_io, dpx.p, 8 * (size_t)n, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipMemcpyAsync(search_level, dlv.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipMemcpyAsync(ok, dok.p, (size_t)n, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipStreamSynchronize(st));
+    return YGZFE_OK;
+}

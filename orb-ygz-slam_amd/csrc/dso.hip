@@ -1,0 +1,218 @@
+// dso.hip — DSO_KEYPOINT mode (ComputeKeyPointsDSOSingleLevel,
+// ORBextractor.cc:1275-1386) on gfx950: per grid cell FAST-10 (Thirdparty/fast
+// semantics), Shi-Tomasi scoring (ORBextractor.cc:1152-1187) and top-3
+// selection.  One 256-thread workgroup per cell; the host drives the
+// grid-shrinking loop (it needs the total count between passes).
+#include "common.hpp"
+
+namespace ygzfe {
+
+constexpr int kDsoHalo = 5;
+constexpr int kDsoMaxGrid = 96;
+constexpr int kDsoS = kDsoMaxGrid + 2 * kDsoHalo;
+
+// longest circular run >= 10 of a 16-bit ring mask
+__device__ __forceinline__ bool run10(uint32_t m16) {
+    uint32_t x = m16 | (m16 << 16);
+    uint32_t y = x & (x >> 1);
+    y &= y >> 2;
+    y &= y >> 4;
+    y &= (x >> 8) & (x >> 9);
+    return (y & 0xFFFFu) != 0;
+}
+
+// fast_10.cpp ring order (x, y): (0,3) (1,3) (2,2) (3,1) (3,0) (3,-1) (2,-2) (1,-3) (0,-3) ...
+__device__ __forceinline__ bool fast10_corner(const uint8_t *p, int S, int b) {
+    const int v = p[0], cb = v + b, c_b = v - b;
+    const int r[16] = {p[3 * S],  p[1 + 3 * S],  p[2 + 2 * S],  p[3 + S],  p[3],  p[3 - S],
+                       p[2 - 2 * S], p[1 - 3 * S], p[-3 * S], p[-1 - 3 * S], p[-2 - 2 * S], p[-3 - S],
+                       p[-3], p[-3 + S], p[-2 + 2 * S], p[-1 + 3 * S]};
+    uint32_t br = 0, dk = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        br |= (uint32_t)(r[k] > cb) << k;
+        dk |= (uint32_t)(r[k] < c_b) << k;
+    }
+    return run10(br) || run10(dk);
+}
+
+// ShiTomasiScore on the LDS tile (pixel p = centre, stride S): float sums in raster order.
+__device__ __forceinline__ float shi_tomasi(const uint8_t *p, int S) {
+    float dXX = 0.f, dYY = 0.f, dXY = 0.f;
+    for (int y = -4; y < 4; ++y)
+        for (int x = -4; x < 4; ++x) {
+            const uint8_t *q = p + y * S + x;
+            const float dx = (float)(q[1] - q[-1]);
+            const float dy = (float)(q[S] - q[-S]);
+            dXX += dx * dx;
+            dYY += dy * dy;
+            dXY += dx * dy;
+        }
+    dXX = (float)(dXX / (2.0 * 64));
+    dYY = (float)(dYY / (2.0 * 64));
+    dXY = (float)(dXY / (2.0 * 64));
+    const float s = dXX + dYY;
+    const float disc = s * s - 4 * (dXX * dYY - dXY * dXY);
+    return (float)(0.5 * (double)(dXX + dYY - sqrtf(disc)));
+}
+
+// cell k of the grid; writes up to 3 keys (x | y << 16, level-0 px) sorted by
+// descending score (NaN last, ties by scan order) and the count.
+__global__ __launch_bounds__(256) void k_dso_cells(const uint8_t *__restrict__ img, int w, int h, int g,
+                                                   const uint8_t *__restrict__ occ,
+                                                   uint32_t *__restrict__ out_keys, int *__restrict__ out_cnt) {
+    __shared__ uint8_t s_img[kDsoS * kDsoS];
+    __shared__ float s_sc[kDsoMaxGrid * kDsoMaxGrid];
+    __shared__ int s_any;
+    __shared__ unsigned long long s_best;
+    const int rows = h / g, cols = w / g;
+    const int k = blockIdx.x;
+    const int nn = k / cols;
+    if (threadIdx.x == 0) out_cnt[k] = 0;
+    if (nn == 0 || nn == rows - 1 || (k % cols) == 0 || (k + 1) % cols == 0) return;
+    const int x_start = (k - nn * cols) * g, y_start = nn * g;
+    const int S = g + 2 * kDsoHalo;
+    for (int i = threadIdx.x; i < S * S; i += 256) {
+        const int yy = clampi(y_start - kDsoHalo + i / S, 0, h - 1);
+        const int xx = clampi(x_start - kDsoHalo + i % S, 0, w - 1);
+        s_img[i] = img[(size_t)yy * w + xx];
+    }
+    // scan region: plain detector (g < 22) covers the whole cell, SSE2 [3, g-3)
+    const int lo = g < 22 ? 0 : 3, hi = g < 22 ? g : g - 3;
+    const int span = hi > lo ? hi - lo : 0;
+    __syncthreads();
+    int barrier = 20;
+    for (int pass = 0; pass < 2; pass++) {
+        if (threadIdx.x == 0) s_any = 0;
+        __syncthreads();
+        int any = 0;
+        for (int i = threadIdx.x; i < span * span; i += 256) {
+            const int cy = lo + i / span, cx = lo + i % span;
+            const bool c = fast10_corner(s_img + (cy + kDsoHalo) * S + cx + kDsoHalo, S, barrier);
+            s_sc[cy * g + cx] = c ? 1.f : 0.f;  // corner flag for now
+            any |= c;
+        }
+        if (any) atomicOr(&s_any, 1);
+        __syncthreads();
+        if (s_any) break;
+        barrier = 5;
+        __syncthreads();
+    }
+    if (!s_any) return;
+    // filter + Shi-Tomasi; non-candidates get -inf, NaN maps to -inf too (sorts last)
+    for (int i = threadIdx.x; i < span * span; i += 256) {
+        const int cy = lo + i / span, cx = lo + i % span;
+        float v = -INFINITY;
+        if (s_sc[cy * g + cx] != 0.f) {
+            const int x = cx + x_start, y = cy + y_start;
+            if (!(x < 20 || y < 20 || x >= w - 20 || y >= h - 20) && occ[(size_t)y * w + x] != 255) {
+                const float s = shi_tomasi(s_img + (cy + kDsoHalo) * S + cx + kDsoHalo, S);
+                v = isnan(s) ? -INFINITY : s;
+                if (v == -INFINITY) v = -3.4e38f;  // a candidate, ordered after every finite score
+            }
+        }
+        s_sc[cy * g + cx] = v;
+    }
+    __syncthreads();
+    int taken = 0;
+    for (int r = 0; r < 3; r++) {
+        if (threadIdx.x == 0) s_best = 0ull;
+        __syncthreads();
+        unsigned long long best = 0ull;
+        for (int i = threadIdx.x; i < span * span; i += 256) {
+            const int cy = lo + i / span, cx = lo + i % span;
+            const float v = s_sc[cy * g + cx];
+            if (v == -INFINITY) continue;
+            // order-preserving float -> uint32, then prefer the lower scan index
+            uint32_t u = __float_as_uint(v);
+            u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+            const unsigned long long key = ((unsigned long long)u << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)i);
+            best = key > best ? key : best;
+        }
+        for (int o = 32; o >= 1; o >>= 1) {
+            const unsigned long long t = __shfl_xor(best, o, 64);
+            best = t > best ? t : best;
+        }
+        if ((threadIdx.x & 63) == 0 && best) atomicMax(&s_best, best);
+        __syncthreads();
+        const unsigned long long b = s_best;
+        if (!b) break;
+        const int i = (int)(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFu));
+        const int cy = lo + i / span, cx = lo + i % span;
+        if (threadIdx.x == 0) {
+            out_keys[(size_t)k * 3 + r] = (uint32_t)(cx + x_start) | ((uint32_t)(cy + y_start) << 16);
+            s_sc[cy * g + cx] = -INFINITY;
+        }
+        taken++;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out_cnt[k] = taken;
+}
+
+// compaction in cell order -> keypoints rows [row0, row0 + total)
+__global__ __launch_bounds__(1024) void k_dso_finish(const uint32_t *__restrict__ keys,
+                                                     const int *__restrict__ cnt, int ncells,
+                                                     ygzfe_kp *__restrict__ kps, int row0,
+                                                     int *__restrict__ total) {
+    __shared__ int s_scan[1024];
+    int base = 0;
+    for (int c0 = 0; c0 < ncells; c0 += 1024) {
+        const int c = c0 + threadIdx.x;
+        const int n = c < ncells ? cnt[c] : 0;
+        s_scan[threadIdx.x] = n;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const int v = threadIdx.x >= o ? s_scan[threadIdx.x - o] : 0;
+            __syncthreads();
+            s_scan[threadIdx.x] += v;
+            __syncthreads();
+        }
+        const int pos = base + s_scan[threadIdx.x] - n;
+        for (int j = 0; j < n; j++) {
+            const uint32_t kk = keys[(size_t)c * 3 + j];
+            ygzfe_kp kp;
+            kp.x = (float)(kk & 0xFFFF);
+            kp.y = (float)(kk >> 16);
+            kp.size = 7.f;
+            kp.angle = -1.f;
+            kp.response = 0.f;
+            kp.octave = 0;
+            kp.class_id = -1;
+            kps[row0 + pos + j] = kp;
+        }
+        base += s_scan[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = base;
+}
+
+__global__ void k_mark_occupancy(const ygzfe_kp *__restrict__ kps, int n, uint8_t *__restrict__ occ, int w,
+                                 int h) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int x = (int)__builtin_rintf(kps[i].x), y = (int)__builtin_rintf(kps[i].y);
+    if (x >= 0 && y >= 0 && x < w && y < h) occ[(size_t)y * w + x] = 255;
+}
+
+hipError_t launch_dso_occupancy(const ygzfe_kp *kps, int n, uint8_t *occ, int w, int h, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(occ, 0, (size_t)w * h, st);
+    if (e != hipSuccess || n <= 0) return e;
+    hipLaunchKernelGGL(k_mark_occupancy, dim3((n + 255) / 256), dim3(256), 0, st, kps, n, occ, w, h);
+    return hipGetLastError();
+}
+
+hipError_t launch_dso_pass(const uint8_t *img, int w, int h, int g, const uint8_t *occ, uint32_t *keys, int *cnt,
+                           hipStream_t st) {
+    const int ncells = (h / g) * (w / g);
+    if (ncells <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dso_cells, dim3(ncells), dim3(256), 0, st, img, w, h, g, occ, keys, cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_dso_finish2(const uint32_t *keys, const int *cnt, int ncells, ygzfe_kp *kps, int row0,
+                              int *total, hipStream_t st) {
+    hipLaunchKernelGGL(k_dso_finish, dim3(1), dim3(1024), 0, st, keys, cnt, ncells, kps, row0, total);
+    return hipGetLastError();
+}
+
+}  // namespace ygzfe

@@ -1,0 +1,69 @@
+// kernels.hpp — host launchers of the gfx950 kernels (defined in *.hip).
+#pragma once
+#include "common.hpp"
+
+namespace ygzfe {
+
+// extract.hip
+hipError_t upload_pattern(const int *pat);
+hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const int *dtabs,
+                          int nframes, hipStream_t st);
+hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
+                       int nframes, hipStream_t st);
+hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const CellDesc *dcells,
+                       uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st);
+hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
+                         uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int nframes,
+                         hipStream_t st);
+hipError_t launch_orient_desc(const uint8_t *pyr, const uint8_t *blur, uint32_t pitch, const Plan &hp,
+                              const Plan *dp, const uint32_t *sel, const int *selcnt, const int *n_existing,
+                              ygzfe_kp *kps, uint8_t *desc, int *counts, int row_cap, int nframes,
+                              hipStream_t st);
+hipError_t launch_desc_existing(const uint8_t *pyr, const uint8_t *blur, const Plan *dp, ygzfe_kp *kps,
+                                uint8_t *desc, int n, int recompute_angle, hipStream_t st);
+
+// dso.hip
+hipError_t launch_dso_occupancy(const ygzfe_kp *kps, int n, uint8_t *occ, int w, int h, hipStream_t st);
+hipError_t launch_dso_pass(const uint8_t *img, int w, int h, int g, const uint8_t *occ, uint32_t *keys, int *cnt,
+                           hipStream_t st);
+hipError_t launch_dso_finish2(const uint32_t *keys, const int *cnt, int ncells, ygzfe_kp *kps, int row0,
+                              int *total, hipStream_t st);
+constexpr int kDsoMaxGridHost = 96;
+
+// hamming.hip
+hipError_t launch_hamming_best2(const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *bi, int32_t *bd,
+                                int32_t *sd, hipStream_t st);
+hipError_t launch_hamming_best2_pairs(const uint8_t *desc, const int32_t *counts, int row_cap, int npairs,
+                                      const int32_t *qframe, const int32_t *tframe, int32_t *bi, int32_t *bd,
+                                      int32_t *sd, hipStream_t st);
+hipError_t launch_hamming_csr(const uint8_t *q, int nq, const uint8_t *t, const int32_t *row_ptr,
+                              const int32_t *cand, int32_t *dist, hipStream_t st);
+
+// align.hip
+struct AlignLevels {
+    int w[kMaxLevels], h[kMaxLevels];
+    uint32_t off[kMaxLevels];
+    float inv_scale[kMaxLevels];
+};
+struct AlignJob {
+    const uint8_t *ref_pyr, *cur_pyr;
+    const ygzfe_kp *kps;
+    const float *xyz;
+    const uint8_t *usable;
+    int n;
+    int max_level, min_level;
+    ygzfe_se3 T_init;
+};
+hipError_t launch_sparse_align(const AlignLevels &lv, const ygzfe_camera &cam, const AlignJob *jobs,
+                               int njobs, float *scratch, size_t scratch_per_job, ygzfe_align_result *out,
+                               hipStream_t st);
+size_t sparse_align_scratch_floats(int n);
+hipError_t launch_align2d(const uint8_t *img, int w, int h, int n, const uint8_t *pwb, const uint8_t *p,
+                          int n_iter, float *px, uint8_t *conv, hipStream_t st);
+hipError_t launch_find_direct(const uint8_t *const *ref_pyrs, const AlignLevels &ref_lv, const uint8_t *cur_pyr,
+                              const AlignLevels &cur_lv, int nlevels, const float *scale, float inv_sigma2_1,
+                              const ygzfe_camera &cam, int n, const int32_t *ref_index, const ygzfe_kp *kp_ref,
+                              const float *pt_ref, const ygzfe_se3 *T_cr, float *px, int32_t *level,
+                              uint8_t *ok, hipStream_t st);
+
+}  // namespace ygzfe

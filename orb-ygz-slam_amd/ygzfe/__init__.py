@@ -1,0 +1,417 @@
+"""ygzfe — Python view of the MI355X front-end C ABI (include/ygzfe.h).
+
+Mirrors the reference's hot-path interfaces so tests read like the reference:
+  ORBextractor      ORBextractor.h:37-192   (ctor, operator(), ComputePyramid, getters)
+  Frame             Frame::mvImagePyramid   (device-resident pyramid)
+  ORBmatcher        ORBmatcher.h:38-178     (DescriptorDistance, dense / windowed search)
+  SparseImgAlign    SparseImageAlign.h:37-60 (run)
+  Align2D / FindDirectProjection            Align.h:20-26, ORBmatcher.cc:1573-1602
+  Batch             many frames resident in HBM (bench / multi-GPU path)
+
+All compute runs in lib/libygzfe.so on the GPU; there is no CPU fallback: the
+module raises if the library or a HIP device is missing.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libygzfe.so")
+SYNTH_PATH = os.path.join(PKG_ROOT, "lib", "libygzsynth.so")
+
+MAX_LEVELS = 16
+ORBSLAM_KEYPOINT, FAST_KEYPOINT, DSO_KEYPOINT = 0, 1, 2
+BLUR_CV4, BLUR_CV3 = 0, 1
+OK, EINVAL, EHIP, ECAP, ENOMEM, ESTATE = 0, -1, -2, -3, -4, -5
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+class YgzfeError(RuntimeError):
+    pass
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32), ("blur_variant", C.c_int32)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float)]
+
+
+class SE3(C.Structure):
+    _fields_ = [("q", C.c_float * 4), ("t", C.c_float * 3)]
+
+    @staticmethod
+    def make(q=(0, 0, 0, 1), t=(0, 0, 0)):
+        s = SE3()
+        for i in range(4):
+            s.q[i] = float(q[i])
+        for i in range(3):
+            s.t[i] = float(t[i])
+        return s
+
+    def as_arrays(self):
+        return np.array(self.q[:], np.float32), np.array(self.t[:], np.float32)
+
+
+class AlignResult(C.Structure):
+    _fields_ = [("T_cur_ref", SE3), ("n_visible", C.c_int32), ("chi2", C.c_float), ("H", C.c_float * 36)]
+
+
+SE3_DTYPE = np.dtype([("q", "<f4", 4), ("t", "<f4", 3)])
+ALIGN_RESULT_DTYPE = np.dtype([("q", "<f4", 4), ("t", "<f4", 3), ("n_visible", "<i4"), ("chi2", "<f4"),
+                               ("H", "<f4", 36)])
+
+_lib = None
+
+
+def lib():
+    """Load libygzfe.so; raise loudly when it is absent (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise YgzfeError(f"{LIB_PATH} missing: run `make -C orb-ygz-slam_amd` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        L.ygzfe_last_error.restype = C.c_char_p
+        L.ygzfe_batch_stream.restype = C.c_void_p
+        _lib = L
+    return _lib
+
+
+def _check(rc, what=""):
+    if rc != OK:
+        msg = lib().ygzfe_last_error().decode(errors="replace")
+        raise YgzfeError(f"{what} failed ({rc}): {msg}")
+    return rc
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+def device_count():
+    return lib().ygzfe_device_count()
+
+
+class Frame:
+    """Device-resident pyramid (Frame::mvImagePyramid)."""
+
+    def __init__(self, extractor, width, height):
+        self.ex = extractor
+        self.width, self.height = width, height
+        self.h = C.c_void_p()
+        _check(lib().ygzfe_frame_create(extractor.h, width, height, C.byref(self.h)), "frame_create")
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().ygzfe_frame_destroy(self.h)
+            self.h = None
+
+    def level(self, l):
+        w = C.c_int()
+        h = C.c_int()
+        _check(lib().ygzfe_frame_level(self.h, l, C.byref(w), C.byref(h), None, 0), "frame_level")
+        out = np.zeros((h.value, w.value), np.uint8)
+        _check(lib().ygzfe_frame_level(self.h, l, None, None, _p(out), w.value), "frame_level")
+        return out
+
+    def levels(self):
+        return [self.level(l) for l in range(self.ex.nlevels)]
+
+    def set_level(self, l, img):
+        img = np.ascontiguousarray(img, np.uint8)
+        _check(lib().ygzfe_frame_set_level(self.h, l, _p(img), img.shape[1]), "frame_set_level")
+
+
+class ORBextractor:
+    """ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST) (ORBextractor.h:53-57)."""
+
+    def __init__(self, nfeatures=500, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7, device=0,
+                 blur=BLUR_CV4):
+        self.params = OrbParams(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, blur)
+        self.nlevels = nlevels
+        self.h = C.c_void_p()
+        _check(lib().ygzfe_extractor_create(C.byref(self.params), device, C.byref(self.h)), "extractor_create")
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().ygzfe_extractor_destroy(self.h)
+            self.h = None
+
+    # getters (ORBextractor.h:87-109)
+    def GetLevels(self):
+        return self.nlevels
+
+    def GetScaleFactor(self):
+        return self.params.scale_factor
+
+    def _levels(self):
+        arrs = [np.zeros(MAX_LEVELS, np.float32) for _ in range(4)]
+        _check(lib().ygzfe_extractor_levels(self.h, None, *[_p(a) for a in arrs]), "levels")
+        return [a[:self.nlevels] for a in arrs]
+
+    def GetScaleFactors(self):
+        return self._levels()[0]
+
+    def GetInverseScaleFactors(self):
+        return self._levels()[1]
+
+    def GetScaleSigmaSquares(self):
+        return self._levels()[2]
+
+    def GetInverseScaleSigmaSquares(self):
+        return self._levels()[3]
+
+    def FeaturesPerLevel(self):
+        out = np.zeros(MAX_LEVELS, np.int32)
+        _check(lib().ygzfe_extractor_features_per_level(self.h, _p(out)), "features_per_level")
+        return out[:self.nlevels].tolist()
+
+    @property
+    def dso_grid(self):
+        g = C.c_int32()
+        _check(lib().ygzfe_extractor_dso_grid(self.h, C.byref(g), None), "dso_grid")
+        return g.value
+
+    @dso_grid.setter
+    def dso_grid(self, v):
+        g = C.c_int32(v)
+        _check(lib().ygzfe_extractor_dso_grid(self.h, None, C.byref(g)), "dso_grid")
+
+    def ComputePyramid(self, image, frame=None):
+        """Frame::ComputeImagePyramid -> a device Frame holding mvImagePyramid."""
+        image = np.ascontiguousarray(image, np.uint8)
+        H, W = image.shape
+        frame = frame if frame is not None else Frame(self, W, H)
+        _check(lib().ygzfe_compute_pyramid(self.h, frame.h, _p(image), W), "compute_pyramid")
+        return frame
+
+    def extract(self, frame, method=ORBSLAM_KEYPOINT, existing=None, cap=None):
+        """operator()(Frame*, keypoints, descriptors, method) (ORBextractor.cc:1031-1127).
+
+        Returns (keypoints[KP_DTYPE], descriptors uint8[n,32]); rows of `existing`
+        come first (their angles are recomputed in DSO mode, as the reference does)."""
+        existing = np.zeros(0, KP_DTYPE) if existing is None else np.ascontiguousarray(existing, KP_DTYPE)
+        ne = len(existing)
+        cap = cap or (ne + 8192)
+        kps = np.zeros(cap, KP_DTYPE)
+        kps[:ne] = existing
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int()
+        rc = lib().ygzfe_extract(self.h, frame.h, method, _p(kps), ne, cap, _p(desc), C.byref(n))
+        if rc == ECAP:
+            return self.extract(frame, method, existing, cap=n.value)
+        _check(rc, "extract")
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def __call__(self, image, mask=None):
+        """operator()(image, mask, keypoints, descriptors) (ORBextractor.cc:970-1028)."""
+        frame = self.ComputePyramid(image)
+        return self.extract(frame, ORBSLAM_KEYPOINT)
+
+
+class ORBmatcher:
+    """Hamming hot subset of ORBmatcher (ORBmatcher.h:38-178)."""
+
+    TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30
+
+    def __init__(self, nnratio=0.6, checkOri=True, device=0):
+        self.nnratio, self.checkOri, self.device = nnratio, checkOri, device
+
+    @staticmethod
+    def DescriptorDistance(a, b):
+        a = np.ascontiguousarray(a, np.uint8)
+        b = np.ascontiguousarray(b, np.uint8)
+        return lib().ygzfe_descriptor_distance(_p(a), _p(b))
+
+    def best2(self, query, train):
+        q = np.ascontiguousarray(query, np.uint8).reshape(-1, 32)
+        t = np.ascontiguousarray(train, np.uint8).reshape(-1, 32)
+        nq = len(q)
+        bi = np.zeros(nq, np.int32)
+        bd = np.zeros(nq, np.int32)
+        sd = np.zeros(nq, np.int32)
+        _check(lib().ygzfe_hamming_best2(self.device, _p(q), nq, _p(t), len(t), _p(bi), _p(bd), _p(sd)),
+               "hamming_best2")
+        return bi, bd, sd
+
+    def window_distances(self, query, train, row_ptr, cand):
+        q = np.ascontiguousarray(query, np.uint8).reshape(-1, 32)
+        t = np.ascontiguousarray(train, np.uint8).reshape(-1, 32)
+        row_ptr = np.ascontiguousarray(row_ptr, np.int32)
+        cand = np.ascontiguousarray(cand, np.int32)
+        out = np.zeros(max(1, len(cand)), np.int32)
+        _check(lib().ygzfe_hamming_csr(self.device, _p(q), len(q), _p(t), len(t), _p(row_ptr), _p(cand), _p(out)),
+               "hamming_csr")
+        return out[:len(cand)]
+
+
+class SparseImgAlign:
+    """SparseImgAlign(n_levels, min_level, n_iter=10) (SparseImageAlign.h:37-60)."""
+
+    def __init__(self, max_level, min_level, n_iter=10):
+        self.max_level, self.min_level = max_level, min_level
+
+    def run(self, ref_frame, cur_frame, cam, kps, xyz_ref, usable, T_init):
+        kps = np.ascontiguousarray(kps, KP_DTYPE)
+        xyz = np.ascontiguousarray(xyz_ref, np.float32).reshape(-1, 3)
+        us = np.ascontiguousarray(usable, np.uint8)
+        res = AlignResult()
+        _check(lib().ygzfe_sparse_align(ref_frame.h, cur_frame.h, C.byref(cam), _p(kps), _p(xyz), _p(us), len(kps),
+                                        self.max_level, self.min_level, C.byref(T_init), C.byref(res)),
+               "sparse_align")
+        return res
+
+
+def align2d_batch(cur_frame, level, patches_with_border, patches, px, n_iter=10):
+    pwb = np.ascontiguousarray(patches_with_border, np.uint8).reshape(-1, 100)
+    p = np.ascontiguousarray(patches, np.uint8).reshape(-1, 64)
+    px = np.ascontiguousarray(px, np.float32).reshape(-1, 2).copy()
+    conv = np.zeros(len(px), np.uint8)
+    _check(lib().ygzfe_align2d_batch(cur_frame.h, level, len(px), _p(pwb), _p(p), n_iter, _p(px), _p(conv)),
+           "align2d_batch")
+    return conv.astype(bool), px
+
+
+def find_direct_projection_batch(ref_frames, cur_frame, cam, ref_index, kp_ref, pt_ref, T_cr, px):
+    refs = (C.c_void_p * len(ref_frames))(*[f.h.value for f in ref_frames])
+    ref_index = np.ascontiguousarray(ref_index, np.int32)
+    kp_ref = np.ascontiguousarray(kp_ref, KP_DTYPE)
+    pt_ref = np.ascontiguousarray(pt_ref, np.float32).reshape(-1, 3)
+    T_cr = np.ascontiguousarray(T_cr, SE3_DTYPE)
+    px = np.ascontiguousarray(px, np.float32).reshape(-1, 2).copy()
+    n = len(px)
+    lvl = np.zeros(n, np.int32)
+    ok = np.zeros(n, np.uint8)
+    _check(lib().ygzfe_find_direct_projection_batch(refs, cur_frame.h, C.byref(cam), n, _p(ref_index), _p(kp_ref),
+                                                    _p(pt_ref), _p(T_cr), _p(px), _p(lvl), _p(ok)),
+           "find_direct_projection_batch")
+    return px, lvl, ok.astype(bool)
+
+
+class Batch:
+    """Frames resident in HBM, one launch per stage (the bench / multi-GPU path)."""
+
+    def __init__(self, params_or_extractor_args, device, width, height, max_frames):
+        p = params_or_extractor_args
+        if not isinstance(p, OrbParams):
+            p = OrbParams(*p)
+        self.params = p
+        self.device, self.width, self.height, self.max_frames = device, width, height, max_frames
+        self.h = C.c_void_p()
+        _check(lib().ygzfe_batch_create(C.byref(p), device, width, height, max_frames, C.byref(self.h)),
+               "batch_create")
+        pitch = C.c_size_t()
+        cap = C.c_int()
+        nl = C.c_int()
+        _check(lib().ygzfe_batch_info(self.h, C.byref(pitch), C.byref(cap), C.byref(nl)), "batch_info")
+        self.frame_pitch, self.kp_cap, self.nlevels = pitch.value, cap.value, nl.value
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().ygzfe_batch_destroy(self.h)
+            self.h = None
+
+    @property
+    def stream(self):
+        return lib().ygzfe_batch_stream(self.h)
+
+    def upload(self, frames):
+        frames = np.ascontiguousarray(frames, np.uint8)
+        _check(lib().ygzfe_batch_upload(self.h, _p(frames), len(frames)), "batch_upload")
+
+    def bind(self, pyramids=0, kps=0, desc=0, counts=0):
+        _check(lib().ygzfe_batch_bind_buffers(self.h, C.c_void_p(pyramids or None), C.c_void_p(kps or None),
+                                              C.c_void_p(desc or None), C.c_void_p(counts or None)), "bind")
+
+    def extract(self, n_frames, stream=None):
+        _check(lib().ygzfe_batch_extract(self.h, n_frames, C.c_void_p(stream)), "batch_extract")
+
+    def check(self):
+        _check(lib().ygzfe_batch_check(self.h), "batch_check")
+
+    def result(self, i):
+        kps = np.zeros(self.kp_cap, KP_DTYPE)
+        desc = np.zeros((self.kp_cap, 32), np.uint8)
+        n = C.c_int()
+        _check(lib().ygzfe_batch_result(self.h, i, _p(kps), self.kp_cap, _p(desc), C.byref(n)), "batch_result")
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def match(self, n_pairs, d_qframe, d_tframe, d_bi, d_bd, d_sd, stream=None):
+        _check(lib().ygzfe_batch_match(self.h, n_pairs, C.c_void_p(d_qframe), C.c_void_p(d_tframe), C.c_void_p(d_bi),
+                                       C.c_void_p(d_bd), C.c_void_p(d_sd), C.c_void_p(stream)), "batch_match")
+
+    def sparse_align(self, n_pairs, d_ref_idx, d_cur_idx, d_xyz, d_usable, cam, max_level, min_level, d_T_init,
+                     d_out, stream=None):
+        _check(lib().ygzfe_batch_sparse_align(self.h, n_pairs, C.c_void_p(d_ref_idx), C.c_void_p(d_cur_idx),
+                                              C.c_void_p(d_xyz), C.c_void_p(d_usable), C.byref(cam), max_level,
+                                              min_level, C.c_void_p(d_T_init), C.c_void_p(d_out),
+                                              C.c_void_p(stream)), "batch_sparse_align")
+
+    def timing(self, enable=True):
+        ms = (C.c_float * 16)()
+        names = (C.c_char_p * 16)()
+        n = lib().ygzfe_batch_timing(self.h, int(enable), ms, names, 16)
+        return {names[i].decode(): ms[i] for i in range(n)}
+
+
+# ---------------------------------------------------------------- synthetic inputs (tests / bench)
+_synth = None
+
+
+def synth():
+    global _synth
+    if _synth is None:
+        if not os.path.exists(SYNTH_PATH):
+            raise YgzfeError(f"{SYNTH_PATH} missing: run `make -C orb-ygz-slam_amd`")
+        _synth = C.CDLL(SYNTH_PATH)
+        _synth.ygzs_backproject_plane.restype = C.c_int
+    return _synth
+
+
+def synth_texture(seed, W, H):
+    out = np.zeros((H, W), np.uint8)
+    synth().ygzs_texture(C.c_uint64(seed), W, H, _p(out))
+    return out
+
+
+EUROC_CAM = (458.654, 457.296, 367.215, 248.375)
+
+
+def trajectory_pose(k, xi):
+    q = np.zeros(4, np.float32)
+    t = np.zeros(3, np.float32)
+    xi = np.ascontiguousarray(xi, np.float32)
+    synth().ygzs_trajectory_pose(k, _p(xi), _p(q), _p(t))
+    return q, t
+
+
+def render_plane(tex, texel, plane_z, cam, q_cw, t_cw, W, H, noise_seed=0, noise_amp=2):
+    tex = np.ascontiguousarray(tex, np.uint8)
+    out = np.zeros((H, W), np.uint8)
+    camv = np.array(cam, np.float32)
+    synth().ygzs_render_plane(_p(tex), tex.shape[1], tex.shape[0], C.c_double(texel), C.c_double(plane_z),
+                              _p(camv), _p(np.ascontiguousarray(q_cw, np.float32)),
+                              _p(np.ascontiguousarray(t_cw, np.float32)), W, H, C.c_uint64(noise_seed), noise_amp,
+                              _p(out))
+    return out
+
+
+def backproject_plane(cam, q_cw, t_cw, uv, plane_z):
+    camv = np.array(cam, np.float32)
+    q = np.ascontiguousarray(q_cw, np.float32)
+    t = np.ascontiguousarray(t_cw, np.float32)
+    uv = np.asarray(uv, np.float32).reshape(-1, 2)
+    out = np.zeros((len(uv), 3), np.float32)
+    ok = np.zeros(len(uv), np.uint8)
+    P = np.zeros(3, np.float32)
+    for i, (u, v) in enumerate(uv):
+        ok[i] = synth().ygzs_backproject_plane(_p(camv), _p(q), _p(t), C.c_float(u), C.c_float(v),
+                                               C.c_double(plane_z), _p(P))
+        out[i] = P
+    return out, ok

@@ -1,0 +1,291 @@
+"""ctypes view of the CPU oracle (oracle/build/libygzoracle.so).
+
+TEST INFRASTRUCTURE ONLY: the parity checker for the HIP product path.  The
+functions mirror oracle/ygz_oracle.h; numpy arrays in, numpy arrays out.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "build", "libygzoracle.so")
+REF_FAST_PATH = os.path.join(ORACLE_DIR, "_ref", "libfastref.so")
+
+MAXL = 16
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KP_DTYPE.itemsize == 28
+
+
+class Orb(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_double), ("nlevels", C.c_int),
+                ("ini_th", C.c_int), ("min_th", C.c_int), ("blur_variant", C.c_int),
+                ("scale", C.c_float * MAXL), ("inv_scale", C.c_float * MAXL),
+                ("sigma2", C.c_float * MAXL), ("inv_sigma2", C.c_float * MAXL),
+                ("feat_per_level", C.c_int * MAXL), ("umax", C.c_int * 16), ("dso_grid", C.c_int)]
+
+
+class Cam(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float)]
+
+
+class SE3(C.Structure):
+    _fields_ = [("q", C.c_float * 4), ("t", C.c_float * 3)]
+
+
+class AlignOut(C.Structure):
+    _fields_ = [("T", SE3), ("n_visible", C.c_int), ("chi2", C.c_float),
+                ("iters", C.c_int * MAXL), ("H", C.c_float * 36)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", ORACLE_DIR], stdout=subprocess.DEVNULL)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def se3_from(q, t):
+    s = SE3()
+    for i in range(4):
+        s.q[i] = float(q[i])
+    for i in range(3):
+        s.t[i] = float(t[i])
+    return s
+
+
+class OrbOracle:
+    """ORBextractor restated (ORBextractor.cc:412-470)."""
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7,
+                 blur_variant=0):
+        self.o = Orb()
+        lib().ygzo_orb_init(C.byref(self.o), nfeatures, C.c_float(scale_factor), nlevels, ini_th,
+                            min_th, blur_variant)
+        self.nlevels = nlevels
+
+    @property
+    def feat_per_level(self):
+        return [self.o.feat_per_level[i] for i in range(self.nlevels)]
+
+    @property
+    def scale(self):
+        return np.array([self.o.scale[i] for i in range(self.nlevels)], np.float32)
+
+    @property
+    def inv_scale(self):
+        return np.array([self.o.inv_scale[i] for i in range(self.nlevels)], np.float32)
+
+    @property
+    def inv_sigma2(self):
+        return np.array([self.o.inv_sigma2[i] for i in range(self.nlevels)], np.float32)
+
+    @property
+    def umax(self):
+        return [self.o.umax[i] for i in range(16)]
+
+    def level_sizes(self, W, H):
+        w = (C.c_int * MAXL)()
+        h = (C.c_int * MAXL)()
+        lib().ygzo_level_sizes(C.byref(self.o), W, H, w, h)
+        return [(w[i], h[i]) for i in range(self.nlevels)]
+
+    def pyramid(self, img):
+        img = np.ascontiguousarray(img, np.uint8)
+        H, W = img.shape
+        sizes = self.level_sizes(W, H)
+        levels = [np.zeros((h, w), np.uint8) for (w, h) in sizes]
+        ptrs = (C.c_void_p * MAXL)(*[l.ctypes.data for l in levels])
+        lib().ygzo_compute_pyramid(C.byref(self.o), _p(img), W, H, W, ptrs)
+        return levels
+
+    def _lvl_args(self, levels):
+        ptrs = (C.c_void_p * MAXL)(*[l.ctypes.data for l in levels])
+        lw = (C.c_int * MAXL)(*[l.shape[1] for l in levels])
+        lh = (C.c_int * MAXL)(*[l.shape[0] for l in levels])
+        return ptrs, lw, lh
+
+    def extract(self, levels, existing=None, cap=None):
+        """ORBSLAM_KEYPOINT extraction on a prebuilt pyramid -> (kps, desc)."""
+        existing = np.zeros(0, KP_DTYPE) if existing is None else np.ascontiguousarray(existing, KP_DTYPE)
+        cap = cap or (sum(self.feat_per_level) + 8 * self.nlevels + len(existing))
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        ptrs, lw, lh = self._lvl_args(levels)
+        n = lib().ygzo_extract_orbslam(C.byref(self.o), ptrs, lw, lh, _p(existing), len(existing),
+                                       _p(kps), _p(desc), cap)
+        assert n >= 0
+        return kps[:n].copy(), desc[:n].copy()
+
+    def extract_dso(self, levels, existing=None, cap=4096):
+        existing = np.zeros(0, KP_DTYPE) if existing is None else np.ascontiguousarray(existing, KP_DTYPE).copy()
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        ptrs, lw, lh = self._lvl_args(levels)
+        n = lib().ygzo_extract_dso(C.byref(self.o), ptrs, lw, lh, _p(existing), len(existing),
+                                   _p(kps), _p(desc), cap)
+        assert n >= 0
+        return kps[:n].copy(), desc[:n].copy(), existing
+
+    def octree_level(self, lvl, level, cap=8192):
+        lvl = np.ascontiguousarray(lvl, np.uint8)
+        out = np.zeros(cap, KP_DTYPE)
+        nc = C.c_int()
+        n = lib().ygzo_octree_level(C.byref(self.o), _p(lvl), lvl.shape[1], lvl.shape[0], level,
+                                    _p(out), cap, C.byref(nc))
+        return out[:n].copy(), nc.value
+
+    def ic_angle(self, img, x, y):
+        lib().ygzo_ic_angle.restype = C.c_float
+        return lib().ygzo_ic_angle(_p(img), img.shape[1], img.shape[0], img.shape[1], C.c_float(x),
+                                   C.c_float(y), self.o.umax)
+
+
+def blur7(img, variant=0):
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros_like(img)
+    lib().ygzo_gaussian_blur7(_p(img), img.shape[1], img.shape[0], img.shape[1], _p(out),
+                              img.shape[1], variant)
+    return out
+
+
+def resize(src, dw, dh):
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros((dh, dw), np.uint8)
+    lib().ygzo_resize(_p(src), src.shape[1], src.shape[0], src.shape[1], _p(out), dw, dh, dw)
+    return out
+
+
+def fast9_roi(roi, threshold, cap=8192):
+    roi = np.ascontiguousarray(roi, np.uint8)
+    xs = np.zeros(cap, np.int16)
+    ys = np.zeros(cap, np.int16)
+    sc = np.zeros(cap, np.uint8)
+    n = lib().ygzo_fast9_roi(_p(roi), roi.shape[1], roi.shape[0], roi.shape[1], threshold,
+                             _p(xs), _p(ys), _p(sc), cap)
+    return xs[:n].copy(), ys[:n].copy(), sc[:n].copy()
+
+
+def fast10_detect(img, barrier, sse=True, x0=0, y0=0, w=None, h=None, cap=1 << 20):
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape
+    w = W - x0 if w is None else w
+    h = H - y0 if h is None else h
+    xs = np.zeros(cap, np.int16)
+    ys = np.zeros(cap, np.int16)
+    fn = lib().ygzo_fast10_detect_sse2 if sse else lib().ygzo_fast10_detect_plain
+    ptr = C.c_void_p(img.ctypes.data + y0 * W + x0)
+    n = fn(ptr, w, h, W, barrier, _p(xs), _p(ys), cap)
+    return xs[:n].copy(), ys[:n].copy()
+
+
+def fast10_scores(img, xs, ys, threshold, x0=0, y0=0):
+    img = np.ascontiguousarray(img, np.uint8)
+    W = img.shape[1]
+    out = np.zeros(len(xs), np.int32)
+    for i, (x, y) in enumerate(zip(xs, ys)):
+        ptr = C.c_void_p(img.ctypes.data + (int(y) + y0) * W + int(x) + x0)
+        out[i] = lib().ygzo_fast10_score(ptr, W, threshold)
+    return out
+
+
+def fast10_nonmax(xs, ys, scores):
+    xs = np.ascontiguousarray(xs, np.int16)
+    ys = np.ascontiguousarray(ys, np.int16)
+    scores = np.ascontiguousarray(scores, np.int32)
+    keep = np.zeros(max(1, len(xs)), np.int32)
+    n = lib().ygzo_fast10_nonmax(_p(xs), _p(ys), _p(scores), len(xs), _p(keep))
+    return keep[:n].copy()
+
+
+def hamming_best2(q, t):
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t, np.uint8)
+    nq = len(q)
+    bi = np.zeros(nq, np.int32)
+    bd = np.zeros(nq, np.int32)
+    sd = np.zeros(nq, np.int32)
+    lib().ygzo_hamming_best2(_p(q), nq, _p(t), len(t), _p(bi), _p(bd), _p(sd))
+    return bi, bd, sd
+
+
+def sparse_align(ref_levels, cur_levels, inv_scale, cam, kps, xyz_ref, usable, max_level,
+                 min_level, T_init):
+    rp = (C.c_void_p * MAXL)(*[l.ctypes.data for l in ref_levels])
+    cp = (C.c_void_p * MAXL)(*[l.ctypes.data for l in cur_levels])
+    lw = (C.c_int * MAXL)(*[l.shape[1] for l in ref_levels])
+    lh = (C.c_int * MAXL)(*[l.shape[0] for l in ref_levels])
+    inv = (C.c_float * MAXL)(*[float(v) for v in inv_scale])
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    xyz = np.ascontiguousarray(xyz_ref, np.float32)
+    us = np.ascontiguousarray(usable, np.uint8)
+    out = AlignOut()
+    lib().ygzo_sparse_align(rp, cp, lw, lh, inv, C.byref(cam), _p(kps), _p(xyz), _p(us), len(kps),
+                            max_level, min_level, C.byref(T_init), C.byref(out))
+    return out
+
+
+def align2d(cur, rpb, rp, px, n_iter=10):
+    cur = np.ascontiguousarray(cur, np.uint8)
+    px = np.array(px, np.float32)
+    ok = lib().ygzo_align2d(_p(cur), cur.shape[1], cur.shape[0], cur.shape[1],
+                            _p(np.ascontiguousarray(rpb, np.uint8)),
+                            _p(np.ascontiguousarray(rp, np.uint8)), n_iter, _p(px))
+    return bool(ok), px
+
+
+class RefFast:
+    """The reference's own Thirdparty/fast, compiled by oracle/Makefile (oracle/_ref)."""
+
+    def __init__(self):
+        self.lib = C.CDLL(REF_FAST_PATH)
+
+    @staticmethod
+    def available():
+        return os.path.exists(REF_FAST_PATH)
+
+    def detect(self, img, barrier, sse=True, x0=0, y0=0, w=None, h=None, cap=1 << 20):
+        img = np.ascontiguousarray(img, np.uint8)
+        H, W = img.shape
+        w = W - x0 if w is None else w
+        h = H - y0 if h is None else h
+        xs = np.zeros(cap, np.int16)
+        ys = np.zeros(cap, np.int16)
+        ptr = C.c_void_p(img.ctypes.data + y0 * W + x0)
+        n = self.lib.ref_fast10_detect(ptr, w, h, W, barrier, int(sse), _p(xs), _p(ys), cap)
+        return xs[:n].copy(), ys[:n].copy()
+
+    def scores(self, img, xs, ys, threshold, x0=0, y0=0):
+        img = np.ascontiguousarray(img, np.uint8)
+        W = img.shape[1]
+        xs = np.ascontiguousarray(xs, np.int16)
+        ys = np.ascontiguousarray(ys, np.int16)
+        out = np.zeros(len(xs), np.int32)
+        ptr = C.c_void_p(img.ctypes.data + y0 * W + x0)
+        self.lib.ref_fast10_score(ptr, W, _p(xs), _p(ys), len(xs), threshold, _p(out))
+        return out
+
+    def nonmax(self, xs, ys, scores):
+        xs = np.ascontiguousarray(xs, np.int16)
+        ys = np.ascontiguousarray(ys, np.int16)
+        scores = np.ascontiguousarray(scores, np.int32)
+        keep = np.zeros(max(1, len(xs)), np.int32)
+        n = self.lib.ref_fast10_nonmax(_p(xs), _p(ys), _p(scores), len(xs), _p(keep))
+        return keep[:n].copy()

@@ -1,0 +1,29 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "orb-ygz-slam_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); runs on the GPU box")
+
+
+def gpu_available():
+    try:
+        import ygzfe
+        return ygzfe.device_count() > 0
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import ygzfe
+    n = ygzfe.device_count()
+    if n <= 0:
+        pytest.fail("no HIP device visible: -m gpu tests must run on the GPU box (no CPU fallback exists)")
+    return ygzfe

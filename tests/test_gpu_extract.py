@@ -1,0 +1,136 @@
+"""GPU ORB extraction vs the CPU oracle: bit-exact keypoints and descriptors.
+
+Reference path: ORBextractor::operator()(Frame*, ..., ORBSLAM_KEYPOINT)
+(ORBextractor.cc:1031-1127) and (..., DSO_KEYPOINT) (ORBextractor.cc:1275-1386).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import _scenes as S
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load_test1_png():
+    from PIL import Image
+    return np.array(Image.open(os.path.join(GOLDEN, "test1.png")))
+
+
+def assert_kps_equal(a, b, what=""):
+    assert len(a) == len(b), f"{what}: {len(a)} vs {len(b)} keypoints"
+    for f in a.dtype.names:
+        if not np.array_equal(a[f], b[f]):
+            bad = np.nonzero(a[f] != b[f])[0]
+            raise AssertionError(f"{what}: field {f} differs at rows {bad[:10]}: {a[f][bad[:5]]} vs {b[f][bad[:5]]}")
+
+
+def make(gpu, cfg, blur=0):
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS[cfg]
+    ex = gpu.ORBextractor(nf, sf, nl, ini, mn, blur=blur)
+    orc = O.OrbOracle(nf, sf, nl, ini, mn, blur_variant=blur)
+    return W, H, ex, orc
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C4"])
+def test_pyramid_bitexact(gpu, cfg):
+    W, H, ex, orc = make(gpu, cfg)
+    for seed in (0, 5):
+        img = S.frame(seed, W, H)
+        fr = ex.ComputePyramid(img)
+        ref = orc.pyramid(img)
+        for l, (g, r) in enumerate(zip(fr.levels(), ref)):
+            assert g.shape == r.shape
+            assert np.array_equal(g, r), f"{cfg} level {l}: {np.count_nonzero(g != r)} px differ"
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C4"])
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_extract_orbslam_bitexact(gpu, cfg, seed):
+    W, H, ex, orc = make(gpu, cfg)
+    img = S.frame(seed, W, H)
+    fr = ex.ComputePyramid(img)
+    kg, dg = ex.extract(fr)
+    kr, dr = orc.extract(orc.pyramid(img))
+    assert len(kr) > 100
+    assert_kps_equal(kg, kr, f"{cfg}/{seed}")
+    assert np.array_equal(dg, dr), f"{np.count_nonzero((dg != dr).any(1))} descriptor rows differ"
+
+
+def test_extract_test1_png(gpu):
+    img = load_test1_png()
+    H, W = img.shape
+    ex = gpu.ORBextractor(1000, 2.0, 4, 20, 7)
+    orc = O.OrbOracle(1000, 2.0, 4, 20, 7)
+    kg, dg = ex(img)
+    kr, dr = orc.extract(orc.pyramid(img))
+    assert_kps_equal(kg, kr, "test1.png")
+    assert np.array_equal(dg, dr)
+
+
+def test_extract_blur_cv3(gpu):
+    W, H, ex, orc = make(gpu, "C2", blur=1)
+    img = S.frame(11, W, H)
+    kg, dg = ex.extract(ex.ComputePyramid(img))
+    kr, dr = orc.extract(orc.pyramid(img))
+    assert_kps_equal(kg, kr)
+    assert np.array_equal(dg, dr)
+
+
+def test_extract_with_existing(gpu):
+    """Frame with direct-tracked keypoints: their descriptor rows come first (ORBextractor.cc:1088-1099)."""
+    W, H, ex, orc = make(gpu, "C1")
+    img = S.frame(3, W, H)
+    lv = orc.pyramid(img)
+    base, _ = orc.extract(lv)
+    rng = np.random.default_rng(0)
+    existing = base[rng.choice(len(base), 40, replace=False)].copy()
+    existing["x"] += rng.uniform(-1.5, 1.5, 40).astype(np.float32)
+    existing["angle"] = rng.uniform(0, 360, 40).astype(np.float32)
+    kg, dg = ex.extract(ex.ComputePyramid(img), existing=existing)
+    kr, dr = orc.extract(lv, existing=existing)
+    assert_kps_equal(kg, kr)
+    assert np.array_equal(dg, dr)
+    assert_kps_equal(kg[:40], existing)
+
+
+def test_extract_dso_bitexact_and_state(gpu):
+    """DSO_KEYPOINT: grid state mnGridSize carries across frames (ORBextractor.cc:1295,1380)."""
+    W, H, ex, orc = make(gpu, "C2")
+    for seed in (4, 5, 6):
+        img = S.frame(seed, W, H)
+        lv = orc.pyramid(img)
+        base, _ = orc.extract(lv)
+        existing = base[:60].copy()
+        kg, dg = ex.extract(ex.ComputePyramid(img), method=gpu.DSO_KEYPOINT, existing=existing)
+        kr, dr, ex_r = orc.extract_dso(lv, existing=existing)
+        assert_kps_equal(kg, kr, f"dso seed {seed}")
+        assert np.array_equal(dg, dr)
+        assert ex.dso_grid == orc.o.dso_grid
+
+
+def test_batch_matches_single(gpu):
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    frames = np.stack([S.frame(s, W, H) for s in range(6)])
+    b = gpu.Batch((nf, sf, nl, ini, mn, 0), 0, W, H, 8)
+    b.upload(frames)
+    b.extract(len(frames))
+    b.check()
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    for i in range(len(frames)):
+        kg, dg = b.result(i)
+        kr, dr = orc.extract(orc.pyramid(frames[i]))
+        assert_kps_equal(kg, kr, f"batch frame {i}")
+        assert np.array_equal(dg, dr)
+
+
+def test_featureless_frame(gpu):
+    """Edge case: a flat image has no FAST corners -> empty result, no hang."""
+    W, H, ex, orc = make(gpu, "C2")
+    img = np.full((H, W), 77, np.uint8)
+    kg, dg = ex.extract(ex.ComputePyramid(img))
+    kr, dr = orc.extract(orc.pyramid(img))
+    assert len(kg) == len(kr) == 0
