@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""bench.py — frames/s of the ORB-YGZ-SLAM front-end hot path on MI355X.
+
+Metric (BASELINE.json): frames/sec ORB-extract + SparseImageAlign, 752x480,
+1000 features.  One "step" = one pass of the hot path over one resident batch
+of B synthetic frames (a rendered textured-plane sequence, EuRoC intrinsics):
+  * ORB extraction of all B frames (C2: nFeatures 1000, scale 2.0, 4 levels,
+    FAST 20/7) — pyramid, blur, FAST-9 cells, octree, angle + rBRIEF;
+  * Hamming best/second-best of frame k against frame k-1 (B-1 pairs);
+  * SparseImgAlign of k-1 -> k (B-1 pairs, levels 3..1, 10 GN iterations)
+    with map points = frame k-1's keypoints back-projected on the plane.
+Frames are in HBM before the timed region.  `value` = frames extracted by all
+ranks / wall time (B per rank per step).  N>1: one process per GPU, each with
+its own contiguous slice of the sequence (weak scaling, no data-path
+collective; the batch gather is offline).
+
+The JSON line also carries `roofline` (dominant kernel: algorithmic bytes per
+launch / HIP-event-timed average launch duration vs 8 TB/s) and
+`cpu_baseline` (the oracle/ CPU restatement, single thread, on a bounded
+sample of the same workload).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "orb-ygz-slam_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="frames resident per GPU")
+    ap.add_argument("--cpu-sample", type=int, default=120, help="frames in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    ap.add_argument("--no-align", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import ygzfe
+    import _scenes as S
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    B = args.batch
+    cam = ygzfe.EUROC_CAM
+    sc = S.PlaneScene(11, W, H)
+    # trajectory: per-frame motion (v, w); frame g has pose exp(g * xi)
+    xi = np.array([0.012, -0.006, 0.009, 0.0025, -0.002, 0.0015], np.float32)
+    g0 = rank * B
+    poses = [ygzfe.trajectory_pose(g0 + i, xi) for i in range(B)]
+    t_r = time.time()
+    frames = np.stack([sc.render(q, t, noise_seed=g0 + i) for i, (q, t) in enumerate(poses)])
+    render_s = time.time() - t_r
+
+    batch = ygzfe.Batch((nf, sf, nl, ini, mn, 0), local, W, H, B)
+    cap = batch.kp_cap
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    kps_t = torch.empty((B, cap, 7), dtype=torch.float32, device=dev)
+    counts_t = torch.zeros(B, dtype=torch.int32, device=dev)
+    batch.bind(kps=kps_t.data_ptr(), counts=counts_t.data_ptr())
+    torch.cuda.synchronize(dev)
+    t_u = time.time()
+    batch.upload(frames)
+    h2d_s = time.time() - t_u
+
+    P = B - 1
+    ref_idx = torch.arange(0, P, dtype=torch.int32, device=dev)
+    cur_idx = torch.arange(1, B, dtype=torch.int32, device=dev)
+    bi = torch.empty((P, cap), dtype=torch.int32, device=dev)
+    bd = torch.empty_like(bi)
+    sd = torch.empty_like(bi)
+    xyz = torch.empty((P, cap, 3), dtype=torch.float32, device=dev)
+    usable = torch.ones((P, cap), dtype=torch.uint8, device=dev)
+    T_init = torch.zeros((P, 7), dtype=torch.float32, device=dev)
+    T_init[:, 3] = 1.0
+    out = torch.zeros((P, 45), dtype=torch.float32, device=dev)
+    # plane Z_w = 3 in each reference camera: X_c = lam * d_c, lam = (Z - C_z) / (r3 . d_c)
+    r3 = np.zeros((B, 3), np.float32)
+    cz = np.zeros(B, np.float32)
+    for i, (q, t) in enumerate(poses):
+        qi, ti = S.se3_inv(q.astype(np.float64), t.astype(np.float64))
+        R_wc = np.array([S.quat_rot(qi, e) for e in np.eye(3)]).T
+        r3[i] = R_wc[2]
+        cz[i] = ti[2]
+    r3_t = torch.from_numpy(r3[:P]).to(dev)
+    cz_t = torch.from_numpy(cz[:P]).to(dev)
+    fx, fy, cx, cy = cam
+    camera = ygzfe.Camera(*cam)
+
+    def step():
+        batch.extract(B, sptr)
+        batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(), sptr)
+        if args.no_align:
+            return
+        k = kps_t[:P]
+        dx = (k[:, :, 0] - cx) / fx
+        dy = (k[:, :, 1] - cy) / fy
+        lam = (S.PLANE_Z - cz_t)[:, None] / (r3_t[:, 0:1] * dx + r3_t[:, 1:2] * dy + r3_t[:, 2:3])
+        xyz[:, :, 0] = dx * lam
+        xyz[:, :, 1] = dy * lam
+        xyz[:, :, 2] = lam
+        batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(), camera, 3, 1,
+                           T_init.data_ptr(), out.data_ptr(), sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    batch.check()
+    if world > 1:
+        dist.barrier()
+    batch.timing(True)  # hipEvents around every stage launch of the timed region (no syncs)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stage_ms = batch.timing(False)
+    batch.check()
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    ms_per_step = elapsed * 1000.0 / args.steps
+    fps = world * B / (elapsed / args.steps)
+
+    # ------------------------------------------------ roofline (dominant kernel)
+    counts = counts_t.cpu().numpy()
+    nvis = out[:, 7].contiguous().view(torch.int32).cpu().numpy()
+    lw = [(W >> l, H >> l) for l in range(nl)]
+    areas = [w * h for w, h in lw]
+    N = float(counts.mean())
+    nv = float(nvis.mean())
+    # algorithmic bytes per launch, B frames per launch
+    alg = {
+        "pyramid": B * sum(areas[l - 1] + areas[l] for l in range(1, nl)),
+        "blur7": B * 2 * sum(areas),
+        "fast9_cells": B * (sum(areas[:3]) + 4 * 5000),
+        "octree": B * (4 * 2 * 5000 + 4 * N),
+        "orient_rbrief": B * N * (961 + 2 * 256 + 60),
+        "hamming_best2": P * (32 * 2 * N + 12 * N),
+        "sparse_align": P * (3 * nv * (36 + 10 * 25) + 12 * nv + 96),
+    }
+    dom = max((k for k in stage_ms if stage_ms[k] > 0), key=lambda k: stage_ms[k])
+    dom_ms = stage_ms[dom]
+    achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
+    roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None, "avg_launch_ms": round(dom_ms, 4),
+            "alg_bytes_per_launch": int(alg[dom]),
+            "stages_ms": {k: round(v, 4) for k, v in stage_ms.items()}}
+    # whole pipeline, SURVEY §8d model: (B_extract + B_align) per frame x fps
+    b_extract = W * H + 2 * sum(areas[1:]) + 2 * sum(areas) + 60 * N
+    b_align = 3 * nv * (36 + 10 * 25) + 12 * nv + 96
+    pipeline_gbps = (b_extract + b_align) * (fps / world) / 1e9
+
+    # ------------------------------------------------ CPU baseline (rank 0, N = 1)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(frames, poses, S, args, sc)
+
+    if rank == 0:
+        line = {
+            "metric": "frames/sec ORB-extract+SparseImageAlign, 752x480, 1000 feat",
+            "value": round(fps, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded textured-plane renders, EuRoC intrinsics; no dataset)",
+            "config": {"workload": "C2 extract + dense Hamming (k vs k-1) + C3 SparseImgAlign levels 3..1",
+                       "frames_per_gpu": B, "image": f"{W}x{H}", "nfeatures": nf, "scale_factor": sf,
+                       "nlevels": nl, "fast_th": [ini, mn], "align_pairs_per_gpu": P,
+                       "mean_keypoints": round(N, 1), "mean_align_visible": round(nv, 1),
+                       "parallelism": f"frame-sharded x{world}"},
+            "roofline": roof,
+            "pipeline_gbps_model": round(pipeline_gbps, 2),
+            "h2d_upload_ms": round(h2d_s * 1e3, 2),
+            "render_s": round(render_s, 2),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(frames, poses, S, args, sc):
+    """oracle/ restatement, single thread: extract (C2) + SparseImgAlign (C3) per frame."""
+    import _oracle as O
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    cam = O.Cam(*sc.cam)
+    fx, fy, cx, cy = sc.cam
+    T0 = O.se3_from((0, 0, 0, 1), (0, 0, 0))
+    n = 0
+    t0 = time.perf_counter()
+    prev = None
+    while n < min(args.cpu_sample, len(frames)):
+        lv = orc.pyramid(frames[n])
+        kps, desc = orc.extract(lv)
+        if prev is not None:
+            plv, pk, pdesc = prev
+            O.hamming_best2(desc, pdesc)
+            q, t = poses[n - 1]
+            qi, ti = S.se3_inv(q.astype(np.float64), t.astype(np.float64))
+            R_wc = np.array([S.quat_rot(qi, e) for e in np.eye(3)]).T
+            d = np.stack([(pk["x"] - cx) / fx, (pk["y"] - cy) / fy, np.ones(len(pk))], 1)
+            lam = (S.PLANE_Z - ti[2]) / (d @ R_wc[2])
+            xyz = (d * lam[:, None]).astype(np.float32)
+            O.sparse_align(plv, lv, orc.inv_scale, cam, pk, xyz, np.ones(len(pk), np.uint8), 3, 1, T0)
+        prev = (lv, kps, desc)
+        n += 1
+        if time.perf_counter() - t0 > args.cpu_budget_s:
+            break
+    el = time.perf_counter() - t0
+    return {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} frames of the same rendered C2 sequence: pyramid + octree ORB + rBRIEF + Hamming vs "
+                      f"previous frame + SparseImgAlign 3..1, oracle/ (gcc -O3 -march=native), 1 thread",
+            "ms_per_frame": round(el * 1e3 / n, 3)}
+
+
+if __name__ == "__main__":
+    main()

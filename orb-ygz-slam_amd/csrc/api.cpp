@@ -183,14 +183,51 @@ struct ygzfe_batch {
     // align scratch
     DevBuf jobs, ascratch, pairs_tmp;
     size_t ascratch_per_job = 0;
-    // timing
+    // per-stage kernel timing with hipEvents on the launch stream (no sync while recording)
     bool timing = false;
-    std::vector<hipEvent_t> ev;
-    std::vector<float> stage_ms;
+    std::vector<hipEvent_t> pool;
+    struct Rec { int stage; hipEvent_t a, b; };
+    std::vector<Rec> pending;
+    double total_ms[8] = {0};
+    long calls[8] = {0};
+    hipEvent_t get_event() {
+        hipEvent_t e = nullptr;
+        if (!pool.empty()) { e = pool.back(); pool.pop_back(); }
+        else if (hipEventCreate(&e) != hipSuccess) e = nullptr;
+        return e;
+    }
+    hipEvent_t begin(hipStream_t st) {
+        if (!timing) return nullptr;
+        hipEvent_t a = get_event();
+        if (a) (void)hipEventRecord(a, st);
+        return a;
+    }
+    void end(int stage, hipEvent_t a, hipStream_t st) {
+        if (!timing || !a) return;
+        hipEvent_t e = get_event();
+        if (!e) return;
+        (void)hipEventRecord(e, st);
+        pending.push_back({stage, a, e});
+    }
+    int collect() {
+        for (auto &r : pending) {
+            float ms = 0.f;
+            YGZ_HIP(hipEventSynchronize(r.b));
+            YGZ_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+            total_ms[r.stage] += ms;
+            calls[r.stage] += 1;
+            pool.push_back(r.a);
+            pool.push_back(r.b);
+        }
+        pending.clear();
+        return YGZFE_OK;
+    }
 };
 
-static const char *kStageNames[] = {"pyramid", "blur7", "fast9_cells", "octree", "orient_rbrief"};
-constexpr int kNumStages = 5;
+static const char *kStageNames[] = {"pyramid", "blur7", "fast9_cells", "octree", "orient_rbrief", "hamming_best2",
+                                    "sparse_align"};
+constexpr int kNumStages = 7;
+enum { ST_PYR, ST_BLUR, ST_FAST, ST_OCT, ST_DESC, ST_HAM, ST_ALIGN };
 
 extern "C" {
 
@@ -480,9 +517,6 @@ int ygzfe_batch_create(const ygzfe_orb_params *p, int device, int width, int hei
     YGZ_TRY(b->pyr.ensure((size_t)max_frames * P.pyr_bytes));
     YGZ_TRY(b->ws.ensure(P, max_frames, P.kp_cap));
     YGZ_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
-    b->ev.resize(kNumStages + 1);
-    for (auto &e : b->ev) YGZ_HIP(hipEventCreate(&e));
-    b->stage_ms.assign(kNumStages, 0.f);
     *out = b.release();
     return YGZFE_OK;
 }
@@ -491,7 +525,8 @@ void ygzfe_batch_destroy(ygzfe_batch *b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
     (void)hipStreamSynchronize(b->stream);
-    for (auto &e : b->ev) (void)hipEventDestroy(e);
+    (void)b->collect();
+    for (auto &e : b->pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(b->stream);
     delete b;
 }
@@ -544,28 +579,27 @@ int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream) {
     const Plan &P = pd.hp();
     Workspace &ws = b->ws;
     uint8_t *pyr = b->pyr.as<uint8_t>();
-    const bool tm = b->timing;
     YGZ_HIP(hipMemsetAsync(ws.err.p, 0, 16, st));
-    if (tm) YGZ_HIP(hipEventRecord(b->ev[0], st));
+    hipEvent_t t0 = b->begin(st);
     YGZ_HIP(launch_pyramid(pyr, P.pyr_bytes, P, pd.dp(), pd.tabs.as<int>(), n_frames, st));
-    if (tm) YGZ_HIP(hipEventRecord(b->ev[1], st));
+    b->end(ST_PYR, t0, st);
+    t0 = b->begin(st);
     YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), n_frames, st));
-    if (tm) YGZ_HIP(hipEventRecord(b->ev[2], st));
+    b->end(ST_BLUR, t0, st);
+    t0 = b->begin(st);
     YGZ_HIP(launch_fast(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(), ws.cellbuf.as<uint32_t>(),
                         ws.cellcnt.as<int>(), n_frames, st));
-    if (tm) YGZ_HIP(hipEventRecord(b->ev[3], st));
+    b->end(ST_FAST, t0, st);
+    t0 = b->begin(st);
     YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
                           ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.err.as<int>(),
                           n_frames, st));
-    if (tm) YGZ_HIP(hipEventRecord(b->ev[4], st));
+    b->end(ST_OCT, t0, st);
+    t0 = b->begin(st);
     YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.sel.as<uint32_t>(),
                                ws.selcnt.as<int>(), nullptr, ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(),
                                ws.counts.as<int>(), P.kp_cap, n_frames, st));
-    if (tm) {
-        YGZ_HIP(hipEventRecord(b->ev[5], st));
-        YGZ_HIP(hipEventSynchronize(b->ev[5]));
-        for (int s = 0; s < kNumStages; s++) YGZ_HIP(hipEventElapsedTime(&b->stage_ms[s], b->ev[s], b->ev[s + 1]));
-    }
+    b->end(ST_DESC, t0, st);
     return YGZFE_OK;
 }
 
@@ -619,10 +653,17 @@ int ygzfe_batch_level(ygzfe_batch *b, int frame, int level, const uint8_t **d_le
 
 int ygzfe_batch_timing(ygzfe_batch *b, int enable, float *ms, const char **names, int cap) {
     if (!b) { set_error("null batch"); return YGZFE_EINVAL; }
-    b->timing = enable != 0;
+    YGZ_TRY(ensure_device(b->device));
+    YGZ_TRY(b->collect());
     for (int s = 0; s < kNumStages && s < cap; s++) {
-        if (ms) ms[s] = b->stage_ms[s];
+        if (ms) ms[s] = b->calls[s] ? (float)(b->total_ms[s] / b->calls[s]) : 0.f;
         if (names) names[s] = kStageNames[s];
+    }
+    if (enable > 0) {  // reset + enable
+        for (int s = 0; s < kNumStages; s++) { b->total_ms[s] = 0; b->calls[s] = 0; }
+        b->timing = true;
+    } else if (enable == 0) {
+        b->timing = false;
     }
     return kNumStages;
 }
@@ -694,8 +735,10 @@ int ygzfe_batch_match(ygzfe_batch *b, int n_pairs, const int32_t *d_qframe, cons
     YGZ_TRY(ensure_device(b->device));
     hipStream_t st = stream ? (hipStream_t)stream : b->stream;
     const Plan &P = b->plan->hp();
+    hipEvent_t t0 = b->begin(st);
     YGZ_HIP(launch_hamming_best2_pairs(b->ws.desc.as<uint8_t>(), b->ws.counts.as<int32_t>(), P.kp_cap, n_pairs,
                                        d_qframe, d_tframe, d_best_idx, d_best_dist, d_second_dist, st));
+    b->end(ST_HAM, t0, st);
     return YGZFE_OK;
 }
 
@@ -811,8 +854,10 @@ extern "C" int ygzfe_batch_sparse_align(ygzfe_batch *b, int n_pairs, const int32
                        d_ref_idx, d_cur_idx, b->pyr.as<uint8_t>(), P.pyr_bytes, b->ws.kps.as<ygzfe_kp>(),
                        b->ws.counts.as<int32_t>(), P.kp_cap, d_xyz_ref, d_usable, max_level, min_level, d_T_init);
     YGZ_HIP(hipGetLastError());
+    hipEvent_t t0 = b->begin(st);
     YGZ_HIP(launch_sparse_align(levels_of(P), *cam, b->jobs.as<AlignJob>(), n_pairs, b->ascratch.as<float>(), spj,
                                 d_out, st));
+    b->end(ST_ALIGN, t0, st);
     return YGZFE_OK;
 }
 

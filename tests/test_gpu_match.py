@@ -1,0 +1,72 @@
+"""GPU Hamming matching vs the oracle (ORBmatcher.cc:1507-1523 + search loops): bit-exact."""
+import numpy as np
+import pytest
+
+import _oracle as O
+import _scenes as S
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_desc(rng, n):
+    return rng.integers(0, 256, (n, 32), dtype=np.uint8)
+
+
+@pytest.mark.parametrize("nq,nt", [(1, 1), (100, 37), (1000, 1000), (300, 2500), (2000, 2000)])
+def test_best2_random(gpu, nq, nt):
+    rng = np.random.default_rng(nq * 7 + nt)
+    q, t = rand_desc(rng, nq), rand_desc(rng, nt)
+    # plant exact duplicates and ties so the first-index rule is exercised
+    t[nt // 2] = q[0]
+    if nt > 3:
+        t[nt - 1] = q[0]
+    m = gpu.ORBmatcher()
+    bi, bd, sd = m.best2(q, t)
+    ri, rd, rs = O.hamming_best2(q, t)
+    assert np.array_equal(bi, ri) and np.array_equal(bd, rd) and np.array_equal(sd, rs)
+    assert bd[0] == 0 and bi[0] == nt // 2
+
+
+def test_best2_empty_train(gpu):
+    rng = np.random.default_rng(1)
+    q = rand_desc(rng, 5)
+    bi, bd, sd = gpu.ORBmatcher().best2(q, np.zeros((0, 32), np.uint8))
+    assert (bi == -1).all() and (bd == 257).all() and (sd == 257).all()
+
+
+def test_descriptor_distance(gpu):
+    rng = np.random.default_rng(2)
+    a, b = rand_desc(rng, 50), rand_desc(rng, 50)
+    for i in range(50):
+        assert gpu.ORBmatcher.DescriptorDistance(a[i], b[i]) == O.lib().ygzo_descriptor_distance(O._p(a[i]), O._p(b[i]))
+
+
+def test_window_csr(gpu):
+    rng = np.random.default_rng(3)
+    q, t = rand_desc(rng, 200), rand_desc(rng, 300)
+    counts = rng.integers(0, 40, 200)
+    row_ptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    cand = rng.integers(0, 300, row_ptr[-1]).astype(np.int32)
+    d = gpu.ORBmatcher().window_distances(q, t, row_ptr, cand)
+    for i in range(200):
+        for k in range(row_ptr[i], row_ptr[i + 1]):
+            assert d[k] == O.lib().ygzo_descriptor_distance(O._p(q[i]), O._p(t[cand[k]]))
+
+
+def test_best2_on_extracted_frames(gpu):
+    """C2: descriptors of frame k vs frame k+1 of a rendered sequence (dense 1000x1000-class search)."""
+    sc = S.PlaneScene(3)
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    ex = gpu.ORBextractor(nf, sf, nl, ini, mn)
+    q0, t0 = np.array([0, 0, 0, 1], np.float32), np.zeros(3, np.float32)
+    v, w = S.motion(0)
+    q1 = S.quat_from_rotvec(w).astype(np.float32)
+    f0 = sc.render(q0, t0, 1)
+    f1 = sc.render(q1, v.astype(np.float32), 2)
+    k0, d0 = ex(f0)
+    k1, d1 = ex(f1)
+    bi, bd, sd = gpu.ORBmatcher().best2(d1, d0)
+    ri, rd, rs = O.hamming_best2(d1, d0)
+    assert np.array_equal(bi, ri) and np.array_equal(bd, rd) and np.array_equal(sd, rs)
+    # sanity: most keypoints find a close match in the previous frame
+    assert np.mean(bd < 50) > 0.5
