@@ -156,7 +156,123 @@ __device__ void ldlt_solve6(const float Hin[36], const float b[6], float x[6]) {
     for (int i = 0; i < 6; i++) x[perm[i]] = y[i];
 }
 
+// The same LDLT with every array index a compile-time constant (pivot swaps
+// and the permutation are applied through selects), so the solver keeps the
+// 6x6 system in VGPRs instead of scratch.  Identical arithmetic to ldlt_solve6.
+__device__ __forceinline__ void ldlt_solve6_reg(const float Hin[36], const float b[6], float x[6]) {
+    float A[36];
+    int perm[6];
+#pragma unroll
+    for (int i = 0; i < 36; i++) A[i] = Hin[i];
+#pragma unroll
+    for (int i = 0; i < 6; i++) perm[i] = i;
+    bool stopped = false;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        if (stopped) break;
+        int piv = k;
+        float big = fabsf(A[k * 6 + k]);
+#pragma unroll
+        for (int i = k + 1; i < 6; i++)
+            if (fabsf(A[i * 6 + i]) > big) { big = fabsf(A[i * 6 + i]); piv = i; }
+#pragma unroll
+        for (int p = k + 1; p < 6; p++) {
+            if (piv == p) {
+#pragma unroll
+                for (int j = 0; j < k; j++) { const float t = A[k * 6 + j]; A[k * 6 + j] = A[p * 6 + j]; A[p * 6 + j] = t; }
+#pragma unroll
+                for (int i = p + 1; i < 6; i++) { const float t = A[i * 6 + k]; A[i * 6 + k] = A[i * 6 + p]; A[i * 6 + p] = t; }
+                { const float t = A[k * 6 + k]; A[k * 6 + k] = A[p * 6 + p]; A[p * 6 + p] = t; }
+#pragma unroll
+                for (int i = k + 1; i < p; i++) { const float t = A[i * 6 + k]; A[i * 6 + k] = A[p * 6 + i]; A[p * 6 + i] = t; }
+                const int t = perm[k]; perm[k] = perm[p]; perm[p] = t;
+            }
+        }
+        float tmp[6];
+#pragma unroll
+        for (int j = 0; j < k; j++) tmp[j] = A[j * 6 + j] * A[k * 6 + j];
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < k; j++) s += A[k * 6 + j] * tmp[j];
+        A[k * 6 + k] -= s;
+#pragma unroll
+        for (int i = k + 1; i < 6; i++) {
+            float t = 0.f;
+#pragma unroll
+            for (int j = 0; j < k; j++) t += A[i * 6 + j] * tmp[j];
+            A[i * 6 + k] -= t;
+        }
+        const float akk = A[k * 6 + k];
+        if (k == 0 && akk == 0.f) {
+#pragma unroll
+            for (int i = 0; i < 6; i++) perm[i] = i;
+            stopped = true;
+        } else if (akk != 0.f) {
+#pragma unroll
+            for (int i = k + 1; i < 6; i++) A[i * 6 + k] /= akk;
+        }
+    }
+    float y[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        float v = 0.f;
+#pragma unroll
+        for (int j = 0; j < 6; j++) v = perm[i] == j ? b[j] : v;
+        y[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        float s = y[i];
+#pragma unroll
+        for (int j = 0; j < i; j++) s -= A[i * 6 + j] * y[j];
+        y[i] = s;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        const float d = A[i * 6 + i];
+        y[i] = fabsf(d) > 1.17549435e-38f ? y[i] / d : 0.f;
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+        float s = y[i];
+#pragma unroll
+        for (int j = i + 1; j < 6; j++) s -= A[j * 6 + i] * y[j];
+        y[i] = s;
+    }
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        float v = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; i++) v = perm[i] == j ? y[i] : v;
+        x[j] = v;
+    }
+}
+
 __device__ __forceinline__ float wmul(double a, double b) { return (float)(a * b); }
+
+// Row gathers for the 7x7 reference / 5x5 current windows: a feature window
+// sits at an arbitrary byte offset, so a lane reads whole dwords from the
+// enclosing 4-byte boundary and realigns them with v_alignbyte: one
+// dwordx3 / dwordx2 load per row instead of 7 / 5 scattered byte loads
+// (each byte load of a wave touches up to 64 distinct cache lines).
+// Frame pyramids carry >= 64 bytes of tail padding for the over-read.
+template <int N>
+__device__ __forceinline__ void load_row(const uint8_t *p, float (&out)[N]) {
+    const uintptr_t a = (uintptr_t)p & ~(uintptr_t)3;
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(a);
+    constexpr int ND = (N + 3 + 3) / 4;  // dwords covering [p, p+N) for any sh <= 3
+    uint32_t d[ND + 1];
+#pragma unroll
+    for (int i = 0; i < ND; i++) d[i] = q[i];
+    d[ND] = 0;
+#pragma unroll
+    for (int w = 0; w * 4 < N; w++) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(d[w + 1], d[w], sh);
+#pragma unroll
+        for (int b = 0; b < 4 && w * 4 + b < N; b++) out[w * 4 + b] = (float)((v >> (8 * b)) & 0xFFu);
+    }
+}
 
 // ------------------------------------------------------------------ sparse align
 constexpr int kPA = 16;    // patch_area_
@@ -164,18 +280,29 @@ constexpr int kRed = 29;   // 21 (upper H) + 6 (Jres) + chi2 + count
 
 size_t sparse_align_scratch_floats(int n) { return (size_t)n * kPA * 7 + (size_t)n; }
 
-__global__ __launch_bounds__(256) void k_sparse_align(AlignLevels lv, ygzfe_camera cam,
-                                                      const AlignJob *__restrict__ jobs, float *__restrict__ scratch,
-                                                      size_t scratch_per_job,
-                                                      ygzfe_align_result *__restrict__ out) {
-    __shared__ float s_red[4][kRed];
+// JacobXYZ2Cam (SparseImageAlign.h:95-116): translation first, pre-negated.
+__device__ __forceinline__ void jacob_xyz2cam_f(float X, float Y, float Z, float fj[12]) {
+    const float z_inv = (float)(1. / (double)Z);
+    const float z_inv_2 = z_inv * z_inv;
+    fj[0] = -z_inv; fj[1] = 0.f; fj[2] = X * z_inv_2; fj[3] = Y * fj[2];
+    fj[4] = (float)(-(1.0 + (double)(X * fj[2]))); fj[5] = Y * z_inv;
+    fj[6] = 0.f; fj[7] = -z_inv; fj[8] = Y * z_inv_2; fj[9] = (float)(1.0 + (double)(Y * fj[8]));
+    fj[10] = -fj[3]; fj[11] = -X * z_inv;
+}
+
+// Generic path (any n): (feature, pixel) terms strided over the workgroup,
+// ref patches and Jacobians cached in a global scratch slab per job.
+template <int NT>
+__device__ __attribute__((noinline)) void sparse_align_generic(const AlignLevels &lv, const ygzfe_camera &cam, const AlignJob &job,
+                                     float *__restrict__ scratch, ygzfe_align_result *__restrict__ outp) {
+    constexpr int NW = NT / 64;
+    __shared__ float s_red[NW][kRed];
     __shared__ SE3 s_T, s_old;
     __shared__ float s_chi2, s_H[36];
     __shared__ int s_stop, s_break, s_nmeas;
-    const AlignJob job = jobs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = job.n;
-    float *patch = scratch + blockIdx.x * scratch_per_job;
+    float *patch = scratch;
     float *jac = patch + (size_t)n * kPA;
     float *vis = jac + (size_t)n * kPA * 6;
     if (tid == 0) {
@@ -186,7 +313,7 @@ __global__ __launch_bounds__(256) void k_sparse_align(AlignLevels lv, ygzfe_came
         s_nmeas = 0;
         for (int i = 0; i < 36; i++) s_H[i] = 0.f;
     }
-    for (int i = tid; i < n; i += 256) vis[i] = 0.f;
+    for (int i = tid; i < n; i += NT) vis[i] = 0.f;
     __syncthreads();
     if (n <= 0) {
         if (tid == 0) {
@@ -196,7 +323,7 @@ __global__ __launch_bounds__(256) void k_sparse_align(AlignLevels lv, ygzfe_came
             r.n_visible = 0;
             r.chi2 = s_chi2;
             for (int i = 0; i < 36; i++) r.H[i] = 0.f;
-            out[blockIdx.x] = r;
+            *outp = r;
         }
         return;
     }
@@ -207,7 +334,7 @@ __global__ __launch_bounds__(256) void k_sparse_align(AlignLevels lv, ygzfe_came
         const uint8_t *rimg = job.ref_pyr + lv.off[level];
         const uint8_t *cimg = job.cur_pyr + lv.off[level];
         // precomputeReferencePatches: (feature, pixel) per thread
-        for (int e = tid; e < n * kPA; e += 256) {
+        for (int e = tid; e < n * kPA; e += NT) {
             const int i = e >> 4, pc = e & 15;
             float *J = jac + (size_t)e * 6;
             bool ok = job.usable[i] != 0;
@@ -247,7 +374,7 @@ __global__ __launch_bounds__(256) void k_sparse_align(AlignLevels lv, ygzfe_came
             const SE3 T = s_T;
             float acc[kRed];
             for (int k = 0; k < kRed; k++) acc[k] = 0.f;
-            for (int e = tid; e < n * kPA; e += 256) {
+            for (int e = tid; e < n * kPA; e += NT) {
                 const int i = e >> 4, pc = e & 15;
                 if (vis[i] == 0.f) continue;
                 float pc3[3];
@@ -280,7 +407,11 @@ __global__ __launch_bounds__(256) void k_sparse_align(AlignLevels lv, ygzfe_came
             __syncthreads();
             if (tid == 0) {
                 float r[kRed];
-                for (int k = 0; k < kRed; k++) r[k] = (s_red[0][k] + s_red[1][k]) + (s_red[2][k] + s_red[3][k]);
+                for (int k = 0; k < kRed; k++) {
+                    float a = 0.f;
+                    for (int w = 0; w < NW; w++) a += s_red[w][k];
+                    r[k] = a;
+                }
                 float Hm[36], b[6], x[6];
                 int m = 0;
                 for (int rr = 0; rr < 6; rr++)
@@ -290,7 +421,7 @@ __global__ __launch_bounds__(256) void k_sparse_align(AlignLevels lv, ygzfe_came
                 const float new_chi2 = r[27] / (float)nmeas;
                 for (int k = 0; k < 36; k++) s_H[k] = Hm[k];
                 s_nmeas = nmeas;
-                ldlt_solve6(Hm, b, x);
+                ldlt_solve6_reg(Hm, b, x);
                 if (isnan(x[0])) s_stop = 1;
                 s_break = 0;
                 if ((it > 0 && (double)new_chi2 > 1.2 * (double)s_chi2) || s_stop) {
@@ -322,14 +453,365 @@ __global__ __launch_bounds__(256) void k_sparse_align(AlignLevels lv, ygzfe_came
         r.n_visible = s_nmeas / kPA;
         r.chi2 = s_chi2;
         for (int i = 0; i < 36; i++) r.H[i] = s_H[i];
-        out[blockIdx.x] = r;
+        *outp = r;
     }
 }
 
+// Register-resident variant (n <= NT features): one thread owns one feature for
+// every level and iteration.  Its 4x4 reference patch and the bilinear
+// reference gradients (gx, gy) stay in VGPRs, so an iteration reads only the
+// 5x5 current-image window of each feature.  Because J_p = (gx_p*Jp0 +
+// gy_p*Jp1) * f*scale (SparseImageAlign.cc:123-125), a feature's Jres and H
+// contributions are closed forms of the per-feature sums
+// Sx = sum gx*res, Sy = sum gy*res, Sxx, Sxy, Syy (same algebra, different
+// float association than the reference's per-pixel sums -> 1e-4 pose parity).
+// 32 partial sums are reduced with a 6-step butterfly (each step halves the
+// values a lane carries) and one LDS pass over the waves.
+__device__ __forceinline__ float wave_butterfly32(float (&v)[32], int lane) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const bool hi = lane & 32;
+        const float send = hi ? v[i] : v[16 + i];
+        const float keep = hi ? v[16 + i] : v[i];
+        v[i] = keep + __shfl_xor(send, 32, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const bool hi = lane & 16;
+        const float send = hi ? v[i] : v[8 + i];
+        const float keep = hi ? v[8 + i] : v[i];
+        v[i] = keep + __shfl_xor(send, 16, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const bool hi = lane & 8;
+        const float send = hi ? v[i] : v[4 + i];
+        const float keep = hi ? v[4 + i] : v[i];
+        v[i] = keep + __shfl_xor(send, 8, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const bool hi = lane & 4;
+        const float send = hi ? v[i] : v[2 + i];
+        const float keep = hi ? v[2 + i] : v[i];
+        v[i] = keep + __shfl_xor(send, 4, 64);
+    }
+    {
+        const bool hi = lane & 2;
+        const float send = hi ? v[0] : v[1];
+        const float keep = hi ? v[1] : v[0];
+        v[0] = keep + __shfl_xor(send, 2, 64);
+    }
+    return v[0] + __shfl_xor(v[0], 1, 64);  // lane holds the total of value (lane >> 1)
+}
+
+#ifdef YGZ_STAMPS
+// diagnostic build only (lib/libygzfe_diag.so): solver-wave timestamps of block 0
+__device__ unsigned long long g_stamps[4096];
+__device__ int g_nstamps;
+#define YGZ_STAMP(tag)                                                                   \
+    do {                                                                                 \
+        if (blockIdx.x == 0 && threadIdx.x == 0 && g_nstamps < 2047) {                   \
+            g_stamps[2 * g_nstamps] = (unsigned long long)(tag);                         \
+            g_stamps[2 * g_nstamps + 1] = __builtin_amdgcn_s_memtime();                  \
+            g_nstamps++;                                                                 \
+        }                                                                                \
+    } while (0)
+extern "C" int ygzfe_diag_stamps(unsigned long long *out, int cap) {
+    int n = 0;
+    (void)hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_nstamps), sizeof(int));
+    n = n * 2 < cap ? n * 2 : cap;
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n);
+    int z = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_nstamps), &z, sizeof(int));
+    return n / 2;
+}
+#else
+#define YGZ_STAMP(tag) do {} while (0)
+#endif
+
+// Wave sum with DPP row operations (no LDS traffic, one temporary per value):
+// quad swaps, half-row / row mirrors, then row_bcast15 / row_bcast31.  The
+// total lands in lane 63.
+#define YGZ_DPP(v, ctrl, rmask) \
+    __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, rmask, 0xF, false))
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v += YGZ_DPP(v, 0xB1, 0xF);   // quad_perm [1,0,3,2]
+    v += YGZ_DPP(v, 0x4E, 0xF);   // quad_perm [2,3,0,1]
+    v += YGZ_DPP(v, 0x141, 0xF);  // row_half_mirror
+    v += YGZ_DPP(v, 0x140, 0xF);  // row_mirror
+    v += YGZ_DPP(v, 0x142, 0xA);  // row_bcast:15 -> rows 1,3
+    v += YGZ_DPP(v, 0x143, 0xC);  // row_bcast:31 -> rows 2,3
+    return v;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_camera cam,
+                                                         const AlignJob *__restrict__ jobs,
+                                                         float *__restrict__ scratch, size_t scratch_per_job,
+                                                         ygzfe_align_result *__restrict__ out) {
+    constexpr int NW = NT / 64;
+    constexpr int NF = NT - 64;  // features are owned by waves 1..NW-1; wave 0 is the solver
+    if (jobs[blockIdx.x].n > NF) {  // more features than feature threads: generic path
+        sparse_align_generic<NT>(lv, cam, jobs[blockIdx.x], scratch + blockIdx.x * scratch_per_job, out + blockIdx.x);
+        return;
+    }
+    __shared__ float s_part[NW][32];
+    __shared__ float s_patch[16][NF];  // ref_patch_cache_ of the owned features (column = feature)
+    __shared__ float s_Hf[21][NF];     // per-feature H contribution of the level (upper triangle)
+    __shared__ float s_Hvis[21];       // sum of s_Hf over the level's features
+    __shared__ uint16_t s_out[NF];     // features projected out of bounds this iteration
+    __shared__ int s_nout;
+    __shared__ SE3 s_T, s_old;
+    __shared__ float s_chi2, s_H[36];
+    __shared__ int s_stop, s_break, s_nmeas;
+    const AlignJob &job = jobs[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int border = 3;
+    if (tid == 0) {
+        for (int i = 0; i < 4; i++) s_T.q[i] = job.T_init.q[i];
+        for (int i = 0; i < 3; i++) s_T.t[i] = job.T_init.t[i];
+        s_chi2 = 1e10f;
+        s_stop = 0;
+        s_nmeas = 0;
+        s_break = 0;
+        s_nout = 0;
+        for (int i = 0; i < 36; i++) s_H[i] = 0.f;
+    }
+    __syncthreads();
+    YGZ_STAMP(9);
+    if (wave == 0) {
+        // ---------------- solver wave: reduce partials, LDLT, T <- T exp(-x) (NLSSolver_impl.hpp:18-91)
+        for (int level = job.max_level; level >= job.min_level; level--) {
+            if (tid == 0) s_old = s_T;
+            __syncthreads();  // L0: level start, s_part = per-wave sums of s_Hf
+            YGZ_STAMP(1);
+            if (lane < 21) {
+                float r = 0.f;
+                for (int w = 1; w < NW; w++) r += s_part[w][lane];
+                s_Hvis[lane] = r;
+            }
+            __syncthreads();  // L0b: s_part free again
+            YGZ_STAMP(2);
+            for (int it = 0; it < 10; it++) {
+                __syncthreads();  // A: partials written
+            YGZ_STAMP(3);
+                if (lane < 29) {
+                    float r = 0.f;
+                    if (lane < 8) {  // Jres[6], chi2, n_meas
+                        for (int w = 1; w < NW; w++) r += s_part[w][lane];
+                    } else {  // H = H_vis - sum of the out-of-bounds features' H_f
+                        const int k = lane - 8;
+                        float o = 0.f;
+                        for (int i = 0; i < s_nout; i++) o += s_Hf[k][s_out[i]];
+                        r = s_Hvis[k] - o;
+                    }
+                    s_part[0][lane] = r;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const float *tot = s_part[0];
+                if (tid == 0) {
+                    float Hm[36], b[6], x[6];
+                    int m = 0;
+                    for (int rr = 0; rr < 6; rr++)
+                        for (int c = rr; c < 6; c++) { Hm[rr * 6 + c] = tot[8 + m]; Hm[c * 6 + rr] = tot[8 + m]; m++; }
+                    for (int k = 0; k < 6; k++) b[k] = tot[k];
+                    const int nmeas = (int)tot[7];
+                    const float new_chi2 = tot[6] / (float)nmeas;
+                    s_nout = 0;
+                    for (int k = 0; k < 36; k++) s_H[k] = Hm[k];
+                    s_nmeas = nmeas;
+                    ldlt_solve6_reg(Hm, b, x);
+                    if (isnan(x[0])) s_stop = 1;
+                    s_break = 0;
+                    if ((it > 0 && (double)new_chi2 > 1.2 * (double)s_chi2) || s_stop) {
+                        s_T = s_old;  // rollback
+                        s_break = 1;
+                    } else {
+                        float mx[6];
+                        for (int k = 0; k < 6; k++) mx[k] = -x[k];
+                        SE3 E, Tn;
+                        se3_exp(mx, E);
+                        se3_mul(s_T, E, Tn);
+                        s_old = s_T;
+                        s_T = Tn;
+                        s_chi2 = new_chi2;
+                        float nm = -1.f;
+                        for (int k = 0; k < 6; k++) nm = fabsf(x[k]) > nm ? fabsf(x[k]) : nm;
+                        if (nm <= 0.000001f) s_break = 1;
+                    }
+                }
+                __syncthreads();  // B: pose / decision published
+            YGZ_STAMP(4);
+                if (s_break) break;
+            }
+            __syncthreads();  // L1: level end
+            YGZ_STAMP(5);
+        }
+        if (tid == 0) {
+            ygzfe_align_result res;
+            for (int i = 0; i < 4; i++) res.T_cur_ref.q[i] = s_T.q[i];
+            for (int i = 0; i < 3; i++) res.T_cur_ref.t[i] = s_T.t[i];
+            res.n_visible = s_nmeas / kPA;
+            res.chi2 = s_chi2;
+            for (int i = 0; i < 36; i++) res.H[i] = s_H[i];
+            out[blockIdx.x] = res;
+        }
+        return;
+    }
+    // ---------------- feature waves: one thread per reference feature
+    const int f = tid - 64;
+    const int n = job.n;
+    const bool own = f < n;
+    float X = 0.f, Y = 0.f, Z = 1.f, kx = 0.f, ky = 0.f;
+    bool usable = false, vis = false;
+    if (own) {
+        X = job.xyz[3 * f]; Y = job.xyz[3 * f + 1]; Z = job.xyz[3 * f + 2];
+        usable = job.usable[f] != 0;
+        kx = job.kps[f].x; ky = job.kps[f].y;
+    }
+    float gx[16], gy[16];
+#pragma unroll
+    for (int p = 0; p < 16; p++) { gx[p] = 0.f; gy[p] = 0.f; s_patch[p][f] = 0.f; }
+    for (int level = job.max_level; level >= job.min_level; level--) {
+        const int W = lv.w[level], H = lv.h[level];
+        const float scale = lv.inv_scale[level];
+        const float fs = cam.fx * scale;
+        const uint8_t *rimg = job.ref_pyr + lv.off[level];
+        const uint8_t *cimg = job.cur_pyr + lv.off[level];
+        // precomputeReferencePatches (SparseImageAlign.cc:57-128) for the owned feature
+        bool here = false;
+        if (own && usable) {
+            const float u_ref = kx * scale, v_ref = ky * scale;
+            const int ui = (int)floorf(u_ref), vi = (int)floorf(v_ref);
+            here = !(ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H);
+            if (here) {
+                vis = true;  // visible_fts_ is never reset between levels (SparseImageAlign.cc:34,81)
+                const float su = u_ref - ui, sv = v_ref - vi;
+                const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
+                const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
+                // 7x7 window: rows vi-3..vi+3, cols ui-3..ui+3; R[y][x] = ref(vi-3+y, ui-3+x)
+                const uint8_t *base = rimg + (size_t)(vi - 3) * W + (ui - 3);
+                float rm[7], r0[7], r1[7], r2[7];
+                load_row<7>(base, rm);
+                load_row<7>(base + W, r0);
+                load_row<7>(base + 2 * W, r1);
+#pragma unroll
+                for (int py = 0; py < 4; py++) {
+                    load_row<7>(base + (size_t)(py + 3) * W, r2);
+                    // pixel (py, px): p[0] = R[py+1][px+1]; rows: m = py, a = py+1, b = py+2, c = py+3
+#pragma unroll
+                    for (int px = 0; px < 4; px++) {
+                        const int pi = py * 4 + px, c = px + 1;
+                        const float a0 = r0[c - 1], a1 = r0[c], a2 = r0[c + 1], a3 = r0[c + 2];
+                        const float b0 = r1[c - 1], b1 = r1[c], b2 = r1[c + 1], b3 = r1[c + 2];
+                        const float c1 = r2[c], c2 = r2[c + 1], m1 = rm[c], m2 = rm[c + 1];
+                        s_patch[pi][f] = wtl * a1 + wtr * a2 + wbl * b1 + wbr * b2;
+                        gx[pi] = 0.5f * ((wtl * a2 + wtr * a3 + wbl * b2 + wbr * b3) - (wtl * a0 + wtr * a1 + wbl * b0 + wbr * b1));
+                        gy[pi] = 0.5f * ((wtl * b1 + wtr * b2 + wbl * c1 + wbr * c2) - (wtl * m1 + wtr * m2 + wbl * a1 + wbr * a2));
+                    }
+#pragma unroll
+                    for (int k = 0; k < 7; k++) { rm[k] = r0[k]; r0[k] = r1[k]; r1[k] = r2[k]; }
+                }
+            }
+        }
+        if (!here) {  // jacobian_cache_.setZero() per level; the stale ref patch stays
+#pragma unroll
+            for (int p = 0; p < 16; p++) { gx[p] = 0.f; gy[p] = 0.f; }
+        }
+        {
+            float Sxx = 0.f, Sxy = 0.f, Syy = 0.f;
+#pragma unroll
+            for (int p = 0; p < 16; p++) { Sxx += gx[p] * gx[p]; Sxy += gx[p] * gy[p]; Syy += gy[p] * gy[p]; }
+            const float fs2 = fs * fs;
+            float fj[12];
+            jacob_xyz2cam_f(X, Y, Z, fj);
+            int m = 0;
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int c = r; c < 6; c++) {
+                    const float hrc = fj[r] * fj[c] * Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * Sxy +
+                                      fj[6 + r] * fj[6 + c] * Syy;
+                    const float hv = (own && vis) ? hrc * fs2 : 0.f;
+                    if (own) s_Hf[m][f] = hv;
+                    const float t = wave_sum_dpp(hv);
+                    if (lane == 63) s_part[wave][m] = t;
+                    m++;
+                }
+        }
+        __syncthreads();  // L0
+        __syncthreads();  // L0b
+        for (int it = 0; it < 10; it++) {
+            float acc[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) acc[k] = 0.f;
+            if (own && vis) {
+                const SE3 T = s_T;
+                const float P3[3] = {X, Y, Z};
+                float pc3[3];
+                se3_act(T, P3, pc3);
+                const float u = (cam.fx * pc3[0] / pc3[2] + cam.cx) * scale;
+                const float v = (cam.fy * pc3[1] / pc3[2] + cam.cy) * scale;
+                const int ui = (int)floorf(u), vi = (int)floorf(v);
+                if (ui < 0 || vi < 0 || ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H) {
+                    s_out[atomicAdd(&s_nout, 1)] = (uint16_t)f;
+                } else {
+                    const float su = u - ui, sv = v - vi;
+                    const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
+                    const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
+                    float Sx = 0.f, Sy = 0.f, chi2 = 0.f;
+                    const uint8_t *base = cimg + (size_t)(vi - 2) * W + (ui - 2);
+                    float r0[5];
+                    load_row<5>(base, r0);
+#pragma unroll
+                    for (int py = 0; py < 4; py++) {
+                        float r1[5];
+                        load_row<5>(base + (size_t)(py + 1) * W, r1);
+#pragma unroll
+                        for (int px = 0; px < 4; px++) {
+                            const int pi = py * 4 + px;
+                            const float ic = wtl * r0[px] + wtr * r0[px + 1] + wbl * r1[px] + wbr * r1[px + 1];
+                            const float res = ic - s_patch[pi][f];
+                            Sx += gx[pi] * res;
+                            Sy += gy[pi] * res;
+                            chi2 += res * res;
+                        }
+#pragma unroll
+                        for (int c = 0; c < 5; c++) r0[c] = r1[c];
+                    }
+                    float fj[12];
+                    jacob_xyz2cam_f(X, Y, Z, fj);
+#pragma unroll
+                    for (int r = 0; r < 6; r++) acc[r] = -(fj[r] * Sx + fj[6 + r] * Sy) * fs;
+                    acc[6] = chi2;
+                    acc[7] = 16.f;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const float t = wave_sum_dpp(acc[k]);
+                if (lane == 63) s_part[wave][k] = t;
+            }
+            __syncthreads();  // A
+            __syncthreads();  // B
+            if (s_break) break;
+        }
+        __syncthreads();  // L1
+    }
+}
+
+int sparse_align_reg_capacity() { return 1024; }
+
 hipError_t launch_sparse_align(const AlignLevels &lv, const ygzfe_camera &cam, const AlignJob *jobs, int njobs,
-                               float *scratch, size_t scratch_per_job, ygzfe_align_result *out, hipStream_t st) {
+                               float *scratch, size_t scratch_per_job, ygzfe_align_result *out, hipStream_t st,
+                               int max_n) {
     if (njobs <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sparse_align, dim3(njobs), dim3(256), 0, st, lv, cam, jobs, scratch, scratch_per_job, out);
+    (void)max_n;
+    hipLaunchKernelGGL(k_sparse_align_reg<1024>, dim3(njobs), dim3(1024), 0, st, lv, cam, jobs, scratch,
+                       scratch_per_job, out);
     return hipGetLastError();
 }
 

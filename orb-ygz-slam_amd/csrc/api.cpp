@@ -801,7 +801,7 @@ int ygzfe_sparse_align(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygz
     job.T_init = *T_init;
     YGZ_HIP(hipMemcpyAsync(dj.p, &job, sizeof(job), hipMemcpyHostToDevice, st));
     YGZ_HIP(launch_sparse_align(levels_of(P), *cam, dj.as<AlignJob>(), 1, ds.as<float>(), spj,
-                                dout.as<ygzfe_align_result>(), st));
+                                dout.as<ygzfe_align_result>(), st, n));
     YGZ_HIP(hipMemcpyAsync(result, dout.p, sizeof(*result), hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipStreamSynchronize(st));
     return YGZFE_OK;
@@ -856,7 +856,7 @@ extern "C" int ygzfe_batch_sparse_align(ygzfe_batch *b, int n_pairs, const int32
     YGZ_HIP(hipGetLastError());
     hipEvent_t t0 = b->begin(st);
     YGZ_HIP(launch_sparse_align(levels_of(P), *cam, b->jobs.as<AlignJob>(), n_pairs, b->ascratch.as<float>(), spj,
-                                d_out, st));
+                                d_out, st, P.kp_cap));
     b->end(ST_ALIGN, t0, st);
     return YGZFE_OK;
 }

@@ -82,35 +82,56 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 __global__ __launch_bounds__(256) void k_blur7(const uint8_t *__restrict__ pyr,
                                                uint8_t *__restrict__ blur, uint32_t pitch,
                                                const Plan *__restrict__ plan) {
-    constexpr int TW = 64, TH = 16, SW = TW + 6, SH = TH + 6;
+    // 64 x 32 output tile; lane = column, the four waves stride over rows, so
+    // every global load / store instruction moves 64 consecutive bytes.
+    constexpr int TW = 64, TH = 32, SW = TW + 6, SH = TH + 6;
     __shared__ uint8_t s_src[SH * SW];
     __shared__ int s_row[SH * TW];
     const int f = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int tile = blockIdx.x, l = 0;
     while (l + 1 < plan->nlevels && tile >= plan->lv[l + 1].blur_tile_begin) l++;
     const LevelDesc &L = plan->lv[l];
     tile -= L.blur_tile_begin;
     const int tx0 = (tile % L.blur_tiles_x) * TW, ty0 = (tile / L.blur_tiles_x) * TH;
     const uint8_t *src = pyr + (size_t)f * pitch + L.off;
-    for (int i = threadIdx.x; i < SH * SW; i += 256) {
-        const int yy = reflect101(ty0 + i / SW - 3, L.h), xx = reflect101(tx0 + i % SW - 3, L.w);
-        s_src[i] = src[(size_t)yy * L.w + xx];
+    // all of a wave's source rows are loaded before any LDS store (one round trip)
+    constexpr int RPW = (SH + 3) / 4;  // rows per wave
+    const int xa = reflect101(tx0 + lane - 3, L.w);
+    const int xb = lane + 64 < SW ? reflect101(tx0 + lane + 64 - 3, L.w) : 0;
+    uint8_t va[RPW], vb[RPW];
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+        const int r = wave + 4 * k;
+        const int yy = reflect101(ty0 + min(r, SH - 1) - 3, L.h);
+        const uint8_t *row = src + (size_t)yy * L.w;
+        va[k] = row[xa];
+        vb[k] = lane + 64 < SW ? row[xb] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+        const int r = wave + 4 * k;
+        if (r < SH) {
+            s_src[r * SW + lane] = va[k];
+            if (lane + 64 < SW) s_src[r * SW + lane + 64] = vb[k];
+        }
     }
     __syncthreads();
     const int k0 = 18, k1 = 34;  // CV4 [18,34,48,56,48,34,18] / CV3 [18,34,49,55,49,34,18]
     const int k2 = plan->blur_variant == YGZFE_BLUR_CV3 ? 49 : 48;
     const int k3 = plan->blur_variant == YGZFE_BLUR_CV3 ? 55 : 56;
-    for (int i = threadIdx.x; i < SH * TW; i += 256) {
-        const uint8_t *p = s_src + (i / TW) * SW + (i % TW);
-        s_row[i] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
+    for (int r = wave; r < SH; r += 4) {
+        const uint8_t *p = s_src + r * SW + lane;
+        s_row[r * TW + lane] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
     }
     __syncthreads();
     uint8_t *dst = blur + (size_t)f * pitch + L.off;
-    for (int i = threadIdx.x; i < TH * TW; i += 256) {
-        const int ry = i / TW, rx = i % TW;
-        const int x = tx0 + rx, y = ty0 + ry;
-        if (x >= L.w || y >= L.h) continue;
-        const int *c = s_row + ry * TW + rx;
+    const int x = tx0 + lane;
+    if (x >= L.w) return;
+    for (int r = wave; r < TH; r += 4) {
+        const int y = ty0 + r;
+        if (y >= L.h) break;
+        const int *c = s_row + r * TW + lane;
         const int acc = k0 * (c[0] + c[6 * TW]) + k1 * (c[TW] + c[5 * TW]) + k2 * (c[2 * TW] + c[4 * TW]) +
                         k3 * c[3 * TW];
         dst[(size_t)y * L.w + x] = (uint8_t)clampi((acc + 32768) >> 16, 0, 255);
@@ -175,373 +196,488 @@ __device__ __forceinline__ int fast9_score(const uint8_t *p, int t) {
     return best - 1;
 }
 
+// One wave per cell (four cells per 256-thread workgroup): the ROI and its
+// score map live in the wave's own LDS slice, pixels are visited in raster
+// order in 64-pixel chunks, and the NMS survivors are compacted with a ballot
+// + mbcnt rank, which keeps cv::FAST's raster order without any workgroup
+// barrier or scan.
+__device__ __forceinline__ void advance_xy(int &x, int &y, int step, int x0, int iw) {
+    x += step;
+    while (x >= x0 + iw) { x -= iw; y++; }
+}
+
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t *__restrict__ pyr, uint32_t pitch,
                                                     const Plan *__restrict__ plan,
                                                     const CellDesc *__restrict__ cells,
                                                     uint32_t *__restrict__ cellbuf,
                                                     int *__restrict__ cellcnt) {
     constexpr int S = kMaxRoi;
-    __shared__ uint8_t s_img[S * S];
-    __shared__ uint8_t s_sc[S * S];
-    __shared__ int s_scan[256];
-    const int c = blockIdx.x, f = blockIdx.y;
+    __shared__ uint8_t s_img[4][S * S];
+    __shared__ uint8_t s_sc[4][S * S];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + wave, f = blockIdx.y;
+    if (c >= plan->ncells) return;
+    uint8_t *img = s_img[wave];
+    uint8_t *sc = s_sc[wave];
     const CellDesc cd = cells[c];
     const LevelDesc &L = plan->lv[cd.level];
     const uint8_t *src = pyr + (size_t)f * pitch + L.off + (size_t)cd.y0 * L.w + cd.x0;
     const int rw = cd.rw, rh = cd.rh;
-    for (int i = threadIdx.x; i < rw * rh; i += 256) {
-        const int y = i / rw, x = i - y * rw;
-        s_img[y * S + x] = src[(size_t)y * L.w + x];
+    // ROI -> LDS: lane = column; 8 rows of loads are issued before their LDS
+    // stores so the wave pays one memory round trip per 8 rows, not per row.
+    for (int r0 = 0; r0 < rh; r0 += 8) {
+        uint8_t v0[8], v1[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int r = r0 + k;
+            const uint8_t *row = src + (size_t)min(r, rh - 1) * L.w;
+            v0[k] = lane < rw ? row[lane] : 0;
+            v1[k] = lane + 64 < rw ? row[lane + 64] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int r = r0 + k;
+            if (r < rh) {
+                if (lane < rw) img[r * S + lane] = v0[k];
+                if (lane + 64 < rw) img[r * S + lane + 64] = v1[k];
+            }
+        }
     }
     const int iw = rw - 6, ih = rh - 6, n = iw > 0 && ih > 0 ? iw * ih : 0;
-    const int per = (n + 255) / 256;
     uint32_t *out = cellbuf + ((size_t)f * plan->ncells + c) * plan->cell_cap;
     int total = 0;
     for (int pass = 0; pass < 2; pass++) {
         const int th = pass == 0 ? plan->ini_th : plan->min_th;
-        for (int i = threadIdx.x; i < S * S; i += 256) s_sc[i] = 0;
-        __syncthreads();
-        for (int i = threadIdx.x; i < n; i += 256) {
-            const int y = 3 + i / iw, x = 3 + i % iw;
-            const int s = fast9_score(s_img + y * S + x, th);
-            if (s >= 0) s_sc[y * S + x] = (uint8_t)s;
-        }
-        __syncthreads();
-        // NMS + order-preserving compaction: thread t owns interior pixels [t*per, (t+1)*per)
-        const int b = threadIdx.x * per, e = min(n, b + per);
-        int cnt = 0;
-        for (int i = b; i < e; i++) {
-            const int y = 3 + i / iw, x = 3 + i % iw;
-            const uint8_t *r = s_sc + y * S + x;
-            const int s = r[0];
-            cnt += s > 0 && s > r[-1] && s > r[1] && s > r[-S - 1] && s > r[-S] && s > r[-S + 1] &&
-                   s > r[S - 1] && s > r[S] && s > r[S + 1];
-        }
-        s_scan[threadIdx.x] = cnt;
-        __syncthreads();
-        for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan
-            const int v = threadIdx.x >= o ? s_scan[threadIdx.x - o] : 0;
-            __syncthreads();
-            s_scan[threadIdx.x] += v;
-            __syncthreads();
-        }
-        total = s_scan[255];
-        int pos = s_scan[threadIdx.x] - cnt;
-        for (int i = b; i < e; i++) {
-            const int y = 3 + i / iw, x = 3 + i % iw;
-            const uint8_t *r = s_sc + y * S + x;
-            const int s = r[0];
-            if (s > 0 && s > r[-1] && s > r[1] && s > r[-S - 1] && s > r[-S] && s > r[-S + 1] &&
-                s > r[S - 1] && s > r[S] && s > r[S + 1]) {
-                if (pos < plan->cell_cap) out[pos] = pack_key(x + cd.offx, y + cd.offy, s);
-                pos++;
+        for (int i = lane; i < rh * (S / 4); i += 64) reinterpret_cast<uint32_t *>(sc)[i] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int x = 3, y = 3;
+        advance_xy(x, y, lane, 3, iw);
+        for (int i = 0; i < n; i += 64) {
+            if (i + lane < n) {
+                const int s = fast9_score(img + y * S + x, th);
+                if (s >= 0) sc[y * S + x] = (uint8_t)s;
             }
+            advance_xy(x, y, 64, 3, iw);
         }
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        x = 3;
+        y = 3;
+        advance_xy(x, y, lane, 3, iw);
+        for (int i = 0; i < n; i += 64) {
+            bool keep = false;
+            int s = 0;
+            if (i + lane < n) {
+                const uint8_t *r = sc + y * S + x;
+                s = r[0];
+                keep = s > 0 && s > r[-1] && s > r[1] && s > r[-S - 1] && s > r[-S] && s > r[-S + 1] &&
+                       s > r[S - 1] && s > r[S] && s > r[S + 1];
+            }
+            const uint64_t m = __ballot(keep);
+            const int pos = total + popc_below(m);
+            if (keep && pos < plan->cell_cap) out[pos] = pack_key(x + cd.offx, y + cd.offy, s);
+            total += __popcll(m);
+            advance_xy(x, y, 64, 3, iw);
+        }
         if (total > 0) break;
     }
-    if (threadIdx.x == 0) cellcnt[(size_t)f * plan->ncells + c] = min(total, plan->cell_cap);
+    if (lane == 0) cellcnt[(size_t)f * plan->ncells + c] = min(total, plan->cell_cap);
 }
 
 // ---------------------------------------------------------------------------
-// Octree distribution (DistributeOctTree, ORBextractor.cc:533-723), one wave per
-// (level, frame).  The std::list is a node pool in LDS with prev/next links;
-// every list operation is executed uniformly by the whole wave.  Node key sets
-// are contiguous segments of a key array; DivideNode is a stable 4-way
-// partition of the segment into the other buffer of a ping-pong pair
-// (ballot + mbcnt ranks), so keys keep their candidate order and "first max
-// response wins" is preserved.  The std::sort tie-break on node pointers is
-// the node creation order (seq), as in oracle/orb.c.
+// Octree distribution (DistributeOctTree, ORBextractor.cc:533-723 with
+// ExtractorNode::DivideNode :479-531), one 256-thread workgroup per
+// (frame, level), level-synchronous.
+//
+// The reference walks a std::list and divides one node at a time, pushing the
+// non-empty children (n1..n4) to the front.  One walk of the main loop (:593-635)
+// therefore yields   [children of the last divided node, n4..n1] ... [children of
+// the first divided node, n4..n1] ++ [undivided nodes in their old order],
+// and the children are created (= the std::sort pointer tie-break, :656, taken
+// as creation order like oracle/orb.c) in division order, n1..n4.  The same
+// holds for one round of the final loop (:648-672), whose division order is the
+// (size, creation) descending sort and which stops at the first division that
+// makes size >= N: a prefix sum over the sorted candidates finds that cut.
+// So every pass is: quadrant histogram of the keys of the dividing nodes (LDS
+// atomics), prefix sums over nodes for the new list positions and creation
+// numbers, then every key relabels itself with its new node's list position.
+// Keys never move: a node's keys are the keys carrying its label, in candidate
+// order, so the retained key (:700-716, first maximum response) is the
+// max of (score << 24 | (0xFFFFFF - candidate index)).
 
-constexpr uint16_t NIL = 0xFFFF;
-
-template <int NODE_CAP>
-struct OctShared {
-    uint32_t x0y0[NODE_CAP], x1y1[NODE_CAP], beg[NODE_CAP], cnt[NODE_CAP], seq[NODE_CAP];
-    uint16_t prev[NODE_CAP], next[NODE_CAP], freel[NODE_CAP];
-    uint64_t vsp[NODE_CAP], vprev[NODE_CAP];
+template <int NC>
+struct OctLds {
+    uint64_t bnd[2][NC];  // x0 | y0 << 16 | x1 << 32 | y1 << 48, list order
+    uint32_t cnt[2][NC];
+    uint32_t seq[2][NC];  // creation number; bit 31: created with > 1 key by the last pass
+    uint32_t cq[NC][2];   // quadrant key counts (u16 pairs); best key at the end
+    uint32_t mid[NC];     // mx | my << 12 | hist << 30 | div << 31
+    uint32_t remap[NC];   // div << 31 | non-empty quadrant mask << 16 | position
+    uint64_t sortk[NC];   // final-round candidates: cnt << 48 | seq << 16 | node
+    int red[8];
+    int scal[8];
 };
 
-template <int NODE_CAP>
-struct OctState {
-    OctShared<NODE_CAP> *s;
-    uint32_t *A, *B;
-    int head, size, seq, free_top, nvsp;
-    int overflow;
-
-    __device__ int alloc() {
-        if (free_top == 0) { overflow = 1; return 0; }
-        return s->freel[--free_top];
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
     }
-    __device__ void push_front(int id) {
-        s->prev[id] = NIL;
-        s->next[id] = (uint16_t)head;
-        if (head != NIL) s->prev[head] = (uint16_t)id;
-        head = id;
-        size++;
-    }
-    __device__ int erase(int id) {
-        const int p = s->prev[id], nx = s->next[id];
-        if (p != NIL) s->next[p] = (uint16_t)nx; else head = nx;
-        if (nx != NIL) s->prev[nx] = (uint16_t)p;
-        size--;
-        s->freel[free_top++] = (uint16_t)id;
-        return nx;
-    }
-    __device__ void vsp_push(int id) {
-        if (nvsp >= NODE_CAP) { overflow = 1; return; }
-        s->vsp[nvsp++] = ((uint64_t)s->cnt[id] << 40) | ((uint64_t)s->seq[id] << 16) | (uint64_t)id;
-    }
-
-    // ExtractorNode::DivideNode + push_front of the non-empty children (n1..n4);
-    // returns the number of children with more than one key.
-    __device__ int divide(int pid, bool record) {
-        const int lane = threadIdx.x;
-        const uint32_t a = s->x0y0[pid], b = s->x1y1[pid];
-        const int x0 = (int)(a & 0xFFFF), y0 = (int)(a >> 16), x1 = (int)(b & 0xFFFF), y1 = (int)(b >> 16);
-        const uint32_t bg = s->beg[pid];
-        const int flag = (int)(bg >> 31), beg = (int)(bg & 0x7FFFFFFF), n = (int)s->cnt[pid];
-        const int halfX = (int)ceilf((float)(x1 - x0) / 2), halfY = (int)ceilf((float)(y1 - y0) / 2);
-        const int mx = x0 + halfX, my = y0 + halfY;
-        const uint32_t *src = flag ? B : A;
-        uint32_t *dst = flag ? A : B;
-        int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-        if (n <= 64) {
-            const bool act = lane < n;
-            const uint32_t k = act ? src[beg + lane] : 0u;
-            const int x = key_x(k), y = key_y(k);
-            const int q = x < mx ? (y < my ? 0 : 2) : (y < my ? 1 : 3);
-            const uint64_t m0 = __ballot(act && q == 0), m1 = __ballot(act && q == 1);
-            const uint64_t m2 = __ballot(act && q == 2), m3 = __ballot(act && q == 3);
-            c0 = __popcll(m0); c1 = __popcll(m1); c2 = __popcll(m2); c3 = __popcll(m3);
-            const uint64_t mq = q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
-            const int base = q == 0 ? 0 : q == 1 ? c0 : q == 2 ? c0 + c1 : c0 + c1 + c2;
-            if (act) dst[beg + base + popc_below(mq)] = k;
-        } else {
-            for (int i = 0; i < n; i += 64) {
-                const bool act = i + lane < n;
-                const uint32_t k = act ? src[beg + i + lane] : 0u;
-                const int x = key_x(k), y = key_y(k);
-                const int q = x < mx ? (y < my ? 0 : 2) : (y < my ? 1 : 3);
-                c0 += __popcll(__ballot(act && q == 0));
-                c1 += __popcll(__ballot(act && q == 1));
-                c2 += __popcll(__ballot(act && q == 2));
-            }
-            c3 = n - c0 - c1 - c2;
-            int r0 = 0, r1 = c0, r2 = c0 + c1, r3 = c0 + c1 + c2;
-            for (int i = 0; i < n; i += 64) {
-                const bool act = i + lane < n;
-                const uint32_t k = act ? src[beg + i + lane] : 0u;
-                const int x = key_x(k), y = key_y(k);
-                const int q = x < mx ? (y < my ? 0 : 2) : (y < my ? 1 : 3);
-                const uint64_t m0 = __ballot(act && q == 0), m1 = __ballot(act && q == 1);
-                const uint64_t m2 = __ballot(act && q == 2), m3 = __ballot(act && q == 3);
-                const uint64_t mq = q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
-                const int base = q == 0 ? r0 : q == 1 ? r1 : q == 2 ? r2 : r3;
-                if (act) dst[beg + base + popc_below(mq)] = k;
-                r0 += __popcll(m0); r1 += __popcll(m1); r2 += __popcll(m2); r3 += __popcll(m3);
-            }
-        }
-        __syncthreads();  // partition stores visible to the wave before later reads
-        const int cc[4] = {c0, c1, c2, c3};
-        const int bx0[4] = {x0, mx, x0, mx}, by0[4] = {y0, y0, my, my};
-        const int bx1[4] = {mx, x1, mx, x1}, by1[4] = {my, my, y1, y1};
-        int off = 0, expand = 0;
-        for (int q = 0; q < 4; q++) {
-            if (cc[q] > 0) {
-                const int id = alloc();
-                s->x0y0[id] = (uint32_t)bx0[q] | ((uint32_t)by0[q] << 16);
-                s->x1y1[id] = (uint32_t)bx1[q] | ((uint32_t)by1[q] << 16);
-                s->beg[id] = (uint32_t)(beg + off) | ((uint32_t)(flag ^ 1) << 31);
-                s->cnt[id] = (uint32_t)cc[q];
-                s->seq[id] = (uint32_t)seq++;
-                push_front(id);
-                if (cc[q] > 1) {
-                    expand++;
-                    if (record) vsp_push(id);
-                }
-            }
-            off += cc[q];
-        }
-        return expand;
-    }
-};
-
-// bitonic sort of s->vprev[0..n) ascending (padded to a power of two with ~0)
-template <int NODE_CAP>
-__device__ void wave_sort_u64(uint64_t *v, int n) {
-    int p2 = 1;
-    while (p2 < n) p2 <<= 1;
-    for (int i = n + threadIdx.x; i < p2; i += 64) v[i] = ~0ull;
-    __syncthreads();
-    for (int k = 2; k <= p2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < p2; i += 64) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const uint64_t a = v[i], b = v[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) { v[i] = b; v[ixj] = a; }
-                }
-            }
-            __syncthreads();
-        }
+    return v;
 }
 
-template <int NODE_CAP>
-__global__ __launch_bounds__(64) void k_octree(const Plan *__restrict__ plan,
-                                               const uint32_t *__restrict__ cellbuf,
-                                               const int *__restrict__ cellcnt,
-                                               uint32_t *__restrict__ candA, uint32_t *__restrict__ candB,
-                                               uint32_t *__restrict__ sel, int *__restrict__ selcnt,
-                                               int *__restrict__ err) {
-    __shared__ OctShared<NODE_CAP> sh;
-    const int l = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
-    const LevelDesc &L = plan->lv[l];
-    uint32_t *A = candA + (size_t)f * plan->cand_total + L.cand_off;
-    uint32_t *B = candB + (size_t)f * plan->cand_total + L.cand_off;
-    // 1. gather the level's candidates in cell order into B (vToDistributeKeys)
-    int n = 0;
-    for (int cb = 0; cb < L.ncells; cb += 64) {
-        const int c = cb + lane;
-        const int cnt = c < L.ncells ? cellcnt[(size_t)f * plan->ncells + L.cell_begin + c] : 0;
-        int incl = cnt;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += v;
-        }
-        const int tot = __shfl(incl, 63, 64);
-        const int excl = incl - cnt;
-        const int m = min(64, L.ncells - cb);
-        for (int k = 0; k < m; k++) {
-            const int cc = __shfl(cnt, k, 64), base = n + __shfl(excl, k, 64);
-            const uint32_t *cs = cellbuf + ((size_t)f * plan->ncells + L.cell_begin + cb + k) * plan->cell_cap;
-            for (int i = lane; i < cc; i += 64) B[base + i] = cs[i];
-        }
-        n += tot;
+// exclusive scan over the 256 threads of the block; *total = block sum
+__device__ __forceinline__ int block_excl_scan(int v, int *red, int *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int incl = wave_incl_scan(v);
+    if (lane == 63) red[w] = incl;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int r = red[i];
+        off += i < w ? r : 0;
+        tot += r;
     }
     __syncthreads();
-    // 2. initial nodes (push_back order) and stable assignment keys -> node (x / hX)
-    OctState<NODE_CAP> st;
-    st.s = &sh; st.A = A; st.B = B;
-    st.head = NIL; st.size = 0; st.seq = 0; st.nvsp = 0; st.overflow = 0;
-    for (int i = lane; i < NODE_CAP; i += 64) sh.freel[i] = (uint16_t)(NODE_CAP - 1 - i);
-    st.free_top = NODE_CAP;
+    *total = tot;
+    return off + incl - v;
+}
+
+__device__ __forceinline__ int oct_quadrant(uint32_t key, uint32_t mid) {
+    const int mx = (int)(mid & 0xFFFu), my = (int)((mid >> 12) & 0xFFFu);
+    return (key_x(key) < mx ? 0 : 1) + (key_y(key) < my ? 0 : 2);
+}
+
+__device__ __forceinline__ int quad_count(const uint32_t c[2], int q) {
+    return (int)((c[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu);
+}
+
+template <int NC>
+__device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, uint16_t *nid, int n, int N,
+                                            bool final_round, int &cur, int &size, int &seqc, int &nexpand,
+                                            int &overflow) {
+    const int tid = threadIdx.x;
+    // a) which nodes get their keys histogrammed: dividing nodes (main loop) or
+    //    the final-round candidates (vSizeAndPointerToNode of the last pass)
+    for (int i = tid; i < size; i += 256) {
+        const uint64_t b = S.bnd[cur][i];
+        const int x0 = (int)(b & 0xFFFF), y0 = (int)((b >> 16) & 0xFFFF);
+        const int x1 = (int)((b >> 32) & 0xFFFF), y1 = (int)(b >> 48);
+        const int mx = x0 + (int)ceilf((float)(x1 - x0) / 2), my = y0 + (int)ceilf((float)(y1 - y0) / 2);
+        const bool hist = final_round ? (S.seq[cur][i] >> 31) != 0 : S.cnt[cur][i] > 1;
+        S.mid[i] = (uint32_t)mx | ((uint32_t)my << 12) | ((uint32_t)hist << 30) | ((uint32_t)(hist && !final_round) << 31);
+        S.cq[i][0] = 0u;
+        S.cq[i][1] = 0u;
+    }
     __syncthreads();
+    for (int j = tid; j < n; j += 256) {
+        const int i = nid[j];
+        const uint32_t md = S.mid[i];
+        if (md & (1u << 30)) {
+            const int q = oct_quadrant(K[j], md);
+            atomicAdd(&S.cq[i][q >> 1], 1u << ((q & 1) * 16));
+        }
+    }
+    __syncthreads();
+    // b) division order -> E (children created before this node's), Ctot
+    int ctot = 0;
+    if (!final_round) {
+        int carry = 0;
+        for (int i0 = 0; i0 < size; i0 += 256) {
+            const int i = i0 + tid;
+            int e = 0;
+            bool div = false;
+            if (i < size) {
+                div = (S.mid[i] >> 31) != 0;
+                if (div) {
+                    const uint32_t c[2] = {S.cq[i][0], S.cq[i][1]};
+                    e = (quad_count(c, 0) > 0) + (quad_count(c, 1) > 0) + (quad_count(c, 2) > 0) + (quad_count(c, 3) > 0);
+                }
+            }
+            int tot;
+            const int ex = block_excl_scan(e, S.red, &tot);
+            if (div) S.remap[i] = (uint32_t)(carry + ex);
+            carry += tot;
+        }
+        ctot = carry;
+    } else {
+        // candidates, list order -> sortk, then ascending sort; division order is descending
+        int nc = 0;
+        for (int i0 = 0; i0 < size; i0 += 256) {
+            const int i = i0 + tid;
+            const bool cand = i < size && (S.mid[i] & (1u << 30));
+            int tot;
+            const int ex = block_excl_scan(cand ? 1 : 0, S.red, &tot);
+            if (cand)
+                S.sortk[nc + ex] = ((uint64_t)S.cnt[cur][i] << 48) | ((uint64_t)(S.seq[cur][i] & 0x7FFFFFFFu) << 16) |
+                                   (uint64_t)i;
+            nc += tot;
+        }
+        int p2 = 1;
+        while (p2 < nc) p2 <<= 1;
+        if (p2 > NC) { overflow = 1; return; }
+        for (int i = nc + tid; i < p2; i += 256) S.sortk[i] = ~0ull;
+        __syncthreads();
+        for (int k = 2; k <= p2; k <<= 1)
+            for (int jj = k >> 1; jj > 0; jj >>= 1) {
+                for (int i = tid; i < p2; i += 256) {
+                    const int ixj = i ^ jj;
+                    if (ixj > i) {
+                        const uint64_t a = S.sortk[i], b = S.sortk[ixj];
+                        if ((a > b) == ((i & k) == 0)) { S.sortk[i] = b; S.sortk[ixj] = a; }
+                    }
+                }
+                __syncthreads();
+            }
+        // processing order p = 0..nc-1 is sortk[nc-1-p]; cut at the first p with size >= N
+        if (tid == 0) S.scal[0] = nc;  // first p reaching N (nc: none)
+        __syncthreads();
+        int carryE = 0, carryD = 0;
+        for (int p0 = 0; p0 < nc; p0 += 256) {
+            const int p = p0 + tid;
+            int e = 0;
+            int i = 0;
+            if (p < nc) {
+                i = (int)(S.sortk[nc - 1 - p] & 0xFFFF);
+                const uint32_t c[2] = {S.cq[i][0], S.cq[i][1]};
+                e = (quad_count(c, 0) > 0) + (quad_count(c, 1) > 0) + (quad_count(c, 2) > 0) + (quad_count(c, 3) > 0);
+            }
+            int totE, totD;
+            const int exE = block_excl_scan(e, S.red, &totE);
+            const int exD = block_excl_scan(p < nc ? e - 1 : 0, S.red, &totD);
+            if (p < nc) {
+                S.remap[i] = (uint32_t)(carryE + exE);
+                if (size + carryD + exD + (e - 1) >= N) atomicMin(&S.scal[0], p);
+            }
+            carryE += totE;
+            carryD += totD;
+        }
+        __syncthreads();
+        const int pstar = min(S.scal[0], nc - 1);  // last dividing position
+        for (int p = tid; p <= pstar; p += 256) {
+            const int i = (int)(S.sortk[nc - 1 - p] & 0xFFFF);
+            S.mid[i] |= 1u << 31;
+        }
+        __syncthreads();
+        if (pstar >= 0 && tid == 0) {
+            const int i = (int)(S.sortk[nc - 1 - pstar] & 0xFFFF);
+            const uint32_t c[2] = {S.cq[i][0], S.cq[i][1]};
+            const int e = (quad_count(c, 0) > 0) + (quad_count(c, 1) > 0) + (quad_count(c, 2) > 0) + (quad_count(c, 3) > 0);
+            S.scal[1] = (int)S.remap[i] + e;
+        } else if (tid == 0) {
+            S.scal[1] = 0;
+        }
+        __syncthreads();
+        ctot = S.scal[1];
+    }
+    // c) positions: divided -> child block at ctot - E - e (reverse division order);
+    //    undivided -> ctot + rank in list order.  New records into the other buffer.
+    const int nxt = cur ^ 1;
+    int carryK = 0, nexp = 0;
+    for (int i0 = 0; i0 < size; i0 += 256) {
+        const int i = i0 + tid;
+        const bool valid = i < size;
+        const bool div = valid && (S.mid[i] >> 31);
+        int tot;
+        const int ex = block_excl_scan(valid && !div ? 1 : 0, S.red, &tot);
+        if (valid) {
+            if (div) {
+                const uint32_t c[2] = {S.cq[i][0], S.cq[i][1]};
+                int cc[4], mask = 0, e = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    cc[q] = quad_count(c, q);
+                    mask |= (cc[q] > 0) << q;
+                    e += cc[q] > 0;
+                }
+                const int E = (int)S.remap[i];
+                const int start = ctot - E - e;
+                S.remap[i] = (1u << 31) | ((uint32_t)mask << 16) | (uint32_t)start;
+                const uint64_t b = S.bnd[cur][i];
+                const uint32_t x0 = (uint32_t)(b & 0xFFFF), y0 = (uint32_t)((b >> 16) & 0xFFFF);
+                const uint32_t x1 = (uint32_t)((b >> 32) & 0xFFFF), y1 = (uint32_t)(b >> 48);
+                const uint32_t md = S.mid[i];
+                const uint32_t mx = md & 0xFFFu, my = (md >> 12) & 0xFFFu;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (cc[q] == 0) continue;
+                    const int pos = start + __popc((uint32_t)mask >> (q + 1));
+                    if (pos >= NC) { overflow = 1; continue; }
+                    const uint64_t cx0 = (q & 1) ? mx : x0, cx1 = (q & 1) ? x1 : mx;
+                    const uint64_t cy0 = (q & 2) ? my : y0, cy1 = (q & 2) ? y1 : my;
+                    S.bnd[nxt][pos] = cx0 | (cy0 << 16) | (cx1 << 32) | (cy1 << 48);
+                    S.cnt[nxt][pos] = (uint32_t)cc[q];
+                    S.seq[nxt][pos] = (uint32_t)(seqc + E + __popc((uint32_t)mask & ((1u << q) - 1))) |
+                                      ((uint32_t)(cc[q] > 1) << 31);
+                    nexp += cc[q] > 1;
+                }
+            } else {
+                const int pos = ctot + carryK + ex;
+                S.remap[i] = (uint32_t)pos;
+                if (pos >= NC) {
+                    overflow = 1;
+                } else {
+                    S.bnd[nxt][pos] = S.bnd[cur][i];
+                    S.cnt[nxt][pos] = S.cnt[cur][i];
+                    S.seq[nxt][pos] = S.seq[cur][i] & 0x7FFFFFFFu;
+                }
+            }
+        }
+        carryK += tot;
+    }
+    int totx;  // expanders | overflow flags << 24, block-uniform; also orders the writes before the sweep
+    block_excl_scan(nexp | (overflow << 24), S.red, &totx);
+    overflow = totx >> 24 ? 1 : 0;
+    totx &= 0xFFFFFF;
+    // d) every key takes its node's new list position
+    for (int j = tid; j < n; j += 256) {
+        const int i = nid[j];
+        const uint32_t r = S.remap[i];
+        if (r >> 31) {
+            const int q = oct_quadrant(K[j], S.mid[i]);
+            nid[j] = (uint16_t)((r & 0xFFFFu) + __popc(((r >> 16) & 15u) >> (q + 1)));
+        } else {
+            nid[j] = (uint16_t)(r & 0xFFFFu);
+        }
+    }
+    cur = nxt;
+    size = ctot + carryK;
+    seqc += ctot;
+    nexpand = totx;
+    if (size > NC) overflow = 1;
+    __syncthreads();
+}
+
+template <int NC>
+__device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const LevelDesc &L, int l, int f,
+                                            OctLds<NC> &S, const uint32_t *__restrict__ cellbuf,
+                                            const int *__restrict__ cellcnt, int *s_pref, uint32_t *K,
+                                            uint16_t *nid, int n, uint32_t *__restrict__ sel,
+                                            int *__restrict__ selcnt, int *__restrict__ err) {
+    const int tid = threadIdx.x;
+    // 1. vToDistributeKeys in cell order: 256 cells per chunk, key index -> cell by
+    //    binary search over the chunk's exclusive prefix
+    {
+        int base = 0;
+        for (int cb = 0; cb < L.ncells; cb += 256) {
+            const int c = cb + tid;
+            const int cnt = c < L.ncells ? cellcnt[(size_t)f * plan->ncells + L.cell_begin + c] : 0;
+            int tot;
+            s_pref[tid] = block_excl_scan(cnt, S.red, &tot);
+            __syncthreads();
+            const int nch = min(L.ncells - cb, 256);
+            const uint32_t *cs0 = cellbuf + ((size_t)f * plan->ncells + L.cell_begin + cb) * plan->cell_cap;
+            for (int j = tid; j < tot; j += 256) {
+                int lo = 0, hi = nch - 1;
+                while (lo < hi) {
+                    const int md = (lo + hi + 1) >> 1;
+                    if (s_pref[md] <= j) lo = md; else hi = md - 1;
+                }
+                K[base + j] = cs0[(size_t)lo * plan->cell_cap + (j - s_pref[lo])];
+            }
+            base += tot;
+            __syncthreads();
+        }
+    }
+    // 2. initial nodes (:535-580): columns of width hX, push_back order, empty ones erased
     const int nIni = L.n_ini;
     const float hX = L.hX;
     const int H0 = L.max_by - kMinBorder;
-    int ini_ids[8];
-    int ini_cnt[8];
-    for (int i = 0; i < nIni; i++) ini_cnt[i] = 0;
-    for (int i = 0; i < n; i += 64) {
-        const bool act = i + lane < n;
-        const uint32_t k = act ? B[i + lane] : 0u;
-        int idx = (int)((float)key_x(k) / hX);
+    if (tid < 8) S.scal[tid] = 0;
+    __syncthreads();
+    for (int j = tid; j < n; j += 256) {
+        int idx = (int)((float)key_x(K[j]) / hX);
         idx = idx >= nIni ? nIni - 1 : idx;
-        for (int q = 0; q < nIni; q++) ini_cnt[q] += __popcll(__ballot(act && idx == q));
+        nid[j] = (uint16_t)idx;
+        atomicAdd(&S.scal[idx], 1);
     }
-    {
-        int run[8], off = 0;
-        for (int q = 0; q < nIni; q++) { run[q] = off; off += ini_cnt[q]; }
-        for (int i = 0; i < n; i += 64) {
-            const bool act = i + lane < n;
-            const uint32_t k = act ? B[i + lane] : 0u;
-            int idx = (int)((float)key_x(k) / hX);
-            idx = idx >= nIni ? nIni - 1 : idx;
-            for (int q = 0; q < nIni; q++) {
-                const uint64_t m = __ballot(act && idx == q);
-                if (act && idx == q) A[run[q] + popc_below(m)] = k;
-                run[q] += __popcll(m);
+    __syncthreads();
+    int size = 0;
+    for (int i = 0; i < nIni; i++) {
+        const int c = S.scal[i];
+        if (c > 0) {
+            if (tid == 0) {
+                const uint64_t x0 = (uint32_t)(int)(hX * (float)i), x1 = (uint32_t)(int)(hX * (float)(i + 1));
+                S.bnd[0][size] = x0 | (x1 << 32) | ((uint64_t)H0 << 48);
+                S.cnt[0][size] = (uint32_t)c;
+                S.seq[0][size] = (uint32_t)i;
             }
+            if (tid == 0) S.remap[i] = (uint32_t)size;
+            size++;
         }
     }
     __syncthreads();
-    {
-        int off = 0;
-        for (int i = 0; i < nIni; i++) {  // push_back: created in order; linked below
-            const int id = st.alloc();
-            ini_ids[i] = id;
-            sh.x0y0[id] = (uint32_t)(int)(hX * (float)i);
-            sh.x1y1[id] = (uint32_t)(int)(hX * (float)(i + 1)) | ((uint32_t)H0 << 16);
-            sh.beg[id] = (uint32_t)off;
-            sh.cnt[id] = (uint32_t)ini_cnt[i];
-            sh.seq[id] = (uint32_t)st.seq++;
-            off += ini_cnt[i];
-        }
-        for (int i = nIni - 1; i >= 0; i--) st.push_front(ini_ids[i]);
-        for (int i = 0; i < nIni; i++)  // erase empty initial nodes (size-1 ones are bNoMore)
-            if (ini_cnt[i] == 0) st.erase(ini_ids[i]);
-    }
+    for (int j = tid; j < n; j += 256) nid[j] = (uint16_t)S.remap[nid[j]];
     __syncthreads();
-    // 3. DistributeOctTree main loop
+    // 3. main loop (:585-680)
     const int N = L.budget;
-    bool finish = false;
-    while (!finish && !st.overflow) {
-        const int prevSize = st.size;
-        int nToExpand = 0;
-        st.nvsp = 0;
-        int it = st.head;
-        while (it != NIL) {
-            if (sh.cnt[it] == 1) { it = sh.next[it]; continue; }
-            nToExpand += st.divide(it, true);
-            it = st.erase(it);
-            __syncthreads();
-            if (st.overflow) break;
-        }
-        if (st.size >= N || st.size == prevSize) {
-            finish = true;
-        } else if (st.size + nToExpand * 3 > N) {
-            while (!finish && !st.overflow) {
-                const int prev2 = st.size;
-                const int nprev = st.nvsp;
-                for (int i = lane; i < nprev; i += 64) sh.vprev[i] = sh.vsp[i];
-                __syncthreads();
-                st.nvsp = 0;
-                wave_sort_u64<NODE_CAP>(sh.vprev, nprev);
-                for (int j = nprev - 1; j >= 0; j--) {
-                    const int id = (int)(sh.vprev[j] & 0xFFFF);
-                    st.divide(id, true);
-                    st.erase(id);
-                    __syncthreads();
-                    if (st.size >= N || st.overflow) break;
-                }
-                if (st.size >= N || st.size == prev2) finish = true;
-            }
-        }
+    int cur = 0, seqc = nIni, overflow = 0, nexpand = 0, guard = 0;
+    bool final_round = false;
+    while (true) {
+        const int prev = size;
+        octree_pass<NC>(S, K, nid, n, N, final_round, cur, size, seqc, nexpand, overflow);
+        if (overflow || ++guard > 4096) { overflow = 1; break; }
+        if (size >= N || size == prev) break;
+        if (!final_round && size + nexpand * 3 > N) final_round = true;
     }
-    // 4. retain the best key per node, list order
+    // 4. retained key per node, list order
     uint32_t *out = sel + (size_t)f * plan->sel_total + L.sel_off;
-    int k = 0;
-    for (int it = st.head; it != NIL && !st.overflow; it = sh.next[it]) {
-        const uint32_t bg = sh.beg[it];
-        const uint32_t *src = (bg >> 31) ? B : A;
-        const int beg = (int)(bg & 0x7FFFFFFF), cnt = (int)sh.cnt[it];
-        uint32_t best;
-        if (cnt == 1) {
-            best = src[beg];
-        } else {
-            uint32_t bestv = 0;  // (score << 24) | (0xFFFFFF - index): max = highest score, first index
-            for (int i = lane; i < cnt; i += 64) {
-                const uint32_t v = ((uint32_t)key_score(src[beg + i]) << 24) | (uint32_t)(0xFFFFFF - i);
-                bestv = v > bestv ? v : bestv;
-            }
-            for (int o = 32; o >= 1; o >>= 1) {
-                const uint32_t t = (uint32_t)__shfl_xor((int)bestv, o, 64);
-                bestv = t > bestv ? t : bestv;
-            }
-            best = src[beg + (0xFFFFFF - (bestv & 0xFFFFFF))];
-        }
-        if (k < L.sel_cap) {
-            if (lane == 0) out[k] = best;
-        } else {
-            st.overflow = 1;
-        }
-        k++;
+    if (!overflow) {
+        for (int i = tid; i < size; i += 256) S.cq[i][0] = 0u;
+        __syncthreads();
+        for (int j = tid; j < n; j += 256)
+            atomicMax(&S.cq[nid[j]][0], ((uint32_t)key_score(K[j]) << 24) | (uint32_t)(0xFFFFFF - j));
+        __syncthreads();
+        if (size > L.sel_cap) overflow = 1;
+        for (int i = tid; i < size && i < L.sel_cap; i += 256) out[i] = K[0xFFFFFF - (S.cq[i][0] & 0xFFFFFFu)];
     }
-    if (lane == 0) {
-        selcnt[(size_t)f * plan->nlevels + l] = min(k, L.sel_cap);
-        if (st.overflow) atomicOr(err, 1);
+    if (tid == 0) {
+        selcnt[(size_t)f * plan->nlevels + l] = overflow ? 0 : min(size, L.sel_cap);
+        if (overflow) atomicOr(err, 1);
+    }
+}
+
+// Keys and labels in LDS when the level has at most kOctLdsKeys candidates
+// (the common case), else in the global scratch; the node lists always in LDS.
+// 4000 keeps the NC=1024 workgroup under 80 KiB: two workgroups per CU.
+constexpr int kOctLdsKeys = 4000;
+
+template <int NC>
+__global__ __launch_bounds__(256) void k_octree(const Plan *__restrict__ plan,
+                                                const uint32_t *__restrict__ cellbuf,
+                                                const int *__restrict__ cellcnt,
+                                                uint32_t *__restrict__ candA, uint32_t *__restrict__ candB,
+                                                uint32_t *__restrict__ sel, int *__restrict__ selcnt,
+                                                int *__restrict__ err) {
+    __shared__ OctLds<NC> S;
+    __shared__ uint32_t sK[kOctLdsKeys];
+    __shared__ uint16_t sNid[kOctLdsKeys];
+    int *s_pref = reinterpret_cast<int *>(S.sortk);  // gather prefix; sortk is free until the final rounds
+    const int f = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
+    const LevelDesc &L = plan->lv[l];
+    int part = 0;
+    for (int c = tid; c < L.ncells; c += 256) part += cellcnt[(size_t)f * plan->ncells + L.cell_begin + c];
+    int n;
+    block_excl_scan(part, S.red, &n);
+    if (n > 65535) {  // u16 labels / quadrant counts
+        if (tid == 0) {
+            selcnt[(size_t)f * plan->nlevels + l] = 0;
+            atomicOr(err, 1);
+        }
+        return;
+    }
+    if (n <= kOctLdsKeys) {
+        octree_body<NC>(plan, L, l, f, S, cellbuf, cellcnt, s_pref, sK, sNid, n, sel, selcnt, err);
+    } else {
+        uint32_t *K = candA + (size_t)f * plan->cand_total + L.cand_off;
+        uint16_t *nid = reinterpret_cast<uint16_t *>(candB + (size_t)f * plan->cand_total + L.cand_off);
+        octree_body<NC>(plan, L, l, f, S, cellbuf, cellcnt, s_pref, K, nid, n, sel, selcnt, err);
     }
 }
 
@@ -621,13 +757,18 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     const int idx = blockIdx.x * 4 + wave;
     const int *sc = selcnt + (size_t)f * plan->nlevels;
     const int ne = n_existing ? n_existing[f] : 0;
-    int l = 0, pre = 0;
-    while (l < plan->nlevels && idx >= pre + sc[l]) { pre += sc[l]; l++; }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        int tot = 0;
-        for (int q = 0; q < plan->nlevels; q++) tot += sc[q];
-        counts[f] = ne + tot;
+    // per-level counts in one load (lane q holds level q), prefix by shuffles
+    const int myc = lane < plan->nlevels ? sc[lane] : 0;
+    int incl = myc;
+    for (int o = 1; o < 16; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
     }
+    const uint64_t below = __ballot(lane < plan->nlevels && incl <= idx);
+    const int l = __popcll(below);  // levels entirely before idx
+    const int tot = __shfl(incl, plan->nlevels - 1, 64);
+    const int pre = l > 0 ? __shfl(incl, l - 1, 64) : 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) counts[f] = ne + tot;
     if (l >= plan->nlevels) return;
     const LevelDesc &L = plan->lv[l];
     const uint32_t key = sel[(size_t)f * plan->sel_total + L.sel_off + (idx - pre)];
@@ -703,7 +844,7 @@ hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const 
 hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const CellDesc *dcells,
                        uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st) {
     if (hp.ncells == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fast_cells, dim3(hp.ncells, nframes), dim3(256), 0, st, pyr, pitch, dp, dcells,
+    hipLaunchKernelGGL(k_fast_cells, dim3((hp.ncells + 3) / 4, nframes), dim3(256), 0, st, pyr, pitch, dp, dcells,
                        cellbuf, cellcnt);
     return hipGetLastError();
 }
@@ -711,13 +852,13 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
 hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
                          uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int nframes,
                          hipStream_t st) {
-    dim3 grid(hp.nlevels, nframes);
+    dim3 grid(nframes, hp.nlevels);  // level-0 workgroups (the longest) dispatch first
     if (hp.node_cap <= 512)
-        hipLaunchKernelGGL(k_octree<512>, grid, dim3(64), 0, st, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err);
+        hipLaunchKernelGGL(k_octree<512>, grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err);
     else if (hp.node_cap <= 1024)
-        hipLaunchKernelGGL(k_octree<1024>, grid, dim3(64), 0, st, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err);
+        hipLaunchKernelGGL(k_octree<1024>, grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err);
     else
-        hipLaunchKernelGGL(k_octree<2048>, grid, dim3(64), 0, st, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err);
+        hipLaunchKernelGGL(k_octree<2048>, grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err);
     return hipGetLastError();
 }
 

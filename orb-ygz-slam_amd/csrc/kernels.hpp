@@ -56,7 +56,7 @@ struct AlignJob {
 };
 hipError_t launch_sparse_align(const AlignLevels &lv, const ygzfe_camera &cam, const AlignJob *jobs,
                                int njobs, float *scratch, size_t scratch_per_job, ygzfe_align_result *out,
-                               hipStream_t st);
+                               hipStream_t st, int max_n);
 size_t sparse_align_scratch_floats(int n);
 hipError_t launch_align2d(const uint8_t *img, int w, int h, int n, const uint8_t *pwb, const uint8_t *p,
                           int n_iter, float *px, uint8_t *conv, hipStream_t st);

@@ -92,7 +92,7 @@ int build_plan(const ygzfe_orb_params &p, int W, int H, PlanHost *ph, char *err,
         L.inv_scale = s.inv_scale[l];
         L.blur_tile_begin = blur_tiles;
         L.blur_tiles_x = (L.w + 63) / 64;
-        L.blur_tiles_y = (L.h + 15) / 16;
+        L.blur_tiles_y = (L.h + 31) / 32;
         blur_tiles += L.blur_tiles_x * L.blur_tiles_y;
         // resize mode (cv::resize, see oracle/orb.c ygzo_resize)
         if (l > 0) {
@@ -195,7 +195,7 @@ int build_plan(const ygzfe_orb_params &p, int W, int H, PlanHost *ph, char *err,
         L.cand_off = cand_total;
         cand_total += L.cand_cap;
     }
-    P.pyr_bytes = off;
+    P.pyr_bytes = off + 64;  // tail padding: dword row gathers may read up to 11 bytes past a window
     P.ncells = (int)ph->cells.size();
     P.cell_cap = cell_cap;
     P.sel_total = sel_total;

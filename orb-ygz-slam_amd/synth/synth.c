@@ -29,7 +29,10 @@ static inline int uni(uint64_t *s, int lo, int hi) { /* inclusive */
 void ygzs_texture(uint64_t seed, int W, int H, uint8_t *out) {
     uint64_t s = seed * 0x2545F4914F6CDD1Dull + 0x1234567ull;
     memset(out, 128, (size_t)W * H);
-    for (int r = 0; r < 600; r++) {
+    /* 600 rectangles per 752x480 of area, at least 600 */
+    long nr = 600L * W * H / (752L * 480L);
+    if (nr < 600) nr = 600;
+    for (long r = 0; r < nr; r++) {
         int x0 = uni(&s, 0, W - 1), y0 = uni(&s, 0, H - 1);
         int w = uni(&s, 4, 60), h = uni(&s, 4, 60), v = uni(&s, 0, 255);
         int x1 = x0 + w > W ? W : x0 + w, y1 = y0 + h > H ? H : y0 + h;
