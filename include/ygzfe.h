@@ -151,6 +151,10 @@ int ygzfe_batch_device_results(ygzfe_batch *b, ygzfe_kp **d_kps, uint8_t **d_des
 /* Per-frame pyramid level view of the batch (device pointer + stride). */
 int ygzfe_batch_level(ygzfe_batch *b, int frame, int level, const uint8_t **d_level, int *w,
                       int *h, int *stride);
+/* Synchronise and copy level `level` of frame `frame` to the host: the pyramid
+ * level (mvImagePyramid, blurred == 0) or its GaussianBlur(7x7, sigma 2) copy
+ * that computeDescriptors reads (ORBextractor.cc:1079-1084, blurred != 0). */
+int ygzfe_batch_read_level(ygzfe_batch *b, int frame, int level, int blurred, uint8_t *dst, int dst_stride);
 /* Kernel timing (hipEvents around each stage launch on the batch stream).
  * enable != 0 turns it on; ms[] receives per-stage milliseconds of the last
  * ygzfe_batch_extract; names[] the stage names. Returns stage count. */

@@ -651,6 +651,21 @@ int ygzfe_batch_level(ygzfe_batch *b, int frame, int level, const uint8_t **d_le
     return YGZFE_OK;
 }
 
+int ygzfe_batch_read_level(ygzfe_batch *b, int frame, int level, int blurred, uint8_t *dst, int dst_stride) {
+    if (!b || !dst || frame < 0 || frame >= b->maxF) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    const Plan &P = b->plan->hp();
+    if (level < 0 || level >= P.nlevels) { set_error("level out of range"); return YGZFE_EINVAL; }
+    const LevelDesc &L = P.lv[level];
+    if (dst_stride < L.w) { set_error("dst_stride < level width"); return YGZFE_EINVAL; }
+    const DevBuf &src = blurred ? b->ws.blur : b->pyr;
+    if (!src.p) { set_error("no %s buffer yet (run ygzfe_batch_extract first)", blurred ? "blurred" : "pyramid"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(b->device));
+    YGZ_HIP(hipStreamSynchronize(b->stream));
+    YGZ_HIP(hipMemcpy2D(dst, dst_stride, (const uint8_t *)src.p + (size_t)frame * P.pyr_bytes + L.off, L.w, L.w, L.h,
+                        hipMemcpyDeviceToHost));
+    return YGZFE_OK;
+}
+
 int ygzfe_batch_timing(ygzfe_batch *b, int enable, float *ms, const char **names, int cap) {
     if (!b) { set_error("null batch"); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(b->device));

@@ -63,6 +63,7 @@ struct Plan {
     int blur_variant;
     int blur_tiles;           // total blur tiles over levels
     int node_cap;             // octree node pool capacity (template instance)
+    int fast_S;               // LDS row stride of a FAST cell ROI (max ROI side, multiple of 4)
     int umax[16];             // IC_Angle circle rows (ORBextractor.cc:453-467)
     LevelDesc lv[kMaxLevels];
 };

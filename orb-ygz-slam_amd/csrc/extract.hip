@@ -79,62 +79,135 @@ __device__ __forceinline__ int reflect101(int i, int n) {
     return i;
 }
 
+// One wave per 256-column x kBlurRows-row strip, no LDS: lane owns 4 adjacent
+// columns; each source row is read as 4 aligned dwords per lane (prefetched two
+// rows ahead), the 10-byte window realigned with v_alignbyte, the horizontal
+// taps are two v_dot4_u32_u8 per pixel, and the vertical taps slide over a
+// 7-row register ring.  The window start is clamped at the row start, so the
+// first four columns (lane 0 of the first strip) and the last three (whose taps
+// reach past the row) come out wrong; they are not stored by the main loop and
+// are recomputed with BORDER_REFLECT_101 taps at the end.
+constexpr int kBlurRows = 16;
+
+struct BlurWin {
+    const uint32_t *q;
+    uint32_t o;
+};
+
+__device__ __forceinline__ void blur_hsum(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t o,
+                                          uint32_t ka, uint32_t kb, int h[4]) {
+    const uint32_t p0 = __builtin_amdgcn_alignbyte(w1, w0, o);
+    const uint32_t p1 = __builtin_amdgcn_alignbyte(w2, w1, o);
+    const uint32_t p2 = __builtin_amdgcn_alignbyte(w3, w2, o);
+    h[0] = (int)__builtin_amdgcn_udot4(p1, kb, __builtin_amdgcn_udot4(p0, ka, 0u, false), false);
+#pragma unroll
+    for (int j = 1; j < 4; j++)
+        h[j] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(p2, p1, j), kb,
+                                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(p1, p0, j), ka, 0u, false),
+                                           false);
+}
+
+// exact 7x7 output at (x, y) with reflected taps (border columns, tiny levels)
+__device__ __forceinline__ uint8_t blur_pixel_reflect(const uint8_t *__restrict__ src, int w, int h, int x, int y,
+                                                      const int kk[7]) {
+    int xs[7], acc = 0;
+#pragma unroll
+    for (int k = 0; k < 7; k++) xs[k] = reflect101(x - 3 + k, w);
+#pragma unroll
+    for (int r = 0; r < 7; r++) {
+        const uint8_t *row = src + (size_t)reflect101(y - 3 + r, h) * w;
+        int hs = 0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) hs += kk[k] * row[xs[k]];
+        acc += kk[r] * hs;
+    }
+    return (uint8_t)min((acc + 32768) >> 16, 255);
+}
+
 __global__ __launch_bounds__(256) void k_blur7(const uint8_t *__restrict__ pyr,
                                                uint8_t *__restrict__ blur, uint32_t pitch,
                                                const Plan *__restrict__ plan) {
-    // 64 x 32 output tile; lane = column, the four waves stride over rows, so
-    // every global load / store instruction moves 64 consecutive bytes.
-    constexpr int TW = 64, TH = 32, SW = TW + 6, SH = TH + 6;
-    __shared__ uint8_t s_src[SH * SW];
-    __shared__ int s_row[SH * TW];
     const int f = blockIdx.y;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int tile = blockIdx.x, l = 0;
-    while (l + 1 < plan->nlevels && tile >= plan->lv[l + 1].blur_tile_begin) l++;
+    const int lane = threadIdx.x & 63;
+    int task = blockIdx.x * 4 + (threadIdx.x >> 6), l = 0;
+    if (task >= plan->blur_tiles) return;
+    while (l + 1 < plan->nlevels && task >= plan->lv[l + 1].blur_tile_begin) l++;
     const LevelDesc &L = plan->lv[l];
-    tile -= L.blur_tile_begin;
-    const int tx0 = (tile % L.blur_tiles_x) * TW, ty0 = (tile / L.blur_tiles_x) * TH;
+    task -= L.blur_tile_begin;
+    const int w = L.w, hgt = L.h;
+    const int sx = (task % L.blur_tiles_x) * 256, x = sx + 4 * lane, y0 = (task / L.blur_tiles_x) * kBlurRows;
     const uint8_t *src = pyr + (size_t)f * pitch + L.off;
-    // all of a wave's source rows are loaded before any LDS store (one round trip)
-    constexpr int RPW = (SH + 3) / 4;  // rows per wave
-    const int xa = reflect101(tx0 + lane - 3, L.w);
-    const int xb = lane + 64 < SW ? reflect101(tx0 + lane + 64 - 3, L.w) : 0;
-    uint8_t va[RPW], vb[RPW];
+    uint8_t *dst = blur + (size_t)f * pitch + L.off;
+    // kernels: CV4 [18,34,48,56,48,34,18] (default) / CV3 [18,34,49,55,49,34,18]
+    const bool cv3 = plan->blur_variant == YGZFE_BLUR_CV3;
+    const int k0 = 18, k1 = 34, k2 = cv3 ? 49 : 48, k3 = cv3 ? 55 : 56;
+    const int kk[7] = {k0, k1, k2, k3, k2, k1, k0};
+    if (w >= 16) {
+        const uint32_t ka = (uint32_t)k0 | ((uint32_t)k1 << 8) | ((uint32_t)k2 << 16) | ((uint32_t)k3 << 24);
+        const uint32_t kb = (uint32_t)k2 | ((uint32_t)k1 << 8) | ((uint32_t)k0 << 16);
+        const int xw = max(x - 3, 0);  // reads at most 13 bytes past a row end (pyramid tail padding)
+        const bool active = x < w;
+        auto window = [&](int r, uint32_t wv[4], uint32_t &o) {
+            const uintptr_t a = (uintptr_t)(src + (size_t)reflect101(y0 + r - 3, hgt) * w + xw);
+            o = (uint32_t)(a & 3u);
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(a - o);
+            if (active) {
+                wv[0] = q[0]; wv[1] = q[1]; wv[2] = q[2]; wv[3] = q[3];
+            } else {
+                wv[0] = wv[1] = wv[2] = wv[3] = 0u;
+            }
+        };
+        uint32_t wa[4], wb[4], oa, ob;
+        window(0, wa, oa);
+        window(1, wb, ob);
+        int ring[7][4];
 #pragma unroll
-    for (int k = 0; k < RPW; k++) {
-        const int r = wave + 4 * k;
-        const int yy = reflect101(ty0 + min(r, SH - 1) - 3, L.h);
-        const uint8_t *row = src + (size_t)yy * L.w;
-        va[k] = row[xa];
-        vb[k] = lane + 64 < SW ? row[xb] : 0;
-    }
+        for (int r = 0; r < kBlurRows + 6; r++) {
+            uint32_t cw[4] = {wa[0], wa[1], wa[2], wa[3]};
+            const uint32_t co = oa;
 #pragma unroll
-    for (int k = 0; k < RPW; k++) {
-        const int r = wave + 4 * k;
-        if (r < SH) {
-            s_src[r * SW + lane] = va[k];
-            if (lane + 64 < SW) s_src[r * SW + lane + 64] = vb[k];
+            for (int k = 0; k < 4; k++) wa[k] = wb[k];
+            oa = ob;
+            if (r + 2 < kBlurRows + 6) window(r + 2, wb, ob);
+            int hs[4];
+            blur_hsum(cw[0], cw[1], cw[2], cw[3], co, ka, kb, hs);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+#pragma unroll
+                for (int k = 0; k < 6; k++) ring[k][j] = ring[k + 1][j];
+                ring[6][j] = hs[j];
+            }
+            const int y = y0 + r - 6;
+            if (r >= 6 && y < hgt && active) {
+                uint32_t pk = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int acc = k0 * (ring[0][j] + ring[6][j]) + k1 * (ring[1][j] + ring[5][j]) +
+                                    k2 * (ring[2][j] + ring[4][j]) + k3 * ring[3][j];
+                    pk |= (uint32_t)min((acc + 32768) >> 16, 255) << (8 * j);  // CV3 taps sum to 257
+                }
+                uint8_t *o = dst + (size_t)y * w + x;
+                if (x >= 4 && x + 4 <= w - 3 && (((uintptr_t)o) & 3u) == 0) {
+                    *reinterpret_cast<uint32_t *>(o) = pk;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (x + j >= 4 && x + j < w - 3) o[j] = (uint8_t)(pk >> (8 * j));
+                }
+            }
         }
     }
-    __syncthreads();
-    const int k0 = 18, k1 = 34;  // CV4 [18,34,48,56,48,34,18] / CV3 [18,34,49,55,49,34,18]
-    const int k2 = plan->blur_variant == YGZFE_BLUR_CV3 ? 49 : 48;
-    const int k3 = plan->blur_variant == YGZFE_BLUR_CV3 ? 55 : 56;
-    for (int r = wave; r < SH; r += 4) {
-        const uint8_t *p = s_src + r * SW + lane;
-        s_row[r * TW + lane] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
-    }
-    __syncthreads();
-    uint8_t *dst = blur + (size_t)f * pitch + L.off;
-    const int x = tx0 + lane;
-    if (x >= L.w) return;
-    for (int r = wave; r < TH; r += 4) {
-        const int y = ty0 + r;
-        if (y >= L.h) break;
-        const int *c = s_row + r * TW + lane;
-        const int acc = k0 * (c[0] + c[6 * TW]) + k1 * (c[TW] + c[5 * TW]) + k2 * (c[2 * TW] + c[4 * TW]) +
-                        k3 * c[3 * TW];
-        dst[(size_t)y * L.w + x] = (uint8_t)clampi((acc + 32768) >> 16, 0, 255);
+    // border columns (x < 4, x >= w - 3; every column when w < 16) of this strip
+    const int ncol = w >= 16 ? 7 : w;
+    const bool left = sx == 0, right = sx + 256 >= w;
+    if (w >= 16 && !left && !right) return;
+    const int nrows = min(kBlurRows, hgt - y0);
+    for (int t = lane; t < ncol * nrows; t += 64) {
+        const int cidx = t % ncol, r = t / ncol;
+        const int xc = w >= 16 ? (cidx < 4 ? cidx : w - 7 + cidx) : cidx;
+        if (w >= 16 && ((xc < 4 && !left) || (xc >= w - 3 && !right))) continue;
+        const int y = y0 + r;
+        dst[(size_t)y * w + xc] = blur_pixel_reflect(src, w, hgt, xc, y, kk);
     }
 }
 
@@ -151,86 +224,82 @@ __device__ __forceinline__ uint32_t run9(uint32_t m16) {
     return y & 0xFFFFu;
 }
 
-// ring offsets in the ROI tile (stride kMaxRoi)
-__device__ __forceinline__ void ring_vals(const uint8_t *p, int d[16]) {
-    constexpr int S = kMaxRoi;
-    d[0] = p[3 * S];       d[1] = p[1 + 3 * S];  d[2] = p[2 + 2 * S];  d[3] = p[3 + S];
-    d[4] = p[3];           d[5] = p[3 - S];      d[6] = p[2 - 2 * S];  d[7] = p[1 - 3 * S];
-    d[8] = p[-3 * S];      d[9] = p[-1 - 3 * S]; d[10] = p[-2 - 2 * S]; d[11] = p[-3 - S];
-    d[12] = p[-3];         d[13] = p[-3 + S];    d[14] = p[-2 + 2 * S]; d[15] = p[-1 + 3 * S];
+// FAST_t<16> segment test + cornerScore<16> closed form on a ROI tile of row
+// stride S (ring offsets ro[k] = dy*S + dx, Bresenham circle of radius 3):
+//   corner  <=> 9 contiguous ring pixels all > v+t or all < v-t
+//   score   = max(t, max_arc9 min(v - r), max_arc9 min(r - v)) - 1
+__device__ __forceinline__ void ring_offsets(int S, int ro[16]) {
+    ro[0] = 3 * S;      ro[1] = 1 + 3 * S;   ro[2] = 2 + 2 * S;   ro[3] = 3 + S;
+    ro[4] = 3;          ro[5] = 3 - S;       ro[6] = 2 - 2 * S;   ro[7] = 1 - 3 * S;
+    ro[8] = -3 * S;     ro[9] = -1 - 3 * S;  ro[10] = -2 - 2 * S; ro[11] = -3 - S;
+    ro[12] = -3;        ro[13] = -3 + S;     ro[14] = -2 + 2 * S; ro[15] = -1 + 3 * S;
 }
 
-// FAST_t segment test + cornerScore<16> closed form:
-// score = max(t, max_arc9 min(v - r), max_arc9 min(r - v)) - 1 ; -1 if not a corner.
-__device__ __forceinline__ int fast9_score(const uint8_t *p, int t) {
-    int d[16];
-    ring_vals(p, d);
+__device__ __forceinline__ bool fast9_is_corner(const uint8_t *p, const int ro[16], int t) {
     const int v = p[0];
     uint32_t dark = 0, bright = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        dark |= (uint32_t)(d[k] < v - t) << k;
-        bright |= (uint32_t)(d[k] > v + t) << k;
+        const int d = p[ro[k]];
+        dark |= (uint32_t)(d < v - t) << k;
+        bright |= (uint32_t)(d > v + t) << k;
     }
-    if (!run9(dark) && !run9(bright)) return -1;
-    int m2[16], best = t;
+    return run9(dark) | run9(bright);
+}
+
+__device__ __forceinline__ int fast9_corner_score(const uint8_t *p, const int ro[16], int t) {
+    const int v = p[0];
+    int d[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = p[ro[k]];
+    int m2[16], m4[16], best = t;
 #pragma unroll
     for (int k = 0; k < 16; k++) m2[k] = min(v - d[k], v - d[(k + 1) & 15]);
-    int m4[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) m4[k] = min(m2[k], m2[(k + 2) & 15]);
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int m9 = min(min(m4[k], m4[(k + 4) & 15]), v - d[(k + 8) & 15]);
-        best = max(best, m9);
-    }
+    for (int k = 0; k < 16; k++) best = max(best, min(min(m4[k], m4[(k + 4) & 15]), v - d[(k + 8) & 15]));
 #pragma unroll
     for (int k = 0; k < 16; k++) m2[k] = min(d[k] - v, d[(k + 1) & 15] - v);
 #pragma unroll
     for (int k = 0; k < 16; k++) m4[k] = min(m2[k], m2[(k + 2) & 15]);
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int m9 = min(min(m4[k], m4[(k + 4) & 15]), d[(k + 8) & 15] - v);
-        best = max(best, m9);
-    }
+    for (int k = 0; k < 16; k++) best = max(best, min(min(m4[k], m4[(k + 4) & 15]), d[(k + 8) & 15] - v));
     return best - 1;
 }
 
-// One wave per cell (four cells per 256-thread workgroup): the ROI and its
-// score map live in the wave's own LDS slice, pixels are visited in raster
-// order in 64-pixel chunks, and the NMS survivors are compacted with a ballot
-// + mbcnt rank, which keeps cv::FAST's raster order without any workgroup
-// barrier or scan.
-__device__ __forceinline__ void advance_xy(int &x, int &y, int step, int x0, int iw) {
-    x += step;
-    while (x >= x0 + iw) { x -= iw; y++; }
-}
-
+// One wave per cell (four per 256-thread workgroup), each with a dynamic-LDS
+// slice: ROI tile S*S, score map S*S, pixel list 2*(S-6)^2.  Per threshold:
+//   A  every interior pixel: 4-point necessary test (a 9-arc holds two
+//      neighbouring compass points 0/4/8/12), survivors ballot-compacted
+//   B  survivors: full segment test, corners compacted in place
+//   C  corners: score into the map
+//   D  corners: strict 3x3 non-max suppression, survivors -> cell list
+// Every list keeps raster order, so the output order is cv::FAST's.
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t *__restrict__ pyr, uint32_t pitch,
                                                     const Plan *__restrict__ plan,
                                                     const CellDesc *__restrict__ cells,
                                                     uint32_t *__restrict__ cellbuf,
                                                     int *__restrict__ cellcnt) {
-    constexpr int S = kMaxRoi;
-    __shared__ uint8_t s_img[4][S * S];
-    __shared__ uint8_t s_sc[4][S * S];
+    extern __shared__ uint8_t s_dyn[];
+    const int S = plan->fast_S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + wave, f = blockIdx.y;
     if (c >= plan->ncells) return;
-    uint8_t *img = s_img[wave];
-    uint8_t *sc = s_sc[wave];
+    const int slice = 2 * S * S + 2 * (S - 6) * (S - 6);
+    uint8_t *img = s_dyn + (size_t)wave * slice;
+    uint8_t *sc = img + S * S;
+    uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * S);
     const CellDesc cd = cells[c];
     const LevelDesc &L = plan->lv[cd.level];
     const uint8_t *src = pyr + (size_t)f * pitch + L.off + (size_t)cd.y0 * L.w + cd.x0;
     const int rw = cd.rw, rh = cd.rh;
-    // ROI -> LDS: lane = column; 8 rows of loads are issued before their LDS
-    // stores so the wave pays one memory round trip per 8 rows, not per row.
+    // ROI -> LDS: lane = column; 8 rows of loads in flight before their stores
     for (int r0 = 0; r0 < rh; r0 += 8) {
         uint8_t v0[8], v1[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-            const int r = r0 + k;
-            const uint8_t *row = src + (size_t)min(r, rh - 1) * L.w;
+            const uint8_t *row = src + (size_t)min(r0 + k, rh - 1) * L.w;
             v0[k] = lane < rw ? row[lane] : 0;
             v1[k] = lane + 64 < rw ? row[lane + 64] : 0;
         }
@@ -243,48 +312,81 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t *__restrict__ 
             }
         }
     }
+    int ro[16];
+    ring_offsets(S, ro);
     const int iw = rw - 6, ih = rh - 6, n = iw > 0 && ih > 0 ? iw * ih : 0;
+    const float inv_iw = iw > 0 ? 1.0f / (float)iw : 0.f;
     uint32_t *out = cellbuf + ((size_t)f * plan->ncells + c) * plan->cell_cap;
     int total = 0;
     for (int pass = 0; pass < 2; pass++) {
         const int th = pass == 0 ? plan->ini_th : plan->min_th;
         for (int i = lane; i < rh * (S / 4); i += 64) reinterpret_cast<uint32_t *>(sc)[i] = 0u;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        int x = 3, y = 3;
-        advance_xy(x, y, lane, 3, iw);
-        for (int i = 0; i < n; i += 64) {
-            if (i + lane < n) {
-                const int s = fast9_score(img + y * S + x, th);
-                if (s >= 0) sc[y * S + x] = (uint8_t)s;
+        // A: 4-point test over all interior pixels (pixel i -> row i / iw, exact in float)
+        int na = 0;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            const int y = (int)(((float)i + 0.5f) * inv_iw);
+            const int x = i - y * iw;
+            bool cand = false;
+            if (i < n) {
+                const uint8_t *p = img + (y + 3) * S + (x + 3);
+                const int v = p[0], d0 = p[ro[0]], d4 = p[ro[4]], d8 = p[ro[8]], d12 = p[ro[12]];
+                const int hi = v + th, lo = v - th;
+                const bool b0 = d0 > hi, b4 = d4 > hi, b8 = d8 > hi, b12 = d12 > hi;
+                const bool k0 = d0 < lo, k4 = d4 < lo, k8 = d8 < lo, k12 = d12 < lo;
+                cand = ((b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0)) |
+                       ((k0 & k4) | (k4 & k8) | (k8 & k12) | (k12 & k0));
             }
-            advance_xy(x, y, 64, 3, iw);
+            const uint64_t m = __ballot(cand);
+            if (cand) list[na + popc_below(m)] = (uint16_t)((x + 3) | ((y + 3) << 8));
+            na += __popcll(m);
+        }
+        // B: full segment test, compacted in place (writes never pass the read front)
+        int nc = 0;
+        for (int i0 = 0; i0 < na; i0 += 64) {
+            const int i = i0 + lane;
+            const uint16_t e = i < na ? list[i] : (uint16_t)0;
+            const bool corner = i < na && fast9_is_corner(img + (e >> 8) * S + (e & 0xFF), ro, th);
+            const uint64_t m = __ballot(corner);
+            if (corner) list[nc + popc_below(m)] = e;
+            nc += __popcll(m);
+        }
+        // C: scores of the corners
+        for (int i = lane; i < nc; i += 64) {
+            const uint16_t e = list[i];
+            const int off = (e >> 8) * S + (e & 0xFF);
+            sc[off] = (uint8_t)fast9_corner_score(img + off, ro, th);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        x = 3;
-        y = 3;
-        advance_xy(x, y, lane, 3, iw);
-        for (int i = 0; i < n; i += 64) {
+        // D: strict 3x3 NMS over the corner list
+        for (int i0 = 0; i0 < nc; i0 += 64) {
+            const int i = i0 + lane;
             bool keep = false;
-            int s = 0;
-            if (i + lane < n) {
+            int s = 0, x = 0, y = 0;
+            if (i < nc) {
+                const uint16_t e = list[i];
+                x = e & 0xFF;
+                y = e >> 8;
                 const uint8_t *r = sc + y * S + x;
                 s = r[0];
-                keep = s > 0 && s > r[-1] && s > r[1] && s > r[-S - 1] && s > r[-S] && s > r[-S + 1] &&
-                       s > r[S - 1] && s > r[S] && s > r[S + 1];
+                keep = s > r[-1] && s > r[1] && s > r[-S - 1] && s > r[-S] && s > r[-S + 1] && s > r[S - 1] &&
+                       s > r[S] && s > r[S + 1];
             }
             const uint64_t m = __ballot(keep);
             const int pos = total + popc_below(m);
             if (keep && pos < plan->cell_cap) out[pos] = pack_key(x + cd.offx, y + cd.offy, s);
             total += __popcll(m);
-            advance_xy(x, y, 64, 3, iw);
         }
         if (total > 0) break;
     }
     if (lane == 0) cellcnt[(size_t)f * plan->ncells + c] = min(total, plan->cell_cap);
+}
+
+size_t fast_cells_lds_bytes(const Plan &hp) {
+    const int S = hp.fast_S;
+    return 4 * (size_t)(2 * S * S + 2 * (S - 6) * (S - 6));
 }
 
 // ---------------------------------------------------------------------------
@@ -837,14 +939,15 @@ hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Pl
 
 hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
                        int nframes, hipStream_t st) {
-    hipLaunchKernelGGL(k_blur7, dim3(hp.blur_tiles, nframes), dim3(256), 0, st, pyr, blur, pitch, dp);
+    hipLaunchKernelGGL(k_blur7, dim3((hp.blur_tiles + 3) / 4, nframes), dim3(256), 0, st, pyr, blur, pitch, dp);
     return hipGetLastError();
 }
 
 hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const CellDesc *dcells,
                        uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st) {
     if (hp.ncells == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fast_cells, dim3((hp.ncells + 3) / 4, nframes), dim3(256), 0, st, pyr, pitch, dp, dcells,
+    hipLaunchKernelGGL(k_fast_cells, dim3((hp.ncells + 3) / 4, nframes), dim3(256), fast_cells_lds_bytes(hp), st,
+                       pyr, pitch, dp, dcells,
                        cellbuf, cellcnt);
     return hipGetLastError();
 }

@@ -91,8 +91,8 @@ int build_plan(const ygzfe_orb_params &p, int W, int H, PlanHost *ph, char *err,
         L.scale = s.scale[l];
         L.inv_scale = s.inv_scale[l];
         L.blur_tile_begin = blur_tiles;
-        L.blur_tiles_x = (L.w + 63) / 64;
-        L.blur_tiles_y = (L.h + 31) / 32;
+        L.blur_tiles_x = (L.w + 255) / 256;  // k_blur7: one wave per 256 x 16 strip
+        L.blur_tiles_y = (L.h + 15) / 16;
         blur_tiles += L.blur_tiles_x * L.blur_tiles_y;
         // resize mode (cv::resize, see oracle/orb.c ygzo_resize)
         if (l > 0) {
@@ -169,6 +169,7 @@ int build_plan(const ygzfe_orb_params &p, int W, int H, PlanHost *ph, char *err,
                     }
                     const int iw = std::max(c.rw - 6, 0), ih = std::max(c.rh - 6, 0);
                     cell_cap = std::max(cell_cap, ((iw + 1) / 2) * ((ih + 1) / 2));
+                    P.fast_S = std::max(P.fast_S, ((std::max((int)c.rw, (int)c.rh) + 3) / 4) * 4);
                     ph->cells.push_back(c);
                 }
             }
@@ -196,6 +197,7 @@ int build_plan(const ygzfe_orb_params &p, int W, int H, PlanHost *ph, char *err,
         cand_total += L.cand_cap;
     }
     P.pyr_bytes = off + 64;  // tail padding: dword row gathers may read up to 11 bytes past a window
+    P.fast_S = std::max(P.fast_S, 8);
     P.ncells = (int)ph->cells.size();
     P.cell_cap = cell_cap;
     P.sel_total = sel_total;

@@ -342,6 +342,18 @@ class Batch:
         _check(lib().ygzfe_batch_result(self.h, i, _p(kps), self.kp_cap, _p(desc), C.byref(n)), "batch_result")
         return kps[:n.value].copy(), desc[:n.value].copy()
 
+    def level_size(self, level):
+        w, h, st = C.c_int(), C.c_int(), C.c_int()
+        _check(lib().ygzfe_batch_level(self.h, 0, level, None, C.byref(w), C.byref(h), C.byref(st)), "batch_level")
+        return w.value, h.value
+
+    def read_level(self, i, level, blurred=False):
+        """Host copy of pyramid level `level` of frame i (or its 7x7 blurred copy)."""
+        w, h = self.level_size(level)
+        out = np.zeros((h, w), np.uint8)
+        _check(lib().ygzfe_batch_read_level(self.h, i, level, int(bool(blurred)), _p(out), w), "batch_read_level")
+        return out
+
     def match(self, n_pairs, d_qframe, d_tframe, d_bi, d_bd, d_sd, stream=None):
         _check(lib().ygzfe_batch_match(self.h, n_pairs, C.c_void_p(d_qframe), C.c_void_p(d_tframe), C.c_void_p(d_bi),
                                        C.c_void_p(d_bd), C.c_void_p(d_sd), C.c_void_p(stream)), "batch_match")

@@ -134,3 +134,27 @@ def test_featureless_frame(gpu):
     kg, dg = ex.extract(ex.ComputePyramid(img))
     kr, dr = orc.extract(orc.pyramid(img))
     assert len(kg) == len(kr) == 0
+
+
+@pytest.mark.parametrize("size,cfg,blur", [((752, 480), "C2", 0), ((640, 480), "C1", 0), ((641, 479), "C1", 1),
+                                           ((97, 61), "C1", 0), ((30, 20), "C2", 1)])
+def test_batch_blur_every_pixel(gpu, size, cfg, blur):
+    """GaussianBlur(7x7, sigma 2, REFLECT_101) of every level, border columns
+    and rows included (ORBextractor.cc:1079-1084), vs the oracle's blur7."""
+    W, H = size
+    _, _, nf, sf, nl, ini, mn = S.CONFIGS[cfg]
+    # levels must stay >= 1 px: cap nlevels for the tiny image
+    while nl > 1 and round(min(W, H) / sf ** (nl - 1)) < 2:
+        nl -= 1
+    frames = np.stack([S.frame(s, W, H) for s in (11, 12)])
+    b = gpu.Batch((nf, sf, nl, ini, mn, blur), 0, W, H, 2)
+    b.upload(frames)
+    b.extract(len(frames))
+    for i in range(len(frames)):
+        for l in range(b.nlevels):
+            lv = b.read_level(i, l)
+            got = b.read_level(i, l, blurred=True)
+            want = O.blur7(lv, blur)
+            if not np.array_equal(got, want):
+                bad = np.argwhere(got != want)
+                raise AssertionError(f"frame {i} level {l} {lv.shape}: {len(bad)} px differ, first {bad[:5].tolist()}")
