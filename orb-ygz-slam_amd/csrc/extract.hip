@@ -15,7 +15,7 @@
 
 namespace ygzfe {
 
-__constant__ int8_t c_pattern[1024];
+__constant__ __attribute__((aligned(16))) int8_t c_pattern[1024];
 
 // ---------------------------------------------------------------------------
 // Pyramid
@@ -845,7 +845,19 @@ __device__ __forceinline__ void orb_desc_wave(const uint8_t *img, int w, int h, 
     if ((lane & 7) == 0) reinterpret_cast<uint32_t *>(desc_out)[lane >> 3] = word;
 }
 
+// 16-lane row reduction (DPP within a row; every lane of the row gets the sum)
+__device__ __forceinline__ int row16_sum(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
+    return v;
+}
+
 // New keypoints of the octree: rows n_existing + prefix(level) + k.
+// One 16-lane DPP row per keypoint (four per wave, sixteen per workgroup):
+//   IC_Angle: lane s sums columns u = s-15 and u = s+1 over the 31 rows
+//   rBRIEF:   lane s evaluates pairs 16s..16s+15 (half of descriptor word s/2)
 __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__ pyr,
                                                      const uint8_t *__restrict__ blur, uint32_t pitch,
                                                      const Plan *__restrict__ plan,
@@ -855,31 +867,75 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
                                                      ygzfe_kp *__restrict__ kps, uint8_t *__restrict__ desc,
                                                      int *__restrict__ counts, int row_cap) {
     const int f = blockIdx.y;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int idx = blockIdx.x * 4 + wave;
-    const int *sc = selcnt + (size_t)f * plan->nlevels;
+    const int lane = threadIdx.x & 63, s = lane & 15;
+    const int idx = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int nl = plan->nlevels;
+    const int *sc = selcnt + (size_t)f * nl;
     const int ne = n_existing ? n_existing[f] : 0;
-    // per-level counts in one load (lane q holds level q), prefix by shuffles
-    const int myc = lane < plan->nlevels ? sc[lane] : 0;
-    int incl = myc;
+    int incl = lane < nl ? sc[lane] : 0;  // per-level counts, prefix over lanes 0..15
+#pragma unroll
     for (int o = 1; o < 16; o <<= 1) {
         const int v = __shfl_up(incl, o, 64);
         if (lane >= o) incl += v;
     }
-    const uint64_t below = __ballot(lane < plan->nlevels && incl <= idx);
-    const int l = __popcll(below);  // levels entirely before idx
-    const int tot = __shfl(incl, plan->nlevels - 1, 64);
-    const int pre = l > 0 ? __shfl(incl, l - 1, 64) : 0;
+    const int tot = __builtin_amdgcn_readlane(incl, nl - 1);
     if (blockIdx.x == 0 && threadIdx.x == 0) counts[f] = ne + tot;
-    if (l >= plan->nlevels) return;
+    int l = 0, pre = 0;
+    for (int q = 0; q < nl; q++) {
+        const int iq = __builtin_amdgcn_readlane(incl, q);
+        if (iq <= idx) { l = q + 1; pre = iq; }
+    }
+    if (l >= nl || ne + idx >= row_cap) return;  // whole rows leave together
     const LevelDesc &L = plan->lv[l];
+    const int w = L.w, h = L.h;
     const uint32_t key = sel[(size_t)f * plan->sel_total + L.sel_off + (idx - pre)];
     const int cx = key_x(key) + kMinBorder, cy = key_y(key) + kMinBorder;
-    const float angle = ic_angle_wave(pyr + (size_t)f * pitch + L.off, L.w, L.h, cx, cy, plan->umax);
+    // IC_Angle (ORBextractor.cc:77-101)
+    const uint8_t *img = pyr + (size_t)f * pitch + L.off;
+    const int ua = s - 15, ub = s + 1;
+    const bool hasb = s < 15;
+    const int xa = clampi(cx + ua, 0, w - 1), xb = clampi(cx + ub, 0, w - 1);
+    const uint8_t *c0 = img + (size_t)clampi(cy, 0, h - 1) * w;
+    int m10 = ua * c0[xa] + (hasb ? ub * c0[xb] : 0), m01 = 0;
+#pragma unroll
+    for (int v = 1; v <= 15; v++) {
+        const int um = plan->umax[v];
+        const uint8_t *rp = img + (size_t)clampi(cy + v, 0, h - 1) * w;
+        const uint8_t *rm = img + (size_t)clampi(cy - v, 0, h - 1) * w;
+        const int pa = rp[xa], ma = rm[xa], pb = rp[xb], mb = rm[xb];
+        if (-ua <= um) { m01 += v * (pa - ma); m10 += ua * (pa + ma); }
+        if (hasb && ub <= um) { m01 += v * (pb - mb); m10 += ub * (pb + mb); }
+    }
+    m01 = row16_sum(m01);
+    m10 = row16_sum(m10);
+    const float angle = fast_atan2_deg((float)m01, (float)m10);
+    // computeOrbDescriptor (ORBextractor.cc:105-149) on the blurred level
+    const uint8_t *bimg = blur + (size_t)f * pitch + L.off;
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float ang = angle * factorPI;
+    const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
+    const int4 *pp = reinterpret_cast<const int4 *>(c_pattern) + s * 4;  // 16 pairs x (x0,y0,x1,y1)
+    uint32_t bits = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int4 P = pp[q];
+        const uint32_t wd[4] = {(uint32_t)P.x, (uint32_t)P.y, (uint32_t)P.z, (uint32_t)P.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const float px0 = (float)(int8_t)(wd[k] & 0xFF), py0 = (float)(int8_t)((wd[k] >> 8) & 0xFF);
+            const float px1 = (float)(int8_t)((wd[k] >> 16) & 0xFF), py1 = (float)(int8_t)(wd[k] >> 24);
+            const int y0 = cy + cv_round(px0 * sb + py0 * ca), x0 = cx + cv_round(px0 * ca - py0 * sb);
+            const int y1 = cy + cv_round(px1 * sb + py1 * ca), x1 = cx + cv_round(px1 * ca - py1 * sb);
+            const int t0 = bimg[(size_t)clampi(y0, 0, h - 1) * w + clampi(x0, 0, w - 1)];
+            const int t1 = bimg[(size_t)clampi(y1, 0, h - 1) * w + clampi(x1, 0, w - 1)];
+            bits |= (uint32_t)(t0 < t1) << (q * 4 + k);
+        }
+    }
+    const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bits, 0xB1, 0xF, 0xF, false);
     const int row = ne + idx;
-    if (row >= row_cap) return;
-    orb_desc_wave(blur + (size_t)f * pitch + L.off, L.w, L.h, cx, cy, angle, desc + ((size_t)f * row_cap + row) * 32);
-    if (lane == 0) {
+    if ((s & 1) == 0)
+        reinterpret_cast<uint32_t *>(desc + ((size_t)f * row_cap + row) * 32)[s >> 1] = bits | (other << 16);
+    if (s == 0) {
         ygzfe_kp kp;
         kp.x = (float)cx;
         kp.y = (float)cy;
@@ -970,7 +1026,7 @@ hipError_t launch_orient_desc(const uint8_t *pyr, const uint8_t *blur, uint32_t 
                               ygzfe_kp *kps, uint8_t *desc, int *counts, int row_cap, int nframes,
                               hipStream_t st) {
     const int max_new = hp.sel_total;
-    hipLaunchKernelGGL(k_orient_desc, dim3((max_new + 3) / 4, nframes), dim3(256), 0, st, pyr, blur, pitch, dp,
+    hipLaunchKernelGGL(k_orient_desc, dim3((max_new + 15) / 16, nframes), dim3(256), 0, st, pyr, blur, pitch, dp,
                        sel, selcnt, n_existing, kps, desc, counts, row_cap);
     return hipGetLastError();
 }
