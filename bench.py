@@ -53,6 +53,7 @@ def main():
     import torch.distributed as dist
 
     import ygzfe
+    from ygzfe import dist as D
     import _scenes as S
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -70,7 +71,7 @@ def main():
     sc = S.PlaneScene(11, W, H)
     # trajectory: per-frame motion (v, w); frame g has pose exp(g * xi)
     xi = np.array([0.012, -0.006, 0.009, 0.0025, -0.002, 0.0015], np.float32)
-    g0 = rank * B
+    g0, _ = D.shard(world * B, rank, world)  # this rank's contiguous slice (weak scaling: B per rank)
     poses = [ygzfe.trajectory_pose(g0 + i, xi) for i in range(B)]
     t_r = time.time()
     frames = np.stack([sc.render(q, t, noise_seed=g0 + i) for i, (q, t) in enumerate(poses)])
@@ -146,10 +147,7 @@ def main():
     elapsed = time.perf_counter() - t0
     stage_ms = batch.timing(False)
     batch.check()
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    elapsed = D.max_over_ranks(elapsed, dev)
 
     ms_per_step = elapsed * 1000.0 / args.steps
     fps = world * B / (elapsed / args.steps)

@@ -90,6 +90,14 @@ int ygzfe_extractor_features_per_level(const ygzfe_extractor *ex, int32_t *out);
 /* DSO grid state mnGridSize (ORBextractor.h:191): get / set (-1 = recompute). */
 int ygzfe_extractor_dso_grid(ygzfe_extractor *ex, int32_t *get, const int32_t *set);
 
+/* Host-only (no device touched): the extraction plan for a width x height image,
+ * i.e. what ORBextractor::operator() derives per call -- level sizes
+ * cvRound(W/scale) (ORBextractor.cc:1131-1132), feature budgets (:434-445),
+ * umax (:453-467) and the number of FAST cells per level (:728-781).  Arrays
+ * hold nlevels entries (umax: 16); any pointer may be NULL. */
+int ygzfe_orb_plan(const ygzfe_orb_params *p, int width, int height, int32_t *level_w, int32_t *level_h,
+                   int32_t *budget, int32_t *ncells, int32_t *umax);
+
 int ygzfe_frame_create(ygzfe_extractor *ex, int width, int height, ygzfe_frame **out);
 void ygzfe_frame_destroy(ygzfe_frame *f);
 /* Frame::ComputeImagePyramid -> ORBextractor::ComputePyramid

@@ -277,6 +277,23 @@ void ygzfe_extractor_destroy(ygzfe_extractor *ex) {
     delete ex;
 }
 
+int ygzfe_orb_plan(const ygzfe_orb_params *p, int width, int height, int32_t *level_w, int32_t *level_h,
+                   int32_t *budget, int32_t *ncells, int32_t *umax) {
+    if (!p) { set_error("null argument"); return YGZFE_EINVAL; }
+    PlanHost ph;
+    char err[256];
+    if (build_plan(*p, width, height, &ph, err, sizeof(err)) != 0) { set_error("%s", err); return YGZFE_EINVAL; }
+    for (int l = 0; l < ph.plan.nlevels; l++) {
+        if (level_w) level_w[l] = ph.plan.lv[l].w;
+        if (level_h) level_h[l] = ph.plan.lv[l].h;
+        if (budget) budget[l] = ph.plan.lv[l].budget;
+        if (ncells) ncells[l] = ph.plan.lv[l].ncells;
+    }
+    if (umax)
+        for (int i = 0; i < 16; i++) umax[i] = ph.plan.umax[i];
+    return YGZFE_OK;
+}
+
 int ygzfe_extractor_levels(const ygzfe_extractor *ex, int *nlevels, float *scale, float *inv_scale,
                            float *sigma2, float *inv_sigma2) {
     if (!ex) { set_error("null extractor"); return YGZFE_EINVAL; }

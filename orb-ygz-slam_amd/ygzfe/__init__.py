@@ -98,6 +98,16 @@ def device_count():
     return lib().ygzfe_device_count()
 
 
+def orb_plan(nfeatures, scale_factor, nlevels, ini_th=20, min_th=7, width=752, height=480, blur=BLUR_CV4):
+    """Host-only extraction plan (ygzfe_orb_plan): level sizes, budgets, FAST cells, umax."""
+    p = OrbParams(nfeatures, scale_factor, nlevels, ini_th, min_th, blur)
+    w, h, b, nc = (np.zeros(nlevels, np.int32) for _ in range(4))
+    um = np.zeros(16, np.int32)
+    _check(lib().ygzfe_orb_plan(C.byref(p), width, height, _p(w), _p(h), _p(b), _p(nc), _p(um)), "orb_plan")
+    return {"sizes": list(zip(w.tolist(), h.tolist())), "budget": b.tolist(), "ncells": nc.tolist(),
+            "umax": um.tolist()}
+
+
 class Frame:
     """Device-resident pyramid (Frame::mvImagePyramid)."""
 

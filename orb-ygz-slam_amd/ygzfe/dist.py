@@ -1,0 +1,109 @@
+"""Frame sharding across GPUs: one process per GPU, contiguous
+slices of the sequence, no data-path collective.
+
+  * extraction is independent per frame;
+  * SparseImgAlign needs (k-1, k) pairs, so a rank whose slice starts at
+    frame b > 0 also extracts frame b-1 (a one-frame halo) and aligns every
+    pair inside [b-1, e);
+  * results are fixed-size per-frame slots; the offline sequence mode (C5)
+    gathers them to rank 0 once, after the run (point-to-point into the root:
+    `torch.distributed.gather`, which RCCL implements with grouped send/recv over
+    the xGMI peer links).  The bench's timed region has no collective at all:
+    only a barrier and the max-over-ranks of the elapsed time.
+
+Everything here is host-side orchestration on top of torch.distributed; it
+runs the same with the "nccl" (RCCL) backend on GPUs and "gloo" in CPU tests.
+"""
+import numpy as np
+
+# slot layout per frame (little endian):
+#   int32 n_kps, int32 n_visible, float32 T_cur_prev q[4] t[3], float32 chi2,
+#   kps [cap x 28 B] (cv::KeyPoint layout), desc [cap x 32 B]
+SLOT_HEADER = 4 * (2 + 7 + 1)
+
+
+def slot_bytes(cap):
+    return SLOT_HEADER + cap * (28 + 32)
+
+
+def shard(n_frames, rank, world):
+    """Contiguous split of [0, n_frames): the first n % world ranks get one extra frame."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} / world {world}")
+    base, rem = divmod(n_frames, world)
+    begin = rank * base + min(rank, rem)
+    return begin, begin + base + (1 if rank < rem else 0)
+
+
+def with_halo(begin, end):
+    """Frames a rank must extract to align every pair (k-1, k), k in [begin, end)."""
+    return (begin - 1 if begin > 0 else begin), end
+
+
+def align_pairs(begin, end):
+    """(ref, cur) global frame pairs owned by the shard [begin, end)."""
+    return [(k - 1, k) for k in range(max(begin, 1), end)]
+
+
+def pack_slots(counts, kps, desc, align=None):
+    """Per-frame slots (uint8 [F, slot_bytes(cap)]) from numpy results.
+
+    counts [F] int, kps [F, cap] structured (28 B), desc [F, cap, 32] uint8,
+    align: optional [F] records with q, t, n_visible, chi2 (frame k's pose
+    relative to k-1; zero for the first frame of the sequence)."""
+    F, cap = kps.shape[0], kps.shape[1]
+    out = np.zeros((F, slot_bytes(cap)), np.uint8)
+    hdr = np.zeros((F, 10), np.float32)
+    hdr_i = hdr.view(np.int32)
+    hdr_i[:, 0] = counts
+    if align is not None:
+        hdr_i[:, 1] = align["n_visible"]
+        hdr[:, 2:6] = align["q"]
+        hdr[:, 6:9] = align["t"]
+        hdr[:, 9] = align["chi2"]
+    out[:, :SLOT_HEADER] = hdr.view(np.uint8).reshape(F, SLOT_HEADER)
+    out[:, SLOT_HEADER:SLOT_HEADER + cap * 28] = np.ascontiguousarray(kps).view(np.uint8).reshape(F, cap * 28)
+    out[:, SLOT_HEADER + cap * 28:] = np.ascontiguousarray(desc, np.uint8).reshape(F, cap * 32)
+    return out
+
+
+def unpack_slot(slot, cap, kp_dtype):
+    hdr = slot[:SLOT_HEADER].view(np.float32)
+    n = int(hdr.view(np.int32)[0])
+    kps = slot[SLOT_HEADER:SLOT_HEADER + cap * 28].view(kp_dtype)[:n]
+    desc = slot[SLOT_HEADER + cap * 28:].reshape(cap, 32)[:n]
+    return {"n": n, "n_visible": int(hdr.view(np.int32)[1]), "q": hdr[2:6].copy(), "t": hdr[6:9].copy(),
+            "chi2": float(hdr[9]), "kps": kps, "desc": desc}
+
+
+def gather_slots(local_slots, n_frames, rank, world, device=None):
+    """Gather every rank's [end-begin, S] uint8 slot tensor into [n_frames, S] on rank 0.
+
+    Shards differ by at most one frame; each rank pads to the largest shard so a
+    single gather moves everything (rank 0 returns the tensor, others None)."""
+    import torch
+    import torch.distributed as dist
+    S = local_slots.shape[1]
+    maxlen = -(-n_frames // world)
+    pad = torch.zeros((maxlen, S), dtype=torch.uint8, device=device or local_slots.device)
+    pad[:local_slots.shape[0]] = local_slots
+    bufs = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
+    dist.gather(pad, bufs, dst=0)
+    if rank != 0:
+        return None
+    parts = []
+    for r in range(world):
+        b, e = shard(n_frames, r, world)
+        parts.append(bufs[r][:e - b])
+    return torch.cat(parts, 0)
+
+
+def max_over_ranks(seconds, device=None):
+    """The bench's wall time: the slowest rank's (all_reduce MAX of one float64)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(seconds)
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -1,0 +1,153 @@
+"""Property tests of the CPU oracle (test infrastructure), independent of the
+reference binaries: each restated primitive against its definition.
+
+  FAST-9/16 + cornerScore<16> (OpenCV, ORBextractor.cc:765)   brute force segment test
+  resize x2 -> INTER_AREA (ORBextractor.cc:1139)             (a+b+c+d+2)>>2 in numpy
+  GaussianBlur 7x7 (ORBextractor.cc:1083)                     constant images, mirror symmetry
+  DescriptorDistance (ORBmatcher.cc:1507-1523)                numpy popcount
+  DistributeOctTree (ORBextractor.cc:533-723)                 output invariants
+  SE3::exp (se3.hpp:407-428)                                  Rodrigues in float64
+  Align2D (Align.cc:8-105)                                    recovers a known sub-pixel shift
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+RING = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3),
+        (0, -3), (-1, -3), (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+
+
+def brute_best_barrier(patch):
+    """Largest b such that 9 contiguous ring pixels are all > v+b or all < v-b (-1: none)."""
+    v = int(patch[3, 3])
+    d = np.array([int(patch[3 + dy, 3 + dx]) for dx, dy in RING])
+    best = -1
+    for s in range(16):
+        arc = d[(s + np.arange(9)) % 16]
+        best = max(best, int(arc.min() - v) - 1, int(v - arc.max()) - 1)
+    return best
+
+
+def test_fast9_score_closed_form_vs_brute_force():
+    rng = np.random.default_rng(0)
+    lib = O.lib()
+    n_corners = 0
+    for trial in range(3000):
+        patch = rng.integers(0, 256, size=(7, 7), dtype=np.uint8)
+        if trial % 2:  # make many of them corners: push an arc up or down
+            s = rng.integers(16)
+            sign = 1 if rng.integers(2) else -1
+            for k in range(int(rng.integers(9, 13))):
+                dx, dy = RING[(s + k) % 16]
+                patch[3 + dy, 3 + dx] = np.clip(int(patch[3, 3]) + sign * int(rng.integers(10, 120)), 0, 255)
+        patch = np.ascontiguousarray(patch)
+        b = brute_best_barrier(patch)
+        for t in (5, 20):
+            is_corner = b >= t
+            ptr = C.c_void_p(patch.ctypes.data + 3 * 7 + 3)
+            if is_corner:
+                n_corners += 1
+                assert lib.ygzo_corner_score16(ptr, 7, t) == b
+            xs, ys, sc = O.fast9_roi(patch, t)
+            # a 7x7 ROI has exactly one testable pixel (3,3); NMS keeps it iff it is a corner
+            assert len(xs) == int(is_corner)
+    assert n_corners > 500
+
+
+def test_resize_exact_half_is_area_average():
+    rng = np.random.default_rng(1)
+    src = rng.integers(0, 256, size=(60, 94), dtype=np.uint8)
+    got = O.resize(src, 47, 30)
+    s = src.astype(np.int32)
+    want = ((s[0::2, 0::2] + s[0::2, 1::2] + s[1::2, 0::2] + s[1::2, 1::2] + 2) >> 2).astype(np.uint8)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("value", [0, 17, 128, 255])
+def test_blur_constant_image(value):
+    img = np.full((40, 53), value, np.uint8)
+    assert np.array_equal(O.blur7(img, 0), img)  # CV4 taps sum to 256
+
+
+def test_blur_mirror_symmetry():
+    """REFLECT_101 borders and a symmetric kernel: blur(flip(x)) == flip(blur(x))."""
+    rng = np.random.default_rng(2)
+    img = rng.integers(0, 256, size=(33, 47), dtype=np.uint8)
+    for variant in (0, 1):
+        b = O.blur7(img, variant)
+        assert np.array_equal(O.blur7(np.ascontiguousarray(img[:, ::-1]), variant), b[:, ::-1])
+        assert np.array_equal(O.blur7(np.ascontiguousarray(img[::-1]), variant), b[::-1])
+
+
+def test_descriptor_distance_and_best2():
+    rng = np.random.default_rng(3)
+    q = rng.integers(0, 256, size=(50, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, size=(70, 32), dtype=np.uint8)
+    t[10] = q[5]  # an exact match
+    t[11] = q[5]  # ... twice: the first index wins
+    dist = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(2)
+    for i in range(5):
+        assert O.lib().ygzo_descriptor_distance(O._p(q[i]), O._p(t[i])) == dist[i, i]
+    bi, bd, sd = O.hamming_best2(q, t)
+    assert np.array_equal(bd, dist.min(1))
+    assert np.array_equal(bi, dist.argmin(1))  # argmin returns the first minimum
+    assert bi[5] == 10 and bd[5] == 0
+    srt = np.sort(dist, 1)
+    assert np.array_equal(sd, srt[:, 1])
+
+
+def test_octree_invariants():
+    rng = np.random.default_rng(4)
+    img = np.full((240, 376), 128, np.int32)
+    for _ in range(300):
+        x, y = rng.integers(0, 376), rng.integers(0, 240)
+        img[y:y + rng.integers(3, 20), x:x + rng.integers(3, 20)] = rng.integers(0, 256)
+    img = np.clip(img + rng.integers(-3, 4, img.shape), 0, 255).astype(np.uint8)
+    orc = O.OrbOracle(1000, 2.0, 4, 20, 7)
+    budget = orc.feat_per_level[1]
+    kps, ncand = orc.octree_level(img, 1)
+    assert ncand > budget
+    assert budget <= len(kps) <= budget + 3  # splitting stops at the first node count >= N
+    pts = {(float(k["x"]), float(k["y"])) for k in kps}
+    assert len(pts) == len(kps)
+    assert np.all(kps["octave"] == 1)
+
+
+def rodrigues(w):
+    th = np.linalg.norm(w)
+    K = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+    if th < 1e-12:
+        return np.eye(3) + K
+    return np.eye(3) + np.sin(th) / th * K + (1 - np.cos(th)) / th ** 2 * K @ K
+
+
+def test_se3_exp_matches_rodrigues():
+    rng = np.random.default_rng(5)
+    for _ in range(50):
+        x = (rng.standard_normal(6) * [0.1, 0.1, 0.1, 0.3, 0.3, 0.3]).astype(np.float32)
+        T = O.SE3()
+        O.lib().ygzo_se3_exp(O._p(x), C.byref(T))
+        p = rng.standard_normal(3).astype(np.float32)
+        out = np.zeros(3, np.float32)
+        O.lib().ygzo_se3_act(C.byref(T), O._p(p), O._p(out))
+        w, v = x[3:].astype(np.float64), x[:3].astype(np.float64)
+        R = rodrigues(w)
+        th = np.linalg.norm(w)
+        K = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+        V = np.eye(3) + (1 - np.cos(th)) / th ** 2 * K + (th - np.sin(th)) / th ** 3 * K @ K
+        want = R @ p + V @ v
+        assert np.allclose(out, want, atol=2e-5)
+
+
+def test_align2d_recovers_subpixel_shift():
+    yy, xx = np.mgrid[0:64, 0:64].astype(np.float64)
+    img = (128 + 60 * np.sin(xx / 5.0) * np.cos(yy / 7.0) + 30 * np.sin((xx + yy) / 9.0)).astype(np.uint8)
+    u0, v0 = 30, 31
+    rpb = np.ascontiguousarray(img[v0 - 5:v0 + 5, u0 - 5:u0 + 5])  # 10x10 with border, centre (u0, v0)
+    rp = np.ascontiguousarray(rpb[1:9, 1:9])
+    ok, px = O.align2d(img, rpb, rp, (u0 + 0.6, v0 - 0.4))
+    assert ok
+    assert abs(px[0] - u0) < 0.1 and abs(px[1] - v0) < 0.1
