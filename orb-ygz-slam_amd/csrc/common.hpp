@@ -43,6 +43,7 @@ struct LevelDesc {
     int xmax;
     int blur_tile_begin, blur_tiles_x, blur_tiles_y;
     int pyr_tile_begin;
+    int fast_roi;        // largest FAST cell ROI side of this level
 };
 
 struct CellDesc {

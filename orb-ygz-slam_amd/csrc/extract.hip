@@ -225,128 +225,160 @@ __device__ __forceinline__ uint32_t run9(uint32_t m16) {
 }
 
 // FAST_t<16> segment test + cornerScore<16> closed form on a ROI tile of row
-// stride S (ring offsets ro[k] = dy*S + dx, Bresenham circle of radius 3):
+// stride S (compile time, so every ring tap is an immediate ds_read offset from
+// q = centre - 3S - 3):
 //   corner  <=> 9 contiguous ring pixels all > v+t or all < v-t
 //   score   = max(t, max_arc9 min(v - r), max_arc9 min(r - v)) - 1
-__device__ __forceinline__ void ring_offsets(int S, int ro[16]) {
-    ro[0] = 3 * S;      ro[1] = 1 + 3 * S;   ro[2] = 2 + 2 * S;   ro[3] = 3 + S;
-    ro[4] = 3;          ro[5] = 3 - S;       ro[6] = 2 - 2 * S;   ro[7] = 1 - 3 * S;
-    ro[8] = -3 * S;     ro[9] = -1 - 3 * S;  ro[10] = -2 - 2 * S; ro[11] = -3 - S;
-    ro[12] = -3;        ro[13] = -3 + S;     ro[14] = -2 + 2 * S; ro[15] = -1 + 3 * S;
-}
+template <int S>
+struct Ring {
+    // Bresenham circle of radius 3 (cv::FAST order), offsets from q
+    static constexpr int off(int k) {
+        constexpr int dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+        constexpr int dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+        return (dy[k] + 3) * S + (dx[k] + 3);
+    }
+    static constexpr int kCentre = 3 * S + 3;
+};
 
-__device__ __forceinline__ bool fast9_is_corner(const uint8_t *p, const int ro[16], int t) {
-    const int v = p[0];
+template <int S>
+__device__ __forceinline__ bool fast9_is_corner(const uint8_t *q, int t) {
+    const int v = q[Ring<S>::kCentre];
     uint32_t dark = 0, bright = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        const int d = p[ro[k]];
-        dark |= (uint32_t)(d < v - t) << k;
-        bright |= (uint32_t)(d > v + t) << k;
+        const int d = q[Ring<S>::off(k)];
+        dark |= ((uint32_t)(d - (v - t)) >> 31) << k;    // d < v - t
+        bright |= ((uint32_t)((v + t) - d) >> 31) << k;  // d > v + t
     }
     return run9(dark) | run9(bright);
 }
 
-__device__ __forceinline__ int fast9_corner_score(const uint8_t *p, const int ro[16], int t) {
-    const int v = p[0];
-    int d[16];
+template <int S>
+__device__ __forceinline__ int fast9_corner_score(const uint8_t *q, int t) {
+    // e[k] = r_k - v.  bright: max_k min(e[k..k+8]); dark: max_k min(-e[k..k+8])
+    // = -min_k max(e[k..k+8]).  4-wide windows first (v_min3/v_max3), so only
+    // e[] and one window array are live (keeps the kernel under 80 VGPRs).
+    const int v = q[Ring<S>::kCentre];
+    int e[16], w4[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = p[ro[k]];
-    int m2[16], m4[16], best = t;
+    for (int k = 0; k < 16; k++) e[k] = (int)q[Ring<S>::off(k)] - v;
 #pragma unroll
-    for (int k = 0; k < 16; k++) m2[k] = min(v - d[k], v - d[(k + 1) & 15]);
+    for (int k = 0; k < 16; k++) w4[k] = min(min(e[k], e[(k + 1) & 15]), min(e[(k + 2) & 15], e[(k + 3) & 15]));
+    int best = t;
 #pragma unroll
-    for (int k = 0; k < 16; k++) m4[k] = min(m2[k], m2[(k + 2) & 15]);
+    for (int k = 0; k < 16; k++) best = max(best, min(min(w4[k], w4[(k + 4) & 15]), e[(k + 8) & 15]));
 #pragma unroll
-    for (int k = 0; k < 16; k++) best = max(best, min(min(m4[k], m4[(k + 4) & 15]), v - d[(k + 8) & 15]));
+    for (int k = 0; k < 16; k++) w4[k] = max(max(e[k], e[(k + 1) & 15]), max(e[(k + 2) & 15], e[(k + 3) & 15]));
 #pragma unroll
-    for (int k = 0; k < 16; k++) m2[k] = min(d[k] - v, d[(k + 1) & 15] - v);
-#pragma unroll
-    for (int k = 0; k < 16; k++) m4[k] = min(m2[k], m2[(k + 2) & 15]);
-#pragma unroll
-    for (int k = 0; k < 16; k++) best = max(best, min(min(m4[k], m4[(k + 4) & 15]), d[(k + 8) & 15] - v));
+    for (int k = 0; k < 16; k++) best = max(best, -max(max(w4[k], w4[(k + 4) & 15]), e[(k + 8) & 15]));
     return best - 1;
 }
 
 // One wave per cell (four per 256-thread workgroup), each with a dynamic-LDS
 // slice: ROI tile S*S, score map S*S, pixel list 2*(S-6)^2.  Per threshold:
-//   A  every interior pixel: 4-point necessary test (a 9-arc holds two
-//      neighbouring compass points 0/4/8/12), survivors ballot-compacted
+//   A  every interior pixel: 4-point necessary test -- a 9-arc holds a
+//      neighbouring pair of the compass points 0/4/8/12, i.e.
+//      (p0|p8) & (p4|p12) -- done on ballot masks (SGPRs); survivors
+//      compacted (ballot + mbcnt) into the list
 //   B  survivors: full segment test, corners compacted in place
 //   C  corners: score into the map
 //   D  corners: strict 3x3 non-max suppression, survivors -> cell list
 // Every list keeps raster order, so the output order is cv::FAST's.
-__global__ __launch_bounds__(256) void k_fast_cells(const uint8_t *__restrict__ pyr, uint32_t pitch,
+template <int S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_fast_cells(const uint8_t *__restrict__ pyr, uint32_t pitch,
                                                     const Plan *__restrict__ plan,
                                                     const CellDesc *__restrict__ cells,
                                                     uint32_t *__restrict__ cellbuf,
-                                                    int *__restrict__ cellcnt) {
+                                                    int *__restrict__ cellcnt, int cell_begin, int cell_end) {
     extern __shared__ uint8_t s_dyn[];
-    const int S = plan->fast_S;
+    constexpr int slice = (2 * S * S + 2 * (S - 6) * (S - 6) + 15) / 16 * 16;  // 16-B aligned slices
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c = blockIdx.x * 4 + wave, f = blockIdx.y;
-    if (c >= plan->ncells) return;
-    const int slice = 2 * S * S + 2 * (S - 6) * (S - 6);
-    uint8_t *img = s_dyn + (size_t)wave * slice;
+    const int c = cell_begin + blockIdx.x * 4 + wave, f = blockIdx.y;
+    if (c >= cell_end) return;
+    uint8_t *img = s_dyn + wave * slice;
     uint8_t *sc = img + S * S;
     uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * S);
     const CellDesc cd = cells[c];
     const LevelDesc &L = plan->lv[cd.level];
     const uint8_t *src = pyr + (size_t)f * pitch + L.off + (size_t)cd.y0 * L.w + cd.x0;
     const int rw = cd.rw, rh = cd.rh;
-    // ROI -> LDS: lane = column; 8 rows of loads in flight before their stores
-    for (int r0 = 0; r0 < rh; r0 += 8) {
-        uint8_t v0[8], v1[8];
+    // ROI -> LDS in ONE batch of global loads: lane = (row offset, dword) with
+    // S/4 dwords per row; each lane reads the two aligned dwords around its 4
+    // bytes and realigns them with v_alignbyte, then writes one ds_write_b32.
+    {
+        constexpr int DW = S / 4, RPI = 64 / DW, NI = (S + RPI - 1) / RPI;
+        const int rlane = lane / DW, dw = lane - rlane * DW;
+        const int ndw = (rw + 3) / 4;
+        constexpr int NB = NI < 8 ? NI : 8;  // loads in flight per batch (one batch for S <= 48)
+        for (int k0 = 0; k0 < NI; k0 += NB) {
+            uint32_t lo[NB], hi[NB];
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint8_t *row = src + (size_t)min(r0 + k, rh - 1) * L.w;
-            v0[k] = lane < rw ? row[lane] : 0;
-            v1[k] = lane + 64 < rw ? row[lane + 64] : 0;
-        }
+            for (int j = 0; j < NB; j++) {
+                const int r = (k0 + j) * RPI + rlane;
+                lo[j] = hi[j] = 0u;
+                if (rlane < RPI && r < rh && dw < ndw) {
+                    const uintptr_t a = (uintptr_t)(src + (size_t)r * L.w) + 4 * dw;
+                    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+                    lo[j] = q[0];
+                    hi[j] = q[1];
+                }
+            }
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int r = r0 + k;
-            if (r < rh) {
-                if (lane < rw) img[r * S + lane] = v0[k];
-                if (lane + 64 < rw) img[r * S + lane + 64] = v1[k];
+            for (int j = 0; j < NB; j++) {
+                const int r = (k0 + j) * RPI + rlane;
+                if (rlane < RPI && r < rh && dw < ndw) {
+                    const uint32_t sh = (uint32_t)(((uintptr_t)(src + (size_t)r * L.w)) & 3u);
+                    reinterpret_cast<uint32_t *>(img + r * S)[dw] = __builtin_amdgcn_alignbyte(hi[j], lo[j], sh);
+                }
             }
         }
     }
-    int ro[16];
-    ring_offsets(S, ro);
-    const int iw = rw - 6, ih = rh - 6, n = iw > 0 && ih > 0 ? iw * ih : 0;
-    const float inv_iw = iw > 0 ? 1.0f / (float)iw : 0.f;
+    const int iw = rw - 6, ih = rh - 6;
+    // lane -> pixel: 32 lanes per row (two rows per chunk) when the interior is
+    // at most 32 wide, else 64 lanes per row (and column chunks past 64)
+    const bool half = iw <= 32;
+    const int xl = half ? (lane & 31) : lane, yl = half ? (lane >> 5) : 0, ystep = half ? 2 : 1;
     uint32_t *out = cellbuf + ((size_t)f * plan->ncells + c) * plan->cell_cap;
     int total = 0;
     for (int pass = 0; pass < 2; pass++) {
         const int th = pass == 0 ? plan->ini_th : plan->min_th;
-        for (int i = lane; i < rh * (S / 4); i += 64) reinterpret_cast<uint32_t *>(sc)[i] = 0u;
-        // A: 4-point test over all interior pixels (pixel i -> row i / iw, exact in float)
+        {
+            uint4 *z = reinterpret_cast<uint4 *>(sc);
+            const uint4 zero = {0u, 0u, 0u, 0u};
+            for (int i = lane; i < (rh * S) / 16; i += 64) z[i] = zero;
+            for (int i = ((rh * S) / 16) * 16 + lane; i < rh * S; i += 64) sc[i] = 0;
+        }
+        // A
         int na = 0;
-        for (int i0 = 0; i0 < n; i0 += 64) {
-            const int i = i0 + lane;
-            const int y = (int)(((float)i + 0.5f) * inv_iw);
-            const int x = i - y * iw;
-            bool cand = false;
-            if (i < n) {
-                const uint8_t *p = img + (y + 3) * S + (x + 3);
-                const int v = p[0], d0 = p[ro[0]], d4 = p[ro[4]], d8 = p[ro[8]], d12 = p[ro[12]];
-                const int hi = v + th, lo = v - th;
-                const bool b0 = d0 > hi, b4 = d4 > hi, b8 = d8 > hi, b12 = d12 > hi;
-                const bool k0 = d0 < lo, k4 = d4 < lo, k8 = d8 < lo, k12 = d12 < lo;
-                cand = ((b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0)) |
-                       ((k0 & k4) | (k4 & k8) | (k8 & k12) | (k12 & k0));
+        if (iw > 0 && ih > 0) {
+            for (int cx0 = 0; cx0 < iw; cx0 += 64) {
+                const int x = cx0 + xl;
+                const bool colok = x < iw;
+                const uint8_t *q = img + yl * S + x;  // q = centre - 3S - 3 of pixel (x+3, yl+3)
+                for (int y0 = 0; y0 < ih; y0 += ystep) {
+                    const uint8_t *qq = q + y0 * S;
+                    const int v = qq[Ring<S>::kCentre];
+                    const int d0 = qq[Ring<S>::off(0)], d4 = qq[Ring<S>::off(4)];
+                    const int d8 = qq[Ring<S>::off(8)], d12 = qq[Ring<S>::off(12)];
+                    const int hi = v + th, lo = v - th;
+                    const uint64_t in = __ballot(colok && y0 + yl < ih);
+                    const uint64_t b0 = __ballot(d0 > hi), b4 = __ballot(d4 > hi);
+                    const uint64_t b8 = __ballot(d8 > hi), b12 = __ballot(d12 > hi);
+                    const uint64_t k0 = __ballot(d0 < lo), k4 = __ballot(d4 < lo);
+                    const uint64_t k8 = __ballot(d8 < lo), k12 = __ballot(d12 < lo);
+                    const uint64_t m = in & (((b0 | b8) & (b4 | b12)) | ((k0 | k8) & (k4 | k12)));
+                    if ((m >> lane) & 1)
+                        list[na + popc_below(m)] = (uint16_t)((x + 3) | ((y0 + yl + 3) << 8));
+                    na += __popcll(m);
+                }
             }
-            const uint64_t m = __ballot(cand);
-            if (cand) list[na + popc_below(m)] = (uint16_t)((x + 3) | ((y + 3) << 8));
-            na += __popcll(m);
         }
         // B: full segment test, compacted in place (writes never pass the read front)
         int nc = 0;
         for (int i0 = 0; i0 < na; i0 += 64) {
             const int i = i0 + lane;
-            const uint16_t e = i < na ? list[i] : (uint16_t)0;
-            const bool corner = i < na && fast9_is_corner(img + (e >> 8) * S + (e & 0xFF), ro, th);
+            const uint16_t e = i < na ? list[i] : (uint16_t)0x0303;
+            const bool corner = i < na && fast9_is_corner<S>(img + ((e >> 8) - 3) * S + ((e & 0xFF) - 3), th);
             const uint64_t m = __ballot(corner);
             if (corner) list[nc + popc_below(m)] = e;
             nc += __popcll(m);
@@ -355,7 +387,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t *__restrict__ 
         for (int i = lane; i < nc; i += 64) {
             const uint16_t e = list[i];
             const int off = (e >> 8) * S + (e & 0xFF);
-            sc[off] = (uint8_t)fast9_corner_score(img + off, ro, th);
+            sc[off] = (uint8_t)fast9_corner_score<S>(img + off - Ring<S>::kCentre, th);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -369,10 +401,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t *__restrict__ 
                 const uint16_t e = list[i];
                 x = e & 0xFF;
                 y = e >> 8;
-                const uint8_t *r = sc + y * S + x;
-                s = r[0];
-                keep = s > r[-1] && s > r[1] && s > r[-S - 1] && s > r[-S] && s > r[-S + 1] && s > r[S - 1] &&
-                       s > r[S] && s > r[S + 1];
+                const uint8_t *r = sc + (y - 1) * S + (x - 1);
+                s = r[S + 1];
+                keep = s > r[0] && s > r[1] && s > r[2] && s > r[S] && s > r[S + 2] && s > r[2 * S] &&
+                       s > r[2 * S + 1] && s > r[2 * S + 2];
             }
             const uint64_t m = __ballot(keep);
             const int pos = total + popc_below(m);
@@ -384,9 +416,14 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t *__restrict__ 
     if (lane == 0) cellcnt[(size_t)f * plan->ncells + c] = min(total, plan->cell_cap);
 }
 
-size_t fast_cells_lds_bytes(const Plan &hp) {
-    const int S = hp.fast_S;
-    return 4 * (size_t)(2 * S * S + 2 * (S - 6) * (S - 6));
+// per-level ROI stride: the level's largest cell ROI rounded up to 8 (>= 40)
+static int fast_stride(int roi) {
+    const int S = ((roi + 7) / 8) * 8;
+    return S < 40 ? 40 : S;
+}
+
+static size_t fast_cells_lds_bytes(int S) {
+    return 4 * (size_t)((2 * S * S + 2 * (S - 6) * (S - 6) + 15) / 16 * 16);
 }
 
 // ---------------------------------------------------------------------------
@@ -1002,9 +1039,25 @@ hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const 
 hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const CellDesc *dcells,
                        uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st) {
     if (hp.ncells == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fast_cells, dim3((hp.ncells + 3) / 4, nframes), dim3(256), fast_cells_lds_bytes(hp), st,
-                       pyr, pitch, dp, dcells,
-                       cellbuf, cellcnt);
+    // one launch per level, each with its own compile-time ROI stride (LDS per
+    // wave ~ 2 S^2: the small-cell levels keep 7 workgroups per CU)
+    for (int l = 0; l < hp.nlevels; l++) {
+        const LevelDesc &L = hp.lv[l];
+        if (L.ncells == 0) continue;
+        const dim3 grid((L.ncells + 3) / 4, nframes);
+        const int S = fast_stride(L.fast_roi);
+        const size_t lds = fast_cells_lds_bytes(S);
+        const int cb = L.cell_begin, ce = L.cell_begin + L.ncells;
+#define YGZ_FAST(SS) hipLaunchKernelGGL(k_fast_cells<SS>, grid, dim3(256), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce)
+        switch (S) {
+        case 40: YGZ_FAST(40); break;
+        case 48: YGZ_FAST(48); break;
+        case 56: YGZ_FAST(56); break;
+        case 64: YGZ_FAST(64); break;
+        default: YGZ_FAST(72); break;
+        }
+#undef YGZ_FAST
+    }
     return hipGetLastError();
 }
 
