@@ -1,0 +1,96 @@
+// tracking_demo.cpp — a Tracking.cc-shaped caller of the drop-in adapters
+// (compat/ygz_compat.hpp).  It mirrors the reference's per-frame sequence:
+//   extractor construction            Tracking.cc:255-261
+//   Frame: ComputePyramid + ExtractORB Frame.cc:332-348, 807-813
+//   matching inner loop               ORBmatcher.cc:1218-1350 (dense best/second)
+//   TrackWithSparseAlignment          Tracking.cc:2145-2189 (SparseImgAlign(3,1).run)
+// on a synthetic pair: frame 1 is frame 0 translated by (dx, dy) pixels, map
+// points on a fronto-parallel plane at depth Z, so the true TCR translation is
+// (-dx*Z/fx, -dy*Z/fy, 0).  Prints one line per check; exit 0 on success.
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "ygz_compat.hpp"
+
+static std::vector<uint8_t> synth(int W, int H, unsigned seed, int dx, int dy) {
+    std::vector<uint8_t> img((size_t)W * H, 128);
+    unsigned s = seed;
+    auto rnd = [&](int n) { s = s * 1664525u + 1013904223u; return (int)((s >> 8) % (unsigned)n); };
+    for (int r = 0; r < 900; r++) {
+        const int x0 = rnd(W + 40) - 20, y0 = rnd(H + 40) - 20, w = 4 + rnd(40), h = 4 + rnd(40), v = rnd(256);
+        for (int y = y0; y < y0 + h; y++)
+            for (int x = x0; x < x0 + w; x++) {
+                const int xx = x + dx, yy = y + dy;
+                if (xx >= 0 && yy >= 0 && xx < W && yy < H) img[(size_t)yy * W + xx] = (uint8_t)v;
+            }
+    }
+    return img;
+}
+
+int main() {
+    const int W = 752, H = 480;
+    const ygzfe_camera cam{458.654f, 457.296f, 367.215f, 248.375f};  // EuRoC.yaml:8-11
+    const float Z = 3.0f;
+    int fails = 0;
+    try {
+        ygz::ORBextractor extractor(1000, 2.0f, 4, 20, 7);  // EuRoC.yaml:32-45
+        std::printf("levels %d scale %.1f features/level", extractor.GetLevels(), extractor.GetScaleFactor());
+        for (int v : extractor.GetFeaturesPerLevel()) std::printf(" %d", v);
+        std::printf("\n");
+
+        const auto img0 = synth(W, H, 7u, 0, 0), img1 = synth(W, H, 7u, 2, -1);
+        ygz::FramePyramid f0, f1;
+        std::vector<ygz::KeyPoint> k0, k1;
+        std::vector<uint8_t> d0, d1;
+        extractor.ComputePyramid(f0, img0.data(), W, H, W);
+        extractor(f0, k0, d0, ygz::ORBSLAM_KEYPOINT);
+        extractor.ComputePyramid(f1, img1.data(), W, H, W);
+        extractor(f1, k1, d1, ygz::ORBSLAM_KEYPOINT);
+        std::printf("keypoints %zu %zu\n", k0.size(), k1.size());
+        if (k0.size() < 300 || k1.size() < 300) fails++;
+
+        ygz::ORBmatcher matcher(0.9f, true);
+        std::vector<int> bi, bd, sd;
+        matcher.SearchBest2(d1.data(), (int)k1.size(), d0.data(), (int)k0.size(), bi, bd, sd);
+        int good = 0;
+        for (size_t i = 0; i < k1.size(); i++)
+            if (bd[i] <= ygz::ORBmatcher::TH_LOW && bd[i] < matcher.mfNNratio * sd[i]) good++;
+        std::printf("matches(TH_LOW, ratio) %d; DescriptorDistance(d1[0], d0[bi0]) %d == %d\n", good,
+                    ygz::ORBmatcher::DescriptorDistance(&d1[0], &d0[(size_t)bi[0] * 32]), bd[0]);
+        if (good < 100 || ygz::ORBmatcher::DescriptorDistance(&d1[0], &d0[(size_t)bi[0] * 32]) != bd[0]) fails++;
+
+        std::vector<float> xyz(3 * k0.size());
+        std::vector<uint8_t> usable(k0.size(), 1);
+        for (size_t i = 0; i < k0.size(); i++) {
+            xyz[3 * i + 0] = (k0[i].pt.x - cam.cx) / cam.fx * Z;
+            xyz[3 * i + 1] = (k0[i].pt.y - cam.cy) / cam.fy * Z;
+            xyz[3 * i + 2] = Z;
+        }
+        ygz::SparseImgAlign align(3, 1);
+        ygz::SE3 TCR;
+        const size_t nvis = align.run(f0, f1, cam, k0, xyz.data(), usable.data(), TCR);
+        const float tx = 2.0f * Z / cam.fx, ty = -1.0f * Z / cam.fy;
+        std::printf("align visible %zu t (%.4f %.4f %.4f) expected (%.4f %.4f 0)\n", nvis, TCR.t[0], TCR.t[1],
+                    TCR.t[2], tx, ty);
+        if (nvis < 100 || std::fabs(TCR.t[0] - tx) > 2e-3f || std::fabs(TCR.t[1] - ty) > 2e-3f) fails++;
+
+        // Align2D on level 0: a patch of frame 1 around a shifted keypoint position
+        const auto lv = f1.level(0);
+        const int u = 300, v = 200;
+        uint8_t pb[100], p[64];
+        for (int y = 0; y < 10; y++)
+            for (int x = 0; x < 10; x++) pb[y * 10 + x] = lv[(size_t)(v - 5 + y) * W + (u - 5 + x)];
+        for (int y = 0; y < 8; y++)
+            for (int x = 0; x < 8; x++) p[y * 8 + x] = pb[(y + 1) * 10 + (x + 1)];
+        float px[2] = {u + 0.7f, v - 0.5f};
+        const bool conv = ygz::Align2D(f1, 0, pb, p, 10, px);
+        std::printf("Align2D converged %d px (%.3f %.3f) expected (%d %d)\n", (int)conv, px[0], px[1], u, v);
+        if (!conv || std::fabs(px[0] - u) > 0.1f || std::fabs(px[1] - v) > 0.1f) fails++;
+    } catch (const std::exception &e) {
+        std::printf("error: %s\n", e.what());
+        return 2;
+    }
+    std::printf(fails ? "FAILED %d\n" : "OK\n", fails);
+    return fails ? 1 : 0;
+}

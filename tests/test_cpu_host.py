@@ -101,3 +101,14 @@ def test_kp_layout_matches_cv_keypoint(ygzfe):
     assert ygzfe.KP_DTYPE.itemsize == 28
     assert list(ygzfe.KP_DTYPE.names) == ["x", "y", "size", "angle", "response", "octave", "class_id"]
     assert C.sizeof(ygzfe.SE3) == 28
+
+
+def test_compat_adapter_builds_and_fails_loudly_without_gpu(ygzfe):
+    """compat/ygz_compat.hpp (the drop-in C++ classes) compiles into a Tracking.cc-shaped
+    caller; with no HIP device the product path reports an error instead of falling back."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "compat")])
+    exe = os.path.join(ROOT, "compat", "build", "tracking_demo")
+    if ygzfe.device_count() > 0:
+        pytest.skip("a GPU is visible: tests/test_gpu_compat.py runs the demo")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "no HIP device" in r.stdout
