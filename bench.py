@@ -152,32 +152,43 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     fps = world * B / (elapsed / args.steps)
 
-    # ------------------------------------------------ roofline (dominant kernel)
+    # ------------------------------------------------ roofline (dominant stage)
     counts = counts_t.cpu().numpy()
     nvis = out[:, 7].contiguous().view(torch.int32).cpu().numpy()
-    lw = [(W >> l, H >> l) for l in range(nl)]
-    areas = [w * h for w, h in lw]
+    plan = ygzfe.orb_plan(nf, sf, nl, ini, mn, W, H)
+    areas = [w * h for w, h in plan["sizes"]]
+    cand, selk = batch.stats(B)  # per-level totals over the B frames of the last extract
     N = float(counts.mean())
     nv = float(nvis.mean())
-    # algorithmic bytes per launch, B frames per launch
+    ncells_tot = int(sum(plan["ncells"]))
+    # algorithmic bytes per launch (per step, B frames): each intermediate crosses
+    # HBM once written and once read
     alg = {
         "pyramid": B * sum(areas[l - 1] + areas[l] for l in range(1, nl)),
         "blur7": B * 2 * sum(areas),
-        "fast9_cells": B * (sum(areas[:3]) + 4 * 5000),
-        "octree": B * (4 * 2 * 5000 + 4 * N),
-        "orient_rbrief": B * N * (961 + 2 * 256 + 60),
-        "hamming_best2": P * (32 * 2 * N + 12 * N),
-        "sparse_align": P * (3 * nv * (36 + 10 * 25) + 12 * nv + 96),
+        "fast9_cells": B * sum(a for a, c in zip(areas, plan["ncells"]) if c > 0) + 4 * int(cand.sum())
+        + 4 * B * ncells_tot,
+        "octree": 4 * int(cand.sum()) + 4 * B * ncells_tot + 4 * int(selk.sum()),
+        "orient_rbrief": int(counts.sum()) * (961 + 512 + 4 + 60),
+        "hamming_best2": int(sum(32 * (counts[i + 1] + counts[i]) + 12 * counts[i + 1] for i in range(P))),
+        "sparse_align": int(P * (3 * nv * (36 + 10 * 25) + 12 * nv + 96)),
     }
     dom = max((k for k in stage_ms if stage_ms[k] > 0), key=lambda k: stage_ms[k])
     dom_ms = stage_ms[dom]
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "r01_traffic.json")
+    if os.path.exists(tpath):  # PMC FETCH_SIZE x2 + WRITE_SIZE of the same command (tools/run_pmc.sh)
+        tj = json.load(open(tpath)).get("per_step", {})
+        if dom in tj:
+            traffic = tj[dom]["traffic_bytes"]
     roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None, "avg_launch_ms": round(dom_ms, 4),
+            "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic, "avg_launch_ms": round(dom_ms, 4),
             "alg_bytes_per_launch": int(alg[dom]),
-            "stages_ms": {k: round(v, 4) for k, v in stage_ms.items()}}
+            "stages_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+            "stages_gbps": {k: round(alg[k] / (stage_ms[k] * 1e-3) / 1e9, 1) for k in alg if stage_ms.get(k, 0) > 0}}
     # whole pipeline, SURVEY §8d model: (B_extract + B_align) per frame x fps
-    b_extract = W * H + 2 * sum(areas[1:]) + 2 * sum(areas) + 60 * N
+    b_extract = areas[0] + 2 * sum(areas[1:]) + 2 * sum(areas) + 60 * N
     b_align = 3 * nv * (36 + 10 * 25) + 12 * nv + 96
     pipeline_gbps = (b_extract + b_align) * (fps / world) / 1e9
 
@@ -204,6 +215,7 @@ def main():
                        "frames_per_gpu": B, "image": f"{W}x{H}", "nfeatures": nf, "scale_factor": sf,
                        "nlevels": nl, "fast_th": [ini, mn], "align_pairs_per_gpu": P,
                        "mean_keypoints": round(N, 1), "mean_align_visible": round(nv, 1),
+                       "mean_fast_candidates": round(float(cand.sum()) / B, 1),
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": roof,
             "pipeline_gbps_model": round(pipeline_gbps, 2),

@@ -75,9 +75,15 @@ int main() {
                     TCR.t[2], tx, ty);
         if (nvis < 100 || std::fabs(TCR.t[0] - tx) > 2e-3f || std::fabs(TCR.t[1] - ty) > 2e-3f) fails++;
 
-        // Align2D on level 0: a patch of frame 1 around a shifted keypoint position
+        // Align2D on level 0: the patch around frame 1's strongest level-0 corner,
+        // started 0.7 / -0.5 px off
         const auto lv = f1.level(0);
-        const int u = 300, v = 200;
+        size_t best = 0;
+        for (size_t i = 0; i < k1.size(); i++)
+            if (k1[i].octave == 0 && k1[i].pt.x > 40 && k1[i].pt.y > 40 && k1[i].pt.x < W - 40 &&
+                k1[i].pt.y < H - 40 && (k1[best].octave != 0 || k1[i].response > k1[best].response))
+                best = i;
+        const int u = (int)std::lround(k1[best].pt.x), v = (int)std::lround(k1[best].pt.y);
         uint8_t pb[100], p[64];
         for (int y = 0; y < 10; y++)
             for (int x = 0; x < 10; x++) pb[y * 10 + x] = lv[(size_t)(v - 5 + y) * W + (u - 5 + x)];

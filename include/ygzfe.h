@@ -163,6 +163,11 @@ int ygzfe_batch_level(ygzfe_batch *b, int frame, int level, const uint8_t **d_le
  * level (mvImagePyramid, blurred == 0) or its GaussianBlur(7x7, sigma 2) copy
  * that computeDescriptors reads (ORBextractor.cc:1079-1084, blurred != 0). */
 int ygzfe_batch_read_level(ygzfe_batch *b, int frame, int level, int blurred, uint8_t *dst, int dst_stride);
+/* Synchronise and report per-level work of the last ygzfe_batch_extract over
+ * frames [0, n_frames): FAST candidates kept by the cell NMS (the octree input,
+ * vToDistributeKeys) and keypoints kept by the octree, each [nlevels] summed
+ * over the frames.  For roofline accounting (bytes per launch). */
+int ygzfe_batch_stats(ygzfe_batch *b, int n_frames, int64_t *candidates, int64_t *selected);
 /* Kernel timing (hipEvents around each stage launch on the batch stream).
  * enable != 0 turns it on; ms[] receives per-stage milliseconds of the last
  * ygzfe_batch_extract; names[] the stage names. Returns stage count. */

@@ -177,6 +177,9 @@ struct ygzfe_batch {
     int device = 0;
     int maxF = 0;
     hipStream_t stream = nullptr;
+    // fork/join inside one extract: the FAST levels >= 1 overlap level 0
+    hipStream_t aux[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
     std::unique_ptr<PlanDev> plan;
     DevBuf pyr;
     Workspace ws;
@@ -534,6 +537,11 @@ int ygzfe_batch_create(const ygzfe_orb_params *p, int device, int width, int hei
     YGZ_TRY(b->pyr.ensure((size_t)max_frames * P.pyr_bytes));
     YGZ_TRY(b->ws.ensure(P, max_frames, P.kp_cap));
     YGZ_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    for (int i = 0; i < 3; i++) {
+        YGZ_HIP(hipStreamCreateWithFlags(&b->aux[i], hipStreamNonBlocking));
+        YGZ_HIP(hipEventCreateWithFlags(&b->ev_join[i], hipEventDisableTiming));
+    }
+    YGZ_HIP(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
     *out = b.release();
     return YGZFE_OK;
 }
@@ -545,6 +553,11 @@ void ygzfe_batch_destroy(ygzfe_batch *b) {
     (void)b->collect();
     for (auto &e : b->pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(b->stream);
+    for (int i = 0; i < 3; i++) {
+        if (b->aux[i]) (void)hipStreamSynchronize(b->aux[i]), (void)hipStreamDestroy(b->aux[i]);
+        if (b->ev_join[i]) (void)hipEventDestroy(b->ev_join[i]);
+    }
+    if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
     delete b;
 }
 
@@ -603,9 +616,18 @@ int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream) {
     t0 = b->begin(st);
     YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), n_frames, st));
     b->end(ST_BLUR, t0, st);
+    // fork: FAST level 0 on st, levels >= 1 on aux[1], aux[2] (their small grids
+    // fill the tail of the level-0 launch instead of running after it)
+    YGZ_HIP(hipEventRecord(b->ev_fork, st));
+    for (int i = 1; i < 3; i++) YGZ_HIP(hipStreamWaitEvent(b->aux[i], b->ev_fork, 0));
     t0 = b->begin(st);
+    const hipStream_t lvl_st[2] = {b->aux[1], b->aux[2]};
     YGZ_HIP(launch_fast(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(), ws.cellbuf.as<uint32_t>(),
-                        ws.cellcnt.as<int>(), n_frames, st));
+                        ws.cellcnt.as<int>(), n_frames, st, lvl_st, 2));
+    YGZ_HIP(hipEventRecord(b->ev_join[1], b->aux[1]));
+    YGZ_HIP(hipEventRecord(b->ev_join[2], b->aux[2]));
+    YGZ_HIP(hipStreamWaitEvent(st, b->ev_join[1], 0));
+    YGZ_HIP(hipStreamWaitEvent(st, b->ev_join[2], 0));
     b->end(ST_FAST, t0, st);
     t0 = b->begin(st);
     YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
@@ -677,9 +699,32 @@ int ygzfe_batch_read_level(ygzfe_batch *b, int frame, int level, int blurred, ui
     const DevBuf &src = blurred ? b->ws.blur : b->pyr;
     if (!src.p) { set_error("no %s buffer yet (run ygzfe_batch_extract first)", blurred ? "blurred" : "pyramid"); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(b->device));
-    YGZ_HIP(hipStreamSynchronize(b->stream));
+    YGZ_HIP(hipDeviceSynchronize());  // extract may have run on a caller stream + side streams
     YGZ_HIP(hipMemcpy2D(dst, dst_stride, (const uint8_t *)src.p + (size_t)frame * P.pyr_bytes + L.off, L.w, L.w, L.h,
                         hipMemcpyDeviceToHost));
+    return YGZFE_OK;
+}
+
+int ygzfe_batch_stats(ygzfe_batch *b, int n_frames, int64_t *candidates, int64_t *selected) {
+    if (!b || n_frames < 0 || n_frames > b->maxF) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    const Plan &P = b->plan->hp();
+    YGZ_TRY(ensure_device(b->device));
+    YGZ_HIP(hipDeviceSynchronize());  // extract may have run on a caller stream + side streams
+    for (int l = 0; l < P.nlevels; l++) {
+        if (candidates) candidates[l] = 0;
+        if (selected) selected[l] = 0;
+    }
+    if (n_frames == 0 || !b->ws.cellcnt.p) return YGZFE_OK;
+    std::vector<int> cc((size_t)n_frames * P.ncells), sc((size_t)n_frames * P.nlevels);
+    if (P.ncells) YGZ_HIP(hipMemcpy(cc.data(), b->ws.cellcnt.p, cc.size() * 4, hipMemcpyDeviceToHost));
+    YGZ_HIP(hipMemcpy(sc.data(), b->ws.selcnt.p, sc.size() * 4, hipMemcpyDeviceToHost));
+    for (int f = 0; f < n_frames; f++)
+        for (int l = 0; l < P.nlevels; l++) {
+            const LevelDesc &L = P.lv[l];
+            if (candidates)
+                for (int c = 0; c < L.ncells; c++) candidates[l] += cc[(size_t)f * P.ncells + L.cell_begin + c];
+            if (selected) selected[l] += sc[(size_t)f * P.nlevels + l];
+        }
     return YGZFE_OK;
 }
 

@@ -72,6 +72,22 @@ struct Plan {
 // --------------------------------------------------------------------------
 // device helpers
 
+// XCD-aware block order (cdna_hip_programming.md T1, bijective form): blocks
+// dealt to one XCD (orig % 8) get one contiguous range of logical ids, so a
+// frame's blocks share an L2.  A speed choice only; results never depend on it.
+__device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, x = orig & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3);
+}
+
+// logical (x, y) block coordinates of a 2D grid after the swizzle
+__device__ __forceinline__ void swizzled_block_2d(int &bx, int &by) {
+    const int orig = blockIdx.x + gridDim.x * blockIdx.y;
+    const int id = xcd_swizzle(orig, gridDim.x * gridDim.y);
+    bx = id % gridDim.x;
+    by = id / gridDim.x;
+}
+
 __device__ __forceinline__ int lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }

@@ -903,9 +903,10 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
                                                      const int *__restrict__ n_existing,
                                                      ygzfe_kp *__restrict__ kps, uint8_t *__restrict__ desc,
                                                      int *__restrict__ counts, int row_cap) {
-    const int f = blockIdx.y;
+    int bx, f;
+    swizzled_block_2d(bx, f);  // one frame's keypoints on one XCD: patch lines shared in its L2
     const int lane = threadIdx.x & 63, s = lane & 15;
-    const int idx = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int idx = bx * 16 + (threadIdx.x >> 4);
     const int nl = plan->nlevels;
     const int *sc = selcnt + (size_t)f * nl;
     const int ne = n_existing ? n_existing[f] : 0;
@@ -916,7 +917,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
         if (lane >= o) incl += v;
     }
     const int tot = __builtin_amdgcn_readlane(incl, nl - 1);
-    if (blockIdx.x == 0 && threadIdx.x == 0) counts[f] = ne + tot;
+    if (bx == 0 && threadIdx.x == 0) counts[f] = ne + tot;
     int l = 0, pre = 0;
     for (int q = 0; q < nl; q++) {
         const int iq = __builtin_amdgcn_readlane(incl, q);
@@ -1037,7 +1038,8 @@ hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const 
 }
 
 hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const CellDesc *dcells,
-                       uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st) {
+                       uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st0, const hipStream_t *lvl_streams,
+                       int n_lvl_streams) {
     if (hp.ncells == 0) return hipSuccess;
     // one launch per level, each with its own compile-time ROI stride (LDS per
     // wave ~ 2 S^2: the small-cell levels keep 7 workgroups per CU)
@@ -1048,6 +1050,9 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
         const int S = fast_stride(L.fast_roi);
         const size_t lds = fast_cells_lds_bytes(S);
         const int cb = L.cell_begin, ce = L.cell_begin + L.ncells;
+        // level 0 on the caller's stream, the others spread over the given side streams
+        const hipStream_t st = (l == 0 || !lvl_streams || n_lvl_streams <= 0) ? st0
+                                                                                : lvl_streams[(l - 1) % n_lvl_streams];
 #define YGZ_FAST(SS) hipLaunchKernelGGL(k_fast_cells<SS>, grid, dim3(256), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce)
         switch (S) {
         case 40: YGZ_FAST(40); break;

@@ -11,7 +11,8 @@ hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Pl
 hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
                        int nframes, hipStream_t st);
 hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const CellDesc *dcells,
-                       uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st);
+                       uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st,
+                       const hipStream_t *lvl_streams = nullptr, int n_lvl_streams = 0);
 hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
                          uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int nframes,
                          hipStream_t st);

@@ -357,6 +357,13 @@ class Batch:
         _check(lib().ygzfe_batch_level(self.h, 0, level, None, C.byref(w), C.byref(h), C.byref(st)), "batch_level")
         return w.value, h.value
 
+    def stats(self, n_frames):
+        """Per-level totals over frames [0, n) of the last extract: (FAST candidates, octree keypoints)."""
+        cand = np.zeros(self.nlevels, np.int64)
+        sel = np.zeros(self.nlevels, np.int64)
+        _check(lib().ygzfe_batch_stats(self.h, n_frames, _p(cand), _p(sel)), "batch_stats")
+        return cand, sel
+
     def read_level(self, i, level, blurred=False):
         """Host copy of pyramid level `level` of frame i (or its 7x7 blurred copy)."""
         w, h = self.level_size(level)

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Per-stage HBM traffic per bench step from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+passes (tools/run_pmc.sh), corrected as MI355X_MICROARCH.md §HBM prescribes:
+FETCH_SIZE (KiB) x 1024 x 2 (gfx950 tallies 128-B read requests at 64 B),
+WRITE_SIZE (KiB) x 1024.  Writes JSON {stage: {fetch_bytes, write_bytes, traffic_bytes}}
+per step (= per stage launch set) for bench.py's roofline.traffic.
+
+    python3 tools/pmc_traffic.py <pmc_dir> <steps_per_pass> > profiles/r01_traffic.json
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+STAGES = [("pyramid", r"k_resize_"), ("blur7", r"k_blur7"), ("fast9_cells", r"k_fast_cells"),
+          ("octree", r"k_octree"), ("orient_rbrief", r"k_orient_desc"), ("hamming_best2", r"k_hamming_best2"),
+          ("sparse_align", r"k_sparse_align|k_build_align_jobs")]
+
+
+def stage_of(kernel):
+    for name, pat in STAGES:
+        if re.search(pat, kernel):
+            return name
+    return None
+
+
+def main(pmc_dir, steps):
+    tot = collections.defaultdict(lambda: collections.defaultdict(float))
+    for path in glob.glob(os.path.join(pmc_dir, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(path)):
+            st = stage_of(r["Kernel_Name"])
+            if st and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
+                tot[st][r["Counter_Name"]] += float(r["Counter_Value"])
+    out = {}
+    for st, c in tot.items():
+        fetch = c["FETCH_SIZE"] * 1024 * 2 / steps
+        write = c["WRITE_SIZE"] * 1024 / steps
+        out[st] = {"fetch_bytes": int(fetch), "write_bytes": int(write), "traffic_bytes": int(fetch + write)}
+    json.dump({"source": pmc_dir, "steps_per_pass": steps,
+               "correction": "FETCH_SIZE x2 (gfx950), KiB -> B", "per_step": out}, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]))
