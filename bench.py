@@ -113,10 +113,15 @@ def main():
     fx, fy, cx, cy = cam
     camera = ygzfe.Camera(*cam)
 
+    side = torch.cuda.Stream(dev)  # Hamming (descriptors only) runs beside SparseImgAlign (pyramids + kps)
+
     def step():
         batch.extract(B, sptr)
-        batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(), sptr)
+        side.wait_stream(stream)
+        batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(),
+                    side.cuda_stream)
         if args.no_align:
+            stream.wait_stream(side)
             return
         k = kps_t[:P]
         dx = (k[:, :, 0] - cx) / fx
@@ -127,6 +132,7 @@ def main():
         xyz[:, :, 2] = lam
         batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(), camera, 3, 1,
                            T_init.data_ptr(), out.data_ptr(), sptr)
+        stream.wait_stream(side)  # the step ends when both branches have
 
     for _ in range(args.warmup):
         step()
