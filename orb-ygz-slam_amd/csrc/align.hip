@@ -258,9 +258,8 @@ __device__ __forceinline__ float wmul(double a, double b) { return (float)(a * b
 // Frame pyramids carry >= 64 bytes of tail padding for the over-read.
 template <int N>
 __device__ __forceinline__ void load_row(const uint8_t *p, float (&out)[N]) {
-    const uintptr_t a = (uintptr_t)p & ~(uintptr_t)3;
     const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(a);
+    const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(p - sh));
     constexpr int ND = (N + 3 + 3) / 4;  // dwords covering [p, p+N) for any sh <= 3
     uint32_t d[ND + 1];
 #pragma unroll

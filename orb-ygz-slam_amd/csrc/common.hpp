@@ -72,6 +72,44 @@ struct Plan {
 // --------------------------------------------------------------------------
 // device helpers
 
+// Global-memory view of a pointer whose address space the compiler cannot
+// infer (struct members, integer arithmetic): loads through it are global_load_*
+// instead of flat_load_*, which also count against lgkmcnt and so serialise
+// with LDS traffic.
+template <class T>
+using gptr_t = const __attribute__((address_space(1))) T *;
+template <class T>
+__device__ __forceinline__ gptr_t<T> as_global(const T *p) {
+    return (gptr_t<T>)p;
+}
+
+// Diagnostic build only (make diag -> lib/libygzfe_diag.so): per-workgroup
+// s_memrealtime (100 MHz, chip-synchronous) at kernel entry / exit, plus the
+// XCC id, for dispatch / duration histograms (tools/diag_blocks.py).
+#ifdef YGZ_STAMPS
+#ifndef YGZ_STAMP_KERNEL
+#define YGZ_STAMP_KERNEL 1  // 1 = k_orient_desc, 2 = k_fast_cells (level 0)
+#endif
+extern __device__ unsigned long long g_bstamps[1 << 20];
+#define YGZ_BSTAMP_K(kern, slot)                                                                 \
+    do {                                                                                          \
+        if ((kern) != YGZ_STAMP_KERNEL) break;                                                    \
+        const unsigned _b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);        \
+        if (threadIdx.x == 0 && _b < (1u << 17))                                                   \
+            g_bstamps[8 * _b + (slot)] = (slot) == 2 ? (unsigned long long)__builtin_amdgcn_s_getreg(   \
+                                                           (20 << 0) | (0 << 6) | (3 << 11))      \
+                                                     : __builtin_amdgcn_s_memrealtime();           \
+    } while (0)
+#else
+#define YGZ_BSTAMP_K(kern, slot) do {} while (0)
+#endif
+
+// Order LDS traffic between lanes of ONE wave: DS instructions of a wave
+// execute in issue order, so only the compiler must not reorder them.  (A
+// wavefront-scope fence would also emit s_waitcnt vmcnt(0) and stall on any
+// global prefetch in flight.)
+__device__ __forceinline__ void wave_lds_order() { __asm__ __volatile__("" ::: "memory"); }
+
 // XCD-aware block order (cdna_hip_programming.md T1, bijective form): blocks
 // dealt to one XCD (orig % 8) get one contiguous range of logical ids, so a
 // frame's blocks share an L2.  A speed choice only; results never depend on it.

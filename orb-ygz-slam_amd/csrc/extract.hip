@@ -13,9 +13,20 @@
 // evaluation order and the library is built with -ffp-contract=off.
 #include "common.hpp"
 
+#include <algorithm>
+
 namespace ygzfe {
 
 __constant__ __attribute__((aligned(16))) int8_t c_pattern[1024];
+
+#ifdef YGZ_STAMPS
+__device__ unsigned long long g_bstamps[1 << 20];
+extern "C" int ygzfe_diag_block_stamps(unsigned long long *out, int n) {
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bstamps), sizeof(unsigned long long) * (size_t)n);
+    return 0;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // Pyramid
@@ -148,9 +159,9 @@ __global__ __launch_bounds__(256) void k_blur7(const uint8_t *__restrict__ pyr,
         const int xw = max(x - 3, 0);  // reads at most 13 bytes past a row end (pyramid tail padding)
         const bool active = x < w;
         auto window = [&](int r, uint32_t wv[4], uint32_t &o) {
-            const uintptr_t a = (uintptr_t)(src + (size_t)reflect101(y0 + r - 3, hgt) * w + xw);
-            o = (uint32_t)(a & 3u);
-            const uint32_t *q = reinterpret_cast<const uint32_t *>(a - o);
+            const uint8_t *pa = src + (size_t)reflect101(y0 + r - 3, hgt) * w + xw;
+            o = (uint32_t)((uintptr_t)pa & 3u);
+            const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(pa - o));
             if (active) {
                 wv[0] = q[0]; wv[1] = q[1]; wv[2] = q[2]; wv[3] = q[3];
             } else {
@@ -274,71 +285,62 @@ __device__ __forceinline__ int fast9_corner_score(const uint8_t *q, int t) {
     return best - 1;
 }
 
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
 // One wave per cell (four per 256-thread workgroup), each with a dynamic-LDS
 // slice: ROI tile S*S, score map S*S, pixel list 2*(S-6)^2.  Per threshold:
 //   A  every interior pixel: 4-point necessary test -- a 9-arc holds a
 //      neighbouring pair of the compass points 0/4/8/12, i.e.
-//      (p0|p8) & (p4|p12) -- done on ballot masks (SGPRs); survivors
-//      compacted (ballot + mbcnt) into the list
+//      (p0|p8) & (p4|p12) -- 4 pixels per lane on packed i16 pairs;
+//      survivors compacted (ballot + mbcnt) into the list
 //   B  survivors: full segment test, corners compacted in place
 //   C  corners: score into the map
 //   D  corners: strict 3x3 non-max suppression, survivors -> cell list
 // Every list keeps raster order, so the output order is cv::FAST's.
+// ROI staging: lane = (row offset, dword) with S/4 dwords per LDS row; each
+// lane reads the two aligned dwords around its 4 bytes (issue) and realigns
+// them with v_alignbyte into one ds_write_b32 (commit).  NI loads per lane.
 template <int S>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_fast_cells(const uint8_t *__restrict__ pyr, uint32_t pitch,
-                                                    const Plan *__restrict__ plan,
-                                                    const CellDesc *__restrict__ cells,
-                                                    uint32_t *__restrict__ cellbuf,
-                                                    int *__restrict__ cellcnt, int cell_begin, int cell_end) {
-    extern __shared__ uint8_t s_dyn[];
-    constexpr int slice = (2 * S * S + 2 * (S - 6) * (S - 6) + 15) / 16 * 16;  // 16-B aligned slices
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c = cell_begin + blockIdx.x * 4 + wave, f = blockIdx.y;
-    if (c >= cell_end) return;
-    uint8_t *img = s_dyn + wave * slice;
-    uint8_t *sc = img + S * S;
-    uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * S);
-    const CellDesc cd = cells[c];
-    const LevelDesc &L = plan->lv[cd.level];
-    const uint8_t *src = pyr + (size_t)f * pitch + L.off + (size_t)cd.y0 * L.w + cd.x0;
-    const int rw = cd.rw, rh = cd.rh;
-    // ROI -> LDS in ONE batch of global loads: lane = (row offset, dword) with
-    // S/4 dwords per row; each lane reads the two aligned dwords around its 4
-    // bytes and realigns them with v_alignbyte, then writes one ds_write_b32.
-    {
-        constexpr int DW = S / 4, RPI = 64 / DW, NI = (S + RPI - 1) / RPI;
-        const int rlane = lane / DW, dw = lane - rlane * DW;
-        const int ndw = (rw + 3) / 4;
-        constexpr int NB = NI < 8 ? NI : 8;  // loads in flight per batch (one batch for S <= 48)
-        for (int k0 = 0; k0 < NI; k0 += NB) {
-            uint32_t lo[NB], hi[NB];
+struct RoiStage {
+    static constexpr int DW = S / 4, RPI = 64 / DW, NI = (S + RPI - 1) / RPI;
+    uint32_t lo[NI], hi[NI];
+    __device__ __forceinline__ void issue(const uint8_t *src, int w, int rw, int rh, int lane) {
+        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + 3) / 4;
 #pragma unroll
-            for (int j = 0; j < NB; j++) {
-                const int r = (k0 + j) * RPI + rlane;
-                lo[j] = hi[j] = 0u;
-                if (rlane < RPI && r < rh && dw < ndw) {
-                    const uintptr_t a = (uintptr_t)(src + (size_t)r * L.w) + 4 * dw;
-                    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-                    lo[j] = q[0];
-                    hi[j] = q[1];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < NB; j++) {
-                const int r = (k0 + j) * RPI + rlane;
-                if (rlane < RPI && r < rh && dw < ndw) {
-                    const uint32_t sh = (uint32_t)(((uintptr_t)(src + (size_t)r * L.w)) & 3u);
-                    reinterpret_cast<uint32_t *>(img + r * S)[dw] = __builtin_amdgcn_alignbyte(hi[j], lo[j], sh);
-                }
+        for (int k = 0; k < NI; k++) {
+            const int r = k * RPI + rlane;
+            lo[k] = hi[k] = 0u;
+            if (rlane < RPI && r < rh && dw < ndw) {
+                const uint8_t *pa = src + (size_t)r * w + 4 * dw;
+                const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(pa - ((uintptr_t)pa & 3u)));
+                lo[k] = q[0];
+                hi[k] = q[1];
             }
         }
     }
+    __device__ __forceinline__ void commit(uint8_t *img, const uint8_t *src, int w, int rw, int rh, int lane) const {
+        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + 3) / 4;
+#pragma unroll
+        for (int k = 0; k < NI; k++) {
+            const int r = k * RPI + rlane;
+            if (rlane < RPI && r < rh && dw < ndw) {
+                const uint32_t sh = (uint32_t)(((uintptr_t)(src + (size_t)r * w)) & 3u);
+                reinterpret_cast<uint32_t *>(img + r * S)[dw] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh);
+            }
+        }
+        wave_lds_order();
+    }
+};
+
+// One (cell, frame) item on a wave whose ROI is already in LDS: phases A-D (+ retry).
+template <int S>
+__device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, const CellDesc &cd, uint8_t *img,
+                                               uint8_t *sc, uint16_t *list, uint32_t *__restrict__ out,
+                                               int *__restrict__ cnt_out, int lane) {
+    const int rw = cd.rw, rh = cd.rh;
     const int iw = rw - 6, ih = rh - 6;
-    // lane -> pixel: 32 lanes per row (two rows per chunk) when the interior is
-    // at most 32 wide, else 64 lanes per row (and column chunks past 64)
-    const bool half = iw <= 32;
-    const int xl = half ? (lane & 31) : lane, yl = half ? (lane >> 5) : 0, ystep = half ? 2 : 1;
-    uint32_t *out = cellbuf + ((size_t)f * plan->ncells + c) * plan->cell_cap;
     int total = 0;
     for (int pass = 0; pass < 2; pass++) {
         const int th = pass == 0 ? plan->ini_th : plan->min_th;
@@ -348,31 +350,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             for (int i = lane; i < (rh * S) / 16; i += 64) z[i] = zero;
             for (int i = ((rh * S) / 16) * 16 + lane; i < rh * S; i += 64) sc[i] = 0;
         }
-        // A
+        // A: 4 pixels per lane, byte pairs as packed i16 (v_pk_add/sub_i16): a
+        //    negative half means "brighter than v+t" / "darker than v-t"; the
+        //    test is (T|B) & (L|R) on those sign bits for either polarity.
         int na = 0;
         if (iw > 0 && ih > 0) {
-            for (int cx0 = 0; cx0 < iw; cx0 += 64) {
-                const int x = cx0 + xl;
-                const bool colok = x < iw;
-                const uint8_t *q = img + yl * S + x;  // q = centre - 3S - 3 of pixel (x+3, yl+3)
-                for (int y0 = 0; y0 < ih; y0 += ystep) {
-                    const uint8_t *qq = q + y0 * S;
-                    const int v = qq[Ring<S>::kCentre];
-                    const int d0 = qq[Ring<S>::off(0)], d4 = qq[Ring<S>::off(4)];
-                    const int d8 = qq[Ring<S>::off(8)], d12 = qq[Ring<S>::off(12)];
-                    const int hi = v + th, lo = v - th;
-                    const uint64_t in = __ballot(colok && y0 + yl < ih);
-                    const uint64_t b0 = __ballot(d0 > hi), b4 = __ballot(d4 > hi);
-                    const uint64_t b8 = __ballot(d8 > hi), b12 = __ballot(d12 > hi);
-                    const uint64_t k0 = __ballot(d0 < lo), k4 = __ballot(d4 < lo);
-                    const uint64_t k8 = __ballot(d8 < lo), k12 = __ballot(d12 < lo);
-                    const uint64_t m = in & (((b0 | b8) & (b4 | b12)) | ((k0 | k8) & (k4 | k12)));
-                    if ((m >> lane) & 1)
-                        list[na + popc_below(m)] = (uint16_t)((x + 3) | ((y0 + yl + 3) << 8));
-                    na += __popcll(m);
+            const int lpr = iw <= 32 ? 8 : (iw <= 64 ? 16 : 32);  // lanes per row (4 px each)
+            const int rpc = 64 / lpr;                                  // rows per chunk
+            const int j = lane & (lpr - 1), rr = lane / lpr;
+            uint32_t colmask = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) colmask |= (uint32_t)(4 * j + k < iw) << k;
+            const s16x2 t2 = {(short)th, (short)th};
+            for (int y0 = 0; y0 < ih; y0 += rpc) {
+                const int y = y0 + rr;  // interior row; its pixels are ROI (4j+3+k, y+3)
+                const uint32_t *rt = reinterpret_cast<const uint32_t *>(img + y * S) + j;
+                const uint32_t *rc = reinterpret_cast<const uint32_t *>(img + (y + 3) * S) + j;
+                const uint32_t *rb = reinterpret_cast<const uint32_t *>(img + (y + 6) * S) + j;
+                const uint32_t D0 = rc[0], D1 = rc[1], D2 = rc[2];
+                const uint32_t C = __builtin_amdgcn_alignbyte(D1, D0, 3);   // x .. x+3
+                const uint32_t Lw = D0;                                      // x-3 .. x
+                const uint32_t Rw = __builtin_amdgcn_alignbyte(D2, D1, 2);  // x+3 .. x+6
+                const uint32_t Tw = __builtin_amdgcn_alignbyte(rt[1], rt[0], 3);
+                const uint32_t Bw = __builtin_amdgcn_alignbyte(rb[1], rb[0], 3);
+                uint32_t sg[2];
+#pragma unroll
+                for (int hlf = 0; hlf < 2; hlf++) {
+                    const uint32_t sel = hlf ? 0x0C030C01u : 0x0C020C00u;  // bytes 1,3 / 0,2 -> u16 lanes
+                    const s16x2 v = as_s16x2(__builtin_amdgcn_perm(C, C, sel));
+                    const s16x2 hi = v + t2, lo = v - t2;
+                    const s16x2 dT = as_s16x2(__builtin_amdgcn_perm(Tw, Tw, sel));
+                    const s16x2 dB = as_s16x2(__builtin_amdgcn_perm(Bw, Bw, sel));
+                    const s16x2 dL = as_s16x2(__builtin_amdgcn_perm(Lw, Lw, sel));
+                    const s16x2 dR = as_s16x2(__builtin_amdgcn_perm(Rw, Rw, sel));
+                    const uint32_t bright = (as_u32(hi - dT) | as_u32(hi - dB)) & (as_u32(hi - dL) | as_u32(hi - dR));
+                    const uint32_t dark = (as_u32(dT - lo) | as_u32(dB - lo)) & (as_u32(dL - lo) | as_u32(dR - lo));
+                    sg[hlf] = bright | dark;
                 }
+                uint32_t m = ((sg[0] >> 15) & 1u) | (((sg[1] >> 15) & 1u) << 1) | (((sg[0] >> 31) & 1u) << 2) |
+                             (((sg[1] >> 31) & 1u) << 3);
+                m &= y < ih ? colmask : 0u;
+                const uint64_t M0 = __ballot(m & 1u), M1 = __ballot(m & 2u), M2 = __ballot(m & 4u), M3 = __ballot(m & 8u);
+                int pos = na + popc_below(M0) + popc_below(M1) + popc_below(M2) + popc_below(M3);
+                const uint32_t ey = (uint32_t)(y + 3) << 8;
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if ((m >> k) & 1u) list[pos++] = (uint16_t)(ey | (uint32_t)(4 * j + k + 3));
+                na += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
             }
         }
+        if (S == 40 && pass == 0) YGZ_BSTAMP_K(2, 4);
         // B: full segment test, compacted in place (writes never pass the read front)
         int nc = 0;
         for (int i0 = 0; i0 < na; i0 += 64) {
@@ -383,15 +410,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             if (corner) list[nc + popc_below(m)] = e;
             nc += __popcll(m);
         }
+        if (S == 40 && pass == 0) YGZ_BSTAMP_K(2, 5);
         // C: scores of the corners
         for (int i = lane; i < nc; i += 64) {
             const uint16_t e = list[i];
             const int off = (e >> 8) * S + (e & 0xFF);
             sc[off] = (uint8_t)fast9_corner_score<S>(img + off - Ring<S>::kCentre, th);
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_lds_order();
+        if (S == 40 && pass == 0) YGZ_BSTAMP_K(2, 6);  // after C
         // D: strict 3x3 NMS over the corner list
         for (int i0 = 0; i0 < nc; i0 += 64) {
             const int i = i0 + lane;
@@ -413,7 +440,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         }
         if (total > 0) break;
     }
-    if (lane == 0) cellcnt[(size_t)f * plan->ncells + c] = min(total, plan->cell_cap);
+    if (S == 40) YGZ_BSTAMP_K(2, 7);
+    if (lane == 0) *cnt_out = min(total, plan->cell_cap);
+}
+
+// One wave per (cell, frame) item (four per 256-thread workgroup), each with a
+// dynamic-LDS slice: ROI tile S*S, score map S*S, pixel list 2*(S-6)^2.
+// (A persistent variant -- a resident-sized grid walking item ranges with the
+// next ROI prefetched -- measured slower: item costs vary with texture, and
+// the waves per CU, not the dispatch, bound the throughput.)
+template <int S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_fast_cells(
+    const uint8_t *__restrict__ pyr, uint32_t pitch, const Plan *__restrict__ plan,
+    const CellDesc *__restrict__ cells, uint32_t *__restrict__ cellbuf, int *__restrict__ cellcnt, int cell_begin,
+    int cell_end) {
+    extern __shared__ uint8_t s_dyn[];
+    constexpr int slice = (2 * S * S + 2 * (S - 6) * (S - 6) + 15) / 16 * 16;  // 16-B aligned slices
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.y;
+    const int c = cell_begin + blockIdx.x * 4 + wave;
+    if (c >= cell_end) return;
+    uint8_t *img = s_dyn + wave * slice;
+    uint8_t *sc = img + S * S;
+    uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * S);
+    const CellDesc cd = cells[c];
+    const LevelDesc &L = plan->lv[cd.level];
+    const uint8_t *src = pyr + (size_t)f * pitch + L.off + (size_t)cd.y0 * L.w + cd.x0;
+    if (S == 40) YGZ_BSTAMP_K(2, 0);
+    {
+        RoiStage<S> st;
+        st.issue(src, L.w, cd.rw, cd.rh, lane);
+        st.commit(img, src, L.w, cd.rw, cd.rh, lane);
+    }
+    if (S == 40) YGZ_BSTAMP_K(2, 3);
+    fast_cell_item<S>(plan, cd, img, sc, list, cellbuf + ((size_t)f * plan->ncells + c) * plan->cell_cap,
+                      cellcnt + (size_t)f * plan->ncells + c, lane);
+    if (S == 40) YGZ_BSTAMP_K(2, 1);
+    if (S == 40) YGZ_BSTAMP_K(2, 2);
 }
 
 // per-level ROI stride: the level's largest cell ROI rounded up to 8 (>= 40)
@@ -891,6 +954,37 @@ __device__ __forceinline__ int row16_sum(int v) {
     return v;
 }
 
+constexpr int kPatchStride = 64;  // LDS row of a staged keypoint window: 4 x 16 B (window + 16-B misalignment)
+
+// A keypoint window (rows cy-R .. cy-R+NROWS-1) as 4 lanes x 16 B per row, each
+// row the 64 B at ((img + (cy-R+r)*w + cx-R) & ~15): loaded into registers by
+// load_window (so both windows of a keypoint are in flight together), written
+// unshifted to LDS by store_window (tap (r, c) at P[r*64 + o(r) + c]).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+template <int R, int NROWS>
+struct Window {
+    static constexpr int NK = (NROWS + 3) / 4;
+    u32x4 v[NK];
+    __device__ __forceinline__ void load(const uint8_t *img, int w, int cx, int cy, int s) {
+        const uint8_t *base = img + (size_t)(cy - R) * w + (cx - R);
+        const int j = s & 3, r0 = s >> 2;
+#pragma unroll
+        for (int k = 0; k < NK; k++) {  // rows past the window re-read its last row (not stored)
+            const uint8_t *rowp = base + (size_t)min(r0 + 4 * k, NROWS - 1) * w;
+            v[k] = as_global(reinterpret_cast<const u32x4 *>(rowp - ((uintptr_t)rowp & 15u)))[j];
+        }
+    }
+    __device__ __forceinline__ void store(uint8_t *P, int s) const {
+        const int j = s & 3, r0 = s >> 2;
+#pragma unroll
+        for (int k = 0; k + 1 < NK; k++) *reinterpret_cast<u32x4 *>(P + (r0 + 4 * k) * kPatchStride + 16 * j) = v[k];
+        if (r0 + 4 * (NK - 1) < NROWS)
+            *reinterpret_cast<u32x4 *>(P + (r0 + 4 * (NK - 1)) * kPatchStride + 16 * j) = v[NK - 1];
+        wave_lds_order();
+    }
+};
+
 // New keypoints of the octree: rows n_existing + prefix(level) + k.
 // One 16-lane DPP row per keypoint (four per wave, sixteen per workgroup):
 //   IC_Angle: lane s sums columns u = s-15 and u = s+1 over the 31 rows
@@ -903,6 +997,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
                                                      const int *__restrict__ n_existing,
                                                      ygzfe_kp *__restrict__ kps, uint8_t *__restrict__ desc,
                                                      int *__restrict__ counts, int row_cap) {
+    __shared__ uint8_t s_patch[16][37 * kPatchStride];  // one 37x37 window per keypoint row
+    YGZ_BSTAMP_K(1, 0);
     int bx, f;
     swizzled_block_2d(bx, f);  // one frame's keypoints on one XCD: patch lines shared in its L2
     const int lane = threadIdx.x & 63, s = lane & 15;
@@ -928,47 +1024,82 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     const int w = L.w, h = L.h;
     const uint32_t key = sel[(size_t)f * plan->sel_total + L.sel_off + (idx - pre)];
     const int cx = key_x(key) + kMinBorder, cy = key_y(key) + kMinBorder;
-    // IC_Angle (ORBextractor.cc:77-101)
+    float angle;
+    // The row's keypoint windows are staged in LDS by 16-B aligned dwordx4 loads
+    // (4 lanes x 16 B per window row, kept unshifted: window row r starts at byte
+    // o(r) = (row address) & 15 of LDS row r), then every tap is an LDS byte read.
+    // Octree keypoints sit >= 19 px inside the level, so the 31x31 IC window and
+    // the 37x37 rotated-pattern window never leave it.
+    uint8_t *P = s_patch[threadIdx.x >> 4];
+    // IC_Angle (ORBextractor.cc:77-101) on the unblurred level
     const uint8_t *img = pyr + (size_t)f * pitch + L.off;
-    const int ua = s - 15, ub = s + 1;
+    const uint8_t *bimg = blur + (size_t)f * pitch + L.off;
+    Window<15, 31> wic;
+    Window<18, 37> wdesc;
+    // per-lane IC row masks (umax, ORBextractor.cc:453-467) and the lane's 16
+    // pattern pairs are read before the LDS fences, which loads cannot cross
+    const int ua = s - 15, ub = s + 1;  // columns owned by this lane
     const bool hasb = s < 15;
-    const int xa = clampi(cx + ua, 0, w - 1), xb = clampi(cx + ub, 0, w - 1);
-    const uint8_t *c0 = img + (size_t)clampi(cy, 0, h - 1) * w;
-    int m10 = ua * c0[xa] + (hasb ? ub * c0[xb] : 0), m01 = 0;
+    uint32_t va = 0, vb = 0;  // bit v: row offset v is inside the IC disc for column ua / ub
 #pragma unroll
     for (int v = 1; v <= 15; v++) {
         const int um = plan->umax[v];
-        const uint8_t *rp = img + (size_t)clampi(cy + v, 0, h - 1) * w;
-        const uint8_t *rm = img + (size_t)clampi(cy - v, 0, h - 1) * w;
-        const int pa = rp[xa], ma = rm[xa], pb = rp[xb], mb = rm[xb];
-        if (-ua <= um) { m01 += v * (pa - ma); m10 += ua * (pa + ma); }
-        if (hasb && ub <= um) { m01 += v * (pb - mb); m10 += ub * (pb + mb); }
+        va |= (uint32_t)(-ua <= um) << v;
+        vb |= (uint32_t)(hasb && ub <= um) << v;
     }
-    m01 = row16_sum(m01);
-    m10 = row16_sum(m10);
-    const float angle = fast_atan2_deg((float)m01, (float)m10);
+    const int4 *pp = reinterpret_cast<const int4 *>(c_pattern) + s * 4;  // 16 pairs x (x0,y0,x1,y1)
+    int4 pat[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) pat[q] = pp[q];
+    YGZ_BSTAMP_K(1, 3);
+    wic.load(img, w, cx, cy, s);  // both windows in flight before the first wait
+    wdesc.load(bimg, w, cx, cy, s);
+    {
+        wic.store(P, s);
+        YGZ_BSTAMP_K(1, 4);
+        const uint32_t o0 = (uint32_t)(uintptr_t)(img + (size_t)(cy - 15) * w + (cx - 15));
+        auto row = [&](int r) { return P + r * kPatchStride + ((o0 + (uint32_t)(r * w)) & 15u); };
+        const uint8_t *c0 = row(15);
+        int m10 = ua * c0[s] + (hasb ? ub * c0[s + 16] : 0), m01 = 0;
+#pragma unroll
+        for (int v = 1; v <= 15; v++) {
+            const uint8_t *rp = row(15 + v), *rm = row(15 - v);
+            const int pa = rp[s], ma = rm[s], pb = rp[s + 16], mb = rm[s + 16];
+            if ((va >> v) & 1) { m01 += v * (pa - ma); m10 += ua * (pa + ma); }
+            if ((vb >> v) & 1) { m01 += v * (pb - mb); m10 += ub * (pb + mb); }
+        }
+        m01 = row16_sum(m01);
+        m10 = row16_sum(m10);
+        angle = fast_atan2_deg((float)m01, (float)m10);
+    }
     // computeOrbDescriptor (ORBextractor.cc:105-149) on the blurred level
-    const uint8_t *bimg = blur + (size_t)f * pitch + L.off;
+    YGZ_BSTAMP_K(1, 5);
+    wave_lds_order();  // IC taps read before the window is replaced
+    wdesc.store(P, s);
+    const uint32_t o0 = (uint32_t)(uintptr_t)(bimg + (size_t)(cy - 18) * w + (cx - 18));
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float ang = angle * factorPI;
     const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
-    const int4 *pp = reinterpret_cast<const int4 *>(c_pattern) + s * 4;  // 16 pairs x (x0,y0,x1,y1)
+    YGZ_BSTAMP_K(1, 6);
+    auto tap = [&](int dy, int dx) {  // blurred pixel (cy + dy, cx + dx)
+        const int r = dy + 18;
+        return (int)P[r * kPatchStride + ((o0 + (uint32_t)(r * w)) & 15u) + dx + 18];
+    };
     uint32_t bits = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        const int4 P = pp[q];
-        const uint32_t wd[4] = {(uint32_t)P.x, (uint32_t)P.y, (uint32_t)P.z, (uint32_t)P.w};
+        const int4 Pq = pat[q];
+        const uint32_t wd[4] = {(uint32_t)Pq.x, (uint32_t)Pq.y, (uint32_t)Pq.z, (uint32_t)Pq.w};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const float px0 = (float)(int8_t)(wd[k] & 0xFF), py0 = (float)(int8_t)((wd[k] >> 8) & 0xFF);
             const float px1 = (float)(int8_t)((wd[k] >> 16) & 0xFF), py1 = (float)(int8_t)(wd[k] >> 24);
-            const int y0 = cy + cv_round(px0 * sb + py0 * ca), x0 = cx + cv_round(px0 * ca - py0 * sb);
-            const int y1 = cy + cv_round(px1 * sb + py1 * ca), x1 = cx + cv_round(px1 * ca - py1 * sb);
-            const int t0 = bimg[(size_t)clampi(y0, 0, h - 1) * w + clampi(x0, 0, w - 1)];
-            const int t1 = bimg[(size_t)clampi(y1, 0, h - 1) * w + clampi(x1, 0, w - 1)];
+            const int t0 = tap(cv_round(px0 * sb + py0 * ca), cv_round(px0 * ca - py0 * sb));
+            const int t1 = tap(cv_round(px1 * sb + py1 * ca), cv_round(px1 * ca - py1 * sb));
             bits |= (uint32_t)(t0 < t1) << (q * 4 + k);
         }
     }
+    YGZ_BSTAMP_K(1, 7);
     const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bits, 0xB1, 0xF, 0xF, false);
     const int row = ne + idx;
     if ((s & 1) == 0)
@@ -985,6 +1116,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
         kp.class_id = -1;
         kps[(size_t)f * row_cap + row] = kp;
     }
+    YGZ_BSTAMP_K(1, 1);
+    YGZ_BSTAMP_K(1, 2);
 }
 
 // Existing keypoints (Frame::mvKeys of a direct-tracked frame): descriptor on
@@ -1011,6 +1144,14 @@ __global__ __launch_bounds__(256) void k_desc_existing(const uint8_t *__restrict
 
 // ---------------------------------------------------------------------------
 // host launchers
+
+// compute units of the current device (persistent grids are sized from it)
+static int device_cus() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        return 256;
+    return n;
+}
 
 hipError_t upload_pattern(const int *pat) {
     int8_t p8[1024];
@@ -1046,10 +1187,10 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
     for (int l = 0; l < hp.nlevels; l++) {
         const LevelDesc &L = hp.lv[l];
         if (L.ncells == 0) continue;
-        const dim3 grid((L.ncells + 3) / 4, nframes);
         const int S = fast_stride(L.fast_roi);
         const size_t lds = fast_cells_lds_bytes(S);
         const int cb = L.cell_begin, ce = L.cell_begin + L.ncells;
+        const dim3 grid((L.ncells + 3) / 4, nframes);
         // level 0 on the caller's stream, the others spread over the given side streams
         const hipStream_t st = (l == 0 || !lvl_streams || n_lvl_streams <= 0) ? st0
                                                                                 : lvl_streams[(l - 1) % n_lvl_streams];
