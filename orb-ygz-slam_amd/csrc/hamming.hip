@@ -4,8 +4,9 @@
 // Dense best/second-best: the inner candidate loops of SearchByProjection /
 // SearchForInitialization / SearchByBoW (ORBmatcher.cc:43-126,375-478,1218-1350)
 // keep `dist < bestDist` (first index wins on ties) and the second best.
-// One thread per query keeps its descriptor in 8 VGPRs; train descriptors are
-// staged through LDS in 1024-row tiles (32 KiB) shared by the workgroup.
+// A query descriptor lives in 8 VGPRs of its lane; train descriptors are
+// staged through LDS in 1024-row tiles (32 KiB) shared by the workgroup and
+// read as broadcasts, 4 rows per step.
 #include "common.hpp"
 
 namespace ygzfe {
@@ -17,11 +18,33 @@ __device__ __forceinline__ void best2_update(int d, int j, int &b1, int &b2, int
     else if (d < b2) b2 = d;
 }
 
+__device__ __forceinline__ int ham256(const uint32_t a[8], const uint4 &v0, const uint4 &v1) {
+    int d = __popc(a[0] ^ v0.x);
+    d = __popc(a[1] ^ v0.y) + d;
+    d = __popc(a[2] ^ v0.z) + d;
+    d = __popc(a[3] ^ v0.w) + d;
+    d = __popc(a[4] ^ v1.x) + d;
+    d = __popc(a[5] ^ v1.y) + d;
+    d = __popc(a[6] ^ v1.z) + d;
+    d = __popc(a[7] ^ v1.w) + d;
+    return d;
+}
+
+// A workgroup serves 64 queries (one per lane); its 4 waves scan the four
+// contiguous quarters of the train set (4x the waves of a query-per-thread
+// layout), then the partial results merge in train order: best = smallest b1,
+// earliest quarter on ties (so the first minimum index wins, as in the
+// sequential loop); second = min(winner's b2, the other quarters' b1) -- the
+// sequential b2 is the smallest distance over all trains but the winner.
+constexpr int kQPB = 64;
+
 __device__ void hamming_block(const uint8_t *__restrict__ q, int nq, const uint8_t *__restrict__ t, int nt,
                               int32_t *__restrict__ bi_out, int32_t *__restrict__ bd_out,
                               int32_t *__restrict__ sd_out, int qblock) {
     __shared__ uint4 s_t[kHamTile * 2];
-    const int qi = qblock * blockDim.x + threadIdx.x;
+    __shared__ int s_part[4][3][kQPB];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int qi = qblock * kQPB + lane;
     uint32_t a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (qi < nq) {
         const uint4 *qp = reinterpret_cast<const uint4 *>(q + (size_t)qi * 32);
@@ -36,15 +59,33 @@ __device__ void hamming_block(const uint8_t *__restrict__ q, int nq, const uint8
         const uint4 *tp = reinterpret_cast<const uint4 *>(t + (size_t)t0 * 32);
         for (int i = threadIdx.x; i < m * 2; i += blockDim.x) s_t[i] = tp[i];
         __syncthreads();
-        for (int j = 0; j < m; j++) {
-            const uint4 v0 = s_t[2 * j], v1 = s_t[2 * j + 1];
-            const int d = __popc(a[0] ^ v0.x) + __popc(a[1] ^ v0.y) + __popc(a[2] ^ v0.z) +
-                          __popc(a[3] ^ v0.w) + __popc(a[4] ^ v1.x) + __popc(a[5] ^ v1.y) +
-                          __popc(a[6] ^ v1.z) + __popc(a[7] ^ v1.w);
-            best2_update(d, t0 + j, b1, b2, bi);
+        const int qlen = (m + 3) >> 2, jb = wave * qlen, je = min(m, jb + qlen);  // this wave's quarter
+        int j = jb;
+        for (; j + 4 <= je; j += 4) {
+            uint4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = s_t[2 * j + u];
+#pragma unroll
+            for (int u = 0; u < 4; u++) best2_update(ham256(a, v[2 * u], v[2 * u + 1]), t0 + j + u, b1, b2, bi);
+        }
+        for (; j < je; j++) best2_update(ham256(a, s_t[2 * j], s_t[2 * j + 1]), t0 + j, b1, b2, bi);
+        // merge this tile's quarters in order into wave 0's running result
+        s_part[wave][0][lane] = b1;
+        s_part[wave][1][lane] = b2;
+        s_part[wave][2][lane] = bi;
+        __syncthreads();
+        if (wave == 0) {
+#pragma unroll
+            for (int w = 1; w < 4; w++) {
+                const int c1 = s_part[w][0][lane], c2 = s_part[w][1][lane], ci = s_part[w][2][lane];
+                if (c1 < b1) { b2 = min(b1, c2); b1 = c1; bi = ci; }
+                else b2 = min(b2, c1);
+            }
+        } else {
+            b1 = 257; b2 = 257; bi = -1;
         }
     }
-    if (qi < nq) {
+    if (wave == 0 && qi < nq) {
         bi_out[qi] = bi;
         bd_out[qi] = b1;
         sd_out[qi] = b2;
@@ -70,7 +111,7 @@ __global__ __launch_bounds__(256) void k_hamming_best2_pairs(const uint8_t *__re
     const int p = blockIdx.y;
     const int qf = qframe[p], tf = tframe[p];
     const int nq = counts[qf], nt = counts[tf];
-    if ((int)(blockIdx.x * blockDim.x) >= nq) return;
+    if ((int)(blockIdx.x * kQPB) >= nq) return;
     hamming_block(desc + (size_t)qf * row_cap * 32, nq, desc + (size_t)tf * row_cap * 32, nt,
                   bi + (size_t)p * row_cap, bd + (size_t)p * row_cap, sd + (size_t)p * row_cap, blockIdx.x);
 }
@@ -96,7 +137,7 @@ __global__ __launch_bounds__(256) void k_hamming_csr(const uint8_t *__restrict__
 hipError_t launch_hamming_best2(const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *bi, int32_t *bd,
                                 int32_t *sd, hipStream_t st) {
     if (nq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hamming_best2, dim3((nq + 255) / 256), dim3(256), 0, st, q, nq, t, nt, bi, bd, sd);
+    hipLaunchKernelGGL(k_hamming_best2, dim3((nq + kQPB - 1) / kQPB), dim3(256), 0, st, q, nq, t, nt, bi, bd, sd);
     return hipGetLastError();
 }
 
@@ -104,7 +145,8 @@ hipError_t launch_hamming_best2_pairs(const uint8_t *desc, const int32_t *counts
                                       const int32_t *qframe, const int32_t *tframe, int32_t *bi, int32_t *bd,
                                       int32_t *sd, hipStream_t st) {
     if (npairs <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hamming_best2_pairs, dim3((row_cap + 255) / 256, npairs), dim3(256), 0, st, desc, counts,
+    hipLaunchKernelGGL(k_hamming_best2_pairs, dim3((row_cap + kQPB - 1) / kQPB, npairs), dim3(256), 0, st,
+                       desc, counts,
                        row_cap, qframe, tframe, bi, bd, sd);
     return hipGetLastError();
 }
