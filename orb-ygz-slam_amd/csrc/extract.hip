@@ -449,8 +449,10 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
 // (A persistent variant -- a resident-sized grid walking item ranges with the
 // next ROI prefetched -- measured slower: item costs vary with texture, and
 // the waves per CU, not the dispatch, bound the throughput.)
+constexpr int kFastWaves = 4;  // cells (waves) per workgroup (8 measured slower: a block holds its LDS until its slowest cell ends)
+
 template <int S>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_fast_cells(
+__global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(6))) void k_fast_cells(
     const uint8_t *__restrict__ pyr, uint32_t pitch, const Plan *__restrict__ plan,
     const CellDesc *__restrict__ cells, uint32_t *__restrict__ cellbuf, int *__restrict__ cellcnt, int cell_begin,
     int cell_end) {
@@ -458,7 +460,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     constexpr int slice = (2 * S * S + 2 * (S - 6) * (S - 6) + 15) / 16 * 16;  // 16-B aligned slices
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
-    const int c = cell_begin + blockIdx.x * 4 + wave;
+    const int c = cell_begin + blockIdx.x * kFastWaves + wave;
     if (c >= cell_end) return;
     uint8_t *img = s_dyn + wave * slice;
     uint8_t *sc = img + S * S;
@@ -486,7 +488,7 @@ static int fast_stride(int roi) {
 }
 
 static size_t fast_cells_lds_bytes(int S) {
-    return 4 * (size_t)((2 * S * S + 2 * (S - 6) * (S - 6) + 15) / 16 * 16);
+    return kFastWaves * (size_t)((2 * S * S + 2 * (S - 6) * (S - 6) + 15) / 16 * 16);
 }
 
 // ---------------------------------------------------------------------------
@@ -1190,11 +1192,11 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
         const int S = fast_stride(L.fast_roi);
         const size_t lds = fast_cells_lds_bytes(S);
         const int cb = L.cell_begin, ce = L.cell_begin + L.ncells;
-        const dim3 grid((L.ncells + 3) / 4, nframes);
+        const dim3 grid((L.ncells + kFastWaves - 1) / kFastWaves, nframes);
         // level 0 on the caller's stream, the others spread over the given side streams
         const hipStream_t st = (l == 0 || !lvl_streams || n_lvl_streams <= 0) ? st0
                                                                                 : lvl_streams[(l - 1) % n_lvl_streams];
-#define YGZ_FAST(SS) hipLaunchKernelGGL(k_fast_cells<SS>, grid, dim3(256), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce)
+#define YGZ_FAST(SS) hipLaunchKernelGGL(k_fast_cells<SS>, grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce)
         switch (S) {
         case 40: YGZ_FAST(40); break;
         case 48: YGZ_FAST(48); break;
