@@ -222,6 +222,7 @@ def main():
                        "nlevels": nl, "fast_th": [ini, mn], "align_pairs_per_gpu": P,
                        "mean_keypoints": round(N, 1), "mean_align_visible": round(nv, 1),
                        "mean_fast_candidates": round(float(cand.sum()) / B, 1),
+                       "mean_fast_candidates_per_level": [round(float(c) / B, 1) for c in cand],
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": roof,
             "pipeline_gbps_model": round(pipeline_gbps, 2),

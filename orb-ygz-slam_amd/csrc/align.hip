@@ -100,6 +100,48 @@ __device__ void se3_exp(const float a[6], SE3 &out) {
     for (int i = 0; i < 4; i++) out.q[i] = q[i];
 }
 
+// se3_exp with the four transcendentals evaluated in parallel lanes (lane 0:
+// sincos(theta/2), lane 1: sincos(theta)) and broadcast by readlane; every lane
+// of the calling wave must be active and pass the same argument.
+__device__ void se3_exp_wave(const float a[6], SE3 &out) {
+    const float eps = 1e-5f;
+    const float w0 = a[3], w1 = a[4], w2 = a[5];
+    const float theta_sq = w0 * w0 + w1 * w1 + w2 * w2;
+    const float theta = sqrtf(theta_sq);
+    const float half_theta = 0.5f * theta;
+    float sn, cs;
+    sincosf((threadIdx.x & 1) ? theta : half_theta, &sn, &cs);
+    const float s_half = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sn), 0));
+    const float c_half = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cs), 0));
+    const float s_th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sn), 1));
+    const float c_th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cs), 1));
+    float imag, real;
+    if (theta < eps) {
+        const float theta_po4 = theta_sq * theta_sq;
+        imag = 0.5f - (float)(1.0 / 48.0) * theta_sq + (float)(1.0 / 3840.0) * theta_po4;
+        real = 1.f - 0.5f * theta_sq + (float)(1.0 / 384.0) * theta_po4;
+    } else {
+        imag = s_half / theta;
+        real = c_half;
+    }
+    const float q[4] = {imag * w0, imag * w1, imag * w2, real};
+    const float O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+    float V[9];
+    if (theta < eps) {
+        quat_to_mat(q, V);
+    } else {
+        float O2[9];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++)
+                O2[i * 3 + j] = O[i * 3 + 0] * O[0 * 3 + j] + O[i * 3 + 1] * O[1 * 3 + j] + O[i * 3 + 2] * O[2 * 3 + j];
+        const float c1 = (1.f - c_th) / theta_sq;
+        const float c2 = (theta - s_th) / (theta_sq * theta);
+        for (int i = 0; i < 9; i++) V[i] = ((i % 4 == 0) ? 1.f : 0.f) + c1 * O[i] + c2 * O2[i];
+    }
+    for (int i = 0; i < 3; i++) out.t[i] = V[i * 3 + 0] * a[0] + V[i * 3 + 1] * a[1] + V[i * 3 + 2] * a[2];
+    for (int i = 0; i < 4; i++) out.q[i] = q[i];
+}
+
 // Eigen LDLT (diagonal pivoting, lower-triangle transpositions), solve with
 // |D_i| <= FLT_MIN treated as 0.  Same algorithm as oracle/align.c.
 __device__ void ldlt_solve6(const float Hin[36], const float b[6], float x[6]) {
@@ -595,8 +637,8 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
             for (int it = 0; it < 10; it++) {
                 __syncthreads();  // A: partials written
             YGZ_STAMP(3);
+                float r = 0.f;
                 if (lane < 29) {
-                    float r = 0.f;
                     if (lane < 8) {  // Jres[6], chi2, n_meas
                         for (int w = 1; w < NW; w++) r += s_part[w][lane];
                     } else {  // H = H_vis - sum of the out-of-bounds features' H_f
@@ -605,41 +647,59 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                         for (int i = 0; i < s_nout; i++) o += s_Hf[k][s_out[i]];
                         r = s_Hvis[k] - o;
                     }
-                    s_part[0][lane] = r;
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const float *tot = s_part[0];
-                if (tid == 0) {
+                YGZ_STAMP(6);
+                // the 29 sums become wave-uniform values (readlane, no LDS round
+                // trip); every lane of the solver wave then runs the same solve
+                float tot[29];
+#pragma unroll
+                for (int k = 0; k < 29; k++) tot[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), k));
+                {
                     float Hm[36], b[6], x[6];
                     int m = 0;
+#pragma unroll
                     for (int rr = 0; rr < 6; rr++)
+#pragma unroll
                         for (int c = rr; c < 6; c++) { Hm[rr * 6 + c] = tot[8 + m]; Hm[c * 6 + rr] = tot[8 + m]; m++; }
+#pragma unroll
                     for (int k = 0; k < 6; k++) b[k] = tot[k];
                     const int nmeas = (int)tot[7];
                     const float new_chi2 = tot[6] / (float)nmeas;
-                    s_nout = 0;
-                    for (int k = 0; k < 36; k++) s_H[k] = Hm[k];
-                    s_nmeas = nmeas;
+                    if (lane == 0) {
+                        s_nout = 0;
+#pragma unroll
+                        for (int k = 0; k < 36; k++) s_H[k] = Hm[k];
+                        s_nmeas = nmeas;
+                    }
+                    YGZ_STAMP(7);
                     ldlt_solve6_reg(Hm, b, x);
-                    if (isnan(x[0])) s_stop = 1;
-                    s_break = 0;
-                    if ((it > 0 && (double)new_chi2 > 1.2 * (double)s_chi2) || s_stop) {
-                        s_T = s_old;  // rollback
-                        s_break = 1;
+                    YGZ_STAMP(8);
+                    const bool stop = s_stop || isnan(x[0]);
+                    const bool rollback = (it > 0 && (double)new_chi2 > 1.2 * (double)s_chi2) || stop;
+                    if (rollback) {
+                        if (lane == 0) {
+                            s_stop = stop ? 1 : 0;
+                            s_T = s_old;
+                            s_break = 1;
+                        }
                     } else {
                         float mx[6];
+#pragma unroll
                         for (int k = 0; k < 6; k++) mx[k] = -x[k];
                         SE3 E, Tn;
-                        se3_exp(mx, E);
-                        se3_mul(s_T, E, Tn);
-                        s_old = s_T;
-                        s_T = Tn;
-                        s_chi2 = new_chi2;
+                        se3_exp_wave(mx, E);
+                        const SE3 Tc = s_T;
+                        se3_mul(Tc, E, Tn);
+                        YGZ_STAMP(10);
                         float nm = -1.f;
+#pragma unroll
                         for (int k = 0; k < 6; k++) nm = fabsf(x[k]) > nm ? fabsf(x[k]) : nm;
-                        if (nm <= 0.000001f) s_break = 1;
+                        if (lane == 0) {
+                            s_old = Tc;
+                            s_T = Tn;
+                            s_chi2 = new_chi2;
+                            s_break = nm <= 0.000001f ? 1 : 0;
+                        }
                     }
                 }
                 __syncthreads();  // B: pose / decision published

@@ -32,8 +32,8 @@ for rep in range(3):
     n = ygzfe.lib().ygzfe_diag_stamps(buf, 4096)
 st = [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
 t0 = st[0][1]
-names = {9: "start", 1: "L0 (precompute done)", 2: "L0b (H_vis)", 3: "A (features done)", 4: "B (solve done)",
-         5: "L1"}
+names = {9: "start", 1: "L0 (precompute done)", 2: "L0b (H_vis)", 3: "A (features done)", 4: "B (published)",
+         5: "L1", 6: "partials reduced", 7: "H/b unpacked", 8: "LDLT done", 10: "exp+mul done"}
 prev = t0
 tot = {}
 for tag, t in st:
