@@ -100,8 +100,15 @@ extern __device__ unsigned long long g_bstamps[1 << 20];
                                                            (20 << 0) | (0 << 6) | (3 << 11))      \
                                                      : __builtin_amdgcn_s_memrealtime();           \
     } while (0)
+#define YGZ_BVAL_K(kern, slot, val)                                                              \
+    do {                                                                                          \
+        if ((kern) != YGZ_STAMP_KERNEL) break;                                                    \
+        const unsigned _b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);        \
+        if (threadIdx.x == 0 && _b < (1u << 17)) g_bstamps[8 * _b + (slot)] = (unsigned long long)(val); \
+    } while (0)
 #else
 #define YGZ_BSTAMP_K(kern, slot) do {} while (0)
+#define YGZ_BVAL_K(kern, slot, val) do {} while (0)
 #endif
 
 // Order LDS traffic between lanes of ONE wave: DS instructions of a wave

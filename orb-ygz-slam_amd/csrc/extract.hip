@@ -580,6 +580,7 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
         S.cq[i][1] = 0u;
     }
     __syncthreads();
+#pragma unroll 4
     for (int j = tid; j < n; j += 256) {
         const int i = nid[j];
         const uint32_t md = S.mid[i];
@@ -740,6 +741,7 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
     overflow = totx >> 24 ? 1 : 0;
     totx &= 0xFFFFFF;
     // d) every key takes its node's new list position
+#pragma unroll 4
     for (int j = tid; j < n; j += 256) {
         const int i = nid[j];
         const uint32_t r = S.remap[i];
@@ -777,18 +779,32 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
             __syncthreads();
             const int nch = min(L.ncells - cb, 256);
             const uint32_t *cs0 = cellbuf + ((size_t)f * plan->ncells + L.cell_begin + cb) * plan->cell_cap;
-            for (int j = tid; j < tot; j += 256) {
-                int lo = 0, hi = nch - 1;
-                while (lo < hi) {
-                    const int md = (lo + hi + 1) >> 1;
-                    if (s_pref[md] <= j) lo = md; else hi = md - 1;
+            for (int j0 = 0; j0 < tot; j0 += 256 * 8) {  // 8 independent key loads in flight per thread
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int j = j0 + 256 * u + tid;
+                    v[u] = 0u;
+                    if (j < tot) {
+                        int lo = 0, hi = nch - 1;
+                        while (lo < hi) {
+                            const int md = (lo + hi + 1) >> 1;
+                            if (s_pref[md] <= j) lo = md; else hi = md - 1;
+                        }
+                        v[u] = cs0[(size_t)lo * plan->cell_cap + (j - s_pref[lo])];
+                    }
                 }
-                K[base + j] = cs0[(size_t)lo * plan->cell_cap + (j - s_pref[lo])];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int j = j0 + 256 * u + tid;
+                    if (j < tot) K[base + j] = v[u];
+                }
             }
             base += tot;
             __syncthreads();
         }
     }
+    if (l == 0) YGZ_BSTAMP_K(3, 3);
     // 2. initial nodes (:535-580): columns of width hX, push_back order, empty ones erased
     const int nIni = L.n_ini;
     const float hX = L.hX;
@@ -819,6 +835,7 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
     __syncthreads();
     for (int j = tid; j < n; j += 256) nid[j] = (uint16_t)S.remap[nid[j]];
     __syncthreads();
+    if (l == 0) YGZ_BSTAMP_K(3, 4);
     // 3. main loop (:585-680)
     const int N = L.budget;
     int cur = 0, seqc = nIni, overflow = 0, nexpand = 0, guard = 0;
@@ -830,6 +847,8 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
         if (size >= N || size == prev) break;
         if (!final_round && size + nexpand * 3 > N) final_round = true;
     }
+    if (l == 0) YGZ_BSTAMP_K(3, 5);
+    if (l == 0) YGZ_BVAL_K(3, 6, guard);
     // 4. retained key per node, list order
     uint32_t *out = sel + (size_t)f * plan->sel_total + L.sel_off;
     if (!overflow) {
@@ -845,6 +864,8 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
         selcnt[(size_t)f * plan->nlevels + l] = overflow ? 0 : min(size, L.sel_cap);
         if (overflow) atomicOr(err, 1);
     }
+    if (l == 0) YGZ_BSTAMP_K(3, 1);
+    if (l == 0) YGZ_BSTAMP_K(3, 2);
 }
 
 // Keys and labels in LDS when the level has at most kOctLdsKeys candidates
@@ -864,6 +885,7 @@ __global__ __launch_bounds__(256) void k_octree(const Plan *__restrict__ plan,
     __shared__ uint16_t sNid[kOctLdsKeys];
     int *s_pref = reinterpret_cast<int *>(S.sortk);  // gather prefix; sortk is free until the final rounds
     const int f = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
+    if (l == 0) YGZ_BSTAMP_K(3, 0);
     const LevelDesc &L = plan->lv[l];
     int part = 0;
     for (int c = tid; c < L.ncells; c += 256) part += cellcnt[(size_t)f * plan->ncells + L.cell_begin + c];
