@@ -237,6 +237,32 @@ int ygzfe_find_direct_projection_batch(const ygzfe_frame *const *ref, const ygzf
                                        const ygzfe_se3 *T_cr, float *px_io, int32_t *search_level,
                                        uint8_t *ok);
 
+/* ------------------------------------------------------------------------ */
+/* Undistortion (Frame::ComputeImagePyramid, Frame.cc:775-790):              */
+/*   initUndistortRectifyMap(K, D, I, K, size, CV_16SC2, map1, map2) once     */
+/*   per camera, remap(img, map1, map2, INTER_LINEAR) per frame.              */
+/* K = (fx, fy, cx, cy), D = mDistCoef (Tracking.cc:171-199): ndist 4 or 5   */
+/* (k1 k2 p1 p2 [k3]) or 8 (k1 k2 p1 p2 k3 k4 k5 k6), up to 12 (+ s1..s4).   */
+typedef struct ygzfe_undistort ygzfe_undistort;
+int ygzfe_undistort_create(int device, const ygzfe_camera *K, const float *dist, int ndist, int width, int height,
+                           ygzfe_undistort **out);
+void ygzfe_undistort_destroy(ygzfe_undistort *u);
+/* host copies of the fixed-point maps: map1 = 2*W*H int16 (x, y), map2 = W*H u16 */
+int ygzfe_undistort_maps(const ygzfe_undistort *u, int16_t *map1, uint16_t *map2);
+/* remap n device images (pitch between images, row stride inside one) */
+int ygzfe_undistort_apply_device(const ygzfe_undistort *u, const uint8_t *d_src, size_t src_pitch, int src_stride,
+                                 uint8_t *d_dst, size_t dst_pitch, int dst_stride, int n_images, void *stream);
+/* ComputeImagePyramid with undistortion: remap(img) -> level 0, then levels */
+int ygzfe_compute_pyramid_undistorted(ygzfe_extractor *ex, ygzfe_frame *f, ygzfe_undistort *u, const uint8_t *img,
+                                      int stride);
+/* batch: raw device frames (W*H each, pitch raw_pitch) -> undistorted
+ * level-0 slots of the batch pyramids (run before ygzfe_batch_extract) */
+int ygzfe_batch_undistort_device(ygzfe_batch *b, const ygzfe_undistort *u, const uint8_t *d_raw, size_t raw_pitch,
+                                 int n_frames, void *stream);
+/* batch: host raw frames (W*H each, contiguous) -> staged on the device,
+ * undistorted into the level-0 slots */
+int ygzfe_batch_upload_undistorted(ygzfe_batch *b, ygzfe_undistort *u, const uint8_t *frames, int n_frames);
+
 #ifdef __cplusplus
 }
 #endif

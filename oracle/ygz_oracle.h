@@ -173,6 +173,15 @@ int ygzo_find_direct_projection(const ygzo_cam *cam, uint8_t **ref_levels, const
                                 const float pt_ref[3], const ygzo_kp *kp_ref, float *px_curr,
                                 int *search_level);
 
+/* ---------------- undistort (Frame.cc:775-790) ---------------- */
+/* cv::initUndistortRectifyMap(K, D, I, K, (W,H), CV_16SC2): map1 [H][W][2]
+ * (integer source x, y), map2 [H][W] (5-bit fractions, y*32 + x). */
+void ygzo_undistort_map(const float cam[4], const float *dist, int ndist, int W, int H, int16_t *map1,
+                        uint16_t *map2);
+/* cv::remap(src, dst, map1, map2, INTER_LINEAR), BORDER_CONSTANT 0 */
+void ygzo_remap_linear(const uint8_t *src, int W, int H, int sstride, const int16_t *map1, const uint16_t *map2,
+                       int DW, int DH, uint8_t *dst, int dstride);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1018,3 +1018,142 @@ extern "C" int ygzfe_find_direct_projection_batch(const ygzfe_frame *const *ref,
     YGZ_HIP(hipStreamSynchronize(st));
     return YGZFE_OK;
 }
+
+// --------------------------------------------------------------------------
+// Undistortion (Frame.cc:775-790)
+struct ygzfe_undistort {
+    int device = 0;
+    int W = 0, H = 0;
+    hipStream_t stream = nullptr;
+    DevBuf map1, map2, boxes, raw;  // boxes: per-tile source boxes; raw: host-frame staging
+    int max_box = 0;                // largest LDS-staged box (bytes)
+};
+
+extern "C" int ygzfe_undistort_create(int device, const ygzfe_camera *K, const float *dist, int ndist, int width,
+                                      int height, ygzfe_undistort **out) {
+    if (!K || !out || (ndist > 0 && !dist) || ndist < 0 || ndist > 12 || width < 2 || height < 2 ||
+        (size_t)width * height > (1u << 30)) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (width > 32767 || height > 32767) { set_error("image too large for CV_16SC2 maps"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(device));
+    std::unique_ptr<ygzfe_undistort> u(new ygzfe_undistort());
+    u->device = device;
+    u->W = width;
+    u->H = height;
+    const size_t n = (size_t)width * height;
+    YGZ_TRY(u->map1.ensure(4 * n));
+    YGZ_TRY(u->map2.ensure(2 * n));
+    YGZ_TRY(u->boxes.ensure(16 * (size_t)remap_tiles(width, height)));
+    YGZ_HIP(hipStreamCreateWithFlags(&u->stream, hipStreamNonBlocking));
+    const float cam[4] = {K->fx, K->fy, K->cx, K->cy};
+    YGZ_HIP(launch_undistort_map(cam, dist, ndist, width, height, u->map1.as<int16_t>(), u->map2.as<uint16_t>(),
+                                 u->stream));
+    YGZ_HIP(launch_remap_boxes(width, height, u->map1.as<int16_t>(), u->boxes.p, u->stream));
+    std::vector<int32_t> boxes(4 * (size_t)remap_tiles(width, height));
+    YGZ_HIP(hipMemcpyAsync(boxes.data(), u->boxes.p, 4 * boxes.size(), hipMemcpyDeviceToHost, u->stream));
+    YGZ_HIP(hipStreamSynchronize(u->stream));
+    for (size_t i = 0; i < boxes.size(); i += 4)
+        if (boxes[i + 3] > 0) u->max_box = std::max(u->max_box, boxes[i + 2] * boxes[i + 3]);
+    *out = u.release();
+    return YGZFE_OK;
+}
+
+extern "C" void ygzfe_undistort_destroy(ygzfe_undistort *u) {
+    if (!u) return;
+    (void)hipSetDevice(u->device);
+    (void)hipStreamSynchronize(u->stream);
+    (void)hipStreamDestroy(u->stream);
+    delete u;
+}
+
+extern "C" int ygzfe_undistort_maps(const ygzfe_undistort *u, int16_t *map1, uint16_t *map2) {
+    if (!u) { set_error("null handle"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(u->device));
+    const size_t n = (size_t)u->W * u->H;
+    if (map1) YGZ_HIP(hipMemcpy(map1, u->map1.p, 4 * n, hipMemcpyDeviceToHost));
+    if (map2) YGZ_HIP(hipMemcpy(map2, u->map2.p, 2 * n, hipMemcpyDeviceToHost));
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_undistort_apply_device(const ygzfe_undistort *u, const uint8_t *d_src, size_t src_pitch,
+                                            int src_stride, uint8_t *d_dst, size_t dst_pitch, int dst_stride,
+                                            int n_images, void *stream) {
+    if (!u || n_images < 0 || (n_images > 0 && (!d_src || !d_dst)) || src_stride < u->W || dst_stride < u->W ||
+        (n_images > 1 && (src_pitch < (size_t)src_stride * u->H || dst_pitch < (size_t)dst_stride * u->H)) ||
+        n_images > 65535) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (n_images == 0) return YGZFE_OK;
+    YGZ_TRY(ensure_device(u->device));
+    hipStream_t st = stream ? (hipStream_t)stream : u->stream;
+    YGZ_HIP(launch_remap_linear(d_src, src_pitch, u->W, u->H, src_stride, u->map1.as<int16_t>(),
+                                u->map2.as<uint16_t>(), u->boxes.p, u->max_box, d_dst, dst_pitch, dst_stride,
+                                n_images, st));
+    if (!stream) YGZ_HIP(hipStreamSynchronize(st));
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_compute_pyramid_undistorted(ygzfe_extractor *ex, ygzfe_frame *f, ygzfe_undistort *u,
+                                                 const uint8_t *img, int stride) {
+    if (!ex || !f || !u || !img || stride < f->W) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    if (u->W != f->W || u->H != f->H || u->device != ex->device) {
+        set_error("undistort maps are %dx%d on device %d, frame is %dx%d on device %d", u->W, u->H, u->device, f->W,
+                  f->H, ex->device);
+        return YGZFE_EINVAL;
+    }
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    const size_t n = (size_t)f->W * f->H;
+    YGZ_TRY(u->raw.ensure(n));
+    YGZ_HIP(hipMemcpy2DAsync(u->raw.p, f->W, img, stride, f->W, f->H, hipMemcpyHostToDevice, ex->stream));
+    YGZ_HIP(launch_remap_linear(u->raw.as<uint8_t>(), n, f->W, f->H, f->W, u->map1.as<int16_t>(),
+                                u->map2.as<uint16_t>(), u->boxes.p, u->max_box, f->pyr.as<uint8_t>(), n, f->W, 1,
+                                ex->stream));
+    YGZ_TRY(pyramid_from_level0(f, ex->stream));
+    YGZ_HIP(hipStreamSynchronize(ex->stream));
+    return YGZFE_OK;
+}
+
+static int batch_undistort_check(const ygzfe_batch *b, const ygzfe_undistort *u, int n_frames) {
+    if (!b || !u || n_frames < 0 || n_frames > b->maxF) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    const Plan &P = b->plan->hp();
+    if (u->W != P.W || u->H != P.H || u->device != b->device) {
+        set_error("undistort maps are %dx%d on device %d, batch is %dx%d on device %d", u->W, u->H, u->device, P.W,
+                  P.H, b->device);
+        return YGZFE_EINVAL;
+    }
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_batch_undistort_device(ygzfe_batch *b, const ygzfe_undistort *u, const uint8_t *d_raw,
+                                            size_t raw_pitch, int n_frames, void *stream) {
+    YGZ_TRY(batch_undistort_check(b, u, n_frames));
+    if (n_frames == 0) return YGZFE_OK;
+    const Plan &P = b->plan->hp();
+    if (!d_raw || (n_frames > 1 && raw_pitch < (size_t)P.W * P.H)) { set_error("invalid raw frames"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(b->device));
+    hipStream_t st = stream ? (hipStream_t)stream : b->stream;
+    YGZ_HIP(launch_remap_linear(d_raw, raw_pitch, P.W, P.H, P.W, u->map1.as<int16_t>(), u->map2.as<uint16_t>(),
+                                u->boxes.p, u->max_box, b->pyr.as<uint8_t>(), P.pyr_bytes, P.W, n_frames, st));
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_batch_upload_undistorted(ygzfe_batch *b, ygzfe_undistort *u, const uint8_t *frames,
+                                              int n_frames) {
+    YGZ_TRY(batch_undistort_check(b, u, n_frames));
+    if (n_frames == 0) return YGZFE_OK;
+    if (!frames) { set_error("null frames"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(b->device));
+    const Plan &P = b->plan->hp();
+    const size_t n = (size_t)P.W * P.H;
+    YGZ_TRY(u->raw.ensure(n * n_frames));
+    YGZ_HIP(hipMemcpyAsync(u->raw.p, frames, n * n_frames, hipMemcpyHostToDevice, b->stream));
+    YGZ_HIP(launch_remap_linear(u->raw.as<uint8_t>(), n, P.W, P.H, P.W, u->map1.as<int16_t>(),
+                                u->map2.as<uint16_t>(), u->boxes.p, u->max_box, b->pyr.as<uint8_t>(), P.pyr_bytes,
+                                P.W, n_frames, b->stream));
+    YGZ_HIP(hipStreamSynchronize(b->stream));
+    return YGZFE_OK;
+}

@@ -76,6 +76,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise YgzfeError(f"{LIB_PATH} missing: run `make -C orb-ygz-slam_amd` (or __graft_entry__.build())")
+        # torch ships its own libamdhip64.so.7; whichever copy loads first
+        # serves the whole process, and torch refuses to run on a runtime it
+        # was not built with.  Load torch's first so device pointers and
+        # streams can be shared with it later in the same process.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         L.ygzfe_last_error.restype = C.c_char_p
         L.ygzfe_batch_stream.restype = C.c_void_p
@@ -118,8 +126,8 @@ class Frame:
         _check(lib().ygzfe_frame_create(extractor.h, width, height, C.byref(self.h)), "frame_create")
 
     def __del__(self):
-        if getattr(self, "h", None) and self.h.value:
-            lib().ygzfe_frame_destroy(self.h)
+        if getattr(self, "h", None) and self.h.value and _lib is not None:
+            _lib.ygzfe_frame_destroy(self.h)
             self.h = None
 
     def level(self, l):
@@ -149,8 +157,8 @@ class ORBextractor:
         _check(lib().ygzfe_extractor_create(C.byref(self.params), device, C.byref(self.h)), "extractor_create")
 
     def __del__(self):
-        if getattr(self, "h", None) and self.h.value:
-            lib().ygzfe_extractor_destroy(self.h)
+        if getattr(self, "h", None) and self.h.value and _lib is not None:
+            _lib.ygzfe_extractor_destroy(self.h)
             self.h = None
 
     # getters (ORBextractor.h:87-109)
@@ -223,6 +231,46 @@ class ORBextractor:
         """operator()(image, mask, keypoints, descriptors) (ORBextractor.cc:970-1028)."""
         frame = self.ComputePyramid(image)
         return self.extract(frame, ORBSLAM_KEYPOINT)
+
+
+class Undistort:
+    """Frame::ComputeImagePyramid's undistortion (Frame.cc:775-790): the CV_16SC2
+    initUndistortRectifyMap maps, built on the device once per camera, and the
+    INTER_LINEAR remap applied per frame."""
+
+    def __init__(self, cam, dist, width, height, device=0):
+        cam = cam if isinstance(cam, Camera) else Camera(*[float(c) for c in cam])
+        d = np.ascontiguousarray(dist, np.float32).ravel()
+        self.width, self.height, self.device = width, height, device
+        self.h = C.c_void_p()
+        _check(lib().ygzfe_undistort_create(device, C.byref(cam), _p(d) if len(d) else None, len(d), width, height,
+                                            C.byref(self.h)), "undistort_create")
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value and _lib is not None:
+            _lib.ygzfe_undistort_destroy(self.h)
+            self.h = None
+
+    def maps(self):
+        """(map1 int16[H, W, 2], map2 uint16[H, W]) -- OpenCV's CV_16SC2 + CV_16UC1 pair."""
+        m1 = np.zeros((self.height, self.width, 2), np.int16)
+        m2 = np.zeros((self.height, self.width), np.uint16)
+        _check(lib().ygzfe_undistort_maps(self.h, _p(m1), _p(m2)), "undistort_maps")
+        return m1, m2
+
+    def apply_device(self, d_src, src_pitch, src_stride, d_dst, dst_pitch, dst_stride, n_images, stream=None):
+        _check(lib().ygzfe_undistort_apply_device(self.h, C.c_void_p(d_src), C.c_size_t(src_pitch), src_stride,
+                                                  C.c_void_p(d_dst), C.c_size_t(dst_pitch), dst_stride, n_images,
+                                                  C.c_void_p(stream)), "undistort_apply")
+
+    def ComputePyramid(self, extractor, image, frame=None):
+        """ComputeImagePyramid with mDistCoef != 0: remap(image) -> level 0 -> levels."""
+        image = np.ascontiguousarray(image, np.uint8)
+        H, W = image.shape
+        frame = frame if frame is not None else Frame(extractor, W, H)
+        _check(lib().ygzfe_compute_pyramid_undistorted(extractor.h, frame.h, self.h, _p(image), W),
+               "compute_pyramid_undistorted")
+        return frame
 
 
 class ORBmatcher:
@@ -323,8 +371,8 @@ class Batch:
         self.frame_pitch, self.kp_cap, self.nlevels = pitch.value, cap.value, nl.value
 
     def __del__(self):
-        if getattr(self, "h", None) and self.h.value:
-            lib().ygzfe_batch_destroy(self.h)
+        if getattr(self, "h", None) and self.h.value and _lib is not None:
+            _lib.ygzfe_batch_destroy(self.h)
             self.h = None
 
     @property
@@ -334,6 +382,14 @@ class Batch:
     def upload(self, frames):
         frames = np.ascontiguousarray(frames, np.uint8)
         _check(lib().ygzfe_batch_upload(self.h, _p(frames), len(frames)), "batch_upload")
+
+    def upload_undistorted(self, und, frames):
+        frames = np.ascontiguousarray(frames, np.uint8)
+        _check(lib().ygzfe_batch_upload_undistorted(self.h, und.h, _p(frames), len(frames)), "upload_undistorted")
+
+    def undistort_device(self, und, d_raw, raw_pitch, n_frames, stream=None):
+        _check(lib().ygzfe_batch_undistort_device(self.h, und.h, C.c_void_p(d_raw), C.c_size_t(raw_pitch), n_frames,
+                                                  C.c_void_p(stream)), "batch_undistort")
 
     def bind(self, pyramids=0, kps=0, desc=0, counts=0):
         _check(lib().ygzfe_batch_bind_buffers(self.h, C.c_void_p(pyramids or None), C.c_void_p(kps or None),

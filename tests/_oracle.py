@@ -215,6 +215,27 @@ def fast10_nonmax(xs, ys, scores):
     return keep[:n].copy()
 
 
+def undistort_map(cam, dist, W, H):
+    """initUndistortRectifyMap(K, D, I, K, (W, H), CV_16SC2) -> (map1[H,W,2] i16, map2[H,W] u16)."""
+    c = np.ascontiguousarray(cam, np.float32)
+    d = np.ascontiguousarray(dist, np.float32).ravel()
+    m1 = np.zeros((H, W, 2), np.int16)
+    m2 = np.zeros((H, W), np.uint16)
+    lib().ygzo_undistort_map(_p(c), _p(d) if len(d) else None, len(d), W, H, _p(m1), _p(m2))
+    return m1, m2
+
+
+def remap_linear(src, map1, map2):
+    """remap(src, map1, map2, INTER_LINEAR, BORDER_CONSTANT 0) for CV_8U."""
+    src = np.ascontiguousarray(src, np.uint8)
+    H, W = src.shape
+    DH, DW = map2.shape
+    out = np.zeros((DH, DW), np.uint8)
+    lib().ygzo_remap_linear(_p(src), W, H, W, _p(np.ascontiguousarray(map1)), _p(np.ascontiguousarray(map2)),
+                            DW, DH, _p(out), DW)
+    return out
+
+
 def hamming_best2(q, t):
     q = np.ascontiguousarray(q, np.uint8)
     t = np.ascontiguousarray(t, np.uint8)
