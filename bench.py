@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=120, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-align", action="store_true")
+    ap.add_argument("--no-undistort", action="store_true", help="skip the undistort-remap side measurement")
     return ap.parse_args()
 
 
@@ -79,7 +80,11 @@ def main():
 
     batch = ygzfe.Batch((nf, sf, nl, ini, mn, 0), local, W, H, B)
     cap = batch.kp_cap
-    stream = torch.cuda.current_stream(dev)
+    # a real stream shared by torch and ygzfe: torch's default stream is the
+    # legacy null stream (handle 0), which ygzfe reads as "the handle's own
+    # stream" and which does not order against ygzfe's non-blocking streams
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     kps_t = torch.empty((B, cap, 7), dtype=torch.float32, device=dev)
     counts_t = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -198,10 +203,46 @@ def main():
     b_align = 3 * nv * (36 + 10 * 25) + 12 * nv + 96
     pipeline_gbps = (b_extract + b_align) * (fps / world) / 1e9
 
+    # ------------------------------------------------ §8(f) rank 1: undistort remap
+    # (not part of the headline metric; Frame.cc:775-790 runs it ahead of the
+    # pyramid on every EuRoC frame): raw frames resident in HBM -> level-0 slots
+    und_line = None
+    if not args.no_undistort:
+        import _cameras as CAM
+        ucam, udist, _ = CAM.EUROC
+        und = ygzfe.Undistort(ucam, udist, W, H, device=local)
+        raw = torch.from_numpy(frames).to(dev)
+        for _ in range(2):
+            batch.undistort_device(und, raw.data_ptr(), W * H, B, sptr)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = max(args.steps, 5)
+        ev0.record(stream)
+        for _ in range(reps):
+            batch.undistort_device(und, raw.data_ptr(), W * H, B, sptr)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        ums = ev0.elapsed_time(ev1) / reps
+        ualg = B * W * H * 2  # each frame read once and written once (map: cache-resident, shared)
+        ugbps = ualg / (ums * 1e-3) / 1e9
+        und_line = {"kernel": "remap_tiles", "frames_per_s": round(B / (ums * 1e-3), 1),
+                    "ms_per_launch": round(ums, 4), "alg_bytes_per_launch": ualg, "achieved_gbps": round(ugbps, 1),
+                    "frac": round(ugbps / HBM_PEAK_GBPS, 4), "camera": "EuRoC (Examples/Monocular/EuRoC.yaml)"}
+
     # ------------------------------------------------ CPU baseline (rank 0, N = 1)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu = cpu_baseline(frames, poses, S, args, sc)
+        if und_line is not None:
+            import _cameras as CAM
+            import _oracle as O
+            ucam, udist, _ = CAM.EUROC
+            m1, m2 = O.undistort_map(ucam, udist, W, H)
+            t_c = time.perf_counter()
+            nrm = 0
+            while nrm < 8 or time.perf_counter() - t_c < 0.5:
+                O.remap_linear(frames[nrm % B], m1, m2)
+                nrm += 1
+            und_line["cpu_port_frames_per_s"] = round(nrm / (time.perf_counter() - t_c), 1)
 
     if rank == 0:
         line = {
@@ -229,6 +270,7 @@ def main():
             "h2d_upload_ms": round(h2d_s * 1e3, 2),
             "render_s": round(render_s, 2),
             "cpu_baseline": cpu,
+            "next_rows": {"undistort_remap": und_line},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1027,6 +1027,7 @@ struct ygzfe_undistort {
     hipStream_t stream = nullptr;
     DevBuf map1, map2, boxes, raw;  // boxes: per-tile source boxes; raw: host-frame staging
     int max_box = 0;                // largest LDS-staged box (bytes)
+    bool any_large = false;         // some tile's box exceeds the LDS stage (global-gather kernel)
 };
 
 extern "C" int ygzfe_undistort_create(int device, const ygzfe_camera *K, const float *dist, int ndist, int width,
@@ -1056,6 +1057,7 @@ extern "C" int ygzfe_undistort_create(int device, const ygzfe_camera *K, const f
     YGZ_HIP(hipStreamSynchronize(u->stream));
     for (size_t i = 0; i < boxes.size(); i += 4)
         if (boxes[i + 3] > 0) u->max_box = std::max(u->max_box, boxes[i + 2] * boxes[i + 3]);
+        else if (boxes[i + 3] < 0) u->any_large = true;
     *out = u.release();
     return YGZFE_OK;
 }
@@ -1090,8 +1092,8 @@ extern "C" int ygzfe_undistort_apply_device(const ygzfe_undistort *u, const uint
     YGZ_TRY(ensure_device(u->device));
     hipStream_t st = stream ? (hipStream_t)stream : u->stream;
     YGZ_HIP(launch_remap_linear(d_src, src_pitch, u->W, u->H, src_stride, u->map1.as<int16_t>(),
-                                u->map2.as<uint16_t>(), u->boxes.p, u->max_box, d_dst, dst_pitch, dst_stride,
-                                n_images, st));
+                                u->map2.as<uint16_t>(), u->boxes.p, u->max_box, u->any_large, d_dst, dst_pitch,
+                                dst_stride, n_images, st));
     if (!stream) YGZ_HIP(hipStreamSynchronize(st));
     return YGZFE_OK;
 }
@@ -1110,8 +1112,8 @@ extern "C" int ygzfe_compute_pyramid_undistorted(ygzfe_extractor *ex, ygzfe_fram
     YGZ_TRY(u->raw.ensure(n));
     YGZ_HIP(hipMemcpy2DAsync(u->raw.p, f->W, img, stride, f->W, f->H, hipMemcpyHostToDevice, ex->stream));
     YGZ_HIP(launch_remap_linear(u->raw.as<uint8_t>(), n, f->W, f->H, f->W, u->map1.as<int16_t>(),
-                                u->map2.as<uint16_t>(), u->boxes.p, u->max_box, f->pyr.as<uint8_t>(), n, f->W, 1,
-                                ex->stream));
+                                u->map2.as<uint16_t>(), u->boxes.p, u->max_box, u->any_large, f->pyr.as<uint8_t>(),
+                                n, f->W, 1, ex->stream));
     YGZ_TRY(pyramid_from_level0(f, ex->stream));
     YGZ_HIP(hipStreamSynchronize(ex->stream));
     return YGZFE_OK;
@@ -1137,7 +1139,8 @@ extern "C" int ygzfe_batch_undistort_device(ygzfe_batch *b, const ygzfe_undistor
     YGZ_TRY(ensure_device(b->device));
     hipStream_t st = stream ? (hipStream_t)stream : b->stream;
     YGZ_HIP(launch_remap_linear(d_raw, raw_pitch, P.W, P.H, P.W, u->map1.as<int16_t>(), u->map2.as<uint16_t>(),
-                                u->boxes.p, u->max_box, b->pyr.as<uint8_t>(), P.pyr_bytes, P.W, n_frames, st));
+                                u->boxes.p, u->max_box, u->any_large, b->pyr.as<uint8_t>(), P.pyr_bytes, P.W,
+                                n_frames, st));
     return YGZFE_OK;
 }
 
@@ -1152,8 +1155,8 @@ extern "C" int ygzfe_batch_upload_undistorted(ygzfe_batch *b, ygzfe_undistort *u
     YGZ_TRY(u->raw.ensure(n * n_frames));
     YGZ_HIP(hipMemcpyAsync(u->raw.p, frames, n * n_frames, hipMemcpyHostToDevice, b->stream));
     YGZ_HIP(launch_remap_linear(u->raw.as<uint8_t>(), n, P.W, P.H, P.W, u->map1.as<int16_t>(),
-                                u->map2.as<uint16_t>(), u->boxes.p, u->max_box, b->pyr.as<uint8_t>(), P.pyr_bytes,
-                                P.W, n_frames, b->stream));
+                                u->map2.as<uint16_t>(), u->boxes.p, u->max_box, u->any_large, b->pyr.as<uint8_t>(),
+                                P.pyr_bytes, P.W, n_frames, b->stream));
     YGZ_HIP(hipStreamSynchronize(b->stream));
     return YGZFE_OK;
 }

@@ -72,7 +72,7 @@ hipError_t launch_undistort_map(const float cam[4], const float *dist, int ndist
 int remap_tiles(int W, int H);  // entries of the per-tile source-box table (16 B each: x0, y0, w, h)
 hipError_t launch_remap_boxes(int W, int H, const int16_t *map1, void *boxes, hipStream_t st);
 hipError_t launch_remap_linear(const uint8_t *src, size_t src_pitch, int W, int H, int sstride, const int16_t *map1,
-                               const uint16_t *map2, const void *boxes, int max_box, uint8_t *dst, size_t dst_pitch,
-                               int dstride, int n_images, hipStream_t st);
+                               const uint16_t *map2, const void *boxes, int max_box, bool any_large, uint8_t *dst,
+                               size_t dst_pitch, int dstride, int n_images, hipStream_t st);
 
 }  // namespace ygzfe

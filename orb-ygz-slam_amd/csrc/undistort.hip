@@ -86,23 +86,31 @@ __device__ __forceinline__ uint32_t remap_px(const uint8_t *__restrict__ S, int 
 //    weight 0 and a clamped in-box address, so the BORDER_CONSTANT pixels take
 //    the same straight-line code as the interior;
 //  - the boxes of a group of 16/DW frames are loaded at once (coalesced
-//    dwords, DW per thread per frame, all in flight together: a remap is
-//    bound by bytes in flight per CU, not by arithmetic), staged into LDS,
-//    and each output pixel is then 4 ds_read_u8 + 4 mad24 + a shift.
+//    dwords through a range-checked buffer descriptor, DW per thread per
+//    frame, all in flight together), staged into LDS, and each output pixel
+//    is then 4 ds_read_u8 + 4 mul24 + a shift;
+//  - lanes are columns (a tap read of a wave is ~64 consecutive LDS bytes,
+//    free of bank conflicts) and each lane owns 4 rows; a DPP transpose in
+//    each quad turns that into dword stores of 4 horizontal pixels.
 // HBM traffic per frame: ~1.01 B/px read (box overlap) + 1 B/px written.
-constexpr int kRemapTileW = 64, kRemapTileH = 16;  // 256 threads x 4 px
-constexpr int kRemapFramesPerBlock = 8;
+constexpr int kRemapTileW = 64, kRemapTileH = 16;  // 256 threads x 4 rows of one column
+constexpr int kRemapLanesX = kRemapTileW / 4;      // (k_remap_boxes: 4 horizontal pixels per thread)
+constexpr int kRemapFramesPerBlock = 16;  // 4, 8, 16, 32 measured: 85, 67, 60, 62 us per 256 frames
 constexpr int kRemapLdsBytes = 16384;             // one group of boxes
 constexpr int kRemapMaxBox = 4096;                // larger boxes gather from global memory
 
-struct RemapBox { int x0, y0, w, h; };  // w, h == 0: no tap in the image; h < 0: too large for LDS
+struct RemapBox { int x0, y0, w, h; };
+
+// raw buffer descriptors: offsets at or past num_records load 0 / drop the store
+constexpr uint32_t kOutOfRange = 0x80000000u;
+constexpr int kRsrcFlags = 0x00020000;  // w, h == 0: no tap in the image; h < 0: too large for LDS
 
 __global__ __launch_bounds__(256) void k_remap_boxes(int W, int H, const int16_t *__restrict__ map1,
                                                      RemapBox *__restrict__ boxes, int tiles_x) {
     __shared__ int red[4];
     const int t = threadIdx.x;
     const int X0 = (blockIdx.x % tiles_x) * kRemapTileW, Y0 = (blockIdx.x / tiles_x) * kRemapTileH;
-    const int y = Y0 + (t >> 4), xb = X0 + (t & 15) * 4;
+    const int y = Y0 + t / kRemapLanesX, xb = X0 + (t % kRemapLanesX) * 4;
     int mnx = INT_MAX, mny = INT_MAX, mxx = INT_MIN, mxy = INT_MIN;
     if (y < H)
         for (int k = 0; k < 4; k++) {
@@ -136,9 +144,20 @@ __global__ __launch_bounds__(256) void k_remap_boxes(int W, int H, const int16_t
     }
 }
 
-// VEC: W, source/destination strides, pitches and bases are multiples of 4,
-// so box rows load as dwords (the box never passes column W) and each
-// thread's 4 output pixels store as one dword.  DW: box dwords per thread per
+// 4x4 byte transpose across the 4 lanes of a quad: lane q enters with byte r
+// = (row r, column q) and leaves with byte c = (row q, column c).  Step 1
+// swaps bytes with lane q^1 (DPP quad_perm [1,0,3,2]), step 2 byte pairs with
+// lane q^2 ([2,3,0,1]); v_perm picks the bytes with lane-parity selectors.
+__device__ __forceinline__ uint32_t remap_quad_transpose(uint32_t d, uint32_t sel1, uint32_t sel2) {
+    const uint32_t p = (uint32_t)__builtin_amdgcn_mov_dpp((int)d, 0xB1, 0xF, 0xF, false);
+    const uint32_t e = __builtin_amdgcn_perm(d, p, sel1);
+    const uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0x4E, 0xF, 0xF, false);
+    return __builtin_amdgcn_perm(e, r, sel2);
+}
+
+// VEC: W and the source/destination strides, pitches and bases are
+// multiples of 4, so box rows load as dwords (the box never passes column W)
+// and each thread's 4 transposed outputs store as one dword.  DW: box dwords per thread per
 // frame (boxes up to DW KiB); G = 16 / DW frames per group.
 template <bool VEC, int DW>
 __global__ __launch_bounds__(256) void k_remap_tiles(const uint8_t *__restrict__ src, size_t src_pitch, int W, int H,
@@ -146,61 +165,54 @@ __global__ __launch_bounds__(256) void k_remap_tiles(const uint8_t *__restrict__
                                                      const uint16_t *__restrict__ map2,
                                                      const RemapBox *__restrict__ boxes, int tiles_x,
                                                      uint8_t *__restrict__ dst, size_t dst_pitch, int dstride,
-                                                     int n_images) {
+                                                     int n_images, int fpb) {
     constexpr int G = 16 / DW, kBox = DW * 1024;
     __shared__ __attribute__((aligned(16))) uint8_t s_box[kRemapLdsBytes];
     const int t = threadIdx.x;
-    const int X0 = (blockIdx.x % tiles_x) * kRemapTileW, Y0 = (blockIdx.x / tiles_x) * kRemapTileH;
-    const int y = Y0 + (t >> 4), x = X0 + (t & 15) * 4;
-    const int np = y < H ? max(0, min(4, W - x)) : 0;
-    const RemapBox B = boxes[blockIdx.x];
-    const int img0 = blockIdx.y * kRemapFramesPerBlock;
-    const int img1 = min(n_images, img0 + kRemapFramesPerBlock);
+    // adjacent tiles share source cache lines: keep them on one XCD's L2
+    int tile, group;
+    swizzled_block_2d(tile, group);
+    const int X0 = (tile % tiles_x) * kRemapTileW, Y0 = (tile / tiles_x) * kRemapTileH;
+    // lane = column, so one tap read of a wave is ~64 consecutive LDS bytes
+    // of (mostly) one box row: no bank conflicts.  Each thread owns 4 rows of
+    // its column; a quad of lanes transposes its 4x4 bytes before storing.
+    const int x = X0 + (t & 63), y0 = Y0 + (t >> 6) * 4;
+    const RemapBox B = boxes[tile];
+    const int img0 = group * fpb;
+    const int img1 = min(n_images, img0 + fpb);
     int sx[4], sy[4], f[4];
-    if (VEC && np == 4) {
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        const size_t p = (size_t)y * W + x;
-        const u32x4 m = *as_global((const u32x4 *)(map1 + 2 * p));
-        const u32x2 g = *as_global((const u32x2 *)(map2 + p));
-        const uint32_t mm[4] = {m.x, m.y, m.z, m.w}, gg[2] = {g.x, g.y};
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            sx[k] = (int16_t)(mm[k] & 0xffff);
-            sy[k] = (int16_t)(mm[k] >> 16);
-            f[k] = (gg[k >> 1] >> (16 * (k & 1))) & 0xffff;
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const size_t p = k < np ? (size_t)y * W + x + k : 0;
-            sx[k] = k < np ? map1[2 * p] : -8;  // past the image edge: no taps
-            sy[k] = k < np ? map1[2 * p + 1] : -8;
-            f[k] = map2[p];
-        }
+    for (int k = 0; k < 4; k++) {
+        const bool on = x < W && y0 + k < H;
+        const size_t p = on ? (size_t)(y0 + k) * W + x : 0;
+        const uint32_t m = *as_global((const uint32_t *)(map1 + 2 * p));
+        sx[k] = on ? (int)(int16_t)(m & 0xffff) : -8;  // off the image: no taps
+        sy[k] = on ? (int)(int16_t)(m >> 16) : -8;
+        f[k] = map2[p];
     }
-    if (B.h < 0) {  // box too large for LDS: gather from global memory
-        for (int im = img0; im < img1; im++) {
-            const uint8_t *S = src + (size_t)im * src_pitch;
-            uint8_t *D = dst + (size_t)im * dst_pitch + (size_t)y * dstride + x;
-            for (int k = 0; k < np; k++) D[k] = (uint8_t)remap_px(S, W, H, sstride, sx[k], sy[k], f[k]);
-        }
-        return;
-    }
-    // staging: dword i = t + 256 j of the box (row r, byte column c)
+    if (B.h < 0) return;  // box too large for LDS: k_remap_gather's tile
+    // staging: dword i = t + 256 j of the box (row r, byte column c), as a
+    // byte offset into the frame; dwords past the box get an offset beyond
+    // the buffer's range, which the hardware turns into a 0 load
     const int bw = max(B.w, 4), bh = max(B.h, 1);
     const int nd = (B.w * B.h) >> 2, dpr = bw >> 2;
-    uint32_t goff[DW];
-    int gcol[DW];
-    bool gon[DW];
+    const uint32_t src_bytes = (uint32_t)((H - 1) * sstride + W), dst_bytes = (uint32_t)((H - 1) * dstride + W);
+    uint32_t boff[DW];
 #pragma unroll
     for (int j = 0; j < DW; j++) {
         const int i = t + 256 * j;
         const int r = i / dpr, c = 4 * (i - r * dpr);
-        goff[j] = (uint32_t)(r * sstride + c);
-        gcol[j] = B.x0 + c;
-        gon[j] = i < nd;
+        boff[j] = i < nd ? (uint32_t)((B.y0 + r) * sstride + B.x0 + c) : kOutOfRange;
     }
+    // after the quad transpose, lane q of a quad holds row y0 + q, columns
+    // xq .. xq + 3; a dword store when all 4 are on the image (and VEC)
+    const int q4 = t & 3, xq = x - q4, yq = y0 + q4;
+    const int nq = yq < H ? max(0, min(4, W - xq)) : 0;
+    const bool dvec = VEC && nq == 4;
+    const uint32_t doff = (uint32_t)(yq * dstride + xq);
+    // v_perm selectors of the two transpose steps (see remap_quad_transpose)
+    const uint32_t sel1 = (q4 & 1) ? 0x07030501u : 0x02060004u;
+    const uint32_t sel2 = (q4 & 2) ? 0x07060302u : 0x01000504u;
     // taps: (sum w' v + 2^9) >> 10 with w' = (32 - t)(32 - t') is OpenCV's
     // (sum w v + 2^14) >> 15 for its 15-bit table w = 32 w'
     uint32_t a[4][4], w[4][4];
@@ -215,51 +227,89 @@ __global__ __launch_bounds__(256) void k_remap_tiles(const uint8_t *__restrict__
         a[k][0] = cy0 + cx0; a[k][1] = cy0 + cx1; a[k][2] = cy1 + cx0; a[k][3] = cy1 + cx1;
         w[k][0] = wy0 * wx0; w[k][1] = wy0 * wx1; w[k][2] = wy1 * wx0; w[k][3] = wy1 * wx1;
     }
-    const uint8_t *S0 = src + (size_t)B.y0 * sstride + B.x0;
-    uint8_t *D0 = dst + (size_t)y * dstride + x;
     for (int g0 = img0; g0 < img1; g0 += G) {
         const int ng = min(G, img1 - g0);
         uint32_t pf[G][DW];
 #pragma unroll
         for (int q = 0; q < G; q++) {
-            const uint8_t *S = S0 + (size_t)(g0 + q) * src_pitch;
+            if (q >= ng) break;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(src + (size_t)(g0 + q) * src_pitch), 0, src_bytes,
+                                                  kRsrcFlags);
 #pragma unroll
             for (int j = 0; j < DW; j++) {
-                pf[q][j] = 0;
-                if (q < ng && gon[j]) {
-                    if (VEC) {
-                        pf[q][j] = *as_global((const uint32_t *)(S + goff[j]));
-                    } else {  // bytes; columns past the image edge read 0 (their weights are 0)
-                        for (int b = 0; b < 4; b++)
-                            if (gcol[j] + b < W) pf[q][j] |= (uint32_t)*as_global(S + goff[j] + b) << (8 * b);
-                    }
+                if (VEC) {
+                    pf[q][j] = __builtin_amdgcn_raw_buffer_load_b32(rs, boff[j], 0, 0);
+                } else {  // bytes: columns past the row end read the next row or 0; their weights are 0
+                    pf[q][j] = 0;
+                    for (int b = 0; b < 4; b++)
+                        pf[q][j] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, boff[j] + b, 0, 0) << (8 * b);
                 }
             }
         }
         if (g0 != img0) __syncthreads();  // the previous group's taps are read
 #pragma unroll
-        for (int q = 0; q < G; q++)
+        for (int q = 0; q < G; q++) {
+            if (q >= ng) break;
 #pragma unroll
             for (int j = 0; j < DW; j++)
-                if (gon[j]) *(uint32_t *)(s_box + q * kBox + 4 * (t + 256 * j)) = pf[q][j];
+                if (j * 256 < kBox / 4) *(uint32_t *)(s_box + q * kBox + 4 * (t + 256 * j)) = pf[q][j];
+        }
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < G; q++) {
             if (q >= ng) break;
             const uint8_t *L = s_box + q * kBox;
+            const __amdgpu_buffer_rsrc_t rd =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(dst + (size_t)(g0 + q) * dst_pitch), 0, dst_bytes,
+                                                  kRsrcFlags);
+            // every tap address is inside the box (off-image taps have weight 0),
+            // so all 16 reads issue back to back
             uint32_t out = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint32_t v = w[k][0] * L[a[k][0]] + w[k][1] * L[a[k][1]] + w[k][2] * L[a[k][2]] +
-                                   w[k][3] * L[a[k][3]];
-                out |= ((v + 512) >> 10) << (8 * k);
+                const uint32_t v = __umul24(w[k][0], L[a[k][0]]) + __umul24(w[k][1], L[a[k][1]]) +
+                                   __umul24(w[k][2], L[a[k][2]]) + __umul24(w[k][3], L[a[k][3]]) + 512;
+                out |= (v >> 10) << (8 * k);
             }
-            uint8_t *D = D0 + (size_t)(g0 + q) * dst_pitch;
-            if (VEC && np == 4)
-                *(uint32_t *)D = out;
-            else
-                for (int k = 0; k < np; k++) D[k] = (uint8_t)(out >> (8 * k));
+            out = remap_quad_transpose(out, sel1, sel2);
+            if (dvec) {
+                __builtin_amdgcn_raw_buffer_store_b32(out, rd, doff, 0, 0);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(out >> (8 * k)), rd,
+                                                         k < nq ? doff + k : kOutOfRange, 0, 0);
+            }
         }
+    }
+}
+
+// Tiles whose source box exceeds kRemapMaxBox (extreme distortion only):
+// plain per-pixel gathers from global memory.  A separate kernel so that its
+// registers do not limit the occupancy of k_remap_tiles.
+__global__ __launch_bounds__(256) void k_remap_gather(const uint8_t *__restrict__ src, size_t src_pitch, int W, int H,
+                                                      int sstride, const int16_t *__restrict__ map1,
+                                                      const uint16_t *__restrict__ map2,
+                                                      const RemapBox *__restrict__ boxes, int tiles_x,
+                                                      uint8_t *__restrict__ dst, size_t dst_pitch, int dstride,
+                                                      int n_images, int fpb) {
+    const int tile = blockIdx.x;
+    if (boxes[tile].h >= 0) return;
+    const int t = threadIdx.x;
+    const int xb = (tile % tiles_x) * kRemapTileW + (t % kRemapLanesX) * 4;
+    const int y = (tile / tiles_x) * kRemapTileH + t / kRemapLanesX;
+    const int img0 = blockIdx.y * fpb;
+    const int img1 = min(n_images, img0 + fpb);
+    if (y >= H) return;
+    for (int k = 0; k < 4; k++) {
+        const int x = xb + k;
+        if (x >= W) break;
+        const size_t p = (size_t)y * W + x;
+        const int sx = map1[2 * p], sy = map1[2 * p + 1], f = map2[p];
+        for (int im = img0; im < img1; im++)
+            dst[(size_t)im * dst_pitch + (size_t)y * dstride + x] =
+                (uint8_t)remap_px(src + (size_t)im * src_pitch, W, H, sstride, sx, sy, f);
     }
 }
 
@@ -303,18 +353,22 @@ hipError_t launch_remap_boxes(int W, int H, const int16_t *map1, void *boxes, hi
 }
 
 hipError_t launch_remap_linear(const uint8_t *src, size_t src_pitch, int W, int H, int sstride, const int16_t *map1,
-                               const uint16_t *map2, const void *boxes, int max_box, uint8_t *dst, size_t dst_pitch,
-                               int dstride, int n_images, hipStream_t st) {
+                               const uint16_t *map2, const void *boxes, int max_box, bool any_large, uint8_t *dst,
+                               size_t dst_pitch, int dstride, int n_images, hipStream_t st) {
     if (n_images <= 0) return hipSuccess;
+    // frames are addressed with 32-bit buffer offsets
+    if ((size_t)(H - 1) * sstride + W >= kOutOfRange || (size_t)(H - 1) * dstride + W >= kOutOfRange)
+        return hipErrorInvalidValue;
     const int tiles_x = (W + kRemapTileW - 1) / kRemapTileW;
-    const dim3 grid(remap_tiles(W, H), (n_images + kRemapFramesPerBlock - 1) / kRemapFramesPerBlock);
+    const int fpb = kRemapFramesPerBlock;
+    const dim3 grid(remap_tiles(W, H), (n_images + fpb - 1) / fpb);
     const bool multi = n_images > 1;
     const bool vec = W % 4 == 0 && sstride % 4 == 0 && dstride % 4 == 0 && (!multi || src_pitch % 4 == 0) &&
                      (!multi || dst_pitch % 4 == 0) && ((uintptr_t)src & 3) == 0 && ((uintptr_t)dst & 3) == 0;
     const RemapBox *bx = (const RemapBox *)boxes;
 #define YGZ_REMAP(V, D)                                                                                           \
     hipLaunchKernelGGL((k_remap_tiles<V, D>), grid, dim3(256), 0, st, src, src_pitch, W, H, sstride, map1, map2, bx, \
-                       tiles_x, dst, dst_pitch, dstride, n_images)
+                       tiles_x, dst, dst_pitch, dstride, n_images, fpb)
     // max_box: the largest LDS-staged box (bytes); 1 or 2 KiB boxes stage 8 frames at once, larger ones 4
     if (vec) {
         if (max_box <= 2048) YGZ_REMAP(true, 2); else YGZ_REMAP(true, 4);
@@ -322,6 +376,9 @@ hipError_t launch_remap_linear(const uint8_t *src, size_t src_pitch, int W, int 
         if (max_box <= 2048) YGZ_REMAP(false, 2); else YGZ_REMAP(false, 4);
     }
 #undef YGZ_REMAP
+    if (any_large)
+        hipLaunchKernelGGL(k_remap_gather, grid, dim3(256), 0, st, src, src_pitch, W, H, sstride, map1, map2, bx,
+                           tiles_x, dst, dst_pitch, dstride, n_images, fpb);
     return hipGetLastError();
 }
 

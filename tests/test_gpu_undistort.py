@@ -35,8 +35,9 @@ def test_remap_batch_bitexact(gpu, name):
     src = torch.from_numpy(frames).cuda()
     pitch = W * H + 64  # padded destination pitch
     dst = torch.full((n, pitch), 7, dtype=torch.uint8, device="cuda")
-    und.apply_device(src.data_ptr(), W * H, W, dst.data_ptr(), pitch, W, n,
-                     torch.cuda.current_stream().cuda_stream)
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    und.apply_device(src.data_ptr(), W * H, W, dst.data_ptr(), pitch, W, n, st.cuda_stream)
     torch.cuda.synchronize()
     out = dst.cpu().numpy()
     for i in range(n):
@@ -108,9 +109,10 @@ def test_batch_undistort_device_then_extract(gpu):
     b = gpu.Batch((nf, sf, nl, ini, mn, 0), 0, W, H, 9)
     frames = np.stack([S.frame(10 + s, W, H) for s in range(9)])
     raw = torch.from_numpy(frames).cuda()
-    st = torch.cuda.current_stream().cuda_stream
-    b.undistort_device(und, raw.data_ptr(), W * H, 9, st)
-    b.extract(9, st)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    b.undistort_device(und, raw.data_ptr(), W * H, 9, s.cuda_stream)
+    b.extract(9, s.cuda_stream)
     torch.cuda.synchronize()
     b.check()
     orc = O.OrbOracle(nf, sf, nl, ini, mn)

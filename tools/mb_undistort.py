@@ -16,7 +16,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 und = ygzfe.Undistort(cam, dist, W, H)
 src = torch.from_numpy(np.stack([ygzfe.synth_texture(s % 16, W, H) for s in range(n)])).cuda()
 dst = torch.empty_like(src)
-st = torch.cuda.current_stream()
+st = torch.cuda.Stream()
+torch.cuda.set_stream(st)
 for _ in range(5):
     und.apply_device(src.data_ptr(), W * H, W, dst.data_ptr(), W * H, W, n, st.cuda_stream)
 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -27,5 +28,6 @@ for _ in range(reps):
 b.record(st)
 torch.cuda.synchronize()
 ms = a.elapsed_time(b) / reps
+assert st.cuda_stream != 0
 alg = n * W * H * 2 + W * H * 6  # read + write each frame, the map once
 print(f"remap {n} frames {W}x{H}: {ms*1e3:.1f} us/launch, {n/ms*1e3:.0f} frames/s, {alg/ms/1e6:.0f} GB/s alg")
