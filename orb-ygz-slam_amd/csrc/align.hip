@@ -56,6 +56,18 @@ __device__ void se3_mul(const SE3 &a, const SE3 &b, SE3 &out) {
     out.t[0] = t0; out.t[1] = t1; out.t[2] = t2;
 }
 
+// se3_mul with the quaternion normalised by one rsqrt (the solver wave's
+// pose update; 1-ulp differences are inside the 1e-4 pose parity)
+__device__ __forceinline__ void se3_mul_fast(const SE3 &a, const SE3 &b, SE3 &out) {
+    float r[3], q[4];
+    quat_rotate(a.q, b.t, r);
+    const float t0 = a.t[0] + r[0], t1 = a.t[1] + r[1], t2 = a.t[2] + r[2];
+    quat_mul(a.q, b.q, q);
+    const float inv = __builtin_amdgcn_rsqf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int i = 0; i < 4; i++) out.q[i] = q[i] * inv;
+    out.t[0] = t0; out.t[1] = t1; out.t[2] = t2;
+}
+
 __device__ void quat_to_mat(const float q[4], float R[9]) {
     const float tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
     const float twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
@@ -116,12 +128,13 @@ __device__ void se3_exp_wave(const float a[6], SE3 &out) {
     const float s_th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sn), 1));
     const float c_th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cs), 1));
     float imag, real;
+    const float inv_theta = __builtin_amdgcn_rcpf(theta);  // 1 ulp: pose parity is 1e-4
     if (theta < eps) {
         const float theta_po4 = theta_sq * theta_sq;
         imag = 0.5f - (float)(1.0 / 48.0) * theta_sq + (float)(1.0 / 3840.0) * theta_po4;
         real = 1.f - 0.5f * theta_sq + (float)(1.0 / 384.0) * theta_po4;
     } else {
-        imag = s_half / theta;
+        imag = s_half * inv_theta;
         real = c_half;
     }
     const float q[4] = {imag * w0, imag * w1, imag * w2, real};
@@ -134,8 +147,9 @@ __device__ void se3_exp_wave(const float a[6], SE3 &out) {
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++)
                 O2[i * 3 + j] = O[i * 3 + 0] * O[0 * 3 + j] + O[i * 3 + 1] * O[1 * 3 + j] + O[i * 3 + 2] * O[2 * 3 + j];
-        const float c1 = (1.f - c_th) / theta_sq;
-        const float c2 = (theta - s_th) / (theta_sq * theta);
+        const float inv_sq = inv_theta * inv_theta;
+        const float c1 = (1.f - c_th) * inv_sq;
+        const float c2 = (theta - s_th) * (inv_sq * inv_theta);
         for (int i = 0; i < 9; i++) V[i] = ((i % 4 == 0) ? 1.f : 0.f) + c1 * O[i] + c2 * O2[i];
     }
     for (int i = 0; i < 3; i++) out.t[i] = V[i * 3 + 0] * a[0] + V[i * 3 + 1] * a[1] + V[i * 3 + 2] * a[2];
@@ -196,6 +210,114 @@ __device__ void ldlt_solve6(const float Hin[36], const float b[6], float x[6]) {
         y[i] = s;
     }
     for (int i = 0; i < 6; i++) x[perm[i]] = y[i];
+}
+
+// The pivoted LDLT for wave-uniform systems: the pivot index is made
+// provably uniform (readfirstlane), so the row/column exchange is a scalar
+// branch to one straight-line case with constant indices instead of selects
+// over every candidate pivot; columns are scaled by one reciprocal per pivot.
+// Same pivot order and zero-pivot rules as ldlt_solve6 (the division by a
+// reciprocal product rounds differently: pose parity is 1e-4).
+template <int K, int P>
+__device__ __forceinline__ void ldlt6_exchange(float (&A)[36], int (&perm)[6]) {
+#pragma unroll
+    for (int j = 0; j < K; j++) { const float t = A[K * 6 + j]; A[K * 6 + j] = A[P * 6 + j]; A[P * 6 + j] = t; }
+#pragma unroll
+    for (int i = P + 1; i < 6; i++) { const float t = A[i * 6 + K]; A[i * 6 + K] = A[i * 6 + P]; A[i * 6 + P] = t; }
+    { const float t = A[K * 6 + K]; A[K * 6 + K] = A[P * 6 + P]; A[P * 6 + P] = t; }
+#pragma unroll
+    for (int i = K + 1; i < P; i++) { const float t = A[i * 6 + K]; A[i * 6 + K] = A[P * 6 + i]; A[P * 6 + i] = t; }
+    const int t = perm[K]; perm[K] = perm[P]; perm[P] = t;
+}
+
+template <int K>
+__device__ __forceinline__ void ldlt6_pivot(float (&A)[36], int (&perm)[6], int piv) {
+    if constexpr (K + 1 < 6) { if (piv == K + 1) { ldlt6_exchange<K, K + 1>(A, perm); return; } }
+    if constexpr (K + 2 < 6) { if (piv == K + 2) { ldlt6_exchange<K, K + 2>(A, perm); return; } }
+    if constexpr (K + 3 < 6) { if (piv == K + 3) { ldlt6_exchange<K, K + 3>(A, perm); return; } }
+    if constexpr (K + 4 < 6) { if (piv == K + 4) { ldlt6_exchange<K, K + 4>(A, perm); return; } }
+    if constexpr (K + 5 < 6) { if (piv == K + 5) { ldlt6_exchange<K, K + 5>(A, perm); return; } }
+}
+
+template <int K>
+__device__ __forceinline__ bool ldlt6_step(float (&A)[36], int (&perm)[6]) {
+    int piv = K;
+    float big = fabsf(A[K * 6 + K]);
+#pragma unroll
+    for (int i = K + 1; i < 6; i++)
+        if (fabsf(A[i * 6 + i]) > big) { big = fabsf(A[i * 6 + i]); piv = i; }
+    piv = __builtin_amdgcn_readfirstlane(piv);
+    if (piv != K) ldlt6_pivot<K>(A, perm, piv);
+    float tmp[6];
+#pragma unroll
+    for (int j = 0; j < K; j++) tmp[j] = A[j * 6 + j] * A[K * 6 + j];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < K; j++) s += A[K * 6 + j] * tmp[j];
+    A[K * 6 + K] -= s;
+#pragma unroll
+    for (int i = K + 1; i < 6; i++) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < K; j++) t += A[i * 6 + j] * tmp[j];
+        A[i * 6 + K] -= t;
+    }
+    const float akk = A[K * 6 + K];
+    if (K == 0 && akk == 0.f) return false;  // Eigen: a zero first pivot ends the factorization
+    if (akk != 0.f) {
+        const float r = __builtin_amdgcn_rcpf(akk);
+#pragma unroll
+        for (int i = K + 1; i < 6; i++) A[i * 6 + K] *= r;
+    }
+    return true;
+}
+
+__device__ __forceinline__ void ldlt_solve6_uni(float (&A)[36], const float b[6], float x[6]) {
+    int perm[6] = {0, 1, 2, 3, 4, 5};
+    if (!ldlt6_step<0>(A, perm)) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) perm[i] = i;
+    } else {
+        ldlt6_step<1>(A, perm);
+        ldlt6_step<2>(A, perm);
+        ldlt6_step<3>(A, perm);
+        ldlt6_step<4>(A, perm);
+        ldlt6_step<5>(A, perm);
+    }
+    float y[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        float v = 0.f;
+#pragma unroll
+        for (int j = 0; j < 6; j++) v = perm[i] == j ? b[j] : v;
+        y[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        float s = y[i];
+#pragma unroll
+        for (int j = 0; j < i; j++) s -= A[i * 6 + j] * y[j];
+        y[i] = s;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        const float d = A[i * 6 + i];
+        y[i] = fabsf(d) > 1.17549435e-38f ? y[i] * __builtin_amdgcn_rcpf(d) : 0.f;
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+        float s = y[i];
+#pragma unroll
+        for (int j = i + 1; j < 6; j++) s -= A[j * 6 + i] * y[j];
+        y[i] = s;
+    }
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        float v = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; i++) v = perm[i] == j ? y[i] : v;
+        x[j] = v;
+    }
 }
 
 // The same LDLT with every array index a compile-time constant (pivot swaps
@@ -315,6 +437,19 @@ __device__ __forceinline__ void load_row(const uint8_t *p, float (&out)[N]) {
     }
 }
 
+template <int N>
+__device__ __forceinline__ void load_row_packed(const uint8_t *p, uint32_t (&out)[(N + 3) / 4]) {
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(p - sh));
+    constexpr int ND = (N + 3 + 3) / 4;
+    uint32_t d[ND + 1];
+#pragma unroll
+    for (int i = 0; i < ND; i++) d[i] = q[i];
+    d[ND] = 0;
+#pragma unroll
+    for (int w = 0; w < (N + 3) / 4; w++) out[w] = __builtin_amdgcn_alignbyte(d[w + 1], d[w], sh);
+}
+
 // ------------------------------------------------------------------ sparse align
 constexpr int kPA = 16;    // patch_area_
 constexpr int kRed = 29;   // 21 (upper H) + 6 (Jres) + chi2 + count
@@ -329,6 +464,14 @@ __device__ __forceinline__ void jacob_xyz2cam_f(float X, float Y, float Z, float
     fj[4] = (float)(-(1.0 + (double)(X * fj[2]))); fj[5] = Y * z_inv;
     fj[6] = 0.f; fj[7] = -z_inv; fj[8] = Y * z_inv_2; fj[9] = (float)(1.0 + (double)(Y * fj[8]));
     fj[10] = -fj[3]; fj[11] = -X * z_inv;
+}
+
+// The Jacobian recomputed where it is used: without the opaque copy the
+// compiler hoists the 12 (loop-invariant) entries and their products out of
+// every level and iteration loop and spills them across the whole kernel.
+__device__ __forceinline__ void jacob_xyz2cam_fresh(float X, float Y, float Z, float fj[12]) {
+    asm volatile("" : "+v"(X), "+v"(Y), "+v"(Z));
+    jacob_xyz2cam_f(X, Y, Z, fj);
 }
 
 // Generic path (any n): (feature, pixel) terms strided over the workgroup,
@@ -586,6 +729,51 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
     return v;
 }
 
+// Transposing wave reductions (every lane active).  A step pairs two values
+// and two lane sets: the lanes of one set keep the sum of value x over both
+// sets, the other lanes the sum of value y, so each step halves the values a
+// lane carries.  Lanes 0-31 | 32-63 by v_permlane32_swap, rows 0,2 | 1,3 by
+// v_permlane16_swap, then DPP row_mirror (i <-> 15-i), row_half_mirror
+// (i <-> 7-i) and quad_perm [2,3,0,1] inside the rows.
+__device__ __forceinline__ float pair_pl32(float x, float y) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float pair_pl16(float x, float y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+template <int CTRL, int BIT>
+__device__ __forceinline__ float pair_dpp(float x, float y, int lane) {
+    const bool hi = lane & BIT;
+    const float keep = hi ? y : x, send = hi ? x : y;
+    return keep + YGZ_DPP(send, CTRL, 0xF);
+}
+// 32 values -> lane l holds the wave total of value l >> 1
+__device__ __forceinline__ float wave_reduce32(float (&v)[32], int lane) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = pair_pl32(v[i], v[16 + i]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = pair_pl16(v[i], v[8 + i]);
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = pair_dpp<0x140, 8>(v[i], v[4 + i], lane);
+#pragma unroll
+    for (int i = 0; i < 2; i++) v[i] = pair_dpp<0x141, 4>(v[i], v[2 + i], lane);
+    const float t = pair_dpp<0x4E, 2>(v[0], v[1], lane);
+    return t + YGZ_DPP(t, 0xB1, 0xF);
+}
+// 8 values -> lane l holds the wave total of value (l >> 3) & 7
+__device__ __forceinline__ float wave_reduce8(float (&v)[8], int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = pair_pl32(v[i], v[4 + i]);
+#pragma unroll
+    for (int i = 0; i < 2; i++) v[i] = pair_pl16(v[i], v[2 + i]);
+    float t = pair_dpp<0x140, 8>(v[0], v[1], lane);
+    t += YGZ_DPP(t, 0x141, 0xF);
+    t += YGZ_DPP(t, 0x4E, 0xF);
+    return t + YGZ_DPP(t, 0xB1, 0xF);
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_camera cam,
                                                          const AlignJob *__restrict__ jobs,
@@ -593,7 +781,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                                                          ygzfe_align_result *__restrict__ out) {
     constexpr int NW = NT / 64;
     constexpr int NF = NT - 64;  // features are owned by waves 1..NW-1; wave 0 is the solver
-    if (jobs[blockIdx.x].n > NF) {  // more features than feature threads: generic path
+    if (jobs[blockIdx.x].n > NF) {  // more features than feature threads: generic path (not inlined)
         sparse_align_generic<NT>(lv, cam, jobs[blockIdx.x], scratch + blockIdx.x * scratch_per_job, out + blockIdx.x);
         return;
     }
@@ -672,7 +860,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                         s_nmeas = nmeas;
                     }
                     YGZ_STAMP(7);
-                    ldlt_solve6_reg(Hm, b, x);
+                    ldlt_solve6_uni(Hm, b, x);
                     YGZ_STAMP(8);
                     const bool stop = s_stop || isnan(x[0]);
                     const bool rollback = (it > 0 && (double)new_chi2 > 1.2 * (double)s_chi2) || stop;
@@ -689,7 +877,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                         SE3 E, Tn;
                         se3_exp_wave(mx, E);
                         const SE3 Tc = s_T;
-                        se3_mul(Tc, E, Tn);
+                        se3_mul_fast(Tc, E, Tn);
                         YGZ_STAMP(10);
                         float nm = -1.f;
 #pragma unroll
@@ -751,28 +939,38 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                 const float su = u_ref - ui, sv = v_ref - vi;
                 const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
                 const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
-                // 7x7 window: rows vi-3..vi+3, cols ui-3..ui+3; R[y][x] = ref(vi-3+y, ui-3+x)
+                // 7x7 window: rows vi-3..vi+3, cols ui-3..ui+3; R[y][x] = ref(vi-3+y, ui-3+x),
+                // kept as packed bytes (all 7 rows in flight at once)
                 const uint8_t *base = rimg + (size_t)(vi - 3) * W + (ui - 3);
-                float rm[7], r0[7], r1[7], r2[7];
-                load_row<7>(base, rm);
-                load_row<7>(base + W, r0);
-                load_row<7>(base + 2 * W, r1);
+                uint32_t R[7][2];
+#pragma unroll
+                for (int y = 0; y < 7; y++) load_row_packed<7>(base + (size_t)y * W, R[y]);
+                auto rpx = [&](int y, int x) -> float { return (float)((R[y][x >> 2] >> (8 * (x & 3))) & 0xFFu); };
+                // J[y][x]: the bilinear sample at (x + su, y + sv) of the window; the
+                // reference's patch and central differences are entries of J:
+                // patch = J[py+1][px+1], gx = (J[py+1][px+2] - J[py+1][px]) / 2,
+                // gy = (J[py+2][px+1] - J[py][px+1]) / 2 -- the same expressions
+                // as SparseImageAlign.cc:98-125, each evaluated once
+                float J0[6], J1[6], J2[6];
+                auto jrow = [&](int y, float (&o)[6]) {
+#pragma unroll
+                    for (int x = 0; x < 6; x++)
+                        o[x] = wtl * rpx(y, x) + wtr * rpx(y, x + 1) + wbl * rpx(y + 1, x) + wbr * rpx(y + 1, x + 1);
+                };
+                jrow(0, J0);
+                jrow(1, J1);
 #pragma unroll
                 for (int py = 0; py < 4; py++) {
-                    load_row<7>(base + (size_t)(py + 3) * W, r2);
-                    // pixel (py, px): p[0] = R[py+1][px+1]; rows: m = py, a = py+1, b = py+2, c = py+3
+                    jrow(py + 2, J2);  // rows py, py+1, py+2 in J0, J1, J2
 #pragma unroll
                     for (int px = 0; px < 4; px++) {
-                        const int pi = py * 4 + px, c = px + 1;
-                        const float a0 = r0[c - 1], a1 = r0[c], a2 = r0[c + 1], a3 = r0[c + 2];
-                        const float b0 = r1[c - 1], b1 = r1[c], b2 = r1[c + 1], b3 = r1[c + 2];
-                        const float c1 = r2[c], c2 = r2[c + 1], m1 = rm[c], m2 = rm[c + 1];
-                        s_patch[pi][f] = wtl * a1 + wtr * a2 + wbl * b1 + wbr * b2;
-                        gx[pi] = 0.5f * ((wtl * a2 + wtr * a3 + wbl * b2 + wbr * b3) - (wtl * a0 + wtr * a1 + wbl * b0 + wbr * b1));
-                        gy[pi] = 0.5f * ((wtl * b1 + wtr * b2 + wbl * c1 + wbr * c2) - (wtl * m1 + wtr * m2 + wbl * a1 + wbr * a2));
+                        const int pi = py * 4 + px;
+                        s_patch[pi][f] = J1[px + 1];
+                        gx[pi] = 0.5f * (J1[px + 2] - J1[px]);
+                        gy[pi] = 0.5f * (J2[px + 1] - J0[px + 1]);
                     }
 #pragma unroll
-                    for (int k = 0; k < 7; k++) { rm[k] = r0[k]; r0[k] = r1[k]; r1[k] = r2[k]; }
+                    for (int x = 0; x < 6; x++) { J0[x] = J1[x]; J1[x] = J2[x]; }
                 }
             }
         }
@@ -786,7 +984,8 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
             for (int p = 0; p < 16; p++) { Sxx += gx[p] * gx[p]; Sxy += gx[p] * gy[p]; Syy += gy[p] * gy[p]; }
             const float fs2 = fs * fs;
             float fj[12];
-            jacob_xyz2cam_f(X, Y, Z, fj);
+            jacob_xyz2cam_fresh(X, Y, Z, fj);
+            float hv[32];
             int m = 0;
 #pragma unroll
             for (int r = 0; r < 6; r++)
@@ -794,12 +993,14 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                 for (int c = r; c < 6; c++) {
                     const float hrc = fj[r] * fj[c] * Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * Sxy +
                                       fj[6 + r] * fj[6 + c] * Syy;
-                    const float hv = (own && vis) ? hrc * fs2 : 0.f;
-                    if (own) s_Hf[m][f] = hv;
-                    const float t = wave_sum_dpp(hv);
-                    if (lane == 63) s_part[wave][m] = t;
+                    hv[m] = (own && vis) ? hrc * fs2 : 0.f;
+                    if (own) s_Hf[m][f] = hv[m];
                     m++;
                 }
+#pragma unroll
+            for (int k = 21; k < 32; k++) hv[k] = 0.f;
+            const float t = wave_reduce32(hv, lane);
+            if ((lane & 1) == 0 && (lane >> 1) < 21) s_part[wave][lane >> 1] = t;
         }
         __syncthreads();  // L0
         __syncthreads();  // L0b
@@ -842,17 +1043,16 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                         for (int c = 0; c < 5; c++) r0[c] = r1[c];
                     }
                     float fj[12];
-                    jacob_xyz2cam_f(X, Y, Z, fj);
+                    jacob_xyz2cam_fresh(X, Y, Z, fj);
 #pragma unroll
                     for (int r = 0; r < 6; r++) acc[r] = -(fj[r] * Sx + fj[6 + r] * Sy) * fs;
                     acc[6] = chi2;
                     acc[7] = 16.f;
                 }
             }
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const float t = wave_sum_dpp(acc[k]);
-                if (lane == 63) s_part[wave][k] = t;
+            {
+                const float t = wave_reduce8(acc, lane);
+                if ((lane & 7) == 0) s_part[wave][lane >> 3] = t;
             }
             __syncthreads();  // A
             __syncthreads();  // B

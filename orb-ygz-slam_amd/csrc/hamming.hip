@@ -4,91 +4,140 @@
 // Dense best/second-best: the inner candidate loops of SearchByProjection /
 // SearchForInitialization / SearchByBoW (ORBmatcher.cc:43-126,375-478,1218-1350)
 // keep `dist < bestDist` (first index wins on ties) and the second best.
-// A query descriptor lives in 8 VGPRs of its lane; train descriptors are
-// staged through LDS in 1024-row tiles (32 KiB) shared by the workgroup and
-// read as broadcasts, 4 rows per step.
+// The dense search runs on the matrix cores (int8 MFMA, below); the
+// candidate-list (CSR) distances are plain XOR + popcount per lane.
 #include "common.hpp"
 
 namespace ygzfe {
 
-constexpr int kHamTile = 1024;
+// ---------------------------------------------------------------------------
+// Dense best / second best on the matrix cores.  For 256-bit descriptors
+//   ham(q, t) = popc(t) - 2 popc(t & q) + popc(q) = sum_k t_k (1 - 2 q_k) + popc(q),
+// so with the train bits as 0/1 bytes (A) and the query bits as +1/-1 bytes
+// (B), one v_mfma_i32_32x32x32_i8 chain over K = 256 gives D[t][q] =
+// ham(q, t) - popc(q) for a 32 x 32 tile, exactly (integer arithmetic).
+// Lane l of a wave owns query column l & 31; its 16 accumulator registers are
+// train rows (r & 3) + 8 (r >> 2) + 4 (l >> 5) of the tile.  The K order
+// inside an operand is free as long as A and B agree: k-step s, lane half h
+// carries descriptor bits [32 s + 16 h, 32 s + 16 h + 16).
+//
+// A workgroup serves 128 queries (4 waves x 32) and streams the train set in
+// 32-row tiles; each tile is expanded to bytes once into LDS (double buffered)
+// and read by all 4 waves.  Per lane the running best / second best are keys
+//   key = ((D + 256) << 22) | train_index
+// so the smallest key is the smallest distance with the earliest index (the
+// sequential loop's `dist < bestDist`), and second = min over the other keys:
+//   k2 = min(k2, max(k1, key)); k1 = min(k1, key)       (3 VALU, no branches).
+constexpr int kHamQPB = 128;                 // queries per workgroup
+constexpr int kHamRowBytes = 256 + 16;       // expanded train row + pad (conflict-free b128 reads)
+constexpr int kHamTileBytes = 32 * kHamRowBytes;
+constexpr uint32_t kHamNone = 0xFFFFFFFFu;
+constexpr int kHamMaxTrain = 1 << 22;
 
-__device__ __forceinline__ void best2_update(int d, int j, int &b1, int &b2, int &bi) {
-    if (d < b1) { b2 = b1; b1 = d; bi = j; }
-    else if (d < b2) b2 = d;
+typedef int ham_v4i __attribute__((ext_vector_type(4)));
+typedef int ham_v16i __attribute__((ext_vector_type(16)));
+
+// 4 bits -> 4 bytes of 0 / 1 (bit b -> byte b; the shifted copies of the
+// nibble never overlap, so the product has no carries)
+__device__ __forceinline__ uint32_t nib_bytes(uint32_t bits16, int m) {
+    return (__umul24((bits16 >> (4 * m)) & 0xFu, 0x00204081u)) & 0x01010101u;
 }
 
-__device__ __forceinline__ int ham256(const uint32_t a[8], const uint4 &v0, const uint4 &v1) {
-    int d = __popc(a[0] ^ v0.x);
-    d = __popc(a[1] ^ v0.y) + d;
-    d = __popc(a[2] ^ v0.z) + d;
-    d = __popc(a[3] ^ v0.w) + d;
-    d = __popc(a[4] ^ v1.x) + d;
-    d = __popc(a[5] ^ v1.y) + d;
-    d = __popc(a[6] ^ v1.z) + d;
-    d = __popc(a[7] ^ v1.w) + d;
-    return d;
-}
-
-// A workgroup serves 64 queries (one per lane); its 4 waves scan the four
-// contiguous quarters of the train set (4x the waves of a query-per-thread
-// layout), then the partial results merge in train order: best = smallest b1,
-// earliest quarter on ties (so the first minimum index wins, as in the
-// sequential loop); second = min(winner's b2, the other quarters' b1) -- the
-// sequential b2 is the smallest distance over all trains but the winner.
-constexpr int kQPB = 64;
-
-__device__ void hamming_block(const uint8_t *__restrict__ q, int nq, const uint8_t *__restrict__ t, int nt,
-                              int32_t *__restrict__ bi_out, int32_t *__restrict__ bd_out,
-                              int32_t *__restrict__ sd_out, int qblock) {
-    __shared__ uint4 s_t[kHamTile * 2];
-    __shared__ int s_part[4][3][kQPB];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int qi = qblock * kQPB + lane;
-    uint32_t a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (qi < nq) {
-        const uint4 *qp = reinterpret_cast<const uint4 *>(q + (size_t)qi * 32);
-        const uint4 u0 = qp[0], u1 = qp[1];
-        a[0] = u0.x; a[1] = u0.y; a[2] = u0.z; a[3] = u0.w;
-        a[4] = u1.x; a[5] = u1.y; a[6] = u1.z; a[7] = u1.w;
+__device__ __forceinline__ void ham_expand_store(uint8_t *s_tile, int row, int s, uint32_t w) {
+    // dword s of train row `row` -> A operands of k-step s for lane halves 0 and 1
+    ham_v4i lo, hi;
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        lo[m] = (int)nib_bytes(w & 0xFFFFu, m);
+        hi[m] = (int)nib_bytes(w >> 16, m);
     }
-    int b1 = 257, b2 = 257, bi = -1;
-    for (int t0 = 0; t0 < nt; t0 += kHamTile) {
-        const int m = min(kHamTile, nt - t0);
-        __syncthreads();
-        const uint4 *tp = reinterpret_cast<const uint4 *>(t + (size_t)t0 * 32);
-        for (int i = threadIdx.x; i < m * 2; i += blockDim.x) s_t[i] = tp[i];
-        __syncthreads();
-        const int qlen = (m + 3) >> 2, jb = wave * qlen, je = min(m, jb + qlen);  // this wave's quarter
-        int j = jb;
-        for (; j + 4 <= je; j += 4) {
-            uint4 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) v[u] = s_t[2 * j + u];
-#pragma unroll
-            for (int u = 0; u < 4; u++) best2_update(ham256(a, v[2 * u], v[2 * u + 1]), t0 + j + u, b1, b2, bi);
+    ham_v4i *d = (ham_v4i *)(s_tile + row * kHamRowBytes + s * 32);
+    d[0] = lo;
+    d[1] = hi;
+}
+
+__device__ __forceinline__ void hamming_block_mfma(const uint8_t *__restrict__ q, int nq, const uint8_t *__restrict__ t, int nt,
+                                   int32_t *__restrict__ bi_out, int32_t *__restrict__ bd_out,
+                                   int32_t *__restrict__ sd_out, int qblock) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[2][kHamTileBytes];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+    const int qi = qblock * kHamQPB + wave * 32 + (lane & 31);
+    // query operands: +1 / -1 bytes of this lane's half of each descriptor dword
+    ham_v4i bq[8];
+    int pq = 0;
+    {
+        uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (qi < nq) {
+            const uint4 *qp = reinterpret_cast<const uint4 *>(q + (size_t)qi * 32);
+            const uint4 u0 = qp[0], u1 = qp[1];
+            w[0] = u0.x; w[1] = u0.y; w[2] = u0.z; w[3] = u0.w;
+            w[4] = u1.x; w[5] = u1.y; w[6] = u1.z; w[7] = u1.w;
         }
-        for (; j < je; j++) best2_update(ham256(a, s_t[2 * j], s_t[2 * j + 1]), t0 + j, b1, b2, bi);
-        // merge this tile's quarters in order into wave 0's running result
-        s_part[wave][0][lane] = b1;
-        s_part[wave][1][lane] = b2;
-        s_part[wave][2][lane] = bi;
-        __syncthreads();
-        if (wave == 0) {
 #pragma unroll
-            for (int w = 1; w < 4; w++) {
-                const int c1 = s_part[w][0][lane], c2 = s_part[w][1][lane], ci = s_part[w][2][lane];
-                if (c1 < b1) { b2 = min(b1, c2); b1 = c1; bi = ci; }
-                else b2 = min(b2, c1);
+        for (int s = 0; s < 8; s++) {
+            pq += __popc(w[s]);
+            const uint32_t half = (w[s] >> (16 * h)) & 0xFFFFu;
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                const uint32_t e = nib_bytes(half, m);         // 0 / 1 per byte
+                bq[s][m] = (int)(((e << 8) - e) | 0x01010101u);  // 0 -> +1, 1 -> -1 (0xFF)
             }
-        } else {
-            b1 = 257; b2 = 257; bi = -1;
         }
     }
-    if (wave == 0 && qi < nq) {
-        bi_out[qi] = bi;
-        bd_out[qi] = b1;
-        sd_out[qi] = b2;
+    uint32_t k1 = kHamNone, k2 = kHamNone;
+    // key of accumulator register r: (D << 22) + (256 << 22) + tile row base +
+    // this lane half's row offset 4h + the register's row offset (a constant)
+    const uint32_t lane_base = (256u << 22) + 4u * (uint32_t)h;
+    const int ntiles = (nt + 31) >> 5;
+    // staging: thread -> (row tid >> 3, dword tid & 7) of a 32-row tile
+    const int srow = tid >> 3, sdw = tid & 7;
+    auto fetch = [&](int tile) -> uint32_t {
+        const int row = tile * 32 + srow;
+        return row < nt ? reinterpret_cast<const uint32_t *>(t + (size_t)row * 32)[sdw] : 0u;
+    };
+    if (ntiles > 0) ham_expand_store(s_tile[0], srow, sdw, fetch(0));
+    __syncthreads();
+    for (int tile = 0; tile < ntiles; tile++) {
+        const uint8_t *L = s_tile[tile & 1];
+        const bool more = tile + 1 < ntiles;
+        const uint32_t nxt = more ? fetch(tile + 1) : 0u;  // in flight during the MFMAs
+        ham_v16i acc = {};
+        const uint8_t *arow = L + (lane & 31) * kHamRowBytes + h * 16;
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            const ham_v4i a = *(const ham_v4i *)(arow + s * 32);
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[s], acc, 0, 0, 0);
+        }
+        if (more) ham_expand_store(s_tile[(tile + 1) & 1], srow, sdw, nxt);
+        const uint32_t tb = (uint32_t)tile * 32, kb = lane_base + tb;
+        if (tb + 32 <= (uint32_t)nt) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const uint32_t key = ((uint32_t)acc[r] << 22) + kb + (uint32_t)((r & 3) + 8 * (r >> 2));
+                const uint32_t m = max(k1, key);
+                k1 = min(k1, key);
+                k2 = min(k2, m);
+            }
+        } else {  // partial last tile: rows past nt never win
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const uint32_t row = tb + (uint32_t)((r & 3) + 8 * (r >> 2) + 4 * h);
+                const uint32_t key =
+                    row < (uint32_t)nt ? ((uint32_t)acc[r] << 22) + kb + (uint32_t)((r & 3) + 8 * (r >> 2)) : kHamNone;
+                const uint32_t m = max(k1, key);
+                k1 = min(k1, key);
+                k2 = min(k2, m);
+            }
+        }
+        __syncthreads();  // tile + 1 staged; tile's buffer free for tile + 2
+    }
+    // merge the two lane halves (same query, disjoint rows)
+    const uint32_t o1 = (uint32_t)__shfl_xor((int)k1, 32, 64), o2 = (uint32_t)__shfl_xor((int)k2, 32, 64);
+    const uint32_t K1 = min(k1, o1), K2 = min(max(k1, o1), min(k2, o2));
+    if (h == 0 && qi < nq) {
+        bi_out[qi] = K1 == kHamNone ? -1 : (int)(K1 & (kHamMaxTrain - 1));
+        bd_out[qi] = K1 == kHamNone ? 257 : (int)(K1 >> 22) - 256 + pq;
+        sd_out[qi] = K2 == kHamNone ? 257 : (int)(K2 >> 22) - 256 + pq;
     }
 }
 
@@ -96,7 +145,7 @@ __global__ __launch_bounds__(256) void k_hamming_best2(const uint8_t *__restrict
                                                        const uint8_t *__restrict__ t, int nt,
                                                        int32_t *__restrict__ bi, int32_t *__restrict__ bd,
                                                        int32_t *__restrict__ sd) {
-    hamming_block(q, nq, t, nt, bi, bd, sd, blockIdx.x);
+    hamming_block_mfma(q, nq, t, nt, bi, bd, sd, blockIdx.x);
 }
 
 // batched: pair p matches the descriptors of frame qframe[p] against frame
@@ -111,9 +160,9 @@ __global__ __launch_bounds__(256) void k_hamming_best2_pairs(const uint8_t *__re
     const int p = blockIdx.y;
     const int qf = qframe[p], tf = tframe[p];
     const int nq = counts[qf], nt = counts[tf];
-    if ((int)(blockIdx.x * kQPB) >= nq) return;
-    hamming_block(desc + (size_t)qf * row_cap * 32, nq, desc + (size_t)tf * row_cap * 32, nt,
-                  bi + (size_t)p * row_cap, bd + (size_t)p * row_cap, sd + (size_t)p * row_cap, blockIdx.x);
+    if ((int)(blockIdx.x * kHamQPB) >= nq) return;
+    hamming_block_mfma(desc + (size_t)qf * row_cap * 32, nq, desc + (size_t)tf * row_cap * 32, nt,
+                       bi + (size_t)p * row_cap, bd + (size_t)p * row_cap, sd + (size_t)p * row_cap, blockIdx.x);
 }
 
 // CSR candidate distances: dist[k] for k in [row_ptr[i], row_ptr[i+1]) of query i.
@@ -137,7 +186,9 @@ __global__ __launch_bounds__(256) void k_hamming_csr(const uint8_t *__restrict__
 hipError_t launch_hamming_best2(const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *bi, int32_t *bd,
                                 int32_t *sd, hipStream_t st) {
     if (nq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hamming_best2, dim3((nq + kQPB - 1) / kQPB), dim3(256), 0, st, q, nq, t, nt, bi, bd, sd);
+    if (nt > kHamMaxTrain) return hipErrorInvalidValue;  // train index must fit the key's 22 bits
+    hipLaunchKernelGGL(k_hamming_best2, dim3((nq + kHamQPB - 1) / kHamQPB), dim3(256), 0, st, q, nq, t, nt, bi, bd,
+                       sd);
     return hipGetLastError();
 }
 
@@ -145,9 +196,9 @@ hipError_t launch_hamming_best2_pairs(const uint8_t *desc, const int32_t *counts
                                       const int32_t *qframe, const int32_t *tframe, int32_t *bi, int32_t *bd,
                                       int32_t *sd, hipStream_t st) {
     if (npairs <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hamming_best2_pairs, dim3((row_cap + kQPB - 1) / kQPB, npairs), dim3(256), 0, st,
-                       desc, counts,
-                       row_cap, qframe, tframe, bi, bd, sd);
+    if (row_cap > kHamMaxTrain) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_hamming_best2_pairs, dim3((row_cap + kHamQPB - 1) / kHamQPB, npairs), dim3(256), 0, st,
+                       desc, counts, row_cap, qframe, tframe, bi, bd, sd);
     return hipGetLastError();
 }
 

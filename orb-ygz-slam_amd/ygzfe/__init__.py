@@ -20,6 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "libygzfe.so")
 SYNTH_PATH = os.path.join(PKG_ROOT, "lib", "libygzsynth.so")
+SYNTH_HIP_PATH = os.path.join(PKG_ROOT, "lib", "libygzsynth_hip.so")
 
 MAX_LEVELS = 16
 ORBSLAM_KEYPOINT, FAST_KEYPOINT, DSO_KEYPOINT = 0, 1, 2
@@ -500,3 +501,22 @@ def backproject_plane(cam, q_cw, t_cw, uv, plane_z):
                                                C.c_double(plane_z), _p(P))
         out[i] = P
     return out, ok
+
+
+_synth_hip = None
+
+
+def plane_points_device(d_kps, cap, n_frames, cam, d_r3, d_cz, plane_z, d_xyz, stream=None):
+    """Synthetic map points for bench.py: back-project every keypoint of frame i
+    onto the plane Z_w = plane_z (one fused HIP pass; synth/plane_points.hip)."""
+    global _synth_hip
+    if _synth_hip is None:
+        lib()  # torch's HIP runtime first (see lib())
+        if not os.path.exists(SYNTH_HIP_PATH):
+            raise YgzfeError(f"{SYNTH_HIP_PATH} missing: run `make -C orb-ygz-slam_amd`")
+        _synth_hip = C.CDLL(SYNTH_HIP_PATH)
+    c = (C.c_float * 4)(*[float(v) for v in cam])
+    rc = _synth_hip.ygzs_plane_points(C.c_void_p(d_kps), KP_DTYPE.itemsize // 4, cap, n_frames, c, C.c_void_p(d_r3),
+                                      C.c_void_p(d_cz), C.c_float(plane_z), C.c_void_p(d_xyz), C.c_void_p(stream))
+    if rc != 0:
+        raise YgzfeError("plane_points launch failed")

@@ -70,3 +70,57 @@ def test_best2_on_extracted_frames(gpu):
     assert np.array_equal(bi, ri) and np.array_equal(bd, rd) and np.array_equal(sd, rs)
     # sanity: most keypoints find a close match in the previous frame
     assert np.mean(bd < 50) > 0.5
+
+
+@pytest.mark.parametrize("nt", [31, 32, 33, 64, 95])
+def test_best2_tile_edges_and_ties(gpu, nt):
+    """Train sizes around the 32-row MFMA tile; many equal distances (first index wins)."""
+    rng = np.random.default_rng(nt)
+    base = rand_desc(rng, 4)
+    t = base[rng.integers(0, 4, nt)]          # heavy duplication -> ties everywhere
+    q = np.concatenate([base, rand_desc(rng, 61)])
+    bi, bd, sd = gpu.ORBmatcher().best2(q, t)
+    ri, rd, rs = O.hamming_best2(q, t)
+    assert np.array_equal(bi, ri) and np.array_equal(bd, rd) and np.array_equal(sd, rs)
+
+
+def test_best2_extreme_distances(gpu):
+    """All-zero vs all-one descriptors: distances 0 and 256 (the key's full range)."""
+    z, o = np.zeros((1, 32), np.uint8), np.full((1, 32), 255, np.uint8)
+    q = np.concatenate([z, o, z, o])
+    t = np.concatenate([o, o, z, o, z])
+    bi, bd, sd = gpu.ORBmatcher().best2(q, t)
+    ri, rd, rs = O.hamming_best2(q, t)
+    assert np.array_equal(bi, ri) and np.array_equal(bd, rd) and np.array_equal(sd, rs)
+    assert bd[0] == 0 and bi[0] == 2 and sd[0] == 0
+    t1 = np.concatenate([o])
+    bi, bd, sd = gpu.ORBmatcher().best2(z, t1)
+    assert bi[0] == 0 and bd[0] == 256 and sd[0] == 257
+
+
+def test_batch_match_pairs(gpu):
+    """ygzfe_batch_match (the bench path): frame k vs frame k-1 of a batch, every pair."""
+    import torch
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    F = 5
+    frames = np.stack([S.frame(20 + s, W, H) for s in range(F)])
+    b = gpu.Batch((nf, sf, nl, ini, mn, 0), 0, W, H, F)
+    b.upload(frames)
+    b.extract(F)
+    b.check()
+    P = F - 1
+    cap = b.kp_cap
+    qf = torch.arange(1, F, dtype=torch.int32, device="cuda")
+    tf = torch.arange(0, P, dtype=torch.int32, device="cuda")
+    bi = torch.full((P, cap), -7, dtype=torch.int32, device="cuda")
+    bd, sd = torch.empty_like(bi), torch.empty_like(bi)
+    b.match(P, qf.data_ptr(), tf.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr())
+    torch.cuda.synchronize()
+    res = [b.result(i) for i in range(F)]
+    for p in range(P):
+        dq, dt = res[p + 1][1], res[p][1]
+        ri, rd, rs = O.hamming_best2(dq, dt)
+        n = len(dq)
+        assert np.array_equal(bi[p, :n].cpu().numpy(), ri)
+        assert np.array_equal(bd[p, :n].cpu().numpy(), rd)
+        assert np.array_equal(sd[p, :n].cpu().numpy(), rs)
