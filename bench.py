@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--no-align", action="store_true")
     ap.add_argument("--no-undistort", action="store_true", help="skip the undistort-remap side measurement")
     ap.add_argument("--no-stage-timing", action="store_true", help="no per-stage hipEvents in the timed region")
+    ap.add_argument("--no-direct", action="store_true", help="skip the SearchLocalPointsDirect side measurement")
+    ap.add_argument("--latency-frames", type=int, default=200,
+                    help="single-frame latency leg: frames timed one at a time through the host C ABI (0 = skip)")
     return ap.parse_args()
 
 
@@ -227,6 +230,16 @@ def main():
                     "ms_per_launch": round(ums, 4), "alg_bytes_per_launch": ualg, "achieved_gbps": round(ugbps, 1),
                     "frac": round(ugbps / HBM_PEAK_GBPS, 4), "camera": "EuRoC (Examples/Monocular/EuRoC.yaml)"}
 
+    # ------------------------------------------------ §8(f) rank 2: SearchLocalPointsDirect
+    direct_line = None
+    if rank == 0 and world == 1 and not args.no_direct:
+        direct_line = direct_leg(S, args.cpu_sample > 0)
+
+    # ------------------------------------------------ single-frame latency (rank 0, N = 1)
+    lat = None
+    if rank == 0 and world == 1 and args.latency_frames > 0:
+        lat = latency_leg(frames, poses, sc, S, args.latency_frames)
+
     # ------------------------------------------------ CPU baseline (rank 0, N = 1)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
@@ -243,6 +256,10 @@ def main():
                 nrm += 1
             und_line["cpu_port_frames_per_s"] = round(nrm / (time.perf_counter() - t_c), 1)
 
+    if lat is not None and cpu is not None:
+        cpu_lat = cpu["ms_extract"] + cpu["ms_align"]
+        lat["cpu_port_ms"] = round(cpu_lat, 3)
+        lat["speedup_vs_cpu_port"] = round(cpu_lat / lat["median_ms"], 2)
     if rank == 0:
         line = {
             "metric": "frames/sec ORB-extract+SparseImageAlign, 752x480, 1000 feat",
@@ -269,11 +286,114 @@ def main():
             "h2d_upload_ms": round(h2d_s * 1e3, 2),
             "render_s": round(render_s, 2),
             "cpu_baseline": cpu,
-            "next_rows": {"undistort_remap": und_line},
+            "latency": lat,
+            "next_rows": {"undistort_remap": und_line, "search_local_points_direct": direct_line},
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def plane_xyz(S, pose, kps, cam):
+    """xyz_ref = T_ref * P_w for keypoints on the plane Z_w = PLANE_Z (the Tracking
+    snapshot of the reference frame's map points), in reference-camera coordinates."""
+    fx, fy, cx, cy = cam
+    q, t = pose
+    qi, ti = S.se3_inv(q.astype(np.float64), t.astype(np.float64))
+    R_wc = np.array([S.quat_rot(qi, e) for e in np.eye(3)]).T
+    d = np.stack([(kps["x"] - cx) / fx, (kps["y"] - cy) / fy, np.ones(len(kps))], 1)
+    lam = (S.PLANE_Z - ti[2]) / (d @ R_wc[2])
+    return np.ascontiguousarray((d * lam[:, None]).astype(np.float32))
+
+
+def latency_leg(frames, poses, sc, S, n_timed, warm=10):
+    """Single-frame latency, the reference's execution model (one Tracking thread,
+    SURVEY.md §8d): per frame, host image -> ComputePyramid -> ORB extract ->
+    keypoints + descriptors back on the host -> SparseImgAlign(prev -> cur) ->
+    pose on the host, through the host C ABI (pageable host buffers, H2D and D2H
+    included).  Map points of the previous frame (T_ref * P_w) are formed on
+    the host between frames, outside the timed region, as Tracking does."""
+    import ctypes as C
+    import ygzfe
+    L = ygzfe.lib()
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    ex = ygzfe.ORBextractor(nf, sf, nl, ini, mn, device=0)
+    fr = [ygzfe.Frame(ex, W, H), ygzfe.Frame(ex, W, H)]
+    cap = 4096
+    kps = [np.zeros(cap, ygzfe.KP_DTYPE) for _ in range(2)]
+    desc = [np.zeros((cap, 32), np.uint8) for _ in range(2)]
+    n_out = C.c_int()
+    cam = sc.camera()
+    T0 = ygzfe.SE3.make()
+    res = ygzfe.AlignResult()
+    p = ygzfe._p
+    n_frames = min(len(frames), warm + n_timed + 1)
+    ts, te = [], []
+    prev = None
+    for i in range(n_frames):
+        cur = i & 1
+        img = np.ascontiguousarray(frames[i])
+        t0 = time.perf_counter()
+        ygzfe._check(L.ygzfe_compute_pyramid(ex.h, fr[cur].h, p(img), W), "compute_pyramid")
+        ygzfe._check(L.ygzfe_extract(ex.h, fr[cur].h, ygzfe.ORBSLAM_KEYPOINT, p(kps[cur]), 0, cap, p(desc[cur]),
+                                     C.byref(n_out)), "extract")
+        t1 = time.perf_counter()
+        if prev is not None:
+            pk, xyz, us = prev
+            ygzfe._check(L.ygzfe_sparse_align(fr[cur ^ 1].h, fr[cur].h, C.byref(cam), p(pk), p(xyz), p(us), len(pk),
+                                              3, 1, C.byref(T0), C.byref(res)), "sparse_align")
+        t2 = time.perf_counter()
+        if i > warm:
+            ts.append(t2 - t0)
+            te.append(t1 - t0)
+        pk = kps[cur][:n_out.value].copy()
+        prev = (pk, plane_xyz(S, poses[i], pk, sc.cam), np.ones(len(pk), np.uint8))
+    ts = np.array(ts) * 1e3
+    te = np.array(te) * 1e3
+    return {"frames": len(ts), "median_ms": round(float(np.median(ts)), 4), "p90_ms": round(float(np.percentile(ts, 90)), 4),
+            "median_extract_ms": round(float(np.median(te)), 4),
+            "median_align_ms": round(float(np.median(ts - te)), 4),
+            "path": "host C ABI, one frame at a time: H2D 752x480 u8 -> pyramid -> extract -> D2H kps+desc -> "
+                    "SparseImgAlign 3..1 (prev -> cur) -> D2H pose; median over frames after 10 warm-up frames"}
+
+
+def direct_leg(S, with_cpu, reps=50):
+    """Batched SearchLocalPointsDirect (Tracking.cc:2258-2410) for one current frame:
+    4 keyframes, ~750 local map points with 0..5 observations each (~1750
+    (point, keyframe) FindDirectProjection items), host C ABI call -> matches on the
+    host; median over `reps` calls.  CPU: the oracle's sequential loop, 1 thread."""
+    import ygzfe
+    d = S.direct_scene(0, n_kf=4, max_obs=5)
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    ex = ygzfe.ORBextractor(nf, sf, nl, ini, mn, device=0)
+    kf = [ex.ComputePyramid(im) for im in d["kf_images"]]
+    cur = ex.ComputePyramid(d["cur_image"])
+    cam = d["scene"].camera()
+    args = (d["item_ptr"], d["ref_index"], d["kps"], d["pt_ref"], d["T_cr"], d["px_proj"])
+    for _ in range(3):
+        ygzfe.search_direct_batch(kf, cur, cam, *args)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        _, m = ygzfe.search_direct_batch(kf, cur, cam, *args)
+        ts.append(time.perf_counter() - t0)
+    line = {"points": len(m), "items": int(d["item_ptr"][-1]), "matched": int((m >= 0).sum()),
+            "median_ms": round(float(np.median(ts)) * 1e3, 4),
+            "path": "host C ABI (H2D items, FindDirectProjection per item, first in-border success per point, D2H)"}
+    if with_cpu:
+        import _oracle as O
+        orc = O.OrbOracle(nf, sf, nl, ini, mn)
+        kl = [orc.pyramid(im) for im in d["kf_images"]]
+        cl = orc.pyramid(d["cur_image"])
+        oc = O.Cam(*d["scene"].cam)
+        tc = []
+        for _ in range(10):
+            t0 = time.perf_counter()
+            O.search_direct(orc, kl, cl, oc, *args)
+            tc.append(time.perf_counter() - t0)
+        line["cpu_port_ms"] = round(float(np.median(tc)) * 1e3, 4)
+        line["cpu_cores"] = 1
+    return line
 
 
 def cpu_baseline(frames, poses, S, args, sc):
@@ -287,19 +407,28 @@ def cpu_baseline(frames, poses, S, args, sc):
     n = 0
     t0 = time.perf_counter()
     prev = None
+    t_ext = t_ham = t_al = 0.0
+    n_al = 0
     while n < min(args.cpu_sample, len(frames)):
+        ta = time.perf_counter()
         lv = orc.pyramid(frames[n])
         kps, desc = orc.extract(lv)
+        t_ext += time.perf_counter() - ta
         if prev is not None:
             plv, pk, pdesc = prev
+            ta = time.perf_counter()
             O.hamming_best2(desc, pdesc)
+            t_ham += time.perf_counter() - ta
             q, t = poses[n - 1]
             qi, ti = S.se3_inv(q.astype(np.float64), t.astype(np.float64))
             R_wc = np.array([S.quat_rot(qi, e) for e in np.eye(3)]).T
             d = np.stack([(pk["x"] - cx) / fx, (pk["y"] - cy) / fy, np.ones(len(pk))], 1)
             lam = (S.PLANE_Z - ti[2]) / (d @ R_wc[2])
             xyz = (d * lam[:, None]).astype(np.float32)
+            ta = time.perf_counter()
             O.sparse_align(plv, lv, orc.inv_scale, cam, pk, xyz, np.ones(len(pk), np.uint8), 3, 1, T0)
+            t_al += time.perf_counter() - ta
+            n_al += 1
         prev = (lv, kps, desc)
         n += 1
         if time.perf_counter() - t0 > args.cpu_budget_s:
@@ -308,7 +437,9 @@ def cpu_baseline(frames, poses, S, args, sc):
     return {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": f"{n} frames of the same rendered C2 sequence: pyramid + octree ORB + rBRIEF + Hamming vs "
                       f"previous frame + SparseImgAlign 3..1, oracle/ (gcc -O3 -march=native), 1 thread",
-            "ms_per_frame": round(el * 1e3 / n, 3)}
+            "ms_per_frame": round(el * 1e3 / n, 3),
+            "ms_extract": round(t_ext * 1e3 / n, 3), "ms_hamming": round(t_ham * 1e3 / max(1, n_al), 3),
+            "ms_align": round(t_al * 1e3 / max(1, n_al), 3)}
 
 
 if __name__ == "__main__":

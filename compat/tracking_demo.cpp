@@ -93,6 +93,32 @@ int main() {
         const bool conv = ygz::Align2D(f1, 0, pb, p, 10, px);
         std::printf("Align2D converged %d px (%.3f %.3f) expected (%d %d)\n", (int)conv, px[0], px[1], u, v);
         if (!conv || std::fabs(px[0] - u) > 0.1f || std::fabs(px[1] - v) > 0.1f) fails++;
+
+        // SearchLocalPointsDirect (Tracking.cc:2258-2410): frame 0 as the only keyframe,
+        // every frame-0 keypoint a map point predicted 0.6 / -0.4 px off its true
+        // position in frame 1; the batched search must land on the true shift
+        ygz::DirectSearch ds;
+        ygz::SE3 Tcr;
+        Tcr.t = {tx, ty, 0.f};
+        for (size_t i = 0; i < k0.size(); i++) {
+            ds.add_point(k0[i].pt.x + 2.0f + 0.6f, k0[i].pt.y - 1.0f - 0.4f);
+            ds.add_observation(0, k0[i], &xyz[3 * i], Tcr);
+        }
+        ds.run({&f0}, f1, cam);
+        int hit = 0, close = 0, near = 0;
+        for (int i = 0; i < ds.n_points(); i++) {
+            if (!ds.matched(i)) continue;
+            hit++;
+            const float ex = std::fabs(ds.px(i)[0] - (k0[i].pt.x + 2.f)), ey = std::fabs(ds.px(i)[1] - (k0[i].pt.y - 1.f));
+            close += ex < 0.1f && ey < 0.1f;
+            near += ex < 0.5f && ey < 0.5f;
+        }
+        const auto outcome = ds.cache_pass(W, H);
+        int kept = 0;
+        for (auto o : outcome) kept += o == ygz::DirectSearch::kMatched;
+        std::printf("direct search matched %d of %d, %d within 0.1 px, %d within 0.5 px; cache pass keeps %d\n", hit,
+                    ds.n_points(), close, near, kept);
+        if (hit < ds.n_points() / 2 || near < hit * 7 / 10 || close < hit / 2 || kept < 1 || kept > hit) fails++;
     } catch (const std::exception &e) {
         std::printf("error: %s\n", e.what());
         return 2;

@@ -281,4 +281,86 @@ inline bool Align2D(const FramePyramid &cur, int level, const uint8_t *ref_patch
     return ok != 0;
 }
 
+// Tracking::SearchLocalPointsDirect (Tracking.cc:2258-2410) with its per-point
+// FindDirectProjection loop batched on the GPU.  The caller keeps the reference's
+// control flow (isBad / isInFrustum / cache set / UpdateLocalMap) and, per
+// surviving map point, lists its SelectNearestKeyframe observations
+// (Tracking.cc:2412-2432) in order:
+//
+//   ygz::DirectSearch ds;
+//   for (MapPoint *mp : candidates) {            // after isInFrustum(mp, 0.5)
+//       ds.add_point(mp->mTrackProjX, mp->mTrackProjY);
+//       for (auto &o : SelectNearestKeyframe(mp->GetObservations(), 5))
+//           ds.add_observation(slot_of(o.first), o.first->mvKeys[o.second],
+//                              o.first->GetPose() * mp->GetWorldPos(), mCurrentFrame.mTcw * o.first->GetPose().inverse());
+//   }
+//   ds.run(keyframe_pyramids, current_pyramid, cam);   // one GPU pass over all (point, keyframe) items
+//   // ds.matched(i) / ds.px(i): the reference's px_ave for point i (or no match)
+//
+// For the cache pass (Tracking.cc:2268-2325) cache_pass() replays the 5x5-px
+// occupancy grid in cache order: a point whose predicted cell is already
+// taken is kept untried, a matched point marks the cell of its pixel, an
+// unmatched point leaves the cache.
+class DirectSearch {
+public:
+    enum CacheOutcome { kMatched = 0, kKeptUntried = 1, kErased = 2 };
+
+    void clear() { item_ptr_.assign(1, 0); proj_.clear(); ref_.clear(); kps_.clear(); pt_.clear(); T_.clear(); }
+    int add_point(float proj_x, float proj_y) {
+        if (item_ptr_.empty()) item_ptr_.push_back(0);
+        proj_.push_back(proj_x);
+        proj_.push_back(proj_y);
+        item_ptr_.push_back(item_ptr_.back());
+        return (int)proj_.size() / 2 - 1;
+    }
+    void add_observation(int kf_slot, const KeyPoint &kp, const float pt_ref[3], const SE3 &T_cr) {
+        ref_.push_back(kf_slot);
+        kps_.push_back(kp);
+        pt_.insert(pt_.end(), pt_ref, pt_ref + 3);
+        ygzfe_se3 t;
+        std::memcpy(t.q, T_cr.q.data(), sizeof(t.q));
+        std::memcpy(t.t, T_cr.t.data(), sizeof(t.t));
+        T_.push_back(t);
+        item_ptr_.back() += 1;
+    }
+    int n_points() const { return (int)proj_.size() / 2; }
+    // FindDirectProjection over every item + first in-border success per point
+    void run(const std::vector<const FramePyramid *> &keyframes, const FramePyramid &cur, const ygzfe_camera &cam,
+             float border = 20.f) {
+        const int n = n_points();
+        px_.assign(2 * (size_t)n, 0.f);
+        matched_.assign(n, -1);
+        if (n == 0) return;
+        std::vector<const ygzfe_frame *> h(keyframes.size());
+        for (size_t i = 0; i < keyframes.size(); i++) h[i] = keyframes[i]->handle();
+        compat::check(ygzfe_search_direct_batch(h.data(), (int)h.size(), cur.handle(), &cam, n, item_ptr_.data(),
+                                                ref_.data(), compat::as_kp(kps_.data()), pt_.data(), T_.data(),
+                                                proj_.data(), border, px_.data(), matched_.data()),
+                      "search_direct_batch");
+    }
+    bool matched(int i) const { return matched_[i] >= 0; }
+    int matched_observation(int i) const { return matched_[i] < 0 ? -1 : matched_[i] - item_ptr_[i]; }
+    const float *px(int i) const { return &px_[2 * (size_t)i]; }
+    // Tracking.cc:2262-2325: grid_size 5 over level 0 (rows / 5 x cols / 5 cells)
+    std::vector<CacheOutcome> cache_pass(int cols, int rows, int grid_size = 5) const {
+        const int gr = rows / grid_size, gc = cols / grid_size;
+        std::vector<bool> grid((size_t)gr * gc, false);
+        std::vector<CacheOutcome> out(n_points());
+        for (int i = 0; i < n_points(); i++) {
+            const int k = (int)(proj_[2 * i + 1] / grid_size) * gc + (int)(proj_[2 * i] / grid_size);
+            if (grid[k]) { out[i] = kKeptUntried; continue; }
+            if (matched_[i] < 0) { out[i] = kErased; continue; }
+            grid[(size_t)((int)(px_[2 * i + 1] / grid_size) * gc + (int)(px_[2 * i] / grid_size))] = true;
+            out[i] = kMatched;
+        }
+        return out;
+    }
+
+private:
+    std::vector<int32_t> item_ptr_{0}, ref_, matched_;
+    std::vector<float> proj_, pt_, px_;
+    std::vector<KeyPoint> kps_;
+    std::vector<ygzfe_se3> T_;
+};
+
 }  // namespace ygz

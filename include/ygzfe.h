@@ -237,6 +237,23 @@ int ygzfe_find_direct_projection_batch(const ygzfe_frame *const *ref, const ygzf
                                        const ygzfe_se3 *T_cr, float *px_io, int32_t *search_level,
                                        uint8_t *ok);
 
+/* Tracking::SearchLocalPointsDirect (Tracking.cc:2258-2410), batched: for
+ * n_points map points that passed Frame::isInFrustum (Frame.cc:363-422),
+ * point i's candidate observations are items [item_ptr[i], item_ptr[i+1]) in
+ * SelectNearestKeyframe order (Tracking.cc:2412-2432, <= 5 keyframes); item k
+ * uses keyframe ref[ref_index[k]] with kp_ref[k] = ref->mvKeys[index],
+ * pt_ref[3k] = T_ref * P_w, T_cr[k] = T_cur * T_ref^-1.  px_proj[2i] =
+ * (mTrackProjX, mTrackProjY).  Every item runs FindDirectProjection
+ * (ORBmatcher.cc:1573-1602); per point the first item that converged and lies
+ * inside [border, cols - border) x [border, rows - border) of level 0 (border
+ * = 20, Tracking.cc:2287-2293) is kept: px_out[2i] = its px, matched_item[i]
+ * = its item index, or -1 (px_out (0, 0)) when none did. */
+int ygzfe_search_direct_batch(const ygzfe_frame *const *ref, int n_ref, const ygzfe_frame *cur,
+                              const ygzfe_camera *cam, int n_points, const int32_t *item_ptr,
+                              const int32_t *ref_index, const ygzfe_kp *kp_ref, const float *pt_ref,
+                              const ygzfe_se3 *T_cr, const float *px_proj, float border, float *px_out,
+                              int32_t *matched_item);
+
 /* ------------------------------------------------------------------------ */
 /* Undistortion (Frame::ComputeImagePyramid, Frame.cc:775-790):              */
 /*   initUndistortRectifyMap(K, D, I, K, size, CV_16SC2, map1, map2) once     */

@@ -455,3 +455,39 @@ int ygzo_find_direct_projection(const ygzo_cam *cam, uint8_t **ref_levels, const
     px_curr[1] = pxs[1] * scale[sl];
     return ok;
 }
+
+/* Tracking::SearchLocalPointsDirect (Tracking.cc:2337-2395), the per-point
+ * body of the local-map loop: walk the point's observations in
+ * SelectNearestKeyframe order (Tracking.cc:2412-2432; the caller lists them),
+ * FindDirectProjection each from (mTrackProjX, mTrackProjY), skip results
+ * within `border` px of the level-0 edge (Tracking.cc:2356-2364), keep the
+ * first success (`break`), px_ave = that pixel / 1.  ref_levels holds
+ * n_ref * nlevels level pointers (keyframe-major). */
+void ygzo_search_direct(const ygzo_cam *cam, uint8_t **ref_levels, uint8_t **cur_levels, const int *lw,
+                        const int *lh, int nlevels, const float *scale, const float *inv_scale,
+                        float inv_level_sigma2_1, int n_points, const int *item_ptr, const int *ref_index,
+                        const ygzo_kp *kps, const float *pt_ref, const ygzo_se3 *T_cr, const float *px_proj,
+                        float border, float *px_out, int *matched) {
+    const int cols = lw[0], rows = lh[0];
+    for (int i = 0; i < n_points; i++) {
+        int m = -1;
+        float ave[2] = {0.f, 0.f};
+        for (int k = item_ptr[i]; k < item_ptr[i + 1]; k++) {
+            float px[2] = {px_proj[2 * i], px_proj[2 * i + 1]};
+            int sl;
+            if (ygzo_find_direct_projection(cam, ref_levels + (size_t)ref_index[k] * nlevels, lw, lh, cur_levels, lw,
+                                            lh, nlevels, scale, inv_scale, inv_level_sigma2_1, &T_cr[k],
+                                            pt_ref + 3 * (size_t)k, &kps[k], px, &sl)) {
+                if (px[0] < border || px[1] < border || px[0] >= cols - border || px[1] >= rows - border)
+                    continue;
+                m = k;
+                ave[0] = px[0] / 1.0f;
+                ave[1] = px[1] / 1.0f;
+                break;
+            }
+        }
+        px_out[2 * i] = ave[0];
+        px_out[2 * i + 1] = ave[1];
+        matched[i] = m;
+    }
+}

@@ -173,6 +173,14 @@ int ygzo_find_direct_projection(const ygzo_cam *cam, uint8_t **ref_levels, const
                                 const float pt_ref[3], const ygzo_kp *kp_ref, float *px_curr,
                                 int *search_level);
 
+/* SearchLocalPointsDirect (Tracking.cc:2337-2395) per point: first converged
+ * observation inside the border, in the listed (SelectNearestKeyframe) order. */
+void ygzo_search_direct(const ygzo_cam *cam, uint8_t **ref_levels, uint8_t **cur_levels, const int *lw,
+                        const int *lh, int nlevels, const float *scale, const float *inv_scale,
+                        float inv_level_sigma2_1, int n_points, const int *item_ptr, const int *ref_index,
+                        const ygzo_kp *kps, const float *pt_ref, const ygzo_se3 *T_cr, const float *px_proj,
+                        float border, float *px_out, int *matched);
+
 /* ---------------- undistort (Frame.cc:775-790) ---------------- */
 /* cv::initUndistortRectifyMap(K, D, I, K, (W,H), CV_16SC2): map1 [H][W][2]
  * (integer source x, y), map2 [H][W] (5-bit fractions, y*32 + x). */

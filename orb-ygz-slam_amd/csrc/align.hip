@@ -1160,21 +1160,15 @@ hipError_t launch_align2d(const uint8_t *img, int w, int h, int n, const uint8_t
 }
 
 // ------------------------------------------------------------------ FindDirectProjection
-__global__ __launch_bounds__(256) void k_find_direct(const uint8_t *const *__restrict__ ref_pyrs, AlignLevels rlv,
-                                                     const uint8_t *__restrict__ cur_pyr, AlignLevels clv,
-                                                     int nlevels, const float *__restrict__ scale,
-                                                     float inv_sigma2_1, ygzfe_camera cam, int n,
-                                                     const int32_t *__restrict__ ref_index,
-                                                     const ygzfe_kp *__restrict__ kps, const float *__restrict__ pts,
-                                                     const ygzfe_se3 *__restrict__ Tcr, float *__restrict__ px_io,
-                                                     int32_t *__restrict__ level_out, uint8_t *__restrict__ ok_out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const ygzfe_kp kp = kps[i];
+// One (map point, keyframe) item: GetWarpAffineMatrix + GetBestSearchLevel +
+// WarpAffine 10x10 + Align2D at the search level.  px (level-0 px) in/out.
+__device__ int find_direct_one(const uint8_t *__restrict__ ref_pyr, const AlignLevels &rlv,
+                               const uint8_t *__restrict__ cur_pyr, const AlignLevels &clv, int nlevels,
+                               const float *__restrict__ scale, float inv_sigma2_1, const ygzfe_camera &cam,
+                               const ygzfe_kp &kp, const float pt[3], const ygzfe_se3 &Tcr, float px[2], int *level) {
     SE3 T;
-    for (int k = 0; k < 4; k++) T.q[k] = Tcr[i].q[k];
-    for (int k = 0; k < 3; k++) T.t[k] = Tcr[i].t[k];
-    const float pt[3] = {pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
+    for (int k = 0; k < 4; k++) T.q[k] = Tcr.q[k];
+    for (int k = 0; k < 3; k++) T.t[k] = Tcr.t[k];
     const int oc = clampi(kp.octave, 0, nlevels - 1);
     // GetWarpAffineMatrix (ORBmatcher.cc:1525-1547)
     const float depth = pt[2], ls = scale[oc];
@@ -1194,9 +1188,9 @@ __global__ __launch_bounds__(256) void k_find_direct(const uint8_t *const *__res
     int sl = 0;
     float D = A0 * A3 - A2 * A1;
     while (D > 3.0f && sl < nlevels - 1) { sl += 1; D *= inv_sigma2_1; }
-    level_out[i] = sl;
+    *level = sl;
     // WarpAffine 10x10 (ORBmatcher.cc:1549-1571)
-    const uint8_t *rimg = ref_pyrs[ref_index[i]] + rlv.off[oc];
+    const uint8_t *rimg = ref_pyr + rlv.off[oc];
     const int rw = rlv.w[oc], rh = rlv.h[oc];
     const float det = A0 * A3 - A2 * A1;
     const float inv = 1.f / det;
@@ -1220,12 +1214,31 @@ __global__ __launch_bounds__(256) void k_find_direct(const uint8_t *const *__res
         }
     for (int y = 1; y < 9; ++y)
         for (int x = 0; x < 8; ++x) pp[(y - 1) * 8 + x] = pb[y * 10 + 1 + x];
-    const float is = 1.0f / scale[sl];
-    (void)is;
-    float q[2] = {px_io[2 * i] * clv.inv_scale[sl], px_io[2 * i + 1] * clv.inv_scale[sl]};
+    float q[2] = {px[0] * clv.inv_scale[sl], px[1] * clv.inv_scale[sl]};
     const int ok = align2d_lane(cur_pyr + clv.off[sl], clv.w[sl], clv.h[sl], pb, pp, 10, q);
-    px_io[2 * i] = q[0] * scale[sl];
-    px_io[2 * i + 1] = q[1] * scale[sl];
+    px[0] = q[0] * scale[sl];
+    px[1] = q[1] * scale[sl];
+    return ok;
+}
+
+__global__ __launch_bounds__(256) void k_find_direct(const uint8_t *const *__restrict__ ref_pyrs, AlignLevels rlv,
+                                                     const uint8_t *__restrict__ cur_pyr, AlignLevels clv,
+                                                     int nlevels, const float *__restrict__ scale,
+                                                     float inv_sigma2_1, ygzfe_camera cam, int n,
+                                                     const int32_t *__restrict__ ref_index,
+                                                     const ygzfe_kp *__restrict__ kps, const float *__restrict__ pts,
+                                                     const ygzfe_se3 *__restrict__ Tcr, float *__restrict__ px_io,
+                                                     int32_t *__restrict__ level_out, uint8_t *__restrict__ ok_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float pt[3] = {pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
+    float px[2] = {px_io[2 * i], px_io[2 * i + 1]};
+    int sl;
+    const int ok = find_direct_one(ref_pyrs[ref_index[i]], rlv, cur_pyr, clv, nlevels, scale, inv_sigma2_1, cam,
+                                   kps[i], pt, Tcr[i], px, &sl);
+    level_out[i] = sl;
+    px_io[2 * i] = px[0];
+    px_io[2 * i + 1] = px[1];
     ok_out[i] = (uint8_t)ok;
 }
 
@@ -1237,6 +1250,72 @@ hipError_t launch_find_direct(const uint8_t *const *ref_pyrs, const AlignLevels 
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_find_direct, dim3((n + 255) / 256), dim3(256), 0, st, ref_pyrs, ref_lv, cur_pyr, cur_lv,
                        nlevels, scale, inv_sigma2_1, cam, n, ref_index, kp_ref, pt_ref, T_cr, px, level, ok);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ SearchLocalPointsDirect
+// Tracking::SearchLocalPointsDirect (Tracking.cc:2258-2410) as one speculative
+// pass: every (map point, keyframe) item of every point runs FindDirectProjection
+// at once (it is a pure function of the point, the keyframe and the current
+// frame), then k_direct_select walks each point's items in SelectNearestKeyframe
+// order (Tracking.cc:2412-2432) and keeps the first that succeeded and lies
+// inside the 20 px border (Tracking.cc:2287-2296 / 2356-2364): the same answer
+// the reference's sequential loop with its `break` gives.
+
+__global__ __launch_bounds__(256) void k_direct_items(const uint8_t *const *__restrict__ ref_pyrs, AlignLevels lv,
+                                                      const uint8_t *__restrict__ cur_pyr, int nlevels,
+                                                      const float *__restrict__ scale, float inv_sigma2_1,
+                                                      ygzfe_camera cam, int n, const DirectItem *__restrict__ items,
+                                                      const float *__restrict__ px_proj, float *__restrict__ px_out,
+                                                      uint8_t *__restrict__ ok_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const DirectItem it = items[i];
+    float px[2] = {px_proj[2 * it.point], px_proj[2 * it.point + 1]};  // (mTrackProjX, mTrackProjY)
+    int sl;
+    const int ok = find_direct_one(ref_pyrs[it.ref], lv, cur_pyr, lv, nlevels, scale, inv_sigma2_1, cam, it.kp,
+                                   it.pt, it.Tcr, px, &sl);
+    px_out[2 * i] = px[0];
+    px_out[2 * i + 1] = px[1];
+    ok_out[i] = (uint8_t)ok;
+}
+
+__global__ __launch_bounds__(256) void k_direct_select(int n_points, const int32_t *__restrict__ item_ptr,
+                                                       const float *__restrict__ px_item,
+                                                       const uint8_t *__restrict__ ok_item, float border, float cols,
+                                                       float rows, float *__restrict__ px_out,
+                                                       int32_t *__restrict__ matched) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_points) return;
+    int m = -1;
+    float u = 0.f, v = 0.f;
+    for (int k = item_ptr[i]; k < item_ptr[i + 1]; k++) {
+        if (!ok_item[k]) continue;
+        const float x = px_item[2 * k], y = px_item[2 * k + 1];
+        if (x < border || y < border || x >= cols - border || y >= rows - border) continue;
+        m = k;
+        u = x;
+        v = y;
+        break;
+    }
+    // px_ave = sum(matched_pixels) / size() with exactly one pixel (Tracking.cc:2300-2305)
+    px_out[2 * i] = u / 1.0f;
+    px_out[2 * i + 1] = v / 1.0f;
+    matched[i] = m;
+}
+
+hipError_t launch_search_direct(const uint8_t *const *ref_pyrs, const AlignLevels &lv, const uint8_t *cur_pyr,
+                                int nlevels, const float *scale, float inv_sigma2_1, const ygzfe_camera &cam,
+                                int n_points, int n_items, const int32_t *item_ptr, const void *items,
+                                const float *px_proj, float *px_item, uint8_t *ok_item, float border, float *px_out,
+                                int32_t *matched, hipStream_t st) {
+    if (n_points <= 0) return hipSuccess;
+    if (n_items > 0)
+        hipLaunchKernelGGL(k_direct_items, dim3((n_items + 255) / 256), dim3(256), 0, st, ref_pyrs, lv, cur_pyr,
+                           nlevels, scale, inv_sigma2_1, cam, n_items, (const DirectItem *)items, px_proj, px_item,
+                           ok_item);
+    hipLaunchKernelGGL(k_direct_select, dim3((n_points + 255) / 256), dim3(256), 0, st, n_points, item_ptr, px_item,
+                       ok_item, border, (float)lv.w[0], (float)lv.h[0], px_out, matched);
     return hipGetLastError();
 }
 

@@ -162,6 +162,9 @@ struct ygzfe_extractor {
     std::map<std::pair<int, int>, std::unique_ptr<PlanDev>> plans;
     Workspace ws;
     int dso_grid = -1;
+    // SearchLocalPointsDirect staging: one packed H2D, one packed D2H per call
+    DevBuf direct_dev;
+    std::vector<uint8_t> direct_host;
     std::mutex mu;
 };
 
@@ -1015,6 +1018,72 @@ extern "C" int ygzfe_find_direct_projection_batch(const ygzfe_frame *const *ref,
     YGZ_HIP(hipMemcpyAsync(px_io, dpx.p, 8 * (size_t)n, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipMemcpyAsync(search_level, dlv.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipMemcpyAsync(ok, dok.p, (size_t)n, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipStreamSynchronize(st));
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_search_direct_batch(const ygzfe_frame *const *ref, int n_ref, const ygzfe_frame *cur,
+                                         const ygzfe_camera *cam, int n_points, const int32_t *item_ptr,
+                                         const int32_t *ref_index, const ygzfe_kp *kp_ref, const float *pt_ref,
+                                         const ygzfe_se3 *T_cr, const float *px_proj, float border,
+                                         float *px_out, int32_t *matched_item) {
+    if (!ref || n_ref < 0 || !cur || !cam || n_points < 0 ||
+        (n_points > 0 && (!item_ptr || !px_proj || !px_out || !matched_item))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (n_points == 0) return YGZFE_OK;
+    if (item_ptr[0] != 0) { set_error("item_ptr[0] must be 0"); return YGZFE_EINVAL; }
+    for (int i = 0; i < n_points; i++)
+        if (item_ptr[i + 1] < item_ptr[i]) { set_error("item_ptr not monotone at %d", i); return YGZFE_EINVAL; }
+    const int n_items = item_ptr[n_points];
+    if (n_items > 0 && (!ref_index || !kp_ref || !pt_ref || !T_cr)) { set_error("null item array"); return YGZFE_EINVAL; }
+    for (int k = 0; k < n_items; k++)
+        if (ref_index[k] < 0 || ref_index[k] >= n_ref) { set_error("ref_index[%d] out of range", k); return YGZFE_EINVAL; }
+    for (int r = 0; r < n_ref; r++)
+        if (!ref[r] || ref[r]->plan != cur->plan) {
+            set_error("reference keyframe %d missing or of a different size", r);
+            return YGZFE_EINVAL;
+        }
+    ygzfe_extractor *ex = cur->ex;
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    hipStream_t st = ex->stream;
+    const Plan &P = cur->plan->hp();
+    // packed layout: [ref ptrs][scale][item_ptr][px_proj][items] | [px_item][px_out][matched][ok_item]
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_ptr = 0, o_sc = al(o_ptr + sizeof(void *) * std::max(1, n_ref));
+    const size_t o_ip = al(o_sc + 4 * kMaxLevels), o_pp = al(o_ip + 4 * ((size_t)n_points + 1));
+    const size_t o_it = al(o_pp + 8 * (size_t)n_points), in_bytes = al(o_it + sizeof(DirectItem) * (size_t)n_items);
+    const size_t o_pxo = 0, o_m = al(o_pxo + 8 * (size_t)n_points), o_pxi = al(o_m + 4 * (size_t)n_points);
+    const size_t o_ok = al(o_pxi + 8 * (size_t)n_items), out_bytes = al(o_ok + (size_t)n_items);
+    std::vector<uint8_t> &h = ex->direct_host;
+    if (h.size() < in_bytes) h.resize(in_bytes);
+    const uint8_t **ptrs = (const uint8_t **)(h.data() + o_ptr);
+    for (int r = 0; r < n_ref; r++) ptrs[r] = ref[r]->pyr.as<uint8_t>();
+    float *sc = (float *)(h.data() + o_sc);
+    for (int l = 0; l < P.nlevels; l++) sc[l] = P.lv[l].scale;
+    memcpy(h.data() + o_ip, item_ptr, 4 * ((size_t)n_points + 1));
+    memcpy(h.data() + o_pp, px_proj, 8 * (size_t)n_points);
+    DirectItem *it = (DirectItem *)(h.data() + o_it);
+    for (int k = 0; k < n_items; k++) {
+        it[k].kp = kp_ref[k];
+        memcpy(it[k].pt, pt_ref + 3 * (size_t)k, 12);
+        it[k].Tcr = T_cr[k];
+        it[k].ref = ref_index[k];
+    }
+    for (int i = 0; i < n_points; i++)
+        for (int k = item_ptr[i]; k < item_ptr[i + 1]; k++) it[k].point = i;
+    YGZ_TRY(ex->direct_dev.ensure(in_bytes + out_bytes));
+    uint8_t *d = ex->direct_dev.as<uint8_t>(), *dout = d + in_bytes;
+    YGZ_HIP(hipMemcpyAsync(d, h.data(), in_bytes, hipMemcpyHostToDevice, st));
+    YGZ_HIP(launch_search_direct((const uint8_t *const *)(d + o_ptr), levels_of(P), cur->pyr.as<uint8_t>(),
+                                 P.nlevels, (const float *)(d + o_sc), ex->scales.inv_sigma2[1 < P.nlevels ? 1 : 0],
+                                 *cam, n_points, n_items, (const int32_t *)(d + o_ip), d + o_it,
+                                 (const float *)(d + o_pp), (float *)(dout + o_pxi), dout + o_ok, border,
+                                 (float *)(dout + o_pxo), (int32_t *)(dout + o_m), st));
+    YGZ_HIP(hipMemcpyAsync(px_out, dout + o_pxo, 8 * (size_t)n_points, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipMemcpyAsync(matched_item, dout + o_m, 4 * (size_t)n_points, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipStreamSynchronize(st));
     return YGZFE_OK;
 }

@@ -67,6 +67,22 @@ hipError_t launch_find_direct(const uint8_t *const *ref_pyrs, const AlignLevels 
                               const float *pt_ref, const ygzfe_se3 *T_cr, float *px, int32_t *level,
                               uint8_t *ok, hipStream_t st);
 
+// One (map point, keyframe) item of SearchLocalPointsDirect (host-packed, 80 B)
+struct DirectItem {
+    ygzfe_kp kp;        // ref->mvKeys[index] (28 B)
+    float pt[3];        // T_ref * P_w
+    ygzfe_se3 Tcr;      // T_cur * T_ref^-1
+    int32_t ref;        // keyframe slot
+    int32_t point;      // owning map point
+    int32_t pad;
+};
+static_assert(sizeof(DirectItem) == 80, "DirectItem layout");
+hipError_t launch_search_direct(const uint8_t *const *ref_pyrs, const AlignLevels &lv, const uint8_t *cur_pyr,
+                                int nlevels, const float *scale, float inv_sigma2_1, const ygzfe_camera &cam,
+                                int n_points, int n_items, const int32_t *item_ptr, const void *items,
+                                const float *px_proj, float *px_item, uint8_t *ok_item, float border, float *px_out,
+                                int32_t *matched, hipStream_t st);
+
 hipError_t launch_undistort_map(const float cam[4], const float *dist, int ndist, int W, int H, int16_t *map1,
                                 uint16_t *map2, hipStream_t st);
 int remap_tiles(int W, int H);  // entries of the per-tile source-box table (16 B each: x0, y0, w, h)

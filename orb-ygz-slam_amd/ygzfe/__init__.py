@@ -353,6 +353,28 @@ def find_direct_projection_batch(ref_frames, cur_frame, cam, ref_index, kp_ref, 
     return px, lvl, ok.astype(bool)
 
 
+def search_direct_batch(ref_frames, cur_frame, cam, item_ptr, ref_index, kp_ref, pt_ref, T_cr, px_proj, border=20.0):
+    """Tracking::SearchLocalPointsDirect's per-point search (Tracking.cc:2337-2395), batched:
+    point i tries items [item_ptr[i], item_ptr[i+1]) (its keyframes in SelectNearestKeyframe
+    order) with FindDirectProjection from px_proj[i] and keeps the first converged pixel inside
+    the border.  Returns (px_out float32[n,2], matched_item int32[n], -1 = no match)."""
+    refs = (C.c_void_p * max(1, len(ref_frames)))(*[f.h.value for f in ref_frames])
+    item_ptr = np.ascontiguousarray(item_ptr, np.int32)
+    n = len(item_ptr) - 1
+    ref_index = np.ascontiguousarray(ref_index, np.int32)
+    kp_ref = np.ascontiguousarray(kp_ref, KP_DTYPE)
+    pt_ref = np.ascontiguousarray(pt_ref, np.float32).reshape(-1, 3)
+    T_cr = np.ascontiguousarray(T_cr, SE3_DTYPE)
+    px_proj = np.ascontiguousarray(px_proj, np.float32).reshape(-1, 2)
+    px_out = np.zeros((max(n, 0), 2), np.float32)
+    matched = np.zeros(max(n, 0), np.int32)
+    _check(lib().ygzfe_search_direct_batch(refs, len(ref_frames), cur_frame.h, C.byref(cam), n, _p(item_ptr),
+                                           _p(ref_index), _p(kp_ref), _p(pt_ref), _p(T_cr), _p(px_proj),
+                                           C.c_float(border), _p(px_out), _p(matched)),
+           "search_direct_batch")
+    return px_out, matched
+
+
 class Batch:
     """Frames resident in HBM, one launch per stage (the bench / multi-GPU path)."""
 

@@ -272,6 +272,29 @@ def align2d(cur, rpb, rp, px, n_iter=10):
     return bool(ok), px
 
 
+def search_direct(orc, kf_levels, cur_levels, cam, item_ptr, ref_index, kps, pt_ref, T_cr, px_proj, border=20.0):
+    """SearchLocalPointsDirect's per-point search (Tracking.cc:2337-2395) -> (px_out, matched)."""
+    nl = len(cur_levels)
+    flat = [l for lv in kf_levels for l in lv]
+    rp = (C.c_void_p * max(1, len(flat)))(*[l.ctypes.data for l in flat])
+    cp = (C.c_void_p * MAXL)(*[l.ctypes.data for l in cur_levels])
+    lw = (C.c_int * MAXL)(*[l.shape[1] for l in cur_levels])
+    lh = (C.c_int * MAXL)(*[l.shape[0] for l in cur_levels])
+    sc = (C.c_float * MAXL)(*orc.scale.tolist())
+    isc = (C.c_float * MAXL)(*orc.inv_scale.tolist())
+    item_ptr = np.ascontiguousarray(item_ptr, np.int32)
+    n = len(item_ptr) - 1
+    T = (SE3 * max(1, len(T_cr)))(*[se3_from(r["q"], r["t"]) for r in T_cr])
+    px_out = np.zeros((max(n, 0), 2), np.float32)
+    matched = np.zeros(max(n, 0), np.int32)
+    lib().ygzo_search_direct(C.byref(cam), rp, cp, lw, lh, nl, sc, isc, C.c_float(orc.inv_sigma2[1]), n,
+                             _p(item_ptr), _p(np.ascontiguousarray(ref_index, np.int32)),
+                             _p(np.ascontiguousarray(kps, KP_DTYPE)), _p(np.ascontiguousarray(pt_ref, np.float32)),
+                             T, _p(np.ascontiguousarray(px_proj, np.float32)), C.c_float(border), _p(px_out),
+                             _p(matched))
+    return px_out, matched
+
+
 class RefFast:
     """The reference's own Thirdparty/fast, compiled by oracle/Makefile (oracle/_ref)."""
 

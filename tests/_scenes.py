@@ -94,3 +94,79 @@ def motion(seed, scale=1.0):
     v = np.array([0.02, -0.01, 0.015]) * scale + rng.uniform(-0.003, 0.003, 3)
     w = np.array([0.005, -0.004, 0.003]) * scale + rng.uniform(-0.001, 0.001, 3)
     return v, w
+
+
+def project(cam, q_cw, t_cw, Pw):
+    """Level-0 pixel of world points under T_cw (pinhole, Frame::World2Pixel)."""
+    Pc = np.array([quat_rot(q_cw, p) + t_cw for p in Pw]).reshape(-1, 3)
+    fx, fy, cx, cy = cam
+    return np.stack([fx * Pc[:, 0] / Pc[:, 2] + cx, fy * Pc[:, 1] / Pc[:, 2] + cy], 1), Pc
+
+
+def direct_scene(seed, n_kf=4, max_obs=5, W=752, H=480, nlevels=4, scale_factor=2.0, n_points=None):
+    """SearchLocalPointsDirect inputs (Tracking.cc:2258-2410) on the textured plane.
+
+    n_kf keyframes around the origin and a current frame moved by motion(seed).
+    Map points = plane points under keyframe 0's pixel grid; each point is observed
+    by a random ordered subset (0..max_obs) of the keyframes, its keypoint there =
+    the point's projection with a random octave.  px_proj = the projection into the
+    current frame + U(-1.5, 1.5) px (isInFrustum's prediction).  Returns a dict of
+    images, poses and the CSR item arrays of ygzfe.search_direct_batch."""
+    rng = np.random.default_rng(1000 + seed)
+    sc = PlaneScene(seed, W, H)
+    poses = []
+    for k in range(n_kf):
+        q = quat_from_rotvec(rng.uniform(-0.01, 0.01, 3))
+        t = rng.uniform(-0.04, 0.04, 3)
+        poses.append((q, t))
+    v, w = motion(seed)
+    qc, tc = se3_mul(quat_from_rotvec(w), v, *poses[0])
+    imgs = [sc.render(q.astype(np.float32), t.astype(np.float32), seed * 16 + k) for k, (q, t) in enumerate(poses)]
+    cur = sc.render(qc.astype(np.float32), tc.astype(np.float32), seed * 16 + 15)
+    # map points: a jittered pixel grid of keyframe 0, reaching the image edges (border rejections)
+    gx, gy = np.meshgrid(np.arange(6, W - 6, 22), np.arange(6, H - 6, 22))
+    uv = np.stack([gx.ravel(), gy.ravel()], 1).astype(np.float64) + rng.uniform(-3, 3, (gx.size, 2))
+    if n_points is not None:
+        uv = uv[rng.permutation(len(uv))[:n_points]]
+    Pw = backproject_plane_np(sc.cam, poses[0], uv)
+    n = len(Pw)
+    px_cur, _ = project(sc.cam, qc, tc, Pw)
+    px_proj = (px_cur + rng.uniform(-1.5, 1.5, px_cur.shape)).astype(np.float32)
+    item_ptr = [0]
+    ref_index, kps, pt_ref, T_cr = [], [], [], []
+    for i in range(n):
+        m = int(rng.integers(0, max_obs + 1))
+        for k in rng.permutation(n_kf)[:min(m, n_kf)]:
+            q, t = poses[k]
+            px_k, Pc = project(sc.cam, q, t, Pw[i:i + 1])
+            kp = np.zeros(1, ygzfe.KP_DTYPE)
+            kp["x"], kp["y"] = px_k[0]
+            kp["octave"] = int(rng.integers(0, nlevels))
+            kp["size"] = 31.0 * scale_factor ** kp["octave"][0]
+            kp["angle"] = -1.0
+            qi, ti = se3_inv(q, t)
+            qcr, tcr = se3_mul(qc, tc, qi, ti)
+            T = np.zeros(1, ygzfe.SE3_DTYPE)
+            T["q"] = qcr
+            T["t"] = tcr
+            ref_index.append(k)
+            kps.append(kp)
+            pt_ref.append(Pc[0])
+            T_cr.append(T)
+        item_ptr.append(len(ref_index))
+    cat = lambda xs, dt: np.concatenate(xs) if xs else np.zeros(0, dt)  # noqa: E731
+    return {"scene": sc, "kf_images": imgs, "cur_image": cur, "poses": poses, "cur_pose": (qc, tc),
+            "item_ptr": np.array(item_ptr, np.int32), "ref_index": np.array(ref_index, np.int32),
+            "kps": cat(kps, ygzfe.KP_DTYPE), "pt_ref": np.array(pt_ref, np.float32).reshape(-1, 3),
+            "T_cr": cat(T_cr, ygzfe.SE3_DTYPE), "px_proj": px_proj, "Pw": Pw}
+
+
+def backproject_plane_np(cam, pose, uv):
+    """World points on Z_w = PLANE_Z seen at level-0 pixels uv from pose T_cw (float64)."""
+    q, t = pose
+    qi, ti = se3_inv(q, t)
+    fx, fy, cx, cy = cam
+    d = np.stack([(uv[:, 0] - cx) / fx, (uv[:, 1] - cy) / fy, np.ones(len(uv))], 1)
+    dw = np.array([quat_rot(qi, x) for x in d])
+    lam = (PLANE_Z - ti[2]) / dw[:, 2]
+    return ti + dw * lam[:, None]

@@ -151,3 +151,42 @@ def test_align2d_recovers_subpixel_shift():
     ok, px = O.align2d(img, rpb, rp, (u0 + 0.6, v0 - 0.4))
     assert ok
     assert abs(px[0] - u0) < 0.1 and abs(px[1] - v0) < 0.1
+
+
+def test_search_direct_is_first_in_border_success():
+    """ygzo_search_direct (Tracking.cc:2337-2395) == FindDirectProjection per item in
+    order, first converged result inside the 20 px border, and recovers the true pixel."""
+    import _scenes as S
+    d = S.direct_scene(5, n_kf=3, max_obs=3, n_points=120)
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    kl = [orc.pyramid(im) for im in d["kf_images"]]
+    cl = orc.pyramid(d["cur_image"])
+    cam = O.Cam(*d["scene"].cam)
+    px, m = O.search_direct(orc, kl, cl, cam, d["item_ptr"], d["ref_index"], d["kps"], d["pt_ref"], d["T_cr"],
+                            d["px_proj"])
+    cp = (C.c_void_p * 16)(*[l.ctypes.data for l in cl])
+    lw = (C.c_int * 16)(*[l.shape[1] for l in cl])
+    lh = (C.c_int * 16)(*[l.shape[0] for l in cl])
+    sc = (C.c_float * 16)(*orc.scale.tolist())
+    isc = (C.c_float * 16)(*orc.inv_scale.tolist())
+    for i in range(len(m)):
+        want = -1
+        for k in range(d["item_ptr"][i], d["item_ptr"][i + 1]):
+            rp = (C.c_void_p * 16)(*[l.ctypes.data for l in kl[d["ref_index"][k]]])
+            q = np.array(d["px_proj"][i], np.float32)
+            sl = C.c_int()
+            ok = O.lib().ygzo_find_direct_projection(C.byref(cam), rp, lw, lh, cp, lw, lh, nl, sc, isc,
+                                                     C.c_float(orc.inv_sigma2[1]),
+                                                     C.byref(O.se3_from(d["T_cr"][k]["q"], d["T_cr"][k]["t"])),
+                                                     O._p(d["pt_ref"][k]), O._p(d["kps"][k:k + 1]), O._p(q),
+                                                     C.byref(sl))
+            if ok and 20 <= q[0] < W - 20 and 20 <= q[1] < H - 20:
+                want = k
+                assert np.array_equal(q, px[i])
+                break
+        assert m[i] == want, i
+    hit = m >= 0
+    assert hit.sum() > 20
+    true_px, _ = S.project(d["scene"].cam, *d["cur_pose"], d["Pw"])
+    assert np.median(np.abs(px[hit] - true_px[hit])) < 0.5

@@ -155,3 +155,60 @@ def test_find_direct_projection_bitexact(gpu):
         assert np.array_equal(q, px[i]), (i, q, px[i])
         n_ok += okc
     assert n_ok > n // 3
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_search_direct_batch_bitexact(gpu, seed):
+    """Batched SearchLocalPointsDirect (Tracking.cc:2258-2410): every point's first
+    converged in-border observation, in the listed keyframe order, bit-exact."""
+    d = S.direct_scene(seed, n_kf=4, max_obs=5)
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    ex = gpu.ORBextractor(nf, sf, nl, ini, mn)
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    kf_fr = [ex.ComputePyramid(im) for im in d["kf_images"]]
+    cur_fr = ex.ComputePyramid(d["cur_image"])
+    cam = d["scene"].camera()
+    args = (d["item_ptr"], d["ref_index"], d["kps"], d["pt_ref"], d["T_cr"], d["px_proj"])
+    px, m = gpu.search_direct_batch(kf_fr, cur_fr, cam, *args)
+    opx, om = O.search_direct(orc, [orc.pyramid(im) for im in d["kf_images"]], orc.pyramid(d["cur_image"]),
+                              O.Cam(*d["scene"].cam), *args)
+    assert np.array_equal(m, om)
+    assert np.array_equal(px, opx)
+    n = len(m)
+    hit = m >= 0
+    # coverage: most points with observations match, some fall back to a later keyframe,
+    # points without observations never match, and the border rule fires
+    has_obs = np.diff(d["item_ptr"]) > 0
+    assert not hit[~has_obs].any()
+    assert hit[has_obs].mean() > 0.5, hit[has_obs].mean()
+    assert (m[hit] > d["item_ptr"][:-1][hit]).any()
+    assert ((px[hit] >= 20).all() and (px[hit, 0] < W - 20).all() and (px[hit, 1] < H - 20).all())
+    assert n > 500
+
+
+def test_search_direct_batch_edges(gpu):
+    """No points, points without observations, and a keyframe list of length 1."""
+    d = S.direct_scene(3, n_kf=1, max_obs=1, n_points=40)
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    ex = gpu.ORBextractor(nf, sf, nl, ini, mn)
+    kf_fr = [ex.ComputePyramid(im) for im in d["kf_images"]]
+    cur_fr = ex.ComputePyramid(d["cur_image"])
+    cam = d["scene"].camera()
+    px, m = gpu.search_direct_batch(kf_fr, cur_fr, cam, np.zeros(1, np.int32), d["ref_index"][:0], d["kps"][:0],
+                                    d["pt_ref"][:0], d["T_cr"][:0], d["px_proj"][:0])
+    assert len(px) == 0 and len(m) == 0
+    ip = np.zeros(6, np.int32)
+    px, m = gpu.search_direct_batch(kf_fr, cur_fr, cam, ip, d["ref_index"][:0], d["kps"][:0], d["pt_ref"][:0],
+                                    d["T_cr"][:0], d["px_proj"][:5])
+    assert (m == -1).all() and (px == 0).all()
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    args = (d["item_ptr"], d["ref_index"], d["kps"], d["pt_ref"], d["T_cr"], d["px_proj"])
+    px, m = gpu.search_direct_batch(kf_fr, cur_fr, cam, *args)
+    opx, om = O.search_direct(orc, [orc.pyramid(im) for im in d["kf_images"]], orc.pyramid(d["cur_image"]),
+                              O.Cam(*d["scene"].cam), *args)
+    assert np.array_equal(m, om) and np.array_equal(px, opx)
+    with pytest.raises(gpu.YgzfeError):
+        bad = d["ref_index"].copy()
+        bad[:] = 7
+        gpu.search_direct_batch(kf_fr, cur_fr, cam, d["item_ptr"], bad, d["kps"], d["pt_ref"], d["T_cr"],
+                                d["px_proj"])
