@@ -255,6 +255,31 @@ int ygzfe_search_direct_batch(const ygzfe_frame *const *ref, int n_ref, const yg
                               int32_t *matched_item);
 
 /* ------------------------------------------------------------------------ */
+/* Stereo (Frame.cc:509-700)                                                 */
+/* Frame::ComputeStereoMatches (Frame.cc:509-682): left / right frames (their
+ * ORBextractor pyramids, mvImagePyramid), mvKeys + mDescriptors (nl) and
+ * mvKeysRight + mDescriptorsRight (nr <= 65535); mb = baseline, mbf = mb * fx
+ * (Frame.h).  Writes mvuRight[nl] and mvDepth[nl] (-1 where no match), with
+ * the row-band Hamming search, 11x11 SAD sliding window + parabola, and the
+ * 1.5 * 1.4 * median SAD outlier cut of the reference. */
+int ygzfe_stereo_matches(const ygzfe_frame *left, const ygzfe_frame *right, const ygzfe_kp *kl, const uint8_t *dl,
+                         int nl, const ygzfe_kp *kr, const uint8_t *dr, int nr, float mb, float mbf,
+                         float *u_right, float *depth);
+/* Batched: pair p matches batch frame d_left_idx[p] (left eye) against
+ * d_right_idx[p] (right eye), both extracted by ygzfe_batch_extract;
+ * d_u_right / d_depth are [n_pairs][kp_cap] rows of the left frame's keypoints. */
+int ygzfe_batch_stereo(ygzfe_batch *b, int n_pairs, const int32_t *d_left_idx, const int32_t *d_right_idx,
+                       float mb, float mbf, float *d_u_right, float *d_depth, void *stream);
+/* Frame::ComputeStereoFromRGBD (Frame.cc:684-700): d = imDepth(int v, int u)
+ * (CV_32F metres, row stride in floats); d > 0 -> depth d, uRight = u - mbf/d. */
+int ygzfe_stereo_from_rgbd(int device, const float *im_depth, int width, int height, int stride,
+                           const ygzfe_kp *kps, int n, float mbf, float *u_right, float *depth);
+/* Batched over the first n_frames frames of a batch: depth image f at
+ * d_depth_images + f * depth_pitch (floats); outputs [n_frames][kp_cap]. */
+int ygzfe_batch_stereo_rgbd(ygzfe_batch *b, int n_frames, const float *d_depth_images, size_t depth_pitch,
+                            int stride, float mbf, float *d_u_right, float *d_depth, void *stream);
+
+/* ------------------------------------------------------------------------ */
 /* Undistortion (Frame::ComputeImagePyramid, Frame.cc:775-790):              */
 /*   initUndistortRectifyMap(K, D, I, K, size, CV_16SC2, map1, map2) once     */
 /*   per camera, remap(img, map1, map2, INTER_LINEAR) per frame.              */

@@ -181,6 +181,19 @@ void ygzo_search_direct(const ygzo_cam *cam, uint8_t **ref_levels, uint8_t **cur
                         const ygzo_kp *kps, const float *pt_ref, const ygzo_se3 *T_cr, const float *px_proj,
                         float border, float *px_out, int *matched);
 
+/* ---------------- stereo (Frame.cc:509-700) ---------------- */
+/* Frame::ComputeStereoMatches (Frame.cc:509-682): left/right pyramids (same
+ * level sizes), keypoints (level-0 px) + N x 32 descriptors; mb = baseline,
+ * mbf = baseline * fx.  Writes mvuRight / mvDepth (-1 = none) and, if sad_out,
+ * the winning SAD per left keypoint (-1 = none).  Returns #depths kept. */
+int ygzo_stereo_matches(uint8_t **left_levels, uint8_t **right_levels, const int *lw, const int *lh,
+                        int nlevels, const float *scale, const float *inv_scale, const ygzo_kp *kl,
+                        const uint8_t *dl, int nl, const ygzo_kp *kr, const uint8_t *dr, int nr, float mb,
+                        float mbf, float *uRight, float *depth, int *sad_out);
+/* Frame::ComputeStereoFromRGBD (Frame.cc:684-700) */
+void ygzo_stereo_from_rgbd(const float *im_depth, int W, int H, int stride, const ygzo_kp *kps, int n, float mbf,
+                           float *uRight, float *depth);
+
 /* ---------------- undistort (Frame.cc:775-790) ---------------- */
 /* cv::initUndistortRectifyMap(K, D, I, K, (W,H), CV_16SC2): map1 [H][W][2]
  * (integer source x, y), map2 [H][W] (5-bit fractions, y*32 + x). */

@@ -189,13 +189,15 @@ struct ygzfe_batch {
     // align scratch
     DevBuf jobs, ascratch, pairs_tmp;
     size_t ascratch_per_job = 0;
+    // stereo scratch: jobs + winning SADs [pairs][kp_cap]
+    DevBuf sjobs, ssad;
     // per-stage kernel timing with hipEvents on the launch stream (no sync while recording)
     bool timing = false;
     std::vector<hipEvent_t> pool;
     struct Rec { int stage; hipEvent_t a, b; };
     std::vector<Rec> pending;
-    double total_ms[8] = {0};
-    long calls[8] = {0};
+    double total_ms[16] = {0};
+    long calls[16] = {0};
     hipEvent_t get_event() {
         hipEvent_t e = nullptr;
         if (!pool.empty()) { e = pool.back(); pool.pop_back(); }
@@ -231,8 +233,8 @@ struct ygzfe_batch {
 };
 
 static const char *kStageNames[] = {"pyramid", "blur7", "fast9_cells", "octree", "orient_rbrief", "hamming_best2",
-                                    "sparse_align"};
-constexpr int kNumStages = 7;
+                                    "sparse_align", "stereo"};
+constexpr int kNumStages = 8;
 enum { ST_PYR, ST_BLUR, ST_FAST, ST_OCT, ST_DESC, ST_HAM, ST_ALIGN };
 
 extern "C" {
@@ -1085,6 +1087,165 @@ extern "C" int ygzfe_search_direct_batch(const ygzfe_frame *const *ref, int n_re
     YGZ_HIP(hipMemcpyAsync(px_out, dout + o_pxo, 8 * (size_t)n_points, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipMemcpyAsync(matched_item, dout + o_m, 4 * (size_t)n_points, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipStreamSynchronize(st));
+    return YGZFE_OK;
+}
+
+// --------------------------------------------------------------------------
+// Stereo (Frame.cc:509-700)
+static StereoLevels stereo_levels_of(const Plan &P) {
+    StereoLevels lv;
+    memset(&lv, 0, sizeof(lv));
+    for (int l = 0; l < P.nlevels; l++) {
+        lv.w[l] = P.lv[l].w;
+        lv.h[l] = P.lv[l].h;
+        lv.off[l] = P.lv[l].off;
+        lv.scale[l] = P.lv[l].scale;
+        lv.inv_scale[l] = P.lv[l].inv_scale;
+    }
+    return lv;
+}
+
+static bool same_layout(const Plan &a, const Plan &b) {
+    if (a.nlevels != b.nlevels) return false;
+    for (int l = 0; l < a.nlevels; l++)
+        if (a.lv[l].w != b.lv[l].w || a.lv[l].h != b.lv[l].h || a.lv[l].off != b.lv[l].off ||
+            a.lv[l].scale != b.lv[l].scale)
+            return false;
+    return true;
+}
+
+static int check_octaves(const ygzfe_kp *k, int n, int nlevels) {
+    for (int i = 0; i < n; i++)
+        if (k[i].octave < 0 || k[i].octave >= nlevels) {
+            set_error("keypoint %d octave %d outside [0, %d)", i, k[i].octave, nlevels);
+            return YGZFE_EINVAL;
+        }
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_stereo_matches(const ygzfe_frame *left, const ygzfe_frame *right, const ygzfe_kp *kl,
+                                    const uint8_t *dl, int nl, const ygzfe_kp *kr, const uint8_t *dr, int nr,
+                                    float mb, float mbf, float *u_right, float *depth) {
+    if (!left || !right || nl < 0 || nr < 0 || (nl > 0 && (!kl || !dl || !u_right || !depth)) ||
+        (nr > 0 && (!kr || !dr))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (!same_layout(left->plan->hp(), right->plan->hp())) {
+        set_error("left and right pyramids differ in level sizes");
+        return YGZFE_EINVAL;
+    }
+    if (nr > 65535) { set_error("more than 65535 right keypoints"); return YGZFE_EINVAL; }
+    if (!(mb > 0.f)) { set_error("baseline must be positive"); return YGZFE_EINVAL; }
+    if (nl == 0) return YGZFE_OK;
+    const Plan &P = left->plan->hp();
+    YGZ_TRY(check_octaves(kl, nl, P.nlevels));
+    YGZ_TRY(check_octaves(kr, nr, P.nlevels));
+    ygzfe_extractor *ex = left->ex;
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    hipStream_t st = ex->stream;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    // in: [job][counts][kl][kr][dl][dr]  out: [u_right][depth][sad]
+    const size_t o_job = 0, o_cnt = al(sizeof(StereoJob)), o_kl = al(o_cnt + 8);
+    const size_t o_kr = al(o_kl + sizeof(ygzfe_kp) * (size_t)nl), o_dl = al(o_kr + sizeof(ygzfe_kp) * (size_t)nr);
+    const size_t o_dr = al(o_dl + 32 * (size_t)nl), in_bytes = al(o_dr + 32 * (size_t)nr);
+    const size_t o_u = in_bytes, o_d = al(o_u + 4 * (size_t)nl), o_s = al(o_d + 4 * (size_t)nl);
+    const size_t total = al(o_s + 4 * (size_t)nl);
+    YGZ_TRY(ex->direct_dev.ensure(total));
+    uint8_t *d = ex->direct_dev.as<uint8_t>();
+    std::vector<uint8_t> &h = ex->direct_host;
+    if (h.size() < in_bytes) h.resize(in_bytes);
+    StereoJob J;
+    J.left_pyr = left->pyr.as<uint8_t>();
+    J.right_pyr = right->pyr.as<uint8_t>();
+    J.left_kps = (const ygzfe_kp *)(d + o_kl);
+    J.right_kps = (const ygzfe_kp *)(d + o_kr);
+    J.left_desc = d + o_dl;
+    J.right_desc = d + o_dr;
+    J.n_left = (const int *)(d + o_cnt);
+    J.n_right = (const int *)(d + o_cnt + 4);
+    J.u_right = (float *)(d + o_u);
+    J.depth = (float *)(d + o_d);
+    J.sad = (int *)(d + o_s);
+    memcpy(h.data() + o_job, &J, sizeof(J));
+    const int cnt[2] = {nl, nr};
+    memcpy(h.data() + o_cnt, cnt, 8);
+    memcpy(h.data() + o_kl, kl, sizeof(ygzfe_kp) * (size_t)nl);
+    if (nr) memcpy(h.data() + o_kr, kr, sizeof(ygzfe_kp) * (size_t)nr);
+    memcpy(h.data() + o_dl, dl, 32 * (size_t)nl);
+    if (nr) memcpy(h.data() + o_dr, dr, 32 * (size_t)nr);
+    YGZ_HIP(hipMemcpyAsync(d, h.data(), in_bytes, hipMemcpyHostToDevice, st));
+    YGZ_HIP(launch_stereo((const StereoJob *)(d + o_job), 1, nl, stereo_levels_of(P), mb, mbf, st));
+    YGZ_HIP(hipMemcpyAsync(u_right, d + o_u, 4 * (size_t)nl, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipMemcpyAsync(depth, d + o_d, 4 * (size_t)nl, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipStreamSynchronize(st));
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_batch_stereo(ygzfe_batch *b, int n_pairs, const int32_t *d_left_idx, const int32_t *d_right_idx,
+                                  float mb, float mbf, float *d_u_right, float *d_depth, void *stream) {
+    if (!b || n_pairs < 0 || (n_pairs > 0 && (!d_left_idx || !d_right_idx || !d_u_right || !d_depth))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (!(mb > 0.f)) { set_error("baseline must be positive"); return YGZFE_EINVAL; }
+    if (n_pairs == 0) return YGZFE_OK;
+    YGZ_TRY(ensure_device(b->device));
+    hipStream_t st = stream ? (hipStream_t)stream : b->stream;
+    const Plan &P = b->plan->hp();
+    if (P.kp_cap > 65535) { set_error("kp_cap exceeds 65535"); return YGZFE_EINVAL; }
+    YGZ_TRY(b->sjobs.ensure(sizeof(StereoJob) * (size_t)n_pairs));
+    YGZ_TRY(b->ssad.ensure(4 * (size_t)n_pairs * P.kp_cap));
+    hipEvent_t t0 = b->begin(st);
+    YGZ_HIP(launch_build_stereo_jobs(n_pairs, b->pyr.as<uint8_t>(), P.pyr_bytes, b->ws.kps.as<ygzfe_kp>(),
+                                     b->ws.desc.as<uint8_t>(), b->ws.counts.as<int>(), P.kp_cap, d_left_idx,
+                                     d_right_idx, d_u_right, d_depth, b->ssad.as<int>(), b->sjobs.as<StereoJob>(),
+                                     st));
+    YGZ_HIP(launch_stereo(b->sjobs.as<StereoJob>(), n_pairs, P.kp_cap, stereo_levels_of(P), mb, mbf, st));
+    b->end(7, t0, st);
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_stereo_from_rgbd(int device, const float *im_depth, int width, int height, int stride,
+                                      const ygzfe_kp *kps, int n, float mbf, float *u_right, float *depth) {
+    if (!im_depth || width <= 0 || height <= 0 || stride < width || n < 0 ||
+        (n > 0 && (!kps || !u_right || !depth))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (n == 0) return YGZFE_OK;
+    YGZ_TRY(ensure_device(device));
+    const size_t img = 4 * (size_t)stride * height;
+    DevBuf di, dk, du, dd;
+    YGZ_TRY(di.ensure(img));
+    YGZ_TRY(dk.ensure(sizeof(ygzfe_kp) * (size_t)n));
+    YGZ_TRY(du.ensure(4 * (size_t)n));
+    YGZ_TRY(dd.ensure(4 * (size_t)n));
+    YGZ_HIP(hipMemcpy(di.p, im_depth, img, hipMemcpyHostToDevice));
+    YGZ_HIP(hipMemcpy(dk.p, kps, sizeof(ygzfe_kp) * (size_t)n, hipMemcpyHostToDevice));
+    YGZ_HIP(launch_stereo_rgbd(di.as<float>(), 0, width, height, stride, dk.as<ygzfe_kp>(), n, nullptr, n, 1, mbf,
+                               du.as<float>(), dd.as<float>(), nullptr));
+    YGZ_HIP(hipMemcpy(u_right, du.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    YGZ_HIP(hipMemcpy(depth, dd.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_batch_stereo_rgbd(ygzfe_batch *b, int n_frames, const float *d_depth_images,
+                                       size_t depth_pitch, int stride, float mbf, float *d_u_right, float *d_depth,
+                                       void *stream) {
+    if (!b || n_frames < 0 || (n_frames > 0 && (!d_depth_images || !d_u_right || !d_depth))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (n_frames > b->maxF) { set_error("n_frames %d > batch capacity %d", n_frames, b->maxF); return YGZFE_EINVAL; }
+    if (n_frames == 0) return YGZFE_OK;
+    YGZ_TRY(ensure_device(b->device));
+    hipStream_t st = stream ? (hipStream_t)stream : b->stream;
+    const Plan &P = b->plan->hp();
+    if (stride < P.lv[0].w) { set_error("depth stride < width"); return YGZFE_EINVAL; }
+    YGZ_HIP(launch_stereo_rgbd(d_depth_images, depth_pitch, P.lv[0].w, P.lv[0].h, stride, b->ws.kps.as<ygzfe_kp>(),
+                               P.kp_cap, b->ws.counts.as<int>(), P.kp_cap, n_frames, mbf, d_u_right, d_depth, st));
     return YGZFE_OK;
 }
 

@@ -67,6 +67,30 @@ hipError_t launch_find_direct(const uint8_t *const *ref_pyrs, const AlignLevels 
                               const float *pt_ref, const ygzfe_se3 *T_cr, float *px, int32_t *level,
                               uint8_t *ok, hipStream_t st);
 
+// One stereo pair of ComputeStereoMatches (Frame.cc:509-682)
+struct StereoJob {
+    const uint8_t *left_pyr, *right_pyr;
+    const ygzfe_kp *left_kps, *right_kps;
+    const uint8_t *left_desc, *right_desc;
+    const int *n_left, *n_right;
+    float *u_right, *depth;
+    int *sad;
+};
+struct StereoLevels {
+    int w[kMaxLevels], h[kMaxLevels];
+    uint32_t off[kMaxLevels];
+    float scale[kMaxLevels], inv_scale[kMaxLevels];
+};
+hipError_t launch_stereo(const StereoJob *jobs, int n_pairs, int max_left, const StereoLevels &lv, float mb, float mbf,
+                         hipStream_t st);
+hipError_t launch_build_stereo_jobs(int n, const uint8_t *pyr, size_t pyr_pitch, const ygzfe_kp *kps,
+                                    const uint8_t *desc, const int *counts, int kp_cap, const int32_t *left_idx,
+                                    const int32_t *right_idx, float *u_right, float *depth, int *sad,
+                                    StereoJob *jobs, hipStream_t st);
+hipError_t launch_stereo_rgbd(const float *im_depth, size_t depth_pitch, int W, int H, int stride,
+                              const ygzfe_kp *kps, int kp_pitch, const int *n_ptr, int n_max, int n_frames, float mbf,
+                              float *u_right, float *depth, hipStream_t st);
+
 // One (map point, keyframe) item of SearchLocalPointsDirect (host-packed, 80 B)
 struct DirectItem {
     ygzfe_kp kp;        // ref->mvKeys[index] (28 B)

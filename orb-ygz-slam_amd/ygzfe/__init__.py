@@ -353,6 +353,30 @@ def find_direct_projection_batch(ref_frames, cur_frame, cam, ref_index, kp_ref, 
     return px, lvl, ok.astype(bool)
 
 
+def stereo_matches(left_frame, right_frame, kl, dl, kr, dr, mb, mbf):
+    """Frame::ComputeStereoMatches (Frame.cc:509-682) -> (mvuRight, mvDepth), float32[nl], -1 = none."""
+    kl = np.ascontiguousarray(kl, KP_DTYPE)
+    kr = np.ascontiguousarray(kr, KP_DTYPE)
+    dl = np.ascontiguousarray(dl, np.uint8).reshape(-1, 32)
+    dr = np.ascontiguousarray(dr, np.uint8).reshape(-1, 32)
+    ur = np.zeros(len(kl), np.float32)
+    dep = np.zeros(len(kl), np.float32)
+    _check(lib().ygzfe_stereo_matches(left_frame.h, right_frame.h, _p(kl), _p(dl), len(kl), _p(kr), _p(dr), len(kr),
+                                      C.c_float(mb), C.c_float(mbf), _p(ur), _p(dep)), "stereo_matches")
+    return ur, dep
+
+
+def stereo_from_rgbd(im_depth, kps, mbf, device=0):
+    """Frame::ComputeStereoFromRGBD (Frame.cc:684-700) -> (mvuRight, mvDepth)."""
+    im = np.ascontiguousarray(im_depth, np.float32)
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    ur = np.zeros(len(kps), np.float32)
+    dep = np.zeros(len(kps), np.float32)
+    _check(lib().ygzfe_stereo_from_rgbd(device, _p(im), im.shape[1], im.shape[0], im.shape[1], _p(kps), len(kps),
+                                        C.c_float(mbf), _p(ur), _p(dep)), "stereo_from_rgbd")
+    return ur, dep
+
+
 def search_direct_batch(ref_frames, cur_frame, cam, item_ptr, ref_index, kp_ref, pt_ref, T_cr, px_proj, border=20.0):
     """Tracking::SearchLocalPointsDirect's per-point search (Tracking.cc:2337-2395), batched:
     point i tries items [item_ptr[i], item_ptr[i+1]) (its keyframes in SelectNearestKeyframe
@@ -460,6 +484,16 @@ class Batch:
                                               C.c_void_p(d_xyz), C.c_void_p(d_usable), C.byref(cam), max_level,
                                               min_level, C.c_void_p(d_T_init), C.c_void_p(d_out),
                                               C.c_void_p(stream)), "batch_sparse_align")
+
+    def stereo(self, n_pairs, d_left_idx, d_right_idx, mb, mbf, d_u_right, d_depth, stream=None):
+        _check(lib().ygzfe_batch_stereo(self.h, n_pairs, C.c_void_p(d_left_idx), C.c_void_p(d_right_idx),
+                                        C.c_float(mb), C.c_float(mbf), C.c_void_p(d_u_right), C.c_void_p(d_depth),
+                                        C.c_void_p(stream)), "batch_stereo")
+
+    def stereo_rgbd(self, n_frames, d_depth_images, depth_pitch, stride, mbf, d_u_right, d_depth, stream=None):
+        _check(lib().ygzfe_batch_stereo_rgbd(self.h, n_frames, C.c_void_p(d_depth_images), C.c_size_t(depth_pitch),
+                                             stride, C.c_float(mbf), C.c_void_p(d_u_right), C.c_void_p(d_depth),
+                                             C.c_void_p(stream)), "batch_stereo_rgbd")
 
     def timing(self, enable=True):
         ms = (C.c_float * 16)()

@@ -295,6 +295,37 @@ def search_direct(orc, kf_levels, cur_levels, cam, item_ptr, ref_index, kps, pt_
     return px_out, matched
 
 
+def stereo_matches(orc, left_levels, right_levels, kl, dl, kr, dr, mb, mbf):
+    """Frame::ComputeStereoMatches (Frame.cc:509-682) -> (uRight, depth, sad)."""
+    lp = (C.c_void_p * MAXL)(*[l.ctypes.data for l in left_levels])
+    rp = (C.c_void_p * MAXL)(*[l.ctypes.data for l in right_levels])
+    lw = (C.c_int * MAXL)(*[l.shape[1] for l in left_levels])
+    lh = (C.c_int * MAXL)(*[l.shape[0] for l in left_levels])
+    sc = (C.c_float * MAXL)(*orc.scale.tolist())
+    isc = (C.c_float * MAXL)(*orc.inv_scale.tolist())
+    kl = np.ascontiguousarray(kl, KP_DTYPE)
+    kr = np.ascontiguousarray(kr, KP_DTYPE)
+    dl = np.ascontiguousarray(dl, np.uint8)
+    dr = np.ascontiguousarray(dr, np.uint8)
+    ur = np.zeros(max(1, len(kl)), np.float32)
+    dep = np.zeros(max(1, len(kl)), np.float32)
+    sad = np.zeros(max(1, len(kl)), np.int32)
+    lib().ygzo_stereo_matches(lp, rp, lw, lh, len(left_levels), sc, isc, _p(kl), _p(dl), len(kl), _p(kr), _p(dr),
+                              len(kr), C.c_float(mb), C.c_float(mbf), _p(ur), _p(dep), _p(sad))
+    n = len(kl)
+    return ur[:n], dep[:n], sad[:n]
+
+
+def stereo_from_rgbd(im_depth, kps, mbf):
+    im = np.ascontiguousarray(im_depth, np.float32)
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    ur = np.zeros(max(1, len(kps)), np.float32)
+    dep = np.zeros(max(1, len(kps)), np.float32)
+    lib().ygzo_stereo_from_rgbd(_p(im), im.shape[1], im.shape[0], im.shape[1], _p(kps), len(kps), C.c_float(mbf),
+                                _p(ur), _p(dep))
+    return ur[:len(kps)], dep[:len(kps)]
+
+
 class RefFast:
     """The reference's own Thirdparty/fast, compiled by oracle/Makefile (oracle/_ref)."""
 

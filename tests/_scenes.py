@@ -170,3 +170,20 @@ def backproject_plane_np(cam, pose, uv):
     dw = np.array([quat_rot(qi, x) for x in d])
     lam = (PLANE_Z - ti[2]) / dw[:, 2]
     return ti + dw * lam[:, None]
+
+
+EUROC_BASELINE = 0.110073  # m, EuRoC cam0-cam1 (Examples/Stereo/EuRoC.yaml: Camera.bf / fx)
+
+
+def stereo_scene(seed, W=752, H=480, baseline=EUROC_BASELINE):
+    """A rectified stereo pair of the textured plane: the right camera is the left one
+    shifted by `baseline` along its x axis (X_r = X_l - b), so disparity = fx * b / Z."""
+    sc = PlaneScene(seed, W, H)
+    rng = np.random.default_rng(500 + seed)
+    q = quat_from_rotvec(rng.uniform(-0.15, 0.15, 3))  # tilted plane: depth varies over the image
+    t = rng.uniform(-0.2, 0.2, 3)
+    left = sc.render(q.astype(np.float32), t.astype(np.float32), seed * 2 + 1)
+    right = sc.render(q.astype(np.float32), (t - np.array([baseline, 0, 0])).astype(np.float32), seed * 2 + 2)
+    fx = sc.cam[0]
+    return {"scene": sc, "left": left, "right": right, "pose": (q, t), "mb": float(baseline),
+            "mbf": float(np.float32(baseline) * np.float32(fx))}
