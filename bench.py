@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--no-align", action="store_true")
     ap.add_argument("--no-undistort", action="store_true", help="skip the undistort-remap side measurement")
     ap.add_argument("--no-stage-timing", action="store_true", help="no per-stage hipEvents in the timed region")
+    ap.add_argument("--no-stereo", action="store_true", help="skip the stereo-matching side measurement")
     ap.add_argument("--no-direct", action="store_true", help="skip the SearchLocalPointsDirect side measurement")
     ap.add_argument("--latency-frames", type=int, default=200,
                     help="single-frame latency leg: frames timed one at a time through the host C ABI (0 = skip)")
@@ -235,6 +236,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_direct:
         direct_line = direct_leg(S, args.cpu_sample > 0)
 
+    # ------------------------------------------------ §8(f) rank 3: stereo matching
+    stereo_line = None
+    if rank == 0 and world == 1 and not args.no_stereo:
+        stereo_line = stereo_leg(S, dev, args.cpu_sample > 0)
+
     # ------------------------------------------------ single-frame latency (rank 0, N = 1)
     lat = None
     if rank == 0 and world == 1 and args.latency_frames > 0:
@@ -287,7 +293,8 @@ def main():
             "render_s": round(render_s, 2),
             "cpu_baseline": cpu,
             "latency": lat,
-            "next_rows": {"undistort_remap": und_line, "search_local_points_direct": direct_line},
+            "next_rows": {"undistort_remap": und_line, "search_local_points_direct": direct_line,
+                          "stereo_matches": stereo_line},
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -355,6 +362,67 @@ def latency_leg(frames, poses, sc, S, n_timed, warm=10):
             "median_align_ms": round(float(np.median(ts - te)), 4),
             "path": "host C ABI, one frame at a time: H2D 752x480 u8 -> pyramid -> extract -> D2H kps+desc -> "
                     "SparseImgAlign 3..1 (prev -> cur) -> D2H pose; median over frames after 10 warm-up frames"}
+
+
+def stereo_leg(S, dev, with_cpu, n_pairs=64, reps=20):
+    """Frame::ComputeStereoMatches (Frame.cc:509-682) on EuRoC-shaped rectified pairs
+    (C2 extraction, baseline 0.11 m): the batched kernel over n_pairs pairs resident in
+    HBM (HIP events, after the batch extract), and one pair through the host C ABI.
+    CPU: the oracle's restatement, 1 thread."""
+    import torch
+    import ygzfe
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    scenes = [S.stereo_scene(100 + i, W, H) for i in range(n_pairs)]
+    frames = np.stack([im for d in scenes for im in (d["left"], d["right"])])
+    b = ygzfe.Batch((nf, sf, nl, ini, mn, 0), dev.index or 0, W, H, len(frames))
+    b.upload(frames)
+    b.extract(len(frames))
+    b.check()
+    cap = b.kp_cap
+    li = torch.arange(0, 2 * n_pairs, 2, dtype=torch.int32, device=dev)
+    ri = li + 1
+    ur = torch.zeros((n_pairs, cap), dtype=torch.float32, device=dev)
+    dp = torch.zeros((n_pairs, cap), dtype=torch.float32, device=dev)
+    mb, mbf = scenes[0]["mb"], scenes[0]["mbf"]
+    st = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
+    for _ in range(3):
+        b.stereo(n_pairs, li.data_ptr(), ri.data_ptr(), mb, mbf, ur.data_ptr(), dp.data_ptr(), st.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        b.stereo(n_pairs, li.data_ptr(), ri.data_ptr(), mb, mbf, ur.data_ptr(), dp.data_ptr(), st.cuda_stream)
+    e1.record(st)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    kept = float((dp > 0).sum().item()) / n_pairs
+    kl, dl = b.result(0)
+    kr, dr = b.result(1)
+    ex = ygzfe.ORBextractor(nf, sf, nl, ini, mn, device=dev.index or 0)
+    fl, fr = ex.ComputePyramid(scenes[0]["left"]), ex.ComputePyramid(scenes[0]["right"])
+    for _ in range(3):
+        ygzfe.stereo_matches(fl, fr, kl, dl, kr, dr, mb, mbf)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ygzfe.stereo_matches(fl, fr, kl, dl, kr, dr, mb, mbf)
+        ts.append(time.perf_counter() - t0)
+    line = {"pairs": n_pairs, "ms_per_launch": round(ms, 4), "pairs_per_s": round(n_pairs / (ms * 1e-3), 1),
+            "mean_left_kps": round(float(np.mean([b.result(2 * i)[0].shape[0] for i in range(min(8, n_pairs))])), 1),
+            "mean_depths": round(kept, 1), "single_pair_host_ms": round(float(np.median(ts)) * 1e3, 4),
+            "path": "batched: frames + keypoints + descriptors resident (ygzfe_batch_stereo); single: host C ABI"}
+    if with_cpu:
+        import _oracle as O
+        orc = O.OrbOracle(nf, sf, nl, ini, mn)
+        ll, rl = orc.pyramid(scenes[0]["left"]), orc.pyramid(scenes[0]["right"])
+        tc = []
+        for _ in range(10):
+            t0 = time.perf_counter()
+            O.stereo_matches(orc, ll, rl, kl, dl, kr, dr, mb, mbf)
+            tc.append(time.perf_counter() - t0)
+        line["cpu_port_ms_per_pair"] = round(float(np.median(tc)) * 1e3, 4)
+        line["cpu_cores"] = 1
+    return line
 
 
 def direct_leg(S, with_cpu, reps=50):
