@@ -280,6 +280,36 @@ int ygzfe_batch_stereo_rgbd(ygzfe_batch *b, int n_frames, const float *d_depth_i
                             int stride, float mbf, float *d_u_right, float *d_depth, void *stream);
 
 /* ------------------------------------------------------------------------ */
+/* DBoW2 vocabulary / Frame::ComputeBoW (Frame.cc:495-500)                   */
+/* TemplatedVocabulary<FORB::TDescriptor, FORB> (Thirdparty/DBoW2) resident in
+ * HBM.  scoring: L1_NORM 0, L2_NORM 1, CHI_SQUARE 2, KL 3, BHATTACHARYYA 4,
+ * DOT_PRODUCT 5; weighting: TF_IDF 0, TF 1, IDF 2, BINARY 3 (ORBvoc: 0 0). */
+typedef struct ygzfe_vocab ygzfe_vocab;
+/* From node arrays as loadFromTextFile builds them (TemplatedVocabulary.h:
+ * 1362-1448): node 0 = root; node i >= 1 is the next child of parent[i] < i,
+ * desc[32 i], weight[i]; is_leaf[i] gives it the next word id. */
+int ygzfe_vocab_create(int device, int k, int L, int scoring, int weighting, int n_nodes, const int32_t *parent,
+                       const uint8_t *is_leaf, const uint8_t *desc, const double *weight, ygzfe_vocab **out);
+/* loadFromTextFile (ORBvoc.txt, TemplatedVocabulary.h:1362) / loadFromBinaryFile (:1478) */
+int ygzfe_vocab_load_text(int device, const char *path, ygzfe_vocab **out);
+int ygzfe_vocab_load_binary(int device, const char *path, ygzfe_vocab **out);
+void ygzfe_vocab_destroy(ygzfe_vocab *v);
+int ygzfe_vocab_info(const ygzfe_vocab *v, int *k, int *L, int *scoring, int *weighting, int *n_nodes, int *n_words);
+/* transform(feature, word_id, weight, &nid, levelsup) per descriptor (TemplatedVocabulary.h:1241-1281) */
+int ygzfe_bow_transform(ygzfe_vocab *v, const uint8_t *desc, int n, int levelsup, int32_t *word, double *weight,
+                        int32_t *nid);
+/* transform(features, mBowVec, mFeatVec, levelsup) (TemplatedVocabulary.h:1150-1212) for one
+ * frame's n <= 8192 descriptors: BowVector = ascending (bow_words, bow_values)[n_words],
+ * FeatureVector = (fv_nodes, fv_features)[n_fv] in (node, feature) order; arrays sized n. */
+int ygzfe_compute_bow(ygzfe_vocab *v, const uint8_t *desc, int n, int levelsup, int32_t *bow_words,
+                      double *bow_values, int *n_words, int32_t *fv_nodes, int32_t *fv_features, int *n_fv);
+/* Batched over the first n_frames extracted frames of a batch: outputs [n_frames][kp_cap]
+ * rows and per-frame counts, device pointers, on `stream`. */
+int ygzfe_batch_compute_bow(ygzfe_batch *b, ygzfe_vocab *v, int n_frames, int levelsup, int32_t *d_bow_words,
+                            double *d_bow_values, int *d_n_words, int32_t *d_fv_nodes, int32_t *d_fv_features,
+                            int *d_n_fv, void *stream);
+
+/* ------------------------------------------------------------------------ */
 /* Undistortion (Frame::ComputeImagePyramid, Frame.cc:775-790):              */
 /*   initUndistortRectifyMap(K, D, I, K, size, CV_16SC2, map1, map2) once     */
 /*   per camera, remap(img, map1, map2, INTER_LINEAR) per frame.              */

@@ -194,6 +194,22 @@ int ygzo_stereo_matches(uint8_t **left_levels, uint8_t **right_levels, const int
 void ygzo_stereo_from_rgbd(const float *im_depth, int W, int H, int stride, const ygzo_kp *kps, int n, float mbf,
                            float *uRight, float *depth);
 
+/* ---------------- DBoW2 transform (Frame::ComputeBoW, Frame.cc:495-500) ---------------- */
+typedef struct ygzo_vocab ygzo_vocab;
+/* nodes 0..n-1 as loadFromTextFile leaves them: parent[i] < i for i >= 1,
+ * is_leaf / desc (32 B) / weight per node (node 0 = root, unused fields). */
+ygzo_vocab *ygzo_vocab_create(int k, int L, int scoring, int weighting, int n_nodes, const int32_t *parent,
+                              const uint8_t *is_leaf, const uint8_t *desc, const double *weight);
+void ygzo_vocab_destroy(ygzo_vocab *v);
+/* transform(feature, word_id, weight, &nid, levelsup) (TemplatedVocabulary.h:1241-1281) */
+void ygzo_bow_transform_one(const ygzo_vocab *v, const uint8_t *f, int levelsup, int *word, double *weight,
+                            int *nid);
+/* transform(features, BowVector, FeatureVector, levelsup) (TemplatedVocabulary.h:1150-1212):
+ * BowVector as ascending (word, value) arrays, FeatureVector as (node, feature)
+ * pairs in map order; all arrays sized n.  Returns #words. */
+int ygzo_compute_bow(const ygzo_vocab *v, const uint8_t *desc, int n, int levelsup, int32_t *bow_words,
+                     double *bow_values, int *n_words, int32_t *fv_nodes, int32_t *fv_features, int *n_fv);
+
 /* ---------------- undistort (Frame.cc:775-790) ---------------- */
 /* cv::initUndistortRectifyMap(K, D, I, K, (W,H), CV_16SC2): map1 [H][W][2]
  * (integer source x, y), map2 [H][W] (5-bit fractions, y*32 + x). */

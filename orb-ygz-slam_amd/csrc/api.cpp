@@ -191,6 +191,8 @@ struct ygzfe_batch {
     size_t ascratch_per_job = 0;
     // stereo scratch: jobs + winning SADs [pairs][kp_cap]
     DevBuf sjobs, ssad;
+    // BoW scratch: per-feature word / weight / node [frames][kp_cap]
+    DevBuf bow_word, bow_weight, bow_nid;
     // per-stage kernel timing with hipEvents on the launch stream (no sync while recording)
     bool timing = false;
     std::vector<hipEvent_t> pool;
@@ -1246,6 +1248,310 @@ extern "C" int ygzfe_batch_stereo_rgbd(ygzfe_batch *b, int n_frames, const float
     if (stride < P.lv[0].w) { set_error("depth stride < width"); return YGZFE_EINVAL; }
     YGZ_HIP(launch_stereo_rgbd(d_depth_images, depth_pitch, P.lv[0].w, P.lv[0].h, stride, b->ws.kps.as<ygzfe_kp>(),
                                P.kp_cap, b->ws.counts.as<int>(), P.kp_cap, n_frames, mbf, d_u_right, d_depth, st));
+    return YGZFE_OK;
+}
+
+// --------------------------------------------------------------------------
+// DBoW2 vocabulary + Frame::ComputeBoW (Frame.cc:495-500)
+struct ygzfe_vocab {
+    int device = 0;
+    int k = 0, L = 0, scoring = 0, weighting = 0, n_nodes = 0, n_words = 0;
+    DevBuf child_ptr, slot_node, slot_desc, word_id, weight;
+    DevBuf scratch;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    VocabDev dev() const {
+        VocabDev V;
+        V.n_nodes = n_nodes;
+        V.L = L;
+        V.child_ptr = child_ptr.as<int32_t>();
+        V.slot_node = slot_node.as<int32_t>();
+        V.slot_desc = slot_desc.as<uint8_t>();
+        V.word_id = word_id.as<int32_t>();
+        V.weight = weight.as<double>();
+        return V;
+    }
+};
+
+// nodes as TemplatedVocabulary::loadFromTextFile leaves them (TemplatedVocabulary.h:1362-1448)
+static int vocab_build(int device, int k, int L, int scoring, int weighting, int n, const int32_t *parent,
+                       const uint8_t *is_leaf, const uint8_t *desc, const double *weight, ygzfe_vocab **out) {
+    if (!out || n < 1 || (n > 1 && (!parent || !is_leaf || !desc || !weight))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (k < 0 || k > 20 || L < 1 || L > 10 || scoring < 0 || scoring > 5 || weighting < 0 || weighting > 3) {
+        set_error("vocabulary header k=%d L=%d scoring=%d weighting=%d outside DBoW2's accepted ranges", k, L, scoring,
+                  weighting);
+        return YGZFE_EINVAL;
+    }
+    std::vector<int32_t> cptr((size_t)n + 1, 0), slot_node((size_t)std::max(1, n - 1)), wid((size_t)n, 0);
+    std::vector<uint8_t> sdesc((size_t)std::max(1, n - 1) * 32);
+    std::vector<double> w((size_t)n, 0.0);
+    for (int i = 1; i < n; i++) {
+        if (parent[i] < 0 || parent[i] >= i) {
+            set_error("node %d: parent %d is not an earlier node", i, parent[i]);
+            return YGZFE_EINVAL;
+        }
+        cptr[parent[i] + 1]++;
+    }
+    for (int i = 0; i < n; i++) {
+        if (cptr[i + 1] > 255) { set_error("node %d has %d > 255 children", i, cptr[i + 1]); return YGZFE_EINVAL; }
+        cptr[i + 1] += cptr[i];
+    }
+    std::vector<int32_t> fill(cptr.begin(), cptr.end() - 1);
+    int words = 0;
+    for (int i = 1; i < n; i++) {
+        const int sl = fill[parent[i]]++;  // children.push_back in node order
+        slot_node[sl] = i;
+        memcpy(&sdesc[(size_t)sl * 32], desc + (size_t)i * 32, 32);
+        w[i] = weight[i];
+        if (is_leaf[i]) wid[i] = words++;
+    }
+    YGZ_TRY(ensure_device(device));
+    std::unique_ptr<ygzfe_vocab> v(new ygzfe_vocab());
+    v->device = device;
+    v->k = k;
+    v->L = L;
+    v->scoring = scoring;
+    v->weighting = weighting;
+    v->n_nodes = n;
+    v->n_words = words;
+    YGZ_TRY(v->child_ptr.ensure(4 * cptr.size()));
+    YGZ_TRY(v->slot_node.ensure(4 * slot_node.size()));
+    YGZ_TRY(v->slot_desc.ensure(sdesc.size()));
+    YGZ_TRY(v->word_id.ensure(4 * wid.size()));
+    YGZ_TRY(v->weight.ensure(8 * w.size()));
+    YGZ_HIP(hipMemcpy(v->child_ptr.p, cptr.data(), 4 * cptr.size(), hipMemcpyHostToDevice));
+    YGZ_HIP(hipMemcpy(v->slot_node.p, slot_node.data(), 4 * slot_node.size(), hipMemcpyHostToDevice));
+    YGZ_HIP(hipMemcpy(v->slot_desc.p, sdesc.data(), sdesc.size(), hipMemcpyHostToDevice));
+    YGZ_HIP(hipMemcpy(v->word_id.p, wid.data(), 4 * wid.size(), hipMemcpyHostToDevice));
+    YGZ_HIP(hipMemcpy(v->weight.p, w.data(), 8 * w.size(), hipMemcpyHostToDevice));
+    YGZ_HIP(hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking));
+    *out = v.release();
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_vocab_create(int device, int k, int L, int scoring, int weighting, int n_nodes,
+                                  const int32_t *parent, const uint8_t *is_leaf, const uint8_t *desc,
+                                  const double *weight, ygzfe_vocab **out) {
+    return vocab_build(device, k, L, scoring, weighting, n_nodes, parent, is_leaf, desc, weight, out);
+}
+
+extern "C" int ygzfe_vocab_load_text(int device, const char *path, ygzfe_vocab **out) {
+    // TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1362-1448), e.g. Vocabulary/ORBvoc.txt.
+    // Lines holding only whitespace are skipped (the reference turns a trailing
+    // empty line into an uninitialised child of the root).
+    if (!path || !out) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    FILE *fp = fopen(path, "r");
+    if (!fp) { set_error("cannot open %s", path); return YGZFE_EINVAL; }
+    int k = -1, L = -1, n1 = -1, n2 = -1;
+    std::string line;
+    auto getline = [&](std::string &l) {
+        l.clear();
+        int c;
+        while ((c = fgetc(fp)) != EOF && c != '\n') l.push_back((char)c);
+        return !(c == EOF && l.empty());
+    };
+    if (!getline(line) || sscanf(line.c_str(), "%d %d %d %d", &k, &L, &n1, &n2) != 4) {
+        fclose(fp);
+        set_error("%s: not a DBoW2 text vocabulary", path);
+        return YGZFE_EINVAL;
+    }
+    std::vector<int32_t> parent(1, 0);
+    std::vector<uint8_t> leaf(1, 0), desc(32, 0);
+    std::vector<double> weight(1, 0.0);
+    while (getline(line)) {
+        const char *c = line.c_str();
+        while (*c == ' ' || *c == '\t' || *c == '\r') c++;
+        if (!*c) continue;
+        char *end = nullptr;
+        const long pid = strtol(c, &end, 10);
+        c = end;
+        const long isleaf = strtol(c, &end, 10);
+        c = end;
+        uint8_t d[32];
+        for (int i = 0; i < 32; i++) {
+            d[i] = (uint8_t)strtol(c, &end, 10);
+            c = end;
+        }
+        const double w = strtod(c, &end);
+        parent.push_back((int32_t)pid);
+        leaf.push_back(isleaf > 0);
+        desc.insert(desc.end(), d, d + 32);
+        weight.push_back(w);
+    }
+    fclose(fp);
+    return vocab_build(device, k, L, n1, n2, (int)parent.size(), parent.data(), leaf.data(), desc.data(),
+                       weight.data(), out);
+}
+
+extern "C" int ygzfe_vocab_load_binary(int device, const char *path, ygzfe_vocab **out) {
+    // TemplatedVocabulary::loadFromBinaryFile (TemplatedVocabulary.h:1478-1525): header
+    // nb_nodes, size_node, k, L, scoring, weighting; records {int parent; u8 desc[32];
+    // float weight; bool leaf}.  The reference's `while (!f.eof())` runs once more
+    // after the last record with the buffer unchanged, appending a copy of the last
+    // node; that copy is reproduced here.
+    if (!path || !out) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    FILE *fp = fopen(path, "rb");
+    if (!fp) { set_error("cannot open %s", path); return YGZFE_EINVAL; }
+    uint32_t nb = 0, sz = 0;
+    int32_t hk = 0, hL = 0, hs = 0, hw = 0;
+    if (fread(&nb, 4, 1, fp) != 1 || fread(&sz, 4, 1, fp) != 1 || fread(&hk, 4, 1, fp) != 1 ||
+        fread(&hL, 4, 1, fp) != 1 || fread(&hs, 4, 1, fp) != 1 || fread(&hw, 4, 1, fp) != 1 || sz < 41) {
+        fclose(fp);
+        set_error("%s: not a DBoW2 binary vocabulary", path);
+        return YGZFE_EINVAL;
+    }
+    std::vector<int32_t> parent(1, 0);
+    std::vector<uint8_t> leaf(1, 0), desc(32, 0), buf(sz, 0);
+    std::vector<double> weight(1, 0.0);
+    bool any = false;
+    for (;;) {
+        const bool got = fread(buf.data(), 1, sz, fp) == sz;
+        if (!got && !any) break;
+        int32_t pid;
+        float w;
+        memcpy(&pid, buf.data(), 4);
+        memcpy(&w, buf.data() + 36, 4);
+        parent.push_back(pid);
+        desc.insert(desc.end(), buf.data() + 4, buf.data() + 36);
+        weight.push_back((double)w);
+        leaf.push_back(buf[40] != 0);
+        any = true;
+        if (!got) break;
+    }
+    fclose(fp);
+    return vocab_build(device, hk, hL, hs, hw, (int)parent.size(), parent.data(), leaf.data(), desc.data(),
+                       weight.data(), out);
+}
+
+extern "C" void ygzfe_vocab_destroy(ygzfe_vocab *v) {
+    if (!v) return;
+    (void)hipSetDevice(v->device);
+    if (v->stream) (void)hipStreamSynchronize(v->stream), (void)hipStreamDestroy(v->stream);
+    delete v;
+}
+
+extern "C" int ygzfe_vocab_info(const ygzfe_vocab *v, int *k, int *L, int *scoring, int *weighting, int *n_nodes,
+                                int *n_words) {
+    if (!v) { set_error("null vocabulary"); return YGZFE_EINVAL; }
+    if (k) *k = v->k;
+    if (L) *L = v->L;
+    if (scoring) *scoring = v->scoring;
+    if (weighting) *weighting = v->weighting;
+    if (n_nodes) *n_nodes = v->n_nodes;
+    if (n_words) *n_words = v->n_words;
+    return YGZFE_OK;
+}
+
+// one frame: host descriptors -> device -> transform (+ vectors) -> host
+static int bow_one(ygzfe_vocab *v, const uint8_t *desc, int n, int levelsup, bool vectors, int32_t *word,
+                   double *weight, int32_t *nid, int32_t *bow_words, double *bow_values, int *n_words,
+                   int32_t *fv_nodes, int32_t *fv_features, int *n_fv) {
+    if (n > kBowMaxFeatures) { set_error("%d descriptors > %d per frame", n, kBowMaxFeatures); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(v->device));
+    std::lock_guard<std::mutex> lk(v->mu);
+    hipStream_t st = v->stream;
+    const size_t N = (size_t)std::max(n, 1);
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_d = 0, o_w = al(32 * N), o_v = al(o_w + 4 * N), o_n = al(o_v + 8 * N);
+    const size_t o_bw = al(o_n + 4 * N), o_bv = al(o_bw + 4 * N), o_fn = al(o_bv + 8 * N), o_ff = al(o_fn + 4 * N);
+    const size_t o_c = al(o_ff + 4 * N), total = al(o_c + 16);
+    YGZ_TRY(v->scratch.ensure(total));
+    uint8_t *d = v->scratch.as<uint8_t>();
+    int *cnt = (int *)(d + o_c);
+    if (n > 0) YGZ_HIP(hipMemcpyAsync(d + o_d, desc, 32 * (size_t)n, hipMemcpyHostToDevice, st));
+    const int nn = v->n_words > 0 ? n : 0;  // transform() returns early on an empty vocabulary
+    YGZ_HIP(launch_bow_transform(v->dev(), d + o_d, 0, nullptr, nn, 1, levelsup, (int32_t *)(d + o_w),
+                                 (double *)(d + o_v), (int32_t *)(d + o_n), 0, st));
+    if (!vectors) {
+        if (nn > 0) {
+            YGZ_HIP(hipMemcpyAsync(word, d + o_w, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+            YGZ_HIP(hipMemcpyAsync(weight, d + o_v, 8 * (size_t)n, hipMemcpyDeviceToHost, st));
+            YGZ_HIP(hipMemcpyAsync(nid, d + o_n, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+        }
+        YGZ_HIP(hipStreamSynchronize(st));
+        return YGZFE_OK;
+    }
+    YGZ_HIP(launch_bow_vectors(nullptr, nn, 1, (int32_t *)(d + o_w), (double *)(d + o_v), (int32_t *)(d + o_n), 0,
+                               v->weighting, v->scoring, (int32_t *)(d + o_bw), (double *)(d + o_bv), cnt,
+                               (int32_t *)(d + o_fn), (int32_t *)(d + o_ff), cnt + 1, 0, st));
+    int hc[2] = {0, 0};
+    YGZ_HIP(hipMemcpyAsync(hc, cnt, 8, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipStreamSynchronize(st));
+    *n_words = hc[0];
+    *n_fv = hc[1];
+    if (hc[0] > 0) {
+        YGZ_HIP(hipMemcpyAsync(bow_words, d + o_bw, 4 * (size_t)hc[0], hipMemcpyDeviceToHost, st));
+        YGZ_HIP(hipMemcpyAsync(bow_values, d + o_bv, 8 * (size_t)hc[0], hipMemcpyDeviceToHost, st));
+    }
+    if (hc[1] > 0) {
+        YGZ_HIP(hipMemcpyAsync(fv_nodes, d + o_fn, 4 * (size_t)hc[1], hipMemcpyDeviceToHost, st));
+        YGZ_HIP(hipMemcpyAsync(fv_features, d + o_ff, 4 * (size_t)hc[1], hipMemcpyDeviceToHost, st));
+    }
+    YGZ_HIP(hipStreamSynchronize(st));
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_bow_transform(ygzfe_vocab *v, const uint8_t *desc, int n, int levelsup, int32_t *word,
+                                   double *weight, int32_t *nid) {
+    if (!v || n < 0 || (n > 0 && (!desc || !word || !weight || !nid))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (n > 0 && v->n_words == 0) { set_error("empty vocabulary"); return YGZFE_EINVAL; }
+    if (n == 0) return YGZFE_OK;
+    return bow_one(v, desc, n, levelsup, false, word, weight, nid, nullptr, nullptr, nullptr, nullptr, nullptr,
+                   nullptr);
+}
+
+extern "C" int ygzfe_compute_bow(ygzfe_vocab *v, const uint8_t *desc, int n, int levelsup, int32_t *bow_words,
+                                 double *bow_values, int *n_words, int32_t *fv_nodes, int32_t *fv_features,
+                                 int *n_fv) {
+    if (!v || n < 0 || !n_words || !n_fv ||
+        (n > 0 && (!desc || !bow_words || !bow_values || !fv_nodes || !fv_features))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    *n_words = 0;
+    *n_fv = 0;
+    if (n == 0) return YGZFE_OK;
+    return bow_one(v, desc, n, levelsup, true, nullptr, nullptr, nullptr, bow_words, bow_values, n_words, fv_nodes,
+                   fv_features, n_fv);
+}
+
+extern "C" int ygzfe_batch_compute_bow(ygzfe_batch *b, ygzfe_vocab *v, int n_frames, int levelsup,
+                                       int32_t *d_bow_words, double *d_bow_values, int *d_n_words,
+                                       int32_t *d_fv_nodes, int32_t *d_fv_features, int *d_n_fv, void *stream) {
+    if (!b || !v || n_frames < 0 ||
+        (n_frames > 0 && (!d_bow_words || !d_bow_values || !d_n_words || !d_fv_nodes || !d_fv_features || !d_n_fv))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (n_frames > b->maxF) { set_error("n_frames %d > batch capacity %d", n_frames, b->maxF); return YGZFE_EINVAL; }
+    if (b->device != v->device) { set_error("vocabulary and batch live on different devices"); return YGZFE_EINVAL; }
+    if (n_frames == 0) return YGZFE_OK;
+    YGZ_TRY(ensure_device(b->device));
+    hipStream_t st = stream ? (hipStream_t)stream : b->stream;
+    const Plan &P = b->plan->hp();
+    if (P.kp_cap > kBowMaxFeatures) { set_error("kp_cap %d > %d", P.kp_cap, kBowMaxFeatures); return YGZFE_EINVAL; }
+    const size_t cells = (size_t)n_frames * P.kp_cap;
+    YGZ_TRY(b->bow_word.ensure(4 * cells));
+    YGZ_TRY(b->bow_weight.ensure(8 * cells));
+    YGZ_TRY(b->bow_nid.ensure(4 * cells));
+    if (v->n_words == 0) {  // transform() clears the vectors and returns
+        YGZ_HIP(hipMemsetAsync(d_n_words, 0, 4 * (size_t)n_frames, st));
+        YGZ_HIP(hipMemsetAsync(d_n_fv, 0, 4 * (size_t)n_frames, st));
+        return YGZFE_OK;
+    }
+    YGZ_HIP(launch_bow_transform(v->dev(), b->ws.desc.as<uint8_t>(), (size_t)P.kp_cap * 32, b->ws.counts.as<int>(),
+                                 P.kp_cap, n_frames, levelsup, b->bow_word.as<int32_t>(), b->bow_weight.as<double>(),
+                                 b->bow_nid.as<int32_t>(), P.kp_cap, st));
+    YGZ_HIP(launch_bow_vectors(b->ws.counts.as<int>(), 0, n_frames, b->bow_word.as<int32_t>(),
+                               b->bow_weight.as<double>(), b->bow_nid.as<int32_t>(), P.kp_cap, v->weighting,
+                               v->scoring, d_bow_words, d_bow_values, d_n_words, d_fv_nodes, d_fv_features, d_n_fv,
+                               P.kp_cap, st));
     return YGZFE_OK;
 }
 

@@ -1,0 +1,234 @@
+// bow.hip — DBoW2 TemplatedVocabulary::transform for Frame::ComputeBoW
+// (Frame.cc:495-500) on gfx950.
+//
+// Vocabulary in HBM (VocabDev): per node its children as a CSR slot range
+// [child_ptr[n], child_ptr[n+1]) and, per slot, the child's node id and its
+// 32-byte descriptor stored in slot order, so the k children of a node are k
+// consecutive 32-byte rows (one coalesced read per level).  word_id / weight
+// (double, DBoW2's WordValue) per node.
+//
+// k_bow_transform: 16 lanes per descriptor (16 descriptors per 256-thread
+// workgroup, blockIdx.y = frame).  Per level the lanes take one child each,
+// key = (FORB::distance << 8) | child slot, and a 16-lane min gives the first
+// strict minimum — TemplatedVocabulary.h:1259-1270's `d < best_d` from the
+// first child.  The descent stops at a node without children (isLeaf());
+// the node reached at level L - levelsup is the FeatureVector node.
+//
+// k_bow_vectors: one 1024-thread workgroup per frame builds the BowVector and
+// FeatureVector of TemplatedVocabulary::transform(features, v, fv, levelsup)
+// (:1150-1212): bitonic sort of (word, feature) keys in LDS; per word run the
+// value is w folded c times in feature order (addWeight; addIfNotExist keeps
+// w); DotProduct scoring divides TF / TF_IDF values by v.size(); the others
+// normalise (BowVector.cpp:62-84) with the norm summed sequentially in word
+// order, as std::map iteration does.  The FeatureVector is the (node,
+// feature)-sorted list of the same features.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace ygzfe {
+
+constexpr int kBowLanes = 16;
+
+__global__ __launch_bounds__(256) void k_bow_transform(VocabDev V, const uint8_t *__restrict__ desc,
+                                                       size_t desc_pitch, const int *__restrict__ counts,
+                                                       int n_static, int levelsup, int32_t *__restrict__ word_out,
+                                                       double *__restrict__ weight_out,
+                                                       int32_t *__restrict__ nid_out, size_t out_pitch) {
+    const int f = blockIdx.y;
+    const int n = counts ? counts[f] : n_static;
+    const int i = blockIdx.x * (256 / kBowLanes) + (threadIdx.x / kBowLanes);
+    const int sub = threadIdx.x & (kBowLanes - 1);
+    if (i >= n) return;  // whole 16-lane group
+    const uint4 *fp = (const uint4 *)(desc + (size_t)f * desc_pitch + (size_t)i * 32);
+    const uint4 a0 = fp[0], a1 = fp[1];
+    const int nid_level = V.L - levelsup;
+    int nid = 0;
+    int node = 0, level = 0;
+    for (int guard = 0; guard < V.n_nodes; guard++) {
+        const int b = V.child_ptr[node], e = V.child_ptr[node + 1];
+        if (e == b) break;  // isLeaf()
+        uint32_t key = 0xFFFFFFFFu;
+        for (int c = sub; c < e - b; c += kBowLanes) {
+            const uint4 *dp = (const uint4 *)(V.slot_desc + (size_t)(b + c) * 32);
+            const uint4 b0 = dp[0], b1 = dp[1];
+            const int d = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+                          __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+            key = min(key, ((uint32_t)d << 8) | (uint32_t)c);
+        }
+#pragma unroll
+        for (int o = kBowLanes / 2; o >= 1; o >>= 1) key = min(key, (uint32_t)__shfl_xor((int)key, o, 64));
+        node = V.slot_node[b + (int)(key & 0xFFu)];
+        ++level;
+        if (level == nid_level) nid = node;
+    }
+    if (sub == 0) {
+        const size_t o = (size_t)f * out_pitch + i;
+        word_out[o] = V.word_id[node];
+        weight_out[o] = V.weight[node];
+        nid_out[o] = nid;
+    }
+}
+
+hipError_t launch_bow_transform(const VocabDev &V, const uint8_t *desc, size_t desc_pitch, const int *counts,
+                                int n_max, int n_frames, int levelsup, int32_t *word, double *weight, int32_t *nid,
+                                size_t out_pitch, hipStream_t st) {
+    if (n_max <= 0 || n_frames <= 0) return hipSuccess;
+    const int per = 256 / kBowLanes;
+    hipLaunchKernelGGL(k_bow_transform, dim3((n_max + per - 1) / per, n_frames), dim3(256), 0, st, V, desc,
+                       desc_pitch, counts, n_max, levelsup, word, weight, nid, out_pitch);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+constexpr int kBowSortMax = kBowMaxFeatures;  // keys sorted in LDS per frame (64 KB)
+
+__device__ void bow_bitonic(uint64_t *s, int P) {
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = threadIdx.x; t < P; t += blockDim.x) {
+                const int p = t ^ j;
+                if (p > t) {
+                    const uint64_t a = s[t], b = s[p];
+                    const bool up = (t & k) == 0;
+                    if ((a > b) == up) {
+                        s[t] = b;
+                        s[p] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+// exclusive scan of one int per thread over the workgroup (1024 threads)
+__device__ int bow_block_scan(int v, int *s_tmp, int *total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_tmp[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int w = 0; w < nw; w++) {
+            const int t = s_tmp[w];
+            s_tmp[w] = acc;
+            acc += t;
+        }
+        s_tmp[nw] = acc;
+    }
+    __syncthreads();
+    const int r = s_tmp[wave] + x - v;
+    *total = s_tmp[nw];
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(1024) void k_bow_vectors(const int *__restrict__ counts, int n_static,
+                                                      const int32_t *__restrict__ word_in,
+                                                      const double *__restrict__ weight_in,
+                                                      const int32_t *__restrict__ nid_in, size_t in_pitch,
+                                                      int weighting, int scoring, int32_t *__restrict__ bow_words,
+                                                      double *__restrict__ bow_values, int *__restrict__ n_words,
+                                                      int32_t *__restrict__ fv_nodes, int32_t *__restrict__ fv_feats,
+                                                      int *__restrict__ n_fv, size_t out_pitch) {
+    __shared__ uint64_t s_key[kBowSortMax];
+    __shared__ int s_tmp[17];
+    __shared__ double s_norm;
+    const int f = blockIdx.x;
+    const int n = counts ? counts[f] : n_static;
+    const int32_t *wi = word_in + (size_t)f * in_pitch;
+    const double *wv = weight_in + (size_t)f * in_pitch;
+    const int32_t *ni = nid_in + (size_t)f * in_pitch;
+    int32_t *bw = bow_words + (size_t)f * out_pitch;
+    double *bv = bow_values + (size_t)f * out_pitch;
+    int32_t *fn = fv_nodes + (size_t)f * out_pitch;
+    int32_t *ff = fv_feats + (size_t)f * out_pitch;
+    int P = 1;
+    while (P < n) P <<= 1;
+    // (word, feature) keys of the features that are not stopped (weight > 0)
+    for (int t = threadIdx.x; t < P; t += blockDim.x)
+        s_key[t] = (t < n && wv[t] > 0) ? (((uint64_t)(uint32_t)wi[t] << 32) | (uint32_t)t) : ~0ull;
+    __syncthreads();
+    bow_bitonic(s_key, P);
+    const bool tf = weighting == 0 || weighting == 1;  // TF_IDF, TF
+    const bool must = scoring != 5;                     // all but DOT_PRODUCT
+    const bool l2 = scoring == 1;
+    // run heads -> output positions (each thread owns a contiguous chunk)
+    const int chunk = (P + blockDim.x - 1) / blockDim.x;
+    const int t0 = threadIdx.x * chunk;
+    int heads = 0;
+    for (int j = t0; j < t0 + chunk && j < P; j++) {
+        const uint64_t k = s_key[j];
+        if (k != ~0ull && (j == 0 || (s_key[j - 1] >> 32) != (k >> 32))) heads++;
+    }
+    int nw_total;
+    int pos = bow_block_scan(heads, s_tmp, &nw_total);
+    for (int j = t0; j < t0 + chunk && j < P; j++) {
+        const uint64_t k = s_key[j];
+        if (k == ~0ull || (j > 0 && (s_key[j - 1] >> 32) == (k >> 32))) continue;
+        const double w = wv[(uint32_t)k];
+        double v = w;
+        if (tf)
+            for (int r = j + 1; r < P && s_key[r] != ~0ull && (s_key[r] >> 32) == (k >> 32); r++) v += w;
+        bw[pos] = (int32_t)(k >> 32);
+        bv[pos] = v;
+        pos++;
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (tf && !must) {
+        const double nd = (double)nw_total;
+        for (int j = threadIdx.x; j < nw_total; j += blockDim.x) bv[j] /= nd;
+    }
+    if (must) {
+        if (threadIdx.x == 0) {
+            double norm = 0.0;
+            if (!l2) {
+                for (int j = 0; j < nw_total; j++) norm += fabs(bv[j]);
+            } else {
+                for (int j = 0; j < nw_total; j++) norm += bv[j] * bv[j];
+                norm = sqrt(norm);
+            }
+            s_norm = norm;
+        }
+        __syncthreads();
+        const double norm = s_norm;
+        if (norm > 0.0)
+            for (int j = threadIdx.x; j < nw_total; j += blockDim.x) bv[j] /= norm;
+    }
+    __syncthreads();
+    // FeatureVector: (node, feature) in map order
+    int m = 0;
+    for (int t = threadIdx.x; t < P; t += blockDim.x) {
+        const bool ok = t < n && wv[t] > 0;
+        m += ok;
+        s_key[t] = ok ? (((uint64_t)(uint32_t)ni[t] << 32) | (uint32_t)t) : ~0ull;
+    }
+    int m_total;
+    (void)bow_block_scan(m, s_tmp, &m_total);
+    bow_bitonic(s_key, P);
+    for (int j = threadIdx.x; j < m_total; j += blockDim.x) {
+        fn[j] = (int32_t)(s_key[j] >> 32);
+        ff[j] = (int32_t)(uint32_t)s_key[j];
+    }
+    if (threadIdx.x == 0) {
+        n_words[f] = nw_total;
+        n_fv[f] = m_total;
+    }
+}
+
+hipError_t launch_bow_vectors(const int *counts, int n_static, int n_frames, const int32_t *word, const double *weight,
+                              const int32_t *nid, size_t in_pitch, int weighting, int scoring, int32_t *bow_words,
+                              double *bow_values, int *n_words, int32_t *fv_nodes, int32_t *fv_feats, int *n_fv,
+                              size_t out_pitch, hipStream_t st) {
+    if (n_frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bow_vectors, dim3(n_frames), dim3(1024), 0, st, counts, n_static, word, weight, nid, in_pitch,
+                       weighting, scoring, bow_words, bow_values, n_words, fv_nodes, fv_feats, n_fv, out_pitch);
+    return hipGetLastError();
+}
+
+}  // namespace ygzfe

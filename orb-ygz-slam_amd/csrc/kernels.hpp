@@ -91,6 +91,24 @@ hipError_t launch_stereo_rgbd(const float *im_depth, size_t depth_pitch, int W, 
                               const ygzfe_kp *kps, int kp_pitch, const int *n_ptr, int n_max, int n_frames, float mbf,
                               float *u_right, float *depth, hipStream_t st);
 
+// DBoW2 vocabulary in HBM (bow.hip)
+constexpr int kBowMaxFeatures = 8192;
+struct VocabDev {
+    int n_nodes, L;
+    const int32_t *child_ptr;   // [n_nodes + 1] CSR slot ranges
+    const int32_t *slot_node;   // [n_nodes - 1] child node id per slot
+    const uint8_t *slot_desc;   // [n_nodes - 1][32] child descriptor per slot
+    const int32_t *word_id;     // [n_nodes]
+    const double *weight;       // [n_nodes]
+};
+hipError_t launch_bow_transform(const VocabDev &V, const uint8_t *desc, size_t desc_pitch, const int *counts,
+                                int n_max, int n_frames, int levelsup, int32_t *word, double *weight, int32_t *nid,
+                                size_t out_pitch, hipStream_t st);
+hipError_t launch_bow_vectors(const int *counts, int n_static, int n_frames, const int32_t *word, const double *weight,
+                              const int32_t *nid, size_t in_pitch, int weighting, int scoring, int32_t *bow_words,
+                              double *bow_values, int *n_words, int32_t *fv_nodes, int32_t *fv_feats, int *n_fv,
+                              size_t out_pitch, hipStream_t st);
+
 // One (map point, keyframe) item of SearchLocalPointsDirect (host-packed, 80 B)
 struct DirectItem {
     ygzfe_kp kp;        // ref->mvKeys[index] (28 B)

@@ -377,6 +377,69 @@ def stereo_from_rgbd(im_depth, kps, mbf, device=0):
     return ur, dep
 
 
+class Vocabulary:
+    """ORBVocabulary = TemplatedVocabulary<FORB::TDescriptor, FORB> (Thirdparty/DBoW2) in HBM."""
+
+    def __init__(self, handle, device):
+        self.h, self.device = handle, device
+        v = [C.c_int() for _ in range(6)]
+        _check(lib().ygzfe_vocab_info(self.h, *[C.byref(x) for x in v]), "vocab_info")
+        self.k, self.L, self.scoring, self.weighting, self.n_nodes, self.n_words = [x.value for x in v]
+
+    @classmethod
+    def from_arrays(cls, k, L, scoring, weighting, parent, is_leaf, desc, weight, device=0):
+        parent = np.ascontiguousarray(parent, np.int32)
+        is_leaf = np.ascontiguousarray(is_leaf, np.uint8)
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        weight = np.ascontiguousarray(weight, np.float64)
+        h = C.c_void_p()
+        _check(lib().ygzfe_vocab_create(device, k, L, scoring, weighting, len(parent), _p(parent), _p(is_leaf),
+                                        _p(desc), _p(weight), C.byref(h)), "vocab_create")
+        return cls(h, device)
+
+    @classmethod
+    def load_text(cls, path, device=0):
+        """loadFromTextFile (TemplatedVocabulary.h:1362)."""
+        h = C.c_void_p()
+        _check(lib().ygzfe_vocab_load_text(device, str(path).encode(), C.byref(h)), "vocab_load_text")
+        return cls(h, device)
+
+    @classmethod
+    def load_binary(cls, path, device=0):
+        """loadFromBinaryFile (TemplatedVocabulary.h:1478)."""
+        h = C.c_void_p()
+        _check(lib().ygzfe_vocab_load_binary(device, str(path).encode(), C.byref(h)), "vocab_load_binary")
+        return cls(h, device)
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value and _lib is not None:
+            _lib.ygzfe_vocab_destroy(self.h)
+            self.h = None
+
+    def transform_each(self, desc, levelsup=4):
+        """transform(feature, word, weight, &nid, levelsup) per descriptor -> (word, weight, nid)."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        w = np.zeros(n, np.int32)
+        wt = np.zeros(n, np.float64)
+        nid = np.zeros(n, np.int32)
+        _check(lib().ygzfe_bow_transform(self.h, _p(d), n, levelsup, _p(w), _p(wt), _p(nid)), "bow_transform")
+        return w, wt, nid
+
+    def transform(self, desc, levelsup=4):
+        """Frame::ComputeBoW -> (BowVector {word: value}, FeatureVector {node: [features]}), as
+        (words int32[], values float64[]) and (nodes int32[], features int32[]) in map order."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        m = max(n, 1)
+        bw, bv = np.zeros(m, np.int32), np.zeros(m, np.float64)
+        fn, ff = np.zeros(m, np.int32), np.zeros(m, np.int32)
+        nw, nf = C.c_int(), C.c_int()
+        _check(lib().ygzfe_compute_bow(self.h, _p(d), n, levelsup, _p(bw), _p(bv), C.byref(nw), _p(fn), _p(ff),
+                                       C.byref(nf)), "compute_bow")
+        return (bw[:nw.value].copy(), bv[:nw.value].copy()), (fn[:nf.value].copy(), ff[:nf.value].copy())
+
+
 def search_direct_batch(ref_frames, cur_frame, cam, item_ptr, ref_index, kp_ref, pt_ref, T_cr, px_proj, border=20.0):
     """Tracking::SearchLocalPointsDirect's per-point search (Tracking.cc:2337-2395), batched:
     point i tries items [item_ptr[i], item_ptr[i+1]) (its keyframes in SelectNearestKeyframe
@@ -494,6 +557,13 @@ class Batch:
         _check(lib().ygzfe_batch_stereo_rgbd(self.h, n_frames, C.c_void_p(d_depth_images), C.c_size_t(depth_pitch),
                                              stride, C.c_float(mbf), C.c_void_p(d_u_right), C.c_void_p(d_depth),
                                              C.c_void_p(stream)), "batch_stereo_rgbd")
+
+    def compute_bow(self, vocab, n_frames, levelsup, d_bow_words, d_bow_values, d_n_words, d_fv_nodes, d_fv_feats,
+                    d_n_fv, stream=None):
+        _check(lib().ygzfe_batch_compute_bow(self.h, vocab.h, n_frames, levelsup, C.c_void_p(d_bow_words),
+                                             C.c_void_p(d_bow_values), C.c_void_p(d_n_words),
+                                             C.c_void_p(d_fv_nodes), C.c_void_p(d_fv_feats), C.c_void_p(d_n_fv),
+                                             C.c_void_p(stream)), "batch_compute_bow")
 
     def timing(self, enable=True):
         ms = (C.c_float * 16)()

@@ -326,6 +326,42 @@ def stereo_from_rgbd(im_depth, kps, mbf):
     return ur[:len(kps)], dep[:len(kps)]
 
 
+class Vocab:
+    """DBoW2 TemplatedVocabulary restated (oracle/bow.c)."""
+
+    def __init__(self, k, L, scoring, weighting, parent, is_leaf, desc, weight):
+        lib().ygzo_vocab_create.restype = C.c_void_p
+        self.keep = [np.ascontiguousarray(parent, np.int32), np.ascontiguousarray(is_leaf, np.uint8),
+                     np.ascontiguousarray(desc, np.uint8), np.ascontiguousarray(weight, np.float64)]
+        self.h = C.c_void_p(lib().ygzo_vocab_create(k, L, scoring, weighting, len(parent),
+                                                    *[_p(a) for a in self.keep]))
+        assert self.h.value
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().ygzo_vocab_destroy(self.h)
+
+    def transform_each(self, desc, levelsup=4):
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        w, wt, nid = np.zeros(n, np.int32), np.zeros(n, np.float64), np.zeros(n, np.int32)
+        for i in range(n):
+            a, b, c = C.c_int(), C.c_double(), C.c_int(0)
+            lib().ygzo_bow_transform_one(self.h, _p(d[i]), levelsup, C.byref(a), C.byref(b), C.byref(c))
+            w[i], wt[i], nid[i] = a.value, b.value, c.value
+        return w, wt, nid
+
+    def transform(self, desc, levelsup=4):
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        m = max(n, 1)
+        bw, bv = np.zeros(m, np.int32), np.zeros(m, np.float64)
+        fn, ff = np.zeros(m, np.int32), np.zeros(m, np.int32)
+        nw, nf = C.c_int(), C.c_int()
+        lib().ygzo_compute_bow(self.h, _p(d), n, levelsup, _p(bw), _p(bv), C.byref(nw), _p(fn), _p(ff), C.byref(nf))
+        return (bw[:nw.value].copy(), bv[:nw.value].copy()), (fn[:nf.value].copy(), ff[:nf.value].copy())
+
+
 class RefFast:
     """The reference's own Thirdparty/fast, compiled by oracle/Makefile (oracle/_ref)."""
 

@@ -190,3 +190,70 @@ def test_search_direct_is_first_in_border_success():
     assert hit.sum() > 20
     true_px, _ = S.project(d["scene"].cam, *d["cur_pose"], d["Pw"])
     assert np.median(np.abs(px[hit] - true_px[hit])) < 0.5
+
+
+def _py_transform(parent, is_leaf, desc, weight, f, levelsup, L):
+    """TemplatedVocabulary::transform (TemplatedVocabulary.h:1241-1281) in plain Python."""
+    children = {}
+    for i in range(1, len(parent)):
+        children.setdefault(int(parent[i]), []).append(i)
+    words = np.cumsum(is_leaf) - 1
+    node, level, nid = 0, 0, 0
+    while children.get(node):
+        level += 1
+        ch = children[node]
+        d = [int(np.unpackbits(np.bitwise_xor(f, desc[c])).sum()) for c in ch]
+        node = ch[int(np.argmin(d))]  # argmin = first minimum
+        if level == L - levelsup:
+            nid = node
+    return (int(words[node]) if is_leaf[node] else 0), float(weight[node]), nid
+
+
+@pytest.mark.parametrize("scoring,weighting", [(0, 0), (1, 0), (5, 1), (0, 2), (5, 3)])
+def test_bow_oracle_matches_python_restatement(scoring, weighting):
+    """oracle/bow.c == a plain-Python DBoW2 transform + BowVector / FeatureVector
+    (addWeight / addIfNotExist, normalize L1 / L2, DotProduct's / size())."""
+    import _vocab as V
+    k, L = 6, 3
+    parent, is_leaf, desc, weight = V.synth_vocab(1, k, L)
+    voc = O.Vocab(k, L, scoring, weighting, parent, is_leaf, desc, weight)
+    rng = np.random.default_rng(2)
+    # features near vocabulary leaves (repeats -> shared words), plus random ones
+    leaves = np.where(is_leaf)[0]
+    f = desc[rng.choice(leaves, 60)] ^ (rng.integers(0, 256, (60, 32), dtype=np.uint8) &
+                                        rng.integers(0, 256, (60, 32), dtype=np.uint8) &
+                                        rng.integers(0, 256, (60, 32), dtype=np.uint8))
+    f = np.concatenate([f, f[:10], rng.integers(0, 256, (10, 32), dtype=np.uint8)])
+    w, wt, nid = voc.transform_each(f, 1)
+    bow = {}
+    fv = {}
+    for i, x in enumerate(f):
+        ew, ewt, enid = _py_transform(parent, is_leaf, desc, weight, x, 1, L)
+        assert (w[i], wt[i], nid[i]) == (ew, ewt, enid), i
+        if ewt > 0:
+            if weighting in (0, 1):
+                bow[ew] = bow.get(ew, 0.0) + ewt
+            else:
+                bow.setdefault(ew, ewt)
+            fv.setdefault(enid, []).append(i)
+    keys = sorted(bow)
+    vals = [bow[kk] for kk in keys]
+    if scoring == 5:
+        if weighting in (0, 1):
+            vals = [v / float(len(vals)) for v in vals]
+    else:
+        norm = 0.0
+        if scoring == 1:
+            for v in vals:
+                norm += v * v
+            norm = norm ** 0.5
+        else:
+            for v in vals:
+                norm += abs(v)
+        if norm > 0:
+            vals = [v / norm for v in vals]
+    (bw, bv), (fn, ff) = voc.transform(f, 1)
+    assert bw.tolist() == keys
+    assert bv.tolist() == vals
+    assert fn.tolist() == [n for n in sorted(fv) for _ in fv[n]]
+    assert ff.tolist() == [i for n in sorted(fv) for i in fv[n]]
