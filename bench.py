@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--no-align", action="store_true")
     ap.add_argument("--no-undistort", action="store_true", help="skip the undistort-remap side measurement")
     ap.add_argument("--no-stage-timing", action="store_true", help="no per-stage hipEvents in the timed region")
+    ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2-transform side measurement")
     ap.add_argument("--no-stereo", action="store_true", help="skip the stereo-matching side measurement")
     ap.add_argument("--no-direct", action="store_true", help="skip the SearchLocalPointsDirect side measurement")
     ap.add_argument("--latency-frames", type=int, default=200,
@@ -241,6 +242,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_stereo:
         stereo_line = stereo_leg(S, dev, args.cpu_sample > 0)
 
+    # ------------------------------------------------ §8(f) rank 4: DBoW2 transform (Frame::ComputeBoW)
+    bow_line = None
+    if rank == 0 and world == 1 and not args.no_bow:
+        bow_line = bow_leg(S, batch, B, dev, stream, args.cpu_sample > 0)
+
     # ------------------------------------------------ single-frame latency (rank 0, N = 1)
     lat = None
     if rank == 0 and world == 1 and args.latency_frames > 0:
@@ -294,7 +300,7 @@ def main():
             "cpu_baseline": cpu,
             "latency": lat,
             "next_rows": {"undistort_remap": und_line, "search_local_points_direct": direct_line,
-                          "stereo_matches": stereo_line},
+                          "stereo_matches": stereo_line, "dbow2_transform": bow_line},
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -362,6 +368,62 @@ def latency_leg(frames, poses, sc, S, n_timed, warm=10):
             "median_align_ms": round(float(np.median(ts - te)), 4),
             "path": "host C ABI, one frame at a time: H2D 752x480 u8 -> pyramid -> extract -> D2H kps+desc -> "
                     "SparseImgAlign 3..1 (prev -> cur) -> D2H pose; median over frames after 10 warm-up frames"}
+
+
+def bow_leg(S, batch, B, dev, stream, with_cpu, reps=10):
+    """Frame::ComputeBoW (Frame.cc:495-500) with an ORBvoc-shaped synthetic vocabulary
+    (k = 10, L = 6: 1,111,111 nodes, 10^6 words; the real ORBvoc.txt is absent), levelsup 4,
+    over the B frames the timed region extracted (batched, HIP events), one frame through
+    the host C ABI, and the oracle's restatement on one frame (1 thread)."""
+    import torch
+    import ygzfe
+    import _vocab as V
+    t0 = time.time()
+    parent, is_leaf, desc, weight = V.synth_vocab(6, 10, 6)
+    voc = ygzfe.Vocabulary.from_arrays(10, 6, 0, 0, parent, is_leaf, desc, weight, device=dev.index or 0)
+    build_s = time.time() - t0
+    cap = batch.kp_cap
+    bw = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+    bv = torch.zeros((B, cap), dtype=torch.float64, device=dev)
+    nw = torch.zeros(B, dtype=torch.int32, device=dev)
+    fn = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+    ff = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+    nfv = torch.zeros(B, dtype=torch.int32, device=dev)
+    args = (bw.data_ptr(), bv.data_ptr(), nw.data_ptr(), fn.data_ptr(), ff.data_ptr(), nfv.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    for _ in range(2):
+        batch.compute_bow(voc, B, 4, *args)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        batch.compute_bow(voc, B, 4, *args)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    _, d0 = batch.result(0)
+    for _ in range(3):
+        voc.transform(d0, 4)
+    ts = []
+    for _ in range(reps):
+        t1 = time.perf_counter()
+        voc.transform(d0, 4)
+        ts.append(time.perf_counter() - t1)
+    line = {"vocabulary": "synthetic k=10 L=6 (1111111 nodes), TF_IDF / L1", "frames": B,
+            "ms_per_launch": round(ms, 4), "frames_per_s": round(B / (ms * 1e-3), 1),
+            "mean_words": round(float(nw.float().mean().item()), 1),
+            "single_frame_host_ms": round(float(np.median(ts)) * 1e3, 4), "vocab_build_s": round(build_s, 2),
+            "path": "batched on the extracted batch (ygzfe_batch_compute_bow); single: host C ABI"}
+    if with_cpu:
+        import _oracle as O
+        ovoc = O.Vocab(10, 6, 0, 0, parent, is_leaf, desc, weight)
+        tc = []
+        for _ in range(5):
+            t1 = time.perf_counter()
+            ovoc.transform(d0, 4)
+            tc.append(time.perf_counter() - t1)
+        line["cpu_port_ms_per_frame"] = round(float(np.median(tc)) * 1e3, 4)
+        line["cpu_cores"] = 1
+    return line
 
 
 def stereo_leg(S, dev, with_cpu, n_pairs=64, reps=20):
