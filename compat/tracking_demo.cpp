@@ -119,6 +119,58 @@ int main() {
         std::printf("direct search matched %d of %d, %d within 0.1 px, %d within 0.5 px; cache pass keeps %d\n", hit,
                     ds.n_points(), close, near, kept);
         if (hit < ds.n_points() / 2 || near < hit * 7 / 10 || close < hit / 2 || kept < 1 || kept > hit) fails++;
+
+        // Stereo (Frame::ComputeStereoMatches, Frame.cc:509-682): the right image is the
+        // left one moved 6 px left, so every match has disparity 6 and depth mbf / 6
+        // (+-1 noise on the right image: with identical windows every SAD is 0 and the
+        // reference's median cut, SAD >= 2.1 * median, drops all matches)
+        auto imgR = synth(W, H, 7u, -6, 0);
+        for (size_t i = 0; i < imgR.size(); i++) {
+            const int v = imgR[i] + (int)(((uint32_t)i * 2654435761u) >> 30) - 1;
+            imgR[i] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+        }
+        ygz::FramePyramid fR;
+        std::vector<ygz::KeyPoint> kR;
+        std::vector<uint8_t> dR;
+        ygz::ORBextractor extractorRight(1000, 2.0f, 4, 20, 7);
+        extractorRight.ComputePyramid(fR, imgR.data(), W, H, W);
+        extractorRight(fR, kR, dR, ygz::ORBSLAM_KEYPOINT, false);
+        const float mb = 0.11f, mbf = mb * cam.fx;
+        std::vector<float> uRight, depth;
+        ygz::ComputeStereoMatches(f0, fR, k0, d0, kR, dR, mb, mbf, uRight, depth);
+        int nd = 0, good_d = 0;
+        for (size_t i = 0; i < k0.size(); i++)
+            if (depth[i] > 0) {
+                nd++;
+                good_d += std::fabs((k0[i].pt.x - uRight[i]) - 6.f) < 1.0f;  // sub-pixel disparity within 1 px
+            }
+        std::printf("stereo depths %d of %zu, %d with disparity 6 +- 1 px\n", nd, k0.size(), good_d);
+        if (nd < (int)k0.size() / 5 || good_d < nd * 9 / 10) fails++;
+
+        // ORBVocabulary (DBoW2) + Frame::ComputeBoW (Frame.cc:495-500) with a small
+        // text vocabulary: 4 random words under the root
+        const char *voc_path = "/tmp/ygzfe_demo_voc.txt";
+        if (FILE *vf = std::fopen(voc_path, "w")) {
+            std::fprintf(vf, "4 1  0 0\n");
+            unsigned s = 11u;
+            for (int n = 0; n < 4; n++) {
+                std::fprintf(vf, "0 1 ");
+                for (int b = 0; b < 32; b++) { s = s * 1664525u + 1013904223u; std::fprintf(vf, "%u ", (s >> 24) & 255u); }
+                std::fprintf(vf, " %.3f\n", 0.5 + n);
+            }
+            std::fclose(vf);
+        }
+        ygz::ORBVocabulary voc;
+        std::vector<std::pair<int, double>> bow;
+        std::vector<std::pair<int, std::vector<unsigned>>> feat;
+        const bool loaded = voc.loadFromTextFile(voc_path);
+        if (loaded) voc.transform(d0.data(), (int)k0.size(), bow, feat, 4);
+        double l1 = 0;
+        size_t nfeat = 0;
+        for (auto &b : bow) l1 += b.second;
+        for (auto &f : feat) nfeat += f.second.size();
+        std::printf("BoW: %zu words, L1 %.6f, %zu features in the FeatureVector\n", bow.size(), l1, nfeat);
+        if (!loaded || bow.empty() || std::fabs(l1 - 1.0) > 1e-9 || nfeat != k0.size()) fails++;
     } catch (const std::exception &e) {
         std::printf("error: %s\n", e.what());
         return 2;

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "ygzfe.h"
@@ -361,6 +362,70 @@ private:
     std::vector<float> proj_, pt_, px_;
     std::vector<KeyPoint> kps_;
     std::vector<ygzfe_se3> T_;
+};
+
+// Frame::ComputeStereoMatches (Frame.cc:509-682): fills mvuRight / mvDepth (-1 = none)
+// from the two extractors' pyramids, keypoints and descriptors.
+inline void ComputeStereoMatches(const FramePyramid &left, const FramePyramid &right,
+                                 const std::vector<KeyPoint> &keys, const std::vector<uint8_t> &desc,
+                                 const std::vector<KeyPoint> &keys_right, const std::vector<uint8_t> &desc_right,
+                                 float mb, float mbf, std::vector<float> &uRight, std::vector<float> &depth) {
+    uRight.assign(keys.size(), -1.f);
+    depth.assign(keys.size(), -1.f);
+    if (keys.empty()) return;
+    compat::check(ygzfe_stereo_matches(left.handle(), right.handle(), compat::as_kp(keys.data()), desc.data(),
+                                       (int)keys.size(), compat::as_kp(keys_right.data()), desc_right.data(),
+                                       (int)keys_right.size(), mb, mbf, uRight.data(), depth.data()),
+                  "stereo_matches");
+}
+
+// ORBVocabulary (TemplatedVocabulary<FORB::TDescriptor, FORB>) resident on the GPU, with the
+// loaders System.cc:187-189 calls and the transform Frame::ComputeBoW (Frame.cc:495-500) calls.
+// BowVector / FeatureVector come back as their std::map contents in map order.
+class ORBVocabulary {
+public:
+    explicit ORBVocabulary(int device = 0) : device_(device) {}
+    ~ORBVocabulary() { ygzfe_vocab_destroy(v_); }
+    ORBVocabulary(const ORBVocabulary &) = delete;
+    ORBVocabulary &operator=(const ORBVocabulary &) = delete;
+    bool loadFromTextFile(const std::string &path) { return reload(ygzfe_vocab_load_text(device_, path.c_str(), &n_)); }
+    bool loadFromBinaryFile(const std::string &path) {
+        return reload(ygzfe_vocab_load_binary(device_, path.c_str(), &n_));
+    }
+    bool empty() const {
+        int words = 0;
+        return !v_ || ygzfe_vocab_info(v_, nullptr, nullptr, nullptr, nullptr, nullptr, &words) != YGZFE_OK ||
+               words == 0;
+    }
+    // transform(features, BowVector&, FeatureVector&, levelsup); desc = n x 32 bytes
+    void transform(const uint8_t *desc, int n, std::vector<std::pair<int, double>> &bow,
+                   std::vector<std::pair<int, std::vector<unsigned>>> &feat, int levelsup) const {
+        bow.clear();
+        feat.clear();
+        if (!v_ || n <= 0) return;
+        std::vector<int32_t> w(n), fn(n), ff(n);
+        std::vector<double> val(n);
+        int nw = 0, nf = 0;
+        compat::check(ygzfe_compute_bow(v_, desc, n, levelsup, w.data(), val.data(), &nw, fn.data(), ff.data(), &nf),
+                      "compute_bow");
+        for (int i = 0; i < nw; i++) bow.emplace_back(w[i], val[i]);
+        for (int i = 0; i < nf; i++) {
+            if (feat.empty() || feat.back().first != fn[i]) feat.emplace_back(fn[i], std::vector<unsigned>());
+            feat.back().second.push_back((unsigned)ff[i]);
+        }
+    }
+    const ygzfe_vocab *handle() const { return v_; }
+
+private:
+    bool reload(int rc) {
+        if (rc != YGZFE_OK) return false;
+        ygzfe_vocab_destroy(v_);
+        v_ = n_;
+        n_ = nullptr;
+        return true;
+    }
+    int device_;
+    ygzfe_vocab *v_ = nullptr, *n_ = nullptr;
 };
 
 }  // namespace ygz
