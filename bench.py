@@ -40,7 +40,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="frames resident per GPU")
+    ap.add_argument("--batch", type=int, default=1024,
+                    help="frames resident per GPU (one chunk of a batched sequence; EuRoC MH sequences are 2033-3682 frames)")
     ap.add_argument("--cpu-sample", type=int, default=120, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-align", action="store_true")
@@ -127,8 +128,10 @@ def main():
     side = torch.cuda.Stream(dev)  # Hamming (descriptors only) runs beside SparseImgAlign (pyramids + kps)
 
     def step():
-        batch.extract(B, sptr)
+        # keypoint rows on `stream`, descriptors on `side`; Hamming (descriptors only)
+        # then runs on `side` beside SparseImgAlign (pyramids + keypoint positions)
         side.wait_stream(stream)
+        batch.extract_split(B, sptr, side.cuda_stream)
         batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(),
                     side.cuda_stream)
         if args.no_align:

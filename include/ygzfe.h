@@ -145,6 +145,11 @@ int ygzfe_batch_bind_buffers(ygzfe_batch *b, uint8_t *d_pyramids, ygzfe_kp *d_kp
 int ygzfe_batch_upload(ygzfe_batch *b, const uint8_t *frames, int n_frames);
 /* Pyramid + FAST + octree + orientation + blur + rBRIEF on frames [0, n). */
 int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream);
+/* The same extraction split over two streams: work queued on kp_stream after
+ * this call sees the keypoint rows (position, octave, size, response; not
+ * the angle) and the counts; work queued on desc_stream sees the complete
+ * rows and the descriptors.  The blur runs on desc_stream, beside FAST. */
+int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, void *desc_stream);
 /* Synchronise and report kernel-side errors (octree pool overflow). */
 int ygzfe_batch_check(ygzfe_batch *b);
 /* Dense best/second-best Hamming of frame qframe[p] against tframe[p] for each

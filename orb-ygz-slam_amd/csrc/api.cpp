@@ -459,6 +459,8 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
         YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
                               ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.err.as<int>(), 1,
                               st));
+        YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.nexist.as<int>(),
+                                ws.kps.as<ygzfe_kp>(), ws.counts.as<int>(), rows, 1, st));
         YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.sel.as<uint32_t>(),
                                    ws.selcnt.as<int>(), ws.nexist.as<int>(), ws.kps.as<ygzfe_kp>(),
                                    ws.desc.as<uint8_t>(), ws.counts.as<int>(), rows, 1, st));
@@ -607,11 +609,19 @@ int ygzfe_batch_upload(ygzfe_batch *b, const uint8_t *frames, int n_frames) {
     return YGZFE_OK;
 }
 
-int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream) {
+// Extraction as a small DAG over the launch stream and two helpers:
+//   kp_stream:   pyramid -> FAST levels -> octree -> keypoint rows
+//   desc_stream: (after the pyramid) GaussianBlur, concurrent with FAST;
+//                (after the keypoint rows) angle + rBRIEF
+// Work queued on kp_stream afterwards sees the keypoint rows (positions,
+// octave, size, response; not the angle); work on desc_stream sees the
+// complete rows and descriptors.
+int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, void *desc_stream) {
     if (!b || n_frames < 0 || n_frames > b->maxF) { set_error("invalid argument"); return YGZFE_EINVAL; }
     if (n_frames == 0) return YGZFE_OK;
     YGZ_TRY(ensure_device(b->device));
-    hipStream_t st = stream ? (hipStream_t)stream : b->stream;
+    hipStream_t st = kp_stream ? (hipStream_t)kp_stream : b->stream;
+    hipStream_t ds = desc_stream ? (hipStream_t)desc_stream : st;
     const PlanDev &pd = *b->plan;
     const Plan &P = pd.hp();
     Workspace &ws = b->ws;
@@ -620,11 +630,16 @@ int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream) {
     hipEvent_t t0 = b->begin(st);
     YGZ_HIP(launch_pyramid(pyr, P.pyr_bytes, P, pd.dp(), pd.tabs.as<int>(), n_frames, st));
     b->end(ST_PYR, t0, st);
-    t0 = b->begin(st);
-    YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), n_frames, st));
-    b->end(ST_BLUR, t0, st);
-    // FAST levels run back to back on st (overlapping them on side streams
-    // measured no gain and blurs per-kernel timing)
+    // the blur feeds only the descriptors: on desc_stream, beside FAST (a
+    // separate stream of ygzfe's own may share the caller's hardware queue)
+    hipStream_t bs = ds;
+    if (ds != st) {
+        YGZ_HIP(hipEventRecord(b->ev_fork, st));
+        YGZ_HIP(hipStreamWaitEvent(ds, b->ev_fork, 0));
+    }
+    t0 = b->begin(bs);
+    YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), n_frames, bs));
+    b->end(ST_BLUR, t0, bs);
     t0 = b->begin(st);
     YGZ_HIP(launch_fast(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(), ws.cellbuf.as<uint32_t>(),
                         ws.cellcnt.as<int>(), n_frames, st));
@@ -633,13 +648,25 @@ int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream) {
     YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
                           ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.err.as<int>(),
                           n_frames, st));
+    YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), nullptr, ws.kps.as<ygzfe_kp>(),
+                            ws.counts.as<int>(), P.kp_cap, n_frames, st));
     b->end(ST_OCT, t0, st);
-    t0 = b->begin(st);
+    // descriptors: after the blur (already on ds) and the keypoint rows
+    if (ds != st) {
+        YGZ_HIP(hipEventRecord(b->ev_join[1], st));
+        YGZ_HIP(hipStreamWaitEvent(ds, b->ev_join[1], 0));
+    }
+    t0 = b->begin(ds);
     YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.sel.as<uint32_t>(),
                                ws.selcnt.as<int>(), nullptr, ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(),
-                               ws.counts.as<int>(), P.kp_cap, n_frames, st));
-    b->end(ST_DESC, t0, st);
+                               ws.counts.as<int>(), P.kp_cap, n_frames, ds));
+    b->end(ST_DESC, t0, ds);
     return YGZFE_OK;
+}
+
+int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream) {
+    // everything complete on `stream` when the last launch retires
+    return ygzfe_batch_extract_split(b, n_frames, stream, stream);
 }
 
 int ygzfe_batch_check(ygzfe_batch *b) {

@@ -45,6 +45,63 @@ __global__ __launch_bounds__(256) void k_resize_area2(uint8_t *__restrict__ pyr,
     pyr[(size_t)f * pitch + D.off + (size_t)y * D.w + x] = (uint8_t)(v >> 2);
 }
 
+// The whole chain of exact x2 INTER_AREA levels 1..K in one pass: one lane per
+// level-K pixel reads its 2^K x 2^K level-0 block (one 2^K-byte load per row,
+// a wave's loads of a row are contiguous), forms every intermediate level in
+// registers with the same (a+b+c+d+2)>>2 rounding, and writes each level's
+// rows of the block (dword / ushort / byte stores).  Levels nest exactly
+// (resize_mode 1 <=> w_{l-1} = 2 w_l, h_{l-1} = 2 h_l), so level 0 holds
+// 2^K-aligned rows.
+template <int K>
+__global__ __launch_bounds__(256) void k_pyramid_area_chain(uint8_t *__restrict__ pyr, uint32_t pitch,
+                                                            const Plan *__restrict__ plan) {
+    constexpr int B = 1 << K;
+    const LevelDesc &LK = plan->lv[K];
+    const int f = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= LK.w * LK.h) return;
+    const int y = i / LK.w, x = i - y * LK.w;
+    uint8_t *fr = pyr + (size_t)f * pitch;
+    const int W0 = plan->lv[0].w;
+    int v[B][B];
+    const uint8_t *src = fr + (size_t)(B * y) * W0 + B * x;
+#pragma unroll
+    for (int r = 0; r < B; r++) {
+        if constexpr (B == 8) {
+            const uint2 q = *reinterpret_cast<const uint2 *>(src + (size_t)r * W0);
+#pragma unroll
+            for (int c = 0; c < 4; c++) { v[r][c] = (q.x >> (8 * c)) & 0xFF; v[r][4 + c] = (q.y >> (8 * c)) & 0xFF; }
+        } else if constexpr (B == 4) {
+            const uint32_t q = *reinterpret_cast<const uint32_t *>(src + (size_t)r * W0);
+#pragma unroll
+            for (int c = 0; c < 4; c++) v[r][c] = (q >> (8 * c)) & 0xFF;
+        } else {
+            const uint16_t q = *reinterpret_cast<const uint16_t *>(src + (size_t)r * W0);
+            v[r][0] = q & 0xFF;
+            v[r][1] = q >> 8;
+        }
+    }
+#pragma unroll
+    for (int l = 1; l <= K; l++) {
+        const int n = B >> l;  // this level's block side
+        const LevelDesc &D = plan->lv[l];
+#pragma unroll
+        for (int r = 0; r < n; r++) {
+#pragma unroll
+            for (int c = 0; c < n; c++)
+                v[r][c] = (v[2 * r][2 * c] + v[2 * r][2 * c + 1] + v[2 * r + 1][2 * c] + v[2 * r + 1][2 * c + 1] + 2) >> 2;
+            uint8_t *dst = fr + D.off + (size_t)(n * y + r) * D.w + n * x;
+            if (n == 4)
+                *reinterpret_cast<uint32_t *>(dst) =
+                    (uint32_t)v[r][0] | ((uint32_t)v[r][1] << 8) | ((uint32_t)v[r][2] << 16) | ((uint32_t)v[r][3] << 24);
+            else if (n == 2)
+                *reinterpret_cast<uint16_t *>(dst) = (uint16_t)(v[r][0] | (v[r][1] << 8));
+            else
+                *dst = (uint8_t)v[r][0];
+        }
+    }
+}
+
 // OpenCV fixed-point INTER_LINEAR (11-bit coefficients), scalar rounding
 // (b0*S0 + b1*S1 + 2^21) >> 22.  xtab[dx] = {sx, a0|a1<<16}, ytab[dy] = {ya, yb, b0|b1<<16}.
 __global__ __launch_bounds__(256) void k_resize_linear(uint8_t *__restrict__ pyr, uint32_t pitch,
@@ -1013,6 +1070,40 @@ struct Window {
 // One 16-lane DPP row per keypoint (four per wave, sixteen per workgroup):
 //   IC_Angle: lane s sums columns u = s-15 and u = s+1 over the 31 rows
 //   rBRIEF:   lane s evaluates pairs 16s..16s+15 (half of descriptor word s/2)
+// Keypoint rows of the octree selection (ORBextractor.cc:785-797): level-0
+// coordinates (x, y) * scale, size = PATCH_SIZE * scale, response = FAST
+// score, octave, class_id -1; angle is filled in by k_orient_desc.  Written
+// as soon as the octree is done, so consumers of positions only (map-point
+// snapshots, SparseImgAlign) need not wait for the descriptors.
+__global__ __launch_bounds__(256) void k_emit_kps(const Plan *__restrict__ plan, const uint32_t *__restrict__ sel,
+                                                  const int *__restrict__ selcnt, const int *__restrict__ n_existing,
+                                                  ygzfe_kp *__restrict__ kps, int *__restrict__ counts, int row_cap) {
+    const int f = blockIdx.y;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nl = plan->nlevels;
+    const int *sc = selcnt + (size_t)f * nl;
+    const int ne = n_existing ? n_existing[f] : 0;
+    int l = 0, pre = 0, acc = 0;
+    for (int q = 0; q < nl; q++) {
+        acc += sc[q];
+        if (acc <= idx) { l = q + 1; pre = acc; }
+    }
+    if (idx == 0) counts[f] = ne + acc;
+    if (l >= nl || ne + idx >= row_cap) return;
+    const LevelDesc &L = plan->lv[l];
+    const uint32_t key = sel[(size_t)f * plan->sel_total + L.sel_off + (idx - pre)];
+    ygzfe_kp kp;
+    kp.x = (float)(key_x(key) + kMinBorder);
+    kp.y = (float)(key_y(key) + kMinBorder);
+    if (l != 0) { kp.x *= L.scale; kp.y *= L.scale; }
+    kp.size = (float)L.patch_size;
+    kp.angle = 0.f;
+    kp.response = (float)key_score(key);
+    kp.octave = l;
+    kp.class_id = -1;
+    kps[(size_t)f * row_cap + ne + idx] = kp;
+}
+
 __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__ pyr,
                                                      const uint8_t *__restrict__ blur, uint32_t pitch,
                                                      const Plan *__restrict__ plan,
@@ -1036,8 +1127,6 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
         const int v = __shfl_up(incl, o, 64);
         if (lane >= o) incl += v;
     }
-    const int tot = __builtin_amdgcn_readlane(incl, nl - 1);
-    if (bx == 0 && threadIdx.x == 0) counts[f] = ne + tot;
     int l = 0, pre = 0;
     for (int q = 0; q < nl; q++) {
         const int iq = __builtin_amdgcn_readlane(incl, q);
@@ -1128,18 +1217,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     const int row = ne + idx;
     if ((s & 1) == 0)
         reinterpret_cast<uint32_t *>(desc + ((size_t)f * row_cap + row) * 32)[s >> 1] = bits | (other << 16);
-    if (s == 0) {
-        ygzfe_kp kp;
-        kp.x = (float)cx;
-        kp.y = (float)cy;
-        if (l != 0) { kp.x *= L.scale; kp.y *= L.scale; }
-        kp.size = (float)L.patch_size;
-        kp.angle = angle;
-        kp.response = (float)key_score(key);
-        kp.octave = l;
-        kp.class_id = -1;
-        kps[(size_t)f * row_cap + row] = kp;
-    }
+    if (s == 0) kps[(size_t)f * row_cap + row].angle = angle;  // the rest of the row: k_emit_kps
     YGZ_BSTAMP_K(1, 1);
     YGZ_BSTAMP_K(1, 2);
 }
@@ -1185,7 +1263,17 @@ hipError_t upload_pattern(const int *pat) {
 
 hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const int *dtabs,
                           int nframes, hipStream_t st) {
-    for (int l = 1; l < hp.nlevels; l++) {
+    // levels 1..K exact x2 INTER_AREA (every C2 level): one fused pass
+    int K = 0;
+    while (K + 1 < hp.nlevels && K < 3 && hp.lv[K + 1].resize_mode == 1) K++;
+    if (K > 0) {
+        const int n = hp.lv[K].w * hp.lv[K].h;
+        dim3 grid((n + 255) / 256, nframes);
+        if (K == 3) hipLaunchKernelGGL(k_pyramid_area_chain<3>, grid, dim3(256), 0, st, pyr, pitch, dp);
+        else if (K == 2) hipLaunchKernelGGL(k_pyramid_area_chain<2>, grid, dim3(256), 0, st, pyr, pitch, dp);
+        else hipLaunchKernelGGL(k_pyramid_area_chain<1>, grid, dim3(256), 0, st, pyr, pitch, dp);
+    }
+    for (int l = K + 1; l < hp.nlevels; l++) {
         const LevelDesc &D = hp.lv[l];
         dim3 grid((D.w + 63) / 64, (D.h + 3) / 4, nframes);
         if (D.resize_mode == 1)
@@ -1251,6 +1339,14 @@ hipError_t launch_orient_desc(const uint8_t *pyr, const uint8_t *blur, uint32_t 
     const int max_new = hp.sel_total;
     hipLaunchKernelGGL(k_orient_desc, dim3((max_new + 15) / 16, nframes), dim3(256), 0, st, pyr, blur, pitch, dp,
                        sel, selcnt, n_existing, kps, desc, counts, row_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_emit_kps(const Plan &hp, const Plan *dp, const uint32_t *sel, const int *selcnt,
+                           const int *n_existing, ygzfe_kp *kps, int *counts, int row_cap, int nframes,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(k_emit_kps, dim3((hp.sel_total + 255) / 256 + 1, nframes), dim3(256), 0, st, dp, sel, selcnt,
+                       n_existing, kps, counts, row_cap);
     return hipGetLastError();
 }
 

@@ -16,6 +16,9 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
 hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
                          uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int nframes,
                          hipStream_t st);
+hipError_t launch_emit_kps(const Plan &hp, const Plan *dp, const uint32_t *sel, const int *selcnt,
+                           const int *n_existing, ygzfe_kp *kps, int *counts, int row_cap, int nframes,
+                           hipStream_t st);
 hipError_t launch_orient_desc(const uint8_t *pyr, const uint8_t *blur, uint32_t pitch, const Plan &hp,
                               const Plan *dp, const uint32_t *sel, const int *selcnt, const int *n_existing,
                               ygzfe_kp *kps, uint8_t *desc, int *counts, int row_cap, int nframes,

@@ -508,6 +508,10 @@ class Batch:
     def extract(self, n_frames, stream=None):
         _check(lib().ygzfe_batch_extract(self.h, n_frames, C.c_void_p(stream)), "batch_extract")
 
+    def extract_split(self, n_frames, kp_stream, desc_stream):
+        _check(lib().ygzfe_batch_extract_split(self.h, n_frames, C.c_void_p(kp_stream), C.c_void_p(desc_stream)),
+               "batch_extract_split")
+
     def check(self):
         _check(lib().ygzfe_batch_check(self.h), "batch_check")
 
