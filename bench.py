@@ -33,6 +33,13 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SWEEP = 240  # frames per sweep of the synthetic trajectory
+
+
+def sweep_index(g):
+    """Trajectory position of global frame g: 0..SWEEP and back (triangle wave)."""
+    k = g % (2 * SWEEP)
+    return k if k <= SWEEP else 2 * SWEEP - k
 
 
 def parse():
@@ -80,7 +87,11 @@ def main():
     # trajectory: per-frame motion (v, w); frame g has pose exp(g * xi)
     xi = np.array([0.012, -0.006, 0.009, 0.0025, -0.002, 0.0015], np.float32)
     g0, _ = D.shard(world * B, rank, world)  # this rank's contiguous slice (weak scaling: B per rank)
-    poses = [ygzfe.trajectory_pose(g0 + i, xi) for i in range(B)]
+    # the camera sweeps back and forth over the plane (triangle wave of period
+    # 2*SWEEP frames) so every frame of every rank's slice sees the full
+    # textured view: ~1000 keypoints per frame like an EuRoC frame, whatever B
+    # and the rank; without it a long slice drifts off the plane.
+    poses = [ygzfe.trajectory_pose(sweep_index(g0 + i), xi) for i in range(B)]
     t_r = time.time()
     frames = np.stack([sc.render(q, t, noise_seed=g0 + i) for i, (q, t) in enumerate(poses)])
     render_s = time.time() - t_r

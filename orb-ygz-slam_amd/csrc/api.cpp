@@ -183,6 +183,7 @@ struct ygzfe_batch {
     // fork/join inside one extract: the FAST levels >= 1 overlap level 0
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_oct_fork = nullptr, ev_oct_join[2] = {nullptr, nullptr};
     std::unique_ptr<PlanDev> plan;
     DevBuf pyr;
     Workspace ws;
@@ -551,6 +552,8 @@ int ygzfe_batch_create(const ygzfe_orb_params *p, int device, int width, int hei
         YGZ_HIP(hipEventCreateWithFlags(&b->ev_join[i], hipEventDisableTiming));
     }
     YGZ_HIP(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
+    YGZ_HIP(hipEventCreateWithFlags(&b->ev_oct_fork, hipEventDisableTiming));
+    for (int i = 0; i < 2; i++) YGZ_HIP(hipEventCreateWithFlags(&b->ev_oct_join[i], hipEventDisableTiming));
     *out = b.release();
     return YGZFE_OK;
 }
@@ -567,6 +570,9 @@ void ygzfe_batch_destroy(ygzfe_batch *b) {
         if (b->ev_join[i]) (void)hipEventDestroy(b->ev_join[i]);
     }
     if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
+    if (b->ev_oct_fork) (void)hipEventDestroy(b->ev_oct_fork);
+    for (int i = 0; i < 2; i++)
+        if (b->ev_oct_join[i]) (void)hipEventDestroy(b->ev_oct_join[i]);
     delete b;
 }
 
@@ -647,7 +653,7 @@ int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, voi
     t0 = b->begin(st);
     YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
                           ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.err.as<int>(),
-                          n_frames, st));
+                          n_frames, st, &b->aux[1], 2, b->ev_oct_fork, b->ev_oct_join));
     YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), nullptr, ws.kps.as<ygzfe_kp>(),
                             ws.counts.as<int>(), P.kp_cap, n_frames, st));
     b->end(ST_OCT, t0, st);

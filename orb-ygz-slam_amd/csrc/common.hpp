@@ -195,6 +195,13 @@ namespace ygzfe {
 void set_error(const char *fmt, ...);
 }
 
+// hipError_t-returning variant for launch helpers
+#define YGZ_HIPR(call)                 \
+    do {                               \
+        hipError_t e_ = (call);        \
+        if (e_ != hipSuccess) return e_; \
+    } while (0)
+
 #define YGZ_HIP(call)                                                                  \
     do {                                                                               \
         hipError_t e_ = (call);                                                        \

@@ -578,7 +578,7 @@ struct OctLds {
     uint32_t mid[NC];     // mx | my << 12 | hist << 30 | div << 31
     uint32_t remap[NC];   // div << 31 | non-empty quadrant mask << 16 | position
     uint64_t sortk[NC];   // final-round candidates: cnt << 48 | seq << 16 | node
-    int red[8];
+    int red[16];
     int scal[8];
 };
 
@@ -593,6 +593,7 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 }
 
 // exclusive scan over the 256 threads of the block; *total = block sum
+template <int NT>
 __device__ __forceinline__ int block_excl_scan(int v, int *red, int *total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int incl = wave_incl_scan(v);
@@ -600,7 +601,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int *red, int *total) {
     __syncthreads();
     int off = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < NT / 64; i++) {
         const int r = red[i];
         off += i < w ? r : 0;
         tot += r;
@@ -619,14 +620,14 @@ __device__ __forceinline__ int quad_count(const uint32_t c[2], int q) {
     return (int)((c[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu);
 }
 
-template <int NC>
+template <int NC, int NT>
 __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, uint16_t *nid, int n, int N,
                                             bool final_round, int &cur, int &size, int &seqc, int &nexpand,
                                             int &overflow) {
     const int tid = threadIdx.x;
     // a) which nodes get their keys histogrammed: dividing nodes (main loop) or
     //    the final-round candidates (vSizeAndPointerToNode of the last pass)
-    for (int i = tid; i < size; i += 256) {
+    for (int i = tid; i < size; i += NT) {
         const uint64_t b = S.bnd[cur][i];
         const int x0 = (int)(b & 0xFFFF), y0 = (int)((b >> 16) & 0xFFFF);
         const int x1 = (int)((b >> 32) & 0xFFFF), y1 = (int)(b >> 48);
@@ -638,7 +639,7 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
     }
     __syncthreads();
 #pragma unroll 4
-    for (int j = tid; j < n; j += 256) {
+    for (int j = tid; j < n; j += NT) {
         const int i = nid[j];
         const uint32_t md = S.mid[i];
         if (md & (1u << 30)) {
@@ -651,7 +652,7 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
     int ctot = 0;
     if (!final_round) {
         int carry = 0;
-        for (int i0 = 0; i0 < size; i0 += 256) {
+        for (int i0 = 0; i0 < size; i0 += NT) {
             const int i = i0 + tid;
             int e = 0;
             bool div = false;
@@ -663,7 +664,7 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
                 }
             }
             int tot;
-            const int ex = block_excl_scan(e, S.red, &tot);
+            const int ex = block_excl_scan<NT>(e, S.red, &tot);
             if (div) S.remap[i] = (uint32_t)(carry + ex);
             carry += tot;
         }
@@ -671,11 +672,11 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
     } else {
         // candidates, list order -> sortk, then ascending sort; division order is descending
         int nc = 0;
-        for (int i0 = 0; i0 < size; i0 += 256) {
+        for (int i0 = 0; i0 < size; i0 += NT) {
             const int i = i0 + tid;
             const bool cand = i < size && (S.mid[i] & (1u << 30));
             int tot;
-            const int ex = block_excl_scan(cand ? 1 : 0, S.red, &tot);
+            const int ex = block_excl_scan<NT>(cand ? 1 : 0, S.red, &tot);
             if (cand)
                 S.sortk[nc + ex] = ((uint64_t)S.cnt[cur][i] << 48) | ((uint64_t)(S.seq[cur][i] & 0x7FFFFFFFu) << 16) |
                                    (uint64_t)i;
@@ -684,11 +685,11 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
         int p2 = 1;
         while (p2 < nc) p2 <<= 1;
         if (p2 > NC) { overflow = 1; return; }
-        for (int i = nc + tid; i < p2; i += 256) S.sortk[i] = ~0ull;
+        for (int i = nc + tid; i < p2; i += NT) S.sortk[i] = ~0ull;
         __syncthreads();
         for (int k = 2; k <= p2; k <<= 1)
             for (int jj = k >> 1; jj > 0; jj >>= 1) {
-                for (int i = tid; i < p2; i += 256) {
+                for (int i = tid; i < p2; i += NT) {
                     const int ixj = i ^ jj;
                     if (ixj > i) {
                         const uint64_t a = S.sortk[i], b = S.sortk[ixj];
@@ -701,7 +702,7 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
         if (tid == 0) S.scal[0] = nc;  // first p reaching N (nc: none)
         __syncthreads();
         int carryE = 0, carryD = 0;
-        for (int p0 = 0; p0 < nc; p0 += 256) {
+        for (int p0 = 0; p0 < nc; p0 += NT) {
             const int p = p0 + tid;
             int e = 0;
             int i = 0;
@@ -711,8 +712,8 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
                 e = (quad_count(c, 0) > 0) + (quad_count(c, 1) > 0) + (quad_count(c, 2) > 0) + (quad_count(c, 3) > 0);
             }
             int totE, totD;
-            const int exE = block_excl_scan(e, S.red, &totE);
-            const int exD = block_excl_scan(p < nc ? e - 1 : 0, S.red, &totD);
+            const int exE = block_excl_scan<NT>(e, S.red, &totE);
+            const int exD = block_excl_scan<NT>(p < nc ? e - 1 : 0, S.red, &totD);
             if (p < nc) {
                 S.remap[i] = (uint32_t)(carryE + exE);
                 if (size + carryD + exD + (e - 1) >= N) atomicMin(&S.scal[0], p);
@@ -722,7 +723,7 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
         }
         __syncthreads();
         const int pstar = min(S.scal[0], nc - 1);  // last dividing position
-        for (int p = tid; p <= pstar; p += 256) {
+        for (int p = tid; p <= pstar; p += NT) {
             const int i = (int)(S.sortk[nc - 1 - p] & 0xFFFF);
             S.mid[i] |= 1u << 31;
         }
@@ -742,12 +743,12 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
     //    undivided -> ctot + rank in list order.  New records into the other buffer.
     const int nxt = cur ^ 1;
     int carryK = 0, nexp = 0;
-    for (int i0 = 0; i0 < size; i0 += 256) {
+    for (int i0 = 0; i0 < size; i0 += NT) {
         const int i = i0 + tid;
         const bool valid = i < size;
         const bool div = valid && (S.mid[i] >> 31);
         int tot;
-        const int ex = block_excl_scan(valid && !div ? 1 : 0, S.red, &tot);
+        const int ex = block_excl_scan<NT>(valid && !div ? 1 : 0, S.red, &tot);
         if (valid) {
             if (div) {
                 const uint32_t c[2] = {S.cq[i][0], S.cq[i][1]};
@@ -794,12 +795,12 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
         carryK += tot;
     }
     int totx;  // expanders | overflow flags << 24, block-uniform; also orders the writes before the sweep
-    block_excl_scan(nexp | (overflow << 24), S.red, &totx);
+    block_excl_scan<NT>(nexp | (overflow << 24), S.red, &totx);
     overflow = totx >> 24 ? 1 : 0;
     totx &= 0xFFFFFF;
     // d) every key takes its node's new list position
 #pragma unroll 4
-    for (int j = tid; j < n; j += 256) {
+    for (int j = tid; j < n; j += NT) {
         const int i = nid[j];
         const uint32_t r = S.remap[i];
         if (r >> 31) {
@@ -817,7 +818,7 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
     __syncthreads();
 }
 
-template <int NC>
+template <int NC, int NT>
 __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const LevelDesc &L, int l, int f,
                                             OctLds<NC> &S, const uint32_t *__restrict__ cellbuf,
                                             const int *__restrict__ cellcnt, int *s_pref, uint32_t *K,
@@ -828,19 +829,19 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
     //    binary search over the chunk's exclusive prefix
     {
         int base = 0;
-        for (int cb = 0; cb < L.ncells; cb += 256) {
+        for (int cb = 0; cb < L.ncells; cb += NT) {
             const int c = cb + tid;
             const int cnt = c < L.ncells ? cellcnt[(size_t)f * plan->ncells + L.cell_begin + c] : 0;
             int tot;
-            s_pref[tid] = block_excl_scan(cnt, S.red, &tot);
+            s_pref[tid] = block_excl_scan<NT>(cnt, S.red, &tot);
             __syncthreads();
-            const int nch = min(L.ncells - cb, 256);
+            const int nch = min(L.ncells - cb, NT);
             const uint32_t *cs0 = cellbuf + ((size_t)f * plan->ncells + L.cell_begin + cb) * plan->cell_cap;
-            for (int j0 = 0; j0 < tot; j0 += 256 * 8) {  // 8 independent key loads in flight per thread
+            for (int j0 = 0; j0 < tot; j0 += NT * 8) {  // 8 independent key loads in flight per thread
                 uint32_t v[8];
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
-                    const int j = j0 + 256 * u + tid;
+                    const int j = j0 + NT * u + tid;
                     v[u] = 0u;
                     if (j < tot) {
                         int lo = 0, hi = nch - 1;
@@ -853,7 +854,7 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
                 }
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
-                    const int j = j0 + 256 * u + tid;
+                    const int j = j0 + NT * u + tid;
                     if (j < tot) K[base + j] = v[u];
                 }
             }
@@ -868,7 +869,7 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
     const int H0 = L.max_by - kMinBorder;
     if (tid < 8) S.scal[tid] = 0;
     __syncthreads();
-    for (int j = tid; j < n; j += 256) {
+    for (int j = tid; j < n; j += NT) {
         int idx = (int)((float)key_x(K[j]) / hX);
         idx = idx >= nIni ? nIni - 1 : idx;
         nid[j] = (uint16_t)idx;
@@ -890,7 +891,7 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
         }
     }
     __syncthreads();
-    for (int j = tid; j < n; j += 256) nid[j] = (uint16_t)S.remap[nid[j]];
+    for (int j = tid; j < n; j += NT) nid[j] = (uint16_t)S.remap[nid[j]];
     __syncthreads();
     if (l == 0) YGZ_BSTAMP_K(3, 4);
     // 3. main loop (:585-680)
@@ -899,7 +900,7 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
     bool final_round = false;
     while (true) {
         const int prev = size;
-        octree_pass<NC>(S, K, nid, n, N, final_round, cur, size, seqc, nexpand, overflow);
+        octree_pass<NC, NT>(S, K, nid, n, N, final_round, cur, size, seqc, nexpand, overflow);
         if (overflow || ++guard > 4096) { overflow = 1; break; }
         if (size >= N || size == prev) break;
         if (!final_round && size + nexpand * 3 > N) final_round = true;
@@ -909,13 +910,13 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
     // 4. retained key per node, list order
     uint32_t *out = sel + (size_t)f * plan->sel_total + L.sel_off;
     if (!overflow) {
-        for (int i = tid; i < size; i += 256) S.cq[i][0] = 0u;
+        for (int i = tid; i < size; i += NT) S.cq[i][0] = 0u;
         __syncthreads();
-        for (int j = tid; j < n; j += 256)
+        for (int j = tid; j < n; j += NT)
             atomicMax(&S.cq[nid[j]][0], ((uint32_t)key_score(K[j]) << 24) | (uint32_t)(0xFFFFFF - j));
         __syncthreads();
         if (size > L.sel_cap) overflow = 1;
-        for (int i = tid; i < size && i < L.sel_cap; i += 256) out[i] = K[0xFFFFFF - (S.cq[i][0] & 0xFFFFFFu)];
+        for (int i = tid; i < size && i < L.sel_cap; i += NT) out[i] = K[0xFFFFFF - (S.cq[i][0] & 0xFFFFFFu)];
     }
     if (tid == 0) {
         selcnt[(size_t)f * plan->nlevels + l] = overflow ? 0 : min(size, L.sel_cap);
@@ -930,24 +931,28 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
 // 4000 keeps the NC=1024 workgroup under 80 KiB: two workgroups per CU.
 constexpr int kOctLdsKeys = 4000;
 
-template <int NC>
-__global__ __launch_bounds__(256) void k_octree(const Plan *__restrict__ plan,
+// One launch per level (or a group of levels, l = level0 + blockIdx.y) so that
+// the node pool NC and the LDS key capacity NK fit that level's budget: the
+// small levels' workgroups then need a fraction of level 0's LDS and many fit
+// per CU.
+template <int NC, int NK, int NT = 256>
+__global__ __launch_bounds__(NT) void k_octree(const Plan *__restrict__ plan,
                                                 const uint32_t *__restrict__ cellbuf,
                                                 const int *__restrict__ cellcnt,
                                                 uint32_t *__restrict__ candA, uint32_t *__restrict__ candB,
                                                 uint32_t *__restrict__ sel, int *__restrict__ selcnt,
-                                                int *__restrict__ err) {
+                                                int *__restrict__ err, int level0) {
     __shared__ OctLds<NC> S;
-    __shared__ uint32_t sK[kOctLdsKeys];
-    __shared__ uint16_t sNid[kOctLdsKeys];
+    __shared__ uint32_t sK[NK];
+    __shared__ uint16_t sNid[NK];
     int *s_pref = reinterpret_cast<int *>(S.sortk);  // gather prefix; sortk is free until the final rounds
-    const int f = blockIdx.x, l = blockIdx.y, tid = threadIdx.x;
+    const int f = blockIdx.x, l = level0 + blockIdx.y, tid = threadIdx.x;
     if (l == 0) YGZ_BSTAMP_K(3, 0);
     const LevelDesc &L = plan->lv[l];
     int part = 0;
-    for (int c = tid; c < L.ncells; c += 256) part += cellcnt[(size_t)f * plan->ncells + L.cell_begin + c];
+    for (int c = tid; c < L.ncells; c += NT) part += cellcnt[(size_t)f * plan->ncells + L.cell_begin + c];
     int n;
-    block_excl_scan(part, S.red, &n);
+    block_excl_scan<NT>(part, S.red, &n);
     if (n > 65535) {  // u16 labels / quadrant counts
         if (tid == 0) {
             selcnt[(size_t)f * plan->nlevels + l] = 0;
@@ -955,21 +960,15 @@ __global__ __launch_bounds__(256) void k_octree(const Plan *__restrict__ plan,
         }
         return;
     }
-    if (n <= kOctLdsKeys) {
-        octree_body<NC>(plan, L, l, f, S, cellbuf, cellcnt, s_pref, sK, sNid, n, sel, selcnt, err);
+    if (n <= NK) {
+        octree_body<NC, NT>(plan, L, l, f, S, cellbuf, cellcnt, s_pref, sK, sNid, n, sel, selcnt, err);
     } else {
         uint32_t *K = candA + (size_t)f * plan->cand_total + L.cand_off;
         uint16_t *nid = reinterpret_cast<uint16_t *>(candB + (size_t)f * plan->cand_total + L.cand_off);
-        octree_body<NC>(plan, L, l, f, S, cellbuf, cellcnt, s_pref, K, nid, n, sel, selcnt, err);
+        octree_body<NC, NT>(plan, L, l, f, S, cellbuf, cellcnt, s_pref, K, nid, n, sel, selcnt, err);
     }
 }
 
-template __global__ void k_octree<512>(const Plan *, const uint32_t *, const int *, uint32_t *, uint32_t *,
-                                       uint32_t *, int *, int *);
-template __global__ void k_octree<1024>(const Plan *, const uint32_t *, const int *, uint32_t *, uint32_t *,
-                                        uint32_t *, int *, int *);
-template __global__ void k_octree<2048>(const Plan *, const uint32_t *, const int *, uint32_t *, uint32_t *,
-                                        uint32_t *, int *, int *);
 
 // ---------------------------------------------------------------------------
 // Orientation (IC_Angle on the unblurred level, ORBextractor.cc:77-101) and
@@ -1319,17 +1318,59 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
     return hipGetLastError();
 }
 
+// node pool per level: budget + 4 nIni + 16 (plan.cpp), rounded up to a power of two
+static int octree_nc(const LevelDesc &L) {
+    const int need = L.budget + 4 * L.n_ini + 16;
+    return need <= 256 ? 256 : need <= 512 ? 512 : need <= 1024 ? 1024 : 2048;
+}
+
+static hipError_t launch_octree_levels(int nc, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
+                                       uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err,
+                                       int nframes, int l0, int nl, hipStream_t st) {
+    dim3 grid(nframes, nl);
+    // LDS keys: 4000 with NC 1024 (two workgroups per CU), the larger levels' share below
+    if (nc <= 256)
+        hipLaunchKernelGGL((k_octree<256, 1536>), grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel,
+                           selcnt, err, l0);
+    else if (nc <= 512)
+        hipLaunchKernelGGL((k_octree<512, 3072>), grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel,
+                           selcnt, err, l0);
+    else if (nc <= 1024)
+        hipLaunchKernelGGL((k_octree<1024, 4000>), grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel,
+                           selcnt, err, l0);
+    else
+        hipLaunchKernelGGL((k_octree<2048, 4000>), grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel,
+                           selcnt, err, l0);
+    return hipGetLastError();
+}
+
+// Levels grouped by node-pool class, each group one launch; groups after the
+// first run on the side streams (fork after, join before the caller's next work).
 hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
                          uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int nframes,
-                         hipStream_t st) {
-    dim3 grid(nframes, hp.nlevels);  // level-0 workgroups (the longest) dispatch first
-    if (hp.node_cap <= 512)
-        hipLaunchKernelGGL(k_octree<512>, grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err);
-    else if (hp.node_cap <= 1024)
-        hipLaunchKernelGGL(k_octree<1024>, grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err);
-    else
-        hipLaunchKernelGGL(k_octree<2048>, grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err);
-    return hipGetLastError();
+                         hipStream_t st, const hipStream_t *side, int nside, hipEvent_t fork, const hipEvent_t *join) {
+    int l = 0, g = 0;
+    bool forked = false;
+    while (l < hp.nlevels) {
+        const int nc = octree_nc(hp.lv[l]);
+        int e = l + 1;
+        while (e < hp.nlevels && octree_nc(hp.lv[e]) == nc) e++;
+        hipStream_t s = st;
+        if (g > 0 && g - 1 < nside && side) {
+            if (!forked) {
+                YGZ_HIPR(hipEventRecord(fork, st));
+                forked = true;
+            }
+            s = side[g - 1];
+            YGZ_HIPR(hipStreamWaitEvent(s, fork, 0));
+        }
+        YGZ_HIPR(launch_octree_levels(nc, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, nframes, l, e - l, s));
+        if (s != st) YGZ_HIPR(hipEventRecord(join[g - 1], s));
+        l = e;
+        g++;
+    }
+    for (int k = 1; k < g && k - 1 < nside && side; k++) YGZ_HIPR(hipStreamWaitEvent(st, join[k - 1], 0));
+    return hipSuccess;
 }
 
 hipError_t launch_orient_desc(const uint8_t *pyr, const uint8_t *blur, uint32_t pitch, const Plan &hp,
