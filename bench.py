@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=120, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-align", action="store_true")
+    ap.add_argument("--schedule", choices=["split", "overlap", "serial"], default="split",
+                    help="split: blur + descriptors + Hamming on a side stream beside FAST / octree, "
+                         "SparseImgAlign after them; overlap: SparseImgAlign beside orient + Hamming too; "
+                         "serial: every stage on one stream")
     ap.add_argument("--no-undistort", action="store_true", help="skip the undistort-remap side measurement")
     ap.add_argument("--no-stage-timing", action="store_true", help="no per-stage hipEvents in the timed region")
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2-transform side measurement")
@@ -138,9 +142,21 @@ def main():
 
     side = torch.cuda.Stream(dev)  # Hamming (descriptors only) runs beside SparseImgAlign (pyramids + kps)
 
+    def step_serial():
+        batch.extract(B, sptr)
+        batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(), sptr)
+        if args.no_align:
+            return
+        ygzfe.plane_points_device(kps_t.data_ptr(), cap, P, cam, r3_t.data_ptr(), cz_t.data_ptr(), S.PLANE_Z,
+                                  xyz.data_ptr(), sptr)
+        batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(), camera, 3, 1,
+                           T_init.data_ptr(), out.data_ptr(), sptr)
+
     def step():
-        # keypoint rows on `stream`, descriptors on `side`; Hamming (descriptors only)
-        # then runs on `side` beside SparseImgAlign (pyramids + keypoint positions)
+        if args.schedule == "serial":
+            return step_serial()
+        # keypoint rows on `stream`, blur + descriptors on `side` (the blur runs
+        # beside FAST); Hamming (descriptors only) follows on `side`
         side.wait_stream(stream)
         batch.extract_split(B, sptr, side.cuda_stream)
         batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(),
@@ -151,6 +167,11 @@ def main():
         # synthetic map points (the stand-in for Tracking's T_ref * P_w snapshot)
         ygzfe.plane_points_device(kps_t.data_ptr(), cap, P, cam, r3_t.data_ptr(), cz_t.data_ptr(), S.PLANE_Z,
                                   xyz.data_ptr(), sptr)
+        if args.schedule == "split":
+            # a SparseImgAlign workgroup takes a whole CU (1024 threads x 128 VGPRs,
+            # 148 KB LDS): beside orient/Hamming it waits for free CUs and the
+            # overlap costs more than it hides, so it runs after them
+            stream.wait_stream(side)
         batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(), camera, 3, 1,
                            T_init.data_ptr(), out.data_ptr(), sptr)
         stream.wait_stream(side)  # the step ends when both branches have
@@ -306,7 +327,7 @@ def main():
                        "mean_keypoints": round(N, 1), "mean_align_visible": round(nv, 1),
                        "mean_fast_candidates": round(float(cand.sum()) / B, 1),
                        "mean_fast_candidates_per_level": [round(float(c) / B, 1) for c in cand],
-                       "parallelism": f"frame-sharded x{world}"},
+                       "parallelism": f"frame-sharded x{world}", "schedule": args.schedule},
             "roofline": roof,
             "pipeline_gbps_model": round(pipeline_gbps, 2),
             "h2d_upload_ms": round(h2d_s * 1e3, 2),

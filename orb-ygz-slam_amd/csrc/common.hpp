@@ -21,6 +21,7 @@
 namespace ygzfe {
 
 constexpr int kMaxLevels = YGZFE_MAX_LEVELS;
+constexpr int kBlurRows = 32;  // k_blur7 strip height (plan.cpp tiles the levels with it)
 constexpr int kEdgeThreshold = 19;  // ORBextractor.cc:75
 constexpr int kMinBorder = kEdgeThreshold - 3;
 constexpr int kPatchSize = 31, kHalfPatch = 15;

@@ -148,31 +148,30 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 }
 
 // One wave per 256-column x kBlurRows-row strip, no LDS: lane owns 4 adjacent
-// columns; each source row is read as 4 aligned dwords per lane (prefetched two
-// rows ahead), the 10-byte window realigned with v_alignbyte, the horizontal
-// taps are two v_dot4_u32_u8 per pixel, and the vertical taps slide over a
-// 7-row register ring.  The window start is clamped at the row start, so the
-// first four columns (lane 0 of the first strip) and the last three (whose taps
-// reach past the row) come out wrong; they are not stored by the main loop and
-// are recomputed with BORDER_REFLECT_101 taps at the end.
-constexpr int kBlurRows = 16;
-
-struct BlurWin {
-    const uint32_t *q;
-    uint32_t o;
-};
+// columns.  Each source row is read ONCE, as one dword per lane (a wave reads
+// the 256 strip bytes with a single coalesced 256-B load; 3 more lanes fetch
+// the dwords just left / right of the strip), and the 10-byte tap window
+// [x-3, x+6] is assembled from the neighbouring lanes' dwords with DPP wave
+// shifts.  The row index, its BORDER_REFLECT_101 mirror and the row address
+// are wave-uniform (SGPRs).  Rows are prefetched kBlurAhead rows ahead.  The
+// horizontal taps are two v_dot4_u32_u8 per pixel; the vertical taps slide
+// over a 7-row register ring with 24-bit multiply-adds.  The first four
+// columns (x < 4) and the last three (whose taps reach past the row) come out
+// wrong; they are not stored by the main loop and are recomputed with
+// BORDER_REFLECT_101 taps at the end.
+constexpr int kBlurAhead = 6;
 
 __device__ __forceinline__ void blur_hsum(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t o,
-                                          uint32_t ka, uint32_t kb, int h[4]) {
+                                          uint32_t ka, uint32_t kb, uint32_t h[4]) {
     const uint32_t p0 = __builtin_amdgcn_alignbyte(w1, w0, o);
     const uint32_t p1 = __builtin_amdgcn_alignbyte(w2, w1, o);
     const uint32_t p2 = __builtin_amdgcn_alignbyte(w3, w2, o);
-    h[0] = (int)__builtin_amdgcn_udot4(p1, kb, __builtin_amdgcn_udot4(p0, ka, 0u, false), false);
+    h[0] = __builtin_amdgcn_udot4(p1, kb, __builtin_amdgcn_udot4(p0, ka, 0u, false), false);
 #pragma unroll
     for (int j = 1; j < 4; j++)
-        h[j] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(p2, p1, j), kb,
-                                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(p1, p0, j), ka, 0u, false),
-                                           false);
+        h[j] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(p2, p1, j), kb,
+                                      __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(p1, p0, j), ka, 0u, false),
+                                      false);
 }
 
 // exact 7x7 output at (x, y) with reflected taps (border columns, tiny levels)
@@ -192,12 +191,112 @@ __device__ __forceinline__ uint8_t blur_pixel_reflect(const uint8_t *__restrict_
     return (uint8_t)min((acc + 32768) >> 16, 255);
 }
 
+// DPP whole-wave shifts by one lane (GFX9 wave_shl:1 / wave_shr:1): lane l
+// receives lane l+1's / l-1's value; the lane shifted in from outside keeps 0
+__device__ __forceinline__ uint32_t wave_from_next(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_from_prev(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+struct BlurRow {
+    uint32_t a;     // the lane's dword of the row (aligned)
+    uint32_t halo;  // lane 0: dword left of the strip, lanes 1-2: the two right of it
+    uint32_t o;     // row misalignment (row start & 3), wave-uniform
+};
+
+// Rows whose width is a multiple of 4 (every row dword-aligned: C2 levels
+// 0-2): lane l's dword A_l holds columns x..x+3 and the tap window [x-3, x+6]
+// is bytes 1..3 of A_{l-1}, A_l and bytes 0..2 of A_{l+1}.  The neighbours'
+// dwords come by DPP wave shifts whose shifted-in lane keeps its own halo
+// dword (lane 0: the dword left of the strip, lane 63: the one right of it).
+// BORDER_REFLECT_101 is applied to the bytes themselves: at the left edge lane
+// 0's left neighbour dword becomes (b4, b3, b2, b1); at the right edge the
+// dword holding columns w..w+2 becomes (b[w-2], b[w-3], b[w-4]), so every
+// output column, border ones included, comes out of the main loop.
+// The horizontal sums use the kernel shifted over the window bytes (10
+// v_dot4_u32_u8 per 4 pixels, no byte realignment).
+__device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, int w,
+                                                   int hgt, int sx, int y0, int lane, uint32_t k0, uint32_t k1,
+                                                   uint32_t k2, uint32_t k3, bool cv3) {
+    const int x = sx + 4 * lane;
+    const bool need = x < w;  // the lane's dword lies in the row (w % 4 == 0)
+    const bool left_edge = sx == 0, right_edge = sx + 256 >= w;
+    // halo: lane 0 the dword at sx - 4 (none at the left edge), lane 63 the one at sx + 256
+    const int hoff = lane == 0 ? -4 : 256;
+    const bool hneed = (lane == 0 && sx > 0) || (lane == 63 && sx + 256 < w);
+    // shifted kernels: h[j] = dot4(p0, K0j) + dot4(p1, K1j) + dot4(p2, K2j)
+    const uint32_t K00 = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), K10 = k2 | (k1 << 8) | (k0 << 16);
+    const uint32_t K01 = K00 << 8, K11 = k3 | (k2 << 8) | (k1 << 16) | (k0 << 24);
+    const uint32_t K02 = (k0 << 16) | (k1 << 24), K12 = k2 | (k3 << 8) | (k2 << 16) | (k1 << 24), K22 = k0;
+    const uint32_t K03 = k0 << 24, K13 = k1 | (k2 << 8) | (k3 << 16) | (k2 << 24), K23 = k1 | (k0 << 8);
+    struct Row {
+        uint32_t a, halo;
+    };
+    auto fetch = [&](int r, Row &R) {
+        const int yy = reflect101(y0 + r - 3, hgt);  // wave-uniform
+        const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(src + (size_t)yy * w + sx));
+        R.a = need ? q[lane] : 0u;
+        R.halo = hneed ? q[hoff >> 2] : 0u;
+    };
+    Row buf[kBlurAhead];
+#pragma unroll
+    for (int r = 0; r < kBlurAhead; r++) fetch(r, buf[r]);
+    // the lane holding columns w..w+2 (right edge inside the wave); lane 63's halo when w == sx + 256
+    const bool fix_r = right_edge && x == w;
+    const bool fix_halo = right_edge && lane == 63 && w == sx + 256;
+    uint32_t ring[7][4];
+#pragma unroll
+    for (int r = 0; r < kBlurRows + 6; r++) {
+        Row cur = buf[r % kBlurAhead];
+        if (r + kBlurAhead < kBlurRows + 6) fetch(r + kBlurAhead, buf[r % kBlurAhead]);
+        uint32_t am1 = (uint32_t)__builtin_amdgcn_update_dpp((int)cur.halo, (int)cur.a, 0x138, 0xF, 0xF, false);
+        if (right_edge) {
+            if (fix_r) cur.a = __builtin_amdgcn_perm(cur.a, am1, 0x03000102u);
+            if (fix_halo) cur.halo = __builtin_amdgcn_perm(cur.halo, cur.a, 0x03000102u);
+        }
+        const uint32_t ap1 = (uint32_t)__builtin_amdgcn_update_dpp((int)cur.halo, (int)cur.a, 0x130, 0xF, 0xF, false);
+        if (left_edge && lane == 0) am1 = __builtin_amdgcn_perm(ap1, cur.a, 0x01020304u);
+        const uint32_t p0 = __builtin_amdgcn_alignbyte(cur.a, am1, 1), p1 = __builtin_amdgcn_alignbyte(ap1, cur.a, 1);
+        const uint32_t p2 = ap1 >> 8;
+        uint32_t hs[4];
+        hs[0] = __builtin_amdgcn_udot4(p1, K10, __builtin_amdgcn_udot4(p0, K00, 0u, false), false);
+        hs[1] = __builtin_amdgcn_udot4(p1, K11, __builtin_amdgcn_udot4(p0, K01, 0u, false), false);
+        hs[2] = __builtin_amdgcn_udot4(
+            p2, K22, __builtin_amdgcn_udot4(p1, K12, __builtin_amdgcn_udot4(p0, K02, 0u, false), false), false);
+        hs[3] = __builtin_amdgcn_udot4(
+            p2, K23, __builtin_amdgcn_udot4(p1, K13, __builtin_amdgcn_udot4(p0, K03, 0u, false), false), false);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) ring[k][j] = ring[k + 1][j];
+            ring[6][j] = hs[j];
+        }
+        const int y = y0 + r - 6;
+        if (r >= 6 && y < hgt && need) {
+            uint32_t pk = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                // 24-bit multiply-adds (taps <= 56, tap-pair sums <= 2 * 255 * 256)
+                uint32_t v = (__umul24(k0, ring[0][j] + ring[6][j]) + __umul24(k1, ring[1][j] + ring[5][j]) +
+                              __umul24(k2, ring[2][j] + ring[4][j]) + __umul24(k3, ring[3][j]) + 32768u) >> 16;
+                if (cv3) v = min(v, 255u);  // CV3 taps sum to 257; CV4 (256 x 256) cannot exceed 255
+                pk |= v << (8 * j);
+            }
+            *reinterpret_cast<uint32_t *>(dst + (size_t)y * w + x) = pk;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_blur7(const uint8_t *__restrict__ pyr,
                                                uint8_t *__restrict__ blur, uint32_t pitch,
                                                const Plan *__restrict__ plan) {
     const int f = blockIdx.y;
     const int lane = threadIdx.x & 63;
-    int task = blockIdx.x * 4 + (threadIdx.x >> 6), l = 0;
+    // wave-uniform strip index (readfirstlane: row indices, reflections and row
+    // base addresses then live in SGPRs)
+    int task = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)), l = 0;
     if (task >= plan->blur_tiles) return;
     while (l + 1 < plan->nlevels && task >= plan->lv[l + 1].blur_tile_begin) l++;
     const LevelDesc &L = plan->lv[l];
@@ -208,37 +307,52 @@ __global__ __launch_bounds__(256) void k_blur7(const uint8_t *__restrict__ pyr,
     uint8_t *dst = blur + (size_t)f * pitch + L.off;
     // kernels: CV4 [18,34,48,56,48,34,18] (default) / CV3 [18,34,49,55,49,34,18]
     const bool cv3 = plan->blur_variant == YGZFE_BLUR_CV3;
-    const int k0 = 18, k1 = 34, k2 = cv3 ? 49 : 48, k3 = cv3 ? 55 : 56;
-    const int kk[7] = {k0, k1, k2, k3, k2, k1, k0};
+    const uint32_t k0 = 18, k1 = 34, k2 = cv3 ? 49 : 48, k3 = cv3 ? 55 : 56;
+    const int kk[7] = {(int)k0, (int)k1, (int)k2, (int)k3, (int)k2, (int)k1, (int)k0};
+    if (w >= 16 && (w & 3) == 0) {
+        blur_strip_aligned(src, dst, w, hgt, sx, y0, lane, k0, k1, k2, k3, cv3);
+        return;
+    }
     if (w >= 16) {
-        const uint32_t ka = (uint32_t)k0 | ((uint32_t)k1 << 8) | ((uint32_t)k2 << 16) | ((uint32_t)k3 << 24);
-        const uint32_t kb = (uint32_t)k2 | ((uint32_t)k1 << 8) | ((uint32_t)k0 << 16);
-        const int xw = max(x - 3, 0);  // reads at most 13 bytes past a row end (pyramid tail padding)
-        const bool active = x < w;
-        auto window = [&](int r, uint32_t wv[4], uint32_t &o) {
-            const uint8_t *pa = src + (size_t)reflect101(y0 + r - 3, hgt) * w + xw;
-            o = (uint32_t)((uintptr_t)pa & 3u);
-            const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(pa - o));
-            if (active) {
-                wv[0] = q[0]; wv[1] = q[1]; wv[2] = q[2]; wv[3] = q[3];
-            } else {
-                wv[0] = wv[1] = wv[2] = wv[3] = 0u;
-            }
+        const uint32_t ka = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24);
+        const uint32_t kb = k2 | (k1 << 8) | (k0 << 16);
+        // lanes whose dword is needed: bytes up to x + 6 of the last output lane
+        // (reads stay within the level + the pyramid's 64-B tail padding)
+        const bool need = x < w + 8;
+        const int hoff = lane == 0 ? -4 : lane == 1 ? 256 : 260;  // halo dwords (relative to the strip start)
+        const bool hneed = lane < 3 && (lane == 0 ? sx > 0 : sx + hoff < w + 8);
+        auto fetch = [&](int r, BlurRow &R) {
+            const int yy = reflect101(y0 + r - 3, hgt);
+            const uint8_t *row = src + (size_t)yy * w;  // wave-uniform
+            R.o = (uint32_t)((uintptr_t)row & 3u);
+            const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(row - R.o + sx));
+            R.a = need ? q[lane] : 0u;
+            R.halo = hneed ? q[hoff >> 2] : 0u;
         };
-        uint32_t wa[4], wb[4], oa, ob;
-        window(0, wa, oa);
-        window(1, wb, ob);
-        int ring[7][4];
+        BlurRow buf[kBlurAhead];
+#pragma unroll
+        for (int r = 0; r < kBlurAhead; r++) fetch(r, buf[r]);
+        const bool active = x < w;
+        uint32_t ring[7][4];
 #pragma unroll
         for (int r = 0; r < kBlurRows + 6; r++) {
-            uint32_t cw[4] = {wa[0], wa[1], wa[2], wa[3]};
-            const uint32_t co = oa;
-#pragma unroll
-            for (int k = 0; k < 4; k++) wa[k] = wb[k];
-            oa = ob;
-            if (r + 2 < kBlurRows + 6) window(r + 2, wb, ob);
-            int hs[4];
-            blur_hsum(cw[0], cw[1], cw[2], cw[3], co, ka, kb, hs);
+            const BlurRow cur = buf[r % kBlurAhead];
+            if (r + kBlurAhead < kBlurRows + 6) fetch(r + kBlurAhead, buf[r % kBlurAhead]);
+            // A[l-1], A[l], A[l+1], A[l+2] (row dwords around the lane's own)
+            const uint32_t hl = __builtin_amdgcn_readlane(cur.halo, 0);
+            const uint32_t hr1 = __builtin_amdgcn_readlane(cur.halo, 1), hr2 = __builtin_amdgcn_readlane(cur.halo, 2);
+            uint32_t am1 = wave_from_prev(cur.a);
+            if (lane == 0) am1 = hl;
+            uint32_t ap1 = wave_from_next(cur.a);
+            if (lane == 63) ap1 = hr1;
+            uint32_t ap2 = wave_from_next(ap1);
+            if (lane == 63) ap2 = hr2;
+            // taps [x-3, x+6] start o + 1 bytes into A[l-1] (o = 3: at A[l])
+            uint32_t hs[4];
+            if (cur.o == 3u)
+                blur_hsum(cur.a, ap1, ap2, 0u, 0u, ka, kb, hs);
+            else
+                blur_hsum(am1, cur.a, ap1, ap2, cur.o + 1u, ka, kb, hs);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
 #pragma unroll
@@ -250,9 +364,11 @@ __global__ __launch_bounds__(256) void k_blur7(const uint8_t *__restrict__ pyr,
                 uint32_t pk = 0;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const int acc = k0 * (ring[0][j] + ring[6][j]) + k1 * (ring[1][j] + ring[5][j]) +
-                                    k2 * (ring[2][j] + ring[4][j]) + k3 * ring[3][j];
-                    pk |= (uint32_t)min((acc + 32768) >> 16, 255) << (8 * j);  // CV3 taps sum to 257
+                    // 24-bit multiplies (taps <= 56, tap-pair sums <= 2 * 255 * 256): v_mad_u32_u24
+                    // at full rate instead of the quarter-rate v_mul_lo_u32 of a 32-bit product
+                    const uint32_t acc = __umul24(k0, ring[0][j] + ring[6][j]) + __umul24(k1, ring[1][j] + ring[5][j]) +
+                                         __umul24(k2, ring[2][j] + ring[4][j]) + __umul24(k3, ring[3][j]) + 32768u;
+                    pk |= min(acc >> 16, 255u) << (8 * j);  // CV3 taps sum to 257
                 }
                 uint8_t *o = dst + (size_t)y * w + x;
                 if (x >= 4 && x + 4 <= w - 3 && (((uintptr_t)o) & 3u) == 0) {
@@ -266,6 +382,9 @@ __global__ __launch_bounds__(256) void k_blur7(const uint8_t *__restrict__ pyr,
         }
     }
     // border columns (x < 4, x >= w - 3; every column when w < 16) of this strip
+#ifdef YGZ_NO_BLUR_BORDER
+    if (w >= 16) return;  // A/B timing experiment only
+#endif
     const int ncol = w >= 16 ? 7 : w;
     const bool left = sx == 0, right = sx + 256 >= w;
     if (w >= 16 && !left && !right) return;
@@ -1350,17 +1469,13 @@ hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf
                          uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int nframes,
                          hipStream_t st, const hipStream_t *side, int nside, hipEvent_t fork, const hipEvent_t *join) {
     int l = 0, g = 0;
-    bool forked = false;
+    if (side && nside > 0) YGZ_HIPR(hipEventRecord(fork, st));  // before the first group: the groups are independent
     while (l < hp.nlevels) {
         const int nc = octree_nc(hp.lv[l]);
         int e = l + 1;
         while (e < hp.nlevels && octree_nc(hp.lv[e]) == nc) e++;
         hipStream_t s = st;
         if (g > 0 && g - 1 < nside && side) {
-            if (!forked) {
-                YGZ_HIPR(hipEventRecord(fork, st));
-                forked = true;
-            }
             s = side[g - 1];
             YGZ_HIPR(hipStreamWaitEvent(s, fork, 0));
         }

@@ -91,8 +91,8 @@ int build_plan(const ygzfe_orb_params &p, int W, int H, PlanHost *ph, char *err,
         L.scale = s.scale[l];
         L.inv_scale = s.inv_scale[l];
         L.blur_tile_begin = blur_tiles;
-        L.blur_tiles_x = (L.w + 255) / 256;  // k_blur7: one wave per 256 x 16 strip
-        L.blur_tiles_y = (L.h + 15) / 16;
+        L.blur_tiles_x = (L.w + 255) / 256;  // k_blur7: one wave per 256 x kBlurRows strip
+        L.blur_tiles_y = (L.h + kBlurRows - 1) / kBlurRows;
         blur_tiles += L.blur_tiles_x * L.blur_tiles_y;
         // resize mode (cv::resize, see oracle/orb.c ygzo_resize)
         if (l > 0) {

@@ -18,7 +18,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libygzfe.so")
+LIB_PATH = os.environ.get("YGZFE_LIB") or os.path.join(PKG_ROOT, "lib", "libygzfe.so")  # YGZFE_LIB: A/B builds
 SYNTH_PATH = os.path.join(PKG_ROOT, "lib", "libygzsynth.so")
 SYNTH_HIP_PATH = os.path.join(PKG_ROOT, "lib", "libygzsynth_hip.so")
 
