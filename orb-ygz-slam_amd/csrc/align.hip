@@ -477,7 +477,7 @@ __device__ __forceinline__ void jacob_xyz2cam_fresh(float X, float Y, float Z, f
 // Generic path (any n): (feature, pixel) terms strided over the workgroup,
 // ref patches and Jacobians cached in a global scratch slab per job.
 template <int NT>
-__device__ __attribute__((noinline)) void sparse_align_generic(const AlignLevels &lv, const ygzfe_camera &cam, const AlignJob &job,
+__device__ __attribute__((noinline)) void sparse_align_generic(const AlignLevels lv, const ygzfe_camera cam, const AlignJob &job,
                                      float *__restrict__ scratch, ygzfe_align_result *__restrict__ outp) {
     constexpr int NW = NT / 64;
     __shared__ float s_red[NW][kRed];

@@ -636,8 +636,10 @@ int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, voi
     hipEvent_t t0 = b->begin(st);
     YGZ_HIP(launch_pyramid(pyr, P.pyr_bytes, P, pd.dp(), pd.tabs.as<int>(), n_frames, st));
     b->end(ST_PYR, t0, st);
-    // the blur feeds only the descriptors: on desc_stream, beside FAST (a
-    // separate stream of ygzfe's own may share the caller's hardware queue)
+    // the blur feeds only the descriptors: on desc_stream, beside FAST.  (Both
+    // are VALU-bound; beside the octree instead, the blur slows the octree's
+    // latency-bound passes by as much as it would slow FAST.)  A separate
+    // stream of ygzfe's own may share the caller's hardware queue.
     hipStream_t bs = ds;
     if (ds != st) {
         YGZ_HIP(hipEventRecord(b->ev_fork, st));

@@ -15,9 +15,15 @@
 
 #include <algorithm>
 
+#include "plan.hpp"
+
 namespace ygzfe {
 
 __constant__ __attribute__((aligned(16))) int8_t c_pattern[1024];
+// IC_Angle row weights for k_orient_desc, lane s = |row offset| - 1 (lane 15: the
+// centre row): byte b of dword k is column u = 4k + b - 15 of the window row;
+// [s][k] = 1 where |u| <= umax[|v|] (else 0), [s][8 + k] = u + 15 there (else 0)
+__constant__ __attribute__((aligned(16))) uint32_t c_icw[16][16];
 
 #ifdef YGZ_STAMPS
 __device__ unsigned long long g_bstamps[1 << 20];
@@ -1267,17 +1273,12 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     const uint8_t *bimg = blur + (size_t)f * pitch + L.off;
     Window<15, 31> wic;
     Window<18, 37> wdesc;
-    // per-lane IC row masks (umax, ORBextractor.cc:453-467) and the lane's 16
-    // pattern pairs are read before the LDS fences, which loads cannot cross
-    const int ua = s - 15, ub = s + 1;  // columns owned by this lane
-    const bool hasb = s < 15;
-    uint32_t va = 0, vb = 0;  // bit v: row offset v is inside the IC disc for column ua / ub
+    // the lane's IC row weights (c_icw) and its 16 pattern pairs are read
+    // before the LDS fences, which loads cannot cross
+    const uint4 *icw = reinterpret_cast<const uint4 *>(c_icw[s]);
+    uint4 wq[4];
 #pragma unroll
-    for (int v = 1; v <= 15; v++) {
-        const int um = plan->umax[v];
-        va |= (uint32_t)(-ua <= um) << v;
-        vb |= (uint32_t)(hasb && ub <= um) << v;
-    }
+    for (int q = 0; q < 4; q++) wq[q] = icw[q];
     const int4 *pp = reinterpret_cast<const int4 *>(c_pattern) + s * 4;  // 16 pairs x (x0,y0,x1,y1)
     int4 pat[4];
 #pragma unroll
@@ -1288,17 +1289,36 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     {
         wic.store(P, s);
         YGZ_BSTAMP_K(1, 4);
+        // IC_Angle (ORBextractor.cc:77-101): lane s takes the window rows 15 +- (s+1)
+        // (lane 15 the centre row).  Per row, with I the 31 row bytes (32nd
+        // weighted 0): S0 = sum of I over the disc (dot4 with the 0/1 weights),
+        // S1 = sum of (u + 15) I (dot4 with the u + 15 weights); then
+        // m01 += v (S0(+v) - S0(-v)), m10 += S1 - 15 S0.  Integer sums: the
+        // moments equal the reference's exactly.
         const uint32_t o0 = (uint32_t)(uintptr_t)(img + (size_t)(cy - 15) * w + (cx - 15));
-        auto row = [&](int r) { return P + r * kPatchStride + ((o0 + (uint32_t)(r * w)) & 15u); };
-        const uint8_t *c0 = row(15);
-        int m10 = ua * c0[s] + (hasb ? ub * c0[s + 16] : 0), m01 = 0;
+        const uint32_t W0[8] = {wq[0].x, wq[0].y, wq[0].z, wq[0].w, wq[1].x, wq[1].y, wq[1].z, wq[1].w};
+        const uint32_t W1[8] = {wq[2].x, wq[2].y, wq[2].z, wq[2].w, wq[3].x, wq[3].y, wq[3].z, wq[3].w};
+        auto row_sums = [&](int r, uint32_t &s0, uint32_t &s1) {
+            const uint32_t o = (o0 + (uint32_t)(r * w)) & 15u;  // window start inside LDS row r
+            const uint32_t *d = reinterpret_cast<const uint32_t *>(P + r * kPatchStride + (o & ~3u));
+            uint32_t dw[9];
 #pragma unroll
-        for (int v = 1; v <= 15; v++) {
-            const uint8_t *rp = row(15 + v), *rm = row(15 - v);
-            const int pa = rp[s], ma = rm[s], pb = rp[s + 16], mb = rm[s + 16];
-            if ((va >> v) & 1) { m01 += v * (pa - ma); m10 += ua * (pa + ma); }
-            if ((vb >> v) & 1) { m01 += v * (pb - mb); m10 += ub * (pb + mb); }
-        }
+            for (int k = 0; k < 9; k++) dw[k] = d[k];
+            s0 = 0u;
+            s1 = 0u;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t q = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], o & 3u);
+                s0 = __builtin_amdgcn_udot4(q, W0[k], s0, false);
+                s1 = __builtin_amdgcn_udot4(q, W1[k], s1, false);
+            }
+        };
+        const int v = s == 15 ? 0 : s + 1;
+        uint32_t s0p, s1p, s0m = 0u, s1m = 0u;
+        row_sums(15 + v, s0p, s1p);
+        if (s < 15) row_sums(15 - v, s0m, s1m);
+        int m01 = v * ((int)s0p - (int)s0m);
+        int m10 = (int)(s1p + s1m) - 15 * (int)(s0p + s0m);
         m01 = row16_sum(m01);
         m10 = row16_sum(m10);
         angle = fast_atan2_deg((float)m01, (float)m10);
@@ -1376,7 +1396,21 @@ static int device_cus() {
 hipError_t upload_pattern(const int *pat) {
     int8_t p8[1024];
     for (int i = 0; i < 1024; i++) p8[i] = (int8_t)pat[i];
-    return hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), p8, sizeof(p8));
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), p8, sizeof(p8));
+    if (e != hipSuccess) return e;
+    int umax[16];
+    ic_umax(umax);
+    uint32_t w[16][16] = {};
+    for (int s = 0; s < 16; s++) {
+        const int um = umax[s == 15 ? 0 : s + 1];
+        for (int b = 0; b < 31; b++) {
+            const int u = b - 15;
+            if (u < -um || u > um) continue;
+            w[s][b >> 2] |= 1u << (8 * (b & 3));
+            w[s][8 + (b >> 2)] |= (uint32_t)b << (8 * (b & 3));
+        }
+    }
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_icw), w, sizeof(w));
 }
 
 hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const int *dtabs,

@@ -39,15 +39,19 @@ void orb_scales(const ygzfe_orb_params &p, ScaleInfo *s) {
         desired *= factor;
     }
     s->budget[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
-    // :453-467
+    ic_umax(s->umax);
+}
+
+// IC_Angle circle rows, ORBextractor.cc:453-467 (HALF_PATCH_SIZE = 15: the same for every config)
+void ic_umax(int umax[16]) {
     const int vmax = (int)floorf(kHalfPatch * sqrtf(2.f) / 2 + 1);
     const int vmin = (int)ceilf(kHalfPatch * sqrtf(2.f) / 2);
     const double hp2 = kHalfPatch * kHalfPatch;
     int v, v0;
-    for (v = 0; v <= vmax; ++v) s->umax[v] = cv_round_d(sqrt(hp2 - v * v));
+    for (v = 0; v <= vmax; ++v) umax[v] = cv_round_d(sqrt(hp2 - v * v));
     for (v = kHalfPatch, v0 = 0; v >= vmin; --v) {
-        while (s->umax[v0] == s->umax[v0 + 1]) ++v0;
-        s->umax[v] = v0;
+        while (umax[v0] == umax[v0 + 1]) ++v0;
+        umax[v] = v0;
         ++v0;
     }
 }

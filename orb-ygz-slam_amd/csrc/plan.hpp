@@ -21,6 +21,7 @@ struct PlanHost {
     std::vector<int> tabs;  // bilinear resize tables
 };
 
+void ic_umax(int umax[16]);  // IC_Angle circle rows (ORBextractor.cc:453-467)
 void orb_scales(const ygzfe_orb_params &p, ScaleInfo *s);
 int build_plan(const ygzfe_orb_params &p, int W, int H, PlanHost *ph, char *err, size_t errlen);
 
