@@ -320,6 +320,124 @@ __device__ __forceinline__ void ldlt_solve6_uni(float (&A)[36], const float b[6]
     }
 }
 
+// Eigen's LDLT is left-looking: step k searches the pivot among the diagonal
+// entries k..5 that no update has touched yet, i.e. among the ORIGINAL
+// diagonal in its current (transposed) order.  The transposition sequence is
+// therefore fixed by |H_ii| alone, and pivoting = factoring P H P^T with P
+// known upfront: the same values meet the same operations in the same order as
+// in ldlt_solve6_uni (bit-identical results), without data-dependent register
+// exchanges.  The wave-uniform system is read from the lanes of r (lanes 0..5
+// b, lanes 8.. the upper triangle of H, row-major); the transposition sequence
+// runs on the scalar unit (|x| float bits order like |x| for non-NaN x) and the
+// permuted system is gathered by readlane with scalar lane indices.
+__device__ __forceinline__ int hpack6(int i, int j) {  // row-major upper-triangle index of (i, j)
+    const int a = i < j ? i : j, c = i < j ? j : i;
+    return a * 6 - ((a * (a - 1)) >> 1) + (c - a);
+}
+
+template <int K>
+__device__ __forceinline__ bool ldlt6_step_nopiv(float (&A)[36]) {
+    float tmp[6];
+#pragma unroll
+    for (int j = 0; j < K; j++) tmp[j] = A[j * 6 + j] * A[K * 6 + j];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < K; j++) s += A[K * 6 + j] * tmp[j];
+    A[K * 6 + K] -= s;
+#pragma unroll
+    for (int i = K + 1; i < 6; i++) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < K; j++) t += A[i * 6 + j] * tmp[j];
+        A[i * 6 + K] -= t;
+    }
+    const float akk = A[K * 6 + K];
+    if (K == 0 && akk == 0.f) return false;  // Eigen: a zero first pivot ends the factorization
+    if (akk != 0.f) {
+        const float r = __builtin_amdgcn_rcpf(akk);
+#pragma unroll
+        for (int i = K + 1; i < 6; i++) A[i * 6 + K] *= r;
+    }
+    return true;
+}
+
+__device__ __forceinline__ void ldlt_solve6_presorted(float r, int lane, float x[6]) {
+    const int ri = __float_as_int(r);
+    uint32_t d[6];
+    int pk[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        d[i] = (uint32_t)__builtin_amdgcn_readlane(ri, 8 + hpack6(i, i)) & 0x7FFFFFFFu;
+        pk[i] = i;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) {  // Eigen's transpositions: first maximum of the remaining diagonal
+        int piv = k;
+        uint32_t big = d[k];
+#pragma unroll
+        for (int i = k + 1; i < 6; i++)
+            if (d[i] > big) { big = d[i]; piv = i; }
+#pragma unroll
+        for (int i = k + 1; i < 6; i++)
+            if (piv == i) {
+                const uint32_t td = d[k]; d[k] = d[i]; d[i] = td;
+                const int tp = pk[k]; pk[k] = pk[i]; pk[i] = tp;
+            }
+    }
+    float A[36], b[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        b[i] = __int_as_float(__builtin_amdgcn_readlane(ri, pk[i]));
+#pragma unroll
+        for (int j = 0; j <= i; j++) {
+            const float v = __int_as_float(__builtin_amdgcn_readlane(ri, 8 + hpack6(pk[i], pk[j])));
+            A[i * 6 + j] = v;
+            A[j * 6 + i] = v;
+        }
+    }
+    if (ldlt6_step_nopiv<0>(A)) {
+        ldlt6_step_nopiv<1>(A);
+        ldlt6_step_nopiv<2>(A);
+        ldlt6_step_nopiv<3>(A);
+        ldlt6_step_nopiv<4>(A);
+        ldlt6_step_nopiv<5>(A);
+    }
+    float y[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        float t = b[i];
+#pragma unroll
+        for (int j = 0; j < i; j++) t -= A[i * 6 + j] * y[j];
+        y[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        const float dd = A[i * 6 + i];
+        y[i] = fabsf(dd) > 1.17549435e-38f ? y[i] * __builtin_amdgcn_rcpf(dd) : 0.f;
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+        float t = y[i];
+#pragma unroll
+        for (int j = i + 1; j < 6; j++) t -= A[j * 6 + i] * y[j];
+        y[i] = t;
+    }
+    // x[pk[i]] = y[i]: y spread over lanes 0..5, read back through the inverse permutation
+    float yl = 0.f;
+#pragma unroll
+    for (int i = 0; i < 6; i++) yl = lane == i ? y[i] : yl;
+    int inv[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        int v = 0;
+#pragma unroll
+        for (int q = 0; q < 6; q++) v = pk[q] == i ? q : v;
+        inv[i] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < 6; j++) x[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yl), inv[j]));
+}
+
 // The same LDLT with every array index a compile-time constant (pivot swaps
 // and the permutation are applied through selects), so the solver keeps the
 // 6x6 system in VGPRs instead of scratch.  Identical arithmetic to ldlt_solve6.
@@ -472,6 +590,27 @@ __device__ __forceinline__ void jacob_xyz2cam_f(float X, float Y, float Z, float
 __device__ __forceinline__ void jacob_xyz2cam_fresh(float X, float Y, float Z, float fj[12]) {
     asm volatile("" : "+v"(X), "+v"(Y), "+v"(Z));
     jacob_xyz2cam_f(X, Y, Z, fj);
+}
+
+// Single-precision forms of the reference's mixed float/double expressions,
+// with identical results:
+//  * bilinear weights (1.0 - su) * (1.0 - sv) (SparseImageAlign.cc:84-87,
+//    167-170): su, sv are u - floor(u) with u >= 3 (the border test), so
+//    1 - su is exact in float and the double product of two 24-bit values is
+//    exact; rounding it to float = one correctly rounded float product;
+//  * JacobXYZ2Cam's 1. / z and 1.0 + t (SparseImageAlign.h:98,104,110):
+//    double has >= 2*24 + 2 bits, so double-then-float rounding of a quotient
+//    or sum of floats equals the correctly rounded float operation.
+__device__ __forceinline__ float wmulf(float a, float b) { return a * b; }
+
+__device__ __forceinline__ void jacob_xyz2cam_ff(float X, float Y, float Z, float fj[12]) {
+    asm volatile("" : "+v"(X), "+v"(Y), "+v"(Z));  // recomputed where used (see jacob_xyz2cam_fresh)
+    const float z_inv = 1.0f / Z;
+    const float z_inv_2 = z_inv * z_inv;
+    fj[0] = -z_inv; fj[1] = 0.f; fj[2] = X * z_inv_2; fj[3] = Y * fj[2];
+    fj[4] = -(1.0f + X * fj[2]); fj[5] = Y * z_inv;
+    fj[6] = 0.f; fj[7] = -z_inv; fj[8] = Y * z_inv_2; fj[9] = 1.0f + Y * fj[8];
+    fj[10] = -fj[3]; fj[11] = -X * z_inv;
 }
 
 // Generic path (any n): (feature, pixel) terms strided over the workgroup,
@@ -860,7 +999,8 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                         s_nmeas = nmeas;
                     }
                     YGZ_STAMP(7);
-                    ldlt_solve6_uni(Hm, b, x);
+                    (void)b;
+                    ldlt_solve6_presorted(r, lane, x);
                     YGZ_STAMP(8);
                     const bool stop = s_stop || isnan(x[0]);
                     const bool rollback = (it > 0 && (double)new_chi2 > 1.2 * (double)s_chi2) || stop;
@@ -1009,19 +1149,25 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
 #pragma unroll
             for (int k = 0; k < 8; k++) acc[k] = 0.f;
             if (own && vis) {
+                // The residual loop runs in fused multiply-adds and projects with
+                // one reciprocal of z: rounding-level differences from the
+                // reference's separate products, inside the 1e-4 pose parity of
+                // SparseImgAlign (the Jacobian and the bilinear weights keep the
+                // reference's values: jacob_xyz2cam_ff, wmulf)
                 const SE3 T = s_T;
                 const float P3[3] = {X, Y, Z};
                 float pc3[3];
                 se3_act(T, P3, pc3);
-                const float u = (cam.fx * pc3[0] / pc3[2] + cam.cx) * scale;
-                const float v = (cam.fy * pc3[1] / pc3[2] + cam.cy) * scale;
+                const float izc = 1.0f / pc3[2];
+                const float u = __builtin_fmaf(cam.fx * pc3[0], izc, cam.cx) * scale;
+                const float v = __builtin_fmaf(cam.fy * pc3[1], izc, cam.cy) * scale;
                 const int ui = (int)floorf(u), vi = (int)floorf(v);
                 if (ui < 0 || vi < 0 || ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H) {
                     s_out[atomicAdd(&s_nout, 1)] = (uint16_t)f;
                 } else {
                     const float su = u - ui, sv = v - vi;
-                    const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
-                    const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
+                    const float wtl = wmulf(1.f - su, 1.f - sv), wtr = wmulf(su, 1.f - sv);
+                    const float wbl = wmulf(1.f - su, sv), wbr = wmulf(su, sv);
                     float Sx = 0.f, Sy = 0.f, chi2 = 0.f;
                     const uint8_t *base = cimg + (size_t)(vi - 2) * W + (ui - 2);
                     float r0[5];
@@ -1033,17 +1179,18 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
 #pragma unroll
                         for (int px = 0; px < 4; px++) {
                             const int pi = py * 4 + px;
-                            const float ic = wtl * r0[px] + wtr * r0[px + 1] + wbl * r1[px] + wbr * r1[px + 1];
+                            const float ic = __builtin_fmaf(
+                                wbr, r1[px + 1], __builtin_fmaf(wbl, r1[px], __builtin_fmaf(wtr, r0[px + 1], wtl * r0[px])));
                             const float res = ic - s_patch[pi][f];
-                            Sx += gx[pi] * res;
-                            Sy += gy[pi] * res;
-                            chi2 += res * res;
+                            Sx = __builtin_fmaf(gx[pi], res, Sx);
+                            Sy = __builtin_fmaf(gy[pi], res, Sy);
+                            chi2 = __builtin_fmaf(res, res, chi2);
                         }
 #pragma unroll
                         for (int c = 0; c < 5; c++) r0[c] = r1[c];
                     }
                     float fj[12];
-                    jacob_xyz2cam_fresh(X, Y, Z, fj);
+                    jacob_xyz2cam_ff(X, Y, Z, fj);
 #pragma unroll
                     for (int r = 0; r < 6; r++) acc[r] = -(fj[r] * Sx + fj[6 + r] * Sy) * fs;
                     acc[6] = chi2;
