@@ -221,30 +221,40 @@ struct BlurRow {
 // 0's left neighbour dword becomes (b4, b3, b2, b1); at the right edge the
 // dword holding columns w..w+2 becomes (b[w-2], b[w-3], b[w-4]), so every
 // output column, border ones included, comes out of the main loop.
-// The horizontal sums use the kernel shifted over the window bytes (10
-// v_dot4_u32_u8 per 4 pixels, no byte realignment).
+// Loads and stores are buffer operations on the level (32-bit lane offsets,
+// the row offset a scalar; reads past the level return 0 and are never used).
+// Horizontal taps: the kernel shifted over the window bytes, 10 v_dot4_u32_u8
+// per 4 pixels.  Vertical taps: the row sums (<= 255 * 256, 16 bits) of
+// consecutive rows packed in pairs, three v_dot2_u32_u16 + one 24-bit
+// multiply-add per pixel.
+template <bool CV3>
 __device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, int w,
-                                                   int hgt, int sx, int y0, int lane, uint32_t k0, uint32_t k1,
-                                                   uint32_t k2, uint32_t k3, bool cv3) {
+                                                   int hgt, int sx, int y0, int lane) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    constexpr uint32_t k0 = 18, k1 = 34, k2 = CV3 ? 49 : 48, k3 = CV3 ? 55 : 56;
     const int x = sx + 4 * lane;
-    const bool need = x < w;  // the lane's dword lies in the row (w % 4 == 0)
     const bool left_edge = sx == 0, right_edge = sx + 256 >= w;
-    // halo: lane 0 the dword at sx - 4 (none at the left edge), lane 63 the one at sx + 256
-    const int hoff = lane == 0 ? -4 : 256;
-    const bool hneed = (lane == 0 && sx > 0) || (lane == 63 && sx + 256 < w);
-    // shifted kernels: h[j] = dot4(p0, K0j) + dot4(p1, K1j) + dot4(p2, K2j)
-    const uint32_t K00 = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), K10 = k2 | (k1 << 8) | (k0 << 16);
-    const uint32_t K01 = K00 << 8, K11 = k3 | (k2 << 8) | (k1 << 16) | (k0 << 24);
-    const uint32_t K02 = (k0 << 16) | (k1 << 24), K12 = k2 | (k3 << 8) | (k2 << 16) | (k1 << 24), K22 = k0;
-    const uint32_t K03 = k0 << 24, K13 = k1 | (k2 << 8) | (k3 << 16) | (k2 << 24), K23 = k1 | (k0 << 8);
+    const uint32_t nbytes = (uint32_t)w * (uint32_t)hgt;
+    const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, (int)nbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc((void *)dst, 0, (int)nbytes, 0x00020000);
+    const uint32_t voff = (uint32_t)x;
+    // halo: lane 0 the dword at x - 4 (ignored at the left edge), lane 63 the one at x + 4
+    const uint32_t hoff = lane == 0 ? voff - 4u : voff + 4u;
+    // shifted horizontal kernels: h[j] = dot4(p0, K0j) + dot4(p1, K1j) + dot4(p2, K2j)
+    constexpr uint32_t K00 = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), K10 = k2 | (k1 << 8) | (k0 << 16);
+    constexpr uint32_t K01 = K00 << 8, K11 = k3 | (k2 << 8) | (k1 << 16) | (k0 << 24);
+    constexpr uint32_t K02 = (k0 << 16) | (k1 << 24), K12 = k2 | (k3 << 8) | (k2 << 16) | (k1 << 24), K22 = k0;
+    constexpr uint32_t K03 = k0 << 24, K13 = k1 | (k2 << 8) | (k3 << 16) | (k2 << 24), K23 = k1 | (k0 << 8);
+    // vertical pair kernels (low half = older row)
+    const u16x2 V01 = {(unsigned short)k0, (unsigned short)k1}, V23 = {(unsigned short)k2, (unsigned short)k3};
+    const u16x2 V21 = {(unsigned short)k2, (unsigned short)k1};
     struct Row {
         uint32_t a, halo;
     };
     auto fetch = [&](int r, Row &R) {
-        const int yy = reflect101(y0 + r - 3, hgt);  // wave-uniform
-        const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(src + (size_t)yy * w + sx));
-        R.a = need ? q[lane] : 0u;
-        R.halo = hneed ? q[hoff >> 2] : 0u;
+        const uint32_t so = (uint32_t)(reflect101(y0 + r - 3, hgt) * w);  // wave-uniform
+        R.a = __builtin_amdgcn_raw_buffer_load_b32(rin, voff, so, 0);
+        R.halo = __builtin_amdgcn_raw_buffer_load_b32(rin, hoff, so, 0);
     };
     Row buf[kBlurAhead];
 #pragma unroll
@@ -252,7 +262,9 @@ __device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ s
     // the lane holding columns w..w+2 (right edge inside the wave); lane 63's halo when w == sx + 256
     const bool fix_r = right_edge && x == w;
     const bool fix_halo = right_edge && lane == 63 && w == sx + 256;
-    uint32_t ring[7][4];
+    const bool store_lane = x < w;
+    uint32_t prv[4] = {0u, 0u, 0u, 0u};  // row sums of the previous row
+    uint32_t pr[5][4];                   // pr[m]: (row n-5+m-1, row n-5+m) packed, m = 0..4
 #pragma unroll
     for (int r = 0; r < kBlurRows + 6; r++) {
         Row cur = buf[r % kBlurAhead];
@@ -273,24 +285,28 @@ __device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ s
             p2, K22, __builtin_amdgcn_udot4(p1, K12, __builtin_amdgcn_udot4(p0, K02, 0u, false), false), false);
         hs[3] = __builtin_amdgcn_udot4(
             p2, K23, __builtin_amdgcn_udot4(p1, K13, __builtin_amdgcn_udot4(p0, K03, 0u, false), false), false);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-#pragma unroll
-            for (int k = 0; k < 6; k++) ring[k][j] = ring[k + 1][j];
-            ring[6][j] = hs[j];
-        }
-        const int y = y0 + r - 6;
-        if (r >= 6 && y < hgt && need) {
+        const int y = y0 + r - 6;  // output row: taps rows y-3 .. y+3 = this row (n) and the six before
+        if (r >= 6 && y < hgt && store_lane) {
             uint32_t pk = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                // 24-bit multiply-adds (taps <= 56, tap-pair sums <= 2 * 255 * 256)
-                uint32_t v = (__umul24(k0, ring[0][j] + ring[6][j]) + __umul24(k1, ring[1][j] + ring[5][j]) +
-                              __umul24(k2, ring[2][j] + ring[4][j]) + __umul24(k3, ring[3][j]) + 32768u) >> 16;
-                if (cv3) v = min(v, 255u);  // CV3 taps sum to 257; CV4 (256 x 256) cannot exceed 255
+                // rows (n-6, n-5), (n-4, n-3), (n-2, n-1) and n
+                uint32_t acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, pr[0][j]), V01, 32768u, false);
+                acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, pr[2][j]), V23, acc, false);
+                acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, pr[4][j]), V21, acc, false);
+                uint32_t v = (__umul24(k0, hs[j]) + acc) >> 16;
+                if (CV3) v = min(v, 255u);  // CV3 taps sum to 257; CV4 (256 x 256) cannot exceed 255
                 pk |= v << (8 * j);
             }
-            *reinterpret_cast<uint32_t *>(dst + (size_t)y * w + x) = pk;
+            __builtin_amdgcn_raw_buffer_store_b32(pk, rout, voff, (uint32_t)(y * w), 0);
+        }
+        // slide: pr[m] <- pr[m+1], pr[4] <- (row n-1, row n)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+#pragma unroll
+            for (int m = 0; m < 4; m++) pr[m][j] = pr[m + 1][j];
+            pr[4][j] = prv[j] | (hs[j] << 16);
+            prv[j] = hs[j];
         }
     }
 }
@@ -316,7 +332,10 @@ __global__ __launch_bounds__(256) void k_blur7(const uint8_t *__restrict__ pyr,
     const uint32_t k0 = 18, k1 = 34, k2 = cv3 ? 49 : 48, k3 = cv3 ? 55 : 56;
     const int kk[7] = {(int)k0, (int)k1, (int)k2, (int)k3, (int)k2, (int)k1, (int)k0};
     if (w >= 16 && (w & 3) == 0) {
-        blur_strip_aligned(src, dst, w, hgt, sx, y0, lane, k0, k1, k2, k3, cv3);
+        if (cv3)
+            blur_strip_aligned<true>(src, dst, w, hgt, sx, y0, lane);
+        else
+            blur_strip_aligned<false>(src, dst, w, hgt, sx, y0, lane);
         return;
     }
     if (w >= 16) {
