@@ -52,7 +52,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=120, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-align", action="store_true")
-    ap.add_argument("--schedule", choices=["split", "overlap", "serial"], default="split",
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: capture one step into a HIP graph and replay it (measured: same throughput as eager launches)")
+    ap.add_argument("--schedule", choices=["split", "overlap", "serial"], default="serial",
                     help="split: blur + descriptors + Hamming on a side stream beside FAST / octree, "
                          "SparseImgAlign after them; overlap: SparseImgAlign beside orient + Hamming too; "
                          "serial: every stage on one stream")
@@ -182,20 +184,48 @@ def main():
     batch.check()
     if world > 1:
         dist.barrier()
-    batch.timing(not args.no_stage_timing)  # hipEvents around every stage launch of the timed region (no syncs)
+    batch.timing(False)  # `value`: no per-stage events inside the timed region
+    run = step
+    graph_ok = False
+    if args.graph:
+        # one step captured as a HIP graph (every launch of the library, its
+        # fork/join events and the side streams), replayed per step
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream):
+                step()
+            g.replay()
+            torch.cuda.synchronize(dev)
+            batch.check()
+            run = g.replay
+            graph_ok = True
+        except Exception as e:  # capture unsupported: eager launches
+            print(f"bench: graph capture failed ({e}); eager launches", file=sys.stderr)
+            torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    stage_ms = batch.timing(False)
     batch.check()
     elapsed = D.max_over_ranks(elapsed, dev)
+    # roofline: the same K steps again with hipEvents around every stage launch
+    # (a stage event between two kernels adds ~10 us of dispatch gap, so they
+    # stay out of the throughput run)
+    stage_ms = {}
+    if not args.no_stage_timing:
+        batch.timing(True)
+        torch.cuda.synchronize(dev)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        stage_ms = batch.timing(False)
+        batch.check()
 
     ms_per_step = elapsed * 1000.0 / args.steps
     fps = world * B / (elapsed / args.steps)
@@ -327,7 +357,8 @@ def main():
                        "mean_keypoints": round(N, 1), "mean_align_visible": round(nv, 1),
                        "mean_fast_candidates": round(float(cand.sum()) / B, 1),
                        "mean_fast_candidates_per_level": [round(float(c) / B, 1) for c in cand],
-                       "parallelism": f"frame-sharded x{world}", "schedule": args.schedule},
+                       "parallelism": f"frame-sharded x{world}", "schedule": args.schedule,
+                       "hip_graph": graph_ok},
             "roofline": roof,
             "pipeline_gbps_model": round(pipeline_gbps, 2),
             "h2d_upload_ms": round(h2d_s * 1e3, 2),
