@@ -1496,6 +1496,14 @@ static int octree_nc(const LevelDesc &L) {
     return need <= 256 ? 256 : need <= 512 ? 512 : need <= 1024 ? 1024 : 2048;
 }
 
+// threads per workgroup of the larger octree classes: the workgroup holds its
+// LDS (two per CU) through a chain of barrier-separated passes, so more waves
+// per workgroup shorten every pass's strided loops over keys and nodes
+#ifndef YGZ_OCT_THREADS
+#define YGZ_OCT_THREADS 512
+#endif
+constexpr int kOctThreads = YGZ_OCT_THREADS;
+
 static hipError_t launch_octree_levels(int nc, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
                                        uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err,
                                        int nframes, int l0, int nl, hipStream_t st) {
@@ -1505,14 +1513,14 @@ static hipError_t launch_octree_levels(int nc, const Plan *dp, const uint32_t *c
         hipLaunchKernelGGL((k_octree<256, 1536>), grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel,
                            selcnt, err, l0);
     else if (nc <= 512)
-        hipLaunchKernelGGL((k_octree<512, 3072>), grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel,
-                           selcnt, err, l0);
+        hipLaunchKernelGGL((k_octree<512, 3072, kOctThreads>), grid, dim3(kOctThreads), 0, st, dp, cellbuf, cellcnt,
+                           candA, candB, sel, selcnt, err, l0);
     else if (nc <= 1024)
-        hipLaunchKernelGGL((k_octree<1024, 4000>), grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel,
-                           selcnt, err, l0);
+        hipLaunchKernelGGL((k_octree<1024, 4000, kOctThreads>), grid, dim3(kOctThreads), 0, st, dp, cellbuf, cellcnt,
+                           candA, candB, sel, selcnt, err, l0);
     else
-        hipLaunchKernelGGL((k_octree<2048, 4000>), grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel,
-                           selcnt, err, l0);
+        hipLaunchKernelGGL((k_octree<2048, 4000, kOctThreads>), grid, dim3(kOctThreads), 0, st, dp, cellbuf, cellcnt,
+                           candA, candB, sel, selcnt, err, l0);
     return hipGetLastError();
 }
 
