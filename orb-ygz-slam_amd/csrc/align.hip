@@ -931,7 +931,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
     __shared__ uint16_t s_out[NF];     // features projected out of bounds this iteration
     __shared__ int s_nout;
     __shared__ SE3 s_T, s_old;
-    __shared__ float s_chi2, s_H[36];
+    __shared__ float s_chi2, s_Hpk[21];  // H of the last iteration, upper triangle row-major
     __shared__ int s_stop, s_break, s_nmeas;
     const AlignJob &job = jobs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -944,7 +944,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
         s_nmeas = 0;
         s_break = 0;
         s_nout = 0;
-        for (int i = 0; i < 36; i++) s_H[i] = 0.f;
+        for (int i = 0; i < 21; i++) s_Hpk[i] = 0.f;
     }
     __syncthreads();
     YGZ_STAMP(9);
@@ -964,42 +964,47 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
             for (int it = 0; it < 10; it++) {
                 __syncthreads();  // A: partials written
             YGZ_STAMP(3);
+                // Jres[6], chi2, n_meas over waves 1..NW-1: lane 8g + k adds waves
+                // 2g+1, 2g+2 of value k, then the 8 groups are folded by cross-lane adds
+                float pk8;
+                {
+                    const int k8 = lane & 7, w1 = 2 * (lane >> 3) + 1, w2 = w1 + 1;
+                    pk8 = (w1 < NW ? s_part[w1][k8] : 0.f) + (w2 < NW ? s_part[w2][k8] : 0.f);
+                    pk8 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(pk8), 0x128, 0xF, 0xF, false));
+                    pk8 += __shfl_xor(pk8, 16, 64);
+                    pk8 += __shfl_xor(pk8, 32, 64);
+                }
                 float r = 0.f;
                 if (lane < 29) {
-                    if (lane < 8) {  // Jres[6], chi2, n_meas
-                        for (int w = 1; w < NW; w++) r += s_part[w][lane];
+                    if (lane < 8) {
+                        r = pk8;
                     } else {  // H = H_vis - sum of the out-of-bounds features' H_f
-                        const int k = lane - 8;
+                        const int k = lane - 8, nout = s_nout;
                         float o = 0.f;
-                        for (int i = 0; i < s_nout; i++) o += s_Hf[k][s_out[i]];
+                        int i = 0;
+                        for (; i + 4 <= nout; i += 4) {  // independent LDS reads, same summation order
+                            const int a0 = s_out[i], a1 = s_out[i + 1], a2 = s_out[i + 2], a3 = s_out[i + 3];
+                            const float v0 = s_Hf[k][a0], v1 = s_Hf[k][a1], v2 = s_Hf[k][a2], v3 = s_Hf[k][a3];
+                            o += v0;
+                            o += v1;
+                            o += v2;
+                            o += v3;
+                        }
+                        for (; i < nout; i++) o += s_Hf[k][s_out[i]];
                         r = s_Hvis[k] - o;
+                        s_Hpk[k] = r;  // H of this iteration (the result's Fisher information)
                     }
                 }
                 YGZ_STAMP(6);
-                // the 29 sums become wave-uniform values (readlane, no LDS round
-                // trip); every lane of the solver wave then runs the same solve
-                float tot[29];
-#pragma unroll
-                for (int k = 0; k < 29; k++) tot[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), k));
                 {
-                    float Hm[36], b[6], x[6];
-                    int m = 0;
-#pragma unroll
-                    for (int rr = 0; rr < 6; rr++)
-#pragma unroll
-                        for (int c = rr; c < 6; c++) { Hm[rr * 6 + c] = tot[8 + m]; Hm[c * 6 + rr] = tot[8 + m]; m++; }
-#pragma unroll
-                    for (int k = 0; k < 6; k++) b[k] = tot[k];
-                    const int nmeas = (int)tot[7];
-                    const float new_chi2 = tot[6] / (float)nmeas;
+                    float x[6];
+                    const int nmeas = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 7));
+                    const float new_chi2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 6)) / (float)nmeas;
                     if (lane == 0) {
                         s_nout = 0;
-#pragma unroll
-                        for (int k = 0; k < 36; k++) s_H[k] = Hm[k];
                         s_nmeas = nmeas;
                     }
                     YGZ_STAMP(7);
-                    (void)b;
                     ldlt_solve6_presorted(r, lane, x);
                     YGZ_STAMP(8);
                     const bool stop = s_stop || isnan(x[0]);
@@ -1043,7 +1048,8 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
             for (int i = 0; i < 3; i++) res.T_cur_ref.t[i] = s_T.t[i];
             res.n_visible = s_nmeas / kPA;
             res.chi2 = s_chi2;
-            for (int i = 0; i < 36; i++) res.H[i] = s_H[i];
+            for (int rr = 0, m = 0; rr < 6; rr++)
+                for (int c = rr; c < 6; c++, m++) { res.H[rr * 6 + c] = s_Hpk[m]; res.H[c * 6 + rr] = s_Hpk[m]; }
             out[blockIdx.x] = res;
         }
         return;
