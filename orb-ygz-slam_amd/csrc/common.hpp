@@ -45,6 +45,7 @@ struct LevelDesc {
     int blur_tile_begin, blur_tiles_x, blur_tiles_y;
     int pyr_tile_begin;
     int fast_roi;        // largest FAST cell ROI side of this level
+    int fast_rw, fast_rh;  // largest FAST cell ROI width / height of this level
 };
 
 struct CellDesc {

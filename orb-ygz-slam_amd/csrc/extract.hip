@@ -503,9 +503,9 @@ __device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(
 // ROI staging: lane = (row offset, dword) with S/4 dwords per LDS row; each
 // lane reads the two aligned dwords around its 4 bytes (issue) and realigns
 // them with v_alignbyte into one ds_write_b32 (commit).  NI loads per lane.
-template <int S>
-struct RoiStage {
-    static constexpr int DW = S / 4, RPI = 64 / DW, NI = (S + RPI - 1) / RPI;
+template <int S, int R>
+struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI height)
+    static constexpr int DW = S / 4, RPI = 64 / DW, NI = (R + RPI - 1) / RPI;
     uint32_t lo[NI], hi[NI];
     __device__ __forceinline__ void issue(const uint8_t *src, int w, int rw, int rh, int lane) {
         const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + 3) / 4;
@@ -652,26 +652,26 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
 // the waves per CU, not the dispatch, bound the throughput.)
 constexpr int kFastWaves = 4;  // cells (waves) per workgroup (8 measured slower: a block holds its LDS until its slowest cell ends)
 
-template <int S>
+template <int S, int R>
 __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(6))) void k_fast_cells(
     const uint8_t *__restrict__ pyr, uint32_t pitch, const Plan *__restrict__ plan,
     const CellDesc *__restrict__ cells, uint32_t *__restrict__ cellbuf, int *__restrict__ cellcnt, int cell_begin,
     int cell_end) {
     extern __shared__ uint8_t s_dyn[];
-    constexpr int slice = (2 * S * S + 2 * (S - 6) * (S - 6) + 15) / 16 * 16;  // 16-B aligned slices
+    constexpr int slice = (2 * S * R + 2 * (S - 6) * (R - 6) + 15) / 16 * 16;  // 16-B aligned slices
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     const int c = cell_begin + blockIdx.x * kFastWaves + wave;
     if (c >= cell_end) return;
     uint8_t *img = s_dyn + wave * slice;
-    uint8_t *sc = img + S * S;
-    uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * S);
+    uint8_t *sc = img + S * R;
+    uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * R);
     const CellDesc cd = cells[c];
     const LevelDesc &L = plan->lv[cd.level];
     const uint8_t *src = pyr + (size_t)f * pitch + L.off + (size_t)cd.y0 * L.w + cd.x0;
     if (S == 40) YGZ_BSTAMP_K(2, 0);
     {
-        RoiStage<S> st;
+        RoiStage<S, R> st;
         st.issue(src, L.w, cd.rw, cd.rh, lane);
         st.commit(img, src, L.w, cd.rw, cd.rh, lane);
     }
@@ -688,8 +688,8 @@ static int fast_stride(int roi) {
     return S < 40 ? 40 : S;
 }
 
-static size_t fast_cells_lds_bytes(int S) {
-    return kFastWaves * (size_t)((2 * S * S + 2 * (S - 6) * (S - 6) + 15) / 16 * 16);
+static size_t fast_cells_lds_bytes(int S, int R) {
+    return kFastWaves * (size_t)((2 * S * R + 2 * (S - 6) * (R - 6) + 15) / 16 * 16);
 }
 
 // ---------------------------------------------------------------------------
@@ -1470,21 +1470,25 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
     for (int l = 0; l < hp.nlevels; l++) {
         const LevelDesc &L = hp.lv[l];
         if (L.ncells == 0) continue;
-        const int S = fast_stride(L.fast_roi);
-        const size_t lds = fast_cells_lds_bytes(S);
+        // row stride S >= the widest ROI, row capacity R >= the tallest (LDS per
+        // wave ~ 2 S R: C2 levels 1-2 have 38-px-wide, 41/50-px-tall ROIs)
+        int S = fast_stride(L.fast_rw), R = fast_stride(L.fast_rh);
+        if (!(S == 40 && R <= 56) && S != R) S = R = std::max(S, R);  // other shapes: square slices
+        if (R < S) R = S;
+        const size_t lds = fast_cells_lds_bytes(S, R);
         const int cb = L.cell_begin, ce = L.cell_begin + L.ncells;
         const dim3 grid((L.ncells + kFastWaves - 1) / kFastWaves, nframes);
         // level 0 on the caller's stream, the others spread over the given side streams
         const hipStream_t st = (l == 0 || !lvl_streams || n_lvl_streams <= 0) ? st0
                                                                                 : lvl_streams[(l - 1) % n_lvl_streams];
-#define YGZ_FAST(SS) hipLaunchKernelGGL(k_fast_cells<SS>, grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce)
-        switch (S) {
-        case 40: YGZ_FAST(40); break;
-        case 48: YGZ_FAST(48); break;
-        case 56: YGZ_FAST(56); break;
-        case 64: YGZ_FAST(64); break;
-        default: YGZ_FAST(72); break;
-        }
+#define YGZ_FAST(SS, RR) hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce)
+        if (S == 40 && R == 40) YGZ_FAST(40, 40);
+        else if (S == 40 && R == 48) YGZ_FAST(40, 48);
+        else if (S == 40 && R == 56) YGZ_FAST(40, 56);
+        else if (S == 48) YGZ_FAST(48, 48);
+        else if (S == 56) YGZ_FAST(56, 56);
+        else if (S == 64) YGZ_FAST(64, 64);
+        else YGZ_FAST(72, 72);
 #undef YGZ_FAST
     }
     return hipGetLastError();

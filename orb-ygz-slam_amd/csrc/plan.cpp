@@ -175,6 +175,8 @@ int build_plan(const ygzfe_orb_params &p, int W, int H, PlanHost *ph, char *err,
                     cell_cap = std::max(cell_cap, ((iw + 1) / 2) * ((ih + 1) / 2));
                     P.fast_S = std::max(P.fast_S, ((std::max((int)c.rw, (int)c.rh) + 3) / 4) * 4);
                     L.fast_roi = std::max(L.fast_roi, std::max((int)c.rw, (int)c.rh));
+                    L.fast_rw = std::max(L.fast_rw, (int)c.rw);
+                    L.fast_rh = std::max(L.fast_rh, (int)c.rh);
                     ph->cells.push_back(c);
                 }
             }
