@@ -514,7 +514,7 @@ struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI 
             const int r = k * RPI + rlane;
             lo[k] = hi[k] = 0u;
             if (rlane < RPI && r < rh && dw < ndw) {
-                const uint8_t *pa = src + (size_t)r * w + 4 * dw;
+                const uint8_t *pa = src + __umul24((uint32_t)r, (uint32_t)w) + 4 * dw;
                 const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(pa - ((uintptr_t)pa & 3u)));
                 lo[k] = q[0];
                 hi[k] = q[1];
@@ -527,7 +527,7 @@ struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI 
         for (int k = 0; k < NI; k++) {
             const int r = k * RPI + rlane;
             if (rlane < RPI && r < rh && dw < ndw) {
-                const uint32_t sh = (uint32_t)(((uintptr_t)(src + (size_t)r * w)) & 3u);
+                const uint32_t sh = (uint32_t)(((uintptr_t)(src + __umul24((uint32_t)r, (uint32_t)w))) & 3u);
                 reinterpret_cast<uint32_t *>(img + r * S)[dw] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh);
             }
         }
@@ -1191,12 +1191,16 @@ struct Window {
     static constexpr int NK = (NROWS + 3) / 4;
     u32x4 v[NK];
     __device__ __forceinline__ void load(const uint8_t *img, int w, int cx, int cy, int s) {
-        const uint8_t *base = img + (size_t)(cy - R) * w + (cx - R);
+        // 32-bit in-level offsets (24-bit multiplies) added to the level pointer once per row
+        // (the level can differ between the keypoints of a wave: no wave-uniform buffer resource)
+        const uint32_t base = __umul24((uint32_t)(cy - R), (uint32_t)w) + (uint32_t)(cx - R);
+        const uint32_t a0 = (uint32_t)(uintptr_t)img & 15u;  // level misalignment (0: levels are 16-B aligned)
         const int j = s & 3, r0 = s >> 2;
 #pragma unroll
         for (int k = 0; k < NK; k++) {  // rows past the window re-read its last row (not stored)
-            const uint8_t *rowp = base + (size_t)min(r0 + 4 * k, NROWS - 1) * w;
-            v[k] = as_global(reinterpret_cast<const u32x4 *>(rowp - ((uintptr_t)rowp & 15u)))[j];
+            uint32_t o = ((base + __umul24((uint32_t)min(r0 + 4 * k, NROWS - 1), (uint32_t)w) + a0) & ~15u) - a0 + 16u * j;
+            asm volatile("" : "+v"(o));  // keep the offset 32-bit (no re-fused 64-bit multiply-add)
+            v[k] = as_global(reinterpret_cast<const u32x4 *>(img + o))[0];
         }
     }
     __device__ __forceinline__ void store(uint8_t *P, int s) const {
@@ -1314,11 +1318,11 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
         // S1 = sum of (u + 15) I (dot4 with the u + 15 weights); then
         // m01 += v (S0(+v) - S0(-v)), m10 += S1 - 15 S0.  Integer sums: the
         // moments equal the reference's exactly.
-        const uint32_t o0 = (uint32_t)(uintptr_t)(img + (size_t)(cy - 15) * w + (cx - 15));
+        const uint32_t o0 = (uint32_t)(uintptr_t)img + __umul24((uint32_t)(cy - 15), (uint32_t)w) + (uint32_t)(cx - 15);
         const uint32_t W0[8] = {wq[0].x, wq[0].y, wq[0].z, wq[0].w, wq[1].x, wq[1].y, wq[1].z, wq[1].w};
         const uint32_t W1[8] = {wq[2].x, wq[2].y, wq[2].z, wq[2].w, wq[3].x, wq[3].y, wq[3].z, wq[3].w};
         auto row_sums = [&](int r, uint32_t &s0, uint32_t &s1) {
-            const uint32_t o = (o0 + (uint32_t)(r * w)) & 15u;  // window start inside LDS row r
+            const uint32_t o = (o0 + __umul24((uint32_t)r, (uint32_t)w)) & 15u;  // window start inside LDS row r
             const uint32_t *d = reinterpret_cast<const uint32_t *>(P + r * kPatchStride + (o & ~3u));
             uint32_t dw[9];
 #pragma unroll
@@ -1346,14 +1350,14 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     YGZ_BSTAMP_K(1, 5);
     wave_lds_order();  // IC taps read before the window is replaced
     wdesc.store(P, s);
-    const uint32_t o0 = (uint32_t)(uintptr_t)(bimg + (size_t)(cy - 18) * w + (cx - 18));
+    const uint32_t o0 = (uint32_t)(uintptr_t)bimg + __umul24((uint32_t)(cy - 18), (uint32_t)w) + (uint32_t)(cx - 18);
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float ang = angle * factorPI;
     const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
     YGZ_BSTAMP_K(1, 6);
     auto tap = [&](int dy, int dx) {  // blurred pixel (cy + dy, cx + dx)
         const int r = dy + 18;
-        return (int)P[r * kPatchStride + ((o0 + (uint32_t)(r * w)) & 15u) + dx + 18];
+        return (int)P[r * kPatchStride + ((o0 + __umul24((uint32_t)r, (uint32_t)w)) & 15u) + dx + 18];
     };
     uint32_t bits = 0;
 #pragma unroll
