@@ -1186,6 +1186,14 @@ constexpr int kPatchStride = 64;  // LDS row of a staged keypoint window: 4 x 16
 // unshifted to LDS by store_window (tap (r, c) at P[r*64 + o(r) + c]).
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+// a * b + c on 24-bit operands (v_mad_u32_u24, full rate); inline asm so the
+// compiler cannot widen it into a quarter-rate v_mad_u64_u32
+__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm volatile("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 template <int R, int NROWS>
 struct Window {
     static constexpr int NK = (NROWS + 3) / 4;
@@ -1198,8 +1206,7 @@ struct Window {
         const int j = s & 3, r0 = s >> 2;
 #pragma unroll
         for (int k = 0; k < NK; k++) {  // rows past the window re-read its last row (not stored)
-            uint32_t o = ((base + __umul24((uint32_t)min(r0 + 4 * k, NROWS - 1), (uint32_t)w) + a0) & ~15u) - a0 + 16u * j;
-            asm volatile("" : "+v"(o));  // keep the offset 32-bit (no re-fused 64-bit multiply-add)
+            const uint32_t o = ((mad24((uint32_t)min(r0 + 4 * k, NROWS - 1), (uint32_t)w, base) + a0) & ~15u) - a0 + 16u * j;
             v[k] = as_global(reinterpret_cast<const u32x4 *>(img + o))[0];
         }
     }
@@ -1322,7 +1329,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
         const uint32_t W0[8] = {wq[0].x, wq[0].y, wq[0].z, wq[0].w, wq[1].x, wq[1].y, wq[1].z, wq[1].w};
         const uint32_t W1[8] = {wq[2].x, wq[2].y, wq[2].z, wq[2].w, wq[3].x, wq[3].y, wq[3].z, wq[3].w};
         auto row_sums = [&](int r, uint32_t &s0, uint32_t &s1) {
-            const uint32_t o = (o0 + __umul24((uint32_t)r, (uint32_t)w)) & 15u;  // window start inside LDS row r
+            const uint32_t o = mad24((uint32_t)r, (uint32_t)w, o0) & 15u;  // window start inside LDS row r
             const uint32_t *d = reinterpret_cast<const uint32_t *>(P + r * kPatchStride + (o & ~3u));
             uint32_t dw[9];
 #pragma unroll
@@ -1355,9 +1362,10 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     const float ang = angle * factorPI;
     const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
     YGZ_BSTAMP_K(1, 6);
+    const uint32_t w16 = (uint32_t)w & 15u;  // only the row start's offset mod 16 matters
     auto tap = [&](int dy, int dx) {  // blurred pixel (cy + dy, cx + dx)
         const int r = dy + 18;
-        return (int)P[r * kPatchStride + ((o0 + __umul24((uint32_t)r, (uint32_t)w)) & 15u) + dx + 18];
+        return (int)P[r * kPatchStride + (mad24((uint32_t)r, w16, o0) & 15u) + dx + 18];
     };
     uint32_t bits = 0;
 #pragma unroll
