@@ -20,7 +20,9 @@ nblocks = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
 sc = S.PlaneScene(11, W, H)
 xi = np.array([0.012, -0.006, 0.009, 0.0025, -0.002, 0.0015], np.float32)
-frames = np.stack([sc.render(*ygzfe.trajectory_pose(i, xi), noise_seed=i) for i in range(B)])
+sys.path.insert(0, ROOT)
+from bench import sweep_index  # noqa: E402  (the bench's back-and-forth trajectory: full views at any B)
+frames = np.stack([sc.render(*ygzfe.trajectory_pose(sweep_index(i), xi), noise_seed=i) for i in range(B)])
 b = ygzfe.Batch((nf, sf, nl, ini, mn, 0), 0, W, H, B)
 b.upload(frames)
 for _ in range(3):
