@@ -156,181 +156,9 @@ __device__ void se3_exp_wave(const float a[6], SE3 &out) {
     for (int i = 0; i < 4; i++) out.q[i] = q[i];
 }
 
-// Eigen LDLT (diagonal pivoting, lower-triangle transpositions), solve with
-// |D_i| <= FLT_MIN treated as 0.  Same algorithm as oracle/align.c.
-__device__ void ldlt_solve6(const float Hin[36], const float b[6], float x[6]) {
-    float A[36];
-    int perm[6];
-    for (int i = 0; i < 36; i++) A[i] = Hin[i];
-    for (int i = 0; i < 6; i++) perm[i] = i;
-    for (int k = 0; k < 6; k++) {
-        int piv = k;
-        float big = fabsf(A[k * 6 + k]);
-        for (int i = k + 1; i < 6; i++)
-            if (fabsf(A[i * 6 + i]) > big) { big = fabsf(A[i * 6 + i]); piv = i; }
-        if (piv != k) {
-            for (int j = 0; j < k; j++) { const float t = A[k * 6 + j]; A[k * 6 + j] = A[piv * 6 + j]; A[piv * 6 + j] = t; }
-            for (int i = piv + 1; i < 6; i++) { const float t = A[i * 6 + k]; A[i * 6 + k] = A[i * 6 + piv]; A[i * 6 + piv] = t; }
-            { const float t = A[k * 6 + k]; A[k * 6 + k] = A[piv * 6 + piv]; A[piv * 6 + piv] = t; }
-            for (int i = k + 1; i < piv; i++) { const float t = A[i * 6 + k]; A[i * 6 + k] = A[piv * 6 + i]; A[piv * 6 + i] = t; }
-            const int t = perm[k]; perm[k] = perm[piv]; perm[piv] = t;
-        }
-        float tmp[6];
-        for (int j = 0; j < k; j++) tmp[j] = A[j * 6 + j] * A[k * 6 + j];
-        float s = 0.f;
-        for (int j = 0; j < k; j++) s += A[k * 6 + j] * tmp[j];
-        A[k * 6 + k] -= s;
-        for (int i = k + 1; i < 6; i++) {
-            float t = 0.f;
-            for (int j = 0; j < k; j++) t += A[i * 6 + j] * tmp[j];
-            A[i * 6 + k] -= t;
-        }
-        const float akk = A[k * 6 + k];
-        if (k == 0 && akk == 0.f) {
-            for (int i = 0; i < 6; i++) perm[i] = i;
-            break;
-        }
-        if (akk != 0.f)
-            for (int i = k + 1; i < 6; i++) A[i * 6 + k] /= akk;
-    }
-    float y[6];
-    for (int i = 0; i < 6; i++) y[i] = b[perm[i]];
-    for (int i = 0; i < 6; i++) {
-        float s = y[i];
-        for (int j = 0; j < i; j++) s -= A[i * 6 + j] * y[j];
-        y[i] = s;
-    }
-    for (int i = 0; i < 6; i++) {
-        const float d = A[i * 6 + i];
-        y[i] = fabsf(d) > 1.17549435e-38f ? y[i] / d : 0.f;
-    }
-    for (int i = 5; i >= 0; i--) {
-        float s = y[i];
-        for (int j = i + 1; j < 6; j++) s -= A[j * 6 + i] * y[j];
-        y[i] = s;
-    }
-    for (int i = 0; i < 6; i++) x[perm[i]] = y[i];
-}
-
-// The pivoted LDLT for wave-uniform systems: the pivot index is made
-// provably uniform (readfirstlane), so the row/column exchange is a scalar
-// branch to one straight-line case with constant indices instead of selects
-// over every candidate pivot; columns are scaled by one reciprocal per pivot.
-// Same pivot order and zero-pivot rules as ldlt_solve6 (the division by a
-// reciprocal product rounds differently: pose parity is 1e-4).
-template <int K, int P>
-__device__ __forceinline__ void ldlt6_exchange(float (&A)[36], int (&perm)[6]) {
-#pragma unroll
-    for (int j = 0; j < K; j++) { const float t = A[K * 6 + j]; A[K * 6 + j] = A[P * 6 + j]; A[P * 6 + j] = t; }
-#pragma unroll
-    for (int i = P + 1; i < 6; i++) { const float t = A[i * 6 + K]; A[i * 6 + K] = A[i * 6 + P]; A[i * 6 + P] = t; }
-    { const float t = A[K * 6 + K]; A[K * 6 + K] = A[P * 6 + P]; A[P * 6 + P] = t; }
-#pragma unroll
-    for (int i = K + 1; i < P; i++) { const float t = A[i * 6 + K]; A[i * 6 + K] = A[P * 6 + i]; A[P * 6 + i] = t; }
-    const int t = perm[K]; perm[K] = perm[P]; perm[P] = t;
-}
-
-template <int K>
-__device__ __forceinline__ void ldlt6_pivot(float (&A)[36], int (&perm)[6], int piv) {
-    if constexpr (K + 1 < 6) { if (piv == K + 1) { ldlt6_exchange<K, K + 1>(A, perm); return; } }
-    if constexpr (K + 2 < 6) { if (piv == K + 2) { ldlt6_exchange<K, K + 2>(A, perm); return; } }
-    if constexpr (K + 3 < 6) { if (piv == K + 3) { ldlt6_exchange<K, K + 3>(A, perm); return; } }
-    if constexpr (K + 4 < 6) { if (piv == K + 4) { ldlt6_exchange<K, K + 4>(A, perm); return; } }
-    if constexpr (K + 5 < 6) { if (piv == K + 5) { ldlt6_exchange<K, K + 5>(A, perm); return; } }
-}
-
-template <int K>
-__device__ __forceinline__ bool ldlt6_step(float (&A)[36], int (&perm)[6]) {
-    int piv = K;
-    float big = fabsf(A[K * 6 + K]);
-#pragma unroll
-    for (int i = K + 1; i < 6; i++)
-        if (fabsf(A[i * 6 + i]) > big) { big = fabsf(A[i * 6 + i]); piv = i; }
-    piv = __builtin_amdgcn_readfirstlane(piv);
-    if (piv != K) ldlt6_pivot<K>(A, perm, piv);
-    float tmp[6];
-#pragma unroll
-    for (int j = 0; j < K; j++) tmp[j] = A[j * 6 + j] * A[K * 6 + j];
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < K; j++) s += A[K * 6 + j] * tmp[j];
-    A[K * 6 + K] -= s;
-#pragma unroll
-    for (int i = K + 1; i < 6; i++) {
-        float t = 0.f;
-#pragma unroll
-        for (int j = 0; j < K; j++) t += A[i * 6 + j] * tmp[j];
-        A[i * 6 + K] -= t;
-    }
-    const float akk = A[K * 6 + K];
-    if (K == 0 && akk == 0.f) return false;  // Eigen: a zero first pivot ends the factorization
-    if (akk != 0.f) {
-        const float r = __builtin_amdgcn_rcpf(akk);
-#pragma unroll
-        for (int i = K + 1; i < 6; i++) A[i * 6 + K] *= r;
-    }
-    return true;
-}
-
-__device__ __forceinline__ void ldlt_solve6_uni(float (&A)[36], const float b[6], float x[6]) {
-    int perm[6] = {0, 1, 2, 3, 4, 5};
-    if (!ldlt6_step<0>(A, perm)) {
-#pragma unroll
-        for (int i = 0; i < 6; i++) perm[i] = i;
-    } else {
-        ldlt6_step<1>(A, perm);
-        ldlt6_step<2>(A, perm);
-        ldlt6_step<3>(A, perm);
-        ldlt6_step<4>(A, perm);
-        ldlt6_step<5>(A, perm);
-    }
-    float y[6];
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        float v = 0.f;
-#pragma unroll
-        for (int j = 0; j < 6; j++) v = perm[i] == j ? b[j] : v;
-        y[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        float s = y[i];
-#pragma unroll
-        for (int j = 0; j < i; j++) s -= A[i * 6 + j] * y[j];
-        y[i] = s;
-    }
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        const float d = A[i * 6 + i];
-        y[i] = fabsf(d) > 1.17549435e-38f ? y[i] * __builtin_amdgcn_rcpf(d) : 0.f;
-    }
-#pragma unroll
-    for (int i = 5; i >= 0; i--) {
-        float s = y[i];
-#pragma unroll
-        for (int j = i + 1; j < 6; j++) s -= A[j * 6 + i] * y[j];
-        y[i] = s;
-    }
-#pragma unroll
-    for (int j = 0; j < 6; j++) {
-        float v = 0.f;
-#pragma unroll
-        for (int i = 0; i < 6; i++) v = perm[i] == j ? y[i] : v;
-        x[j] = v;
-    }
-}
-
-// Eigen's LDLT is left-looking: step k searches the pivot among the diagonal
-// entries k..5 that no update has touched yet, i.e. among the ORIGINAL
-// diagonal in its current (transposed) order.  The transposition sequence is
-// therefore fixed by |H_ii| alone, and pivoting = factoring P H P^T with P
-// known upfront: the same values meet the same operations in the same order as
-// in ldlt_solve6_uni (bit-identical results), without data-dependent register
-// exchanges.  The wave-uniform system is read from the lanes of r (lanes 0..5
-// b, lanes 8.. the upper triangle of H, row-major); the transposition sequence
-// runs on the scalar unit (|x| float bits order like |x| for non-NaN x) and the
-// permuted system is gathered by readlane with scalar lane indices.
-__device__ __forceinline__ int hpack6(int i, int j) {  // row-major upper-triangle index of (i, j)
+// Row-major upper-triangle index of (i, j): the lane order of the H components
+// (lane 8 + hpack6) in the solver wave.
+__device__ __forceinline__ int hpack6(int i, int j) {
     const int a = i < j ? i : j, c = i < j ? j : i;
     return a * 6 - ((a * (a - 1)) >> 1) + (c - a);
 }
@@ -361,36 +189,21 @@ __device__ __forceinline__ bool ldlt6_step_nopiv(float (&A)[36]) {
     return true;
 }
 
-__device__ __forceinline__ void ldlt_solve6_presorted(float r, int lane, float x[6]) {
+// H = J^T J is symmetric positive semi-definite, for which LDL^T needs no
+// pivoting to be backward stable: this variant factors H in place (no pivot
+// search, no permutation), straight-line code on wave-uniform values.  Against
+// Eigen's diagonally pivoted LDLT the solution differs by rounding only (pose
+// parity is 1e-4).  The zero rules are Eigen's: a zero first pivot leaves the
+// factorization, |D_i| <= FLT_MIN gives y_i = 0 (an all-zero H solves to x = 0).
+__device__ __forceinline__ void ldlt_solve6_nopiv(float r, float x[6]) {
     const int ri = __float_as_int(r);
-    uint32_t d[6];
-    int pk[6];
+    float A[36], y[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) {
-        d[i] = (uint32_t)__builtin_amdgcn_readlane(ri, 8 + hpack6(i, i)) & 0x7FFFFFFFu;
-        pk[i] = i;
-    }
+        y[i] = __int_as_float(__builtin_amdgcn_readlane(ri, i));
 #pragma unroll
-    for (int k = 0; k < 6; k++) {  // Eigen's transpositions: first maximum of the remaining diagonal
-        int piv = k;
-        uint32_t big = d[k];
-#pragma unroll
-        for (int i = k + 1; i < 6; i++)
-            if (d[i] > big) { big = d[i]; piv = i; }
-#pragma unroll
-        for (int i = k + 1; i < 6; i++)
-            if (piv == i) {
-                const uint32_t td = d[k]; d[k] = d[i]; d[i] = td;
-                const int tp = pk[k]; pk[k] = pk[i]; pk[i] = tp;
-            }
-    }
-    float A[36], b[6];
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        b[i] = __int_as_float(__builtin_amdgcn_readlane(ri, pk[i]));
-#pragma unroll
-        for (int j = 0; j <= i; j++) {
-            const float v = __int_as_float(__builtin_amdgcn_readlane(ri, 8 + hpack6(pk[i], pk[j])));
+        for (int j = i; j < 6; j++) {
+            const float v = __int_as_float(__builtin_amdgcn_readlane(ri, 8 + hpack6(i, j)));
             A[i * 6 + j] = v;
             A[j * 6 + i] = v;
         }
@@ -402,10 +215,9 @@ __device__ __forceinline__ void ldlt_solve6_presorted(float r, int lane, float x
         ldlt6_step_nopiv<4>(A);
         ldlt6_step_nopiv<5>(A);
     }
-    float y[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) {
-        float t = b[i];
+        float t = y[i];
 #pragma unroll
         for (int j = 0; j < i; j++) t -= A[i * 6 + j] * y[j];
         y[i] = t;
@@ -422,25 +234,14 @@ __device__ __forceinline__ void ldlt_solve6_presorted(float r, int lane, float x
         for (int j = i + 1; j < 6; j++) t -= A[j * 6 + i] * y[j];
         y[i] = t;
     }
-    // x[pk[i]] = y[i]: y spread over lanes 0..5, read back through the inverse permutation
-    float yl = 0.f;
 #pragma unroll
-    for (int i = 0; i < 6; i++) yl = lane == i ? y[i] : yl;
-    int inv[6];
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        int v = 0;
-#pragma unroll
-        for (int q = 0; q < 6; q++) v = pk[q] == i ? q : v;
-        inv[i] = v;
-    }
-#pragma unroll
-    for (int j = 0; j < 6; j++) x[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yl), inv[j]));
+    for (int i = 0; i < 6; i++) x[i] = y[i];
 }
 
-// The same LDLT with every array index a compile-time constant (pivot swaps
-// and the permutation are applied through selects), so the solver keeps the
-// 6x6 system in VGPRs instead of scratch.  Identical arithmetic to ldlt_solve6.
+// Eigen's diagonally pivoted LDLT (lower-triangle transpositions; |D_i| <=
+// FLT_MIN gives 0), the algorithm of oracle/align.c, with every array index a
+// compile-time constant (pivot swaps and the permutation applied through
+// selects) so the 6x6 system stays in VGPRs: the generic (> 960 features) path.
 __device__ __forceinline__ void ldlt_solve6_reg(const float Hin[36], const float b[6], float x[6]) {
     float A[36];
     int perm[6];
@@ -788,46 +589,8 @@ __device__ __attribute__((noinline)) void sparse_align_generic(const AlignLevels
 // contributions are closed forms of the per-feature sums
 // Sx = sum gx*res, Sy = sum gy*res, Sxx, Sxy, Syy (same algebra, different
 // float association than the reference's per-pixel sums -> 1e-4 pose parity).
-// 32 partial sums are reduced with a 6-step butterfly (each step halves the
-// values a lane carries) and one LDS pass over the waves.
-__device__ __forceinline__ float wave_butterfly32(float (&v)[32], int lane) {
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        const bool hi = lane & 32;
-        const float send = hi ? v[i] : v[16 + i];
-        const float keep = hi ? v[16 + i] : v[i];
-        v[i] = keep + __shfl_xor(send, 32, 64);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const bool hi = lane & 16;
-        const float send = hi ? v[i] : v[8 + i];
-        const float keep = hi ? v[8 + i] : v[i];
-        v[i] = keep + __shfl_xor(send, 16, 64);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const bool hi = lane & 8;
-        const float send = hi ? v[i] : v[4 + i];
-        const float keep = hi ? v[4 + i] : v[i];
-        v[i] = keep + __shfl_xor(send, 8, 64);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const bool hi = lane & 4;
-        const float send = hi ? v[i] : v[2 + i];
-        const float keep = hi ? v[2 + i] : v[i];
-        v[i] = keep + __shfl_xor(send, 4, 64);
-    }
-    {
-        const bool hi = lane & 2;
-        const float send = hi ? v[0] : v[1];
-        const float keep = hi ? v[1] : v[0];
-        v[0] = keep + __shfl_xor(send, 2, 64);
-    }
-    return v[0] + __shfl_xor(v[0], 1, 64);  // lane holds the total of value (lane >> 1)
-}
-
+// The per-feature sums are reduced by transposing DPP / permlane steps
+// (wave_reduce8 / wave_reduce32) and one LDS pass over the waves.
 #ifdef YGZ_STAMPS
 // diagnostic build only (lib/libygzfe_diag.so): solver-wave timestamps of block 0
 __device__ unsigned long long g_stamps[4096];
@@ -1005,7 +768,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                         s_nmeas = nmeas;
                     }
                     YGZ_STAMP(7);
-                    ldlt_solve6_presorted(r, lane, x);
+                    ldlt_solve6_nopiv(r, x);
                     YGZ_STAMP(8);
                     const bool stop = s_stop || isnan(x[0]);
                     const bool rollback = (it > 0 && (double)new_chi2 > 1.2 * (double)s_chi2) || stop;
