@@ -113,16 +113,17 @@ __device__ void se3_exp(const float a[6], SE3 &out) {
 }
 
 // se3_exp with the four transcendentals evaluated in parallel lanes (lane 0:
-// sincos(theta/2), lane 1: sincos(theta)) and broadcast by readlane; every lane
-// of the calling wave must be active and pass the same argument.
+// sincos(theta/2), lane 1: sincos(theta), hardware sin/cos) and broadcast by
+// readlane; every lane of the calling wave must be active and pass the same argument.
 __device__ void se3_exp_wave(const float a[6], SE3 &out) {
     const float eps = 1e-5f;
     const float w0 = a[3], w1 = a[4], w2 = a[5];
     const float theta_sq = w0 * w0 + w1 * w1 + w2 * w2;
     const float theta = sqrtf(theta_sq);
     const float half_theta = 0.5f * theta;
-    float sn, cs;
-    sincosf((threadIdx.x & 1) ? theta : half_theta, &sn, &cs);
+    // hardware v_sin/v_cos (GN increments are small angles; the pose parity is 1e-4)
+    const float arg = (threadIdx.x & 1) ? theta : half_theta;
+    const float sn = __sinf(arg), cs = __cosf(arg);
     const float s_half = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sn), 0));
     const float c_half = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cs), 0));
     const float s_th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sn), 1));
