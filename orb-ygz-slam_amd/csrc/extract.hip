@@ -407,9 +407,6 @@ __global__ __launch_bounds__(256) void k_blur7(const uint8_t *__restrict__ pyr,
         }
     }
     // border columns (x < 4, x >= w - 3; every column when w < 16) of this strip
-#ifdef YGZ_NO_BLUR_BORDER
-    if (w >= 16) return;  // A/B timing experiment only
-#endif
     const int ncol = w >= 16 ? 7 : w;
     const bool left = sx == 0, right = sx + 256 >= w;
     if (w >= 16 && !left && !right) return;
