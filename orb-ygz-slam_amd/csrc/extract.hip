@@ -723,13 +723,17 @@ struct OctLds {
     int scal[8];
 };
 
+// Inclusive wave scan on DPP: Hillis-Steele inside each 16-lane row
+// (row_shr:1,2,4,8; lanes shifted in from outside the row add 0), then
+// row_bcast:15 / row_bcast:31 carry rows 0-1 / 0-2 into the rows above.
+// Six DPP adds instead of six LDS-routed shuffles.
 __device__ __forceinline__ int wave_incl_scan(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
     return v;
 }
 
@@ -1039,9 +1043,16 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
     const int N = L.budget;
     int cur = 0, seqc = nIni, overflow = 0, nexpand = 0, guard = 0;
     bool final_round = false;
+    if (l == 0) YGZ_BSTAMP_K(4, 3);
     while (true) {
         const int prev = size;
         octree_pass<NC, NT>(S, K, nid, n, N, final_round, cur, size, seqc, nexpand, overflow);
+        if (l == 0 && guard < 4) {  // diagnostic build (STAMPK=4): the first four passes
+            if (guard == 0) YGZ_BSTAMP_K(4, 4);
+            if (guard == 1) YGZ_BSTAMP_K(4, 5);
+            if (guard == 2) YGZ_BSTAMP_K(4, 6);
+            if (guard == 3) YGZ_BSTAMP_K(4, 7);
+        }
         if (overflow || ++guard > 4096) { overflow = 1; break; }
         if (size >= N || size == prev) break;
         if (!final_round && size + nexpand * 3 > N) final_round = true;
@@ -1065,6 +1076,8 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
     }
     if (l == 0) YGZ_BSTAMP_K(3, 1);
     if (l == 0) YGZ_BSTAMP_K(3, 2);
+    if (l == 0) YGZ_BSTAMP_K(4, 1);
+    if (l == 0) YGZ_BSTAMP_K(4, 2);
 }
 
 // Keys and labels in LDS when the level has at most kOctLdsKeys candidates
@@ -1089,6 +1102,7 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan *__restrict__ plan,
     int *s_pref = reinterpret_cast<int *>(S.sortk);  // gather prefix; sortk is free until the final rounds
     const int f = blockIdx.x, l = level0 + blockIdx.y, tid = threadIdx.x;
     if (l == 0) YGZ_BSTAMP_K(3, 0);
+    if (l == 0) YGZ_BSTAMP_K(4, 0);
     const LevelDesc &L = plan->lv[l];
     int part = 0;
     for (int c = tid; c < L.ncells; c += NT) part += cellcnt[(size_t)f * plan->ncells + L.cell_begin + c];
