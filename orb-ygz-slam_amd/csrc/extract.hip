@@ -1286,12 +1286,12 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     const int nl = plan->nlevels;
     const int *sc = selcnt + (size_t)f * nl;
     const int ne = n_existing ? n_existing[f] : 0;
-    int incl = lane < nl ? sc[lane] : 0;  // per-level counts, prefix over lanes 0..15
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-        const int v = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += v;
-    }
+    // per-level counts, inclusive prefix over lanes 0..15 (DPP row_shr inside the first row)
+    int incl = lane < nl ? sc[lane] : 0;
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, false);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, false);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, false);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, false);
     int l = 0, pre = 0;
     for (int q = 0; q < nl; q++) {
         const int iq = __builtin_amdgcn_readlane(incl, q);
