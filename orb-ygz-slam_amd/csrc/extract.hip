@@ -647,10 +647,13 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
 // (A persistent variant -- a resident-sized grid walking item ranges with the
 // next ROI prefetched -- measured slower: item costs vary with texture, and
 // the waves per CU, not the dispatch, bound the throughput.)
+#ifndef YGZ_FAST_WAVES_EU
+#define YGZ_FAST_WAVES_EU 6  // waves per SIMD the FAST kernels are register-limited to
+#endif
 constexpr int kFastWaves = 4;  // cells (waves) per workgroup (8 measured slower: a block holds its LDS until its slowest cell ends)
 
 template <int S, int R>
-__global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(6))) void k_fast_cells(
+__global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(YGZ_FAST_WAVES_EU))) void k_fast_cells(
     const uint8_t *__restrict__ pyr, uint32_t pitch, const Plan *__restrict__ plan,
     const CellDesc *__restrict__ cells, uint32_t *__restrict__ cellbuf, int *__restrict__ cellcnt, int cell_begin,
     int cell_end) {
