@@ -21,14 +21,23 @@ namespace ygzfe {
 // inside an operand is free as long as A and B agree: k-step s, lane half h
 // carries descriptor bits [32 s + 16 h, 32 s + 16 h + 16).
 //
-// A workgroup serves 128 queries (4 waves x 32) and streams the train set in
-// 32-row tiles; each tile is expanded to bytes once into LDS (double buffered)
-// and read by all 4 waves.  Per lane the running best / second best are keys
+// A workgroup serves kHamWaves x 32 queries and streams the train set in
+// 32-row tiles; each tile is expanded to bytes once into LDS (double buffered,
+// by the first 256 threads) and read by all waves.  Per lane the running best /
+// second best are keys
 //   key = ((D + 256) << 22) | train_index
 // so the smallest key is the smallest distance with the earliest index (the
-// sequential loop's `dist < bestDist`), and second = min over the other keys:
-//   k2 = min(k2, max(k1, key)); k1 = min(k1, key)       (3 VALU, no branches).
-constexpr int kHamQPB = 128;                 // queries per workgroup
+// sequential loop's `dist < bestDist`), and second = min over the other keys.
+// With k1 <= k2 that is  k2 = med3(k1, key, k2); k1 = min(k1, key)  (2 VALU,
+// no branches), and the key itself is one v_lshl_add_u32 of the accumulator
+// and a wave-uniform (SGPR) index base: inside the loop the index omits the
+// lane half's row offset 4h, which is added once before the two halves merge
+// (a constant per lane, so it keeps each lane's order).
+#ifndef YGZ_HAM_WAVES
+#define YGZ_HAM_WAVES 8
+#endif
+constexpr int kHamWaves = YGZ_HAM_WAVES;     // query waves per workgroup
+constexpr int kHamQPB = 32 * kHamWaves;      // queries per workgroup
 constexpr int kHamRowBytes = 256 + 16;       // expanded train row + pad (conflict-free b128 reads)
 constexpr int kHamTileBytes = 32 * kHamRowBytes;
 constexpr uint32_t kHamNone = 0xFFFFFFFFu;
@@ -41,6 +50,22 @@ typedef int ham_v16i __attribute__((ext_vector_type(16)));
 // nibble never overlap, so the product has no carries)
 __device__ __forceinline__ uint32_t nib_bytes(uint32_t bits16, int m) {
     return (__umul24((bits16 >> (4 * m)) & 0xFu, 0x00204081u)) & 0x01010101u;
+}
+
+// (a << 22) + (u + c), u + c wave-uniform: one v_lshl_add_u32 with an SGPR
+// operand (the SALU add is opaque, so the constant is not re-associated into a
+// second VALU add; the shift-add stays plain C, so the MFMA -> VALU read
+// hazard is still the compiler's to pad)
+__device__ __forceinline__ uint32_t ham_key(int a, uint32_t u, uint32_t c) {
+    uint32_t b;
+    asm("s_add_u32 %0, %1, %2" : "=s"(b) : "s"(u), "s"(c) : "scc");
+    return ((uint32_t)a << 22) + b;
+}
+
+__device__ __forceinline__ uint32_t ham_med3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
 }
 
 __device__ __forceinline__ void ham_expand_store(uint8_t *s_tile, int row, int s, uint32_t w) {
@@ -85,53 +110,55 @@ __device__ __forceinline__ void hamming_block_mfma(const uint8_t *__restrict__ q
         }
     }
     uint32_t k1 = kHamNone, k2 = kHamNone;
-    // key of accumulator register r: (D << 22) + (256 << 22) + tile row base +
-    // this lane half's row offset 4h + the register's row offset (a constant)
-    const uint32_t lane_base = (256u << 22) + 4u * (uint32_t)h;
+    // waves whose 32 queries all lie past nq only stage tiles
+    const bool active = qblock * kHamQPB + wave * 32 < nq;
     const int ntiles = (nt + 31) >> 5;
-    // staging: thread -> (row tid >> 3, dword tid & 7) of a 32-row tile
+    // staging (threads < 256): thread -> (row tid >> 3, dword tid & 7) of a 32-row tile
     const int srow = tid >> 3, sdw = tid & 7;
+    const bool stager = tid < 256;
     auto fetch = [&](int tile) -> uint32_t {
         const int row = tile * 32 + srow;
-        return row < nt ? reinterpret_cast<const uint32_t *>(t + (size_t)row * 32)[sdw] : 0u;
+        return stager && row < nt ? reinterpret_cast<const uint32_t *>(t + (size_t)row * 32)[sdw] : 0u;
     };
-    if (ntiles > 0) ham_expand_store(s_tile[0], srow, sdw, fetch(0));
+    if (ntiles > 0 && stager) ham_expand_store(s_tile[0], srow, sdw, fetch(0));
     __syncthreads();
     for (int tile = 0; tile < ntiles; tile++) {
         const uint8_t *L = s_tile[tile & 1];
         const bool more = tile + 1 < ntiles;
         const uint32_t nxt = more ? fetch(tile + 1) : 0u;  // in flight during the MFMAs
-        ham_v16i acc = {};
-        const uint8_t *arow = L + (lane & 31) * kHamRowBytes + h * 16;
+        if (active) {
+            ham_v16i acc = {};
+            const uint8_t *arow = L + (lane & 31) * kHamRowBytes + h * 16;
 #pragma unroll
-        for (int s = 0; s < 8; s++) {
-            const ham_v4i a = *(const ham_v4i *)(arow + s * 32);
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[s], acc, 0, 0, 0);
-        }
-        if (more) ham_expand_store(s_tile[(tile + 1) & 1], srow, sdw, nxt);
-        const uint32_t tb = (uint32_t)tile * 32, kb = lane_base + tb;
-        if (tb + 32 <= (uint32_t)nt) {
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const uint32_t key = ((uint32_t)acc[r] << 22) + kb + (uint32_t)((r & 3) + 8 * (r >> 2));
-                const uint32_t m = max(k1, key);
-                k1 = min(k1, key);
-                k2 = min(k2, m);
+            for (int s = 0; s < 8; s++) {
+                const ham_v4i a = *(const ham_v4i *)(arow + s * 32);
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[s], acc, 0, 0, 0);
             }
-        } else {  // partial last tile: rows past nt never win
+            const uint32_t tb = (uint32_t)tile * 32, tu = (256u << 22) + tb;
+            if (tb + 32 <= (uint32_t)nt) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const uint32_t row = tb + (uint32_t)((r & 3) + 8 * (r >> 2) + 4 * h);
-                const uint32_t key =
-                    row < (uint32_t)nt ? ((uint32_t)acc[r] << 22) + kb + (uint32_t)((r & 3) + 8 * (r >> 2)) : kHamNone;
-                const uint32_t m = max(k1, key);
-                k1 = min(k1, key);
-                k2 = min(k2, m);
+                for (int r = 0; r < 16; r++) {
+                    const uint32_t key = ham_key(acc[r], tu, (uint32_t)((r & 3) + 8 * (r >> 2)));
+                    k2 = ham_med3(k1, key, k2);
+                    k1 = min(k1, key);
+                }
+            } else {  // partial last tile: rows past nt never win
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const uint32_t row = tb + (uint32_t)((r & 3) + 8 * (r >> 2) + 4 * h);
+                    const uint32_t key =
+                        row < (uint32_t)nt ? ham_key(acc[r], tu, (uint32_t)((r & 3) + 8 * (r >> 2))) : kHamNone;
+                    k2 = ham_med3(k1, key, k2);
+                    k1 = min(k1, key);
+                }
             }
         }
+        if (more && stager) ham_expand_store(s_tile[(tile + 1) & 1], srow, sdw, nxt);
         __syncthreads();  // tile + 1 staged; tile's buffer free for tile + 2
     }
-    // merge the two lane halves (same query, disjoint rows)
+    // the lane half's row offset, then merge the two halves (same query, disjoint rows)
+    if (k1 != kHamNone) k1 += 4u * (uint32_t)h;
+    if (k2 != kHamNone) k2 += 4u * (uint32_t)h;
     const uint32_t o1 = (uint32_t)__shfl_xor((int)k1, 32, 64), o2 = (uint32_t)__shfl_xor((int)k2, 32, 64);
     const uint32_t K1 = min(k1, o1), K2 = min(max(k1, o1), min(k2, o2));
     if (h == 0 && qi < nq) {
@@ -141,7 +168,7 @@ __device__ __forceinline__ void hamming_block_mfma(const uint8_t *__restrict__ q
     }
 }
 
-__global__ __launch_bounds__(256) void k_hamming_best2(const uint8_t *__restrict__ q, int nq,
+__global__ __launch_bounds__(64 * kHamWaves) void k_hamming_best2(const uint8_t *__restrict__ q, int nq,
                                                        const uint8_t *__restrict__ t, int nt,
                                                        int32_t *__restrict__ bi, int32_t *__restrict__ bd,
                                                        int32_t *__restrict__ sd) {
@@ -151,7 +178,7 @@ __global__ __launch_bounds__(256) void k_hamming_best2(const uint8_t *__restrict
 // batched: pair p matches the descriptors of frame qframe[p] against frame
 // tframe[p] of a batch (rows [0, counts[f]) of a [F][row_cap][32] array);
 // outputs at [p][row_cap].
-__global__ __launch_bounds__(256) void k_hamming_best2_pairs(const uint8_t *__restrict__ desc,
+__global__ __launch_bounds__(64 * kHamWaves) void k_hamming_best2_pairs(const uint8_t *__restrict__ desc,
                                                              const int32_t *__restrict__ counts, int row_cap,
                                                              const int32_t *__restrict__ qframe,
                                                              const int32_t *__restrict__ tframe,
@@ -187,7 +214,7 @@ hipError_t launch_hamming_best2(const uint8_t *q, int nq, const uint8_t *t, int 
                                 int32_t *sd, hipStream_t st) {
     if (nq <= 0) return hipSuccess;
     if (nt > kHamMaxTrain) return hipErrorInvalidValue;  // train index must fit the key's 22 bits
-    hipLaunchKernelGGL(k_hamming_best2, dim3((nq + kHamQPB - 1) / kHamQPB), dim3(256), 0, st, q, nq, t, nt, bi, bd,
+    hipLaunchKernelGGL(k_hamming_best2, dim3((nq + kHamQPB - 1) / kHamQPB), dim3(64 * kHamWaves), 0, st, q, nq, t, nt, bi, bd,
                        sd);
     return hipGetLastError();
 }
@@ -197,7 +224,7 @@ hipError_t launch_hamming_best2_pairs(const uint8_t *desc, const int32_t *counts
                                       int32_t *sd, hipStream_t st) {
     if (npairs <= 0) return hipSuccess;
     if (row_cap > kHamMaxTrain) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_hamming_best2_pairs, dim3((row_cap + kHamQPB - 1) / kHamQPB, npairs), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_hamming_best2_pairs, dim3((row_cap + kHamQPB - 1) / kHamQPB, npairs), dim3(64 * kHamWaves), 0, st,
                        desc, counts, row_cap, qframe, tframe, bi, bd, sd);
     return hipGetLastError();
 }
