@@ -357,6 +357,7 @@ def main():
                        "mean_keypoints": round(N, 1), "mean_align_visible": round(nv, 1),
                        "mean_fast_candidates": round(float(cand.sum()) / B, 1),
                        "mean_fast_candidates_per_level": [round(float(c) / B, 1) for c in cand],
+                       "mean_keypoints_per_level": [round(float(c) / B, 1) for c in selk],
                        "parallelism": f"frame-sharded x{world}", "schedule": args.schedule,
                        "hip_graph": graph_ok},
             "roofline": roof,
