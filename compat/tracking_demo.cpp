@@ -74,6 +74,20 @@ int main() {
         std::printf("align visible %zu t (%.4f %.4f %.4f) expected (%.4f %.4f 0)\n", nvis, TCR.t[0], TCR.t[1],
                     TCR.t[2], tx, ty);
         if (nvis < 100 || std::fabs(TCR.t[0] - tx) > 2e-3f || std::fabs(TCR.t[1] - ty) > 2e-3f) fails++;
+        // getFisherInformation() = H_ / (float)(5e-4 * 255 * 255) (SparseImageAlign.cc:51-55)
+        const auto fisher = align.getFisherInformation();
+        int fisher_bad = 0;
+        for (int i = 0; i < 36; i++)
+            fisher_bad += fisher[i] != align.hessian()[i] / (float)(5e-4 * 255 * 255);
+        std::printf("fisher information H/32.5125: %s (I00 %.4g, H00 %.4g)\n", fisher_bad ? "WRONG" : "ok", fisher[0],
+                    align.hessian()[0]);
+        if (fisher_bad || !(align.hessian()[0] > 0.f)) fails++;
+        // n_iter is ignored like the reference's (iterations[] overrides it, SparseImageAlign.cc:38-43)
+        ygz::SparseImgAlign align30(3, 1, 30);
+        ygz::SE3 TCR30;
+        const size_t nvis30 = align30.run(f0, f1, cam, k0, xyz.data(), usable.data(), TCR30);
+        std::printf("n_iter=30 ignored: visible %zu, same pose %d\n", nvis30, (int)(TCR30.t == TCR.t && TCR30.q == TCR.q));
+        if (nvis30 != nvis || !(TCR30.t == TCR.t && TCR30.q == TCR.q)) fails++;
 
         // Align2D on level 0: the patch around frame 1's strongest level-0 corner,
         // started 0.7 / -0.5 px off

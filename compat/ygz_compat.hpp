@@ -236,8 +236,10 @@ struct SE3 {
 class SparseImgAlign {
 public:
     // SparseImgAlign(int n_levels, int min_level, int n_iter = 10, Method = GaussNewton, ...) (SparseImageAlign.h:37-43)
+    // n_iter is accepted and ignored, as in the reference: run() overrides it per level
+    // with iterations[] = {10, ...} (SparseImageAlign.cc:38-43).
     SparseImgAlign(int n_levels, int min_level, int n_iter = 10) : max_level_(n_levels), min_level_(min_level) {
-        if (n_iter != 10) throw std::invalid_argument("SparseImgAlign: the kernels run the reference's 10 GN iterations");
+        (void)n_iter;
     }
     // size_t run(Frame* ref, Frame* cur, SE3f& TCR) (SparseImageAlign.cc:20-49): the ref
     // frame's keypoints, xyz_ref = T_ref * P_w per keypoint, usable = has a good MapPoint.
@@ -256,13 +258,16 @@ public:
         std::memcpy(H_, r.H, sizeof(H_));
         return (size_t)(r.n_visible > 0 ? r.n_visible : 0);
     }
-    // getFisherInformation() (SparseImageAlign.h:52-56): H / (sigma_i^2), sigma_i = 5e-4 * 255
+    // getFisherInformation() (SparseImageAlign.cc:51-55): H_ / sigma_i_sq with
+    // float sigma_i_sq = 5e-4 * 255 * 255 (double product, 32.5125, rounded to float)
     std::array<float, 36> getFisherInformation() const {
-        const float s2 = (5e-4f * 255.f) * (5e-4f * 255.f);
+        const float s2 = (float)(5e-4 * 255 * 255);
         std::array<float, 36> I;
         for (int i = 0; i < 36; i++) I[i] = H_[i] / s2;
         return I;
     }
+    // H_ of the last linearisation (NLLSSolver::H_), row-major 6x6
+    const float *hessian() const { return H_; }
 
 private:
     int max_level_, min_level_;

@@ -141,14 +141,18 @@ int ygzfe_batch_frames(ygzfe_batch *b, uint8_t **d_frames);
  * [max_frames * kp_cap * 32], counts [max_frames]. */
 int ygzfe_batch_bind_buffers(ygzfe_batch *b, uint8_t *d_pyramids, ygzfe_kp *d_kps, uint8_t *d_desc,
                              int32_t *d_counts);
-/* H2D of n_frames tight width x height images into the level-0 slots. */
+/* H2D of n_frames tight width x height images into the level-0 slots.  Waits
+ * for the previous extraction of this batch; work the caller queued on its own
+ * streams after that extraction (match, align, ...) must be complete. */
 int ygzfe_batch_upload(ygzfe_batch *b, const uint8_t *frames, int n_frames);
 /* Pyramid + FAST + octree + orientation + blur + rBRIEF on frames [0, n). */
 int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream);
 /* The same extraction split over two streams: work queued on kp_stream after
  * this call sees the keypoint rows (position, octave, size, response; not
  * the angle) and the counts; work queued on desc_stream sees the complete
- * rows and the descriptors.  The blur runs on desc_stream, beside FAST. */
+ * rows and the descriptors.  The blur runs on desc_stream, beside FAST.  A
+ * call orders itself after the previous call's descriptor pass (its last
+ * reader of the batch buffers), whatever streams the two calls use. */
 int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, void *desc_stream);
 /* Synchronise and report kernel-side errors (octree pool overflow). */
 int ygzfe_batch_check(ygzfe_batch *b);

@@ -108,7 +108,12 @@ int ygzo_fast10_nonmax(const int16_t *xs, const int16_t *ys, const int *scores, 
 }
 
 /* ShiTomasiScore (ORBextractor.cc:1152-1187): float accumulation in raster
- * order; the /(2.0*area) divisions and the final 0.5* are done in double. */
+ * order (exact: integer-valued sums < 2^24); the /(2.0*area) divisions are
+ * exact powers of two.  The discriminant (:1186) is evaluated as the
+ * reference's own build compiles it (g++ -std=c++11 -O3 -march=native,
+ * CMakeLists.txt:14; C++ keeps -ffp-contract=fast): two fused multiply-subs,
+ * disc = fma(s, s, -(4 * fma(dXX, dYY, -(dXY * dXY)))).
+ * tests/test_cpu_ref_arith.py pins this against that compiler and flags. */
 float ygzo_shi_tomasi(const uint8_t *img, int w, int h, int stride, int u, int v) {
     float dXX = 0.0f, dYY = 0.0f, dXY = 0.0f;
     const int half = 4, box = 8, area = 64;
@@ -128,7 +133,7 @@ float ygzo_shi_tomasi(const uint8_t *img, int w, int h, int stride, int u, int v
     dYY = (float)(dYY / (2.0 * area));
     dXY = (float)(dXY / (2.0 * area));
     float s = dXX + dYY;
-    float disc = s * s - 4 * (dXX * dYY - dXY * dXY);
+    float disc = fmaf(s, s, -(4.0f * fmaf(dXX, dYY, -(dXY * dXY))));
     return (float)(0.5 * (double)(dXX + dYY - sqrtf(disc)));
 }
 

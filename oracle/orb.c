@@ -4,6 +4,9 @@
  *
  * Build with -ffp-contract=off: every float expression below is evaluated as
  * written (no FMA contraction), which is the arithmetic the HIP kernels use.
+ * Where the reference's own build (g++ -std=c++11 -O3 -march=native,
+ * CMakeLists.txt:14) fuses a multiply-add, the restatement writes the fma
+ * explicitly (rBRIEF sample coordinates; tests/test_cpu_ref_arith.py pins it).
  */
 #include "ygz_oracle.h"
 
@@ -573,14 +576,164 @@ void ygzo_gaussian_blur7(const uint8_t *src, int w, int h, int stride, uint8_t *
     free(rows);
 }
 
-/* computeOrbDescriptor (ORBextractor.cc:105-149).  cos/sin are the correctly
- * rounded float values (computed in double); sample coordinates are clamped
- * to the image (out-of-bounds reads in the reference are UB). */
+/*
+ * glibc's single-precision sin/cos (glibc >= 2.28: sysdeps/ieee754/flt-32
+ * s_sinf.c / s_cosf.c / s_sincosf.c with sincosf.h and s_sincosf_data.c, the
+ * double-evaluated "ARM optimized-routines" algorithm), restated for the
+ * argument range rBRIEF uses: angle * pi/180 with angle = fastAtan2 in
+ * [0, 360), i.e. |y| < 120 (the large-argument reduction is not needed).
+ *   computeOrbDescriptor does `float angle; cos(angle), sin(angle)` under
+ *   `using namespace std` (ORBextractor.cc:68-69, 108-109): std::cos(float) =
+ *   cosf / sinf of the C library (g++ -O3 merges the pair into one sincosf
+ *   call; sincosf_poly and sinf_poly are the same arithmetic).
+ * Pinned to this image's glibc 2.35 (x86-64; the FMA and non-FMA ifunc
+ * variants agree on [0, 2pi)): tests/test_cpu_ref_arith.py compares every
+ * float in [0, 2pi) bit for bit with libm's cosf / sinf.
+ */
+typedef struct {
+    double sign[4];               /* sign of the sine per quadrant */
+    double hpi_inv, hpi;          /* 2/pi * 2^24 (no TOINT intrinsics on x86-64), pi/2 */
+    double c0, c1, c2, c3, c4;    /* cosine polynomial */
+    double s1, s2, s3;            /* sine polynomial */
+} glibc_sincos_t;
+
+static const glibc_sincos_t kSinCos[2] = {
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0,
+     0x1p0, -0x1.ffffffd0c621cp-2, 0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16,
+     -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13},
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0,
+     -0x1p0, 0x1.ffffffd0c621cp-2, -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16,
+     -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13},
+};
+
+static inline uint32_t abstop12(float x) {
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    return (u >> 20) & 0x7ff;
+}
+
+/* sinf_poly (sincosf.h): odd n -> the cosine polynomial, even n -> the sine one */
+static inline float glibc_sinf_poly(double x, double x2, const glibc_sincos_t *p, int n) {
+    if ((n & 1) == 0) {
+        double x3 = x * x2;
+        double s1 = p->s2 + x2 * p->s3;
+        double x7 = x3 * x2;
+        double s = x + x3 * p->s1;
+        return (float)(s + x7 * s1);
+    }
+    double x4 = x2 * x2;
+    double c2 = p->c3 + x2 * p->c4;
+    double c1 = p->c0 + x2 * p->c1;
+    double x6 = x4 * x2;
+    double c = c1 + x4 * p->c2;
+    return (float)(c + x6 * c2);
+}
+
+/* 4/pi bits, a sliding window of 24 words (s_sincosf_data.c __inv_pio4). */
+static const uint32_t kInvPio4[24] = {
+    0xa2,       0xa2f9,     0xa2f983,   0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529,
+    0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd, 0xf534ddc0,
+    0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43, 0x993c4390, 0x3c439041,
+};
+
+/* reduce_large (sincosf.h): |y| >= 120, integer multiply by 4/pi bits. */
+static inline double glibc_reduce_large(uint32_t xi, int *np) {
+    const uint32_t *arr = &kInvPio4[(xi >> 26) & 15];
+    int shift = (xi >> 23) & 7;
+    uint64_t n, res0, res1, res2;
+    xi = (xi & 0xffffff) | 0x800000;
+    xi <<= shift;
+    res0 = (uint64_t)(uint32_t)(xi * arr[0]);
+    res1 = (uint64_t)xi * arr[4];
+    res2 = (uint64_t)xi * arr[8];
+    res0 = (res2 >> 32) | (res0 << 32);
+    res0 += res1;
+    n = (res0 + (1ULL << 61)) >> 62;
+    res0 -= n << 62;
+    double x = (double)(int64_t)res0;
+    *np = (int)n;
+    return x * 0x1.921FB54442D18p-62; /* pi * 2^-63 */
+}
+
+void ygzo_sincosf(float y, float *sinp, float *cosp) {
+    const glibc_sincos_t *p = &kSinCos[0];
+    double x = y;
+    if (abstop12(y) >= abstop12(120.0f)) {
+        if (!(fabsf(y) <= FLT_MAX)) { /* inf / nan: __math_invalidf */
+            *sinp = *cosp = (y - y) / (y - y);
+            return;
+        }
+        uint32_t xi;
+        memcpy(&xi, &y, 4);
+        int sign = xi >> 31, n;
+        x = glibc_reduce_large(xi, &n);
+        double s = p->sign[(n + sign) & 3];
+        if ((n + sign) & 2) p = &kSinCos[1];
+        *sinp = glibc_sinf_poly(x * s, x * x, p, n);
+        *cosp = glibc_sinf_poly(x * s, x * x, p, n ^ 1);
+        return;
+    }
+    if (abstop12(y) < abstop12((float)0x1.921FB54442D18p-1)) { /* |y| < pi/4 (top-12-bit compare) */
+        if (abstop12(y) < abstop12(0x1p-12f)) {
+            *sinp = y;
+            *cosp = 1.0f;
+            return;
+        }
+        double x2 = x * x;
+        *sinp = glibc_sinf_poly(x, x2, p, 0);
+        *cosp = glibc_sinf_poly(x, x2, p, 1);
+        return;
+    }
+    /* reduce_fast: quadrant from the 2^24-prescaled product, truncating conversion */
+    double r = x * p->hpi_inv;
+    int n = ((int32_t)r + 0x800000) >> 24;
+    x = x - n * p->hpi;
+    double s = p->sign[n & 3];
+    if (n & 2) p = &kSinCos[1];
+    *sinp = glibc_sinf_poly(x * s, x * x, p, n);
+    *cosp = glibc_sinf_poly(x * s, x * x, p, n ^ 1);
+}
+
+/* Test hook: restated sincosf vs this process's libm sinf / cosf over the float
+ * bit patterns [lo, hi); returns the number of inputs where either differs. */
+int64_t ygzo_sincosf_sweep(uint32_t lo, uint32_t hi) {
+    int64_t bad = 0;
+    for (uint32_t u = lo; u < hi; u++) {
+        float y, s, c;
+        memcpy(&y, &u, 4);
+        ygzo_sincosf(y, &s, &c);
+        volatile float ls = sinf(y), lc = cosf(y);
+        float lsv = ls, lcv = lc;
+        bad += memcmp(&s, &lsv, 4) != 0 || memcmp(&c, &lcv, 4) != 0;
+    }
+    return bad;
+}
+
+/* Test hook: the 512 rotated sample offsets (row, column) GET_VALUE reads for
+ * a keypoint angle (ORBextractor.cc:108-116), as ygzo_orb_descriptor forms them. */
+void ygzo_orb_sample_offsets(float angle_deg, int *dy, int *dx) {
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    float a, b;
+    ygzo_sincosf(angle_deg * factorPI, &b, &a);
+    for (int j = 0; j < 512; j++) {
+        float px = (float)kPattern[2 * j], py = (float)kPattern[2 * j + 1];
+        dy[j] = cv_round_f(fmaf(px, b, py * a));
+        dx[j] = cv_round_f(fmaf(px, a, -(py * b)));
+    }
+}
+
+/* computeOrbDescriptor (ORBextractor.cc:105-149).  (a, b) = glibc cosf / sinf
+ * of the float angle (ygzo_sincosf above).  GET_VALUE (:114-116) as g++
+ * -O3 -march=native compiles it: the first product fused into the add / sub,
+ * y = fma(x, b, y*a), x = fma(x, a, -(y*b)); cvRound = round half even.
+ * Sample coordinates are clamped to the image (out-of-bounds reads in the
+ * reference are UB). */
 void ygzo_orb_descriptor(const uint8_t *img, int w, int h, int stride, const ygzo_kp *kp,
                          uint8_t desc[32]) {
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float angle = kp->angle * factorPI;
-    float a = (float)cos((double)angle), b = (float)sin((double)angle);
+    float a, b;
+    ygzo_sincosf(angle, &b, &a);
     int cx = cv_round_f(kp->x), cy = cv_round_f(kp->y);
     const int *pat = kPattern;
     for (int i = 0; i < 32; ++i) {
@@ -588,8 +741,8 @@ void ygzo_orb_descriptor(const uint8_t *img, int w, int h, int stride, const ygz
         for (int k = 0; k < 8; k++) {
             const int *p = pat + (i * 8 + k) * 4;
             float px0 = (float)p[0], py0 = (float)p[1], px1 = (float)p[2], py1 = (float)p[3];
-            int y0 = cy + cv_round_f(px0 * b + py0 * a), x0 = cx + cv_round_f(px0 * a - py0 * b);
-            int y1 = cy + cv_round_f(px1 * b + py1 * a), x1 = cx + cv_round_f(px1 * a - py1 * b);
+            int y0 = cy + cv_round_f(fmaf(px0, b, py0 * a)), x0 = cx + cv_round_f(fmaf(px0, a, -(py0 * b)));
+            int y1 = cy + cv_round_f(fmaf(px1, b, py1 * a)), x1 = cx + cv_round_f(fmaf(px1, a, -(py1 * b)));
             int t0 = img[(size_t)clampi(y0, 0, h - 1) * stride + clampi(x0, 0, w - 1)];
             int t1 = img[(size_t)clampi(y1, 0, h - 1) * stride + clampi(x1, 0, w - 1)];
             val |= (t0 < t1) << k;

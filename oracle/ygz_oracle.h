@@ -92,6 +92,12 @@ void ygzo_gaussian_blur7(const uint8_t *src, int w, int h, int stride, uint8_t *
 void ygzo_orb_descriptor(const uint8_t *img, int w, int h, int stride, const ygzo_kp *kp,
                          uint8_t desc[32]);
 const int *ygzo_bit_pattern(void);
+/* glibc 2.35 sinf / cosf restated (|y| < 120; ORBextractor.cc:109 std::cos(float)). */
+void ygzo_sincosf(float y, float *sinp, float *cosp);
+/* Test hook: #inputs in float bit range [lo, hi) where ygzo_sincosf != libm. */
+int64_t ygzo_sincosf_sweep(uint32_t lo, uint32_t hi);
+/* Test hook: the 512 rotated rBRIEF sample offsets for one angle (degrees). */
+void ygzo_orb_sample_offsets(float angle_deg, int *dy, int *dx);
 
 /* ORBextractor::operator()(Frame*, kps, desc, ORBSLAM_KEYPOINT, leftEye=true)
  * (ORBextractor.cc:1031-1127) on a prebuilt pyramid.  `existing` (n_existing)

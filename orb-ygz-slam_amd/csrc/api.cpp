@@ -184,6 +184,10 @@ struct ygzfe_batch {
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_oct_fork = nullptr, ev_oct_join[2] = {nullptr, nullptr};
+    // end of the last extraction's descriptor pass (the last reader of the pyramid,
+    // FAST / octree scratch): the next extraction and uploads wait on it
+    hipEvent_t ev_desc_done = nullptr;
+    bool desc_pending = false;
     std::unique_ptr<PlanDev> plan;
     DevBuf pyr;
     Workspace ws;
@@ -553,6 +557,7 @@ int ygzfe_batch_create(const ygzfe_orb_params *p, int device, int width, int hei
     }
     YGZ_HIP(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
     YGZ_HIP(hipEventCreateWithFlags(&b->ev_oct_fork, hipEventDisableTiming));
+    YGZ_HIP(hipEventCreateWithFlags(&b->ev_desc_done, hipEventDisableTiming));
     for (int i = 0; i < 2; i++) YGZ_HIP(hipEventCreateWithFlags(&b->ev_oct_join[i], hipEventDisableTiming));
     *out = b.release();
     return YGZFE_OK;
@@ -571,6 +576,7 @@ void ygzfe_batch_destroy(ygzfe_batch *b) {
     }
     if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
     if (b->ev_oct_fork) (void)hipEventDestroy(b->ev_oct_fork);
+    if (b->ev_desc_done) (void)hipEventSynchronize(b->ev_desc_done), (void)hipEventDestroy(b->ev_desc_done);
     for (int i = 0; i < 2; i++)
         if (b->ev_oct_join[i]) (void)hipEventDestroy(b->ev_oct_join[i]);
     delete b;
@@ -608,6 +614,8 @@ int ygzfe_batch_upload(ygzfe_batch *b, const uint8_t *frames, int n_frames) {
     if (!b || !frames || n_frames < 0 || n_frames > b->maxF) { set_error("invalid argument"); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(b->device));
     const Plan &P = b->plan->hp();
+    // the previous extraction (possibly on caller streams) may still read the slots
+    if (b->desc_pending) YGZ_HIP(hipStreamWaitEvent(b->stream, b->ev_desc_done, 0));
     // frame i -> level-0 slot of pyramid i (pitch P.pyr_bytes)
     YGZ_HIP(hipMemcpy2DAsync(b->pyr.p, P.pyr_bytes, frames, (size_t)P.W * P.H, (size_t)P.W * P.H, n_frames,
                              hipMemcpyHostToDevice, b->stream));
@@ -632,6 +640,12 @@ int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, voi
     const Plan &P = pd.hp();
     Workspace &ws = b->ws;
     uint8_t *pyr = b->pyr.as<uint8_t>();
+    // write-after-read across calls: the previous call's descriptor pass (on its
+    // desc_stream) still reads the pyramid, blur and octree selection this call rewrites
+    // (not while capturing a graph: a replay retires as a whole before the next)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    YGZ_HIP(hipStreamIsCapturing(st, &cap));
+    if (b->desc_pending && cap == hipStreamCaptureStatusNone) YGZ_HIP(hipStreamWaitEvent(st, b->ev_desc_done, 0));
     YGZ_HIP(hipMemsetAsync(ws.err.p, 0, 16, st));
     hipEvent_t t0 = b->begin(st);
     YGZ_HIP(launch_pyramid(pyr, P.pyr_bytes, P, pd.dp(), pd.tabs.as<int>(), n_frames, st));
@@ -669,6 +683,10 @@ int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, voi
                                ws.selcnt.as<int>(), nullptr, ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(),
                                ws.counts.as<int>(), P.kp_cap, n_frames, ds));
     b->end(ST_DESC, t0, ds);
+    if (cap == hipStreamCaptureStatusNone) {
+        YGZ_HIP(hipEventRecord(b->ev_desc_done, ds));
+        b->desc_pending = true;
+    }
     return YGZFE_OK;
 }
 

@@ -188,6 +188,82 @@ __device__ __forceinline__ float fast_atan2_deg(float y, float x) {
     return a;
 }
 
+// glibc's sinf / cosf for |y| < 120 (the rBRIEF angle, ORBextractor.cc:109
+// std::cos(float) -> the C library's cosf): the double-evaluated polynomial of
+// glibc >= 2.28 (sincosf.h), restated in oracle/orb.c ygzo_sincosf and pinned
+// there bit for bit against this image's libm over [0, 2pi).  v_fma_f64 is not
+// used: the file is built with -ffp-contract=off, as glibc's generic variant.
+__device__ __forceinline__ float glibc_sinf_poly(double x, double x2, bool cos_branch, bool neg_cos) {
+    if (!cos_branch) {
+        const double x3 = x * x2;
+        const double s1 = 0x1.1107605230bc4p-7 + x2 * -0x1.994eb3774cf24p-13;
+        const double x7 = x3 * x2;
+        const double s = x + x3 * -0x1.555545995a603p-3;
+        return (float)(s + x7 * s1);
+    }
+    const double g = neg_cos ? -1.0 : 1.0;  // the table[1] cosine coefficients are negated (exact)
+    const double x4 = x2 * x2;
+    const double c2 = g * -0x1.6c087e89a359dp-10 + x2 * (g * 0x1.99343027bf8c3p-16);
+    const double c1 = g * 0x1p0 + x2 * (g * -0x1.ffffffd0c621cp-2);
+    const double x6 = x4 * x2;
+    const double c = c1 + x4 * (g * 0x1.55553e1068f19p-5);
+    return (float)(c + x6 * c2);
+}
+
+static __constant__ const uint32_t c_inv_pio4[24] = {
+    0xa2,       0xa2f9,     0xa2f983,   0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529,
+    0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd, 0xf534ddc0,
+    0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43, 0x993c4390, 0x3c439041};
+
+__device__ __forceinline__ void glibc_sincosf(float y, float &sinv, float &cosv) {
+    const uint32_t top = (__float_as_uint(y) >> 20) & 0x7ffu;
+    double x = y;
+    if (top >= ((__float_as_uint(120.0f) >> 20) & 0x7ffu)) {  // never reached by octree angles
+        if (!(fabsf(y) <= 3.40282347e38f)) {
+            sinv = cosv = __builtin_nanf("");
+            return;
+        }
+        // reduce_large: integer product with the 4/pi bit window (s_sincosf_data.c __inv_pio4)
+        const uint32_t *kInvPio4 = c_inv_pio4;
+        uint32_t xi = __float_as_uint(y);
+        const int sign = (int)(xi >> 31);
+        const int a = (xi >> 26) & 15, shift = (xi >> 23) & 7;
+        xi = ((xi & 0xffffffu) | 0x800000u) << shift;
+        uint64_t res0 = (uint64_t)(uint32_t)(xi * kInvPio4[a]);
+        const uint64_t res1 = (uint64_t)xi * kInvPio4[a + 4];
+        const uint64_t res2 = (uint64_t)xi * kInvPio4[a + 8];
+        res0 = ((res2 >> 32) | (res0 << 32)) + res1;
+        const uint64_t nq = (res0 + (1ull << 61)) >> 62;
+        res0 -= nq << 62;
+        x = (double)(int64_t)res0 * 0x1.921FB54442D18p-62;
+        const int n = (int)nq, ns = n + sign;
+        const double s = ((ns + 1) & 2) ? -1.0 : 1.0;
+        const bool neg = (ns & 2) != 0;
+        sinv = glibc_sinf_poly(x * s, x * x, (n & 1) != 0, neg);
+        cosv = glibc_sinf_poly(x * s, x * x, (n & 1) == 0, neg);
+        return;
+    }
+    if (top < ((__float_as_uint((float)0x1.921FB54442D18p-1) >> 20) & 0x7ffu)) {
+        if (top < ((__float_as_uint(0x1p-12f) >> 20) & 0x7ffu)) {
+            sinv = y;
+            cosv = 1.0f;
+            return;
+        }
+        const double x2 = x * x;
+        sinv = glibc_sinf_poly(x, x2, false, false);
+        cosv = glibc_sinf_poly(x, x2, true, false);
+        return;
+    }
+    const double r = x * 0x1.45F306DC9C883p+23;  // reduce_fast: 2/pi * 2^24, truncating conversion
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    x = x - n * 0x1.921FB54442D18p0;
+    const double s = ((n + 1) & 2) ? -1.0 : 1.0;  // sign[n & 3] = {1, -1, -1, 1}
+    const bool neg = (n & 2) != 0;
+    const double xs = x * s, x2 = x * x;
+    sinv = glibc_sinf_poly(xs, x2, (n & 1) != 0, neg);
+    cosv = glibc_sinf_poly(xs, x2, (n & 1) == 0, neg);
+}
+
 }  // namespace ygzfe
 
 // --------------------------------------------------------------------------

@@ -52,7 +52,9 @@ __device__ __forceinline__ float shi_tomasi(const uint8_t *p, int S) {
     dYY = (float)(dYY / (2.0 * 64));
     dXY = (float)(dXY / (2.0 * 64));
     const float s = dXX + dYY;
-    const float disc = s * s - 4 * (dXX * dYY - dXY * dXY);
+    // ORBextractor.cc:1186 as the reference's -O3 -march=native C++ build contracts it
+    // (oracle/fast10.c ygzo_shi_tomasi): two fused multiply-subtracts
+    const float disc = __builtin_fmaf(s, s, -(4.0f * __builtin_fmaf(dXX, dYY, -(dXY * dXY))));
     return (float)(0.5 * (double)(dXX + dYY - sqrtf(disc)));
 }
 

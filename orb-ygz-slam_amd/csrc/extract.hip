@@ -1164,15 +1164,16 @@ __device__ __forceinline__ void orb_desc_wave(const uint8_t *img, int w, int h, 
     const int lane = threadIdx.x & 63;
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float ang = angle_deg * factorPI;
-    const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+    float a, b;
+    glibc_sincosf(ang, b, a);
     uint32_t nib = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int pi = (lane * 4 + k) * 4;
         const float px0 = (float)c_pattern[pi], py0 = (float)c_pattern[pi + 1];
         const float px1 = (float)c_pattern[pi + 2], py1 = (float)c_pattern[pi + 3];
-        const int y0 = cy + cv_round(px0 * b + py0 * a), x0 = cx + cv_round(px0 * a - py0 * b);
-        const int y1 = cy + cv_round(px1 * b + py1 * a), x1 = cx + cv_round(px1 * a - py1 * b);
+        const int y0 = cy + cv_round(__builtin_fmaf(px0, b, py0 * a)), x0 = cx + cv_round(__builtin_fmaf(px0, a, -(py0 * b)));
+        const int y1 = cy + cv_round(__builtin_fmaf(px1, b, py1 * a)), x1 = cx + cv_round(__builtin_fmaf(px1, a, -(py1 * b)));
         const int t0 = img[(size_t)clampi(y0, 0, h - 1) * w + clampi(x0, 0, w - 1)];
         const int t1 = img[(size_t)clampi(y1, 0, h - 1) * w + clampi(x1, 0, w - 1)];
         nib |= (uint32_t)(t0 < t1) << k;
@@ -1374,7 +1375,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     const uint32_t o0 = (uint32_t)(uintptr_t)bimg + __umul24((uint32_t)(cy - 18), (uint32_t)w) + (uint32_t)(cx - 18);
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float ang = angle * factorPI;
-    const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
+    float ca, sb;
+    glibc_sincosf(ang, sb, ca);  // the reference's std::cos(float) / std::sin(float) = glibc cosf / sinf
     YGZ_BSTAMP_K(1, 6);
     const uint32_t w16 = (uint32_t)w & 15u;  // only the row start's offset mod 16 matters
     auto tap = [&](int dy, int dx) {  // blurred pixel (cy + dy, cx + dx)
@@ -1390,8 +1392,10 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
         for (int k = 0; k < 4; k++) {
             const float px0 = (float)(int8_t)(wd[k] & 0xFF), py0 = (float)(int8_t)((wd[k] >> 8) & 0xFF);
             const float px1 = (float)(int8_t)((wd[k] >> 16) & 0xFF), py1 = (float)(int8_t)(wd[k] >> 24);
-            const int t0 = tap(cv_round(px0 * sb + py0 * ca), cv_round(px0 * ca - py0 * sb));
-            const int t1 = tap(cv_round(px1 * sb + py1 * ca), cv_round(px1 * ca - py1 * sb));
+            // GET_VALUE (ORBextractor.cc:114-116) as the reference's -O3 -march=native build
+            // fuses it (oracle/orb.c ygzo_orb_descriptor)
+            const int t0 = tap(cv_round(__builtin_fmaf(px0, sb, py0 * ca)), cv_round(__builtin_fmaf(px0, ca, -(py0 * sb))));
+            const int t1 = tap(cv_round(__builtin_fmaf(px1, sb, py1 * ca)), cv_round(__builtin_fmaf(px1, ca, -(py1 * sb))));
             bits |= (uint32_t)(t0 < t1) << (q * 4 + k);
         }
     }
