@@ -2,27 +2,41 @@
 """bench.py — frames/s of the ORB-YGZ-SLAM front-end hot path on MI355X.
 
 Metric (BASELINE.json): frames/sec ORB-extract + SparseImageAlign, 752x480,
-1000 features.  One "step" = one pass of the hot path over one resident batch
-of B synthetic frames (a rendered textured-plane sequence, EuRoC intrinsics):
-  * ORB extraction of all B frames (C2: nFeatures 1000, scale 2.0, 4 levels,
-    FAST 20/7) — pyramid, blur, FAST-9 cells, octree, angle + rBRIEF;
-  * Hamming best/second-best of frame k against frame k-1 (B-1 pairs);
-  * SparseImgAlign of k-1 -> k (B-1 pairs, levels 3..1, 10 GN iterations)
-    with map points = frame k-1's keypoints back-projected on the plane.
-Frames are in HBM before the timed region.  `value` = frames extracted by all
-ranks / wall time (B per rank per step).  N>1: one process per GPU, each with
-its own contiguous slice of the sequence (weak scaling, no data-path
-collective; the batch gather is offline).
+1000 features, 1/2/4/8 GPUs.  Default workload = BASELINE config C5, the
+offline batched-sequence mode: the 13,728 frames of EuRoC MH01..MH05
+(Examples/Monocular/EuRoC_TimeStamps/MH0*.txt: 3682+3040+2700+2033+2273) as a
+synthetic sequence (a rendered textured plane under a back-and-forth camera
+sweep, EuRoC intrinsics; no dataset in the image), sharded contiguously over
+the ranks (one process per GPU).  One "step" = the whole job over the
+sequence, per rank on its shard plus a one-frame halo:
+  * ORB extraction (C2: nFeatures 1000, scale 2.0, 4 levels, FAST 20/7) --
+    pyramid, blur, FAST-9 cells, octree, angle + rBRIEF;
+  * Hamming best/second-best of frame k against frame k-1;
+  * SparseImgAlign k-1 -> k (C3: levels 3..1, 10 GN iterations), map points =
+    frame k-1's keypoints back-projected on the plane;
+  * the per-frame result slots (keypoints, descriptors, TCR) packed on the
+    device and gathered to rank 0 over RCCL (`torch.distributed.gather`).
+Frames are rendered on the device into HBM before the timed region.  `value` =
+13,728 / the slowest rank's step time ("scaling": "strong": the job is fixed).
+`--workload c2batch` is round 1's form instead: `--batch` frames per GPU
+(weak scaling), same stages.
+
+`--gpus N` without torchrun spawns the N ranks itself (torch.distributed.run,
+127.0.0.1) before anything touches a GPU; under torchrun WORLD_SIZE must equal
+--gpus, and fewer visible GPUs than --gpus is an error, never a silent N=1 run.
 
 The JSON line also carries `roofline` (dominant kernel: algorithmic bytes per
-launch / HIP-event-timed average launch duration vs 8 TB/s) and
-`cpu_baseline` (the oracle/ CPU restatement, single thread, on a bounded
+launch / HIP-event-timed average launch duration vs 8 TB/s, plus the VALU
+issue fraction from the committed PMC pass) and `cpu_baseline` (the oracle/
+CPU restatement on the host cores, 1 thread and all threads, on a bounded
 sample of the same workload).
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,6 +48,8 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SWEEP = 240  # frames per sweep of the synthetic trajectory
+C5_FRAMES = 3682 + 3040 + 2700 + 2033 + 2273  # EuRoC MH01..MH05 (Examples/Monocular/EuRoC_TimeStamps)
+XI = np.array([0.012, -0.006, 0.009, 0.0025, -0.002, 0.0015], np.float32)  # per-frame motion (v, w)
 
 
 def sweep_index(g):
@@ -47,8 +63,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024,
-                    help="frames resident per GPU (one chunk of a batched sequence; EuRoC MH sequences are 2033-3682 frames)")
+    ap.add_argument("--workload", choices=["c5", "c2batch"], default="c5",
+                    help="c5: the 13,728-frame MH01..05 sequence sharded over the ranks + RCCL gather (strong); "
+                         "c2batch: --batch frames per GPU (weak)")
+    ap.add_argument("--frames", type=int, default=0, help="c5 sequence length override (0 = 13,728)")
+    ap.add_argument("--batch", type=int, default=1024, help="c2batch: frames per GPU")
     ap.add_argument("--cpu-sample", type=int, default=120, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-align", action="store_true")
@@ -63,13 +82,46 @@ def parse():
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2-transform side measurement")
     ap.add_argument("--no-stereo", action="store_true", help="skip the stereo-matching side measurement")
     ap.add_argument("--no-direct", action="store_true", help="skip the SearchLocalPointsDirect side measurement")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 (TUM 640x480, 2000 features) throughput line")
     ap.add_argument("--latency-frames", type=int, default=200,
                     help="single-frame latency leg: frames timed one at a time through the host C ABI (0 = skip)")
     return ap.parse_args()
 
 
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def self_launch(args):
+    """`--gpus N` run directly: start N ranks with torch.distributed.run as a child
+    (no GPU has been touched in this process: torch.cuda.device_count() does not
+    initialise HIP on this image) and exit with its status."""
+    import torch
+    n_vis = torch.cuda.device_count()
+    if n_vis < args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, {n_vis} visible; refusing to "
+                 f"report a smaller run")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return self_launch(args)
+    world = int(world_env or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
 
@@ -77,32 +129,33 @@ def main():
     from ygzfe import dist as D
     import _scenes as S
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if torch.cuda.device_count() < max(args.gpus, local + 1):
+        sys.exit(f"bench.py: rank {rank} needs GPU {local}; {torch.cuda.device_count()} visible")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != args.gpus:
+            sys.exit(f"bench.py: RCCL sees {dist.get_world_size()} ranks, --gpus {args.gpus}")
+        one = torch.ones(1, device=dev)
+        dist.all_reduce(one)
+        if int(one.item()) != args.gpus:
+            sys.exit(f"bench.py: all_reduce over RCCL counted {int(one.item())} ranks, expected {args.gpus}")
 
     W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
-    B = args.batch
+    n_seq = (args.frames or C5_FRAMES) if args.workload == "c5" else world * args.batch
+    b0, e0 = D.shard(n_seq, rank, world)       # this rank's frames (global indices)
+    hb, he = D.with_halo(b0, e0)               # + the halo frame whose pair (b0-1, b0) this rank aligns
+    h = b0 - hb
+    F = he - hb                                # frames extracted locally
+    n_own = e0 - b0
+    P = F - 1                                  # align / match pairs (ref p -> cur p+1)
+    maxlen = -(-n_seq // world)
     cam = ygzfe.EUROC_CAM
     sc = S.PlaneScene(11, W, H)
-    # trajectory: per-frame motion (v, w); frame g has pose exp(g * xi)
-    xi = np.array([0.012, -0.006, 0.009, 0.0025, -0.002, 0.0015], np.float32)
-    g0, _ = D.shard(world * B, rank, world)  # this rank's contiguous slice (weak scaling: B per rank)
-    # the camera sweeps back and forth over the plane (triangle wave of period
-    # 2*SWEEP frames) so every frame of every rank's slice sees the full
-    # textured view: ~1000 keypoints per frame like an EuRoC frame, whatever B
-    # and the rank; without it a long slice drifts off the plane.
-    poses = [ygzfe.trajectory_pose(sweep_index(g0 + i), xi) for i in range(B)]
-    t_r = time.time()
-    frames = np.stack([sc.render(q, t, noise_seed=g0 + i) for i, (q, t) in enumerate(poses)])
-    render_s = time.time() - t_r
+    poses = [ygzfe.trajectory_pose(sweep_index(g), XI) for g in range(hb, he)]
 
-    batch = ygzfe.Batch((nf, sf, nl, ini, mn, 0), local, W, H, B)
+    batch = ygzfe.Batch((nf, sf, nl, ini, mn, 0), local, W, H, max(F, 2))
     cap = batch.kp_cap
     # a real stream shared by torch and ygzfe: torch's default stream is the
     # legacy null stream (handle 0), which ygzfe reads as "the handle's own
@@ -110,73 +163,97 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
-    kps_t = torch.empty((B, cap, 7), dtype=torch.float32, device=dev)
-    counts_t = torch.zeros(B, dtype=torch.int32, device=dev)
-    batch.bind(kps=kps_t.data_ptr(), counts=counts_t.data_ptr())
-    torch.cuda.synchronize(dev)
-    t_u = time.time()
-    batch.upload(frames)
-    h2d_s = time.time() - t_u
+    kps_t = torch.empty((max(F, 2), cap, 7), dtype=torch.float32, device=dev)
+    counts_t = torch.zeros(max(F, 2), dtype=torch.int32, device=dev)
+    pyr_t = torch.zeros(max(F, 2) * batch.frame_pitch, dtype=torch.uint8, device=dev)
+    batch.bind(pyramids=pyr_t.data_ptr(), kps=kps_t.data_ptr(), counts=counts_t.data_ptr())
 
-    P = B - 1
-    ref_idx = torch.arange(0, P, dtype=torch.int32, device=dev)
-    cur_idx = torch.arange(1, B, dtype=torch.int32, device=dev)
-    bi = torch.empty((P, cap), dtype=torch.int32, device=dev)
+    # the sequence rendered on the device straight into the level-0 slots
+    t_r = time.time()
+    tex_d = torch.from_numpy(sc.tex).to(dev)
+    q_d = torch.from_numpy(np.stack([q for q, _ in poses])).to(dev)
+    t_d = torch.from_numpy(np.stack([t for _, t in poses])).to(dev)
+    seeds_d = torch.arange(hb, he, dtype=torch.int64, device=dev)
+    ygzfe.render_plane_device(tex_d.data_ptr(), S.TEX_W, S.TEX_H, S.TEXEL, S.PLANE_Z, cam, q_d.data_ptr(),
+                              t_d.data_ptr(), seeds_d.data_ptr(), F, W, H, pyr_t.data_ptr(), batch.frame_pitch,
+                              noise_amp=2, stream=sptr)
+    torch.cuda.synchronize(dev)
+    render_s = time.time() - t_r
+    del tex_d
+
+    ref_idx = torch.arange(0, max(P, 1), dtype=torch.int32, device=dev)
+    cur_idx = ref_idx + 1
+    bi = torch.empty((max(P, 1), cap), dtype=torch.int32, device=dev)
     bd = torch.empty_like(bi)
     sd = torch.empty_like(bi)
-    xyz = torch.empty((P, cap, 3), dtype=torch.float32, device=dev)
-    usable = torch.ones((P, cap), dtype=torch.uint8, device=dev)
-    T_init = torch.zeros((P, 7), dtype=torch.float32, device=dev)
+    xyz = torch.empty((max(P, 1), cap, 3), dtype=torch.float32, device=dev)
+    usable = torch.ones((max(P, 1), cap), dtype=torch.uint8, device=dev)
+    T_init = torch.zeros((max(P, 1), 7), dtype=torch.float32, device=dev)
     T_init[:, 3] = 1.0
-    out = torch.zeros((P, 45), dtype=torch.float32, device=dev)
+    out = torch.zeros((max(P, 1), 45), dtype=torch.float32, device=dev)
     # plane Z_w = 3 in each reference camera: X_c = lam * d_c, lam = (Z - C_z) / (r3 . d_c)
-    r3 = np.zeros((B, 3), np.float32)
-    cz = np.zeros(B, np.float32)
+    r3 = np.zeros((F, 3), np.float32)
+    cz = np.zeros(F, np.float32)
     for i, (q, t) in enumerate(poses):
         qi, ti = S.se3_inv(q.astype(np.float64), t.astype(np.float64))
         R_wc = np.array([S.quat_rot(qi, e) for e in np.eye(3)]).T
         r3[i] = R_wc[2]
         cz[i] = ti[2]
-    r3_t = torch.from_numpy(r3[:P]).to(dev)
-    cz_t = torch.from_numpy(cz[:P]).to(dev)
-    fx, fy, cx, cy = cam
+    r3_t = torch.from_numpy(r3).to(dev)
+    cz_t = torch.from_numpy(cz).to(dev)
     camera = ygzfe.Camera(*cam)
+    # result slots: this rank's own frames, padded to the longest shard for the gather
+    S_b = ygzfe.slot_bytes(cap)
+    slots = torch.zeros((maxlen, S_b), dtype=torch.uint8, device=dev)
+    gathered = [torch.empty_like(slots) for _ in range(world)] if (rank == 0 and world > 1) else None
+    gather_ms = []
 
     side = torch.cuda.Stream(dev)  # Hamming (descriptors only) runs beside SparseImgAlign (pyramids + kps)
 
-    def step_serial():
-        batch.extract(B, sptr)
-        batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(), sptr)
-        if args.no_align:
-            return
-        ygzfe.plane_points_device(kps_t.data_ptr(), cap, P, cam, r3_t.data_ptr(), cz_t.data_ptr(), S.PLANE_Z,
-                                  xyz.data_ptr(), sptr)
-        batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(), camera, 3, 1,
-                           T_init.data_ptr(), out.data_ptr(), sptr)
+    def pack_and_gather(timed_gather=False):
+        batch.pack_slots(h, n_own, out.data_ptr() if P > 0 else 0, b0, slots.data_ptr(), S_b, sptr)
+        if world > 1:
+            if timed_gather:
+                e0_, e1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0_.record(stream)
+            dist.gather(slots, gathered, dst=0)
+            if timed_gather:
+                e1_.record(stream)
+                gather_ms.append((e0_, e1_))
 
-    def step():
-        if args.schedule == "serial":
-            return step_serial()
+    def step_serial(timed_gather=False):
+        batch.extract(F, sptr)
+        if P > 0:
+            batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(),
+                        sptr)
+            if not args.no_align:
+                ygzfe.plane_points_device(kps_t.data_ptr(), cap, P, cam, r3_t.data_ptr(), cz_t.data_ptr(),
+                                          S.PLANE_Z, xyz.data_ptr(), sptr)
+                batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(),
+                                   camera, 3, 1, T_init.data_ptr(), out.data_ptr(), sptr)
+        pack_and_gather(timed_gather)
+
+    def step(timed_gather=False):
+        if args.schedule == "serial" or P == 0:
+            return step_serial(timed_gather)
         # keypoint rows on `stream`, blur + descriptors on `side` (the blur runs
         # beside FAST); Hamming (descriptors only) follows on `side`
         side.wait_stream(stream)
-        batch.extract_split(B, sptr, side.cuda_stream)
+        batch.extract_split(F, sptr, side.cuda_stream)
         batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(),
                     side.cuda_stream)
-        if args.no_align:
-            stream.wait_stream(side)
-            return
-        # synthetic map points (the stand-in for Tracking's T_ref * P_w snapshot)
-        ygzfe.plane_points_device(kps_t.data_ptr(), cap, P, cam, r3_t.data_ptr(), cz_t.data_ptr(), S.PLANE_Z,
-                                  xyz.data_ptr(), sptr)
-        if args.schedule == "split":
-            # a SparseImgAlign workgroup takes a whole CU (1024 threads x 128 VGPRs,
-            # 148 KB LDS): beside orient/Hamming it waits for free CUs and the
-            # overlap costs more than it hides, so it runs after them
-            stream.wait_stream(side)
-        batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(), camera, 3, 1,
-                           T_init.data_ptr(), out.data_ptr(), sptr)
-        stream.wait_stream(side)  # the step ends when both branches have
+        if not args.no_align:
+            ygzfe.plane_points_device(kps_t.data_ptr(), cap, P, cam, r3_t.data_ptr(), cz_t.data_ptr(), S.PLANE_Z,
+                                      xyz.data_ptr(), sptr)
+            if args.schedule == "split":
+                # a SparseImgAlign workgroup takes a whole CU (1024 threads x 128 VGPRs,
+                # 148 KB LDS): beside orient/Hamming it waits for free CUs and the
+                # overlap costs more than it hides, so it runs after them
+                stream.wait_stream(side)
+            batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(), camera,
+                               3, 1, T_init.data_ptr(), out.data_ptr(), sptr)
+        stream.wait_stream(side)  # the slots need the descriptors
+        pack_and_gather(timed_gather)
 
     for _ in range(args.warmup):
         step()
@@ -187,7 +264,7 @@ def main():
     batch.timing(False)  # `value`: no per-stage events inside the timed region
     run = step
     graph_ok = False
-    if args.graph:
+    if args.graph and world == 1:
         # one step captured as a HIP graph (every launch of the library, its
         # fork/join events and the side streams), replayed per step
         try:
@@ -205,12 +282,14 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     batch.check()
     elapsed = D.max_over_ranks(elapsed, dev)
@@ -222,55 +301,84 @@ def main():
         batch.timing(True)
         torch.cuda.synchronize(dev)
         for _ in range(args.steps):
-            step()
+            step(timed_gather=True)
         torch.cuda.synchronize(dev)
         stage_ms = batch.timing(False)
         batch.check()
+        if gather_ms:
+            stage_ms["rccl_gather"] = float(np.mean([a.elapsed_time(b) for a, b in gather_ms]))
+        if world > 1:
+            dist.barrier()
 
     ms_per_step = elapsed * 1000.0 / args.steps
-    fps = world * B / (elapsed / args.steps)
+    fps = n_seq / (elapsed / args.steps)
+
+    # ------------------------------------------------ results check: rank 0 holds every frame's slot
+    seq_check = None
+    if rank == 0:
+        full = torch.cat([gg[:D.shard(n_seq, r, world)[1] - D.shard(n_seq, r, world)[0]]
+                          for r, gg in enumerate(gathered)]) if world > 1 else slots[:n_own]
+        hdr = full[:, :64].contiguous().view(torch.int32).cpu().numpy()
+        seq_check = {"frames_at_root": int(full.shape[0]),
+                     "frame_index_ok": bool(np.array_equal(hdr[:, 10], np.arange(n_seq))),
+                     "frames_with_align": int(hdr[:, 11].sum()),
+                     "mean_kps_at_root": round(float(hdr[:, 0].mean()), 1),
+                     "slot_bytes": S_b}
 
     # ------------------------------------------------ roofline (dominant stage)
-    counts = counts_t.cpu().numpy()
-    nvis = out[:, 7].contiguous().view(torch.int32).cpu().numpy()
+    counts = counts_t[:F].cpu().numpy()
+    nvis = out[:max(P, 1), 7].contiguous().view(torch.int32).cpu().numpy() if P > 0 else np.zeros(1, np.int32)
     plan = ygzfe.orb_plan(nf, sf, nl, ini, mn, W, H)
-    areas = [w * h for w, h in plan["sizes"]]
-    cand, selk = batch.stats(B)  # per-level totals over the B frames of the last extract
+    areas = [w * hh for w, hh in plan["sizes"]]
+    cand, selk = batch.stats(F)  # per-level totals over the F frames of the last extract
     N = float(counts.mean())
     nv = float(nvis.mean())
     ncells_tot = int(sum(plan["ncells"]))
-    # algorithmic bytes per launch (per step, B frames): each intermediate crosses
+    # algorithmic bytes per launch (per step, F frames): each intermediate crosses
     # HBM once written and once read
     alg = {
-        "pyramid": B * sum(areas[l - 1] + areas[l] for l in range(1, nl)),
-        "blur7": B * 2 * sum(areas),
-        "fast9_cells": B * sum(a for a, c in zip(areas, plan["ncells"]) if c > 0) + 4 * int(cand.sum())
-        + 4 * B * ncells_tot,
-        "octree": 4 * int(cand.sum()) + 4 * B * ncells_tot + 4 * int(selk.sum()),
+        "pyramid": F * sum(areas[l - 1] + areas[l] for l in range(1, nl)),
+        "blur7": F * 2 * sum(areas),
+        "fast9_cells": F * sum(a for a, c in zip(areas, plan["ncells"]) if c > 0) + 4 * int(cand.sum())
+        + 4 * F * ncells_tot,
+        "octree": 4 * int(cand.sum()) + 4 * F * ncells_tot + 4 * int(selk.sum()),
         "orient_rbrief": int(counts.sum()) * (961 + 512 + 4 + 60),
         "hamming_best2": int(sum(32 * (counts[i + 1] + counts[i]) + 12 * counts[i + 1] for i in range(P))),
         "sparse_align": int(P * (3 * nv * (36 + 10 * 25) + 12 * nv + 96)),
+        "pack_slots": int(n_own * (2 * S_b)),
     }
-    if not any(v > 0 for v in stage_ms.values()):  # --no-stage-timing
+    if not any(v > 0 for k, v in stage_ms.items() if k in alg):  # --no-stage-timing
         stage_ms = {k: 1e-9 for k in alg}
-    dom = max((k for k in stage_ms if stage_ms[k] > 0), key=lambda k: stage_ms[k])
+    dom = max((k for k in stage_ms if k in alg and stage_ms[k] > 0), key=lambda k: stage_ms[k])
     dom_ms = stage_ms[dom]
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r01_traffic.json")
-    if os.path.exists(tpath):  # PMC FETCH_SIZE x2 + WRITE_SIZE of the same command (tools/run_pmc.sh)
-        tj = json.load(open(tpath)).get("per_step", {})
-        if dom in tj:
-            traffic = tj[dom]["traffic_bytes"]
+    traffic = valu_frac = None
+    tpath = os.path.join(ROOT, "profiles", "r02_traffic.json")
+    if not os.path.exists(tpath):
+        tpath = os.path.join(ROOT, "profiles", "r01_traffic.json")
+    if os.path.exists(tpath):  # PMC FETCH_SIZE x2 + WRITE_SIZE of the same kernel (tools/run_pmc.sh)
+        tj = json.load(open(tpath))
+        per = tj.get("per_frame", {}).get(dom)
+        if per is not None:  # scaled to this launch's frame count
+            traffic = int(per["traffic_bytes"] * F)
+            valu_frac = per.get("valu_frac")
+        elif dom in tj.get("per_step", {}):
+            traffic = tj["per_step"][dom]["traffic_bytes"]
     roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic, "avg_launch_ms": round(dom_ms, 4),
-            "alg_bytes_per_launch": int(alg[dom]),
+            "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic, "valu_frac": valu_frac,
+            "avg_launch_ms": round(dom_ms, 4), "alg_bytes_per_launch": int(alg[dom]), "frames_per_launch": F,
             "stages_ms": {k: round(v, 4) for k, v in stage_ms.items()},
             "stages_gbps": {k: round(alg[k] / (stage_ms[k] * 1e-3) / 1e9, 1) for k in alg if stage_ms.get(k, 0) > 0}}
     # whole pipeline, SURVEY §8d model: (B_extract + B_align) per frame x fps
     b_extract = areas[0] + 2 * sum(areas[1:]) + 2 * sum(areas) + 60 * N
     b_align = 3 * nv * (36 + 10 * 25) + 12 * nv + 96
     pipeline_gbps = (b_extract + b_align) * (fps / world) / 1e9
+
+    # host copies of a bounded prefix of the rendered sequence for the single-frame legs
+    n_host = 0
+    if rank == 0 and world == 1:
+        n_host = min(F, max(args.cpu_sample, args.latency_frames + 12, 16))
+    frames = np.stack([batch.read_level(i, 0) for i in range(n_host)]) if n_host else None
 
     # ------------------------------------------------ §8(f) rank 1: undistort remap
     # (not part of the headline metric; Frame.cc:775-790 runs it ahead of the
@@ -280,22 +388,32 @@ def main():
         import _cameras as CAM
         ucam, udist, _ = CAM.EUROC
         und = ygzfe.Undistort(ucam, udist, W, H, device=local)
-        raw = torch.from_numpy(frames).to(dev)
+        Bu = min(F, 1024)
+        raw = pyr_t.view(-1, batch.frame_pitch)[:Bu, :W * H].contiguous()  # level 0 of the first Bu frames
         for _ in range(2):
-            batch.undistort_device(und, raw.data_ptr(), W * H, B, sptr)
+            batch.undistort_device(und, raw.data_ptr(), W * H, Bu, sptr)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = max(args.steps, 5)
         ev0.record(stream)
         for _ in range(reps):
-            batch.undistort_device(und, raw.data_ptr(), W * H, B, sptr)
+            batch.undistort_device(und, raw.data_ptr(), W * H, Bu, sptr)
         ev1.record(stream)
         torch.cuda.synchronize(dev)
         ums = ev0.elapsed_time(ev1) / reps
-        ualg = B * W * H * 2  # each frame read once and written once (map: cache-resident, shared)
+        ualg = Bu * W * H * 2  # each frame read once and written once (map: cache-resident, shared)
         ugbps = ualg / (ums * 1e-3) / 1e9
-        und_line = {"kernel": "remap_tiles", "frames_per_s": round(B / (ums * 1e-3), 1),
+        und_line = {"kernel": "remap_tiles", "frames": Bu, "frames_per_s": round(Bu / (ums * 1e-3), 1),
                     "ms_per_launch": round(ums, 4), "alg_bytes_per_launch": ualg, "achieved_gbps": round(ugbps, 1),
                     "frac": round(ugbps / HBM_PEAK_GBPS, 4), "camera": "EuRoC (Examples/Monocular/EuRoC.yaml)"}
+        if frames is not None and args.cpu_sample > 0:
+            import _oracle as O
+            m1, m2 = O.undistort_map(ucam, udist, W, H)
+            t_c = time.perf_counter()
+            nrm = 0
+            while nrm < 8 or time.perf_counter() - t_c < 0.5:
+                O.remap_linear(frames[nrm % len(frames)], m1, m2)
+                nrm += 1
+            und_line["cpu_port_frames_per_s"] = round(nrm / (time.perf_counter() - t_c), 1)
 
     # ------------------------------------------------ §8(f) rank 2: SearchLocalPointsDirect
     direct_line = None
@@ -310,7 +428,12 @@ def main():
     # ------------------------------------------------ §8(f) rank 4: DBoW2 transform (Frame::ComputeBoW)
     bow_line = None
     if rank == 0 and world == 1 and not args.no_bow:
-        bow_line = bow_leg(S, batch, B, dev, stream, args.cpu_sample > 0)
+        bow_line = bow_leg(S, batch, min(F, 1024), dev, stream, args.cpu_sample > 0)
+
+    # ------------------------------------------------ C4 throughput (TUM1.yaml, batched 256 frames)
+    c4_line = None
+    if rank == 0 and world == 1 and not args.no_c4:
+        c4_line = c4_leg(S, dev, args)
 
     # ------------------------------------------------ single-frame latency (rank 0, N = 1)
     lat = None
@@ -321,23 +444,17 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu = cpu_baseline(frames, poses, S, args, sc)
-        if und_line is not None:
-            import _cameras as CAM
-            import _oracle as O
-            ucam, udist, _ = CAM.EUROC
-            m1, m2 = O.undistort_map(ucam, udist, W, H)
-            t_c = time.perf_counter()
-            nrm = 0
-            while nrm < 8 or time.perf_counter() - t_c < 0.5:
-                O.remap_linear(frames[nrm % B], m1, m2)
-                nrm += 1
-            und_line["cpu_port_frames_per_s"] = round(nrm / (time.perf_counter() - t_c), 1)
 
     if lat is not None and cpu is not None:
         cpu_lat = cpu["ms_extract"] + cpu["ms_align"]
         lat["cpu_port_ms"] = round(cpu_lat, 3)
         lat["speedup_vs_cpu_port"] = round(cpu_lat / lat["median_ms"], 2)
     if rank == 0:
+        wl = (f"C5 offline sequence: {n_seq} frames (EuRoC MH01..05 length) sharded over {world} GPU(s), per frame "
+              f"C2 extract + dense Hamming (k vs k-1) + C3 SparseImgAlign levels 3..1, device-packed result slots "
+              f"gathered to rank 0 over RCCL") if args.workload == "c5" else \
+             (f"C2 batch: {args.batch} frames per GPU, extract + dense Hamming (k vs k-1) + C3 SparseImgAlign "
+              f"levels 3..1 + result slots")
         line = {
             "metric": "frames/sec ORB-extract+SparseImageAlign, 752x480, 1000 feat",
             "value": round(fps, 2),
@@ -347,25 +464,28 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.workload == "c5" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (seeded textured-plane renders, EuRoC intrinsics; no dataset)",
-            "config": {"workload": "C2 extract + dense Hamming (k vs k-1) + C3 SparseImgAlign levels 3..1",
-                       "frames_per_gpu": B, "image": f"{W}x{H}", "nfeatures": nf, "scale_factor": sf,
+            "data": "synthetic (seeded textured-plane renders on the device, EuRoC intrinsics; no dataset)",
+            "config": {"workload": wl, "sequence_frames": n_seq, "frames_per_gpu": n_own,
+                       "frames_extracted_per_gpu": F, "image": f"{W}x{H}", "nfeatures": nf, "scale_factor": sf,
                        "nlevels": nl, "fast_th": [ini, mn], "align_pairs_per_gpu": P,
                        "mean_keypoints": round(N, 1), "mean_align_visible": round(nv, 1),
-                       "mean_fast_candidates": round(float(cand.sum()) / B, 1),
-                       "mean_fast_candidates_per_level": [round(float(c) / B, 1) for c in cand],
-                       "mean_keypoints_per_level": [round(float(c) / B, 1) for c in selk],
-                       "parallelism": f"frame-sharded x{world}", "schedule": args.schedule,
-                       "hip_graph": graph_ok},
+                       "mean_fast_candidates": round(float(cand.sum()) / F, 1),
+                       "mean_fast_candidates_per_level": [round(float(c) / F, 1) for c in cand],
+                       "mean_keypoints_per_level": [round(float(c) / F, 1) for c in selk],
+                       "parallelism": f"frame-sharded x{world} (contiguous shards + 1-frame halo)",
+                       "collective": "RCCL gather of result slots to rank 0 (torch.distributed.gather)"
+                       if world > 1 else "none (N=1: rank 0 is the root)",
+                       "schedule": args.schedule, "hip_graph": graph_ok},
             "roofline": roof,
             "pipeline_gbps_model": round(pipeline_gbps, 2),
-            "h2d_upload_ms": round(h2d_s * 1e3, 2),
             "render_s": round(render_s, 2),
+            "sequence_check": seq_check,
             "cpu_baseline": cpu,
             "latency": lat,
+            "c4_batched": c4_line,
             "next_rows": {"undistort_remap": und_line, "search_local_points_direct": direct_line,
                           "stereo_matches": stereo_line, "dbow2_transform": bow_line},
         }
@@ -435,6 +555,67 @@ def latency_leg(frames, poses, sc, S, n_timed, warm=10):
             "median_align_ms": round(float(np.median(ts - te)), 4),
             "path": "host C ABI, one frame at a time: H2D 752x480 u8 -> pyramid -> extract -> D2H kps+desc -> "
                     "SparseImgAlign 3..1 (prev -> cur) -> D2H pose; median over frames after 10 warm-up frames"}
+
+
+TUM1_CAM = (517.306408, 516.469215, 318.643040, 255.313989)  # Examples/RGB-D/TUM1.yaml Camera.fx/fy/cx/cy
+
+
+def c4_leg(S, dev, args, B=256):
+    """BASELINE config C4: TUM fr1_desk-shaped 640x480 frames, ORBextractor(2000, 1.2, 8, 20, 7)
+    (Examples/RGB-D/TUM1.yaml), batched 256-frame extract + dense Hamming (k vs k-1) throughput:
+    frames rendered on the device (the textured plane under the TUM intrinsics), resident in HBM,
+    HIP-event timed over `--steps` repetitions after 2 warm-up passes."""
+    import torch
+    import ygzfe
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C4"]
+    sc = S.PlaneScene(23, W, H)
+    poses = [ygzfe.trajectory_pose(sweep_index(g), XI) for g in range(B)]
+    b = ygzfe.Batch((nf, sf, nl, ini, mn, 0), dev.index or 0, W, H, B)
+    st = torch.cuda.current_stream(dev)
+    tex = torch.from_numpy(sc.tex).to(dev)
+    q = torch.from_numpy(np.stack([p[0] for p in poses])).to(dev)
+    t = torch.from_numpy(np.stack([p[1] for p in poses])).to(dev)
+    seeds = torch.arange(50000, 50000 + B, dtype=torch.int64, device=dev)
+    ygzfe.render_plane_device(tex.data_ptr(), S.TEX_W, S.TEX_H, S.TEXEL, S.PLANE_Z, TUM1_CAM, q.data_ptr(),
+                              t.data_ptr(), seeds.data_ptr(), B, W, H, b.frames_ptr(), b.frame_pitch, noise_amp=2,
+                              stream=st.cuda_stream)
+    cap = b.kp_cap
+    P = B - 1
+    ri = torch.arange(0, P, dtype=torch.int32, device=dev)
+    ci = ri + 1
+    bi = torch.empty((P, cap), dtype=torch.int32, device=dev)
+    bd, sd = torch.empty_like(bi), torch.empty_like(bi)
+
+    def step():
+        b.extract(B, st.cuda_stream)
+        b.match(P, ci.data_ptr(), ri.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(), st.cuda_stream)
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize(dev)
+    b.check()
+    reps = max(args.steps, 5)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        step()
+    e1.record(st)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    b.timing(True)
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize(dev)
+    stages = b.timing(False)
+    b.check()
+    cand, selk = b.stats(B)
+    n_kp = [b.result(i)[0].shape[0] for i in range(0, B, 32)]
+    return {"config": "C4 TUM1.yaml: 640x480, nFeatures 2000, scale 1.2, 8 levels, FAST 20/7",
+            "frames": B, "ms_per_step": round(ms, 4), "frames_per_s": round(B / (ms * 1e-3), 1),
+            "mean_keypoints": round(float(np.mean(n_kp)), 1),
+            "mean_keypoints_per_level": [round(float(c) / B, 1) for c in selk],
+            "stages_ms": {k: round(v, 4) for k, v in stages.items() if v > 0},
+            "path": "device-rendered frames resident in HBM; batch extract + dense Hamming (k vs k-1), HIP events"}
 
 
 def bow_leg(S, batch, B, dev, stream, with_cpu, reps=10):

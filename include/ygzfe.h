@@ -177,6 +177,22 @@ int ygzfe_batch_read_level(ygzfe_batch *b, int frame, int level, int blurred, ui
  * vToDistributeKeys) and keypoints kept by the octree, each [nlevels] summed
  * over the frames.  For roofline accounting (bytes per launch). */
 int ygzfe_batch_stats(ygzfe_batch *b, int n_frames, int64_t *candidates, int64_t *selected);
+/* Offline sequence mode: fixed-size per-frame result slots,
+ * packed on the device and gathered to rank 0 over RCCL.  Slot layout:
+ *   [0, 64)  int32 n_kps, int32 n_visible, f32 q[4] (x,y,z,w), f32 t[3], f32 chi2,
+ *            int32 global frame index, int32 has_align, 4 x int32 0;
+ *   then kp_cap keypoint rows (ygzfe_kp) and kp_cap x 32 descriptor bytes,
+ *   rows >= n_kps zero; zero padding to a 16-B multiple.
+ * The align fields of frame f are SparseImgAlign's TCR of the pair (f-1 -> f). */
+#define YGZFE_SLOT_HEADER 64
+size_t ygzfe_slot_bytes(int kp_cap);
+/* Pack batch frames [frame_begin, frame_begin + n_frames) into slots
+ * d_slots + k * slot_pitch (slot_pitch >= ygzfe_slot_bytes, multiple of 16);
+ * frame f takes d_align[f - 1] (the result of the pair aligning f-1 -> f) when
+ * d_align != NULL and f >= 1; global index = global_first + (f - frame_begin).
+ * Device pointers, one launch on `stream`. */
+int ygzfe_batch_pack_slots(ygzfe_batch *b, int frame_begin, int n_frames, const struct ygzfe_align_result *d_align,
+                           int global_first, uint8_t *d_slots, size_t slot_pitch, void *stream);
 /* Kernel timing (hipEvents around each stage launch on the batch stream).
  * enable != 0 turns it on; ms[] receives per-stage milliseconds of the last
  * ygzfe_batch_extract; names[] the stage names. Returns stage count. */

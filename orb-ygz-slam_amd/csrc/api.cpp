@@ -240,9 +240,9 @@ struct ygzfe_batch {
 };
 
 static const char *kStageNames[] = {"pyramid", "blur7", "fast9_cells", "octree", "orient_rbrief", "hamming_best2",
-                                    "sparse_align", "stereo"};
-constexpr int kNumStages = 8;
-enum { ST_PYR, ST_BLUR, ST_FAST, ST_OCT, ST_DESC, ST_HAM, ST_ALIGN };
+                                    "sparse_align", "stereo", "pack_slots"};
+constexpr int kNumStages = 9;
+enum { ST_PYR, ST_BLUR, ST_FAST, ST_OCT, ST_DESC, ST_HAM, ST_ALIGN, ST_STEREO, ST_PACK };
 
 extern "C" {
 
@@ -800,6 +800,32 @@ int ygzfe_batch_timing(ygzfe_batch *b, int enable, float *ms, const char **names
 
 void *ygzfe_batch_stream(ygzfe_batch *b) { return b ? (void *)b->stream : nullptr; }
 
+size_t ygzfe_slot_bytes(int kp_cap) {
+    if (kp_cap < 0) return 0;
+    return ((size_t)YGZFE_SLOT_HEADER + (size_t)kp_cap * 60 + 15) & ~(size_t)15;
+}
+
+int ygzfe_batch_pack_slots(ygzfe_batch *b, int frame_begin, int n_frames, const struct ygzfe_align_result *d_align,
+                           int global_first, uint8_t *d_slots, size_t slot_pitch, void *stream) {
+    if (!b || frame_begin < 0 || n_frames < 0 || frame_begin + n_frames > b->maxF || (n_frames > 0 && !d_slots)) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    const Plan &P = b->plan->hp();
+    if (slot_pitch < ygzfe_slot_bytes(P.kp_cap) || (slot_pitch & 15) || ((uintptr_t)d_slots & 15)) {
+        set_error("slot pitch %zu (need >= %zu, 16-B multiple, 16-B aligned base)", slot_pitch,
+                  ygzfe_slot_bytes(P.kp_cap));
+        return YGZFE_EINVAL;
+    }
+    YGZ_TRY(ensure_device(b->device));
+    hipStream_t st = stream ? (hipStream_t)stream : b->stream;
+    hipEvent_t t0 = b->begin(st);
+    YGZ_HIP(launch_pack_slots(b->ws.kps.as<ygzfe_kp>(), b->ws.desc.as<uint8_t>(), b->ws.counts.as<int>(), P.kp_cap,
+                              d_align, frame_begin, n_frames, global_first, d_slots, slot_pitch, st));
+    b->end(ST_PACK, t0, st);
+    return YGZFE_OK;
+}
+
 // ------------------------------------------------------------------ hamming
 int ygzfe_hamming_best2_device(const uint8_t *d_query, int nq, const uint8_t *d_train, int nt, int32_t *d_best_idx,
                                int32_t *d_best_dist, int32_t *d_second_dist, void *stream) {
@@ -1258,7 +1284,7 @@ extern "C" int ygzfe_batch_stereo(ygzfe_batch *b, int n_pairs, const int32_t *d_
                                      d_right_idx, d_u_right, d_depth, b->ssad.as<int>(), b->sjobs.as<StereoJob>(),
                                      st));
     YGZ_HIP(launch_stereo(b->sjobs.as<StereoJob>(), n_pairs, P.kp_cap, stereo_levels_of(P), mb, mbf, st));
-    b->end(7, t0, st);
+    b->end(ST_STEREO, t0, st);
     return YGZFE_OK;
 }
 

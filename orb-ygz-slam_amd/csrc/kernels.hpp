@@ -129,6 +129,11 @@ hipError_t launch_search_direct(const uint8_t *const *ref_pyrs, const AlignLevel
                                 const float *px_proj, float *px_item, uint8_t *ok_item, float border, float *px_out,
                                 int32_t *matched, hipStream_t st);
 
+// slots.hip: offline sequence mode result slots
+hipError_t launch_pack_slots(const ygzfe_kp *kps, const uint8_t *desc, const int *counts, int kp_cap,
+                             const ygzfe_align_result *align, int frame_begin, int n_frames, int global_first,
+                             uint8_t *slots, size_t slot_pitch, hipStream_t st);
+
 hipError_t launch_undistort_map(const float cam[4], const float *dist, int ndist, int W, int H, int16_t *map1,
                                 uint16_t *map2, hipStream_t st);
 int remap_tiles(int W, int H);  // entries of the per-tile source-box table (16 B each: x0, y0, w, h)

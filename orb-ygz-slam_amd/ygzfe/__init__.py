@@ -107,6 +107,13 @@ def device_count():
     return lib().ygzfe_device_count()
 
 
+def slot_bytes(kp_cap):
+    """Bytes of one offline-sequence result slot (ygzfe_slot_bytes)."""
+    L = lib()
+    L.ygzfe_slot_bytes.restype = C.c_size_t
+    return int(L.ygzfe_slot_bytes(kp_cap))
+
+
 def orb_plan(nfeatures, scale_factor, nlevels, ini_th=20, min_th=7, width=752, height=480, blur=BLUR_CV4):
     """Host-only extraction plan (ygzfe_orb_plan): level sizes, budgets, FAST cells, umax."""
     p = OrbParams(nfeatures, scale_factor, nlevels, ini_th, min_th, blur)
@@ -489,6 +496,12 @@ class Batch:
     def stream(self):
         return lib().ygzfe_batch_stream(self.h)
 
+    def frames_ptr(self):
+        """Device pointer of the pyramid slots (frame i level 0 at + i * frame_pitch)."""
+        p = C.c_void_p()
+        _check(lib().ygzfe_batch_frames(self.h, C.byref(p)), "batch_frames")
+        return p.value
+
     def upload(self, frames):
         frames = np.ascontiguousarray(frames, np.uint8)
         _check(lib().ygzfe_batch_upload(self.h, _p(frames), len(frames)), "batch_upload")
@@ -569,6 +582,13 @@ class Batch:
                                              C.c_void_p(d_fv_nodes), C.c_void_p(d_fv_feats), C.c_void_p(d_n_fv),
                                              C.c_void_p(stream)), "batch_compute_bow")
 
+    def pack_slots(self, frame_begin, n_frames, d_align, global_first, d_slots, slot_pitch, stream=None):
+        """Device-side packing of the offline sequence mode's per-frame result slots
+        (ygzfe_batch_pack_slots; layout in include/ygzfe.h and ygzfe.dist)."""
+        _check(lib().ygzfe_batch_pack_slots(self.h, frame_begin, n_frames, C.c_void_p(d_align or None), global_first,
+                                            C.c_void_p(d_slots), C.c_size_t(slot_pitch), C.c_void_p(stream)),
+               "batch_pack_slots")
+
     def timing(self, enable=True):
         ms = (C.c_float * 16)()
         names = (C.c_char_p * 16)()
@@ -636,17 +656,34 @@ def backproject_plane(cam, q_cw, t_cw, uv, plane_z):
 _synth_hip = None
 
 
-def plane_points_device(d_kps, cap, n_frames, cam, d_r3, d_cz, plane_z, d_xyz, stream=None):
-    """Synthetic map points for bench.py: back-project every keypoint of frame i
-    onto the plane Z_w = plane_z (one fused HIP pass; synth/plane_points.hip)."""
+def _synth_hip_lib():
     global _synth_hip
     if _synth_hip is None:
         lib()  # torch's HIP runtime first (see lib())
         if not os.path.exists(SYNTH_HIP_PATH):
             raise YgzfeError(f"{SYNTH_HIP_PATH} missing: run `make -C orb-ygz-slam_amd`")
         _synth_hip = C.CDLL(SYNTH_HIP_PATH)
+    return _synth_hip
+
+
+def render_plane_device(d_tex, tex_w, tex_h, texel, plane_z, cam, d_q, d_t, d_seeds, n_frames, W, H, d_out, pitch,
+                        noise_amp=2, stream=None):
+    """The synthetic plane sequence rendered on the device (synth/plane_points.hip):
+    frame i (pose d_q[i], d_t[i], noise seed d_seeds[i]) -> d_out + i * pitch."""
     c = (C.c_float * 4)(*[float(v) for v in cam])
-    rc = _synth_hip.ygzs_plane_points(C.c_void_p(d_kps), KP_DTYPE.itemsize // 4, cap, n_frames, c, C.c_void_p(d_r3),
+    rc = _synth_hip_lib().ygzs_render_plane_device(C.c_void_p(d_tex), tex_w, tex_h, C.c_double(texel),
+                                                   C.c_double(plane_z), c, C.c_void_p(d_q), C.c_void_p(d_t),
+                                                   C.c_void_p(d_seeds), n_frames, W, H, noise_amp, C.c_void_p(d_out),
+                                                   C.c_size_t(pitch), C.c_void_p(stream))
+    if rc != 0:
+        raise YgzfeError("render_plane_device launch failed")
+
+
+def plane_points_device(d_kps, cap, n_frames, cam, d_r3, d_cz, plane_z, d_xyz, stream=None):
+    """Synthetic map points for bench.py: back-project every keypoint of frame i
+    onto the plane Z_w = plane_z (one fused HIP pass; synth/plane_points.hip)."""
+    c = (C.c_float * 4)(*[float(v) for v in cam])
+    rc = _synth_hip_lib().ygzs_plane_points(C.c_void_p(d_kps), KP_DTYPE.itemsize // 4, cap, n_frames, c, C.c_void_p(d_r3),
                                       C.c_void_p(d_cz), C.c_float(plane_z), C.c_void_p(d_xyz), C.c_void_p(stream))
     if rc != 0:
         raise YgzfeError("plane_points launch failed")

@@ -5,25 +5,29 @@ slices of the sequence, no data-path collective.
   * SparseImgAlign needs (k-1, k) pairs, so a rank whose slice starts at
     frame b > 0 also extracts frame b-1 (a one-frame halo) and aligns every
     pair inside [b-1, e);
-  * results are fixed-size per-frame slots; the offline sequence mode (C5)
-    gathers them to rank 0 once, after the run (point-to-point into the root:
-    `torch.distributed.gather`, which RCCL implements with grouped send/recv over
-    the xGMI peer links).  The bench's timed region has no collective at all:
-    only a barrier and the max-over-ranks of the elapsed time.
+  * results are fixed-size per-frame slots packed on the device; the offline
+    sequence mode (C5) gathers them to rank 0 in every step (point-to-point into
+    the root: `torch.distributed.gather`, which RCCL implements with grouped
+    send/recv over the xGMI peer links).  That gather is the only data-path
+    collective; the timed region is bracketed by barriers and the elapsed time
+    is the max over ranks.
 
 Everything here is host-side orchestration on top of torch.distributed; it
 runs the same with the "nccl" (RCCL) backend on GPUs and "gloo" in CPU tests.
 """
 import numpy as np
 
-# slot layout per frame (little endian):
-#   int32 n_kps, int32 n_visible, float32 T_cur_prev q[4] t[3], float32 chi2,
-#   kps [cap x 28 B] (cv::KeyPoint layout), desc [cap x 32 B]
-SLOT_HEADER = 4 * (2 + 7 + 1)
+# slot layout per frame (include/ygzfe.h YGZFE_SLOT_*, packed on the device by
+# ygzfe_batch_pack_slots; this numpy form is the reference the tests compare):
+#   [0, 64)  int32 n_kps, int32 n_visible, float32 T_cur_prev q[4] t[3], float32 chi2,
+#            int32 global frame index, int32 has_align, 4 x 0
+#   kps [cap x 28 B] (cv::KeyPoint layout), desc [cap x 32 B]; rows >= n_kps zero;
+#   zero padding to a multiple of 16 B
+SLOT_HEADER = 64
 
 
 def slot_bytes(cap):
-    return SLOT_HEADER + cap * (28 + 32)
+    return (SLOT_HEADER + cap * (28 + 32) + 15) // 16 * 16
 
 
 def shard(n_frames, rank, world):
@@ -45,35 +49,50 @@ def align_pairs(begin, end):
     return [(k - 1, k) for k in range(max(begin, 1), end)]
 
 
-def pack_slots(counts, kps, desc, align=None):
+ALIGN_DTYPE = np.dtype([("q", "<f4", 4), ("t", "<f4", 3), ("n_visible", "<i4"), ("chi2", "<f4")])
+
+
+def pack_slots(counts, kps, desc, align=None, global_first=0, has_align=None):
     """Per-frame slots (uint8 [F, slot_bytes(cap)]) from numpy results.
 
     counts [F] int, kps [F, cap] structured (28 B), desc [F, cap, 32] uint8,
-    align: optional [F] records with q, t, n_visible, chi2 (frame k's pose
-    relative to k-1; zero for the first frame of the sequence)."""
+    align: optional [F] ALIGN_DTYPE records (frame k's pose relative to k-1);
+    has_align [F] bool (default: every frame but global frame 0 when align is given)."""
     F, cap = kps.shape[0], kps.shape[1]
     out = np.zeros((F, slot_bytes(cap)), np.uint8)
-    hdr = np.zeros((F, 10), np.float32)
+    hdr = np.zeros((F, 16), np.float32)
     hdr_i = hdr.view(np.int32)
+    counts = np.asarray(counts, np.int32)
     hdr_i[:, 0] = counts
+    hdr[:, 5] = 1.0  # identity q when there is no align record
+    gidx = global_first + np.arange(F)
+    hdr_i[:, 10] = gidx
     if align is not None:
-        hdr_i[:, 1] = align["n_visible"]
-        hdr[:, 2:6] = align["q"]
-        hdr[:, 6:9] = align["t"]
-        hdr[:, 9] = align["chi2"]
+        has = (gidx >= 1) if has_align is None else np.asarray(has_align, bool)
+        hdr_i[has, 1] = align["n_visible"][has]
+        hdr[has, 2:6] = align["q"][has]
+        hdr[has, 6:9] = align["t"][has]
+        hdr[has, 9] = align["chi2"][has]
+        hdr_i[has, 11] = 1
     out[:, :SLOT_HEADER] = hdr.view(np.uint8).reshape(F, SLOT_HEADER)
-    out[:, SLOT_HEADER:SLOT_HEADER + cap * 28] = np.ascontiguousarray(kps).view(np.uint8).reshape(F, cap * 28)
-    out[:, SLOT_HEADER + cap * 28:] = np.ascontiguousarray(desc, np.uint8).reshape(F, cap * 32)
+    kb = np.ascontiguousarray(kps).view(np.uint8).reshape(F, cap, 28).copy()
+    db = np.ascontiguousarray(desc, np.uint8).reshape(F, cap, 32).copy()
+    rows = np.arange(cap)[None, :] >= counts[:, None]
+    kb[rows] = 0
+    db[rows] = 0
+    out[:, SLOT_HEADER:SLOT_HEADER + cap * 28] = kb.reshape(F, cap * 28)
+    out[:, SLOT_HEADER + cap * 28:SLOT_HEADER + cap * 60] = db.reshape(F, cap * 32)
     return out
 
 
 def unpack_slot(slot, cap, kp_dtype):
     hdr = slot[:SLOT_HEADER].view(np.float32)
-    n = int(hdr.view(np.int32)[0])
+    hi = hdr.view(np.int32)
+    n = int(hi[0])
     kps = slot[SLOT_HEADER:SLOT_HEADER + cap * 28].view(kp_dtype)[:n]
-    desc = slot[SLOT_HEADER + cap * 28:].reshape(cap, 32)[:n]
-    return {"n": n, "n_visible": int(hdr.view(np.int32)[1]), "q": hdr[2:6].copy(), "t": hdr[6:9].copy(),
-            "chi2": float(hdr[9]), "kps": kps, "desc": desc}
+    desc = slot[SLOT_HEADER + cap * 28:SLOT_HEADER + cap * 60].reshape(cap, 32)[:n]
+    return {"n": n, "n_visible": int(hi[1]), "q": hdr[2:6].copy(), "t": hdr[6:9].copy(), "chi2": float(hdr[9]),
+            "frame": int(hi[10]), "has_align": bool(hi[11]), "kps": kps, "desc": desc}
 
 
 def gather_slots(local_slots, n_frames, rank, world, device=None):

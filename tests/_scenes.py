@@ -88,6 +88,13 @@ class PlaneScene:
         return ygzfe.Camera(*self.cam)
 
 
+def world_to_cam(pose, Pw):
+    """xyz_ref = T_cw * P_w (the SparseImgAlign map-point snapshot), float32 [n, 3]."""
+    q, t = (np.asarray(a, np.float64) for a in pose)
+    Pw = np.asarray(Pw, np.float64).reshape(-1, 3)
+    return np.array([quat_rot(q, p) + t for p in Pw], np.float32).reshape(-1, 3)
+
+
 def motion(seed, scale=1.0):
     """True relative motion delta = (0.02,-0.01,0.015 m; 0.005,-0.004,0.003 rad) + seeded jitter (§8d)."""
     rng = np.random.default_rng(seed)

@@ -66,7 +66,7 @@ def _worker(rank, world, port, n_frames, cap, ret):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     b, e = D.shard(n_frames, rank, world)
     counts, kps, desc, align = fake_results(list(range(b, e)), cap)
-    slots = torch.from_numpy(D.pack_slots(counts, kps, desc, align))
+    slots = torch.from_numpy(D.pack_slots(counts, kps, desc, align, global_first=b))
     full = D.gather_slots(slots, n_frames, rank, world)
     t = D.max_over_ranks(1.0 + rank)
     if rank == 0:
@@ -89,4 +89,112 @@ def test_gloo_world2_gather_and_timing(n_frames):
     assert np.array_equal(full, D.pack_slots(counts, kps, desc, align))
     s = D.unpack_slot(full[7], cap, ygzfe.KP_DTYPE)
     assert s["n"] == counts[7] and np.array_equal(s["kps"], kps[7][:counts[7]])
-    assert np.allclose(s["t"], (7, -7, 0.5))
+    assert np.allclose(s["t"], (7, -7, 0.5)) and s["frame"] == 7 and s["has_align"]
+    assert not D.unpack_slot(full[0], cap, ygzfe.KP_DTYPE)["has_align"]
+
+
+# ---------------------------------------------------------------- real extractor output
+# The C5 pipeline per rank (bench.py): extract the shard plus its one-frame halo,
+# align every pair (k-1, k) of the shard, pack the slots, gather to rank 0 -- here
+# with the CPU oracle standing in for the HIP extractor, so the sharding, halo and
+# gather logic is checked against one single-rank run of the same sequence.
+SEQ = 5
+
+
+def _sequence():
+    import _scenes as S
+    sc = S.PlaneScene(11)
+    xi = np.array([0.012, -0.006, 0.009, 0.0025, -0.002, 0.0015], np.float32)
+    poses = [ygzfe.trajectory_pose(g, xi) for g in range(SEQ)]
+    return sc, poses
+
+
+def _rank_slots(frames, first, sc, poses, cap):
+    """Oracle extraction of global frames [first, first + len(frames)) plus SparseImgAlign of
+    each consecutive pair; returns the slots of frames[1:] if first > 0 (halo), else all."""
+    import _oracle as O
+    import _scenes as S
+    orc = O.OrbOracle(1000, 2.0, 4, 20, 7)
+    cam = O.Cam(*sc.cam)
+    F = len(frames)
+    kps = np.zeros((F, cap), ygzfe.KP_DTYPE)
+    desc = np.zeros((F, cap, 32), np.uint8)
+    counts = np.zeros(F, np.int32)
+    align = np.zeros(F, D.ALIGN_DTYPE)
+    levels = []
+    for i, g in enumerate(frames):
+        lv = orc.pyramid(sc.render(*poses[g], noise_seed=g))
+        k, d = orc.extract(lv)
+        counts[i] = len(k)
+        kps[i, :len(k)] = k
+        desc[i, :len(k)] = d
+        levels.append(lv)
+        if i > 0:
+            Pw, ok = sc.map_points(*poses[g - 1], kps[i - 1, :counts[i - 1]])
+            T0 = O.se3_from((0, 0, 0, 1), (0, 0, 0))
+            r = O.sparse_align(levels[i - 1], lv, orc.inv_scale, cam, kps[i - 1, :counts[i - 1]],
+                               S.world_to_cam(poses[g - 1], Pw), ok, 3, 1, T0)
+            align[i] = (tuple(r.T.q), tuple(r.T.t), r.n_visible, r.chi2)
+    h = 1 if first > 0 else 0
+    return D.pack_slots(counts[h:], kps[h:], desc[h:], align[h:], global_first=first + h,
+                        has_align=np.arange(h, F) + first >= 1)
+
+
+def _real_worker(rank, world, port, cap, ret):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc, poses = _sequence()
+    b, e = D.shard(SEQ, rank, world)
+    hb, he = D.with_halo(b, e)
+    slots = torch.from_numpy(_rank_slots(list(range(hb, he)), hb, sc, poses, cap))
+    full = D.gather_slots(slots, SEQ, rank, world)
+    if rank == 0:
+        ret["full"] = full.numpy()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_gather_real_extraction_equals_single_rank():
+    cap = 1100
+    sc, poses = _sequence()
+    single = _rank_slots(list(range(SEQ)), 0, sc, poses, cap)
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_real_worker, args=(2, free_port(), cap, ret), nprocs=2, join=True)
+    full = ret["full"]
+    assert full.shape == single.shape
+    assert np.array_equal(full, single)
+    # every frame but the first carries its align record (the halo pair included)
+    hdr = [D.unpack_slot(full[g], cap, ygzfe.KP_DTYPE) for g in range(SEQ)]
+    assert [h["has_align"] for h in hdr] == [False] + [True] * (SEQ - 1)
+    assert all(h["n"] > 300 for h in hdr) and all(h["n_visible"] > 100 for h in hdr[1:])
+
+
+# ---------------------------------------------------------------- bench.py --gpus N contract
+def _bench(args, env_extra=None):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=120, env=env)
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """--gpus 2 with fewer visible GPUs fails loudly (never a silent n_gpus: 1 line)."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("two GPUs visible")
+    r = _bench(["--gpus", "2", "--steps", "1"])
+    assert r.returncode != 0
+    assert "--gpus 2 needs 2 visible GPUs" in r.stderr
+    assert '"n_gpus"' not in r.stdout
+
+
+def test_bench_world_size_must_match_gpus():
+    r = _bench(["--gpus", "2", "--steps", "1"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
