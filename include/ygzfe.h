@@ -215,10 +215,74 @@ int ygzfe_hamming_best2_device(const uint8_t *d_query, int nq, const uint8_t *d_
 int ygzfe_hamming_best2(int device, const uint8_t *query, int nq, const uint8_t *train, int nt,
                         int32_t *best_idx, int32_t *best_dist, int32_t *second_dist);
 /* Windowed search (Frame::GetFeaturesInArea candidate lists, Frame.cc:424-481):
- * CSR candidates; writes the distance of every (query, candidate) pair so the
- * caller replays the reference's sequential assignment rules exactly. */
+ * CSR candidates; writes the distance of every (query, candidate) pair. */
 int ygzfe_hamming_csr(int device, const uint8_t *query, int nq, const uint8_t *train, int nt,
                       const int32_t *row_ptr, const int32_t *cand, int32_t *dist_out);
+
+/* The tracking-path searches, complete with the reference's sequential rules
+ * (TH_HIGH / TH_LOW, nnratio, "already matched" skips, the 30-bin rotation
+ * histogram and ComputeThreeMaxima), bit-exact with oracle/match.c.
+ *
+ * A match frame is the searched Frame's state the searches read: mvKeys
+ * (level-0 px), mDescriptors, mvuRight (NULL = none) and the image bounds
+ * mnMinX / mnMaxX / mnMinY / mnMaxY (Frame.cc:501-507); its 64 x 48 grid
+ * (AssignFeaturesToGrid / PosInGrid, Frame.cc:314-330, 483-493) is built on
+ * the device.  n <= 65535 keypoints. */
+typedef struct ygzfe_bounds { float min_x, max_x, min_y, max_y; } ygzfe_bounds;
+typedef struct ygzfe_match_frame ygzfe_match_frame;
+int ygzfe_match_frame_create(int device, ygzfe_match_frame **out);
+void ygzfe_match_frame_destroy(ygzfe_match_frame *f);
+int ygzfe_match_frame_set(ygzfe_match_frame *f, const ygzfe_kp *kps, const uint8_t *desc, int n, const float *u_right,
+                          const ygzfe_bounds *bounds);
+/* Diagnostics of the last search on this frame: queries re-scanned because the
+ * sequential skips exhausted their K best candidates (the result never depends on it). */
+int ygzfe_match_frame_stats(const ygzfe_match_frame *f, int *rescans);
+/* The same from frame `frame` of a batch (device-to-device copy of its rows). */
+int ygzfe_match_frame_from_batch(ygzfe_match_frame *f, ygzfe_batch *b, int frame, const ygzfe_bounds *bounds);
+
+#define YGZFE_MQ_VALID 1   /* the query takes part (MapPoint present, not bad / outlier, projected inside) */
+#define YGZFE_MQ_BLOCKS 2  /* assigning it makes later queries skip the keypoint (Observations() > 0) */
+#define YGZFE_MQ_STEREO 4  /* the projection searches' mvuRight test applies */
+/* One query: the GetFeaturesInArea(u, v, radius, min_level, max_level)
+ * window (-1 levels as the reference's defaults), the projected right u for
+ * the stereo test, the query keypoint's angle (rotation histogram), flags. */
+typedef struct ygzfe_match_query {
+    float u, v, radius, u_right;
+    int32_t min_level, max_level;
+    float angle;
+    int32_t flags;
+} ygzfe_match_query;
+enum ygzfe_match_mode { YGZFE_MATCH_BEST = 0, YGZFE_MATCH_RATIO = 1, YGZFE_MATCH_INIT = 2, YGZFE_MATCH_BOW = 3 };
+
+/* SearchByProjection(CurrentFrame, LastFrame, th, bMono, checkLevel)
+ * (ORBmatcher.cc:1218-1350), and the relocalisation form
+ * SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (:1352-1469):
+ * query i = the i-th projected MapPoint (the caller projects with its own pose
+ * types; radius = th * mvScaleFactors[octave], levels per bForward / bBackward /
+ * checkLevel), q_desc[i] = MapPoint::GetDescriptor().  train_blocked[i2] != 0
+ * where CurrentFrame.mvpMapPoints[i2] makes the reference skip i2.  Best only,
+ * bestDist <= th_dist (TH_HIGH = 100 / ORBdist), rotation check.  train_match[i2]:
+ * -1 untouched, -2 set to NULL by the rotation check, >= 0 the query assigned. */
+int ygzfe_search_projection_best(ygzfe_match_frame *cur, const ygzfe_match_query *q, const uint8_t *q_desc, int nq,
+                                 const uint8_t *train_blocked, int th_dist, int check_ori, int32_t *train_match,
+                                 int *nmatches);
+/* SearchByProjection(F, vpMapPoints, th, checkLevel) (ORBmatcher.cc:43-126): best
+ * and second best with their octaves, bestDist <= TH_HIGH, the nnratio test when
+ * both share an octave.  train_match[idx]: -1 or the query assigned. */
+int ygzfe_search_projection_ratio(ygzfe_match_frame *F, const ygzfe_match_query *q, const uint8_t *q_desc, int nq,
+                                  const uint8_t *train_blocked, float nnratio, int32_t *train_match, int *nmatches);
+/* SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+ * (ORBmatcher.cc:375-478): prev_matched [2 * F1.n] in / out, matches12 [F1.n]. */
+int ygzfe_search_for_initialization(ygzfe_match_frame *F1, ygzfe_match_frame *F2, float *prev_matched,
+                                    int window_size, float nnratio, int check_ori, int32_t *matches12, int *nmatches);
+/* SearchByBoW(pKF, F, vpMapPointMatches) (ORBmatcher.cc:155-263).  The two
+ * FeatureVectors (DBoW2, node-sorted) as CSR: node k = nodes[k], features
+ * feats[ptr[k] .. ptr[k+1]).  kf_usable[i] = pKF's MapPoint i present and not bad.
+ * f_match[F.n]: the KF keypoint index matched to F's keypoint, or -1. */
+int ygzfe_search_by_bow(ygzfe_match_frame *kf, ygzfe_match_frame *F, const uint8_t *kf_usable, int n_kf_nodes,
+                        const int32_t *kf_nodes, const int32_t *kf_ptr, const int32_t *kf_feats, int n_f_nodes,
+                        const int32_t *f_nodes, const int32_t *f_ptr, const int32_t *f_feats, float nnratio,
+                        int check_ori, int32_t *f_match, int *nmatches);
 
 /* ------------------------------------------------------------------------ */
 /* SparseImgAlign (SparseImageAlign.h:37-60)                                 */

@@ -135,6 +135,42 @@ int ygzo_descriptor_distance(const uint8_t *a, const uint8_t *b);
 void ygzo_hamming_best2(const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *best_idx,
                         int32_t *best_dist, int32_t *second_dist);
 
+/* ---------------- ORBmatcher tracking-path searches (oracle/match.c) ---------------- */
+/* The searched frame: mvKeys (level-0 px), mDescriptors, mvuRight (NULL = none),
+ * image bounds mnMinX / mnMaxX / mnMinY / mnMaxY (Frame::ComputeImageBounds). */
+typedef struct ygzo_mframe {
+    const ygzo_kp *kps;
+    const uint8_t *desc;
+    const float *u_right;
+    int n;
+    float min_x, max_x, min_y, max_y;
+} ygzo_mframe;
+#define YGZO_MQ_VALID 1   /* query takes part (pMP present, not bad / outlier, projected inside) */
+#define YGZO_MQ_BLOCKS 2  /* assigning it blocks the keypoint for later queries (Observations() > 0) */
+#define YGZO_MQ_STEREO 4  /* the mvuRight test of the projection searches applies */
+/* One query: GetFeaturesInArea(u, v, radius, min_level, max_level) window, the
+ * stereo u_right, the query keypoint angle (rotation histogram), flags. */
+typedef struct ygzo_mquery {
+    float u, v, radius, u_right;
+    int32_t min_level, max_level;
+    float angle;
+    int32_t flags;
+} ygzo_mquery;
+int ygzo_pos_in_grid(const ygzo_mframe *f, float x, float y, int *px, int *py);
+int ygzo_features_in_area(const ygzo_mframe *f, float x, float y, float r, int min_level, int max_level, int *out);
+void ygzo_compute_three_maxima(const int *histo, int L, int *ind1, int *ind2, int *ind3);
+int ygzo_rot_bin(float angle_query, float angle_train);
+int ygzo_search_projection_best(const ygzo_mframe *cur, const ygzo_mquery *q, const uint8_t *q_desc, int nq,
+                                const uint8_t *train_blocked, int th_dist, int check_ori, int32_t *train_match);
+int ygzo_search_projection_ratio(const ygzo_mframe *F, const ygzo_mquery *q, const uint8_t *q_desc, int nq,
+                                 const uint8_t *train_blocked, float nnratio, int32_t *train_match);
+int ygzo_search_for_initialization(const ygzo_mframe *F1, const ygzo_mframe *F2, float *prev_matched, int window,
+                                   float nnratio, int check_ori, int32_t *matches12);
+int ygzo_search_by_bow(const ygzo_mframe *kf, const ygzo_mframe *F, const uint8_t *kf_usable, int n_kf_nodes,
+                       const int32_t *kf_nodes, const int32_t *kf_ptr, const int32_t *kf_feats, int n_f_nodes,
+                       const int32_t *f_nodes, const int32_t *f_ptr, const int32_t *f_feats, float nnratio,
+                       int check_ori, int32_t *f_match);
+
 /* ---------------- SparseImgAlign (SparseImageAlign.cc) ---------------- */
 typedef struct ygzo_cam { float fx, fy, cx, cy; } ygzo_cam;
 /* SE3f as unit quaternion (x,y,z,w) + translation: matches Sophus SE3f. */

@@ -8,6 +8,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -1773,5 +1774,358 @@ extern "C" int ygzfe_batch_upload_undistorted(ygzfe_batch *b, ygzfe_undistort *u
                                 u->map2.as<uint16_t>(), u->boxes.p, u->max_box, u->any_large, b->pyr.as<uint8_t>(),
                                 P.pyr_bytes, P.W, n_frames, b->stream));
     YGZ_HIP(hipStreamSynchronize(b->stream));
+    return YGZFE_OK;
+}
+
+// --------------------------------------------------------------------------
+// ORBmatcher searches (match.hip): the searched frame's state on the device,
+// one packed H2D of the queries, two launches, one packed D2H of the results.
+struct ygzfe_match_frame {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int n = 0;
+    bool has_uright = false;
+    ygzfe_bounds bounds{0.f, 0.f, 0.f, 0.f};
+    float inv_w = 0.f, inv_h = 0.f;
+    DevBuf kps, desc, uright, cell;
+    std::vector<ygzfe_kp> host_kps;  // angles / octaves / positions the host-side query building reads
+    int last_rescans = 0;            // queries of the last search whose top-K list the skips exhausted
+    // per-call staging
+    DevBuf in, out, scratch;
+    std::vector<uint8_t> hin, hout;
+};
+
+namespace {
+
+constexpr int kMatchTopK = 8;  // match.hip kTopK
+
+struct Arena {
+    size_t off = 0;
+    size_t take(size_t bytes) {
+        const size_t o = off;
+        off = (off + bytes + 255) & ~(size_t)255;
+        return o;
+    }
+};
+
+int match_frame_finish(ygzfe_match_frame *f, const ygzfe_bounds *bounds) {
+    f->bounds = *bounds;
+    // Frame.cc:296-297
+    f->inv_w = (float)64 / (float)(bounds->max_x - bounds->min_x);
+    f->inv_h = (float)48 / (float)(bounds->max_y - bounds->min_y);
+    YGZ_TRY(f->cell.ensure(sizeof(int32_t) * (size_t)std::max(f->n, 1)));
+    YGZ_HIP(launch_match_cells(f->kps.as<ygzfe_kp>(), f->n, bounds->min_x, bounds->min_y, f->inv_w, f->inv_h,
+                               f->cell.as<int32_t>(), f->stream));
+    YGZ_HIP(hipStreamSynchronize(f->stream));
+    return YGZFE_OK;
+}
+
+// Run one search problem: the job's host-side arrays are staged into one H2D
+// copy; outputs come back in one D2H copy.
+struct MatchCall {
+    ygzfe_match_frame *train;
+    std::vector<ygzfe_match_query> q;
+    const uint8_t *qdesc_host = nullptr;  // [n_qdesc][32] (host) or
+    const uint8_t *qdesc_dev = nullptr;   // device descriptors (INIT / BoW: a match frame's)
+    int n_qdesc = 0;
+    std::vector<int32_t> qid, cand_ptr;
+    const int32_t *cand_host = nullptr;
+    int n_cand = 0;
+    const uint8_t *blocked_host = nullptr;
+    int mode = 0, th_dist = 100, check_ori = 0;
+    float nnratio = 0.6f;
+    // outputs
+    int32_t *train_out = nullptr, *query_out = nullptr;
+    int nmatches = 0;
+};
+
+int run_match(MatchCall &c) {
+    ygzfe_match_frame *f = c.train;
+    const int nq = (int)c.q.size(), n = f->n;
+    if (n > 65535) { set_error("match frame holds %d keypoints (<= 65535 supported)", n); return YGZFE_EINVAL; }
+    if (c.mode == YGZFE_MATCH_INIT && (n > 16384 || nq > 32767)) {
+        set_error("SearchForInitialization: %d x %d keypoints exceed 32767 x 16384", nq, n);
+        return YGZFE_EINVAL;
+    }
+    YGZ_TRY(ensure_device(f->device));
+    hipStream_t st = f->stream;
+    // device input layout
+    Arena ai;
+    const size_t o_job = ai.take(sizeof(MatchJob));
+    const size_t o_q = ai.take(sizeof(ygzfe_match_query) * (size_t)std::max(nq, 1));
+    const size_t o_qd = c.qdesc_host ? ai.take((size_t)32 * std::max(c.n_qdesc, 1)) : 0;
+    const size_t o_qid = c.qid.empty() ? 0 : ai.take(sizeof(int32_t) * c.qid.size());
+    const size_t o_cp = c.cand_ptr.empty() ? 0 : ai.take(sizeof(int32_t) * c.cand_ptr.size());
+    const size_t o_c = c.cand_host ? ai.take(sizeof(int32_t) * (size_t)std::max(c.n_cand, 1)) : 0;
+    const size_t o_bl = c.blocked_host ? ai.take((size_t)std::max(n, 1)) : 0;
+    // device outputs / scratch
+    Arena ao;
+    const size_t o_tout = ao.take(sizeof(int32_t) * (size_t)std::max(n, 1));
+    const size_t o_qout = ao.take(sizeof(int32_t) * (size_t)std::max(nq, 1));
+    const size_t o_nm = ao.take(2 * sizeof(int32_t));
+    const size_t out_bytes = ao.off;
+    const size_t o_topk = ao.take(sizeof(uint64_t) * kMatchTopK * (size_t)std::max(nq, 1));
+    const size_t o_ncand = ao.take(sizeof(int32_t) * (size_t)std::max(nq, 1));
+    const size_t o_push = ao.take(sizeof(int32_t) * (size_t)std::max(nq, 1));
+    YGZ_TRY(f->in.ensure(ai.off));
+    YGZ_TRY(f->out.ensure(ao.off));
+    uint8_t *din = f->in.as<uint8_t>(), *dout = f->out.as<uint8_t>();
+    f->hin.resize(ai.off);
+    uint8_t *h = f->hin.data();
+    MatchJob J;
+    memset(&J, 0, sizeof(J));
+    J.kps = f->kps.as<ygzfe_kp>();
+    J.desc = f->desc.as<uint8_t>();
+    J.u_right = f->has_uright ? f->uright.as<float>() : nullptr;
+    J.cell = f->cell.as<int32_t>();
+    J.n_train = n;
+    J.min_x = f->bounds.min_x;
+    J.min_y = f->bounds.min_y;
+    J.inv_w = f->inv_w;
+    J.inv_h = f->inv_h;
+    J.q = reinterpret_cast<const ygzfe_match_query *>(din + o_q);
+    J.qdesc = c.qdesc_host ? din + o_qd : c.qdesc_dev;
+    J.qid = c.qid.empty() ? nullptr : reinterpret_cast<const int32_t *>(din + o_qid);
+    J.nq = nq;
+    J.cand_ptr = c.cand_ptr.empty() ? nullptr : reinterpret_cast<const int32_t *>(din + o_cp);
+    J.cand = c.cand_host ? reinterpret_cast<const int32_t *>(din + o_c) : nullptr;
+    J.blocked0 = c.blocked_host ? din + o_bl : nullptr;
+    J.topk = reinterpret_cast<uint64_t *>(dout + o_topk);
+    J.ncand = reinterpret_cast<int32_t *>(dout + o_ncand);
+    J.train_out = reinterpret_cast<int32_t *>(dout + o_tout);
+    J.query_out = reinterpret_cast<int32_t *>(dout + o_qout);
+    J.pushes = reinterpret_cast<int32_t *>(dout + o_push);
+    J.nmatches = reinterpret_cast<int32_t *>(dout + o_nm);
+    memcpy(h + o_job, &J, sizeof(J));
+    if (nq) memcpy(h + o_q, c.q.data(), sizeof(ygzfe_match_query) * nq);
+    if (c.qdesc_host && c.n_qdesc) memcpy(h + o_qd, c.qdesc_host, (size_t)32 * c.n_qdesc);
+    if (!c.qid.empty()) memcpy(h + o_qid, c.qid.data(), sizeof(int32_t) * c.qid.size());
+    if (!c.cand_ptr.empty()) memcpy(h + o_cp, c.cand_ptr.data(), sizeof(int32_t) * c.cand_ptr.size());
+    if (c.cand_host && c.n_cand) memcpy(h + o_c, c.cand_host, sizeof(int32_t) * c.n_cand);
+    if (c.blocked_host && n) memcpy(h + o_bl, c.blocked_host, (size_t)n);
+    YGZ_HIP(hipMemcpyAsync(din, h, ai.off, hipMemcpyHostToDevice, st));
+    YGZ_HIP(launch_match(reinterpret_cast<const MatchJob *>(din + o_job), 1, nq, n, c.mode, c.th_dist, c.check_ori,
+                         c.nnratio, st));
+    f->hout.resize(out_bytes);
+    YGZ_HIP(hipMemcpyAsync(f->hout.data(), dout, out_bytes, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipStreamSynchronize(st));
+    if (c.train_out && n) memcpy(c.train_out, f->hout.data() + o_tout, sizeof(int32_t) * n);
+    if (c.query_out && nq) memcpy(c.query_out, f->hout.data() + o_qout, sizeof(int32_t) * nq);
+    memcpy(&c.nmatches, f->hout.data() + o_nm, sizeof(int32_t));
+    memcpy(&f->last_rescans, f->hout.data() + o_nm + 4, sizeof(int32_t));
+    return YGZFE_OK;
+}
+
+}  // namespace
+
+extern "C" int ygzfe_match_frame_create(int device, ygzfe_match_frame **out) {
+    if (!out) { set_error("null out"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(device));
+    std::unique_ptr<ygzfe_match_frame> f(new ygzfe_match_frame());
+    f->device = device;
+    YGZ_HIP(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking));
+    *out = f.release();
+    return YGZFE_OK;
+}
+
+extern "C" void ygzfe_match_frame_destroy(ygzfe_match_frame *f) {
+    if (!f) return;
+    (void)hipSetDevice(f->device);
+    if (f->stream) (void)hipStreamSynchronize(f->stream), (void)hipStreamDestroy(f->stream);
+    delete f;
+}
+
+extern "C" int ygzfe_match_frame_stats(const ygzfe_match_frame *f, int *rescans) {
+    if (!f || !rescans) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    *rescans = f->last_rescans;
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_match_frame_set(ygzfe_match_frame *f, const ygzfe_kp *kps, const uint8_t *desc, int n,
+                                     const float *u_right, const ygzfe_bounds *bounds) {
+    if (!f || !bounds || n < 0 || n > 65535 || (n > 0 && (!kps || !desc))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (!(bounds->max_x > bounds->min_x) || !(bounds->max_y > bounds->min_y)) {
+        set_error("empty image bounds");
+        return YGZFE_EINVAL;
+    }
+    YGZ_TRY(ensure_device(f->device));
+    f->n = n;
+    f->host_kps.assign(kps, kps + n);
+    YGZ_TRY(f->kps.ensure(sizeof(ygzfe_kp) * (size_t)std::max(n, 1)));
+    YGZ_TRY(f->desc.ensure((size_t)32 * std::max(n, 1)));
+    if (n) {
+        YGZ_HIP(hipMemcpyAsync(f->kps.p, kps, sizeof(ygzfe_kp) * n, hipMemcpyHostToDevice, f->stream));
+        YGZ_HIP(hipMemcpyAsync(f->desc.p, desc, (size_t)32 * n, hipMemcpyHostToDevice, f->stream));
+    }
+    f->has_uright = u_right != nullptr;
+    if (u_right) {
+        YGZ_TRY(f->uright.ensure(sizeof(float) * (size_t)std::max(n, 1)));
+        if (n) YGZ_HIP(hipMemcpyAsync(f->uright.p, u_right, sizeof(float) * n, hipMemcpyHostToDevice, f->stream));
+    }
+    return match_frame_finish(f, bounds);
+}
+
+extern "C" int ygzfe_match_frame_from_batch(ygzfe_match_frame *f, ygzfe_batch *b, int frame,
+                                            const ygzfe_bounds *bounds) {
+    if (!f || !b || !bounds || frame < 0 || frame >= b->maxF) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    if (f->device != b->device) { set_error("match frame and batch on different devices"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(f->device));
+    const Plan &P = b->plan->hp();
+    YGZ_HIP(hipDeviceSynchronize());  // the batch's extraction may run on caller streams
+    int n = 0;
+    YGZ_HIP(hipMemcpy(&n, b->ws.counts.as<int>() + frame, sizeof(int), hipMemcpyDeviceToHost));
+    f->n = n;
+    YGZ_TRY(f->kps.ensure(sizeof(ygzfe_kp) * (size_t)std::max(n, 1)));
+    YGZ_TRY(f->desc.ensure((size_t)32 * std::max(n, 1)));
+    f->host_kps.resize(n);
+    if (n) {
+        YGZ_HIP(hipMemcpyAsync(f->kps.p, b->ws.kps.as<ygzfe_kp>() + (size_t)frame * P.kp_cap, sizeof(ygzfe_kp) * n,
+                               hipMemcpyDeviceToDevice, f->stream));
+        YGZ_HIP(hipMemcpyAsync(f->desc.p, b->ws.desc.as<uint8_t>() + (size_t)frame * P.kp_cap * 32, (size_t)32 * n,
+                               hipMemcpyDeviceToDevice, f->stream));
+        YGZ_HIP(hipMemcpyAsync(f->host_kps.data(), f->kps.p, sizeof(ygzfe_kp) * n, hipMemcpyDeviceToHost, f->stream));
+    }
+    f->has_uright = false;
+    return match_frame_finish(f, bounds);
+}
+
+extern "C" int ygzfe_search_projection_best(ygzfe_match_frame *cur, const ygzfe_match_query *q, const uint8_t *q_desc,
+                                            int nq, const uint8_t *train_blocked, int th_dist, int check_ori,
+                                            int32_t *train_match, int *nmatches) {
+    if (!cur || nq < 0 || (nq > 0 && (!q || !q_desc)) || !train_match || !nmatches) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    MatchCall c;
+    c.train = cur;
+    c.q.assign(q, q + nq);
+    c.qdesc_host = q_desc;
+    c.n_qdesc = nq;
+    c.blocked_host = train_blocked;
+    c.mode = YGZFE_MATCH_BEST;
+    c.th_dist = th_dist;
+    c.check_ori = check_ori;
+    c.train_out = train_match;
+    YGZ_TRY(run_match(c));
+    *nmatches = c.nmatches;
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_search_projection_ratio(ygzfe_match_frame *F, const ygzfe_match_query *q, const uint8_t *q_desc,
+                                             int nq, const uint8_t *train_blocked, float nnratio, int32_t *train_match,
+                                             int *nmatches) {
+    if (!F || nq < 0 || (nq > 0 && (!q || !q_desc)) || !train_match || !nmatches) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    MatchCall c;
+    c.train = F;
+    c.q.assign(q, q + nq);
+    c.qdesc_host = q_desc;
+    c.n_qdesc = nq;
+    c.blocked_host = train_blocked;
+    c.mode = YGZFE_MATCH_RATIO;
+    c.nnratio = nnratio;
+    c.train_out = train_match;
+    YGZ_TRY(run_match(c));
+    *nmatches = c.nmatches;
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_search_for_initialization(ygzfe_match_frame *F1, ygzfe_match_frame *F2, float *prev_matched,
+                                               int window_size, float nnratio, int check_ori, int32_t *matches12,
+                                               int *nmatches) {
+    if (!F1 || !F2 || (F1->n > 0 && (!prev_matched || !matches12)) || !nmatches) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (F1->device != F2->device) { set_error("frames on different devices"); return YGZFE_EINVAL; }
+    // ORBmatcher.cc:388-398: queries = F1's keypoints, level-0 only, window at vbPrevMatched
+    MatchCall c;
+    c.train = F2;
+    c.q.resize(F1->n);
+    for (int i = 0; i < F1->n; i++) {
+        ygzfe_match_query &Q = c.q[i];
+        const ygzfe_kp &kp = F1->host_kps[i];
+        Q.u = prev_matched[2 * i];
+        Q.v = prev_matched[2 * i + 1];
+        Q.radius = (float)window_size;
+        Q.u_right = 0.f;
+        Q.min_level = kp.octave;
+        Q.max_level = kp.octave;
+        Q.angle = kp.angle;
+        Q.flags = kp.octave > 0 ? 0 : YGZFE_MQ_VALID;
+    }
+    c.qdesc_dev = F1->desc.as<uint8_t>();
+    c.mode = YGZFE_MATCH_INIT;
+    c.nnratio = nnratio;
+    c.check_ori = check_ori;
+    c.query_out = matches12;
+    YGZ_TRY(run_match(c));
+    *nmatches = c.nmatches;
+    // :472-475 update prev matched
+    for (int i = 0; i < F1->n; i++)
+        if (matches12[i] >= 0) {
+            prev_matched[2 * i] = F2->host_kps[matches12[i]].x;
+            prev_matched[2 * i + 1] = F2->host_kps[matches12[i]].y;
+        }
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_search_by_bow(ygzfe_match_frame *kf, ygzfe_match_frame *F, const uint8_t *kf_usable,
+                                   int n_kf_nodes, const int32_t *kf_nodes, const int32_t *kf_ptr,
+                                   const int32_t *kf_feats, int n_f_nodes, const int32_t *f_nodes,
+                                   const int32_t *f_ptr, const int32_t *f_feats, float nnratio, int check_ori,
+                                   int32_t *f_match, int *nmatches) {
+    if (!kf || !F || !kf_usable || !f_match || !nmatches || n_kf_nodes < 0 || n_f_nodes < 0 ||
+        (n_kf_nodes > 0 && (!kf_nodes || !kf_ptr || !kf_feats)) || (n_f_nodes > 0 && (!f_nodes || !f_ptr || !f_feats))) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (kf->device != F->device) { set_error("frames on different devices"); return YGZFE_EINVAL; }
+    // ORBmatcher.cc:170-243: walk the two node-sorted FeatureVectors; every KF feature of
+    // a shared node is one query over that node's F features
+    MatchCall c;
+    c.train = F;
+    int KFit = 0, Fit = 0;
+    while (KFit < n_kf_nodes && Fit < n_f_nodes) {
+        if (kf_nodes[KFit] == f_nodes[Fit]) {
+            for (int a = kf_ptr[KFit]; a < kf_ptr[KFit + 1]; a++) {
+                const int idx = kf_feats[a];
+                if (idx < 0 || idx >= kf->n) { set_error("KF feature index %d out of range", idx); return YGZFE_EINVAL; }
+                ygzfe_match_query Q;
+                memset(&Q, 0, sizeof(Q));
+                Q.angle = kf->host_kps[idx].angle;
+                Q.min_level = Q.max_level = -1;
+                Q.flags = kf_usable[idx] ? YGZFE_MQ_VALID : 0;
+                c.q.push_back(Q);
+                c.qid.push_back(idx);
+                c.cand_ptr.push_back(f_ptr[Fit]);
+                c.cand_ptr.push_back(f_ptr[Fit + 1]);
+            }
+            KFit++;
+            Fit++;
+        } else if (kf_nodes[KFit] < f_nodes[Fit]) {
+            KFit = (int)(std::lower_bound(kf_nodes + KFit, kf_nodes + n_kf_nodes, f_nodes[Fit]) - kf_nodes);
+        } else {
+            Fit = (int)(std::lower_bound(f_nodes + Fit, f_nodes + n_f_nodes, kf_nodes[KFit]) - f_nodes);
+        }
+    }
+    const int n_cand = n_f_nodes > 0 ? f_ptr[n_f_nodes] : 0;
+    for (int i = 0; i < n_cand; i++)
+        if (f_feats[i] < 0 || f_feats[i] >= F->n) { set_error("F feature index %d out of range", f_feats[i]); return YGZFE_EINVAL; }
+    c.cand_host = f_feats;
+    c.n_cand = n_cand;
+    if (c.cand_ptr.empty()) c.cand_ptr.assign(2, 0);  // BoW mode even with no query
+    c.qdesc_dev = kf->desc.as<uint8_t>();
+    c.mode = YGZFE_MATCH_BOW;
+    c.nnratio = nnratio;
+    c.check_ori = check_ori;
+    c.train_out = f_match;
+    YGZ_TRY(run_match(c));
+    *nmatches = c.nmatches;
     return YGZFE_OK;
 }

@@ -44,6 +44,36 @@ hipError_t launch_hamming_best2_pairs(const uint8_t *desc, const int32_t *counts
 hipError_t launch_hamming_csr(const uint8_t *q, int nq, const uint8_t *t, const int32_t *row_ptr,
                               const int32_t *cand, int32_t *dist, hipStream_t st);
 
+// match.hip: one ORBmatcher search problem (device pointers)
+struct MatchJob {
+    // the searched frame
+    const ygzfe_kp *kps;
+    const uint8_t *desc;
+    const float *u_right;       // mvuRight or null
+    const int32_t *cell;        // PosInGrid: ix << 8 | iy, -1 outside (k_match_cells)
+    int n_train;
+    float min_x, min_y, inv_w, inv_h;
+    // queries in the reference's order
+    const ygzfe_match_query *q;
+    const uint8_t *qdesc;       // descriptor of query q at qdesc + 32 * (qid ? qid[q] : q)
+    const int32_t *qid;         // reported query id (BoW: the KF keypoint index) or null
+    int nq;
+    const int32_t *cand_ptr;    // BoW: query q's candidates cand[cand_ptr[2q] .. cand_ptr[2q+1]); null = window
+    const int32_t *cand;
+    const uint8_t *blocked0;    // initial skip state per train keypoint, or null
+    // scratch / outputs
+    uint64_t *topk;             // [nq][kTopK]
+    int32_t *ncand;             // [nq]
+    int32_t *train_out;         // [n_train]
+    int32_t *query_out;         // INIT: vnMatches12 [nq]
+    int32_t *pushes;            // [nq] rotation-histogram pushes
+    int32_t *nmatches;          // [1]
+};
+hipError_t launch_match_cells(const ygzfe_kp *kps, int n, float min_x, float min_y, float inv_w, float inv_h,
+                              int32_t *cell, hipStream_t st);
+hipError_t launch_match(const MatchJob *d_jobs, int njobs, int max_q, int max_train, int mode, int th_dist,
+                        int check_ori, float nnratio, hipStream_t st);
+
 // align.hip
 struct AlignLevels {
     int w[kMaxLevels], h[kMaxLevels];

@@ -1,0 +1,406 @@
+// match.hip — the tracking-path ORBmatcher searches (ORBmatcher.cc) on gfx950.
+//
+//   SearchByProjection(CurrentFrame, LastFrame, th, bMono, checkLevel)  :1218-1350  mode BEST
+//   SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)  :1352-1469  mode BEST
+//   SearchByProjection(F, vpMapPoints, th, checkLevel)                 :43-126     mode RATIO
+//   SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, ws)    :375-478    mode INIT
+//   SearchByBoW(pKF, F, vpMapPointMatches)                             :155-263    mode BOW
+//   ComputeThreeMaxima                                                 :1471-1502
+//
+// The reference runs one query after another, and a query's candidates
+// depend on the assignments of the queries before it (a keypoint matched to
+// a MapPoint with observations is skipped later; SearchForInitialization
+// skips keypoints already matched at an equal or smaller distance;
+// SearchByBoW skips matched keypoints).  The work is split in two passes:
+//
+//  k_match_topk   one wave per query, all queries of all problems at once:
+//                 the GetFeaturesInArea window (Frame.cc:424-481: the grid
+//                 cell range, level filter, |dx| < r, |dy| < r; the stereo
+//                 test of the projection searches) or the BoW node's feature
+//                 list, every candidate's Hamming distance, and the K
+//                 smallest (distance, candidate-order) keys — the order in
+//                 which the reference's strict-< scan would rank them, so the
+//                 first entry is its best, the next its second.
+//  k_match_replay one wave per problem: the queries in the reference's order
+//                 against the sequential state in LDS; per query the K
+//                 entries' skip tests run in K lanes and a ballot gives the
+//                 first / second surviving entry.  When the skips exhaust the
+//                 K entries of a longer candidate list the wave re-scans that
+//                 query's whole window under the current state, so the
+//                 result never depends on K.  Then the rotation histogram
+//                 votes (ComputeThreeMaxima) and the removals.
+#include "kernels.hpp"
+
+namespace ygzfe {
+
+constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS / ROWS (Frame.h:27-28)
+constexpr int kTopK = 8;
+constexpr int kHisto = 30;                       // ORBmatcher::HISTO_LENGTH (ORBmatcher.cc:38)
+
+// Frame::PosInGrid (Frame.cc:483-493): std::round(float), cell -1 when outside
+__global__ __launch_bounds__(256) void k_match_cells(const ygzfe_kp *__restrict__ kps, int n, float min_x,
+                                                     float min_y, float inv_w, float inv_h,
+                                                     int32_t *__restrict__ cell) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int px = (int)__builtin_roundf((kps[i].x - min_x) * inv_w);
+    const int py = (int)__builtin_roundf((kps[i].y - min_y) * inv_h);
+    cell[i] = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : (px << 8) | py;
+}
+
+hipError_t launch_match_cells(const ygzfe_kp *kps, int n, float min_x, float min_y, float inv_w, float inv_h,
+                              int32_t *cell, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_match_cells, dim3((n + 255) / 256), dim3(256), 0, st, kps, n, min_x, min_y, inv_w, inv_h,
+                       cell);
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t o = shfl_xor_u64(v, m);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int hamming32(const uint32_t q[8], const uint8_t *d) {
+    const uint4 a = reinterpret_cast<const uint4 *>(d)[0], b = reinterpret_cast<const uint4 *>(d)[1];
+    return __popc(q[0] ^ a.x) + __popc(q[1] ^ a.y) + __popc(q[2] ^ a.z) + __popc(q[3] ^ a.w) + __popc(q[4] ^ b.x) +
+           __popc(q[5] ^ b.y) + __popc(q[6] ^ b.z) + __popc(q[7] ^ b.w);
+}
+
+// The window of GetFeaturesInArea (Frame.cc:429-449) in the reference's float arithmetic.
+struct Window {
+    int cx0, cx1, cy0, cy1;  // cell range (empty when cx0 > cx1)
+    bool check_levels;
+    int min_level, max_level;
+    float x, y, r;
+};
+
+__device__ __forceinline__ Window make_window(const MatchJob &J, const ygzfe_match_query &q) {
+    Window w;
+    w.x = q.u;
+    w.y = q.v;
+    w.r = q.radius;
+    w.min_level = q.min_level;
+    w.max_level = q.max_level;
+    w.check_levels = (q.min_level > 0) || (q.max_level >= 0);
+    const float inv_w = J.inv_w, inv_h = J.inv_h;
+    w.cx0 = max(0, (int)floorf((q.u - J.min_x - q.radius) * inv_w));
+    w.cx1 = min(kGridCols - 1, (int)ceilf((q.u - J.min_x + q.radius) * inv_w));
+    w.cy0 = max(0, (int)floorf((q.v - J.min_y - q.radius) * inv_h));
+    w.cy1 = min(kGridRows - 1, (int)ceilf((q.v - J.min_y + q.radius) * inv_h));
+    if (w.cx0 >= kGridCols || w.cx1 < 0 || w.cy0 >= kGridRows || w.cy1 < 0) w.cx0 = 1, w.cx1 = 0;
+    return w;
+}
+
+// Is train keypoint j in the query's candidate list (window + level + stereo)?
+// Returns its candidate-order key (cell-major, then index) or ~0.
+__device__ __forceinline__ uint32_t window_order(const MatchJob &J, const Window &w, const ygzfe_match_query &q,
+                                                 int j) {
+    const int c = J.cell[j];
+    if (c < 0) return ~0u;
+    const int ix = c >> 8, iy = c & 0xFF;
+    if (ix < w.cx0 || ix > w.cx1 || iy < w.cy0 || iy > w.cy1) return ~0u;
+    const ygzfe_kp &kp = J.kps[j];
+    if (w.check_levels) {
+        if (kp.octave < w.min_level) return ~0u;
+        if (w.max_level >= 0 && kp.octave > w.max_level) return ~0u;
+    }
+    const float dx = kp.x - w.x, dy = kp.y - w.y;
+    if (!(fabsf(dx) < w.r && fabsf(dy) < w.r)) return ~0u;
+    if ((q.flags & YGZFE_MQ_STEREO) && J.u_right && J.u_right[j] > 0) {
+        const float er = fabsf(q.u_right - J.u_right[j]);
+        if (er > q.radius) return ~0u;
+    }
+    return ((uint32_t)(ix * kGridRows + iy) << 16) | (uint32_t)j;  // GetFeaturesInArea order
+}
+
+// key = dist << 52 | order << 20 | train index
+__device__ __forceinline__ uint64_t make_key(int dist, uint32_t order, int j) {
+    return ((uint64_t)dist << 52) | ((uint64_t)order << 20) | (uint64_t)j;
+}
+
+template <class Pred>
+__device__ __forceinline__ void scan_query(const MatchJob &J, int q, const ygzfe_match_query &Q, const uint32_t qd[8],
+                                           Pred skip, uint64_t L[kTopK], int &count) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < kTopK; k++) L[k] = ~0ull;
+    count = 0;
+    auto consider = [&](int j, uint32_t order) {
+        const int dist = hamming32(qd, J.desc + (size_t)j * 32);
+        if (skip(j, dist)) return;
+        count++;
+        uint64_t key = make_key(dist, order, j);
+#pragma unroll
+        for (int k = 0; k < kTopK; k++) {  // sorted insertion, branch-free
+            const uint64_t lo = key < L[k] ? key : L[k], hi = key < L[k] ? L[k] : key;
+            L[k] = lo;
+            key = hi;
+        }
+    };
+    if (J.cand_ptr) {  // BoW node list: order = position in the node's feature vector
+        const int b = J.cand_ptr[2 * q], e = J.cand_ptr[2 * q + 1];
+        for (int p = b + lane; p < e; p += 64) consider(J.cand[p], (uint32_t)(p - b));
+    } else {
+        const Window w = make_window(J, Q);
+        if (w.cx0 <= w.cx1)
+            for (int j = lane; j < J.n_train; j += 64) {
+                const uint32_t o = window_order(J, w, Q, j);
+                if (o != ~0u) consider(j, o);
+            }
+    }
+}
+
+__device__ __forceinline__ void load_qdesc(const MatchJob &J, int q, uint32_t qd[8]) {
+    const int id = J.qid ? J.qid[q] : q;
+    const uint4 *p = reinterpret_cast<const uint4 *>(J.qdesc + (size_t)id * 32);
+    const uint4 a = p[0], b = p[1];
+    qd[0] = a.x; qd[1] = a.y; qd[2] = a.z; qd[3] = a.w;
+    qd[4] = b.x; qd[5] = b.y; qd[6] = b.z; qd[7] = b.w;
+}
+
+// wave-merge of the lanes' sorted lists: the K smallest keys, ascending, in lanes 0..K-1
+__device__ __forceinline__ uint64_t merge_topk(uint64_t L[kTopK]) {
+    const int lane = threadIdx.x & 63;
+    uint64_t mine = ~0ull;
+#pragma unroll
+    for (int e = 0; e < kTopK; e++) {
+        const uint64_t m = wave_min_u64(L[0]);
+        if (lane == e) mine = m;
+        if (L[0] == m && m != ~0ull) {  // keys are unique: one lane pops
+#pragma unroll
+            for (int k = 0; k + 1 < kTopK; k++) L[k] = L[k + 1];
+            L[kTopK - 1] = ~0ull;
+        }
+    }
+    return mine;
+}
+
+__global__ __launch_bounds__(256) void k_match_topk(const MatchJob *__restrict__ jobs, int max_q) {
+    const MatchJob &J = jobs[blockIdx.y];
+    const int q = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (q >= J.nq) return;
+    const int lane = threadIdx.x & 63;
+    const ygzfe_match_query Q = J.q[q];
+    if (!(Q.flags & YGZFE_MQ_VALID)) {
+        if (lane == 0) J.ncand[q] = 0;
+        return;
+    }
+    uint32_t qd[8];
+    load_qdesc(J, q, qd);
+    uint64_t L[kTopK];
+    int count;
+    scan_query(J, q, Q, qd, [](int, int) { return false; }, L, count);
+    count = wave_sum_i(count);
+    const uint64_t mine = merge_topk(L);
+    if (lane < kTopK) J.topk[(size_t)q * kTopK + lane] = mine;
+    if (lane == 0) J.ncand[q] = count;
+}
+
+// ComputeThreeMaxima (ORBmatcher.cc:1471-1502)
+__device__ __forceinline__ void three_maxima(const int *h, int &ind1, int &ind2, int &ind3) {
+    int max1 = 0, max2 = 0, max3 = 0;
+    ind1 = ind2 = ind3 = -1;
+    for (int i = 0; i < kHisto; i++) {
+        const int s = h[i];
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) {
+        ind2 = -1;
+        ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+        ind3 = -1;
+    }
+}
+
+// the rotation bin (ORBmatcher.cc:1318-1323): float rot, std::round(float)
+__device__ __forceinline__ int rot_bin(float aq, float at) {
+    const float factor = 1.0f / kHisto;
+    float rot = aq - at;
+    if (rot < 0.0f) rot += 360.0f;
+    int bin = (int)__builtin_roundf(rot * factor);
+    if (bin == kHisto) bin = 0;
+    return min(max(bin, 0), 63);
+}
+
+__global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict__ jobs, int mode, int th_dist,
+                                                     int check_ori, float nnratio) {
+    extern __shared__ uint8_t lds[];
+    const MatchJob &J = jobs[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int n = J.n_train;
+    __shared__ int rot_count[64];
+    uint8_t *blocked = lds;                                            // [n]
+    uint16_t *mdist = reinterpret_cast<uint16_t *>(lds + ((n + 15) & ~15));  // INIT: vMatchedDistance (0xFFFF = INT_MAX)
+    int16_t *m21 = reinterpret_cast<int16_t *>(mdist + ((n + 7) & ~7));      // INIT: vnMatches21
+    for (int j = lane; j < n; j += 64) {
+        blocked[j] = J.blocked0 ? J.blocked0[j] : 0;
+        if (J.train_out) J.train_out[j] = -1;
+        if (mode == YGZFE_MATCH_INIT) {
+            mdist[j] = 0xFFFF;
+            m21[j] = -1;
+        }
+    }
+    if (mode == YGZFE_MATCH_INIT)
+        for (int i = lane; i < J.nq; i += 64) J.query_out[i] = -1;
+    rot_count[lane] = 0;
+    __syncthreads();
+    int nmatches = 0, npush = 0, rescans = 0;
+    const int need = mode == YGZFE_MATCH_BEST ? 1 : 2;
+    // skip test of the reference's scan against the current state
+    auto skip = [&](int j, int dist) -> bool {
+        if (mode == YGZFE_MATCH_INIT) return (int)mdist[j] <= dist;  // vMatchedDistance[i2] <= dist (0xFFFF: INT_MAX)
+        return blocked[j] != 0;
+    };
+    // prefetch of the next query's entries
+    uint64_t E = ~0ull;
+    int cnt = 0;
+    ygzfe_match_query Q;
+    if (J.nq > 0) {
+        Q = J.q[0];
+        cnt = J.ncand[0];
+        if (lane < kTopK) E = J.topk[lane];
+    }
+    for (int q = 0; q < J.nq; q++) {
+        const ygzfe_match_query cq = Q;
+        const uint64_t cE = E;
+        const int ccnt = cnt;
+        if (q + 1 < J.nq) {
+            Q = J.q[q + 1];
+            cnt = J.ncand[q + 1];
+            E = lane < kTopK ? J.topk[(size_t)(q + 1) * kTopK + lane] : ~0ull;
+        }
+        if (!(cq.flags & YGZFE_MQ_VALID) || ccnt == 0) continue;
+        const int nk = min(ccnt, kTopK);
+        int dist_l = (int)(cE >> 52), j_l = (int)(cE & 0xFFFFF);
+        const bool ok = lane < nk && !skip(j_l, dist_l);
+        const uint64_t bal = __ballot(ok);
+        uint64_t best = ~0ull, second = ~0ull;
+        if (__popcll(bal) >= need || ccnt <= kTopK) {
+            if (bal) {
+                const int b0 = __builtin_ctzll(bal);
+                best = __shfl(cE, b0, 64);
+                const uint64_t rest = bal & (bal - 1);
+                if (rest) second = __shfl(cE, __builtin_ctzll(rest), 64);
+            }
+        } else {  // the skips used up the K entries: re-scan this query under the current state
+            rescans++;
+            uint32_t qd[8];
+            load_qdesc(J, q, qd);
+            uint64_t L[kTopK];
+            int c2;
+            scan_query(J, q, cq, qd, skip, L, c2);
+            best = wave_min_u64(L[0]);
+            if (L[0] == best) L[0] = L[1];
+            second = wave_min_u64(L[0]);
+        }
+        const bool has1 = best != ~0ull, has2 = second != ~0ull;
+        const int bj = (int)(best & 0xFFFFF), bd = has1 ? (int)(best >> 52) : 256;
+        const int sj = (int)(second & 0xFFFFF), sdist = has2 ? (int)(second >> 52) : 256;
+        const int id = J.qid ? J.qid[q] : q;
+        int push_id = -1;
+        if (mode == YGZFE_MATCH_BEST) {
+            if (has1 && bd <= th_dist) {
+                if (lane == 0) J.train_out[bj] = q;
+                blocked[bj] = (cq.flags & YGZFE_MQ_BLOCKS) ? 1 : 0;
+                nmatches++;
+                push_id = bj;
+            }
+        } else if (mode == YGZFE_MATCH_RATIO) {
+            const int bl = has1 ? J.kps[bj].octave : -1, sl = has2 ? J.kps[sj].octave : -1;
+            if (has1 && bd <= 100 && !(bl == sl && bd > nnratio * sdist)) {
+                if (lane == 0) J.train_out[bj] = q;
+                blocked[bj] = (cq.flags & YGZFE_MQ_BLOCKS) ? 1 : 0;
+                nmatches++;
+            }
+        } else if (mode == YGZFE_MATCH_INIT) {
+            const int bdi = has1 ? bd : 0x7FFFFFFF, sdi = has2 ? sdist : 0x7FFFFFFF;
+            if (has1 && bdi <= 50 && bdi < (float)sdi * nnratio) {
+                const int old = m21[bj];
+                if (old >= 0) {
+                    if (lane == 0) J.query_out[old] = -1;
+                    nmatches--;
+                }
+                if (lane == 0) J.query_out[q] = bj;
+                m21[bj] = (int16_t)q;
+                mdist[bj] = (uint16_t)bdi;
+                nmatches++;
+                push_id = q;
+            }
+        } else {  // BOW
+            if (has1 && bd <= 50 && (float)bd < nnratio * (float)sdist) {
+                if (lane == 0) J.train_out[bj] = id;
+                blocked[bj] = 1;
+                nmatches++;
+                push_id = bj;
+            }
+        }
+        if (push_id >= 0 && check_ori && mode != YGZFE_MATCH_RATIO) {
+            const int bin = rot_bin(cq.angle, J.kps[bj].angle);
+            if (lane == 0) {
+                rot_count[bin]++;
+                J.pushes[npush] = (bin << 24) | push_id;
+            }
+            npush++;
+        }
+        wave_lds_order();  // the LDS state updates precede the next query's reads (one wave: DS ops in order)
+    }
+    if (check_ori && mode != YGZFE_MATCH_RATIO && npush > 0) {
+        __threadfence_block();
+        __syncthreads();
+        int i1, i2, i3;
+        three_maxima(rot_count, i1, i2, i3);
+        int removed = 0;
+        for (int p = lane; p < npush; p += 64) {
+            const int v = J.pushes[p], bin = v >> 24, pid = v & 0xFFFFFF;
+            if (bin == i1 || bin == i2 || bin == i3) continue;
+            if (mode == YGZFE_MATCH_BEST) {
+                J.train_out[pid] = -2;
+                removed++;
+            } else if (mode == YGZFE_MATCH_BOW) {
+                J.train_out[pid] = -1;
+                removed++;
+            } else if (J.query_out[pid] >= 0) {  // INIT
+                J.query_out[pid] = -1;
+                removed++;
+            }
+        }
+        nmatches -= wave_sum_i(removed);
+    }
+    if (lane == 0) {
+        J.nmatches[0] = nmatches;
+        J.nmatches[1] = rescans;  // diagnostics: queries whose top-K list the skips exhausted
+    }
+}
+
+hipError_t launch_match(const MatchJob *d_jobs, int njobs, int max_q, int max_train, int mode, int th_dist,
+                        int check_ori, float nnratio, hipStream_t st) {
+    if (njobs <= 0) return hipSuccess;
+    if (max_q > 0)
+        hipLaunchKernelGGL(k_match_topk, dim3((max_q + 3) / 4, njobs), dim3(256), 0, st, d_jobs, max_q);
+    const size_t lds = (size_t)((max_train + 15) & ~15) +
+                       (mode == YGZFE_MATCH_INIT ? 2 * (size_t)((max_train + 7) & ~7) * 2 : 0) + 64;
+    hipLaunchKernelGGL(k_match_replay, dim3(njobs), dim3(64), lds, st, d_jobs, mode, th_dist, check_ori, nnratio);
+    return hipGetLastError();
+}
+
+}  // namespace ygzfe

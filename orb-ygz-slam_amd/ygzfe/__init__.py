@@ -317,6 +317,101 @@ class ORBmatcher:
         return out[:len(cand)]
 
 
+MATCH_QUERY_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("radius", "<f4"), ("u_right", "<f4"),
+                              ("min_level", "<i4"), ("max_level", "<i4"), ("angle", "<f4"), ("flags", "<i4")])
+MQ_VALID, MQ_BLOCKS, MQ_STEREO = 1, 2, 4
+
+
+class Bounds(C.Structure):
+    """Frame::mnMinX / mnMaxX / mnMinY / mnMaxY (Frame.cc:501-507)."""
+    _fields_ = [("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float)]
+
+
+class MatchFrame:
+    """The searched Frame's state on the device (mvKeys, mDescriptors, mvuRight, bounds;
+    the 64 x 48 grid of AssignFeaturesToGrid is built there)."""
+
+    def __init__(self, device=0):
+        self.h = C.c_void_p()
+        _check(lib().ygzfe_match_frame_create(device, C.byref(self.h)), "match_frame_create")
+        self.n = 0
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value and _lib is not None:
+            _lib.ygzfe_match_frame_destroy(self.h)
+            self.h = None
+
+    def set(self, kps, desc, u_right=None, bounds=(0.0, 752.0, 0.0, 480.0)):
+        kps = np.ascontiguousarray(kps, KP_DTYPE)
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        ur = None if u_right is None else np.ascontiguousarray(u_right, np.float32)
+        b = Bounds(*[float(x) for x in bounds])
+        _check(lib().ygzfe_match_frame_set(self.h, _p(kps), _p(desc), len(kps), None if ur is None else _p(ur),
+                                           C.byref(b)), "match_frame_set")
+        self.n = len(kps)
+        return self
+
+    def rescans(self):
+        """Queries of the last search whose top-K candidates the sequential skips used up."""
+        r = C.c_int()
+        _check(lib().ygzfe_match_frame_stats(self.h, C.byref(r)), "match_frame_stats")
+        return r.value
+
+    def from_batch(self, batch, frame, bounds=(0.0, 752.0, 0.0, 480.0)):
+        b = Bounds(*[float(x) for x in bounds])
+        _check(lib().ygzfe_match_frame_from_batch(self.h, batch.h, frame, C.byref(b)), "match_frame_from_batch")
+        return self
+
+
+def search_projection_best(cur, queries, q_desc, blocked=None, th_dist=100, check_ori=True):
+    """SearchByProjection(CurrentFrame, LastFrame | pKF, ...) (ORBmatcher.cc:1218-1469):
+    -> (train_match int32[cur.n]: -1 untouched / -2 NULLed by the rotation check / query, nmatches)."""
+    q = np.ascontiguousarray(queries, MATCH_QUERY_DTYPE)
+    d = np.ascontiguousarray(q_desc, np.uint8).reshape(-1, 32)
+    bl = None if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+    out = np.zeros(max(cur.n, 1), np.int32)
+    nm = C.c_int()
+    _check(lib().ygzfe_search_projection_best(cur.h, _p(q), _p(d), len(q), None if bl is None else _p(bl), th_dist,
+                                              int(check_ori), _p(out), C.byref(nm)), "search_projection_best")
+    return out[:cur.n], nm.value
+
+
+def search_projection_ratio(F, queries, q_desc, blocked=None, nnratio=0.6):
+    """SearchByProjection(F, vpMapPoints, th, checkLevel) (ORBmatcher.cc:43-126) -> (train_match, nmatches)."""
+    q = np.ascontiguousarray(queries, MATCH_QUERY_DTYPE)
+    d = np.ascontiguousarray(q_desc, np.uint8).reshape(-1, 32)
+    bl = None if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+    out = np.zeros(max(F.n, 1), np.int32)
+    nm = C.c_int()
+    _check(lib().ygzfe_search_projection_ratio(F.h, _p(q), _p(d), len(q), None if bl is None else _p(bl),
+                                               C.c_float(nnratio), _p(out), C.byref(nm)), "search_projection_ratio")
+    return out[:F.n], nm.value
+
+
+def search_for_initialization(F1, F2, prev_matched, window_size=100, nnratio=0.9, check_ori=True):
+    """SearchForInitialization (ORBmatcher.cc:375-478) -> (vnMatches12, nmatches, vbPrevMatched updated)."""
+    prev = np.ascontiguousarray(prev_matched, np.float32).reshape(-1, 2).copy()
+    m12 = np.zeros(max(F1.n, 1), np.int32)
+    nm = C.c_int()
+    _check(lib().ygzfe_search_for_initialization(F1.h, F2.h, _p(prev), window_size, C.c_float(nnratio),
+                                                 int(check_ori), _p(m12), C.byref(nm)), "search_for_initialization")
+    return m12[:F1.n], nm.value, prev
+
+
+def search_by_bow(kf, F, kf_usable, fv_kf, fv_f, nnratio=0.7, check_ori=False):
+    """SearchByBoW(pKF, F, vpMapPointMatches) (ORBmatcher.cc:155-263).  fv_* = (nodes, ptr, feats)
+    node-sorted CSR FeatureVectors -> (f_match int32[F.n]: KF index or -1, nmatches)."""
+    us = np.ascontiguousarray(kf_usable, np.uint8)
+    kn, kp, kfe = (np.ascontiguousarray(a, np.int32) for a in fv_kf)
+    fn, fp, ffe = (np.ascontiguousarray(a, np.int32) for a in fv_f)
+    out = np.zeros(max(F.n, 1), np.int32)
+    nm = C.c_int()
+    _check(lib().ygzfe_search_by_bow(kf.h, F.h, _p(us), len(kn), _p(kn), _p(kp), _p(kfe), len(fn), _p(fn), _p(fp),
+                                     _p(ffe), C.c_float(nnratio), int(check_ori), _p(out), C.byref(nm)),
+           "search_by_bow")
+    return out[:F.n], nm.value
+
+
 class SparseImgAlign:
     """SparseImgAlign(n_levels, min_level, n_iter=10) (SparseImageAlign.h:37-60)."""
 

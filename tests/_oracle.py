@@ -362,6 +362,66 @@ class Vocab:
         return (bw[:nw.value].copy(), bv[:nw.value].copy()), (fn[:nf.value].copy(), ff[:nf.value].copy())
 
 
+# ---------------------------------------------------------------- ORBmatcher searches (oracle/match.c)
+class MFrame(C.Structure):
+    _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("u_right", C.c_void_p), ("n", C.c_int),
+                ("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float)]
+
+
+def mframe(kps, desc, u_right=None, bounds=(0.0, 752.0, 0.0, 480.0)):
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    ur = None if u_right is None else np.ascontiguousarray(u_right, np.float32)
+    f = MFrame(kps.ctypes.data, desc.ctypes.data, None if ur is None else ur.ctypes.data, len(kps), *bounds)
+    f._keep = (kps, desc, ur)
+    return f
+
+
+def search_projection_best(cur, q, q_desc, blocked=None, th_dist=100, check_ori=True):
+    q = np.ascontiguousarray(q)
+    d = np.ascontiguousarray(q_desc, np.uint8)
+    bl = None if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+    out = np.zeros(max(cur.n, 1), np.int32)
+    nm = lib().ygzo_search_projection_best(C.byref(cur), _p(q), _p(d), len(q), None if bl is None else _p(bl),
+                                           th_dist, int(check_ori), _p(out))
+    return out[:cur.n], nm
+
+
+def search_projection_ratio(F, q, q_desc, blocked=None, nnratio=0.6):
+    q = np.ascontiguousarray(q)
+    d = np.ascontiguousarray(q_desc, np.uint8)
+    bl = None if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+    out = np.zeros(max(F.n, 1), np.int32)
+    nm = lib().ygzo_search_projection_ratio(C.byref(F), _p(q), _p(d), len(q), None if bl is None else _p(bl),
+                                            C.c_float(nnratio), _p(out))
+    return out[:F.n], nm
+
+
+def search_for_initialization(F1, F2, prev, window=100, nnratio=0.9, check_ori=True):
+    prev = np.ascontiguousarray(prev, np.float32).reshape(-1, 2).copy()
+    m12 = np.zeros(max(F1.n, 1), np.int32)
+    nm = lib().ygzo_search_for_initialization(C.byref(F1), C.byref(F2), _p(prev), window, C.c_float(nnratio),
+                                              int(check_ori), _p(m12))
+    return m12[:F1.n], nm, prev
+
+
+def search_by_bow(kf, F, kf_usable, fv_kf, fv_f, nnratio=0.7, check_ori=False):
+    us = np.ascontiguousarray(kf_usable, np.uint8)
+    kn, kp, kfe = (np.ascontiguousarray(a, np.int32) for a in fv_kf)
+    fn, fp, ffe = (np.ascontiguousarray(a, np.int32) for a in fv_f)
+    out = np.zeros(max(F.n, 1), np.int32)
+    nm = lib().ygzo_search_by_bow(C.byref(kf), C.byref(F), _p(us), len(kn), _p(kn), _p(kp), _p(kfe), len(fn), _p(fn),
+                                  _p(fp), _p(ffe), C.c_float(nnratio), int(check_ori), _p(out))
+    return out[:F.n], nm
+
+
+def features_in_area(F, x, y, r, min_level=-1, max_level=-1):
+    out = np.zeros(max(F.n, 1), np.int32)
+    n = lib().ygzo_features_in_area(C.byref(F), C.c_float(x), C.c_float(y), C.c_float(r), int(min_level), int(max_level),
+                                    _p(out))
+    return out[:n]
+
+
 class RefFast:
     """The reference's own Thirdparty/fast, compiled by oracle/Makefile (oracle/_ref)."""
 

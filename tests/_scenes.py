@@ -194,3 +194,77 @@ def stereo_scene(seed, W=752, H=480, baseline=EUROC_BASELINE):
     fx = sc.cam[0]
     return {"scene": sc, "left": left, "right": right, "pose": (q, t), "mb": float(baseline),
             "mbf": float(np.float32(baseline) * np.float32(fx))}
+
+
+# ---------------------------------------------------------------- ORBmatcher search inputs
+def _oracle_extract(cfg, img):
+    import _oracle as O
+    W, H, nf, sf, nl, ini, mn = CONFIGS[cfg]
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    return orc.extract(orc.pyramid(img)), orc
+
+
+def match_pair(cfg="C2", seed=0, motion_scale=1.0):
+    """Two rendered frames of the textured plane (frame 1 moved by motion(seed)) with their
+    keypoints / descriptors (oracle extraction, identical to the GPU's) and the map points of
+    frame 0's keypoints on the plane."""
+    W, H = CONFIGS[cfg][:2]
+    sc = PlaneScene(seed, W, H)
+    q0, t0 = np.array([0, 0, 0, 1.0]), np.zeros(3)
+    v, w = motion(seed, motion_scale)
+    q1, t1 = quat_from_rotvec(w), v
+    f0 = sc.render(q0.astype(np.float32), t0.astype(np.float32), 3 * seed + 1)
+    f1 = sc.render(q1.astype(np.float32), t1.astype(np.float32), 3 * seed + 2)
+    (k0, d0), orc = _oracle_extract(cfg, f0)
+    (k1, d1), _ = _oracle_extract(cfg, f1)
+    uv0 = np.stack([k0["x"], k0["y"]], 1).astype(np.float64)
+    Pw = backproject_plane_np(sc.cam, (q0, t0), uv0)
+    return {"cfg": cfg, "W": W, "H": H, "sc": sc, "poses": ((q0, t0), (q1, t1)), "k0": k0, "d0": d0, "k1": k1,
+            "d1": d1, "Pw": Pw, "scale": orc.scale}
+
+
+def projection_queries(p, seed, th=7.0, level_mode="mixed", blocks_frac=0.8, stereo_frac=0.3, valid_frac=0.9,
+                       noise=1.0, flip_bits=8):
+    """SearchByProjection(CurrentFrame, LastFrame, ...) queries: frame 0's map points projected into
+    frame 1 (+ noise), radius th * mvScaleFactors[octave], a level window per `level_mode`
+    (ORBmatcher.cc:1272-1279), the MapPoint descriptor = frame 0's descriptor with a few bits
+    flipped, random VALID / BLOCKS / STEREO flags.  Returns (queries, q_desc, u_right of frame 1,
+    train_blocked)."""
+    import ygzfe
+    rng = np.random.default_rng(7000 + seed)
+    (q1, t1) = p["poses"][1]
+    px, Pc = project(p["sc"].cam, q1, t1, p["Pw"])
+    n = len(px)
+    Q = np.zeros(n, ygzfe.MATCH_QUERY_DTYPE)
+    Q["u"] = px[:, 0] + rng.uniform(-noise, noise, n)
+    Q["v"] = px[:, 1] + rng.uniform(-noise, noise, n)
+    oct_ = p["k0"]["octave"]
+    Q["radius"] = (np.float32(th) * p["scale"][oct_]).astype(np.float32)
+    mode = rng.integers(0, 4, n) if level_mode == "mixed" else np.full(n, {"none": 0, "fwd": 1, "bwd": 2, "band": 3}[level_mode])
+    Q["min_level"] = np.where(mode == 0, -1, np.where(mode == 1, oct_, np.where(mode == 2, 0, oct_ - 1)))
+    Q["max_level"] = np.where(mode == 0, -1, np.where(mode == 1, -1, np.where(mode == 2, oct_, oct_ + 1)))
+    Q["angle"] = p["k0"]["angle"]
+    fx = p["sc"].cam[0]
+    Q["u_right"] = Q["u"] - np.float32(fx * 0.11) / Pc[:, 2].astype(np.float32)
+    inside = (Q["u"] >= 0) & (Q["u"] <= p["W"]) & (Q["v"] >= 0) & (Q["v"] <= p["H"])
+    flags = np.where(inside & (rng.random(n) < valid_frac), ygzfe.MQ_VALID, 0)
+    flags |= np.where(rng.random(n) < blocks_frac, ygzfe.MQ_BLOCKS, 0)
+    flags |= np.where(rng.random(n) < stereo_frac, ygzfe.MQ_STEREO, 0)
+    Q["flags"] = flags
+    qd = p["d0"].copy()
+    for i in range(n):  # MapPoint::GetDescriptor() != the keypoint's: a few bits apart
+        for b in rng.integers(0, 256, rng.integers(0, flip_bits + 1)):
+            qd[i, b // 8] ^= np.uint8(1 << (b % 8))
+    n1 = len(p["k1"])
+    ur = np.where(rng.random(n1) < 0.5, p["k1"]["x"] - rng.uniform(5, 60, n1), -1.0).astype(np.float32)
+    blocked = (rng.random(n1) < 0.1).astype(np.uint8)
+    return Q, qd, ur, blocked
+
+
+def feature_vector(desc, n_nodes, seed):
+    """A DBoW2-like FeatureVector: node of each feature from its descriptor bits (node-sorted CSR)."""
+    node = (desc[:, 0].astype(np.int64) * 131 + desc[:, 5] + seed) % n_nodes
+    order = np.argsort(node, kind="stable")
+    nodes, counts = np.unique(node[order], return_counts=True)
+    ptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    return nodes.astype(np.int32) * 7 + 3, ptr, order.astype(np.int32)
