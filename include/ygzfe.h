@@ -316,6 +316,12 @@ int ygzfe_batch_sparse_align(ygzfe_batch *b, int n_pairs, const int32_t *d_ref_i
  * for n independent patches on one level of `cur`; px_io in/out (level px). */
 int ygzfe_align2d_batch(const ygzfe_frame *cur, int level, int n, const uint8_t *patches_with_border,
                         const uint8_t *patches, int n_iter, float *px_io, uint8_t *converged);
+/* Align2D(const cv::Mat& cur_img, ref_patch_with_border, ref_patch, n_iter,
+ * cur_px_estimate) (Align.h:20-26) on a host image (w x h, row stride): the
+ * window around the estimate is uploaded (the whole image only if the
+ * iterations leave it); px in / out, *converged = the return value. */
+int ygzfe_align2d_image(int device, const uint8_t *img, int w, int h, int stride, const uint8_t *patch_with_border,
+                        const uint8_t *patch, int n_iter, float *px, uint8_t *converged);
 /* FindDirectProjection for n (map point, keyframe) items against `cur`:
  * item i uses keyframe frame ref[ref_index[i]], its keypoint kp_ref[i],
  * pt_ref[3i] = T_ref * P_w, T_cr[i] = T_cur * T_ref^-1, px_io[2i] (level-0 px,

@@ -1006,8 +1006,11 @@ __device__ void inverse3(const float m[9], float r[9]) {
 #undef M
 }
 
-__device__ int align2d_lane(const uint8_t *cur, int w, int h, const uint8_t *rpb, const uint8_t *rp, int n_iter,
-                            float *px) {
+// `win` = the pixel (x0, y0) of a window of the w x h level (stride `stride`,
+// ww x wh pixels); returns -1 when an iteration would read outside the window
+// (the host then re-runs on the whole level).  Whole level: x0 = y0 = 0.
+__device__ int align2d_lane(const uint8_t *win, int stride, int w, int h, int x0, int y0, int ww, int wh,
+                            const uint8_t *rpb, const uint8_t *rp, int n_iter, float *px) {
     const int hp = 4, ps = 8, step = 10;
     float rdx[64], rdy[64], H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int y = 0; y < ps; ++y)
@@ -1030,14 +1033,15 @@ __device__ int align2d_lane(const uint8_t *cur, int w, int h, const uint8_t *rpb
         const int ur = (int)floorf(u), vr = (int)floorf(v);
         if (ur < hp || vr < hp || ur >= w - hp || vr >= h - hp) break;
         if (isnan(u) || isnan(v)) return 0;
+        if (ur - hp < x0 || vr - hp < y0 || ur + hp >= x0 + ww || vr + hp >= y0 + wh) return -1;
         const float sx = u - ur, sy = v - vr;
         const float wTL = wmul(1.0 - sx, 1.0 - sy), wTR = wmul(sx, 1.0 - sy);
         const float wBL = wmul(1.0 - sx, sy), wBR = wmul(sx, sy);
         float Jr0 = 0.f, Jr1 = 0.f, Jr2 = 0.f;
         for (int y = 0; y < ps; ++y) {
-            const uint8_t *it = cur + (size_t)(vr + y - hp) * w + ur - hp;
+            const uint8_t *it = win + (size_t)(vr + y - hp - y0) * stride + (ur - hp - x0);
             for (int x = 0; x < ps; ++x, ++it) {
-                const float sp = wTL * it[0] + wTR * it[1] + wBL * it[w] + wBR * it[w + 1];
+                const float sp = wTL * it[0] + wTR * it[1] + wBL * it[stride] + wBR * it[stride + 1];
                 const float res = sp - rp[y * 8 + x] + mean_diff;
                 Jr0 -= res * rdx[y * 8 + x];
                 Jr1 -= res * rdy[y * 8 + x];
@@ -1063,10 +1067,33 @@ __global__ __launch_bounds__(256) void k_align2d(const uint8_t *__restrict__ img
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     float q[2] = {px[2 * i], px[2 * i + 1]};
-    const int ok = align2d_lane(img, w, h, pwb + (size_t)i * 100, p + (size_t)i * 64, n_iter, q);
+    const int ok = align2d_lane(img, w, w, h, 0, 0, w, h, pwb + (size_t)i * 100, p + (size_t)i * 64, n_iter, q);
     px[2 * i] = q[0];
     px[2 * i + 1] = q[1];
     conv[i] = (uint8_t)ok;
+}
+
+// One Align2D on a window of a host level (the drop-in Align2D(const cv::Mat&, ...)):
+// status 0 / 1 = converged flag, -1 = the window was too small.
+__global__ void k_align2d_window(const uint8_t *__restrict__ win, int stride, int w, int h, int x0, int y0, int ww,
+                                 int wh, const uint8_t *__restrict__ pwb, const uint8_t *__restrict__ p, int n_iter,
+                                 float *__restrict__ px, int *__restrict__ status) {
+    if (threadIdx.x != 0) return;
+    float q[2] = {px[0], px[1]};
+    const int r = align2d_lane(win, stride, w, h, x0, y0, ww, wh, pwb, p, n_iter, q);
+    if (r >= 0) {
+        px[0] = q[0];
+        px[1] = q[1];
+    }
+    status[0] = r;
+}
+
+hipError_t launch_align2d_window(const uint8_t *win, int stride, int w, int h, int x0, int y0, int ww, int wh,
+                                 const uint8_t *pwb, const uint8_t *p, int n_iter, float *px, int *status,
+                                 hipStream_t st) {
+    hipLaunchKernelGGL(k_align2d_window, dim3(1), dim3(64), 0, st, win, stride, w, h, x0, y0, ww, wh, pwb, p, n_iter,
+                       px, status);
+    return hipGetLastError();
 }
 
 hipError_t launch_align2d(const uint8_t *img, int w, int h, int n, const uint8_t *pwb, const uint8_t *p,
@@ -1132,7 +1159,8 @@ __device__ int find_direct_one(const uint8_t *__restrict__ ref_pyr, const AlignL
     for (int y = 1; y < 9; ++y)
         for (int x = 0; x < 8; ++x) pp[(y - 1) * 8 + x] = pb[y * 10 + 1 + x];
     float q[2] = {px[0] * clv.inv_scale[sl], px[1] * clv.inv_scale[sl]};
-    const int ok = align2d_lane(cur_pyr + clv.off[sl], clv.w[sl], clv.h[sl], pb, pp, 10, q);
+    const int ok = align2d_lane(cur_pyr + clv.off[sl], clv.w[sl], clv.w[sl], clv.h[sl], 0, 0, clv.w[sl], clv.h[sl], pb,
+                                pp, 10, q);
     px[0] = q[0] * scale[sl];
     px[1] = q[1] * scale[sl];
     return ok;

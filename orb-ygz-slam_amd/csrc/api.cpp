@@ -1049,6 +1049,73 @@ extern "C" int ygzfe_align2d_batch(const ygzfe_frame *cur, int level, int n, con
     return YGZFE_OK;
 }
 
+// Align2D(const cv::Mat& cur_img, ...) on a host image: the 48 x 48 window around
+// the estimate goes up (the whole image only when the iterations walk out of it).
+namespace {
+struct Align2DStaging {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    DevBuf buf;
+};
+}  // namespace
+
+extern "C" int ygzfe_align2d_image(int device, const uint8_t *img, int w, int h, int stride,
+                                   const uint8_t *patch_with_border, const uint8_t *patch, int n_iter, float *px,
+                                   uint8_t *converged) {
+    if (!img || w <= 0 || h <= 0 || stride < w || !patch_with_border || !patch || !px || !converged) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    YGZ_TRY(ensure_device(device));
+    // one staging area per thread and device, kept for the process lifetime
+    static thread_local std::map<int, Align2DStaging *> staging;
+    Align2DStaging *&S = staging[device];
+    if (!S) {
+        S = new Align2DStaging();
+        S->device = device;
+        YGZ_HIP(hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking));
+    }
+    hipStream_t st = S->stream;
+    const size_t small = 256;  // pwb 100 | p 64 | px 8 | status 4
+    uint8_t host_small[small];
+    memcpy(host_small, patch_with_border, 100);
+    memcpy(host_small + 100, patch, 64);
+    memcpy(host_small + 164, px, 8);
+    const int half = 24;
+    float fu = px[0], fv = px[1];
+    int cu = std::isfinite(fu) ? (int)floorf(fu) : 0, cv = std::isfinite(fv) ? (int)floorf(fv) : 0;
+    cu = std::min(std::max(cu, 0), w - 1);
+    cv = std::min(std::max(cv, 0), h - 1);
+    for (int pass = 0; pass < 2; pass++) {
+        int x0 = 0, y0 = 0, ww = w, wh = h;
+        if (pass == 0) {
+            x0 = std::max(cu - half, 0);
+            y0 = std::max(cv - half, 0);
+            ww = std::min(cu + half, w) - x0;
+            wh = std::min(cv + half, h) - y0;
+        }
+        YGZ_TRY(S->buf.ensure(small + (size_t)ww * wh));
+        uint8_t *d = S->buf.as<uint8_t>();
+        YGZ_HIP(hipMemcpyAsync(d, host_small, 172, hipMemcpyHostToDevice, st));
+        YGZ_HIP(hipMemcpy2DAsync(d + small, ww, img + (size_t)y0 * stride + x0, stride, ww, wh,
+                                 hipMemcpyHostToDevice, st));
+        YGZ_HIP(launch_align2d_window(d + small, ww, w, h, x0, y0, ww, wh, d, d + 100, n_iter,
+                                      reinterpret_cast<float *>(d + 164), reinterpret_cast<int *>(d + 172), st));
+        uint8_t back[12];
+        YGZ_HIP(hipMemcpyAsync(back, d + 164, 12, hipMemcpyDeviceToHost, st));
+        YGZ_HIP(hipStreamSynchronize(st));
+        int status;
+        memcpy(&status, back + 8, 4);
+        if (status >= 0) {
+            memcpy(px, back, 8);
+            *converged = (uint8_t)status;
+            return YGZFE_OK;
+        }
+    }
+    set_error("Align2D window retry failed");
+    return YGZFE_EHIP;
+}
+
 extern "C" int ygzfe_find_direct_projection_batch(const ygzfe_frame *const *ref, const ygzfe_frame *cur,
                                                   const ygzfe_camera *cam, int n, const int32_t *ref_index,
                                                   const ygzfe_kp *kp_ref, const float *pt_ref, const ygzfe_se3 *T_cr,

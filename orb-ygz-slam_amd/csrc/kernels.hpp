@@ -95,6 +95,9 @@ hipError_t launch_sparse_align(const AlignLevels &lv, const ygzfe_camera &cam, c
 size_t sparse_align_scratch_floats(int n);
 hipError_t launch_align2d(const uint8_t *img, int w, int h, int n, const uint8_t *pwb, const uint8_t *p,
                           int n_iter, float *px, uint8_t *conv, hipStream_t st);
+hipError_t launch_align2d_window(const uint8_t *win, int stride, int w, int h, int x0, int y0, int ww, int wh,
+                                 const uint8_t *pwb, const uint8_t *p, int n_iter, float *px, int *status,
+                                 hipStream_t st);
 hipError_t launch_find_direct(const uint8_t *const *ref_pyrs, const AlignLevels &ref_lv, const uint8_t *cur_pyr,
                               const AlignLevels &cur_lv, int nlevels, const float *scale, float inv_sigma2_1,
                               const ygzfe_camera &cam, int n, const int32_t *ref_index, const ygzfe_kp *kp_ref,

@@ -1,0 +1,428 @@
+// dropin_calls.cpp — the reference's hot-path call sites, verbatim, compiled
+// against the drop-in headers (compat/dropin/) and the test stubs of Frame /
+// MapPoint / KeyFrame / ORBmatcher (tests/dropin/stubs/), built -std=c++11 like
+// the reference, then run on the GPU and checked against the CPU oracle
+// (oracle/ygz_oracle.h; TEST INFRASTRUCTURE):
+//
+//   Tracking.cc:255   mpORBextractorLeft = new ORBextractor(nFeatures, fScaleFactor, nLevels, ...)
+//   Tracking.cc:284   mpAlign = new ygz::SparseImgAlign(nLevels - 1, 1);
+//   Frame.cc:807-813  ComputeImagePyramid (stub Frame.h)
+//   Frame.cc:337/340  (*mpORBextractorLeft)(this, mvKeys, mDescriptors, ORBextractor::...)   (stub Frame.h)
+//   Tracking.cc:2170-2171  SE3f TCR; size_t ret = mpAlign->run(&mLastFrame, &mCurrentFrame, TCR);
+//   Tracking.cc:825-826    matcher.SearchForInitialization(mInitialFrame, mCurrentFrame, ...)
+//   Tracking.cc:1156,1171  matcher.SearchByProjection(mCurrentFrame, mLastFrame, th, mSensor == System::MONOCULAR)
+//   Tracking.cc:1662,1674  matcher.SearchByProjection(mCurrentFrame, mvpLocalMapPoints, th, false)
+//   Tracking.cc:1018-1020  matcher.SearchByBoW(mpReferenceKF, mCurrentFrame, vpMapPointMatches)
+//   ORBmatcher.cc:1598-1599 ygz::Align2D(curr->mvImagePyramid[search_level], _patch_with_border, ...)
+//
+// Prints one line per check; exit 0 and "OK" when every check passes.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "Align.h"
+#include "Frame.h"
+#include "KeyFrame.h"
+#include "MapPoint.h"
+#include "ORBmatcher.h"
+#include "ORBmatcherGPU.h"
+#include "SparseImageAlign.h"
+#include "ygz_oracle.h"
+
+namespace ygz {
+#include "ORBmatcher_gpu.inc"
+
+const int ORBmatcher::TH_HIGH = 100;
+const int ORBmatcher::TH_LOW = 50;
+const int ORBmatcher::HISTO_LENGTH = 30;
+float Frame::fx, Frame::fy, Frame::cx, Frame::cy, Frame::invfx, Frame::invfy;
+float Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY, Frame::mnMaxY;
+long unsigned int Frame::nNextId = 0;
+
+struct System {
+    enum eSensor { MONOCULAR = 0, STEREO = 1, RGBD = 2 };
+};
+
+// the Tracking members the call sites use, with those call sites verbatim
+struct Tracking {
+    ORBextractor *mpORBextractorLeft = nullptr;
+    SparseImgAlign *mpAlign = nullptr;
+    Frame mCurrentFrame, mLastFrame, mInitialFrame;
+    std::vector<cv::Point2f> mvbPrevMatched;
+    std::vector<int> mvIniMatches;
+    std::vector<MapPoint *> mvpLocalMapPoints;
+    KeyFrame *mpReferenceKF = nullptr;
+    int mSensor = System::MONOCULAR;
+
+    Tracking(int nFeatures, float fScaleFactor, int nLevels, int fIniThFAST, int fMinThFAST) {
+        mpORBextractorLeft = new ORBextractor(nFeatures, fScaleFactor, nLevels, fIniThFAST, fMinThFAST);
+        mpAlign = new ygz::SparseImgAlign(nLevels - 1, 1);
+    }
+    ~Tracking() {
+        delete mpAlign;
+        delete mpORBextractorLeft;
+    }
+    size_t SparseAlign(SE3f &out) {
+        SE3f TCR;
+        size_t ret = mpAlign->run(&mLastFrame, &mCurrentFrame, TCR);
+        out = TCR;
+        return ret;
+    }
+    int Initialization() {
+        ORBmatcher matcher(0.9, true);
+        int nmatches = matcher.SearchForInitialization(mInitialFrame, mCurrentFrame, mvbPrevMatched, mvIniMatches,
+                                                       100);
+        return nmatches;
+    }
+    int MotionModel(int th) {
+        ORBmatcher matcher(0.9, true);
+        int nmatches = matcher.SearchByProjection(mCurrentFrame, mLastFrame, th, mSensor == System::MONOCULAR);
+        return nmatches;
+    }
+    int LocalPoints(float th) {
+        ORBmatcher matcher(0.8);
+        int cnt = matcher.SearchByProjection(mCurrentFrame, mvpLocalMapPoints, th, false );
+        return cnt;
+    }
+    int ReferenceKF(std::vector<MapPoint *> &vpMapPointMatches) {
+        ORBmatcher matcher(0.7, false);
+        int nmatches = matcher.SearchByBoW(mpReferenceKF, mCurrentFrame, vpMapPointMatches);
+        return nmatches;
+    }
+};
+}  // namespace ygz
+
+using namespace ygz;
+
+static int fails = 0;
+#define CHECK(cond, ...)                       \
+    do {                                       \
+        std::printf(__VA_ARGS__);              \
+        std::printf(" %s\n", (cond) ? "ok" : "FAILED"); \
+        if (!(cond)) fails++;                  \
+    } while (0)
+
+static cv::Mat synth(int W, int H, unsigned seed, int dx, int dy) {
+    cv::Mat img(H, W, CV_8U);
+    std::memset(img.data, 128, (size_t)W * H);
+    unsigned s = seed;
+    auto rnd = [&](int n) { s = s * 1664525u + 1013904223u; return (int)((s >> 8) % (unsigned)n); };
+    for (int r = 0; r < 900; r++) {
+        const int x0 = rnd(W + 40) - 20, y0 = rnd(H + 40) - 20, w = 4 + rnd(40), h = 4 + rnd(40), v = rnd(256);
+        for (int y = y0; y < y0 + h; y++)
+            for (int x = x0; x < x0 + w; x++) {
+                const int xx = x + dx, yy = y + dy;
+                if (xx >= 0 && yy >= 0 && xx < W && yy < H) img.data[(size_t)yy * W + xx] = (uint8_t)v;
+            }
+    }
+    for (int i = 0; i < W * H; i++) {  // +-1 noise so no two frames are identical
+        const int v = img.data[i] + (int)(((uint32_t)(i + seed) * 2654435761u) >> 30) - 1;
+        img.data[i] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+    }
+    return img;
+}
+
+static ygzo_mframe mframe(const Frame &F, bool uright) {
+    ygzo_mframe f;
+    f.kps = reinterpret_cast<const ygzo_kp *>(F.mvKeys.data());
+    f.desc = F.mDescriptors.data;
+    f.u_right = uright ? F.mvuRight.data() : nullptr;
+    f.n = F.N;
+    f.min_x = Frame::mnMinX;
+    f.max_x = Frame::mnMaxX;
+    f.min_y = Frame::mnMinY;
+    f.max_y = Frame::mnMaxY;
+    return f;
+}
+
+int main() {
+    const int W = 752, H = 480, nl = 4;
+    Frame::fx = 458.654f;
+    Frame::fy = 457.296f;
+    Frame::cx = 367.215f;
+    Frame::cy = 248.375f;
+    Frame::invfx = 1.f / Frame::fx;
+    Frame::invfy = 1.f / Frame::fy;
+    const float Z = 3.0f;
+    Tracking T(1000, 2.0f, nl, 20, 7);  // EuRoC.yaml:32-45
+
+    // ---------------------------------------------------------------- pyramid + ORB extraction
+    const cv::Mat im0 = synth(W, H, 7u, 0, 0), im1 = synth(W, H, 7u, 2, -1);
+    T.mLastFrame = Frame(im0, T.mpORBextractorLeft);
+    T.mCurrentFrame = Frame(im1, T.mpORBextractorLeft);
+    T.mLastFrame.ExtractFeatures();
+    T.mCurrentFrame.ExtractFeatures();
+    ygzo_orb o;
+    ygzo_orb_init(&o, 1000, 2.0f, nl, 20, 7, 0);
+    int lw[YGZO_MAX_LEVELS], lh[YGZO_MAX_LEVELS];
+    ygzo_level_sizes(&o, W, H, lw, lh);
+    std::vector<std::vector<uint8_t>> lv(nl);
+    uint8_t *lp[YGZO_MAX_LEVELS];
+    for (int l = 0; l < nl; l++) {
+        lv[l].resize((size_t)lw[l] * lh[l]);
+        lp[l] = lv[l].data();
+    }
+    for (int fi = 0; fi < 2; fi++) {
+        const Frame &F = fi ? T.mCurrentFrame : T.mLastFrame;
+        ygzo_compute_pyramid(&o, (fi ? im1 : im0).data, W, H, W, lp);
+        bool pyr_ok = (int)F.mvImagePyramid.size() == nl;
+        for (int l = 0; l < nl && pyr_ok; l++)
+            pyr_ok = F.mvImagePyramid[l].cols == lw[l] && F.mvImagePyramid[l].rows == lh[l] &&
+                     std::memcmp(F.mvImagePyramid[l].data, lp[l], lv[l].size()) == 0;
+        CHECK(pyr_ok, "Frame::ComputeImagePyramid -> ORBextractor::ComputePyramid (frame %d): levels == oracle", fi);
+        std::vector<ygzo_kp> ok_(4096);
+        std::vector<uint8_t> od(4096 * 32);
+        const int n = ygzo_extract_orbslam(&o, lp, lw, lh, nullptr, 0, ok_.data(), od.data(), 4096);
+        const bool same = n == F.N && n > 300 && std::memcmp(ok_.data(), F.mvKeys.data(), sizeof(ygzo_kp) * n) == 0 &&
+                          std::memcmp(od.data(), F.mDescriptors.data, (size_t)32 * n) == 0;
+        CHECK(same, "(*mpORBextractorLeft)(this, mvKeys, mDescriptors, ORBSLAM_KEYPOINT) (frame %d): %d keypoints "
+                    "+ descriptors == oracle", fi, F.N);
+    }
+
+    // DSO path: a frame with direct-tracked keypoints and no features yet (Frame.cc:335-337)
+    {
+        ORBextractor dso_ex(1000, 2.0f, nl, 20, 7);
+        Frame Fd(im1, &dso_ex);
+        for (int i = 0; i < 60; i++)
+            Fd.mvKeys.push_back(cv::KeyPoint(T.mCurrentFrame.mvKeys[i].pt, 7, -1, 0, 0));
+        Fd.N = (int)Fd.mvKeys.size();
+        std::vector<ygzo_kp> ex(Fd.N);
+        std::memcpy(ex.data(), Fd.mvKeys.data(), sizeof(ygzo_kp) * Fd.N);
+        Fd.ExtractORB(0, Fd.mImGray);
+        ygzo_orb od_;
+        ygzo_orb_init(&od_, 1000, 2.0f, nl, 20, 7, 0);
+        ygzo_compute_pyramid(&od_, im1.data, W, H, W, lp);
+        std::vector<ygzo_kp> ok_(8192);
+        std::vector<uint8_t> odesc(8192 * 32);
+        const int n = ygzo_extract_dso(&od_, lp, lw, lh, ex.data(), 60, ok_.data(), odesc.data(), 8192);
+        const bool same = n == (int)Fd.mvKeys.size() &&
+                          std::memcmp(ok_.data(), Fd.mvKeys.data(), sizeof(ygzo_kp) * n) == 0 &&
+                          std::memcmp(odesc.data(), Fd.mDescriptors.data, (size_t)32 * n) == 0;
+        CHECK(same, "(*mpORBextractorLeft)(this, mvKeys, mDescriptors, DSO_KEYPOINT): %d rows (60 existing) == oracle",
+              (int)Fd.mvKeys.size());
+    }
+
+    // ---------------------------------------------------------------- SparseImgAlign::run
+    // map points of the last frame on the plane Z = 3 m in front of it (identity pose)
+    std::vector<MapPoint> mps(T.mLastFrame.N);
+    for (int i = 0; i < T.mLastFrame.N; i++) {
+        const cv::KeyPoint &kp = T.mLastFrame.mvKeys[i];
+        mps[i].mWorldPos = Vector3f((kp.pt.x - Frame::cx) / Frame::fx * Z, (kp.pt.y - Frame::cy) / Frame::fy * Z, Z);
+        mps[i].mDescriptor = T.mLastFrame.mDescriptors.row(i).clone();
+        mps[i].nObs = 1 + (i % 3 == 0);
+        if (i % 17 == 0) mps[i].mbBad = true;
+        T.mLastFrame.mvpMapPoints[i] = i % 11 == 5 ? nullptr : &mps[i];
+        T.mLastFrame.mvbOutlier[i] = i % 13 == 7;
+    }
+    SE3f TCR;
+    const size_t ret = T.SparseAlign(TCR);
+    {
+        std::vector<float> xyz(3 * (size_t)T.mLastFrame.N);
+        std::vector<uint8_t> us(T.mLastFrame.N);
+        for (int i = 0; i < T.mLastFrame.N; i++) {
+            MapPoint *mp = T.mLastFrame.mvpMapPoints[i];
+            us[i] = mp && !mp->isBad() && !T.mLastFrame.mvbOutlier[i];
+            const Vector3f p = T.mLastFrame.mTcw * mps[i].mWorldPos;
+            for (int k = 0; k < 3; k++) xyz[3 * i + k] = p[k];
+        }
+        uint8_t *rp[YGZO_MAX_LEVELS], *cp[YGZO_MAX_LEVELS];
+        for (int l = 0; l < nl; l++) {
+            rp[l] = T.mLastFrame.mvImagePyramid[l].data;
+            cp[l] = T.mCurrentFrame.mvImagePyramid[l].data;
+        }
+        ygzo_cam cam{Frame::fx, Frame::fy, Frame::cx, Frame::cy};
+        ygzo_se3 T0{{0, 0, 0, 1}, {0, 0, 0}};
+        ygzo_align_out ao;
+        ygzo_sparse_align(rp, cp, lw, lh, o.inv_scale, &cam, reinterpret_cast<const ygzo_kp *>(T.mLastFrame.mvKeys.data()),
+                          xyz.data(), us.data(), T.mLastFrame.N, nl - 1, 1, &T0, &ao);
+        float err = 0.f;
+        const float gq[4] = {TCR.unit_quaternion().x(), TCR.unit_quaternion().y(), TCR.unit_quaternion().z(),
+                             TCR.unit_quaternion().w()};
+        for (int k = 0; k < 4; k++) err = std::fmax(err, std::fabs(gq[k] - ao.T.q[k]));
+        for (int k = 0; k < 3; k++) err = std::fmax(err, std::fabs(TCR.translation()[k] - ao.T.t[k]));
+        const float tx = 2.0f * Z / Frame::fx, ty = -1.0f * Z / Frame::fy;  // image shift (2, -1) px at depth Z
+        CHECK(ret == (size_t)ao.n_visible && err <= 1e-4f && ret > 100,
+              "mpAlign->run(&mLastFrame, &mCurrentFrame, TCR): visible %zu (oracle %d), |dT| %.2e, t (%.4f %.4f) "
+              "expected ~(%.4f %.4f)", ret, ao.n_visible, err, TCR.translation()[0], TCR.translation()[1], tx, ty);
+        const auto I = T.mpAlign->getFisherInformation();
+        CHECK(std::fabs(I(0, 0) - ao.H[0] / (float)(5e-4 * 255 * 255)) <= 1e-3f * std::fabs(I(0, 0)) + 1e-3f,
+              "getFisherInformation() = H / 32.5125: %.4g", I(0, 0));
+    }
+
+    // ---------------------------------------------------------------- SearchByProjection(F, LastF)
+    T.mCurrentFrame.SetPose(TCR * T.mLastFrame.mTcw);
+    for (int i = 0; i < T.mCurrentFrame.N; i++) T.mCurrentFrame.mvpMapPoints[i] = nullptr;
+    {
+        // expected: the oracle over the same windows (ORBmatcher.cc:1241-1280 formed here)
+        Frame &C = T.mCurrentFrame;
+        const Frame &L = T.mLastFrame;
+        const Matrix3f Rcw = C.mTcw.rotationMatrix();
+        const Vector3f tcw = C.mTcw.translation();
+        std::vector<ygzo_mquery> q;
+        std::vector<uint8_t> qd;
+        std::vector<int> src;
+        for (int i = 0; i < L.N; i++) {
+            MapPoint *pMP = L.mvpMapPoints[i];
+            if (!pMP || L.mvbOutlier[i]) continue;
+            const Vector3f x3Dc = Rcw * pMP->GetWorldPos() + tcw;
+            const float invzc = 1.0 / x3Dc[2];
+            if (invzc < 0) continue;
+            const float u = C.fx * x3Dc[0] * invzc + C.cx, v = C.fy * x3Dc[1] * invzc + C.cy;
+            if (u < C.mnMinX || u > C.mnMaxX || v < C.mnMinY || v > C.mnMaxY) continue;
+            const int oc = L.mvKeys[i].octave;
+            ygzo_mquery Q{u, v, 15 * C.mvScaleFactors[oc], u - C.mbf * invzc, oc - 1, oc + 1, L.mvKeys[i].angle,
+                          YGZO_MQ_VALID | YGZO_MQ_STEREO | (pMP->Observations() > 0 ? YGZO_MQ_BLOCKS : 0)};
+            q.push_back(Q);
+            qd.insert(qd.end(), pMP->mDescriptor.data, pMP->mDescriptor.data + 32);
+            src.push_back(i);
+        }
+        std::vector<int32_t> want(C.N);
+        std::vector<uint8_t> blocked(C.N, 0);
+        const ygzo_mframe mf = mframe(C, true);
+        const int wn = ygzo_search_projection_best(&mf, q.data(), qd.data(), (int)q.size(), blocked.data(), 100, 1,
+                                                   want.data());
+        const int nmatches = T.MotionModel(15);
+        int same = nmatches == wn && nmatches > 100;
+        for (int i2 = 0; i2 < C.N && same; i2++) {
+            MapPoint *exp = want[i2] >= 0 ? L.mvpMapPoints[src[want[i2]]] : nullptr;
+            same = C.mvpMapPoints[i2] == exp;
+        }
+        CHECK(same, "matcher.SearchByProjection(mCurrentFrame, mLastFrame, th, MONOCULAR): %d matches (oracle %d)",
+              nmatches, wn);
+    }
+
+    // ---------------------------------------------------------------- SearchByProjection(F, local map points)
+    {
+        Frame &C = T.mCurrentFrame;
+        for (int i = 0; i < C.N; i++) C.mvpMapPoints[i] = nullptr;
+        T.mvpLocalMapPoints.clear();
+        for (int i = 0; i < T.mLastFrame.N; i++) {
+            MapPoint *pMP = &mps[i];
+            const Vector3f x3Dc = C.mTcw * pMP->GetWorldPos();
+            pMP->mbTrackInView = i % 9 != 4;
+            pMP->mTrackProjX = C.fx * x3Dc[0] / x3Dc[2] + C.cx;
+            pMP->mTrackProjY = C.fy * x3Dc[1] / x3Dc[2] + C.cy;
+            pMP->mTrackProjXR = pMP->mTrackProjX - 30.f;
+            pMP->mnTrackScaleLevel = T.mLastFrame.mvKeys[i].octave;
+            pMP->mTrackViewCos = i % 2 ? 0.999f : 0.99f;
+            T.mvpLocalMapPoints.push_back(pMP);
+        }
+        std::vector<ygzo_mquery> q;
+        std::vector<uint8_t> qd;
+        for (MapPoint *pMP : T.mvpLocalMapPoints) {
+            const float r = (pMP->mTrackViewCos > 0.998 ? 2.5f : 4.0f) * 3.0f;
+            const int lvl = pMP->mnTrackScaleLevel;
+            ygzo_mquery Q{pMP->mTrackProjX, pMP->mTrackProjY, r * C.mvScaleFactors[lvl], pMP->mTrackProjXR, -1, -1,
+                          0.f, (pMP->mbTrackInView && !pMP->isBad() ? YGZO_MQ_VALID : 0) | YGZO_MQ_STEREO |
+                                   (pMP->Observations() > 0 ? YGZO_MQ_BLOCKS : 0)};
+            q.push_back(Q);
+            qd.insert(qd.end(), pMP->mDescriptor.data, pMP->mDescriptor.data + 32);
+        }
+        std::vector<int32_t> want(C.N);
+        const ygzo_mframe mf = mframe(C, true);
+        const int wn = ygzo_search_projection_ratio(&mf, q.data(), qd.data(), (int)q.size(), nullptr, 0.8f, want.data());
+        const int cnt = T.LocalPoints(3);
+        int same = cnt == wn && cnt > 100;
+        for (int i = 0; i < C.N && same; i++)
+            same = C.mvpMapPoints[i] == (want[i] >= 0 ? T.mvpLocalMapPoints[want[i]] : nullptr);
+        CHECK(same, "matcher.SearchByProjection(mCurrentFrame, mvpLocalMapPoints, th, false): %d (oracle %d)", cnt, wn);
+    }
+
+    // ---------------------------------------------------------------- SearchForInitialization
+    {
+        T.mInitialFrame = T.mLastFrame;
+        T.mvbPrevMatched.clear();
+        for (const cv::KeyPoint &kp : T.mInitialFrame.mvKeys) T.mvbPrevMatched.push_back(kp.pt);
+        std::vector<float> prev;
+        for (const cv::Point2f &p : T.mvbPrevMatched) {
+            prev.push_back(p.x);
+            prev.push_back(p.y);
+        }
+        std::vector<int32_t> want(T.mInitialFrame.N);
+        const ygzo_mframe f1 = mframe(T.mInitialFrame, false), f2 = mframe(T.mCurrentFrame, false);
+        const int wn = ygzo_search_for_initialization(&f1, &f2, prev.data(), 100, 0.9f, 1, want.data());
+        const int nmatches = T.Initialization();
+        int same = nmatches == wn && nmatches > 100 && (int)T.mvIniMatches.size() == T.mInitialFrame.N;
+        for (int i = 0; i < T.mInitialFrame.N && same; i++)
+            same = T.mvIniMatches[i] == want[i] && T.mvbPrevMatched[i].x == prev[2 * i] &&
+                   T.mvbPrevMatched[i].y == prev[2 * i + 1];
+        CHECK(same, "matcher.SearchForInitialization(mInitialFrame, mCurrentFrame, mvbPrevMatched, mvIniMatches, 100): "
+                    "%d (oracle %d)", nmatches, wn);
+    }
+
+    // ---------------------------------------------------------------- SearchByBoW(pKF, F)
+    {
+        KeyFrame kf;
+        kf.mvKeys = T.mLastFrame.mvKeys;
+        kf.mDescriptors = T.mLastFrame.mDescriptors;
+        for (int i = 0; i < T.mLastFrame.N; i++) kf.mvpMapPoints.push_back(T.mLastFrame.mvpMapPoints[i]);
+        auto node_of = [](const uint8_t *d) { return (unsigned)((d[0] * 131u + d[5]) % 60u) * 7u + 3u; };
+        for (int i = 0; i < T.mLastFrame.N; i++)
+            kf.mFeatVec[node_of(T.mLastFrame.mDescriptors.data + 32 * i)].push_back(i);
+        T.mCurrentFrame.mFeatVec.clear();
+        for (int i = 0; i < T.mCurrentFrame.N; i++)
+            T.mCurrentFrame.mFeatVec[node_of(T.mCurrentFrame.mDescriptors.data + 32 * i)].push_back(i);
+        T.mpReferenceKF = &kf;
+        auto csr = [](const DBoW2::FeatureVector &fv, std::vector<int32_t> &n, std::vector<int32_t> &p,
+                      std::vector<int32_t> &f) {
+            p.push_back(0);
+            for (auto &e : fv) {
+                n.push_back((int)e.first);
+                for (unsigned x : e.second) f.push_back((int)x);
+                p.push_back((int)f.size());
+            }
+        };
+        std::vector<int32_t> kn, kp, kfe, fn, fp, ffe;
+        csr(kf.mFeatVec, kn, kp, kfe);
+        csr(T.mCurrentFrame.mFeatVec, fn, fp, ffe);
+        std::vector<uint8_t> usable(kf.mvKeys.size());
+        for (size_t i = 0; i < usable.size(); i++) usable[i] = kf.mvpMapPoints[i] && !kf.mvpMapPoints[i]->isBad();
+        std::vector<int32_t> want(T.mCurrentFrame.N);
+        const ygzo_mframe fk = mframe(T.mLastFrame, false), ff = mframe(T.mCurrentFrame, false);
+        const int wn = ygzo_search_by_bow(&fk, &ff, usable.data(), (int)kn.size(), kn.data(), kp.data(), kfe.data(),
+                                          (int)fn.size(), fn.data(), fp.data(), ffe.data(), 0.7f, 0, want.data());
+        std::vector<MapPoint *> vpMapPointMatches;
+        const int nmatches = T.ReferenceKF(vpMapPointMatches);
+        int same = nmatches == wn && nmatches > 30 && (int)vpMapPointMatches.size() == T.mCurrentFrame.N;
+        for (int i = 0; i < T.mCurrentFrame.N && same; i++)
+            same = vpMapPointMatches[i] == (want[i] >= 0 ? kf.mvpMapPoints[want[i]] : nullptr);
+        CHECK(same, "matcher.SearchByBoW(mpReferenceKF, mCurrentFrame, vpMapPointMatches): %d (oracle %d)", nmatches,
+              wn);
+    }
+
+    // ---------------------------------------------------------------- Align2D
+    {
+        Frame *curr = &T.mCurrentFrame;
+        int tried = 0, same = 0, conv = 0;
+        for (int i = 0; i < curr->N && tried < 40; i += 7) {
+            const cv::KeyPoint &k = curr->mvKeys[i];
+            const int search_level = k.octave;
+            const cv::Mat &img = curr->mvImagePyramid[search_level];
+            const Vector2f px_curr(k.pt.x + 0.6f * curr->mvScaleFactors[search_level],
+                                   k.pt.y - 0.4f * curr->mvScaleFactors[search_level]);
+            const int u = (int)std::lround(k.pt.x * curr->mvInvScaleFactors[search_level]),
+                      v = (int)std::lround(k.pt.y * curr->mvInvScaleFactors[search_level]);
+            if (u < 8 || v < 8 || u >= img.cols - 8 || v >= img.rows - 8) continue;
+            uint8_t _patch_with_border[100], _patch[64];
+            for (int y = 0; y < 10; y++)
+                for (int x = 0; x < 10; x++) _patch_with_border[y * 10 + x] = img.data[(v - 5 + y) * img.step[0] + u - 5 + x];
+            for (int y = 0; y < 8; y++)
+                for (int x = 0; x < 8; x++) _patch[y * 8 + x] = _patch_with_border[(y + 1) * 10 + x + 1];
+            tried++;
+            Vector2f px_scaled = px_curr * curr->mvInvScaleFactors[search_level];
+            bool success = ygz::Align2D(curr->mvImagePyramid[search_level], _patch_with_border, _patch, 10, px_scaled);
+            float opx[2] = {px_curr[0] * curr->mvInvScaleFactors[search_level],
+                            px_curr[1] * curr->mvInvScaleFactors[search_level]};
+            const int ook = ygzo_align2d(img.data, img.cols, img.rows, (int)img.step[0], _patch_with_border, _patch, 10,
+                                         opx);
+            same += (int)success == ook && px_scaled[0] == opx[0] && px_scaled[1] == opx[1];
+            conv += success;
+        }
+        CHECK(tried >= 20 && same == tried && conv > tried / 2,
+              "ygz::Align2D(curr->mvImagePyramid[search_level], ...): %d / %d bit-exact with the oracle, %d converged",
+              same, tried, conv);
+    }
+
+    std::printf(fails ? "FAILED %d\n" : "OK\n", fails);
+    return fails ? 1 : 0;
+}
