@@ -1,10 +1,11 @@
 """Batched SparseImgAlign (ygzfe_batch_sparse_align, the bench path) vs the oracle, pair by pair.
 
 SparseImgAlign::run (SparseImageAlign.cc:20-49) of frame k-1 -> k for every pair of a resident
-batch; pose within 1e-4 (|log(T_gpu^-1 T_cpu)|_inf) and the same visible-feature count.  Levels
-3..1 of C2 fit the LDS-staged kernel (k_sparse_align_lds); levels 3..0 take k_sparse_align_reg
-(level 0 is larger than the LDS image budget).  Fast motion makes features leave the image during
-the iterations, which exercises the out-of-bounds H correction.
+batch; pose within 1e-4 (|log(T_gpu^-1 T_cpu)|_inf) and the same visible-feature count.  Up to 960
+reference features per pair run in k_sparse_align_reg's register / LDS form (one feature per thread
+of waves 1..15); more take its generic path (sparse_align_generic: global scratch, Eigen's pivoted
+LDLT), exercised here with 2000-feature extractions.  Fast motion makes features leave the image
+during the iterations, which exercises the out-of-bounds H correction.
 """
 import numpy as np
 import pytest
@@ -17,9 +18,10 @@ POSE_TOL = 1e-4
 XI = np.array([0.012, -0.006, 0.009, 0.0025, -0.002, 0.0015], np.float32)
 
 
-def run_batch_align(gpu, F, stride, max_level, min_level, usable_frac=1.0, seed=11):
+def run_batch_align(gpu, F, stride, max_level, min_level, usable_frac=1.0, seed=11, nfeatures=None):
     import torch
     W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    nf = nfeatures or nf
     sc = S.PlaneScene(seed, W, H)
     poses = [gpu.trajectory_pose(k * stride, XI) for k in range(F)]
     frames = np.stack([sc.render(q, t, noise_seed=k) for k, (q, t) in enumerate(poses)])
@@ -84,3 +86,11 @@ def test_batch_align_partial_usable(gpu):
 def test_batch_align_level0_register_kernel(gpu):
     """Level 0 (752x480) exceeds the LDS image budget: the register-resident kernel runs."""
     run_batch_align(gpu, F=3, stride=1, max_level=2, min_level=0)
+
+
+def test_batch_align_generic_path_over_960_features(gpu):
+    """ORBextractor(2000, 2.0, 4) on 752x480: ~1900 reference features per pair (> 960), so every
+    pair runs sparse_align_generic; levels 3..1 and 2..0."""
+    errs, nvis = run_batch_align(gpu, F=4, stride=1, max_level=3, min_level=1, nfeatures=2000, seed=5)
+    assert (nvis > 960).all()
+    run_batch_align(gpu, F=3, stride=2, max_level=2, min_level=0, nfeatures=2000, seed=6, usable_frac=0.8)

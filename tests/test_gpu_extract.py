@@ -158,3 +158,27 @@ def test_batch_blur_every_pixel(gpu, size, cfg, blur):
             if not np.array_equal(got, want):
                 bad = np.argwhere(got != want)
                 raise AssertionError(f"frame {i} level {l} {lv.shape}: {len(bad)} px differ, first {bad[:5].tolist()}")
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C4"])
+@pytest.mark.parametrize("kind", ["uniform", "checker"])
+def test_dense_noise_frames_capacity(gpu, cfg, kind):
+    """Worst-case FAST density: uniform noise (most pixels are corners at minTh 7 / iniTh 20) and
+    a 1-px checkerboard with noise.  The per-cell candidate slots and the per-level key limit
+    must hold whatever the image; extraction stays bit-exact with the oracle."""
+    W, H, ex, orc = make(gpu, cfg)
+    rng = np.random.default_rng(99)
+    if kind == "uniform":
+        img = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    else:
+        yy, xx = np.mgrid[0:H, 0:W]
+        img = np.where((xx + yy) % 2 == 0, 200, 40).astype(np.int32) + rng.integers(-12, 13, (H, W))
+        img = np.clip(img, 0, 255).astype(np.uint8)
+    k, d = ex.extract(ex.ComputePyramid(img))
+    rk, rd = orc.extract(orc.pyramid(img))
+    assert_kps_equal(k, rk, f"{cfg} {kind}")
+    assert np.array_equal(d, rd)
+    assert len(k) >= 0.5 * CONFIG_NF[cfg]
+
+
+CONFIG_NF = {c: S.CONFIGS[c][2] for c in S.CONFIGS}
