@@ -375,9 +375,11 @@ def main():
     pipeline_gbps = (b_extract + b_align) * (fps / world) / 1e9
 
     # host copies of a bounded prefix of the rendered sequence for the single-frame legs
+    # and the CPU baseline (its multi-thread leg gets ~24 frames per host thread)
     n_host = 0
     if rank == 0 and world == 1:
-        n_host = min(F, max(args.cpu_sample, args.latency_frames + 12, 16))
+        n_host = min(F, max(args.cpu_sample, args.latency_frames + 12, 16,
+                            24 * min(16, host_cpu_info()[2]) if args.cpu_sample > 0 else 0))
     frames = np.stack([batch.read_level(i, 0) for i in range(n_host)]) if n_host else None
 
     # ------------------------------------------------ §8(f) rank 1: undistort remap
@@ -443,10 +445,10 @@ def main():
     # ------------------------------------------------ CPU baseline (rank 0, N = 1)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(frames, poses, S, args, sc)
+        cpu = cpu_baseline(frames, r3[:n_host], cz[:n_host], S, args, sc)
 
     if lat is not None and cpu is not None:
-        cpu_lat = cpu["ms_extract"] + cpu["ms_align"]
+        cpu_lat = cpu["ms_pyramid"] + cpu["ms_extract"] + cpu["ms_align"]
         lat["cpu_port_ms"] = round(cpu_lat, 3)
         lat["speedup_vs_cpu_port"] = round(cpu_lat / lat["median_ms"], 2)
     if rank == 0:
@@ -774,50 +776,78 @@ def direct_leg(S, with_cpu, reps=50):
     return line
 
 
-def cpu_baseline(frames, poses, S, args, sc):
-    """oracle/ restatement, single thread: extract (C2) + SparseImgAlign (C3) per frame."""
+def host_cpu_info():
+    """lscpu model name and CPU counts (the whole machine, and this process's affinity)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, aff
+
+
+def cpu_baseline(frames, r3, cz, S, args, sc):
+    """oracle/ restatement driven from C (oracle/bench.c, no per-stage Python hops):
+    pyramid + ORB (C2) + Hamming vs the previous frame + SparseImgAlign 3..1 per frame.
+    1 thread over the sample (the reference's single Tracking thread: per-frame latency),
+    then T threads (min(16, this process's CPUs): the box's CPU share) over the same frames
+    split in contiguous chunks (throughput).  Plus the FAST sanity check of SURVEY.md §8d:
+    the restated cv::FAST vs the reference's own SSE2 FAST-10 (oracle/_ref) on test1.png."""
     import _oracle as O
-    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
-    orc = O.OrbOracle(nf, sf, nl, ini, mn)
-    cam = O.Cam(*sc.cam)
-    fx, fy, cx, cy = sc.cam
-    T0 = O.se3_from((0, 0, 0, 1), (0, 0, 0))
-    n = 0
-    t0 = time.perf_counter()
-    prev = None
-    t_ext = t_ham = t_al = 0.0
-    n_al = 0
-    while n < min(args.cpu_sample, len(frames)):
-        ta = time.perf_counter()
-        lv = orc.pyramid(frames[n])
-        kps, desc = orc.extract(lv)
-        t_ext += time.perf_counter() - ta
-        if prev is not None:
-            plv, pk, pdesc = prev
-            ta = time.perf_counter()
-            O.hamming_best2(desc, pdesc)
-            t_ham += time.perf_counter() - ta
-            q, t = poses[n - 1]
-            qi, ti = S.se3_inv(q.astype(np.float64), t.astype(np.float64))
-            R_wc = np.array([S.quat_rot(qi, e) for e in np.eye(3)]).T
-            d = np.stack([(pk["x"] - cx) / fx, (pk["y"] - cy) / fy, np.ones(len(pk))], 1)
-            lam = (S.PLANE_Z - ti[2]) / (d @ R_wc[2])
-            xyz = (d * lam[:, None]).astype(np.float32)
-            ta = time.perf_counter()
-            O.sparse_align(plv, lv, orc.inv_scale, cam, pk, xyz, np.ones(len(pk), np.uint8), 3, 1, T0)
-            t_al += time.perf_counter() - ta
-            n_al += 1
-        prev = (lv, kps, desc)
-        n += 1
-        if time.perf_counter() - t0 > args.cpu_budget_s:
-            break
-    el = time.perf_counter() - t0
-    return {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} frames of the same rendered C2 sequence: pyramid + octree ORB + rBRIEF + Hamming vs "
-                      f"previous frame + SparseImgAlign 3..1, oracle/ (gcc -O3 -march=native), 1 thread",
-            "ms_per_frame": round(el * 1e3 / n, 3),
-            "ms_extract": round(t_ext * 1e3 / n, 3), "ms_hamming": round(t_ham * 1e3 / max(1, n_al), 3),
-            "ms_align": round(t_al * 1e3 / max(1, n_al), 3)}
+    cfg = S.CONFIGS["C2"]
+    model, ncpu, aff = host_cpu_info()
+    threads = max(1, min(16, aff))
+    n1 = min(args.cpu_sample, len(frames))
+    wall1, st1 = O.bench_pipeline(frames[:n1], sc.cam, S.PLANE_Z, r3[:n1], cz[:n1], cfg, 1)
+    per = 1e3 / max(1, st1.frames)
+    perp = 1e3 / max(1, st1.pairs)
+    nmt = len(frames)
+    # untimed warm pass: the first threaded run pays each thread's malloc-arena
+    # first-touch page faults (measured ~6x slower per thread), not pipeline work
+    O.bench_pipeline(frames[:2 * threads], sc.cam, S.PLANE_Z, r3[:2 * threads], cz[:2 * threads], cfg, threads)
+    wallt, stt = O.bench_pipeline(frames, sc.cam, S.PLANE_Z, r3[:nmt], cz[:nmt], cfg, threads)
+    line = {"value": round(stt.frames / wallt, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{nmt} frames of the same rendered C2 sequence on {threads} threads (contiguous chunks; "
+                      f"{n1} frames on 1 thread for the latency): pyramid + octree ORB + rBRIEF + Hamming vs previous "
+                      f"frame + SparseImgAlign 3..1, oracle/ (gcc -O3 -march=native, scalar)",
+            "cpu_model": model, "host_cpus": ncpu, "process_cpus": aff,
+            "single_thread_frames_per_s": round(st1.frames / wall1, 2),
+            "ms_per_frame": round(wall1 * 1e3 / max(1, st1.frames), 3),
+            "ms_pyramid": round(st1.t_pyr * per, 3), "ms_extract": round(st1.t_extract * per, 3),
+            "ms_hamming": round(st1.t_hamming * perp, 3), "ms_align": round(st1.t_align * perp, 3),
+            "threads_frames_per_s": round(stt.frames / wallt, 2)}
+    # FAST sanity (SURVEY.md §6: SSE2 FAST-10 0.130 / 0.433 ms on test1.png at threshold 75 / 20)
+    try:
+        from PIL import Image
+        img = np.array(Image.open(os.path.join(ROOT, "tests", "golden", "test1.png")))
+        H, W = img.shape
+        fs = {}
+        for th in (75, 20):
+            n9, t9 = O.bench_fast9(img, th, reps=20)
+            fs[f"oracle_fast9_th{th}_ms"] = round(t9 * 1e3, 4)
+            fs[f"oracle_fast9_th{th}_corners"] = n9
+            if O.RefFast.available():
+                ref = O.RefFast()
+                for _ in range(3):
+                    ref.detect(img, th, sse=True, x0=3, y0=3, w=W - 6, h=H - 6)
+                t0 = time.perf_counter()
+                for _ in range(20):
+                    xs, _ = ref.detect(img, th, sse=True, x0=3, y0=3, w=W - 6, h=H - 6)
+                fs[f"ref_fast10_sse2_th{th}_ms"] = round((time.perf_counter() - t0) / 20 * 1e3, 4)
+                fs[f"ref_fast10_sse2_th{th}_corners"] = int(len(xs))
+        fs["note"] = ("oracle = cv::FAST TYPE_9_16 + score + 3x3 NMS restated (FAST_t's pair screening, scalar); "
+                      "ref = the reference's own Thirdparty/fast SSE2 FAST-10 detect (oracle/_ref), detect only")
+        line["fast_sanity"] = fs
+    except Exception as e:  # test image / reference library absent
+        line["fast_sanity"] = {"skipped": str(e)}
+    return line
 
 
 if __name__ == "__main__":

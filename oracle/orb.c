@@ -200,19 +200,39 @@ int ygzo_corner_score16(const uint8_t *ptr, int stride, int threshold) {
 }
 
 /* Segment test of FAST_t: >8 contiguous (of the 25-long wrapped ring) darker
- * than v-t, or brighter than v+t. */
+ * than v-t, or brighter than v+t.  The opposite-pair screening in front is
+ * FAST_t's own (fast.cpp: d = tab[p0] | tab[p8], &= the pairs 2/10, 4/12,
+ * 6/14, then 1/9 .. 7/15): a necessary condition, so it only skips pixels the
+ * full test rejects. */
 static int fast9_test(const uint8_t *p, const int pix[25], int threshold) {
     int v = p[0];
-    int vt = v - threshold, count = 0;
-    for (int k = 0; k < 25; k++) {
-        if (p[pix[k]] < vt) { if (++count > 8) return 1; }
-        else count = 0;
+    const int lo = v - threshold, hi = v + threshold;
+#define YGZO_CLS(k) ((p[pix[k]] < lo ? 1 : 0) | (p[pix[k]] > hi ? 2 : 0))
+    int d = YGZO_CLS(0) | YGZO_CLS(8);
+    if (d == 0) return 0;
+    d &= YGZO_CLS(2) | YGZO_CLS(10);
+    d &= YGZO_CLS(4) | YGZO_CLS(12);
+    d &= YGZO_CLS(6) | YGZO_CLS(14);
+    if (d == 0) return 0;
+    d &= YGZO_CLS(1) | YGZO_CLS(9);
+    d &= YGZO_CLS(3) | YGZO_CLS(11);
+    d &= YGZO_CLS(5) | YGZO_CLS(13);
+    d &= YGZO_CLS(7) | YGZO_CLS(15);
+#undef YGZO_CLS
+    if (d == 0) return 0;
+    int count = 0;
+    if (d & 1) {
+        for (int k = 0; k < 25; k++) {
+            if (p[pix[k]] < lo) { if (++count > 8) return 1; }
+            else count = 0;
+        }
     }
-    vt = v + threshold;
     count = 0;
-    for (int k = 0; k < 25; k++) {
-        if (p[pix[k]] > vt) { if (++count > 8) return 1; }
-        else count = 0;
+    if (d & 2) {
+        for (int k = 0; k < 25; k++) {
+            if (p[pix[k]] > hi) { if (++count > 8) return 1; }
+            else count = 0;
+        }
     }
     return 0;
 }
@@ -558,21 +578,34 @@ static inline int reflect101(int i, int n) {
 void ygzo_gaussian_blur7(const uint8_t *src, int w, int h, int stride, uint8_t *dst,
                          int dstride, int variant) {
     const int *k = variant == YGZO_BLUR_CV3_ROUNDED ? kBlurCV3 : kBlurCV4;
+    /* horizontal pass into int rows: border columns through reflect101, the
+     * interior as a straight 7-tap loop (same sums, vectorisable) */
     int *rows = (int *)malloc(sizeof(int) * (size_t)w * h);
     for (int y = 0; y < h; y++) {
         const uint8_t *s = src + (size_t)y * stride;
+        int *r = rows + (size_t)y * w;
         for (int x = 0; x < w; x++) {
+            if (x == 3 && w - 3 > 3) x = w - 3;  /* the interior is done below */
             int acc = 0;
             for (int t = 0; t < 7; t++) acc += k[t] * s[reflect101(x + t - 3, w)];
-            rows[(size_t)y * w + x] = acc;
+            r[x] = acc;
+        }
+        for (int x = 3; x < w - 3; x++)
+            r[x] = k[0] * s[x - 3] + k[1] * s[x - 2] + k[2] * s[x - 1] + k[3] * s[x] + k[4] * s[x + 1] +
+                   k[5] * s[x + 2] + k[6] * s[x + 3];
+    }
+    /* vertical pass: 7 row pointers (reflect101 at the top / bottom) */
+    for (int y = 0; y < h; y++) {
+        const int *rr[7];
+        for (int t = 0; t < 7; t++) rr[t] = rows + (size_t)reflect101(y + t - 3, h) * w;
+        uint8_t *o = dst + (size_t)y * dstride;
+        for (int x = 0; x < w; x++) {
+            long long acc = (long long)k[0] * rr[0][x] + (long long)k[1] * rr[1][x] + (long long)k[2] * rr[2][x] +
+                            (long long)k[3] * rr[3][x] + (long long)k[4] * rr[4][x] + (long long)k[5] * rr[5][x] +
+                            (long long)k[6] * rr[6][x];
+            o[x] = (uint8_t)clampi((int)((acc + 32768) >> 16), 0, 255);
         }
     }
-    for (int y = 0; y < h; y++)
-        for (int x = 0; x < w; x++) {
-            long long acc = 0;
-            for (int t = 0; t < 7; t++) acc += (long long)k[t] * rows[(size_t)reflect101(y + t - 3, h) * w + x];
-            dst[(size_t)y * dstride + x] = (uint8_t)clampi((int)((acc + 32768) >> 16), 0, 255);
-        }
     free(rows);
 }
 

@@ -261,6 +261,20 @@ void ygzo_undistort_map(const float cam[4], const float *dist, int ndist, int W,
 void ygzo_remap_linear(const uint8_t *src, int W, int H, int sstride, const int16_t *map1, const uint16_t *map2,
                        int DW, int DH, uint8_t *dst, int dstride);
 
+/* ---------------- CPU baseline driver (oracle/bench.c, bench.py's cpu_baseline) ---------------- */
+typedef struct ygzo_bench_stats {
+    double t_pyr, t_extract, t_hamming, t_align; /* summed over threads, seconds */
+    int frames, pairs;
+    long long keypoints, visible;
+} ygzo_bench_stats;
+/* pyramid + ORB + Hamming vs previous + SparseImgAlign (nlevels-1 .. 1) per frame of
+ * frames[n][H][W] on `threads` threads (contiguous chunks); map points of frame g
+ * on the plane Z_w = plane_z through r3[3g], cz[g].  Returns the wall time (s). */
+double ygzo_bench_pipeline(const uint8_t *frames, int n, int W, int H, const float cam[4], float plane_z,
+                           const float *r3, const float *cz, int nfeatures, float scale, int nlevels, int ini,
+                           int min_th, int threads, ygzo_bench_stats *stats);
+int ygzo_bench_fast9(const uint8_t *img, int w, int h, int threshold, int reps, double *seconds);
+
 #ifdef __cplusplus
 }
 #endif

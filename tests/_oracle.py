@@ -460,3 +460,34 @@ class RefFast:
         keep = np.zeros(max(1, len(xs)), np.int32)
         n = self.lib.ref_fast10_nonmax(_p(xs), _p(ys), _p(scores), len(xs), _p(keep))
         return keep[:n].copy()
+
+
+# ---------------------------------------------------------------- CPU baseline driver (oracle/bench.c)
+class BenchStats(C.Structure):
+    _fields_ = [("t_pyr", C.c_double), ("t_extract", C.c_double), ("t_hamming", C.c_double), ("t_align", C.c_double),
+                ("frames", C.c_int), ("pairs", C.c_int), ("keypoints", C.c_longlong), ("visible", C.c_longlong)]
+
+
+def bench_pipeline(frames, cam, plane_z, r3, cz, cfg, threads=1):
+    """The per-frame hot path of the restatement over frames[n][H][W] on `threads`
+    host threads (contiguous chunks) -> (wall seconds, BenchStats)."""
+    frames = np.ascontiguousarray(frames, np.uint8)
+    n, H, W = frames.shape
+    W_, H_, nf, sf, nl, ini, mn = cfg
+    c = (C.c_float * 4)(*[float(v) for v in cam])
+    r3 = np.ascontiguousarray(r3, np.float32)
+    cz = np.ascontiguousarray(cz, np.float32)
+    st = BenchStats()
+    L = lib()
+    L.ygzo_bench_pipeline.restype = C.c_double
+    wall = L.ygzo_bench_pipeline(_p(frames), n, W, H, c, C.c_float(plane_z), _p(r3), _p(cz), nf, C.c_float(sf), nl,
+                                 ini, mn, threads, C.byref(st))
+    return wall, st
+
+
+def bench_fast9(img, threshold, reps=20):
+    """cv::FAST(img, threshold, nonmax) restated, timed -> (corners, mean seconds)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    s = C.c_double()
+    n = lib().ygzo_bench_fast9(_p(img), img.shape[1], img.shape[0], threshold, reps, C.byref(s))
+    return n, s.value
