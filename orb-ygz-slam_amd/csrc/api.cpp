@@ -140,7 +140,7 @@ struct Workspace {
         YGZ_TRY(candA.ensure((size_t)F * P.cand_total * 4 + 16));
         YGZ_TRY(candB.ensure((size_t)F * P.cand_total * 4 + 16));
         YGZ_TRY(sel.ensure((size_t)F * P.sel_total * 4 + 16));
-        YGZ_TRY(selcnt.ensure((size_t)F * P.nlevels * 4 + 16));
+        YGZ_TRY(selcnt.ensure((size_t)F * P.nlevels * 4 + 128));  // tail: k_orient_desc's 8-int scalar load
         YGZ_TRY(kps.ensure((size_t)F * rows * sizeof(ygzfe_kp) + 16));
         YGZ_TRY(desc.ensure((size_t)F * rows * 32 + 16));
         YGZ_TRY(counts.ensure((size_t)F * 4 + 16));
@@ -694,6 +694,33 @@ int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, voi
 int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream) {
     // everything complete on `stream` when the last launch retires
     return ygzfe_batch_extract_split(b, n_frames, stream, stream);
+}
+
+// Measurement helper (tools/mb_fast.py): the FAST stage alone over the first
+// n_frames resident frames (pyramid levels built first when build_pyramid),
+// `reps` back-to-back launch sets on the batch stream, average ms per set
+// (hipEvents).  Writes only the pyramid and the FAST cell scratch.
+int ygzfe_diag_fast_ms(ygzfe_batch *b, int n_frames, int reps, int build_pyramid, float *ms) {
+    if (!b || !ms || n_frames < 1 || n_frames > b->maxF || reps < 1) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    YGZ_TRY(ensure_device(b->device));
+    const PlanDev &pd = *b->plan;
+    const Plan &P = pd.hp();
+    if (build_pyramid)
+        YGZ_HIP(launch_pyramid(b->pyr.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), pd.tabs.as<int>(), n_frames, b->stream));
+    hipEvent_t e0, e1;
+    YGZ_HIP(hipEventCreate(&e0));
+    YGZ_HIP(hipEventCreate(&e1));
+    YGZ_HIP(hipEventRecord(e0, b->stream));
+    for (int r = 0; r < reps; r++)
+        YGZ_HIP(launch_fast(b->pyr.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(),
+                            b->ws.cellbuf.as<uint32_t>(), b->ws.cellcnt.as<int>(), n_frames, b->stream));
+    YGZ_HIP(hipEventRecord(e1, b->stream));
+    YGZ_HIP(hipEventSynchronize(e1));
+    YGZ_HIP(hipEventElapsedTime(ms, e0, e1));
+    *ms /= reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return YGZFE_OK;
 }
 
 int ygzfe_batch_check(ygzfe_batch *b) {

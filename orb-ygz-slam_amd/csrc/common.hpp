@@ -48,7 +48,7 @@ struct LevelDesc {
     int fast_rw, fast_rh;  // largest FAST cell ROI width / height of this level
 };
 
-struct CellDesc {
+struct alignas(16) CellDesc {
     int16_t x0, y0, rw, rh;   // ROI origin / size in level pixels
     int16_t offx, offy;       // j*wCell, i*hCell (key coordinates relative to minBorder)
     int16_t level, pad;
@@ -83,6 +83,25 @@ using gptr_t = const __attribute__((address_space(1))) T *;
 template <class T>
 __device__ __forceinline__ gptr_t<T> as_global(const T *p) {
     return (gptr_t<T>)p;
+}
+// a * b + c on 24-bit operands (v_mad_u32_u24, full rate); inline asm so the
+// compiler cannot widen it into a quarter-rate v_mad_u64_u32
+__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm volatile("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+// read-only data at a wave-uniform address through the scalar cache (constant
+// address space: s_load, no vector-memory round trip)
+template <class T>
+using cptr_t = const __attribute__((address_space(4))) T *;
+template <class T>
+__device__ __forceinline__ T scalar_load(const T *p) {
+    // dword-granular (s_load needs 4-B alignment; the records here are 4-B aligned)
+    static_assert(sizeof(T) % 4 == 0, "scalar_load: dword-sized records only");
+    struct W { uint32_t d[sizeof(T) / 4]; };
+    return __builtin_bit_cast(T, *(cptr_t<W>)p);
 }
 
 // Diagnostic build only (make diag -> lib/libygzfe_diag.so): per-workgroup

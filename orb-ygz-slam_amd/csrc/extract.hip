@@ -424,20 +424,9 @@ __global__ __launch_bounds__(256) void k_blur7(const uint8_t *__restrict__ pyr,
 // FAST-9/16 + cornerScore<16> + 3x3 non-max suppression inside one cell ROI
 // (ORBextractor.cc:747-781).  One 256-thread workgroup per (cell, frame).
 
-__device__ __forceinline__ uint32_t run9(uint32_t m16) {
-    uint32_t x = m16 | (m16 << 16);
-    uint32_t y = x & (x >> 1);   // runs of 2
-    y &= y >> 2;                 // 4
-    y &= y >> 4;                 // 8
-    y &= x >> 8;                 // 9
-    return y & 0xFFFFu;
-}
 
-// FAST_t<16> segment test + cornerScore<16> closed form on a ROI tile of row
-// stride S (compile time, so every ring tap is an immediate ds_read offset from
-// q = centre - 3S - 3):
-//   corner  <=> 9 contiguous ring pixels all > v+t or all < v-t
-//   score   = max(t, max_arc9 min(v - r), max_arc9 min(r - v)) - 1
+// Ring taps on a ROI tile of row stride S (compile time, so every ring tap is
+// an immediate ds_read offset from q = centre - 3S - 3).
 template <int S>
 struct Ring {
     // Bresenham circle of radius 3 (cv::FAST order), offsets from q
@@ -448,40 +437,6 @@ struct Ring {
     }
     static constexpr int kCentre = 3 * S + 3;
 };
-
-template <int S>
-__device__ __forceinline__ bool fast9_is_corner(const uint8_t *q, int t) {
-    const int v = q[Ring<S>::kCentre];
-    uint32_t dark = 0, bright = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int d = q[Ring<S>::off(k)];
-        dark |= ((uint32_t)(d - (v - t)) >> 31) << k;    // d < v - t
-        bright |= ((uint32_t)((v + t) - d) >> 31) << k;  // d > v + t
-    }
-    return run9(dark) | run9(bright);
-}
-
-template <int S>
-__device__ __forceinline__ int fast9_corner_score(const uint8_t *q, int t) {
-    // e[k] = r_k - v.  bright: max_k min(e[k..k+8]); dark: max_k min(-e[k..k+8])
-    // = -min_k max(e[k..k+8]).  4-wide windows first (v_min3/v_max3), so only
-    // e[] and one window array are live (keeps the kernel under 80 VGPRs).
-    const int v = q[Ring<S>::kCentre];
-    int e[16], w4[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) e[k] = (int)q[Ring<S>::off(k)] - v;
-#pragma unroll
-    for (int k = 0; k < 16; k++) w4[k] = min(min(e[k], e[(k + 1) & 15]), min(e[(k + 2) & 15], e[(k + 3) & 15]));
-    int best = t;
-#pragma unroll
-    for (int k = 0; k < 16; k++) best = max(best, min(min(w4[k], w4[(k + 4) & 15]), e[(k + 8) & 15]));
-#pragma unroll
-    for (int k = 0; k < 16; k++) w4[k] = max(max(e[k], e[(k + 1) & 15]), max(e[(k + 2) & 15], e[(k + 3) & 15]));
-#pragma unroll
-    for (int k = 0; k < 16; k++) best = max(best, -max(max(w4[k], w4[(k + 4) & 15]), e[(k + 8) & 15]));
-    return best - 1;
-}
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
@@ -500,31 +455,32 @@ __device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(
 // ROI staging: lane = (row offset, dword) with S/4 dwords per LDS row; each
 // lane reads the two aligned dwords around its 4 bytes (issue) and realigns
 // them with v_alignbyte into one ds_write_b32 (commit).  NI loads per lane.
+// Loads are buffer loads on the frame's level (wave-uniform descriptor, 32-bit
+// lane offsets, one 24-bit multiply-add per row; reads past the level return 0).
 template <int S, int R>
 struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI height)
     static constexpr int DW = S / 4, RPI = 64 / DW, NI = (R + RPI - 1) / RPI;
     uint32_t lo[NI], hi[NI];
-    __device__ __forceinline__ void issue(const uint8_t *src, int w, int rw, int rh, int lane) {
+    __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, uint32_t off0, int w, int rw, int rh, int lane) {
         const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + 3) / 4;
 #pragma unroll
         for (int k = 0; k < NI; k++) {
             const int r = k * RPI + rlane;
             lo[k] = hi[k] = 0u;
             if (rlane < RPI && r < rh && dw < ndw) {
-                const uint8_t *pa = src + __umul24((uint32_t)r, (uint32_t)w) + 4 * dw;
-                const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(pa - ((uintptr_t)pa & 3u)));
-                lo[k] = q[0];
-                hi[k] = q[1];
+                const uint32_t o = (mad24((uint32_t)r, (uint32_t)w, off0) & ~3u) + 4u * (uint32_t)dw;
+                lo[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0);
+                hi[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4u, 0, 0);
             }
         }
     }
-    __device__ __forceinline__ void commit(uint8_t *img, const uint8_t *src, int w, int rw, int rh, int lane) const {
+    __device__ __forceinline__ void commit(uint8_t *img, uint32_t off0, int w, int rw, int rh, int lane) const {
         const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + 3) / 4;
 #pragma unroll
         for (int k = 0; k < NI; k++) {
             const int r = k * RPI + rlane;
             if (rlane < RPI && r < rh && dw < ndw) {
-                const uint32_t sh = (uint32_t)(((uintptr_t)(src + __umul24((uint32_t)r, (uint32_t)w))) & 3u);
+                const uint32_t sh = mad24((uint32_t)r, (uint32_t)w, off0) & 3u;
                 reinterpret_cast<uint32_t *>(img + r * S)[dw] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh);
             }
         }
@@ -598,25 +554,69 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             }
         }
         if (S == 40 && pass == 0) YGZ_BSTAMP_K(2, 4);
-        // B: full segment test, compacted in place (writes never pass the read front)
+#if defined(YGZ_FAST_STOP) && YGZ_FAST_STOP <= 1  // timing experiment only (never in the product build)
+        if (lane == 0) *cnt_out = 0;
+        return;
+#endif
+        // BC: segment test and score in one pass, two survivors per lane as packed
+        //     i16 pairs (low half list[i], high half list[i+1]), e[k] = r_k - v:
+        //       arcmax = max(max_k min(e[k..k+8]), max_k min(-e[k..k+8]))
+        //     corner (FAST_t<16>: 9 contiguous ring pixels all > v+t or all < v-t)
+        //     <=> arcmax > t, and then cornerScore<16> = max(t, arcmax) - 1 =
+        //     arcmax - 1, written to the score map.  Corners are compacted in place
+        //     in raster order (writes never pass the read front).
         int nc = 0;
-        for (int i0 = 0; i0 < na; i0 += 64) {
-            const int i = i0 + lane;
-            const uint16_t e = i < na ? list[i] : (uint16_t)0x0303;
-            const bool corner = i < na && fast9_is_corner<S>(img + ((e >> 8) - 3) * S + ((e & 0xFF) - 3), th);
-            const uint64_t m = __ballot(corner);
-            if (corner) list[nc + popc_below(m)] = e;
-            nc += __popcll(m);
+        for (int i0 = 0; i0 < na; i0 += 128) {
+            const int i = i0 + 2 * lane;
+            const uint32_t pr = reinterpret_cast<const uint32_t *>(list)[i >> 1];  // list[i], list[i+1]
+            const bool v0 = i < na, v1 = i + 1 < na;
+            const uint32_t e0 = v0 ? (pr & 0xFFFFu) : 0x0303u, e1 = v1 ? (pr >> 16) : 0x0303u;
+            // ring bases q = centre - 3S - 3: every tap an immediate, non-negative ds_read offset
+            const uint32_t b0 = ((e0 >> 8) - 3) * S + (e0 & 0xFFu) - 3, b1 = ((e1 >> 8) - 3) * S + (e1 & 0xFFu) - 3;
+            const uint32_t o0 = b0 + Ring<S>::kCentre, o1 = b1 + Ring<S>::kCentre;
+            const uint8_t *q0 = img + b0, *q1 = img + b1;
+            const s16x2 vc = as_s16x2((uint32_t)q0[Ring<S>::kCentre] | ((uint32_t)q1[Ring<S>::kCentre] << 16));
+            s16x2 e[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                e[k] = as_s16x2((uint32_t)q0[Ring<S>::off(k)] | ((uint32_t)q1[Ring<S>::off(k)] << 16)) - vc;
+            s16x2 m2[16], w4[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(e[k], e[(k + 1) & 15]);
+#pragma unroll
+            for (int k = 0; k < 16; k++) w4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+            s16x2 bright = {-256, -256};
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                bright = __builtin_elementwise_max(
+                    bright, __builtin_elementwise_min(__builtin_elementwise_min(w4[k], w4[(k + 4) & 15]), e[(k + 8) & 15]));
+#pragma unroll
+            for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_max(e[k], e[(k + 1) & 15]);
+#pragma unroll
+            for (int k = 0; k < 16; k++) w4[k] = __builtin_elementwise_max(m2[k], m2[(k + 2) & 15]);
+            s16x2 darkmin = {256, 256};
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                darkmin = __builtin_elementwise_min(
+                    darkmin, __builtin_elementwise_max(__builtin_elementwise_max(w4[k], w4[(k + 4) & 15]), e[(k + 8) & 15]));
+            const s16x2 zero2 = {0, 0};
+            const s16x2 am = __builtin_elementwise_max(bright, zero2 - darkmin);
+            const bool c0 = v0 && am.x > th, c1 = v1 && am.y > th;
+            if (c0) sc[o0] = (uint8_t)(am.x - 1);
+            if (c1) sc[o1] = (uint8_t)(am.y - 1);
+            const uint64_t M0 = __ballot(c0), M1 = __ballot(c1);
+            const int pos = nc + popc_below(M0) + popc_below(M1);
+            if (c0) list[pos] = (uint16_t)e0;
+            if (c1) list[pos + (c0 ? 1 : 0)] = (uint16_t)e1;
+            nc += __popcll(M0) + __popcll(M1);
         }
         if (S == 40 && pass == 0) YGZ_BSTAMP_K(2, 5);
-        // C: scores of the corners
-        for (int i = lane; i < nc; i += 64) {
-            const uint16_t e = list[i];
-            const int off = (e >> 8) * S + (e & 0xFF);
-            sc[off] = (uint8_t)fast9_corner_score<S>(img + off - Ring<S>::kCentre, th);
-        }
+#if defined(YGZ_FAST_STOP) && YGZ_FAST_STOP <= 3
+        if (lane == 0) *cnt_out = 0;
+        return;
+#endif
         wave_lds_order();
-        if (S == 40 && pass == 0) YGZ_BSTAMP_K(2, 6);  // after C
+        if (S == 40 && pass == 0) YGZ_BSTAMP_K(2, 6);
         // D: strict 3x3 NMS over the corner list
         for (int i0 = 0; i0 < nc; i0 += 64) {
             const int i = i0 + lane;
@@ -656,26 +656,35 @@ template <int S, int R>
 __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(YGZ_FAST_WAVES_EU))) void k_fast_cells(
     const uint8_t *__restrict__ pyr, uint32_t pitch, const Plan *__restrict__ plan,
     const CellDesc *__restrict__ cells, uint32_t *__restrict__ cellbuf, int *__restrict__ cellcnt, int cell_begin,
-    int cell_end) {
+    int cell_end, int level) {
     extern __shared__ uint8_t s_dyn[];
     constexpr int slice = (2 * S * R + 2 * (S - 6) * (R - 6) + 15) / 16 * 16;  // 16-B aligned slices
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // wave-uniform cell index: the CellDesc and the level record come by scalar
+    // loads (vector loads here put two dependent global round trips in front of
+    // the ROI loads)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     const int c = cell_begin + blockIdx.x * kFastWaves + wave;
     if (c >= cell_end) return;
     uint8_t *img = s_dyn + wave * slice;
     uint8_t *sc = img + S * R;
     uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * R);
-    const CellDesc cd = cells[c];
-    const LevelDesc &L = plan->lv[cd.level];
-    const uint8_t *src = pyr + (size_t)f * pitch + L.off + (size_t)cd.y0 * L.w + cd.x0;
+    const CellDesc cd = scalar_load(cells + c);
+    const LevelDesc &L = plan->lv[level];  // one launch per level: loaded beside cd, not after it
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(pyr + (size_t)f * pitch + L.off), 0, (int)((uint32_t)L.w * (uint32_t)L.h), 0x00020000);
+    const uint32_t off0 = (uint32_t)cd.y0 * (uint32_t)L.w + (uint32_t)cd.x0;  // ROI origin in the level
     if (S == 40) YGZ_BSTAMP_K(2, 0);
     {
         RoiStage<S, R> st;
-        st.issue(src, L.w, cd.rw, cd.rh, lane);
-        st.commit(img, src, L.w, cd.rw, cd.rh, lane);
+        st.issue(rs, off0, L.w, cd.rw, cd.rh, lane);
+        st.commit(img, off0, L.w, cd.rw, cd.rh, lane);
     }
     if (S == 40) YGZ_BSTAMP_K(2, 3);
+#if defined(YGZ_FAST_STOP) && YGZ_FAST_STOP <= 0
+    if (lane == 0) cellcnt[(size_t)f * plan->ncells + c] = img[lane * 7] == 255 ? 1 : 0;  // keep the staging live
+    return;
+#endif
     fast_cell_item<S>(plan, cd, img, sc, list, cellbuf + ((size_t)f * plan->ncells + c) * plan->cell_cap,
                       cellcnt + (size_t)f * plan->ncells + c, lane);
     if (S == 40) YGZ_BSTAMP_K(2, 1);
@@ -1194,6 +1203,13 @@ __device__ __forceinline__ int row16_sum(int v) {
 }
 
 constexpr int kPatchStride = 64;  // LDS row of a staged keypoint window: 4 x 16 B (window + 16-B misalignment)
+constexpr int kPatchBytes = 37 * kPatchStride;
+
+// byte offset of row r in a swizzled window (Window::store<true>)
+__device__ __forceinline__ uint32_t patch_row_swz(uint32_t r) {
+    return r * kPatchStride + ((r >> 2) << 4);
+}
+static_assert(30 * kPatchStride + (30 >> 2) * 16 + kPatchStride <= kPatchBytes, "swizzled IC window fits the slot");
 
 // A keypoint window (rows cy-R .. cy-R+NROWS-1) as 4 lanes x 16 B per row, each
 // row the 64 B at ((img + (cy-R+r)*w + cx-R) & ~15): loaded into registers by
@@ -1201,13 +1217,6 @@ constexpr int kPatchStride = 64;  // LDS row of a staged keypoint window: 4 x 16
 // unshifted to LDS by store_window (tap (r, c) at P[r*64 + o(r) + c]).
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// a * b + c on 24-bit operands (v_mad_u32_u24, full rate); inline asm so the
-// compiler cannot widen it into a quarter-rate v_mad_u64_u32
-__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t d;
-    asm volatile("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
-}
 
 template <int R, int NROWS>
 struct Window {
@@ -1225,12 +1234,19 @@ struct Window {
             v[k] = as_global(reinterpret_cast<const u32x4 *>(img + o))[0];
         }
     }
+    // SWZ: row r at 64 r + 16 (r >> 2) (patch_row_swz), so that the 16 rows a
+    // keypoint's lanes read together fall on 16 different bank groups (a 64-B
+    // row stride alone puts rows r, r+4, r+8, ... on the same banks); rows stay
+    // 16-B aligned and never overlap (31 IC rows: 2,096 B <= the 37-row window)
+    template <bool SWZ>
     __device__ __forceinline__ void store(uint8_t *P, int s) const {
         const int j = s & 3, r0 = s >> 2;
 #pragma unroll
-        for (int k = 0; k + 1 < NK; k++) *reinterpret_cast<u32x4 *>(P + (r0 + 4 * k) * kPatchStride + 16 * j) = v[k];
+        for (int k = 0; k + 1 < NK; k++)
+            *reinterpret_cast<u32x4 *>(P + (r0 + 4 * k) * kPatchStride + (SWZ ? 16 * k : 0) + 16 * j) = v[k];
         if (r0 + 4 * (NK - 1) < NROWS)
-            *reinterpret_cast<u32x4 *>(P + (r0 + 4 * (NK - 1)) * kPatchStride + 16 * j) = v[NK - 1];
+            *reinterpret_cast<u32x4 *>(P + (r0 + 4 * (NK - 1)) * kPatchStride + (SWZ ? 16 * (NK - 1) : 0) +
+                                       16 * j) = v[NK - 1];
         wave_lds_order();
     }
 };
@@ -1281,7 +1297,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
                                                      const int *__restrict__ n_existing,
                                                      ygzfe_kp *__restrict__ kps, uint8_t *__restrict__ desc,
                                                      int *__restrict__ counts, int row_cap) {
-    __shared__ uint8_t s_patch[16][37 * kPatchStride];  // one 37x37 window per keypoint row
+    __shared__ uint8_t s_patch[16][kPatchBytes];  // one 37x37 window per keypoint row
     YGZ_BSTAMP_K(1, 0);
     int bx, f;
     swizzled_block_2d(bx, f);  // one frame's keypoints on one XCD: patch lines shared in its L2
@@ -1290,16 +1306,30 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     const int nl = plan->nlevels;
     const int *sc = selcnt + (size_t)f * nl;
     const int ne = n_existing ? n_existing[f] : 0;
-    // per-level counts, inclusive prefix over lanes 0..15 (DPP row_shr inside the first row)
-    int incl = lane < nl ? sc[lane] : 0;
-    incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, false);
-    incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, false);
-    incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, false);
-    incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, false);
     int l = 0, pre = 0;
-    for (int q = 0; q < nl; q++) {
-        const int iq = __builtin_amdgcn_readlane(incl, q);
-        if (iq <= idx) { l = q + 1; pre = iq; }
+    if (nl <= 8) {
+        // the frame's per-level counts by one scalar load (selcnt carries >= 8
+        // ints of tail padding), inclusive prefix in SGPRs: no vector-memory
+        // round trip ahead of the key load
+        struct Cnt8 { int v[8]; };
+        const Cnt8 c8 = scalar_load(reinterpret_cast<const Cnt8 *>(sc));
+        int iq = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            iq += q < nl ? c8.v[q] : 0;
+            if (q < nl && iq <= idx) { l = q + 1; pre = iq; }
+        }
+    } else {
+        // per-level counts, inclusive prefix over lanes 0..15 (DPP row_shr inside the first row)
+        int incl = lane < nl ? sc[lane] : 0;
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, false);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, false);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, false);
+        incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, false);
+        for (int q = 0; q < nl; q++) {
+            const int iq = __builtin_amdgcn_readlane(incl, q);
+            if (iq <= idx) { l = q + 1; pre = iq; }
+        }
     }
     if (l >= nl || ne + idx >= row_cap) return;  // whole rows leave together
     const LevelDesc &L = plan->lv[l];
@@ -1332,7 +1362,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     wic.load(img, w, cx, cy, s);  // both windows in flight before the first wait
     wdesc.load(bimg, w, cx, cy, s);
     {
-        wic.store(P, s);
+        wic.store<true>(P, s);
         YGZ_BSTAMP_K(1, 4);
         // IC_Angle (ORBextractor.cc:77-101): lane s takes the window rows 15 +- (s+1)
         // (lane 15 the centre row).  Per row, with I the 31 row bytes (32nd
@@ -1345,7 +1375,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
         const uint32_t W1[8] = {wq[2].x, wq[2].y, wq[2].z, wq[2].w, wq[3].x, wq[3].y, wq[3].z, wq[3].w};
         auto row_sums = [&](int r, uint32_t &s0, uint32_t &s1) {
             const uint32_t o = mad24((uint32_t)r, (uint32_t)w, o0) & 15u;  // window start inside LDS row r
-            const uint32_t *d = reinterpret_cast<const uint32_t *>(P + r * kPatchStride + (o & ~3u));
+            const uint32_t *d = reinterpret_cast<const uint32_t *>(P + patch_row_swz((uint32_t)r) + (o & ~3u));
             uint32_t dw[9];
 #pragma unroll
             for (int k = 0; k < 9; k++) dw[k] = d[k];
@@ -1371,7 +1401,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     // computeOrbDescriptor (ORBextractor.cc:105-149) on the blurred level
     YGZ_BSTAMP_K(1, 5);
     wave_lds_order();  // IC taps read before the window is replaced
-    wdesc.store(P, s);
+    wdesc.store<false>(P, s);
     const uint32_t o0 = (uint32_t)(uintptr_t)bimg + __umul24((uint32_t)(cy - 18), (uint32_t)w) + (uint32_t)(cx - 18);
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float ang = angle * factorPI;
@@ -1511,7 +1541,7 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
         // level 0 on the caller's stream, the others spread over the given side streams
         const hipStream_t st = (l == 0 || !lvl_streams || n_lvl_streams <= 0) ? st0
                                                                                 : lvl_streams[(l - 1) % n_lvl_streams];
-#define YGZ_FAST(SS, RR) hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce)
+#define YGZ_FAST(SS, RR) hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce, l)
         if (S == 40 && R == 40) YGZ_FAST(40, 40);
         else if (S == 40 && R == 48) YGZ_FAST(40, 48);
         else if (S == 40 && R == 56) YGZ_FAST(40, 56);

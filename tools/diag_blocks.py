@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(ROOT, "orb-ygz-slam_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import ygzfe  # noqa: E402
 
-ygzfe.LIB_PATH = os.path.join(ROOT, "orb-ygz-slam_amd", "lib", "libygzfe_diag.so")
+ygzfe.LIB_PATH = os.environ.get("YGZ_DIAG_LIB", os.path.join(ROOT, "orb-ygz-slam_amd", "lib", "libygzfe_diag.so"))
 import _scenes as S  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
