@@ -441,6 +441,16 @@ struct Ring {
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
 __device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h16x2 as_h16x2(uint32_t v) { return __builtin_bit_cast(h16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(h16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+// v_pk_minimum3_f16 / v_pk_maximum3_f16 (inputs here are never NaN: plain selection)
+__device__ __forceinline__ h16x2 hmin3(h16x2 a, h16x2 b, h16x2 c) {
+    return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
+__device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
 
 // One wave per cell (four per 256-thread workgroup), each with a dynamic-LDS
 // slice: ROI tile S*S, score map S*S, pixel list 2*(S-6)^2.  Per threshold:
@@ -559,12 +569,15 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
         return;
 #endif
         // BC: segment test and score in one pass, two survivors per lane as packed
-        //     i16 pairs (low half list[i], high half list[i+1]), e[k] = r_k - v:
+        //     pairs (low half list[i], high half list[i+1]), e[k] = r_k - v:
         //       arcmax = max(max_k min(e[k..k+8]), max_k min(-e[k..k+8]))
         //     corner (FAST_t<16>: 9 contiguous ring pixels all > v+t or all < v-t)
         //     <=> arcmax > t, and then cornerScore<16> = max(t, arcmax) - 1 =
         //     arcmax - 1, written to the score map.  Corners are compacted in place
         //     in raster order (writes never pass the read front).
+        //     The min / max run on v_pk_minimum3_f16 / v_pk_maximum3_f16 over the
+        //     bit patterns e + 1280 in [1025, 1535]: normal f16 numbers (exponent
+        //     field 1) whose order is the integers' order, selected exactly.
         int nc = 0;
         for (int i0 = 0; i0 < na; i0 += 128) {
             const int i = i0 + 2 * lane;
@@ -572,35 +585,39 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             const bool v0 = i < na, v1 = i + 1 < na;
             const uint32_t e0 = v0 ? (pr & 0xFFFFu) : 0x0303u, e1 = v1 ? (pr >> 16) : 0x0303u;
             // ring bases q = centre - 3S - 3: every tap an immediate, non-negative ds_read offset
-            const uint32_t b0 = ((e0 >> 8) - 3) * S + (e0 & 0xFFu) - 3, b1 = ((e1 >> 8) - 3) * S + (e1 & 0xFFu) - 3;
+            uint32_t b0 = ((e0 >> 8) - 3) * S + (e0 & 0xFFu) - 3, b1 = ((e1 >> 8) - 3) * S + (e1 & 0xFFu) - 3;
             const uint32_t o0 = b0 + Ring<S>::kCentre, o1 = b1 + Ring<S>::kCentre;
+            asm("" : "+v"(b0), "+v"(b1));  // taps off q (not off the centre): immediate offsets only
             const uint8_t *q0 = img + b0, *q1 = img + b1;
-            const s16x2 vc = as_s16x2((uint32_t)q0[Ring<S>::kCentre] | ((uint32_t)q1[Ring<S>::kCentre] << 16));
-            s16x2 e[16];
+            // v - 1280 per half, so that r - (v - 1280) = e + 1280
+            uint32_t vbu = as_u32(as_s16x2((uint32_t)q0[Ring<S>::kCentre] | ((uint32_t)q1[Ring<S>::kCentre] << 16)) -
+                                  as_s16x2(0x05000500u));
+            asm("" : "+v"(vbu));  // keep one subtraction per tap (no re-association into add + sub)
+            const s16x2 vb = as_s16x2(vbu);
+            h16x2 e[16];
 #pragma unroll
             for (int k = 0; k < 16; k++)
-                e[k] = as_s16x2((uint32_t)q0[Ring<S>::off(k)] | ((uint32_t)q1[Ring<S>::off(k)] << 16)) - vc;
-            s16x2 m2[16], w4[16];
+                e[k] = as_h16x2(as_u32(as_s16x2((uint32_t)q0[Ring<S>::off(k)] | ((uint32_t)q1[Ring<S>::off(k)] << 16)) - vb));
+            h16x2 w3[16];
+            // bright: max_k min(e[k..k+8]) = max_k min3(w3[k], w3[k+3], w3[k+6]), w3 = min of 3
 #pragma unroll
-            for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(e[k], e[(k + 1) & 15]);
+            for (int k = 0; k < 16; k++) w3[k] = hmin3(e[k], e[(k + 1) & 15], e[(k + 2) & 15]);
+            h16x2 b9[16];
 #pragma unroll
-            for (int k = 0; k < 16; k++) w4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
-            s16x2 bright = {-256, -256};
+            for (int k = 0; k < 16; k++) b9[k] = hmin3(w3[k], w3[(k + 3) & 15], w3[(k + 6) & 15]);
+            const h16x2 bright = hmax3(hmax3(hmax3(b9[0], b9[1], b9[2]), hmax3(b9[3], b9[4], b9[5]), hmax3(b9[6], b9[7], b9[8])),
+                                       hmax3(b9[9], b9[10], b9[11]), hmax3(hmax3(b9[12], b9[13], b9[14]), b9[15], b9[15]));
+            // dark: max_k min(-e[k..k+8]) = -(min_k max(e[k..k+8]))
 #pragma unroll
-            for (int k = 0; k < 16; k++)
-                bright = __builtin_elementwise_max(
-                    bright, __builtin_elementwise_min(__builtin_elementwise_min(w4[k], w4[(k + 4) & 15]), e[(k + 8) & 15]));
+            for (int k = 0; k < 16; k++) w3[k] = hmax3(e[k], e[(k + 1) & 15], e[(k + 2) & 15]);
 #pragma unroll
-            for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_max(e[k], e[(k + 1) & 15]);
-#pragma unroll
-            for (int k = 0; k < 16; k++) w4[k] = __builtin_elementwise_max(m2[k], m2[(k + 2) & 15]);
-            s16x2 darkmin = {256, 256};
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-                darkmin = __builtin_elementwise_min(
-                    darkmin, __builtin_elementwise_max(__builtin_elementwise_max(w4[k], w4[(k + 4) & 15]), e[(k + 8) & 15]));
-            const s16x2 zero2 = {0, 0};
-            const s16x2 am = __builtin_elementwise_max(bright, zero2 - darkmin);
+            for (int k = 0; k < 16; k++) b9[k] = hmax3(w3[k], w3[(k + 3) & 15], w3[(k + 6) & 15]);
+            const h16x2 darkmin = hmin3(hmin3(hmin3(b9[0], b9[1], b9[2]), hmin3(b9[3], b9[4], b9[5]), hmin3(b9[6], b9[7], b9[8])),
+                                        hmin3(b9[9], b9[10], b9[11]), hmin3(hmin3(b9[12], b9[13], b9[14]), b9[15], b9[15]));
+            // back to integers: bright = pattern - 1280, dark = 1280 - pattern
+            const s16x2 bi = as_s16x2(as_u32(bright)) - as_s16x2(0x05000500u);
+            const s16x2 di = as_s16x2(0x05000500u) - as_s16x2(as_u32(darkmin));
+            const s16x2 am = __builtin_elementwise_max(bi, di);
             const bool c0 = v0 && am.x > th, c1 = v1 && am.y > th;
             if (c0) sc[o0] = (uint8_t)(am.x - 1);
             if (c1) sc[o1] = (uint8_t)(am.y - 1);
