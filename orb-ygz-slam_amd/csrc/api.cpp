@@ -696,24 +696,36 @@ int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream) {
     return ygzfe_batch_extract_split(b, n_frames, stream, stream);
 }
 
-// Measurement helper (tools/mb_fast.py): the FAST stage alone over the first
-// n_frames resident frames (pyramid levels built first when build_pyramid),
-// `reps` back-to-back launch sets on the batch stream, average ms per set
-// (hipEvents).  Writes only the pyramid and the FAST cell scratch.
-int ygzfe_diag_fast_ms(ygzfe_batch *b, int n_frames, int reps, int build_pyramid, float *ms) {
-    if (!b || !ms || n_frames < 1 || n_frames > b->maxF || reps < 1) { set_error("invalid argument"); return YGZFE_EINVAL; }
+// Measurement helper (tools/mb_fast.py): one stage alone over the first n_frames
+// resident frames, `reps` back-to-back launch sets on the batch stream, average
+// ms per set (hipEvents).  stage 0: FAST (writes only the cell scratch; pyramid
+// levels built first when build_pyramid); stage 1: orientation + rBRIEF on the
+// octree selection of the last full extraction (rewrites its angles and descriptors).
+int ygzfe_diag_stage_ms(ygzfe_batch *b, int stage, int n_frames, int reps, int build_pyramid, float *ms) {
+    if (!b || !ms || n_frames < 1 || n_frames > b->maxF || reps < 1 || stage < 0 || stage > 1) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
     YGZ_TRY(ensure_device(b->device));
     const PlanDev &pd = *b->plan;
     const Plan &P = pd.hp();
+    const uint8_t *pyr = b->pyr.as<uint8_t>();
     if (build_pyramid)
         YGZ_HIP(launch_pyramid(b->pyr.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), pd.tabs.as<int>(), n_frames, b->stream));
     hipEvent_t e0, e1;
     YGZ_HIP(hipEventCreate(&e0));
     YGZ_HIP(hipEventCreate(&e1));
     YGZ_HIP(hipEventRecord(e0, b->stream));
-    for (int r = 0; r < reps; r++)
-        YGZ_HIP(launch_fast(b->pyr.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(),
-                            b->ws.cellbuf.as<uint32_t>(), b->ws.cellcnt.as<int>(), n_frames, b->stream));
+    Workspace &ws = b->ws;
+    for (int r = 0; r < reps; r++) {
+        if (stage == 0)
+            YGZ_HIP(launch_fast(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(), ws.cellbuf.as<uint32_t>(),
+                                ws.cellcnt.as<int>(), n_frames, b->stream));
+        else
+            YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.sel.as<uint32_t>(),
+                                       ws.selcnt.as<int>(), nullptr, ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(),
+                                       ws.counts.as<int>(), P.kp_cap, n_frames, b->stream));
+    }
     YGZ_HIP(hipEventRecord(e1, b->stream));
     YGZ_HIP(hipEventSynchronize(e1));
     YGZ_HIP(hipEventElapsedTime(ms, e0, e1));

@@ -1,6 +1,6 @@
-"""FAST stage alone (ygzfe_diag_fast_ms) on the bench's C2 frames, for A/B library
-variants: python tools/mb_fast.py B lib1.so [lib2.so ...] -- one child process per
-library (each loads its own build); prints ms per 1024-frame launch set."""
+"""FAST and orientation+rBRIEF stages alone (ygzfe_diag_stage_ms) on the bench's C2
+frames, for A/B library variants: python tools/mb_fast.py B lib1.so [lib2.so ...] --
+one child process per library (each loads its own build); prints ms per 1024 frames."""
 import ctypes as C
 import os
 import subprocess
@@ -26,15 +26,21 @@ def child(B, libpath):
     b = ygzfe.Batch((nf, sf, nl, ini, mn, 0), 0, W, H, B)
     b.upload(frames)
     L = ygzfe.lib()
-    L.ygzfe_diag_fast_ms.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
+    L.ygzfe_diag_stage_ms.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
     ms = C.c_float()
-    assert L.ygzfe_diag_fast_ms(b.h, B, 3, 1, C.byref(ms)) == 0, ygzfe.last_error() if hasattr(ygzfe, "last_error") else "diag"
-    vals = []
-    for _ in range(5):
-        assert L.ygzfe_diag_fast_ms(b.h, B, 10, 0, C.byref(ms)) == 0
-        vals.append(ms.value)
-    print(f"{os.path.basename(libpath)}: FAST {np.median(vals) * 1024 / B:.4f} ms / 1024 frames (min {min(vals) * 1024 / B:.4f})",
-          flush=True)
+    out = []
+    stages = [int(x) for x in os.environ.get("YGZ_MB_STAGES", "0,1").split(",")]
+    for stage, name in [(st, ("FAST", "orient")[st]) for st in stages]:
+        if stage == 1:
+            b.extract(B)  # the octree selection the orientation pass reads
+            b.check()
+        assert L.ygzfe_diag_stage_ms(b.h, stage, B, 3, 1 if stage == 0 else 0, C.byref(ms)) == 0, "diag"
+        vals = []
+        for _ in range(5):
+            assert L.ygzfe_diag_stage_ms(b.h, stage, B, 10, 0, C.byref(ms)) == 0
+            vals.append(ms.value)
+        out.append(f"{name} {np.median(vals) * 1024 / B:.4f}")
+    print(f"{os.path.basename(libpath)}: " + "  ".join(out) + " ms / 1024 frames", flush=True)
 
 
 if __name__ == "__main__":
