@@ -91,6 +91,37 @@ struct DevBuf {
     T *as() const { return reinterpret_cast<T *>(p); }
 };
 
+// page-locked host staging (hipHostMalloc): one DMA per direction per call
+// instead of a pageable copy per argument
+struct HostBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    HostBuf() = default;
+    HostBuf(const HostBuf &) = delete;
+    HostBuf &operator=(const HostBuf &) = delete;
+    ~HostBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    int ensure(size_t bytes) {
+        if (p && n >= bytes) return YGZFE_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        bytes = std::max<size_t>(bytes, 4096);
+        if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            set_error("hipHostMalloc(%zu) failed", bytes);
+            return YGZFE_ENOMEM;
+        }
+        n = bytes;
+        return YGZFE_OK;
+    }
+    template <class T>
+    T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+static inline size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
+
 #define YGZ_TRY(x)                          \
     do {                                    \
         int r_ = (x);                       \
@@ -129,7 +160,7 @@ static int make_plan(const ygzfe_orb_params &p, int W, int H, std::unique_ptr<Pl
 // extraction scratch for F frames of one plan
 struct Workspace {
     int F = 0, rows = 0;
-    DevBuf blur, cellbuf, cellcnt, candA, candB, sel, selcnt, kps, desc, counts, nexist, err;
+    DevBuf blur, cellbuf, cellcnt, candA, candB, sel, selcnt, kps, desc, counts, nexist, err, ojobs;
     DevBuf occ, dso_keys, dso_cnt, dso_total;
     int ensure(const Plan &P, int frames, int rows_needed) {
         F = frames;
@@ -140,6 +171,7 @@ struct Workspace {
         YGZ_TRY(candA.ensure((size_t)F * P.cand_total * 4 + 16));
         YGZ_TRY(candB.ensure((size_t)F * P.cand_total * 4 + 16));
         YGZ_TRY(sel.ensure((size_t)F * P.sel_total * 4 + 16));
+        YGZ_TRY(ojobs.ensure((size_t)F * P.sel_total * 8 + 16));
         YGZ_TRY(selcnt.ensure((size_t)F * P.nlevels * 4 + 128));  // tail: k_orient_desc's 8-int scalar load
         YGZ_TRY(kps.ensure((size_t)F * rows * sizeof(ygzfe_kp) + 16));
         YGZ_TRY(desc.ensure((size_t)F * rows * 32 + 16));
@@ -166,7 +198,27 @@ struct ygzfe_extractor {
     // SearchLocalPointsDirect staging: one packed H2D, one packed D2H per call
     DevBuf direct_dev;
     std::vector<uint8_t> direct_host;
+    // single-frame latency path: side streams (blur, FAST levels >= 1, octree
+    // classes after the first) forked from / joined to `stream`, pinned staging,
+    // the packed extraction result (one D2H) and the SparseImgAlign buffers
+    hipStream_t side[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_oct_fork = nullptr, ev_oct_join[2] = {nullptr, nullptr};
+    HostBuf hin, hout;
+    DevBuf res, align_in, align_scratch, align_out;
+    bool err_clean = false;  // ws.err zeroed (k_pack_result re-zeroes it after each read)
     std::mutex mu;
+    int ensure_side() {
+        if (side[0]) return YGZFE_OK;
+        for (int i = 0; i < 3; i++) {
+            YGZ_HIP(hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking));
+            YGZ_HIP(hipEventCreateWithFlags(&ev_join[i], hipEventDisableTiming));
+        }
+        YGZ_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+        YGZ_HIP(hipEventCreateWithFlags(&ev_oct_fork, hipEventDisableTiming));
+        for (int i = 0; i < 2; i++) YGZ_HIP(hipEventCreateWithFlags(&ev_oct_join[i], hipEventDisableTiming));
+        return YGZFE_OK;
+    }
 };
 
 struct ygzfe_frame {
@@ -288,6 +340,14 @@ void ygzfe_extractor_destroy(ygzfe_extractor *ex) {
     if (!ex) return;
     (void)hipSetDevice(ex->device);
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
+    for (int i = 0; i < 3; i++) {
+        if (ex->side[i]) (void)hipStreamSynchronize(ex->side[i]), (void)hipStreamDestroy(ex->side[i]);
+        if (ex->ev_join[i]) (void)hipEventDestroy(ex->ev_join[i]);
+    }
+    if (ex->ev_fork) (void)hipEventDestroy(ex->ev_fork);
+    if (ex->ev_oct_fork) (void)hipEventDestroy(ex->ev_oct_fork);
+    for (int i = 0; i < 2; i++)
+        if (ex->ev_oct_join[i]) (void)hipEventDestroy(ex->ev_oct_join[i]);
     ex->plans.clear();
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
     delete ex;
@@ -380,9 +440,11 @@ int ygzfe_compute_pyramid(ygzfe_extractor *ex, ygzfe_frame *f, const uint8_t *im
     if (!ex || !f || !img || stride < f->W) { set_error("invalid argument"); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(ex->device));
     std::lock_guard<std::mutex> lk(ex->mu);
+    // the pageable H2D returns once `img` is staged (the caller may reuse it);
+    // everything that reads the pyramid is ordered after it on ex->stream or
+    // synchronises first (ygzfe_frame_level), so no synchronisation here
     YGZ_HIP(hipMemcpy2DAsync(f->pyr.p, f->W, img, stride, f->W, f->H, hipMemcpyHostToDevice, ex->stream));
     YGZ_TRY(pyramid_from_level0(f, ex->stream));
-    YGZ_HIP(hipStreamSynchronize(ex->stream));
     return YGZFE_OK;
 }
 
@@ -452,35 +514,80 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
     const int rows = n_existing + (method == YGZFE_DSO_KEYPOINT ? std::max(P.kp_cap, dso_max_rows(P)) : P.kp_cap);
     Workspace &ws = ex->ws;
     YGZ_TRY(ws.ensure(P, 1, rows));
-    if (n_existing > 0)
-        YGZ_HIP(hipMemcpyAsync(ws.kps.p, kps_io, sizeof(ygzfe_kp) * n_existing, hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemcpyAsync(ws.nexist.p, &n_existing, sizeof(int), hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemsetAsync(ws.err.p, 0, 16, st));
     const uint8_t *pyr = f->pyr.as<uint8_t>();
-    YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), 1, st));
     int total = 0;
     if (method == YGZFE_ORBSLAM_KEYPOINT) {
+        // The single-frame DAG (one Tracking thread's latency): blur on side[0]
+        // beside FAST level 0 (st) and FAST levels >= 1 (side[1], side[2]); the
+        // octree's node-pool classes concurrent (side[1..2]); keypoint rows,
+        // angle + rBRIEF after the join; one packing kernel, one D2H into pinned
+        // memory, one synchronisation.
+        YGZ_TRY(ex->ensure_side());
+        const int *d_nexist = nullptr;  // null: no existing rows (the kernels read 0)
+        if (n_existing > 0) {
+            YGZ_TRY(ex->hin.ensure(16 + sizeof(ygzfe_kp) * (size_t)n_existing));
+            ex->hin.as<int>()[0] = n_existing;
+            memcpy(ex->hin.as<uint8_t>() + 16, kps_io, sizeof(ygzfe_kp) * n_existing);
+            YGZ_HIP(hipMemcpyAsync(ws.nexist.p, ex->hin.p, sizeof(int), hipMemcpyHostToDevice, st));
+            YGZ_HIP(hipMemcpyAsync(ws.kps.p, ex->hin.as<uint8_t>() + 16, sizeof(ygzfe_kp) * n_existing,
+                                   hipMemcpyHostToDevice, st));
+            d_nexist = ws.nexist.as<int>();
+        }
+        if (!ex->err_clean) {
+            YGZ_HIP(hipMemsetAsync(ws.err.p, 0, 16, st));
+            ex->err_clean = true;
+        }
+        hipStream_t *sd = ex->side;
+        YGZ_HIP(hipEventRecord(ex->ev_fork, st));
+        for (int i = 0; i < 3; i++) YGZ_HIP(hipStreamWaitEvent(sd[i], ex->ev_fork, 0));
+        YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), 1, sd[0]));
+        YGZ_HIP(hipEventRecord(ex->ev_join[0], sd[0]));
         YGZ_HIP(launch_fast(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(), ws.cellbuf.as<uint32_t>(),
-                            ws.cellcnt.as<int>(), 1, st));
+                            ws.cellcnt.as<int>(), 1, st, &sd[1], 2));
+        for (int i = 1; i < 3; i++) {
+            YGZ_HIP(hipEventRecord(ex->ev_join[i], sd[i]));
+            YGZ_HIP(hipStreamWaitEvent(st, ex->ev_join[i], 0));
+        }
         YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
                               ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.err.as<int>(), 1,
-                              st));
-        YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.nexist.as<int>(),
-                                ws.kps.as<ygzfe_kp>(), ws.counts.as<int>(), rows, 1, st));
-        YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.sel.as<uint32_t>(),
-                                   ws.selcnt.as<int>(), ws.nexist.as<int>(), ws.kps.as<ygzfe_kp>(),
-                                   ws.desc.as<uint8_t>(), ws.counts.as<int>(), rows, 1, st));
+                              st, &sd[1], 2, ex->ev_oct_fork, ex->ev_oct_join));
+        YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_nexist,
+                                ws.kps.as<ygzfe_kp>(), ws.counts.as<int>(), rows, ws.ojobs.as<uint2>(), 1, st));
+        YGZ_HIP(hipStreamWaitEvent(st, ex->ev_join[0], 0));  // the blurred levels
+        YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.ojobs.as<uint2>(),
+                                   d_nexist, ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(), rows, 1, st));
         YGZ_HIP(launch_desc_existing(pyr, ws.blur.as<uint8_t>(), pd.dp(), ws.kps.as<ygzfe_kp>(),
                                      ws.desc.as<uint8_t>(), n_existing, 0, st));
-        int herr = 0;
-        YGZ_HIP(hipMemcpyAsync(&total, ws.counts.p, sizeof(int), hipMemcpyDeviceToHost, st));
-        YGZ_HIP(hipMemcpyAsync(&herr, ws.err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        // [count, overflow flag, 0, 0][rows x 28 B keypoints][16-B aligned: rows x 32 B descriptors]
+        const size_t kbytes = align16(sizeof(ygzfe_kp) * (size_t)rows), rbytes = 16 + kbytes + (size_t)32 * rows;
+        YGZ_TRY(ex->res.ensure(rbytes));
+        YGZ_TRY(ex->hout.ensure(rbytes));
+        YGZ_HIP(launch_pack_result(ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(), ws.counts.as<int>(), ws.err.as<int>(),
+                                   rows, ex->res.as<uint8_t>(), kbytes, st));
+        // the header and, speculatively, as many rows as the caller can take (one DMA)
+        const int cap_rows = std::min(rows, std::max(cap, 0));
+        const size_t copy = desc ? 16 + kbytes + (size_t)32 * cap_rows : 16 + sizeof(ygzfe_kp) * (size_t)cap_rows;
+        YGZ_HIP(hipMemcpyAsync(ex->hout.p, ex->res.p, copy, hipMemcpyDeviceToHost, st));
         YGZ_HIP(hipStreamSynchronize(st));
-        if (herr) {
+        total = ex->hout.as<int>()[0];
+        if (ex->hout.as<int>()[1]) {
             set_error("octree node pool overflow");
             return YGZFE_EINVAL;
         }
+        *n_out = total;
+        if (total > cap) {
+            set_error("capacity %d < %d keypoints", cap, total);
+            return YGZFE_ECAP;
+        }
+        if (total > 0) {
+            memcpy(kps_io, ex->hout.as<uint8_t>() + 16, sizeof(ygzfe_kp) * (size_t)total);
+            if (desc) memcpy(desc, ex->hout.as<uint8_t>() + 16 + kbytes, (size_t)32 * total);
+        }
+        return YGZFE_OK;
     } else {
+        if (n_existing > 0)
+            YGZ_HIP(hipMemcpyAsync(ws.kps.p, kps_io, sizeof(ygzfe_kp) * n_existing, hipMemcpyHostToDevice, st));
+        YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), 1, st));
         // DSO_KEYPOINT: ComputeKeyPointsDSOSingleLevel (ORBextractor.cc:1275-1386)
         const LevelDesc &L0 = P.lv[0];
         const int w = L0.w, h = L0.h, n = ex->p.nfeatures;
@@ -672,7 +779,7 @@ int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, voi
                           ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.err.as<int>(),
                           n_frames, st, &b->aux[1], 2, b->ev_oct_fork, b->ev_oct_join));
     YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), nullptr, ws.kps.as<ygzfe_kp>(),
-                            ws.counts.as<int>(), P.kp_cap, n_frames, st));
+                            ws.counts.as<int>(), P.kp_cap, ws.ojobs.as<uint2>(), n_frames, st));
     b->end(ST_OCT, t0, st);
     // descriptors: after the blur (already on ds) and the keypoint rows
     if (ds != st) {
@@ -680,9 +787,8 @@ int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, voi
         YGZ_HIP(hipStreamWaitEvent(ds, b->ev_join[1], 0));
     }
     t0 = b->begin(ds);
-    YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.sel.as<uint32_t>(),
-                               ws.selcnt.as<int>(), nullptr, ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(),
-                               ws.counts.as<int>(), P.kp_cap, n_frames, ds));
+    YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.ojobs.as<uint2>(), nullptr,
+                               ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(), P.kp_cap, n_frames, ds));
     b->end(ST_DESC, t0, ds);
     if (cap == hipStreamCaptureStatusNone) {
         YGZ_HIP(hipEventRecord(b->ev_desc_done, ds));
@@ -722,9 +828,9 @@ int ygzfe_diag_stage_ms(ygzfe_batch *b, int stage, int n_frames, int reps, int b
             YGZ_HIP(launch_fast(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(), ws.cellbuf.as<uint32_t>(),
                                 ws.cellcnt.as<int>(), n_frames, b->stream));
         else
-            YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.sel.as<uint32_t>(),
-                                       ws.selcnt.as<int>(), nullptr, ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(),
-                                       ws.counts.as<int>(), P.kp_cap, n_frames, b->stream));
+            YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.ojobs.as<uint2>(),
+                                       nullptr, ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(), P.kp_cap, n_frames,
+                                       b->stream));
     }
     YGZ_HIP(hipEventRecord(e1, b->stream));
     YGZ_HIP(hipEventSynchronize(e1));
@@ -974,32 +1080,37 @@ int ygzfe_sparse_align(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygz
     YGZ_TRY(ensure_device(ex->device));
     std::lock_guard<std::mutex> lk(ex->mu);
     hipStream_t st = ex->stream;
-    DevBuf dk, dx, du, dj, ds, dout;
-    YGZ_TRY(dk.ensure(sizeof(ygzfe_kp) * n));
-    YGZ_TRY(dx.ensure(sizeof(float) * 3 * n));
-    YGZ_TRY(du.ensure(n));
-    YGZ_TRY(dj.ensure(sizeof(AlignJob)));
+    // one packed H2D from pinned staging: [job][keypoints][xyz][usable] (16-B aligned
+    // pieces), cached device buffers, one D2H of the result
+    const size_t o_k = align16(sizeof(AlignJob)), o_x = o_k + align16(sizeof(ygzfe_kp) * (size_t)n);
+    const size_t o_u = o_x + align16(sizeof(float) * 3 * (size_t)n), in_bytes = o_u + align16((size_t)n);
     const size_t spj = sparse_align_scratch_floats(n);
-    YGZ_TRY(ds.ensure(sizeof(float) * spj));
-    YGZ_TRY(dout.ensure(sizeof(ygzfe_align_result)));
-    YGZ_HIP(hipMemcpyAsync(dk.p, kps, sizeof(ygzfe_kp) * n, hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemcpyAsync(dx.p, xyz_ref, sizeof(float) * 3 * n, hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemcpyAsync(du.p, usable, n, hipMemcpyHostToDevice, st));
+    YGZ_TRY(ex->align_in.ensure(in_bytes));
+    YGZ_TRY(ex->align_scratch.ensure(sizeof(float) * spj));
+    YGZ_TRY(ex->align_out.ensure(sizeof(ygzfe_align_result)));
+    YGZ_TRY(ex->hin.ensure(in_bytes));
+    YGZ_TRY(ex->hout.ensure(sizeof(ygzfe_align_result)));
+    uint8_t *din = ex->align_in.as<uint8_t>(), *hin = ex->hin.as<uint8_t>();
     AlignJob job;
     job.ref_pyr = ref->pyr.as<uint8_t>();
     job.cur_pyr = cur->pyr.as<uint8_t>();
-    job.kps = dk.as<ygzfe_kp>();
-    job.xyz = dx.as<float>();
-    job.usable = du.as<uint8_t>();
+    job.kps = reinterpret_cast<const ygzfe_kp *>(din + o_k);
+    job.xyz = reinterpret_cast<const float *>(din + o_x);
+    job.usable = din + o_u;
     job.n = n;
     job.max_level = max_level;
     job.min_level = min_level;
     job.T_init = *T_init;
-    YGZ_HIP(hipMemcpyAsync(dj.p, &job, sizeof(job), hipMemcpyHostToDevice, st));
-    YGZ_HIP(launch_sparse_align(levels_of(P), *cam, dj.as<AlignJob>(), 1, ds.as<float>(), spj,
-                                dout.as<ygzfe_align_result>(), st, n));
-    YGZ_HIP(hipMemcpyAsync(result, dout.p, sizeof(*result), hipMemcpyDeviceToHost, st));
+    memcpy(hin, &job, sizeof(job));
+    memcpy(hin + o_k, kps, sizeof(ygzfe_kp) * (size_t)n);
+    memcpy(hin + o_x, xyz_ref, sizeof(float) * 3 * (size_t)n);
+    memcpy(hin + o_u, usable, (size_t)n);
+    YGZ_HIP(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, st));
+    YGZ_HIP(launch_sparse_align(levels_of(P), *cam, reinterpret_cast<const AlignJob *>(din), 1,
+                                ex->align_scratch.as<float>(), spj, ex->align_out.as<ygzfe_align_result>(), st, n));
+    YGZ_HIP(hipMemcpyAsync(ex->hout.p, ex->align_out.p, sizeof(*result), hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipStreamSynchronize(st));
+    memcpy(result, ex->hout.p, sizeof(*result));
     return YGZFE_OK;
 }
 

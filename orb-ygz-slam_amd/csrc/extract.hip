@@ -1219,6 +1219,9 @@ __device__ __forceinline__ int row16_sum(int v) {
     return v;
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+constexpr uint32_t kMagicBits = 0x4B000000u;  // bits of 2^23 (ulp 1 in [2^23, 2^24))
 constexpr int kPatchStride = 64;  // LDS row of a staged keypoint window: 4 x 16 B (window + 16-B misalignment)
 constexpr int kPatchBytes = 37 * kPatchStride;
 
@@ -1239,16 +1242,16 @@ template <int R, int NROWS>
 struct Window {
     static constexpr int NK = (NROWS + 3) / 4;
     u32x4 v[NK];
-    __device__ __forceinline__ void load(const uint8_t *img, int w, int cx, int cy, int s) {
-        // 32-bit in-level offsets (24-bit multiplies) added to the level pointer once per row
-        // (the level can differ between the keypoints of a wave: no wave-uniform buffer resource)
-        const uint32_t base = __umul24((uint32_t)(cy - R), (uint32_t)w) + (uint32_t)(cx - R);
-        const uint32_t a0 = (uint32_t)(uintptr_t)img & 15u;  // level misalignment (0: levels are 16-B aligned)
+    // frame: the frame's pyramid; c: byte offset of the centre pixel in it
+    __device__ __forceinline__ void load(const uint8_t *frame, uint32_t w, uint32_t c, int s) {
+        // 32-bit offsets (24-bit multiplies) added to the frame pointer once per row
+        const uint32_t base = c - (uint32_t)R * w - (uint32_t)R;
+        const uint32_t a0 = (uint32_t)(uintptr_t)frame & 15u;  // 0 unless a caller-bound buffer is unaligned
         const int j = s & 3, r0 = s >> 2;
 #pragma unroll
         for (int k = 0; k < NK; k++) {  // rows past the window re-read its last row (not stored)
-            const uint32_t o = ((mad24((uint32_t)min(r0 + 4 * k, NROWS - 1), (uint32_t)w, base) + a0) & ~15u) - a0 + 16u * j;
-            v[k] = as_global(reinterpret_cast<const u32x4 *>(img + o))[0];
+            const uint32_t o = ((mad24((uint32_t)min(r0 + 4 * k, NROWS - 1), w, base) + a0) & ~15u) - a0 + 16u * j;
+            v[k] = as_global(reinterpret_cast<const u32x4 *>(frame + o))[0];
         }
     }
     // SWZ: row r at 64 r + 16 (r >> 2) (patch_row_swz), so that the 16 rows a
@@ -1268,21 +1271,23 @@ struct Window {
     }
 };
 
-// New keypoints of the octree: rows n_existing + prefix(level) + k.
-// One 16-lane DPP row per keypoint (four per wave, sixteen per workgroup):
-//   IC_Angle: lane s sums columns u = s-15 and u = s+1 over the 31 rows
-//   rBRIEF:   lane s evaluates pairs 16s..16s+15 (half of descriptor word s/2)
 // Keypoint rows of the octree selection (ORBextractor.cc:785-797): level-0
 // coordinates (x, y) * scale, size = PATCH_SIZE * scale, response = FAST
 // score, octave, class_id -1; angle is filled in by k_orient_desc.  Written
 // as soon as the octree is done, so consumers of positions only (map-point
 // snapshots, SparseImgAlign) need not wait for the descriptors.
+// Beside each row: its orientation job {byte offset of the keypoint pixel in the
+// frame's pyramid, level width | level << 16}, kOrientNone for selection slots
+// past the frame's count, so k_orient_desc starts its window loads after one
+// load (no per-level count prefix, plan lookup and key decode on its critical path).
+constexpr uint32_t kOrientNone = 0xFFFFFFFFu;
 __global__ __launch_bounds__(256) void k_emit_kps(const Plan *__restrict__ plan, const uint32_t *__restrict__ sel,
                                                   const int *__restrict__ selcnt, const int *__restrict__ n_existing,
-                                                  ygzfe_kp *__restrict__ kps, int *__restrict__ counts, int row_cap) {
+                                                  ygzfe_kp *__restrict__ kps, int *__restrict__ counts, int row_cap,
+                                                  uint2 *__restrict__ ojobs) {
     const int f = blockIdx.y;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    const int nl = plan->nlevels;
+    const int nl = plan->nlevels, sel_total = plan->sel_total;
     const int *sc = selcnt + (size_t)f * nl;
     const int ne = n_existing ? n_existing[f] : 0;
     int l = 0, pre = 0, acc = 0;
@@ -1291,12 +1296,16 @@ __global__ __launch_bounds__(256) void k_emit_kps(const Plan *__restrict__ plan,
         if (acc <= idx) { l = q + 1; pre = acc; }
     }
     if (idx == 0) counts[f] = ne + acc;
-    if (l >= nl || ne + idx >= row_cap) return;
+    if (l >= nl || ne + idx >= row_cap) {
+        if (idx < sel_total) ojobs[(size_t)f * sel_total + idx] = make_uint2(kOrientNone, 0u);
+        return;
+    }
     const LevelDesc &L = plan->lv[l];
-    const uint32_t key = sel[(size_t)f * plan->sel_total + L.sel_off + (idx - pre)];
+    const uint32_t key = sel[(size_t)f * sel_total + L.sel_off + (idx - pre)];
+    const int cx = key_x(key) + kMinBorder, cy = key_y(key) + kMinBorder;
     ygzfe_kp kp;
-    kp.x = (float)(key_x(key) + kMinBorder);
-    kp.y = (float)(key_y(key) + kMinBorder);
+    kp.x = (float)cx;
+    kp.y = (float)cy;
     if (l != 0) { kp.x *= L.scale; kp.y *= L.scale; }
     kp.size = (float)L.patch_size;
     kp.angle = 0.f;
@@ -1304,69 +1313,43 @@ __global__ __launch_bounds__(256) void k_emit_kps(const Plan *__restrict__ plan,
     kp.octave = l;
     kp.class_id = -1;
     kps[(size_t)f * row_cap + ne + idx] = kp;
+    ojobs[(size_t)f * sel_total + idx] =
+        make_uint2(L.off + (uint32_t)cy * (uint32_t)L.w + (uint32_t)cx, (uint32_t)L.w | ((uint32_t)l << 16));
 }
 
+// New keypoints of the octree: rows n_existing + selection index.
+// One 16-lane DPP row per keypoint (four per wave, sixteen per workgroup):
+//   IC_Angle: lane s takes window rows 15 +- (s + 1) (lane 15: the centre row)
+//   rBRIEF:   lane s evaluates pairs 16s..16s+15 (half of descriptor word s/2)
+// Both windows are staged in LDS by 16-B aligned dwordx4 loads (4 lanes x 16 B
+// per window row, kept unshifted: window row r starts at byte o(r) = (row
+// address) & 15 of LDS row r); every tap is an LDS byte read.  Octree
+// keypoints sit >= 19 px inside the level, so the 31x31 IC window and the
+// 37x37 rotated-pattern window never leave it.
 __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__ pyr,
                                                      const uint8_t *__restrict__ blur, uint32_t pitch,
-                                                     const Plan *__restrict__ plan,
-                                                     const uint32_t *__restrict__ sel,
-                                                     const int *__restrict__ selcnt,
+                                                     const Plan *__restrict__ plan, const uint2 *__restrict__ ojobs,
                                                      const int *__restrict__ n_existing,
                                                      ygzfe_kp *__restrict__ kps, uint8_t *__restrict__ desc,
-                                                     int *__restrict__ counts, int row_cap) {
+                                                     int row_cap) {
     __shared__ uint8_t s_patch[16][kPatchBytes];  // one 37x37 window per keypoint row
-    YGZ_BSTAMP_K(1, 0);
     int bx, f;
-    swizzled_block_2d(bx, f);  // one frame's keypoints on one XCD: patch lines shared in its L2
+    swizzled_block_2d(bx, f);  // one frame's keypoints on one XCD: window lines shared in its L2
     const int lane = threadIdx.x & 63, s = lane & 15;
     const int idx = bx * 16 + (threadIdx.x >> 4);
-    const int nl = plan->nlevels;
-    const int *sc = selcnt + (size_t)f * nl;
-    const int ne = n_existing ? n_existing[f] : 0;
-    int l = 0, pre = 0;
-    if (nl <= 8) {
-        // the frame's per-level counts by one scalar load (selcnt carries >= 8
-        // ints of tail padding), inclusive prefix in SGPRs: no vector-memory
-        // round trip ahead of the key load
-        struct Cnt8 { int v[8]; };
-        const Cnt8 c8 = scalar_load(reinterpret_cast<const Cnt8 *>(sc));
-        int iq = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            iq += q < nl ? c8.v[q] : 0;
-            if (q < nl && iq <= idx) { l = q + 1; pre = iq; }
-        }
-    } else {
-        // per-level counts, inclusive prefix over lanes 0..15 (DPP row_shr inside the first row)
-        int incl = lane < nl ? sc[lane] : 0;
-        incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, false);
-        incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, false);
-        incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, false);
-        incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, false);
-        for (int q = 0; q < nl; q++) {
-            const int iq = __builtin_amdgcn_readlane(incl, q);
-            if (iq <= idx) { l = q + 1; pre = iq; }
-        }
-    }
-    if (l >= nl || ne + idx >= row_cap) return;  // whole rows leave together
-    const LevelDesc &L = plan->lv[l];
-    const int w = L.w, h = L.h;
-    const uint32_t key = sel[(size_t)f * plan->sel_total + L.sel_off + (idx - pre)];
-    const int cx = key_x(key) + kMinBorder, cy = key_y(key) + kMinBorder;
-    float angle;
-    // The row's keypoint windows are staged in LDS by 16-B aligned dwordx4 loads
-    // (4 lanes x 16 B per window row, kept unshifted: window row r starts at byte
-    // o(r) = (row address) & 15 of LDS row r), then every tap is an LDS byte read.
-    // Octree keypoints sit >= 19 px inside the level, so the 31x31 IC window and
-    // the 37x37 rotated-pattern window never leave it.
+    const int sel_total = plan->sel_total;
+    if (idx >= sel_total) return;
+    const uint2 job = ojobs[(size_t)f * sel_total + idx];
+    if (job.x == kOrientNone) return;  // whole rows leave together
+    const uint32_t c = job.x, w = job.y & 0xFFFFu;
+    const uint8_t *fimg = pyr + (size_t)f * pitch;
+    const uint8_t *fblur = blur + (size_t)f * pitch;
     uint8_t *P = s_patch[threadIdx.x >> 4];
-    // IC_Angle (ORBextractor.cc:77-101) on the unblurred level
-    const uint8_t *img = pyr + (size_t)f * pitch + L.off;
-    const uint8_t *bimg = blur + (size_t)f * pitch + L.off;
     Window<15, 31> wic;
     Window<18, 37> wdesc;
-    // the lane's IC row weights (c_icw) and its 16 pattern pairs are read
-    // before the LDS fences, which loads cannot cross
+    wic.load(fimg, w, c, s);  // both windows in flight before the first wait
+    wdesc.load(fblur, w, c, s);
+    // the lane's IC row weights (c_icw) and its 16 pattern pairs
     const uint4 *icw = reinterpret_cast<const uint4 *>(c_icw[s]);
     uint4 wq[4];
 #pragma unroll
@@ -1375,23 +1358,21 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     int4 pat[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) pat[q] = pp[q];
-    YGZ_BSTAMP_K(1, 3);
-    wic.load(img, w, cx, cy, s);  // both windows in flight before the first wait
-    wdesc.load(bimg, w, cx, cy, s);
+    const int ne = n_existing ? n_existing[f] : 0;
+    float angle;
     {
         wic.store<true>(P, s);
-        YGZ_BSTAMP_K(1, 4);
         // IC_Angle (ORBextractor.cc:77-101): lane s takes the window rows 15 +- (s+1)
         // (lane 15 the centre row).  Per row, with I the 31 row bytes (32nd
         // weighted 0): S0 = sum of I over the disc (dot4 with the 0/1 weights),
         // S1 = sum of (u + 15) I (dot4 with the u + 15 weights); then
         // m01 += v (S0(+v) - S0(-v)), m10 += S1 - 15 S0.  Integer sums: the
         // moments equal the reference's exactly.
-        const uint32_t o0 = (uint32_t)(uintptr_t)img + __umul24((uint32_t)(cy - 15), (uint32_t)w) + (uint32_t)(cx - 15);
+        const uint32_t o0 = (uint32_t)(uintptr_t)fimg + c - 15u * w - 15u;
         const uint32_t W0[8] = {wq[0].x, wq[0].y, wq[0].z, wq[0].w, wq[1].x, wq[1].y, wq[1].z, wq[1].w};
         const uint32_t W1[8] = {wq[2].x, wq[2].y, wq[2].z, wq[2].w, wq[3].x, wq[3].y, wq[3].z, wq[3].w};
         auto row_sums = [&](int r, uint32_t &s0, uint32_t &s1) {
-            const uint32_t o = mad24((uint32_t)r, (uint32_t)w, o0) & 15u;  // window start inside LDS row r
+            const uint32_t o = mad24((uint32_t)r, w, o0) & 15u;  // window start inside LDS row r
             const uint32_t *d = reinterpret_cast<const uint32_t *>(P + patch_row_swz((uint32_t)r) + (o & ~3u));
             uint32_t dw[9];
 #pragma unroll
@@ -1416,19 +1397,33 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
         angle = fast_atan2_deg((float)m01, (float)m10);
     }
     // computeOrbDescriptor (ORBextractor.cc:105-149) on the blurred level
-    YGZ_BSTAMP_K(1, 5);
     wave_lds_order();  // IC taps read before the window is replaced
     wdesc.store<false>(P, s);
-    const uint32_t o0 = (uint32_t)(uintptr_t)bimg + __umul24((uint32_t)(cy - 18), (uint32_t)w) + (uint32_t)(cx - 18);
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
-    const float ang = angle * factorPI;
     float ca, sb;
-    glibc_sincosf(ang, sb, ca);  // the reference's std::cos(float) / std::sin(float) = glibc cosf / sinf
-    YGZ_BSTAMP_K(1, 6);
-    const uint32_t w16 = (uint32_t)w & 15u;  // only the row start's offset mod 16 matters
-    auto tap = [&](int dy, int dx) {  // blurred pixel (cy + dy, cx + dx)
-        const int r = dy + 18;
-        return (int)P[r * kPatchStride + (mad24((uint32_t)r, w16, o0) & 15u) + dx + 18];
+    glibc_sincosf(angle * factorPI, sb, ca);  // the reference's std::cos(float) / std::sin(float) = glibc cosf / sinf
+    // tap (dy, dx) at P + 64 r + o(r) + 18 + dx with r = 18 + dy, o(r) = (o0 + r w) & 15.
+    // GET_VALUE's rotation in packed fp32 (the same IEEE products and fused sums
+    // as the reference's -O3 -march=native build, oracle/orb.c ygzo_orb_descriptor);
+    // cvRound as + 2^23 + K: the sum stays in [2^23, 2^24) (ulp 1) for |v| <= 18.4,
+    // rounds half to even with an even K, and its bit pattern carries the integer:
+    //   yb = bits(y + 2^23 + 64)     low bits 46 + r
+    //   xb = bits(x + 2^23 + P + 64)
+    //   o(r) = ((yb & 15) (w & 15) + c0) & 15 with c0 = (o0 - 46 w) & 15
+    //   address = (yb << 6) + xb + o(r) - kFix  ((yb << 6) leaves 0xC0000000 of the exponent)
+    const uint32_t o0 = (uint32_t)(uintptr_t)fblur + c - 18u * w - 18u;
+    const uint32_t w16 = w & 15u;
+    const uint32_t Pa = (uint32_t)(uintptr_t)(lds_u8 *)P;
+    const uint32_t c0 = (o0 - 46u * w16) & 15u;
+    const f32x2 magic = {__uint_as_float(kMagicBits + 64u), __uint_as_float(kMagicBits + Pa + 64u)};
+    constexpr uint32_t kFix = 0xC0000000u + kMagicBits + 46u * 64u + 64u - 18u;
+    const f32x2 rot_a = {sb, ca}, rot_b = {ca, -sb};
+    auto tap = [&](float px, float py) -> uint32_t {
+        const f32x2 m = (f32x2){py, py} * rot_b;
+        const f32x2 yx = __builtin_elementwise_fma((f32x2){px, px}, rot_a, m) + magic;
+        const uint32_t yb = __float_as_uint(yx.x), xb = __float_as_uint(yx.y);
+        const uint32_t a = (yb << 6) + xb, o = (yb & 15u) * w16 + c0;
+        return (uint32_t)*(const lds_u8 *)(uintptr_t)(a + (o & 15u) - kFix);
     };
     uint32_t bits = 0;
 #pragma unroll
@@ -1439,21 +1434,15 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
         for (int k = 0; k < 4; k++) {
             const float px0 = (float)(int8_t)(wd[k] & 0xFF), py0 = (float)(int8_t)((wd[k] >> 8) & 0xFF);
             const float px1 = (float)(int8_t)((wd[k] >> 16) & 0xFF), py1 = (float)(int8_t)(wd[k] >> 24);
-            // GET_VALUE (ORBextractor.cc:114-116) as the reference's -O3 -march=native build
-            // fuses it (oracle/orb.c ygzo_orb_descriptor)
-            const int t0 = tap(cv_round(__builtin_fmaf(px0, sb, py0 * ca)), cv_round(__builtin_fmaf(px0, ca, -(py0 * sb))));
-            const int t1 = tap(cv_round(__builtin_fmaf(px1, sb, py1 * ca)), cv_round(__builtin_fmaf(px1, ca, -(py1 * sb))));
+            const uint32_t t0 = tap(px0, py0), t1 = tap(px1, py1);
             bits |= (uint32_t)(t0 < t1) << (q * 4 + k);
         }
     }
-    YGZ_BSTAMP_K(1, 7);
     const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bits, 0xB1, 0xF, 0xF, false);
     const int row = ne + idx;
     if ((s & 1) == 0)
         reinterpret_cast<uint32_t *>(desc + ((size_t)f * row_cap + row) * 32)[s >> 1] = bits | (other << 16);
     if (s == 0) kps[(size_t)f * row_cap + row].angle = angle;  // the rest of the row: k_emit_kps
-    YGZ_BSTAMP_K(1, 1);
-    YGZ_BSTAMP_K(1, 2);
 }
 
 // Existing keypoints (Frame::mvKeys of a direct-tracked frame): descriptor on
@@ -1631,20 +1620,19 @@ hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf
 }
 
 hipError_t launch_orient_desc(const uint8_t *pyr, const uint8_t *blur, uint32_t pitch, const Plan &hp,
-                              const Plan *dp, const uint32_t *sel, const int *selcnt, const int *n_existing,
-                              ygzfe_kp *kps, uint8_t *desc, int *counts, int row_cap, int nframes,
-                              hipStream_t st) {
+                              const Plan *dp, const uint2 *ojobs, const int *n_existing, ygzfe_kp *kps,
+                              uint8_t *desc, int row_cap, int nframes, hipStream_t st) {
     const int max_new = hp.sel_total;
     hipLaunchKernelGGL(k_orient_desc, dim3((max_new + 15) / 16, nframes), dim3(256), 0, st, pyr, blur, pitch, dp,
-                       sel, selcnt, n_existing, kps, desc, counts, row_cap);
+                       ojobs, n_existing, kps, desc, row_cap);
     return hipGetLastError();
 }
 
 hipError_t launch_emit_kps(const Plan &hp, const Plan *dp, const uint32_t *sel, const int *selcnt,
-                           const int *n_existing, ygzfe_kp *kps, int *counts, int row_cap, int nframes,
+                           const int *n_existing, ygzfe_kp *kps, int *counts, int row_cap, uint2 *ojobs, int nframes,
                            hipStream_t st) {
     hipLaunchKernelGGL(k_emit_kps, dim3((hp.sel_total + 255) / 256 + 1, nframes), dim3(256), 0, st, dp, sel, selcnt,
-                       n_existing, kps, counts, row_cap);
+                       n_existing, kps, counts, row_cap, ojobs);
     return hipGetLastError();
 }
 

@@ -17,13 +17,13 @@ hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf
                          uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int nframes,
                          hipStream_t st, const hipStream_t *side = nullptr, int nside = 0, hipEvent_t fork = nullptr,
                          const hipEvent_t *join = nullptr);
+// keypoint rows + per-row orientation jobs (uint2 per selection slot: centre byte offset, w | level << 16)
 hipError_t launch_emit_kps(const Plan &hp, const Plan *dp, const uint32_t *sel, const int *selcnt,
-                           const int *n_existing, ygzfe_kp *kps, int *counts, int row_cap, int nframes,
+                           const int *n_existing, ygzfe_kp *kps, int *counts, int row_cap, uint2 *ojobs, int nframes,
                            hipStream_t st);
 hipError_t launch_orient_desc(const uint8_t *pyr, const uint8_t *blur, uint32_t pitch, const Plan &hp,
-                              const Plan *dp, const uint32_t *sel, const int *selcnt, const int *n_existing,
-                              ygzfe_kp *kps, uint8_t *desc, int *counts, int row_cap, int nframes,
-                              hipStream_t st);
+                              const Plan *dp, const uint2 *ojobs, const int *n_existing, ygzfe_kp *kps,
+                              uint8_t *desc, int row_cap, int nframes, hipStream_t st);
 hipError_t launch_desc_existing(const uint8_t *pyr, const uint8_t *blur, const Plan *dp, ygzfe_kp *kps,
                                 uint8_t *desc, int n, int recompute_angle, hipStream_t st);
 
@@ -163,6 +163,8 @@ hipError_t launch_search_direct(const uint8_t *const *ref_pyrs, const AlignLevel
                                 int32_t *matched, hipStream_t st);
 
 // slots.hip: offline sequence mode result slots
+hipError_t launch_pack_result(const ygzfe_kp *kps, const uint8_t *desc, const int *counts, int *err, int rows,
+                              uint8_t *out, size_t kbytes, hipStream_t st);
 hipError_t launch_pack_slots(const ygzfe_kp *kps, const uint8_t *desc, const int *counts, int kp_cap,
                              const ygzfe_align_result *align, int frame_begin, int n_frames, int global_first,
                              uint8_t *slots, size_t slot_pitch, hipStream_t st);
