@@ -237,40 +237,140 @@ static int fast9_test(const uint8_t *p, const int pix[25], int threshold) {
     return 0;
 }
 
+/* The segment test on 16 consecutive pixels at once (GCC vector extensions:
+ * int16 lanes, AVX2 / AVX-512 under -march=native), the form FAST_t's own SSE2
+ * path takes: the compass points 0/4/8/12 screen the block, then the masks of
+ * all 16 ring pixels and a run of 9 by doubling (runs of 2, 4, 8, then + 1).
+ * Bit i of the result = fast9_test(p + i); the whole ring of every lane lies
+ * inside the row window [p - 3, p + 18]. */
+typedef int16_t ygzo_i16x16 __attribute__((vector_size(32)));
+typedef uint8_t ygzo_u8x16 __attribute__((vector_size(16)));
+static inline ygzo_i16x16 ld16(const uint8_t *p) {
+    ygzo_u8x16 b;
+    memcpy(&b, p, 16);
+    return __builtin_convertvector(b, ygzo_i16x16);
+}
+static inline int any16(ygzo_i16x16 m) {
+    uint64_t q[4];
+    memcpy(q, &m, 32);
+    return (q[0] | q[1] | q[2] | q[3]) != 0;
+}
+static inline ygzo_i16x16 vmin(ygzo_i16x16 a, ygzo_i16x16 b) {
+    const ygzo_i16x16 m = a < b;
+    return (a & m) | (b & ~m);
+}
+static inline ygzo_i16x16 vmax(ygzo_i16x16 a, ygzo_i16x16 b) {
+    const ygzo_i16x16 m = a > b;
+    return (a & m) | (b & ~m);
+}
+/* Also the 16 scores, cornerScore<16> in the closed form the GPU uses (checked
+ * against ygzo_corner_score16 by tests/test_cpu_oracle_props.py): with
+ * e_k = r_k - v, arcmax = max(max_k min e[k..k+8], max_k min -e[k..k+8]) by
+ * min / max doubling; corner <=> arcmax > t, score = arcmax - 1. */
+static unsigned fast9_test16(const uint8_t *p, const int pix[25], int threshold, int16_t score[16]) {
+    const ygzo_i16x16 v = ld16(p);
+    const ygzo_i16x16 lo = v - (int16_t)threshold, hi = v + (int16_t)threshold;
+    ygzo_i16x16 e[16];
+    for (int k = 0; k < 16; k += 4) e[k] = ld16(p + pix[k]);
+    const ygzo_i16x16 scr = (((e[0] < lo) | (e[8] < lo)) & ((e[4] < lo) | (e[12] < lo))) |
+                            (((e[0] > hi) | (e[8] > hi)) & ((e[4] > hi) | (e[12] > hi)));
+    if (!any16(scr)) return 0u;
+    for (int k = 0; k < 16; k++) {
+        if (k & 3) e[k] = ld16(p + pix[k]);
+        e[k] -= v;
+    }
+    ygzo_i16x16 n2[16], x2[16], n4[16], x4[16];
+    for (int k = 0; k < 16; k++) { n2[k] = vmin(e[k], e[(k + 1) & 15]); x2[k] = vmax(e[k], e[(k + 1) & 15]); }
+    for (int k = 0; k < 16; k++) { n4[k] = vmin(n2[k], n2[(k + 2) & 15]); x4[k] = vmax(x2[k], x2[(k + 2) & 15]); }
+    ygzo_i16x16 bright = vmin(vmin(n4[0], n4[4]), e[8]), darkmin = vmax(vmax(x4[0], x4[4]), e[8]);
+    for (int k = 1; k < 16; k++) {
+        bright = vmax(bright, vmin(vmin(n4[k], n4[(k + 4) & 15]), e[(k + 8) & 15]));
+        darkmin = vmin(darkmin, vmax(vmax(x4[k], x4[(k + 4) & 15]), e[(k + 8) & 15]));
+    }
+    const ygzo_i16x16 am = vmax(bright, -darkmin);
+    const ygzo_i16x16 c = am > (int16_t)threshold;
+    if (!any16(c)) return 0u;
+    unsigned m = 0;
+    for (int i = 0; i < 16; i++) {
+        m |= (unsigned)(c[i] != 0) << i;
+        score[i] = (int16_t)(am[i] - 1);
+    }
+    return m;
+}
+
+/* 0: the 16-pixel vector segment test (default), 1: scalar only (test hook) */
+static int g_fast_scalar = 0;
+void ygzo_fast9_force_scalar(int on) { g_fast_scalar = on; }
+
 int ygzo_fast9_roi(const uint8_t *roi, int w, int h, int stride, int threshold, int16_t *xs,
                    int16_t *ys, uint8_t *scores, int cap) {
     if (threshold < 0) threshold = 0;
     if (threshold > 255) threshold = 255;
     int pix[25];
     ring_offsets(stride, pix);
-    /* score map over the ROI, 0 where no corner (FAST_t's row buffers) */
-    uint8_t *sc = (uint8_t *)calloc((size_t)w * h, 1);
-    for (int y = 3; y < h - 3; y++)
-        for (int x = 3; x < w - 3; x++) {
+    /* score map over the ROI, 0 where no corner (FAST_t's row buffers), and the
+     * corner positions in raster order (the NMS visits only those) */
+    uint8_t sc_stack[96 * 96];
+    int32_t pos_stack[1024];
+    const size_t npx = (size_t)w * h;
+    uint8_t *sc = npx <= sizeof(sc_stack) ? sc_stack : (uint8_t *)malloc(npx);
+    int32_t *pos = npx <= 1024 ? pos_stack : (int32_t *)malloc(sizeof(int32_t) * npx);
+    memset(sc, 0, npx);
+    int nc = 0;
+    for (int y = 3; y < h - 3; y++) {
+        int x = 3;
+        if (!g_fast_scalar)
+            for (; x + 16 <= w - 3; x += 16) {  /* ring of lane 15: columns x + 12 .. x + 18 <= w - 1 */
+                const uint8_t *p = roi + (size_t)y * stride + x;
+                int16_t s16[16];
+                unsigned m = fast9_test16(p, pix, threshold, s16);
+                while (m) {
+                    const int i = __builtin_ctz(m);
+                    m &= m - 1;
+                    sc[(size_t)y * w + x + i] = (uint8_t)s16[i];
+                    pos[nc++] = y * w + x + i;
+                }
+            }
+        if (!g_fast_scalar && x < w - 3 && w - 19 >= 3) {  /* the tail: one block ending at column w - 4 */
+            const int xb = w - 19;
+            const uint8_t *p = roi + (size_t)y * stride + xb;
+            int16_t s16[16];
+            unsigned m = fast9_test16(p, pix, threshold, s16) & (0xFFFFu << (x - xb));
+            while (m) {
+                const int i = __builtin_ctz(m);
+                m &= m - 1;
+                sc[(size_t)y * w + xb + i] = (uint8_t)s16[i];
+                pos[nc++] = y * w + xb + i;
+            }
+            x = w - 3;
+        }
+        for (; x < w - 3; x++) {
             const uint8_t *p = roi + (size_t)y * stride + x;
             if (fast9_test(p, pix, threshold)) {
                 int s = ygzo_corner_score16(p, stride, threshold);
-                sc[(size_t)y * w + x] = (uint8_t)s;
-                if (sc[(size_t)y * w + x] == 0) sc[(size_t)y * w + x] = 0; /* uchar cast as in FAST_t */
+                sc[(size_t)y * w + x] = (uint8_t)s; /* uchar cast as in FAST_t */
+                pos[nc++] = y * w + x;
             }
         }
+    }
     /* nonmax: strictly greater than all 8 neighbours; raster order */
     int n = 0;
-    for (int y = 3; y < h - 3; y++)
-        for (int x = 3; x < w - 3; x++) {
-            int s = sc[(size_t)y * w + x];
-            if (!s) {
-                /* a corner with score 0 can never survive the strict test */
-                continue;
+    for (int k = 0; k < nc; k++) {
+        const uint8_t *r = sc + pos[k];
+        const int s = r[0];
+        if (!s) continue; /* a corner with score 0 can never survive the strict test */
+        if (s > r[-1] && s > r[1] && s > r[-w - 1] && s > r[-w] && s > r[-w + 1] &&
+            s > r[w - 1] && s > r[w] && s > r[w + 1]) {
+            if (n < cap) {
+                xs[n] = (int16_t)(pos[k] % w);
+                ys[n] = (int16_t)(pos[k] / w);
+                scores[n] = (uint8_t)s;
             }
-            const uint8_t *r = sc + (size_t)y * w + x;
-            if (s > r[-1] && s > r[1] && s > r[-w - 1] && s > r[-w] && s > r[-w + 1] &&
-                s > r[w - 1] && s > r[w] && s > r[w + 1]) {
-                if (n < cap) { xs[n] = (int16_t)x; ys[n] = (int16_t)y; scores[n] = (uint8_t)s; }
-                n++;
-            }
+            n++;
         }
-    free(sc);
+    }
+    if (pos != pos_stack) free(pos);
+    if (sc != sc_stack) free(sc);
     return n;
 }
 
@@ -599,11 +699,10 @@ void ygzo_gaussian_blur7(const uint8_t *src, int w, int h, int stride, uint8_t *
         const int *rr[7];
         for (int t = 0; t < 7; t++) rr[t] = rows + (size_t)reflect101(y + t - 3, h) * w;
         uint8_t *o = dst + (size_t)y * dstride;
-        for (int x = 0; x < w; x++) {
-            long long acc = (long long)k[0] * rr[0][x] + (long long)k[1] * rr[1][x] + (long long)k[2] * rr[2][x] +
-                            (long long)k[3] * rr[3][x] + (long long)k[4] * rr[4][x] + (long long)k[5] * rr[5][x] +
-                            (long long)k[6] * rr[6][x];
-            o[x] = (uint8_t)clampi((int)((acc + 32768) >> 16), 0, 255);
+        for (int x = 0; x < w; x++) {  /* <= 257 * 255 * 256 + 32768 < 2^31: int32 (vectorises) */
+            const int acc = k[0] * rr[0][x] + k[1] * rr[1][x] + k[2] * rr[2][x] + k[3] * rr[3][x] +
+                            k[4] * rr[4][x] + k[5] * rr[5][x] + k[6] * rr[6][x];
+            o[x] = (uint8_t)clampi((acc + 32768) >> 16, 0, 255);
         }
     }
     free(rows);

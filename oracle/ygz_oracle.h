@@ -73,6 +73,8 @@ int ygzo_fast9_roi(const uint8_t *roi, int w, int h, int stride, int threshold,
                    int16_t *xs, int16_t *ys, uint8_t *scores, int cap);
 /* OpenCV cornerScore<16>. */
 int ygzo_corner_score16(const uint8_t *ptr, int stride, int threshold);
+/* test hook: 1 = scalar segment test only (default: 16-pixel vectors) */
+void ygzo_fast9_force_scalar(int on);
 
 /* ComputeKeyPointsOctTree for one level (ORBextractor.cc:725-799), without
  * orientation.  Returns the distributed keypoints in list order. */

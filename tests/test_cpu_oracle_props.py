@@ -57,6 +57,28 @@ def test_fast9_score_closed_form_vs_brute_force():
     assert n_corners > 500
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_fast9_vector_segment_test_equals_scalar(seed):
+    """The oracle's 16-pixel vector segment test (the CPU baseline's FAST) finds
+    exactly the scalar test's corners, scores and NMS survivors: ROIs of every
+    width (block and tail columns), corner-rich noise and smooth ramps."""
+    rng = np.random.default_rng(seed)
+    lib = O.lib()
+    for trial in range(60):
+        h, w = int(rng.integers(7, 60)), int(rng.integers(7, 90))
+        img = rng.integers(0, 256, size=(h, w), dtype=np.uint8)
+        if trial % 3 == 1:  # piecewise-flat blocks: long runs, ties
+            img = (rng.integers(0, 6, size=(h // 4 + 2, w // 4 + 2)) * 50).astype(np.uint8).repeat(4, 0).repeat(4, 1)[:h, :w]
+        img = np.ascontiguousarray(img)
+        for t in (5, 20, 60):
+            lib.ygzo_fast9_force_scalar(1)
+            ref = O.fast9_roi(img, t)
+            lib.ygzo_fast9_force_scalar(0)
+            got = O.fast9_roi(img, t)
+            for a, b in zip(ref, got):
+                assert np.array_equal(a, b), (trial, t)
+
+
 def test_resize_exact_half_is_area_average():
     rng = np.random.default_rng(1)
     src = rng.integers(0, 256, size=(60, 94), dtype=np.uint8)
