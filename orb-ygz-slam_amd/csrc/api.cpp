@@ -206,7 +206,7 @@ struct ygzfe_extractor {
     hipEvent_t ev_oct_fork = nullptr, ev_oct_join[2] = {nullptr, nullptr};
     HostBuf hin, hout;
     DevBuf res, align_in, align_scratch, align_out;
-    bool err_clean = false;  // ws.err zeroed (k_pack_result re-zeroes it after each read)
+    bool graph_broken = false;  // stream capture failed once: plain launches
     std::mutex mu;
     int ensure_side() {
         if (side[0]) return YGZFE_OK;
@@ -226,6 +226,19 @@ struct ygzfe_frame {
     PlanDev *plan = nullptr;
     int W = 0, H = 0;
     DevBuf pyr;
+    // the captured single-frame extraction (ygzfe_extract, no existing rows)
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    const void *gkey[9] = {};
+    int grows = 0;
+    size_t gcopy = 0;
+    void drop_graph() {
+        if (gexec) (void)hipGraphExecDestroy(gexec);
+        if (graph) (void)hipGraphDestroy(graph);
+        gexec = nullptr;
+        graph = nullptr;
+    }
+    ~ygzfe_frame() { drop_graph(); }
 };
 
 struct ygzfe_batch {
@@ -523,51 +536,85 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
         // angle + rBRIEF after the join; one packing kernel, one D2H into pinned
         // memory, one synchronisation.
         YGZ_TRY(ex->ensure_side());
+        // The rows, descriptors, count and octree-overflow flag are written straight
+        // into one result buffer -- [count, flag, 0, 0][rows x 28 B keypoints]
+        // [16-B aligned: rows x 32 B descriptors] -- so one D2H returns everything.
+        const size_t kbytes = align16(sizeof(ygzfe_kp) * (size_t)rows), rbytes = 16 + kbytes + (size_t)32 * rows;
+        YGZ_TRY(ex->res.ensure(rbytes));
+        YGZ_TRY(ex->hout.ensure(rbytes));
+        uint8_t *res = ex->res.as<uint8_t>();
+        int *d_count = reinterpret_cast<int *>(res), *d_err = d_count + 1;
+        ygzfe_kp *d_kps = reinterpret_cast<ygzfe_kp *>(res + 16);
+        uint8_t *d_desc = res + 16 + kbytes;
         const int *d_nexist = nullptr;  // null: no existing rows (the kernels read 0)
         if (n_existing > 0) {
             YGZ_TRY(ex->hin.ensure(16 + sizeof(ygzfe_kp) * (size_t)n_existing));
             ex->hin.as<int>()[0] = n_existing;
             memcpy(ex->hin.as<uint8_t>() + 16, kps_io, sizeof(ygzfe_kp) * n_existing);
             YGZ_HIP(hipMemcpyAsync(ws.nexist.p, ex->hin.p, sizeof(int), hipMemcpyHostToDevice, st));
-            YGZ_HIP(hipMemcpyAsync(ws.kps.p, ex->hin.as<uint8_t>() + 16, sizeof(ygzfe_kp) * n_existing,
+            YGZ_HIP(hipMemcpyAsync(d_kps, ex->hin.as<uint8_t>() + 16, sizeof(ygzfe_kp) * n_existing,
                                    hipMemcpyHostToDevice, st));
             d_nexist = ws.nexist.as<int>();
         }
-        if (!ex->err_clean) {
-            YGZ_HIP(hipMemsetAsync(ws.err.p, 0, 16, st));
-            ex->err_clean = true;
-        }
-        hipStream_t *sd = ex->side;
-        YGZ_HIP(hipEventRecord(ex->ev_fork, st));
-        for (int i = 0; i < 3; i++) YGZ_HIP(hipStreamWaitEvent(sd[i], ex->ev_fork, 0));
-        YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), 1, sd[0]));
-        YGZ_HIP(hipEventRecord(ex->ev_join[0], sd[0]));
-        YGZ_HIP(launch_fast(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(), ws.cellbuf.as<uint32_t>(),
-                            ws.cellcnt.as<int>(), 1, st, &sd[1], 2));
-        for (int i = 1; i < 3; i++) {
-            YGZ_HIP(hipEventRecord(ex->ev_join[i], sd[i]));
-            YGZ_HIP(hipStreamWaitEvent(st, ex->ev_join[i], 0));
-        }
-        YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
-                              ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.err.as<int>(), 1,
-                              st, &sd[1], 2, ex->ev_oct_fork, ex->ev_oct_join));
-        YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_nexist,
-                                ws.kps.as<ygzfe_kp>(), ws.counts.as<int>(), rows, ws.ojobs.as<uint2>(), 1, st));
-        YGZ_HIP(hipStreamWaitEvent(st, ex->ev_join[0], 0));  // the blurred levels
-        YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.ojobs.as<uint2>(),
-                                   d_nexist, ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(), rows, 1, st));
-        YGZ_HIP(launch_desc_existing(pyr, ws.blur.as<uint8_t>(), pd.dp(), ws.kps.as<ygzfe_kp>(),
-                                     ws.desc.as<uint8_t>(), n_existing, 0, st));
-        // [count, overflow flag, 0, 0][rows x 28 B keypoints][16-B aligned: rows x 32 B descriptors]
-        const size_t kbytes = align16(sizeof(ygzfe_kp) * (size_t)rows), rbytes = 16 + kbytes + (size_t)32 * rows;
-        YGZ_TRY(ex->res.ensure(rbytes));
-        YGZ_TRY(ex->hout.ensure(rbytes));
-        YGZ_HIP(launch_pack_result(ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(), ws.counts.as<int>(), ws.err.as<int>(),
-                                   rows, ex->res.as<uint8_t>(), kbytes, st));
         // the header and, speculatively, as many rows as the caller can take (one DMA)
         const int cap_rows = std::min(rows, std::max(cap, 0));
         const size_t copy = desc ? 16 + kbytes + (size_t)32 * cap_rows : 16 + sizeof(ygzfe_kp) * (size_t)cap_rows;
-        YGZ_HIP(hipMemcpyAsync(ex->hout.p, ex->res.p, copy, hipMemcpyDeviceToHost, st));
+        hipStream_t *sd = ex->side;
+        // the DAG: blur on side[0] beside FAST (every level in one launch; its first
+        // lane also clears the overflow flag) on st; the octree's node-pool classes on st / side[1] / side[2];
+        // rows + jobs, then angle + rBRIEF after the blur joins; the D2H
+        auto enqueue = [&]() -> int {
+            YGZ_HIP(hipEventRecord(ex->ev_fork, st));
+            for (int i = 0; i < 3; i++) YGZ_HIP(hipStreamWaitEvent(sd[i], ex->ev_fork, 0));
+            YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), 1, sd[0]));
+            YGZ_HIP(hipEventRecord(ex->ev_join[0], sd[0]));
+            YGZ_HIP(launch_fast_merged(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(),
+                                       ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), 1, st, d_err));
+            YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
+                                  ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_err, 1, st,
+                                  &sd[1], 2, ex->ev_oct_fork, ex->ev_oct_join));
+            YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_nexist, d_kps, d_count,
+                                    rows, ws.ojobs.as<uint2>(), 1, st));
+            YGZ_HIP(hipStreamWaitEvent(st, ex->ev_join[0], 0));  // the blurred levels
+            YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.ojobs.as<uint2>(),
+                                       d_nexist, d_kps, d_desc, rows, 1, st));
+            YGZ_HIP(launch_desc_existing(pyr, ws.blur.as<uint8_t>(), pd.dp(), d_kps, d_desc, n_existing, 0, st));
+            YGZ_HIP(hipMemcpyAsync(ex->hout.p, res, copy, hipMemcpyDeviceToHost, st));
+            return YGZFE_OK;
+        };
+        // Without existing rows the whole sequence (9-12 launches, the event fork /
+        // joins and the D2H) is replayed from a HIP graph captured once per frame
+        // handle: one submission instead of one host call per launch.  The graph is
+        // re-captured when any buffer it names has moved or the copy size changed.
+        const void *key[9] = {pyr, ws.blur.p, ws.cellbuf.p, ws.sel.p, ws.candA.p, ws.candB.p, ex->res.p, ex->hout.p,
+                              ws.ojobs.p};
+        static const bool no_graph = getenv("YGZFE_NO_GRAPH") != nullptr;
+        bool launched = false;
+        if (n_existing == 0 && !no_graph && !ex->graph_broken) {
+            if (!f->gexec || memcmp(f->gkey, key, sizeof(key)) != 0 || f->grows != rows || f->gcopy != copy) {
+                f->drop_graph();
+                bool ok = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess;
+                const int rc = ok ? enqueue() : YGZFE_EHIP;
+                hipGraph_t g = nullptr;
+                if (ok) ok = hipStreamEndCapture(st, &g) == hipSuccess && rc == YGZFE_OK && g;
+                if (ok) ok = hipGraphInstantiate(&f->gexec, g, nullptr, nullptr, 0) == hipSuccess;
+                f->graph = g;
+                if (ok) {
+                    memcpy(f->gkey, key, sizeof(key));
+                    f->grows = rows;
+                    f->gcopy = copy;
+                } else {  // capture unsupported here: plain launches from now on
+                    f->drop_graph();
+                    ex->graph_broken = true;
+                    (void)hipGetLastError();
+                }
+            }
+            if (f->gexec) {
+                YGZ_HIP(hipGraphLaunch(f->gexec, st));
+                launched = true;
+            }
+        }
+        if (!launched) YGZ_TRY(enqueue());
         YGZ_HIP(hipStreamSynchronize(st));
         total = ex->hout.as<int>()[0];
         if (ex->hout.as<int>()[1]) {

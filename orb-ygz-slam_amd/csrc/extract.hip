@@ -673,7 +673,7 @@ template <int S, int R>
 __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(YGZ_FAST_WAVES_EU))) void k_fast_cells(
     const uint8_t *__restrict__ pyr, uint32_t pitch, const Plan *__restrict__ plan,
     const CellDesc *__restrict__ cells, uint32_t *__restrict__ cellbuf, int *__restrict__ cellcnt, int cell_begin,
-    int cell_end, int level) {
+    int cell_end, int level, int *__restrict__ clear_flag) {
     extern __shared__ uint8_t s_dyn[];
     constexpr int slice = (2 * S * R + 2 * (S - 6) * (R - 6) + 15) / 16 * 16;  // 16-B aligned slices
     // wave-uniform cell index: the CellDesc and the level record come by scalar
@@ -682,12 +682,15 @@ __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     const int c = cell_begin + blockIdx.x * kFastWaves + wave;
+    if (clear_flag && c == cell_begin && f == 0 && lane == 0) *clear_flag = 0;  // the octree's overflow flag
     if (c >= cell_end) return;
     uint8_t *img = s_dyn + wave * slice;
     uint8_t *sc = img + S * R;
     uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * R);
     const CellDesc cd = scalar_load(cells + c);
-    const LevelDesc &L = plan->lv[level];  // one launch per level: loaded beside cd, not after it
+    // one launch per level: the level record loads beside cd, not after it;
+    // level < 0 (one launch over every level's cells): the cell's own level
+    const LevelDesc &L = plan->lv[level >= 0 ? level : cd.level];
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(pyr + (size_t)f * pitch + L.off), 0, (int)((uint32_t)L.w * (uint32_t)L.h), 0x00020000);
     const uint32_t off0 = (uint32_t)cd.y0 * (uint32_t)L.w + (uint32_t)cd.x0;  // ROI origin in the level
@@ -1547,7 +1550,7 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
         // level 0 on the caller's stream, the others spread over the given side streams
         const hipStream_t st = (l == 0 || !lvl_streams || n_lvl_streams <= 0) ? st0
                                                                                 : lvl_streams[(l - 1) % n_lvl_streams];
-#define YGZ_FAST(SS, RR) hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce, l)
+#define YGZ_FAST(SS, RR) hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce, l, nullptr)
         if (S == 40 && R == 40) YGZ_FAST(40, 40);
         else if (S == 40 && R == 48) YGZ_FAST(40, 48);
         else if (S == 40 && R == 56) YGZ_FAST(40, 56);
@@ -1557,6 +1560,34 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
         else YGZ_FAST(72, 72);
 #undef YGZ_FAST
     }
+    return hipGetLastError();
+}
+
+// Every level's cells in ONE launch (the single-frame path: one frame's 412
+// C2 cells fill the GPU anyway, and three dependent launches cost three
+// dispatch gaps): the LDS slice of the largest ROI of any level.
+hipError_t launch_fast_merged(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp,
+                              const CellDesc *dcells, uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st,
+                              int *clear_flag) {
+    if (hp.ncells == 0) return hipSuccess;
+    int S = 40, R = 40;
+    for (int l = 0; l < hp.nlevels; l++) {
+        if (hp.lv[l].ncells == 0) continue;
+        S = std::max(S, fast_stride(hp.lv[l].fast_rw));
+        R = std::max(R, fast_stride(hp.lv[l].fast_rh));
+    }
+    if (!(S == 40 && R <= 56)) S = R = std::max(S, R);
+    const size_t lds = fast_cells_lds_bytes(S, R);
+    const dim3 grid((hp.ncells + kFastWaves - 1) / kFastWaves, nframes);
+#define YGZ_FAST(SS, RR) hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, 0, hp.ncells, -1, clear_flag)
+    if (S == 40 && R == 40) YGZ_FAST(40, 40);
+    else if (S == 40 && R == 48) YGZ_FAST(40, 48);
+    else if (S == 40 && R == 56) YGZ_FAST(40, 56);
+    else if (S == 48) YGZ_FAST(48, 48);
+    else if (S == 56) YGZ_FAST(56, 56);
+    else if (S == 64) YGZ_FAST(64, 64);
+    else YGZ_FAST(72, 72);
+#undef YGZ_FAST
     return hipGetLastError();
 }
 

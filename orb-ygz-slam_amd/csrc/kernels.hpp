@@ -13,6 +13,10 @@ hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const 
 hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const CellDesc *dcells,
                        uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st,
                        const hipStream_t *lvl_streams = nullptr, int n_lvl_streams = 0);
+// every level's cells in one launch; clear_flag (nullable) is zeroed by the first lane
+hipError_t launch_fast_merged(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp,
+                              const CellDesc *dcells, uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st,
+                              int *clear_flag = nullptr);
 hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
                          uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int nframes,
                          hipStream_t st, const hipStream_t *side = nullptr, int nside = 0, hipEvent_t fork = nullptr,
@@ -163,8 +167,6 @@ hipError_t launch_search_direct(const uint8_t *const *ref_pyrs, const AlignLevel
                                 int32_t *matched, hipStream_t st);
 
 // slots.hip: offline sequence mode result slots
-hipError_t launch_pack_result(const ygzfe_kp *kps, const uint8_t *desc, const int *counts, int *err, int rows,
-                              uint8_t *out, size_t kbytes, hipStream_t st);
 hipError_t launch_pack_slots(const ygzfe_kp *kps, const uint8_t *desc, const int *counts, int kp_cap,
                              const ygzfe_align_result *align, int frame_begin, int n_frames, int global_first,
                              uint8_t *slots, size_t slot_pitch, hipStream_t st);

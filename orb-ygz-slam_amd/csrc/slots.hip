@@ -64,35 +64,6 @@ __global__ __launch_bounds__(256) void k_pack_slots(const ygzfe_kp *__restrict__
     for (int i = used + t; i < total; i += 256) s[i] = 0u;
 }
 
-// Single-frame extraction result in one buffer for one D2H (ygzfe_extract):
-// [count, octree-overflow flag, 0, 0][rows x 28 B keypoints][at 16 + kbytes:
-// rows x 32 B descriptors]; only the first `count` rows are copied.  The flag is
-// re-zeroed for the next call.
-__global__ __launch_bounds__(256) void k_pack_result(const ygzfe_kp *__restrict__ kps,
-                                                     const uint8_t *__restrict__ desc, const int *__restrict__ counts,
-                                                     int *__restrict__ err, int rows, uint8_t *__restrict__ out,
-                                                     size_t kbytes) {
-    const int n = min(max(counts[0], 0), rows);
-    const int t = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
-    if (t == 0) {
-        const int e = err[0];
-        reinterpret_cast<int4 *>(out)[0] = make_int4(counts[0], e, 0, 0);
-        if (e) err[0] = 0;
-    }
-    const uint32_t *ks = reinterpret_cast<const uint32_t *>(kps);
-    uint32_t *kd = reinterpret_cast<uint32_t *>(out + 16);
-    for (int i = t; i < 7 * n; i += nt) kd[i] = ks[i];
-    const uint4 *ds = reinterpret_cast<const uint4 *>(desc);
-    uint4 *dd = reinterpret_cast<uint4 *>(out + 16 + kbytes);
-    for (int i = t; i < 2 * n; i += nt) dd[i] = ds[i];
-}
-
-hipError_t launch_pack_result(const ygzfe_kp *kps, const uint8_t *desc, const int *counts, int *err, int rows,
-                              uint8_t *out, size_t kbytes, hipStream_t st) {
-    hipLaunchKernelGGL(k_pack_result, dim3(4), dim3(256), 0, st, kps, desc, counts, err, rows, out, kbytes);
-    return hipGetLastError();
-}
-
 hipError_t launch_pack_slots(const ygzfe_kp *kps, const uint8_t *desc, const int *counts, int kp_cap,
                              const ygzfe_align_result *align, int frame_begin, int n_frames, int global_first,
                              uint8_t *slots, size_t slot_pitch, hipStream_t st) {
