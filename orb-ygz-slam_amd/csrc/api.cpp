@@ -204,7 +204,8 @@ struct ygzfe_extractor {
     hipStream_t side[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_oct_fork = nullptr, ev_oct_join[2] = {nullptr, nullptr};
-    HostBuf hin, hout;
+    HostBuf hin, hout, himg;
+    hipEvent_t ev_img = nullptr;  // the last image DMA out of himg
     DevBuf res, align_in, align_scratch, align_out;
     bool graph_broken = false;  // stream capture failed once: plain launches
     std::mutex mu;
@@ -216,6 +217,7 @@ struct ygzfe_extractor {
         }
         YGZ_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
         YGZ_HIP(hipEventCreateWithFlags(&ev_oct_fork, hipEventDisableTiming));
+        YGZ_HIP(hipEventCreateWithFlags(&ev_img, hipEventDisableTiming));
         for (int i = 0; i < 2; i++) YGZ_HIP(hipEventCreateWithFlags(&ev_oct_join[i], hipEventDisableTiming));
         return YGZFE_OK;
     }
@@ -358,6 +360,7 @@ void ygzfe_extractor_destroy(ygzfe_extractor *ex) {
         if (ex->ev_join[i]) (void)hipEventDestroy(ex->ev_join[i]);
     }
     if (ex->ev_fork) (void)hipEventDestroy(ex->ev_fork);
+    if (ex->ev_img) (void)hipEventDestroy(ex->ev_img);
     if (ex->ev_oct_fork) (void)hipEventDestroy(ex->ev_oct_fork);
     for (int i = 0; i < 2; i++)
         if (ex->ev_oct_join[i]) (void)hipEventDestroy(ex->ev_oct_join[i]);
@@ -453,10 +456,22 @@ int ygzfe_compute_pyramid(ygzfe_extractor *ex, ygzfe_frame *f, const uint8_t *im
     if (!ex || !f || !img || stride < f->W) { set_error("invalid argument"); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(ex->device));
     std::lock_guard<std::mutex> lk(ex->mu);
-    // the pageable H2D returns once `img` is staged (the caller may reuse it);
-    // everything that reads the pyramid is ordered after it on ex->stream or
-    // synchronises first (ygzfe_frame_level), so no synchronisation here
-    YGZ_HIP(hipMemcpy2DAsync(f->pyr.p, f->W, img, stride, f->W, f->H, hipMemcpyHostToDevice, ex->stream));
+    // the image is copied into pinned staging (the caller may reuse `img` at once)
+    // and DMA'd from there; everything that reads the pyramid is ordered after it
+    // on ex->stream or synchronises first (ygzfe_frame_level), so no
+    // synchronisation here -- only before the staging is overwritten
+    YGZ_TRY(ex->ensure_side());
+    const size_t n = (size_t)f->W * f->H;
+    YGZ_TRY(ex->himg.ensure(n));
+    YGZ_HIP(hipEventSynchronize(ex->ev_img));
+    uint8_t *h = ex->himg.as<uint8_t>();
+    if (stride == f->W) {
+        memcpy(h, img, n);
+    } else {
+        for (int y = 0; y < f->H; y++) memcpy(h + (size_t)y * f->W, img + (size_t)y * stride, (size_t)f->W);
+    }
+    YGZ_HIP(hipMemcpyAsync(f->pyr.p, h, n, hipMemcpyHostToDevice, ex->stream));
+    YGZ_HIP(hipEventRecord(ex->ev_img, ex->stream));
     YGZ_TRY(pyramid_from_level0(f, ex->stream));
     return YGZFE_OK;
 }
@@ -572,7 +587,7 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
                                        ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), 1, st, d_err));
             YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
                                   ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_err, 1, st,
-                                  &sd[1], 2, ex->ev_oct_fork, ex->ev_oct_join));
+                                  &sd[1], 2, ex->ev_oct_fork, ex->ev_oct_join, true));
             YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_nexist, d_kps, d_count,
                                     rows, ws.ojobs.as<uint2>(), 1, st));
             YGZ_HIP(hipStreamWaitEvent(st, ex->ev_join[0], 0));  // the blurred levels

@@ -1607,8 +1607,15 @@ constexpr int kOctThreads = YGZ_OCT_THREADS;
 
 static hipError_t launch_octree_levels(int nc, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
                                        uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err,
-                                       int nframes, int l0, int nl, hipStream_t st) {
+                                       int nframes, int l0, int nl, hipStream_t st, bool wide) {
     dim3 grid(nframes, nl);
+    // one frame (the latency path): a workgroup per level has the CU to itself,
+    // so the largest class takes 1024 threads (shorter strided loops per pass)
+    if (wide && nc > 512 && nc <= 1024) {
+        hipLaunchKernelGGL((k_octree<1024, 4000, 1024>), grid, dim3(1024), 0, st, dp, cellbuf, cellcnt, candA, candB,
+                           sel, selcnt, err, l0);
+        return hipGetLastError();
+    }
     // LDS keys: 4000 with NC 1024 (two workgroups per CU), the larger levels' share below
     if (nc <= 256)
         hipLaunchKernelGGL((k_octree<256, 1536>), grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel,
@@ -1629,7 +1636,8 @@ static hipError_t launch_octree_levels(int nc, const Plan *dp, const uint32_t *c
 // first run on the side streams (fork after, join before the caller's next work).
 hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
                          uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int nframes,
-                         hipStream_t st, const hipStream_t *side, int nside, hipEvent_t fork, const hipEvent_t *join) {
+                         hipStream_t st, const hipStream_t *side, int nside, hipEvent_t fork, const hipEvent_t *join,
+                         bool wide) {
     int l = 0, g = 0;
     if (side && nside > 0) YGZ_HIPR(hipEventRecord(fork, st));  // before the first group: the groups are independent
     while (l < hp.nlevels) {
@@ -1641,7 +1649,8 @@ hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf
             s = side[g - 1];
             YGZ_HIPR(hipStreamWaitEvent(s, fork, 0));
         }
-        YGZ_HIPR(launch_octree_levels(nc, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, nframes, l, e - l, s));
+        YGZ_HIPR(launch_octree_levels(nc, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, nframes, l, e - l, s,
+                                      wide));
         if (s != st) YGZ_HIPR(hipEventRecord(join[g - 1], s));
         l = e;
         g++;
