@@ -868,9 +868,10 @@ int ygzfe_batch_extract(ygzfe_batch *b, int n_frames, void *stream) {
 // resident frames, `reps` back-to-back launch sets on the batch stream, average
 // ms per set (hipEvents).  stage 0: FAST (writes only the cell scratch; pyramid
 // levels built first when build_pyramid); stage 1: orientation + rBRIEF on the
-// octree selection of the last full extraction (rewrites its angles and descriptors).
+// octree selection of the last full extraction (rewrites its angles and descriptors);
+// stage 2: the GaussianBlur of every level.
 int ygzfe_diag_stage_ms(ygzfe_batch *b, int stage, int n_frames, int reps, int build_pyramid, float *ms) {
-    if (!b || !ms || n_frames < 1 || n_frames > b->maxF || reps < 1 || stage < 0 || stage > 1) {
+    if (!b || !ms || n_frames < 1 || n_frames > b->maxF || reps < 1 || stage < 0 || stage > 2) {
         set_error("invalid argument");
         return YGZFE_EINVAL;
     }
@@ -889,6 +890,8 @@ int ygzfe_diag_stage_ms(ygzfe_batch *b, int stage, int n_frames, int reps, int b
         if (stage == 0)
             YGZ_HIP(launch_fast(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(), ws.cellbuf.as<uint32_t>(),
                                 ws.cellcnt.as<int>(), n_frames, b->stream));
+        else if (stage == 2)
+            YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), n_frames, b->stream));
         else
             YGZ_HIP(launch_orient_desc(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), ws.ojobs.as<uint2>(),
                                        nullptr, ws.kps.as<ygzfe_kp>(), ws.desc.as<uint8_t>(), P.kp_cap, n_frames,

@@ -30,7 +30,7 @@ def child(B, libpath):
     ms = C.c_float()
     out = []
     stages = [int(x) for x in os.environ.get("YGZ_MB_STAGES", "0,1").split(",")]
-    for stage, name in [(st, ("FAST", "orient")[st]) for st in stages]:
+    for stage, name in [(st, ("FAST", "orient", "blur")[st]) for st in stages]:
         if stage == 1:
             b.extract(B)  # the octree selection the orientation pass reads
             b.check()
