@@ -842,7 +842,7 @@ def cpu_baseline(frames, r3, cz, S, args, sc):
                     xs, _ = ref.detect(img, th, sse=True, x0=3, y0=3, w=W - 6, h=H - 6)
                 fs[f"ref_fast10_sse2_th{th}_ms"] = round((time.perf_counter() - t0) / 20 * 1e3, 4)
                 fs[f"ref_fast10_sse2_th{th}_corners"] = int(len(xs))
-        fs["note"] = ("oracle = cv::FAST TYPE_9_16 + score + 3x3 NMS restated (FAST_t's pair screening, scalar); "
+        fs["note"] = ("oracle = cv::FAST TYPE_9_16 + cornerScore + 3x3 NMS restated (segment test and score on 16-pixel int16 vectors, as OpenCV's SIMD FAST_t); "
                       "ref = the reference's own Thirdparty/fast SSE2 FAST-10 detect (oracle/_ref), detect only")
         line["fast_sanity"] = fs
     except Exception as e:  # test image / reference library absent
