@@ -1336,15 +1336,26 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
                                                      ygzfe_kp *__restrict__ kps, uint8_t *__restrict__ desc,
                                                      int row_cap) {
     __shared__ uint8_t s_patch[16][kPatchBytes];  // one 37x37 window per keypoint row
+    // the IC row weights (c_icw, 1 KB) and the pattern (c_pattern, 1 KB), staged
+    // once per workgroup instead of 8 vector loads per lane: the stage is bound by
+    // the vector-memory address path, and 16 rows share them
+    __shared__ uint4 s_const[128];
     int bx, f;
     swizzled_block_2d(bx, f);  // one frame's keypoints on one XCD: window lines shared in its L2
     const int lane = threadIdx.x & 63, s = lane & 15;
     const int idx = bx * 16 + (threadIdx.x >> 4);
+    uint4 cst = make_uint4(0u, 0u, 0u, 0u);
+    if (threadIdx.x < 128)
+        cst = threadIdx.x < 64 ? reinterpret_cast<const uint4 *>(c_icw)[threadIdx.x]
+                               : reinterpret_cast<const uint4 *>(c_pattern)[threadIdx.x - 64];
     const int sel_total = plan->sel_total;
-    if (idx >= sel_total) return;
-    const uint2 job = ojobs[(size_t)f * sel_total + idx];
-    if (job.x == kOrientNone) return;  // whole rows leave together
-    const uint32_t c = job.x, w = job.y & 0xFFFFu;
+    uint2 job = make_uint2(kOrientNone, 0u);
+    if (idx < sel_total) job = ojobs[(size_t)f * sel_total + idx];
+    const bool active = job.x != kOrientNone;
+    // inactive rows load a dummy window at the start of the frame (unconditional
+    // loads keep the wait counts static, so the barrier below waits only for the
+    // constants, not for the windows in flight)
+    const uint32_t c = active ? job.x : 18u * 64u + 18u, w = active ? job.y & 0xFFFFu : 64u;
     const uint8_t *fimg = pyr + (size_t)f * pitch;
     const uint8_t *fblur = blur + (size_t)f * pitch;
     uint8_t *P = s_patch[threadIdx.x >> 4];
@@ -1352,15 +1363,22 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     Window<18, 37> wdesc;
     wic.load(fimg, w, c, s);  // both windows in flight before the first wait
     wdesc.load(fblur, w, c, s);
-    // the lane's IC row weights (c_icw) and its 16 pattern pairs
-    const uint4 *icw = reinterpret_cast<const uint4 *>(c_icw[s]);
+    // publish the constants: LDS writes retired, then a bare s_barrier (a
+    // __syncthreads would also wait for the window loads in flight)
+    if (threadIdx.x < 128) s_const[threadIdx.x] = cst;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    wave_lds_order();
+    if (!active) return;  // whole rows leave together
     uint4 wq[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) wq[q] = icw[q];
-    const int4 *pp = reinterpret_cast<const int4 *>(c_pattern) + s * 4;  // 16 pairs x (x0,y0,x1,y1)
-    int4 pat[4];
+    for (int q = 0; q < 4; q++) wq[q] = s_const[s * 4 + q];
+    int4 pat[4];  // 16 pairs x (x0, y0, x1, y1) int8
 #pragma unroll
-    for (int q = 0; q < 4; q++) pat[q] = pp[q];
+    for (int q = 0; q < 4; q++) {
+        const uint4 u = s_const[64 + s * 4 + q];
+        pat[q] = make_int4((int)u.x, (int)u.y, (int)u.z, (int)u.w);
+    }
     const int ne = n_existing ? n_existing[f] : 0;
     float angle;
     {
