@@ -1320,6 +1320,31 @@ __global__ __launch_bounds__(256) void k_emit_kps(const Plan *__restrict__ plan,
         make_uint2(L.off + (uint32_t)cy * (uint32_t)L.w + (uint32_t)cx, (uint32_t)L.w | ((uint32_t)l << 16));
 }
 
+// The IC window (31 rows from cy - 15) staged with the three aligned 16-B
+// chunks a row needs (misalignment + 31 <= 46 B): chunk c = s + 16 k of the
+// keypoint's 93 is row c / 3, chunk c % 3; row r at patch_row_swz(r) in LDS.
+struct IcWindow {
+    u32x4 v[6];
+    __device__ __forceinline__ void load(const uint8_t *frame, uint32_t w, uint32_t c, int s) {
+        const uint32_t base = c - 15u * w - 15u;
+        const uint32_t a0 = (uint32_t)(uintptr_t)frame & 15u;
+#pragma unroll
+        for (int k = 0; k < 6; k++) {  // slots past chunk 92 re-read it (not stored)
+            const uint32_t ch = min((uint32_t)(s + 16 * k), 92u), r = ch / 3u, j = ch - 3u * r;
+            const uint32_t o = ((mad24(r, w, base) + a0) & ~15u) - a0 + 16u * j;
+            v[k] = as_global(reinterpret_cast<const u32x4 *>(frame + o))[0];
+        }
+    }
+    __device__ __forceinline__ void store(uint8_t *P, int s) const {
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const uint32_t ch = (uint32_t)(s + 16 * k), r = ch / 3u, j = ch - 3u * r;
+            if (k < 5 || ch < 93u) *reinterpret_cast<u32x4 *>(P + patch_row_swz(r) + 16u * j) = v[k];
+        }
+        wave_lds_order();
+    }
+};
+
 // New keypoints of the octree: rows n_existing + selection index.
 // One 16-lane DPP row per keypoint (four per wave, sixteen per workgroup):
 //   IC_Angle: lane s takes window rows 15 +- (s + 1) (lane 15: the centre row)
@@ -1359,7 +1384,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     const uint8_t *fimg = pyr + (size_t)f * pitch;
     const uint8_t *fblur = blur + (size_t)f * pitch;
     uint8_t *P = s_patch[threadIdx.x >> 4];
-    Window<15, 31> wic;
+    IcWindow wic;
     Window<18, 37> wdesc;
     wic.load(fimg, w, c, s);  // both windows in flight before the first wait
     wdesc.load(fblur, w, c, s);
@@ -1382,7 +1407,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     const int ne = n_existing ? n_existing[f] : 0;
     float angle;
     {
-        wic.store<true>(P, s);
+        wic.store(P, s);
         // IC_Angle (ORBextractor.cc:77-101): lane s takes the window rows 15 +- (s+1)
         // (lane 15 the centre row).  Per row, with I the 31 row bytes (32nd
         // weighted 0): S0 = sum of I over the disc (dot4 with the 0/1 weights),
