@@ -59,6 +59,7 @@ __device__ void se3_mul(const SE3 &a, const SE3 &b, SE3 &out) {
 // se3_mul with the quaternion normalised by one rsqrt (the solver wave's
 // pose update; 1-ulp differences are inside the 1e-4 pose parity)
 __device__ __forceinline__ void se3_mul_fast(const SE3 &a, const SE3 &b, SE3 &out) {
+#pragma clang fp contract(fast)  // solver wave: fused products (rounding-level, pose parity 1e-4)
     float r[3], q[4];
     quat_rotate(a.q, b.t, r);
     const float t0 = a.t[0] + r[0], t1 = a.t[1] + r[1], t2 = a.t[2] + r[2];
@@ -116,6 +117,7 @@ __device__ void se3_exp(const float a[6], SE3 &out) {
 // sincos(theta/2), lane 1: sincos(theta), hardware sin/cos) and broadcast by
 // readlane; every lane of the calling wave must be active and pass the same argument.
 __device__ void se3_exp_wave(const float a[6], SE3 &out) {
+#pragma clang fp contract(fast)  // solver wave: fused products (rounding-level, pose parity 1e-4)
     const float eps = 1e-5f;
     const float w0 = a[3], w1 = a[4], w2 = a[5];
     const float theta_sq = w0 * w0 + w1 * w1 + w2 * w2;
@@ -166,6 +168,7 @@ __device__ __forceinline__ int hpack6(int i, int j) {
 
 template <int K>
 __device__ __forceinline__ bool ldlt6_step_nopiv(float (&A)[36]) {
+#pragma clang fp contract(fast)  // solver wave: fused products (rounding-level, pose parity 1e-4)
     float tmp[6];
 #pragma unroll
     for (int j = 0; j < K; j++) tmp[j] = A[j * 6 + j] * A[K * 6 + j];
@@ -197,6 +200,7 @@ __device__ __forceinline__ bool ldlt6_step_nopiv(float (&A)[36]) {
 // parity is 1e-4).  The zero rules are Eigen's: a zero first pivot leaves the
 // factorization, |D_i| <= FLT_MIN gives y_i = 0 (an all-zero H solves to x = 0).
 __device__ __forceinline__ void ldlt_solve6_nopiv(float r, float x[6]) {
+#pragma clang fp contract(fast)  // solver wave: fused products (rounding-level, pose parity 1e-4)
     const int ri = __float_as_int(r);
     float A[36], y[6];
 #pragma unroll
