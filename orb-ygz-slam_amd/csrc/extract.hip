@@ -645,8 +645,12 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                 y = e >> 8;
                 const uint8_t *r = sc + (y - 1) * S + (x - 1);
                 s = r[S + 1];
-                keep = s > r[0] && s > r[1] && s > r[2] && s > r[S] && s > r[S + 2] && s > r[2 * S] &&
-                       s > r[2 * S + 1] && s > r[2 * S + 2];
+                // all nine reads in flight together (a short-circuit chain here
+                // compiles to eight dependent LDS round trips)
+                const uint32_t m0 = max(max((uint32_t)r[0], (uint32_t)r[1]), (uint32_t)r[2]);
+                const uint32_t m1 = max(max((uint32_t)r[S], (uint32_t)r[S + 2]), (uint32_t)r[2 * S]);
+                const uint32_t m2 = max((uint32_t)r[2 * S + 1], (uint32_t)r[2 * S + 2]);
+                keep = (uint32_t)s > max(max(m0, m1), m2);
             }
             const uint64_t m = __ballot(keep);
             const int pos = total + popc_below(m);
