@@ -499,6 +499,9 @@ struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI 
 };
 
 // One (cell, frame) item on a wave whose ROI is already in LDS: phases A-D (+ retry).
+#if defined(__FAST_MATH__)
+#error "k_fast_cells orders ring bytes as f16 subnormals: build without fast-math (denormals kept)"
+#endif
 template <int S>
 __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, const CellDesc &cd, uint8_t *img,
                                                uint8_t *sc, uint16_t *list, uint32_t *__restrict__ out,
@@ -514,9 +517,8 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             for (int i = lane; i < (rh * S) / 16; i += 64) z[i] = zero;
             for (int i = ((rh * S) / 16) * 16 + lane; i < rh * S; i += 64) sc[i] = 0;
         }
-        // A: 4 pixels per lane, byte pairs as packed i16 (v_pk_add/sub_i16): a
-        //    negative half means "brighter than v+t" / "darker than v-t"; the
-        //    test is (T|B) & (L|R) on those sign bits for either polarity.
+        // A: 4 pixels per lane, byte pairs as packed u16 / i16 halves; the test
+        //    is (T|B) & (L|R) beyond the threshold for either polarity.
         int na = 0;
         if (iw > 0 && ih > 0) {
             const int lpr = iw <= 32 ? 8 : (iw <= 64 ? 16 : 32);  // lanes per row (4 px each)
@@ -540,16 +542,20 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                 uint32_t sg[2];
 #pragma unroll
                 for (int hlf = 0; hlf < 2; hlf++) {
+                    // bright: (T|B) & (L|R) above v+t <=> min(max(T,B), max(L,R)) - v > t;
+                    // dark:   (T|B) & (L|R) below v-t <=> v - max(min(T,B), min(L,R)) > t;
+                    // sign of t - max(both) marks the survivors (v_pk_max/min_u16, bytes < 256)
                     const uint32_t sel = hlf ? 0x0C030C01u : 0x0C020C00u;  // bytes 1,3 / 0,2 -> u16 lanes
+                    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+                    const u16x2 dT = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Tw, Tw, sel));
+                    const u16x2 dB = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Bw, Bw, sel));
+                    const u16x2 dL = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Lw, Lw, sel));
+                    const u16x2 dR = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Rw, Rw, sel));
+                    const u16x2 bv = __builtin_elementwise_min(__builtin_elementwise_max(dT, dB), __builtin_elementwise_max(dL, dR));
+                    const u16x2 dv = __builtin_elementwise_max(__builtin_elementwise_min(dT, dB), __builtin_elementwise_min(dL, dR));
                     const s16x2 v = as_s16x2(__builtin_amdgcn_perm(C, C, sel));
-                    const s16x2 hi = v + t2, lo = v - t2;
-                    const s16x2 dT = as_s16x2(__builtin_amdgcn_perm(Tw, Tw, sel));
-                    const s16x2 dB = as_s16x2(__builtin_amdgcn_perm(Bw, Bw, sel));
-                    const s16x2 dL = as_s16x2(__builtin_amdgcn_perm(Lw, Lw, sel));
-                    const s16x2 dR = as_s16x2(__builtin_amdgcn_perm(Rw, Rw, sel));
-                    const uint32_t bright = (as_u32(hi - dT) | as_u32(hi - dB)) & (as_u32(hi - dL) | as_u32(hi - dR));
-                    const uint32_t dark = (as_u32(dT - lo) | as_u32(dB - lo)) & (as_u32(dL - lo) | as_u32(dR - lo));
-                    sg[hlf] = bright | dark;
+                    const s16x2 m = __builtin_elementwise_max(__builtin_bit_cast(s16x2, bv) - v, v - __builtin_bit_cast(s16x2, dv));
+                    sg[hlf] = as_u32(t2 - m);
                 }
                 uint32_t m = ((sg[0] >> 15) & 1u) | (((sg[1] >> 15) & 1u) << 1) | (((sg[0] >> 31) & 1u) << 2) |
                              (((sg[1] >> 31) & 1u) << 3);
@@ -576,8 +582,9 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
         //     arcmax - 1, written to the score map.  Corners are compacted in place
         //     in raster order (writes never pass the read front).
         //     The min / max run on v_pk_minimum3_f16 / v_pk_maximum3_f16 over the
-        //     bit patterns e + 1280 in [1025, 1535]: normal f16 numbers (exponent
-        //     field 1) whose order is the integers' order, selected exactly.
+        //     ring bytes r as f16 bit patterns (+0 and subnormals, ordered like the
+        //     integers and selected exactly with f16 denormals kept), and
+        //     min / max commute with "- v": e.g. max_k min(e[..]) = max_k min(r[..]) - v.
         int nc = 0;
         for (int i0 = 0; i0 < na; i0 += 128) {
             const int i = i0 + 2 * lane;
@@ -589,15 +596,20 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             const uint32_t o0 = b0 + Ring<S>::kCentre, o1 = b1 + Ring<S>::kCentre;
             asm("" : "+v"(b0), "+v"(b1));  // taps off q (not off the centre): immediate offsets only
             const uint8_t *q0 = img + b0, *q1 = img + b1;
-            // v - 1280 per half, so that r - (v - 1280) = e + 1280
-            uint32_t vbu = as_u32(as_s16x2((uint32_t)q0[Ring<S>::kCentre] | ((uint32_t)q1[Ring<S>::kCentre] << 16)) -
-                                  as_s16x2(0x05000500u));
-            asm("" : "+v"(vbu));  // keep one subtraction per tap (no re-association into add + sub)
-            const s16x2 vb = as_s16x2(vbu);
+            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+            auto pair = [&](int o) {  // both survivors' bytes as the u16 halves
+                u16x2 p;
+                p.x = q0[o];
+                p.y = q1[o];
+                return __builtin_bit_cast(uint32_t, p);
+            };
+            // the ring bytes themselves as f16 bit patterns (0..255: +0 and subnormals,
+            // ordered like the integers; the kernels keep f16 denormals): min / max
+            // commute with "- v", so v is subtracted once at the end
+            const s16x2 vb = as_s16x2(pair(Ring<S>::kCentre));
             h16x2 e[16];
 #pragma unroll
-            for (int k = 0; k < 16; k++)
-                e[k] = as_h16x2(as_u32(as_s16x2((uint32_t)q0[Ring<S>::off(k)] | ((uint32_t)q1[Ring<S>::off(k)] << 16)) - vb));
+            for (int k = 0; k < 16; k++) e[k] = as_h16x2(pair(Ring<S>::off(k)));
             h16x2 w3[16];
             // bright: max_k min(e[k..k+8]) = max_k min3(w3[k], w3[k+3], w3[k+6]), w3 = min of 3
 #pragma unroll
@@ -614,9 +626,7 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             for (int k = 0; k < 16; k++) b9[k] = hmax3(w3[k], w3[(k + 3) & 15], w3[(k + 6) & 15]);
             const h16x2 darkmin = hmin3(hmin3(hmin3(b9[0], b9[1], b9[2]), hmin3(b9[3], b9[4], b9[5]), hmin3(b9[6], b9[7], b9[8])),
                                         hmin3(b9[9], b9[10], b9[11]), hmin3(hmin3(b9[12], b9[13], b9[14]), b9[15], b9[15]));
-            // back to integers: bright = pattern - 1280, dark = 1280 - pattern
-            const s16x2 bi = as_s16x2(as_u32(bright)) - as_s16x2(0x05000500u);
-            const s16x2 di = as_s16x2(0x05000500u) - as_s16x2(as_u32(darkmin));
+            const s16x2 bi = as_s16x2(as_u32(bright)) - vb, di = vb - as_s16x2(as_u32(darkmin));
             const s16x2 am = __builtin_elementwise_max(bi, di);
             const bool c0 = v0 && am.x > th, c1 = v1 && am.y > th;
             if (c0) sc[o0] = (uint8_t)(am.x - 1);
