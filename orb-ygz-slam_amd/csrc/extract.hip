@@ -165,7 +165,10 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 // columns (x < 4) and the last three (whose taps reach past the row) come out
 // wrong; they are not stored by the main loop and are recomputed with
 // BORDER_REFLECT_101 taps at the end.
-constexpr int kBlurAhead = 6;
+#ifndef YGZ_BLUR_AHEAD
+#define YGZ_BLUR_AHEAD 10  // rows in flight per wave
+#endif
+constexpr int kBlurAhead = YGZ_BLUR_AHEAD;
 
 __device__ __forceinline__ void blur_hsum(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t o,
                                           uint32_t ka, uint32_t kb, uint32_t h[4]) {
@@ -311,7 +314,18 @@ __device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ s
     }
 }
 
-__global__ __launch_bounds__(256) void k_blur7(const uint8_t *__restrict__ pyr,
+// 7 waves / SIMD (68 VGPRs, no spills; uncapped it took 74 and 6 waves) and 10
+// rows ahead: the strips are load-latency bound (0-3 % faster than 6 / 6 on two
+// boxes; 8 waves spill)
+#ifndef YGZ_BLUR_EU
+#define YGZ_BLUR_EU 7
+#endif
+#if YGZ_BLUR_EU > 0
+#define YGZ_BLUR_ATTR __attribute__((amdgpu_waves_per_eu(YGZ_BLUR_EU)))
+#else
+#define YGZ_BLUR_ATTR
+#endif
+__global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(const uint8_t *__restrict__ pyr,
                                                uint8_t *__restrict__ blur, uint32_t pitch,
                                                const Plan *__restrict__ plan) {
     const int f = blockIdx.y;
