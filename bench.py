@@ -211,7 +211,9 @@ def main():
     side = torch.cuda.Stream(dev)  # Hamming (descriptors only) runs beside SparseImgAlign (pyramids + kps)
 
     def pack_and_gather(timed_gather=False):
-        batch.pack_slots(h, n_own, out.data_ptr() if P > 0 else 0, b0, slots.data_ptr(), S_b, sptr)
+        # no align record when align did not run (P == 0 or --no-align): has_align stays 0
+        batch.pack_slots(h, n_own, out.data_ptr() if (P > 0 and not args.no_align) else 0, b0, slots.data_ptr(), S_b,
+                         sptr)
         if world > 1:
             if timed_gather:
                 e0_, e1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -379,7 +381,7 @@ def main():
     n_host = 0
     if rank == 0 and world == 1:
         n_host = min(F, max(args.cpu_sample, args.latency_frames + 12, 16,
-                            24 * min(16, host_cpu_info()[2]) if args.cpu_sample > 0 else 0))
+                            24 * cpu_threads() if args.cpu_sample > 0 else 0))
     frames = np.stack([batch.read_level(i, 0) for i in range(n_host)]) if n_host else None
 
     # ------------------------------------------------ §8(f) rank 1: undistort remap
@@ -511,10 +513,15 @@ def plane_xyz(S, pose, kps, cam):
 def latency_leg(frames, poses, sc, S, n_timed, warm=10):
     """Single-frame latency, the reference's execution model (one Tracking thread,
     SURVEY.md §8d): per frame, host image -> ComputePyramid -> ORB extract ->
-    keypoints + descriptors back on the host -> SparseImgAlign(prev -> cur) ->
-    pose on the host, through the host C ABI (pageable host buffers, H2D and D2H
-    included).  Map points of the previous frame (T_ref * P_w) are formed on
-    the host between frames, outside the timed region, as Tracking does."""
+    keypoints + descriptors back on the host, and SparseImgAlign(prev -> cur) ->
+    pose on the host, through the host C ABI (H2D and D2H included).  Both need
+    only the frame's pyramid (the reference runs TrackWithSparseAlignment before
+    any extraction, Tracking.cc:471 / 2145-2189), so the align is queued first
+    (ygzfe_sparse_align_begin) and runs on its own stream beside the extraction;
+    the frame is done when both results are on the host.  The same frames are
+    also timed with the two calls back to back (`serial`).  Map points of the
+    previous frame (T_ref * P_w) are formed on the host between frames, outside
+    the timed region, as Tracking does."""
     import ctypes as C
     import ygzfe
     L = ygzfe.lib()
@@ -530,33 +537,47 @@ def latency_leg(frames, poses, sc, S, n_timed, warm=10):
     res = ygzfe.AlignResult()
     p = ygzfe._p
     n_frames = min(len(frames), warm + n_timed + 1)
-    ts, te = [], []
-    prev = None
-    for i in range(n_frames):
-        cur = i & 1
-        img = np.ascontiguousarray(frames[i])
-        t0 = time.perf_counter()
-        ygzfe._check(L.ygzfe_compute_pyramid(ex.h, fr[cur].h, p(img), W), "compute_pyramid")
-        ygzfe._check(L.ygzfe_extract(ex.h, fr[cur].h, ygzfe.ORBSLAM_KEYPOINT, p(kps[cur]), 0, cap, p(desc[cur]),
-                                     C.byref(n_out)), "extract")
-        t1 = time.perf_counter()
-        if prev is not None:
-            pk, xyz, us = prev
-            ygzfe._check(L.ygzfe_sparse_align(fr[cur ^ 1].h, fr[cur].h, C.byref(cam), p(pk), p(xyz), p(us), len(pk),
-                                              3, 1, C.byref(T0), C.byref(res)), "sparse_align")
-        t2 = time.perf_counter()
-        if i > warm:
-            ts.append(t2 - t0)
-            te.append(t1 - t0)
-        pk = kps[cur][:n_out.value].copy()
-        prev = (pk, plane_xyz(S, poses[i], pk, sc.cam), np.ones(len(pk), np.uint8))
-    ts = np.array(ts) * 1e3
-    te = np.array(te) * 1e3
+    out = {}
+    for mode in ("overlap", "serial"):
+        ts, te = [], []
+        prev = None
+        for i in range(n_frames):
+            cur = i & 1
+            img = np.ascontiguousarray(frames[i])
+            t0 = time.perf_counter()
+            ygzfe._check(L.ygzfe_compute_pyramid(ex.h, fr[cur].h, p(img), W), "compute_pyramid")
+            if prev is not None and mode == "overlap":
+                pk, xyz, us = prev
+                ygzfe._check(L.ygzfe_sparse_align_begin(fr[cur ^ 1].h, fr[cur].h, C.byref(cam), p(pk), p(xyz), p(us),
+                                                        len(pk), 3, 1, C.byref(T0)), "sparse_align_begin")
+            ygzfe._check(L.ygzfe_extract(ex.h, fr[cur].h, ygzfe.ORBSLAM_KEYPOINT, p(kps[cur]), 0, cap, p(desc[cur]),
+                                         C.byref(n_out)), "extract")
+            t1 = time.perf_counter()
+            if prev is not None:
+                if mode == "overlap":
+                    ygzfe._check(L.ygzfe_sparse_align_end(fr[cur].h, C.byref(res)), "sparse_align_end")
+                else:
+                    pk, xyz, us = prev
+                    ygzfe._check(L.ygzfe_sparse_align(fr[cur ^ 1].h, fr[cur].h, C.byref(cam), p(pk), p(xyz), p(us),
+                                                      len(pk), 3, 1, C.byref(T0), C.byref(res)), "sparse_align")
+            t2 = time.perf_counter()
+            if i > warm:
+                ts.append(t2 - t0)
+                te.append(t1 - t0)
+            pk = kps[cur][:n_out.value].copy()
+            prev = (pk, plane_xyz(S, poses[i], pk, sc.cam), np.ones(len(pk), np.uint8))
+        out[mode] = (np.array(ts) * 1e3, np.array(te) * 1e3)
+    ts, te = out["overlap"]
+    ss, se = out["serial"]
     return {"frames": len(ts), "median_ms": round(float(np.median(ts)), 4), "p90_ms": round(float(np.percentile(ts, 90)), 4),
             "median_extract_ms": round(float(np.median(te)), 4),
-            "median_align_ms": round(float(np.median(ts - te)), 4),
-            "path": "host C ABI, one frame at a time: H2D 752x480 u8 -> pyramid -> extract -> D2H kps+desc -> "
-                    "SparseImgAlign 3..1 (prev -> cur) -> D2H pose; median over frames after 10 warm-up frames"}
+            "median_align_wait_ms": round(float(np.median(ts - te)), 4),
+            "serial": {"median_ms": round(float(np.median(ss)), 4),
+                       "median_extract_ms": round(float(np.median(se)), 4),
+                       "median_align_ms": round(float(np.median(ss - se)), 4)},
+            "path": "host C ABI, one frame at a time: H2D 752x480 u8 -> pyramid -> [SparseImgAlign 3..1 (prev -> cur) "
+                    "on its own stream | extract] -> D2H kps+desc and pose; median over frames after 10 warm-up "
+                    "frames ('serial': the same calls back to back)"}
 
 
 TUM1_CAM = (517.306408, 516.469215, 318.643040, 255.313989)  # Examples/RGB-D/TUM1.yaml Camera.fx/fy/cx/cy
@@ -790,20 +811,36 @@ def host_cpu_info():
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = os.cpu_count() or 1
-    return model, os.cpu_count() or 1, aff
+    # the cgroup's CPU bandwidth limit (cgroup v2 cpu.max "quota period"), if any: more
+    # threads than that only time-slice the same CPUs
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return model, os.cpu_count() or 1, aff, quota
+
+
+def cpu_threads():
+    """Threads for the CPU throughput leg: every CPU of this process's affinity (nproc),
+    capped by the cgroup CPU quota when one is set."""
+    _, _, aff, quota = host_cpu_info()
+    return max(1, min(aff, quota) if quota else aff)
 
 
 def cpu_baseline(frames, r3, cz, S, args, sc):
     """oracle/ restatement driven from C (oracle/bench.c, no per-stage Python hops):
     pyramid + ORB (C2) + Hamming vs the previous frame + SparseImgAlign 3..1 per frame.
     1 thread over the sample (the reference's single Tracking thread: per-frame latency),
-    then T threads (min(16, this process's CPUs): the box's CPU share) over the same frames
-    split in contiguous chunks (throughput).  Plus the FAST sanity check of SURVEY.md §8d:
+    then T threads (every CPU of this process's affinity, capped by a cgroup CPU quota if
+    one is set) over the same frames split in contiguous chunks (throughput).  Plus the FAST sanity check of SURVEY.md §8d:
     the restated cv::FAST vs the reference's own SSE2 FAST-10 (oracle/_ref) on test1.png."""
     import _oracle as O
     cfg = S.CONFIGS["C2"]
-    model, ncpu, aff = host_cpu_info()
-    threads = max(1, min(16, aff))
+    model, ncpu, aff, quota = host_cpu_info()
+    threads = cpu_threads()
     n1 = min(args.cpu_sample, len(frames))
     wall1, st1 = O.bench_pipeline(frames[:n1], sc.cam, S.PLANE_Z, r3[:n1], cz[:n1], cfg, 1)
     per = 1e3 / max(1, st1.frames)
@@ -816,34 +853,41 @@ def cpu_baseline(frames, r3, cz, S, args, sc):
     line = {"value": round(stt.frames / wallt, 2), "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"{nmt} frames of the same rendered C2 sequence on {threads} threads (contiguous chunks; "
                       f"{n1} frames on 1 thread for the latency): pyramid + octree ORB + rBRIEF + Hamming vs previous "
-                      f"frame + SparseImgAlign 3..1, oracle/ (gcc -O3 -march=native, scalar)",
-            "cpu_model": model, "host_cpus": ncpu, "process_cpus": aff,
+                      f"frame + SparseImgAlign 3..1, oracle/ (gcc -O3 -march=native; FAST-9 segment test, blur and resize on vectors like OpenCV's SIMD paths, the reference's own code scalar as in the reference)",
+            "cpu_model": model, "host_cpus": ncpu, "process_cpus": aff, "cgroup_cpu_quota": quota,
             "single_thread_frames_per_s": round(st1.frames / wall1, 2),
             "ms_per_frame": round(wall1 * 1e3 / max(1, st1.frames), 3),
             "ms_pyramid": round(st1.t_pyr * per, 3), "ms_extract": round(st1.t_extract * per, 3),
             "ms_hamming": round(st1.t_hamming * perp, 3), "ms_align": round(st1.t_align * perp, 3),
             "threads_frames_per_s": round(stt.frames / wallt, 2)}
-    # FAST sanity (SSE2 FAST-10 0.130 / 0.433 ms on test1.png at threshold 75 / 20)
+    # FAST sanity (the CPU FAST stage must be no slower than the reference's
+    # SSE2 FAST-10).  Like for like: the same FAST-10 pipeline -- detect (SSE2 variant) +
+    # fast_corner_score_10 + fast_nonmax_3x3 -- restated (oracle, 16-pixel vectors) and the
+    # reference's own (oracle/_ref), both timed in C over the same ROI of test1.png, same
+    # survivors.  The restated cv::FAST-9 (+ cornerScore + NMS) of the C2 path is listed too.
     try:
         from PIL import Image
         img = np.array(Image.open(os.path.join(ROOT, "tests", "golden", "test1.png")))
         H, W = img.shape
         fs = {}
         for th in (75, 20):
+            O.bench_fast10(img, th, 3, 3, W - 6, H - 6, reps=5)
+            n10, t10 = O.bench_fast10(img, th, 3, 3, W - 6, H - 6, reps=100)
+            fs[f"oracle_fast10_th{th}_ms"] = round(t10 * 1e3, 4)
+            fs[f"oracle_fast10_th{th}_kept"] = int(n10)
+            if O.RefFast.available():
+                ref = O.RefFast()
+                ref.pipeline_bench(img, th, 3, 3, W - 6, H - 6, reps=5)
+                nr, tr = ref.pipeline_bench(img, th, 3, 3, W - 6, H - 6, reps=100)
+                fs[f"ref_fast10_th{th}_ms"] = round(tr * 1e3, 4)
+                fs[f"ref_fast10_th{th}_kept"] = int(nr)
+                fs[f"oracle_no_slower_th{th}"] = bool(t10 <= tr * 1.05)
             n9, t9 = O.bench_fast9(img, th, reps=20)
             fs[f"oracle_fast9_th{th}_ms"] = round(t9 * 1e3, 4)
             fs[f"oracle_fast9_th{th}_corners"] = n9
-            if O.RefFast.available():
-                ref = O.RefFast()
-                for _ in range(3):
-                    ref.detect(img, th, sse=True, x0=3, y0=3, w=W - 6, h=H - 6)
-                t0 = time.perf_counter()
-                for _ in range(20):
-                    xs, _ = ref.detect(img, th, sse=True, x0=3, y0=3, w=W - 6, h=H - 6)
-                fs[f"ref_fast10_sse2_th{th}_ms"] = round((time.perf_counter() - t0) / 20 * 1e3, 4)
-                fs[f"ref_fast10_sse2_th{th}_corners"] = int(len(xs))
-        fs["note"] = ("oracle = cv::FAST TYPE_9_16 + cornerScore + 3x3 NMS restated (segment test and score on 16-pixel int16 vectors, as OpenCV's SIMD FAST_t); "
-                      "ref = the reference's own Thirdparty/fast SSE2 FAST-10 detect (oracle/_ref), detect only")
+        fs["note"] = ("fast10: detect_sse2 + score + nonmax_3x3 on test1.png's interior, restated (oracle) vs the "
+                      "reference's own Thirdparty/fast (oracle/_ref), 1 thread, mean of 100; fast9: the restated "
+                      "cv::FAST TYPE_9_16 + cornerScore + NMS of the C2 path (a different detector, for reference)")
         line["fast_sanity"] = fs
     except Exception as e:  # test image / reference library absent
         line["fast_sanity"] = {"skipped": str(e)}

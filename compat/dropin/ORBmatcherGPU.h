@@ -30,7 +30,10 @@ namespace gpu {
 
 constexpr int kTH_HIGH = 100, kTH_LOW = 50;  // ORBmatcher.cc:36-37
 
-// a per-thread device view of one Frame / KeyFrame (mvKeys, mDescriptors, mvuRight)
+// a per-thread device view of one Frame / KeyFrame (mvKeys, mDescriptors, mvuRight).
+// Tracking searches one CurrentFrame several times (motion model, then the local
+// map, ...): a view whose rows, descriptors, mvuRight and bounds are byte-equal to
+// the last upload is reused without a new upload or grid build.
 class MatchView {
 public:
     explicit MatchView(int slot) {
@@ -40,14 +43,41 @@ public:
     ~MatchView() { ygzfe_match_frame_destroy(h_); }
     template <class KeyVec, class DescMat>
     bool set(const KeyVec &keys, const DescMat &desc, int n, const float *u_right, const ygzfe_bounds &b) {
-        if (!h_) return false;
+        if (!h_) {
+            dropin::log_once("ORBmatcher search", "no device match frame (ygzfe_match_frame_create failed)");
+            return false;
+        }
         const std::vector<uint8_t> d = dropin::desc_rows(desc, n);
-        return ygzfe_match_frame_set(h_, dropin::as_kp(keys.data()), d.data(), n, u_right, &b) == YGZFE_OK;
+        const ygzfe_kp *k = dropin::as_kp(keys.data());
+        const size_t kb = sizeof(ygzfe_kp) * (size_t)n;
+        if (valid_ && n == n_ && (u_right != nullptr) == has_ur_ && std::memcmp(&b, &b_, sizeof(b)) == 0 &&
+            std::memcmp(k, kps_.data(), kb) == 0 && d == desc_ &&
+            (!u_right || std::memcmp(u_right, ur_.data(), 4 * (size_t)n) == 0))
+            return true;
+        valid_ = false;
+        if (ygzfe_match_frame_set(h_, k, d.data(), n, u_right, &b) != YGZFE_OK) {
+            dropin::log_once("ORBmatcher search", ygzfe_last_error());
+            return false;
+        }
+        n_ = n;
+        b_ = b;
+        has_ur_ = u_right != nullptr;
+        kps_.assign(k, k + n);
+        desc_ = d;
+        ur_.assign(u_right ? u_right : nullptr, u_right ? u_right + n : nullptr);
+        valid_ = true;
+        return true;
     }
     ygzfe_match_frame *get() const { return h_; }
 
 private:
     ygzfe_match_frame *h_ = nullptr;
+    bool valid_ = false, has_ur_ = false;
+    int n_ = 0;
+    ygzfe_bounds b_{};
+    std::vector<ygzfe_kp> kps_;
+    std::vector<uint8_t> desc_;
+    std::vector<float> ur_;
 };
 
 inline MatchView &view(int slot) {
@@ -79,6 +109,11 @@ inline void append_desc(std::vector<uint8_t> &out, const Mat &d) {
     const size_t o = out.size();
     out.resize(o + 32);
     std::memcpy(&out[o], d.data, 32);
+}
+
+inline int failed(const char *where) {
+    dropin::log_once(where, ygzfe_last_error());
+    return 0;
 }
 
 // ORBmatcher::RadiusByViewingCos (ORBmatcher.cc:128-133)
@@ -123,7 +158,7 @@ int SearchByProjection(FrameT &F, const std::vector<MapPointT *> &vpMapPoints, c
     int nmatches = 0;
     if (ygzfe_search_projection_ratio(v.get(), q.data(), qd.data(), (int)q.size(), blocked.data(), nnratio, out.data(),
                                       &nmatches) != YGZFE_OK)
-        return 0;
+        return failed("SearchByProjection(F, vpMapPoints)");
     for (int i = 0; i < F.N; i++)
         if (out[i] >= 0) F.mvpMapPoints[i] = vpMapPoints[out[i]];
     return nmatches;
@@ -193,7 +228,7 @@ int SearchByProjection(FrameT &CurrentFrame, const FrameT &LastFrame, const floa
     int nmatches = 0;
     if (ygzfe_search_projection_best(mv.get(), q.data(), qd.data(), (int)q.size(), blocked.data(), kTH_HIGH,
                                      checkOri ? 1 : 0, out.data(), &nmatches) != YGZFE_OK)
-        return 0;
+        return failed("SearchByProjection(CurrentFrame, LastFrame)");
     for (int i2 = 0; i2 < CurrentFrame.N; i2++) {
         if (out[i2] >= 0) CurrentFrame.mvpMapPoints[i2] = LastFrame.mvpMapPoints[src[out[i2]]];
         else if (out[i2] == -2) CurrentFrame.mvpMapPoints[i2] = nullptr;
@@ -251,7 +286,7 @@ int SearchByProjection(FrameT &CurrentFrame, KeyFrameT *pKF, const std::set<MapP
     int nmatches = 0;
     if (ygzfe_search_projection_best(mv.get(), q.data(), qd.data(), (int)q.size(), blocked.data(), ORBdist,
                                      checkOri ? 1 : 0, out.data(), &nmatches) != YGZFE_OK)
-        return 0;
+        return failed("SearchByProjection(CurrentFrame, pKF, sAlreadyFound)");
     for (int i2 = 0; i2 < CurrentFrame.N; i2++) {
         if (out[i2] >= 0) CurrentFrame.mvpMapPoints[i2] = vpMPs[src[out[i2]]];
         else if (out[i2] == -2) CurrentFrame.mvpMapPoints[i2] = nullptr;
@@ -276,8 +311,10 @@ int SearchForInitialization(FrameT &F1, FrameT &F2, std::vector<Point2fT> &vbPre
     }
     int nmatches = 0;
     if (ygzfe_search_for_initialization(a.get(), b.get(), prev.data(), windowSize, nnratio, checkOri ? 1 : 0,
-                                        vnMatches12.data(), &nmatches) != YGZFE_OK)
-        return 0;
+                                        vnMatches12.data(), &nmatches) != YGZFE_OK) {
+        vnMatches12.assign(n1, -1);
+        return failed("SearchForInitialization");
+    }
     for (int i = 0; i < n1; i++)
         if (vnMatches12[i] >= 0) vbPrevMatched[i] = F2.mvKeys[vnMatches12[i]].pt;
     return nmatches;
@@ -315,7 +352,7 @@ int SearchByBoW(KeyFrameT *pKF, FrameT &F, std::vector<MapPointT *> &vpMapPointM
     if (ygzfe_search_by_bow(a.get(), b.get(), usable.data(), (int)kn.size(), kn.data(), kp.data(), kfe.data(),
                             (int)fn.size(), fn.data(), fp.data(), ffe.data(), nnratio, checkOri ? 1 : 0, out.data(),
                             &nmatches) != YGZFE_OK)
-        return 0;
+        return failed("SearchByBoW");
     for (int i = 0; i < F.N; i++)
         if (out[i] >= 0) vpMapPointMatches[i] = vpMapPointsKF[out[i]];
     return nmatches;

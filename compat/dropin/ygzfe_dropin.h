@@ -21,11 +21,14 @@
 #define YGZFE_DROPIN_H_
 
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <iterator>
 #include <list>
 #include <mutex>
+#include <set>
+#include <string>
 #include <vector>
 
 #include "ygzfe.h"
@@ -41,6 +44,17 @@ inline int device() {
 // The reference never throws: failures become empty results;
 // the last message is kept for the caller's logging.
 inline const char *last_error() { return ygzfe_last_error(); }
+
+// A failed call keeps the reference's empty-result convention, but says why on
+// stderr once per (call site, message): Tracking would otherwise go LOST silently.
+inline void log_once(const char *where, const char *why) {
+    static std::mutex mu;
+    static std::set<std::string> seen;
+    std::lock_guard<std::mutex> lk(mu);
+    std::string key = std::string(where) + ": " + (why ? why : "");
+    if (seen.size() > 256 || !seen.insert(key).second) return;
+    std::fprintf(stderr, "[ygzfe] %s failed: %s (returning the reference's empty result)\n", where, why ? why : "");
+}
 
 class PyramidPool {
 public:
@@ -65,15 +79,24 @@ public:
     }
 
     // The device copy of a host pyramid (levels[l]: .data / .cols / .rows / .step).
+    // An entry whose level 0 last came from the same host pointer is checked
+    // first (a KeyFrame shares its Frame's pyramid, KeyFrame.cc:257-260, so a
+    // keyframe is found on its first entry); every hit is confirmed by a full
+    // compare of level 0, so a reused host buffer never returns a stale pyramid.
     template <class MatVec>
     ygzfe_frame *find_or_upload(const MatVec &levels) {
         if (levels.empty()) return nullptr;
         const int w = levels[0].cols, h = levels[0].rows;
+        const uint8_t *key = levels[0].data;
         std::lock_guard<std::mutex> lk(mu_);
-        for (auto it = lru_.begin(); it != lru_.end(); ++it)
-            if (it->w == w && it->h == h && it->nlevels == (int)levels.size() && same_level0(*it, levels[0])) {
-                lru_.splice(lru_.begin(), lru_, it);
-                return lru_.front().f;
+        for (int pass = 0; pass < 2; pass++)
+            for (auto it = lru_.begin(); it != lru_.end(); ++it) {
+                if ((pass == 0) != (it->host_ptr == key)) continue;
+                if (it->w == w && it->h == h && it->nlevels == (int)levels.size() && same_level0(*it, levels[0])) {
+                    it->host_ptr = key;
+                    lru_.splice(lru_.begin(), lru_, it);
+                    return lru_.front().f;
+                }
             }
         if (!ex_) return nullptr;  // no extractor yet: nothing defines the level geometry
         Entry &e = slot(ex_, (int)levels.size(), w, h);
@@ -83,8 +106,12 @@ public:
         e.level0.resize((size_t)w * h);
         for (int y = 0; y < h; y++)
             std::memcpy(&e.level0[(size_t)y * w], levels[0].data + (size_t)y * levels[0].step[0], (size_t)w);
+        e.host_ptr = key;
         return e.f;
     }
+
+    // pyramids a caller may hold at once (a newer lookup can recycle an older entry)
+    static int capacity() { return kCapacity; }
 
     // the extractor whose level geometry uploads use (the latest one constructed)
     void set_extractor(ygzfe_extractor *ex, int nlevels) {
@@ -105,11 +132,15 @@ public:
     }
 
 private:
-    static constexpr int kCapacity = 6;
+    // a local map's keyframes (SearchLocalPointsDirect: <= 5 per map point, the
+    // local keyframe set is capped at 80, Tracking.cc UpdateLocalKeyFrames) plus the
+    // frames in flight: 96 pyramids of 752 x 480 are ~46 MB of HBM
+    static constexpr int kCapacity = 96;
     struct Entry {
         ygzfe_extractor *ex = nullptr;
         ygzfe_frame *f = nullptr;
         int w = 0, h = 0, nlevels = 0;
+        const uint8_t *host_ptr = nullptr;  // the host level 0 this content was last seen at
         std::vector<uint8_t> level0;
     };
     template <class Mat>
@@ -136,6 +167,7 @@ private:
         e.w = w;
         e.h = h;
         e.nlevels = nlevels;
+        e.host_ptr = nullptr;
         e.level0.clear();
         return e;
     }

@@ -301,6 +301,19 @@ int ygzfe_sparse_align(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygz
                        const ygzfe_kp *kps, const float *xyz_ref, const uint8_t *usable, int n,
                        int max_level, int min_level, const ygzfe_se3 *T_init,
                        ygzfe_align_result *result);
+/* The same split in two, so the alignment of a frame overlaps its own
+ * extraction: both need only the frame's pyramid (the reference runs
+ * TrackWithSparseAlignment before any extraction, Tracking.cc:471, 2145-2189).
+ * _begin stages the inputs and queues the alignment on the extractor's align
+ * stream, ordered after the work already queued on the extractor (the
+ * pyramids), and returns at once; ygzfe_extract / ygzfe_compute_pyramid may be
+ * called meanwhile (a later pyramid rewrite waits for the alignment); _end
+ * waits and writes the result.  One alignment in flight per extractor
+ * (YGZFE_ESTATE otherwise). */
+int ygzfe_sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam,
+                             const ygzfe_kp *kps, const float *xyz_ref, const uint8_t *usable, int n,
+                             int max_level, int min_level, const ygzfe_se3 *T_init);
+int ygzfe_sparse_align_end(const ygzfe_frame *cur, ygzfe_align_result *result);
 
 /* Batched: pair p aligns frame ref_idx[p] -> cur_idx[p] of a batch, with the
  * ref frame's batch keypoints (level-0 px); d_xyz_ref [n_pairs][kp_cap][3] and
@@ -348,6 +361,36 @@ int ygzfe_search_direct_batch(const ygzfe_frame *const *ref, int n_ref, const yg
                               const int32_t *ref_index, const ygzfe_kp *kp_ref, const float *pt_ref,
                               const ygzfe_se3 *T_cr, const float *px_proj, float border, float *px_out,
                               int32_t *matched_item);
+
+/* The whole of Tracking::SearchLocalPointsDirect (Tracking.cc:2258-2410) in one
+ * call, with its sequential rules.  Points [0, n_cache) are the
+ * mvpDirectMapPointsCache members in the cache's iteration order that are not
+ * bad and pass isInFrustum (Tracking.cc:2269-2275; the caller erases the
+ * others); points [n_cache, n_cache + n_local) are mvpLocalMapPoints that are
+ * not in the cache, not bad and in the frustum (:2348-2361).  Items, px_proj and
+ * border as ygzfe_search_direct_batch.
+ *  - cache phase: a point whose projection cell (int(mTrackProjX / grid_size),
+ *    int(mTrackProjY / grid_size)) of the coverage grid (grid_size = 5, rows /
+ *    grid_size x cols / grid_size cells of level 0) is already marked is skipped
+ *    (status GRID_SKIP, it stays in the cache, :2277-2284); a success marks the
+ *    cell of its pixel (:2320-2323); a failure leaves the cache (status FAILED).
+ *  - if the cache phase had more than cache_hit_th (mnCacheHitTh) successes the
+ *    local points are not searched (status NOT_RUN, *local_ran = 0, :2334-2340);
+ *    otherwise each is searched without the grid (MATCHED / FAILED).
+ * Successes are the rows Tracking appends to mvKeys / mvpMapPoints / mvMatchedFrom
+ * in point order.  status may be NULL; *cache_success, *local_ran may be NULL.
+ * Cells outside the grid (the reference indexes past its vector<bool>) count as
+ * free and are never marked. */
+#define YGZFE_DIRECT_FAILED 0
+#define YGZFE_DIRECT_MATCHED 1
+#define YGZFE_DIRECT_GRID_SKIP 2
+#define YGZFE_DIRECT_NOT_RUN 3
+int ygzfe_search_local_points_direct(const ygzfe_frame *const *ref, int n_ref, const ygzfe_frame *cur,
+                                     const ygzfe_camera *cam, int n_cache, int n_local, const int32_t *item_ptr,
+                                     const int32_t *ref_index, const ygzfe_kp *kp_ref, const float *pt_ref,
+                                     const ygzfe_se3 *T_cr, const float *px_proj, float border, int grid_size,
+                                     int cache_hit_th, float *px_out, int32_t *matched_item, int32_t *status,
+                                     int *cache_success, int *local_ran);
 
 /* ------------------------------------------------------------------------ */
 /* Stereo (Frame.cc:509-700)                                                 */

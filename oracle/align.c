@@ -491,3 +491,86 @@ void ygzo_search_direct(const ygzo_cam *cam, uint8_t **ref_levels, uint8_t **cur
         matched[i] = m;
     }
 }
+
+/* The whole of Tracking::SearchLocalPointsDirect (Tracking.cc:2258-2410) over
+ * the points the caller's own filters let through, in the reference's loop order:
+ *
+ *  - points [0, n_cache): mvpDirectMapPointsCache members that are not bad and
+ *    pass isInFrustum (Tracking.cc:2269-2275; the caller erases the others).  A
+ *    point whose projection cell (int(mTrackProjX / grid_size),
+ *    int(mTrackProjY / grid_size)) of the 5-px coverage grid is already taken is
+ *    skipped and stays in the cache (:2277-2284); otherwise its observations are
+ *    tried in SelectNearestKeyframe order, the first converged in-border result
+ *    is taken (:2286-2303) and the cell of px_ave is marked (:2320-2323); a point
+ *    with no result leaves the cache (:2327-2330).
+ *  - if the cache gave more than cache_hit_th successes (mnCacheHitTh,
+ *    :2334-2340) the local-map points are not searched (status NOT_RUN);
+ *    otherwise points [n_cache, n_cache + n_local): mvpLocalMapPoints that are not
+ *    in the cache, not bad and in the frustum (:2348-2361), each tried like a
+ *    cache point but without the grid (:2363-2405).
+ *
+ * Grid: grid_rows = rows / grid_size, grid_cols = cols / grid_size of level 0,
+ * cell k = gy * grid_cols + gx (:2261-2264, 2277-2279).  A projection on the
+ * last partial column aliases into the next row's first cell, as in the
+ * reference; an index outside [0, grid_rows * grid_cols) (the reference reads
+ * past the vector<bool>) counts as a free cell and is never written.
+ *
+ * status[i]: 1 matched, 0 no match (cache: erased; local: rejected), 2 grid
+ * skip (cache only), 3 not run.  Returns the cache-phase success count;
+ * *local_ran = whether the local-map phase ran. */
+int ygzo_search_local_points_direct(const ygzo_cam *cam, uint8_t **ref_levels, uint8_t **cur_levels, const int *lw,
+                                    const int *lh, int nlevels, const float *scale, const float *inv_scale,
+                                    float inv_level_sigma2_1, int n_cache, int n_local, const int *item_ptr,
+                                    const int *ref_index, const ygzo_kp *kps, const float *pt_ref,
+                                    const ygzo_se3 *T_cr, const float *px_proj, float border, int grid_size,
+                                    int cache_hit_th, float *px_out, int *matched, int *status, int *local_ran) {
+    const int cols = lw[0], rows = lh[0];
+    const int grid_rows = rows / grid_size, grid_cols = cols / grid_size;
+    const long ncell = (long)grid_rows * grid_cols;
+    uint8_t *grid = (uint8_t *)calloc(ncell > 0 ? (size_t)ncell : 1, 1);
+    int cnt_success = 0;
+    for (int i = 0; i < n_cache + n_local; i++) {
+        const int in_cache = i < n_cache;
+        px_out[2 * i] = px_out[2 * i + 1] = 0.f;
+        matched[i] = -1;
+        if (i == n_cache) {
+            *local_ran = !(cnt_success > cache_hit_th);
+        }
+        if (!in_cache && !*local_ran) { status[i] = 3; continue; }
+        if (in_cache) {
+            const int gx = (int)(px_proj[2 * i] / grid_size), gy = (int)(px_proj[2 * i + 1] / grid_size);
+            const long k = (long)gy * grid_cols + gx;
+            if (k >= 0 && k < ncell && grid[k]) { status[i] = 2; continue; }
+        }
+        int m = -1;
+        float ave[2] = {0.f, 0.f};
+        for (int it = item_ptr[i]; it < item_ptr[i + 1]; it++) {
+            float px[2] = {px_proj[2 * i], px_proj[2 * i + 1]};
+            int sl;
+            if (ygzo_find_direct_projection(cam, ref_levels + (size_t)ref_index[it] * nlevels, lw, lh, cur_levels, lw,
+                                            lh, nlevels, scale, inv_scale, inv_level_sigma2_1, &T_cr[it],
+                                            pt_ref + 3 * (size_t)it, &kps[it], px, &sl)) {
+                if (px[0] < border || px[1] < border || px[0] >= cols - border || px[1] >= rows - border)
+                    continue;
+                m = it;
+                ave[0] = px[0] / 1.0f;
+                ave[1] = px[1] / 1.0f;
+                break;
+            }
+        }
+        if (m < 0) { status[i] = 0; continue; }
+        status[i] = 1;
+        matched[i] = m;
+        px_out[2 * i] = ave[0];
+        px_out[2 * i + 1] = ave[1];
+        if (in_cache) {
+            const int gx = (int)(ave[0] / grid_size), gy = (int)(ave[1] / grid_size);
+            const long k = (long)gy * grid_cols + gx;
+            if (k >= 0 && k < ncell) grid[k] = 1;
+            cnt_success++;
+        }
+    }
+    if (n_local == 0) *local_ran = !(cnt_success > cache_hit_th);
+    free(grid);
+    return cnt_success;
+}

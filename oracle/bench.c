@@ -154,3 +154,21 @@ int ygzo_bench_fast9(const uint8_t *img, int w, int h, int threshold, int reps, 
     free(sc);
     return n;
 }
+
+/* FAST-10 sanity: the restated Thirdparty/fast pipeline
+ * (detect_sse2 + score + 3x3 NMS, ygzo_fast10_detect_score_nms) over one ROI,
+ * `reps` times; returns the kept-corner count, *seconds = mean per pipeline. */
+int ygzo_bench_fast10(const uint8_t *img, int w, int h, int stride, int barrier, int reps, double *seconds) {
+    const size_t cap = (size_t)w * h / 2 + 16;
+    int16_t *xs = (int16_t *)malloc(sizeof(int16_t) * cap);
+    int16_t *ys = (int16_t *)malloc(sizeof(int16_t) * cap);
+    int *sc = (int *)malloc(sizeof(int) * cap);
+    int n = 0;
+    const double t0 = now_s();
+    for (int r = 0; r < reps; r++) n = ygzo_fast10_detect_score_nms(img, w, h, stride, barrier, xs, ys, sc, (int)cap);
+    *seconds = (now_s() - t0) / (reps > 0 ? reps : 1);
+    free(xs);
+    free(ys);
+    free(sc);
+    return n;
+}

@@ -17,6 +17,9 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#if defined(__AVX2__)
+#include <immintrin.h>
+#endif
 
 /* fast_10.cpp:18-35 ring order */
 static const int kRing[16][2] = {{0, 3},  {1, 3},  {2, 2},   {3, 1},   {3, 0},   {3, -1},
@@ -77,17 +80,220 @@ int ygzo_fast10_detect_plain(const uint8_t *img, int w, int h, int stride, int b
     return n;
 }
 
+/* The segment test on 16 consecutive pixels at once (GCC vector extensions,
+ * int16 lanes: AVX2 / AVX-512 under -march=native), as the reference's own SSE2
+ * detector works on 16 pixels per step (faster_corner_10_sse.cpp:24-183): the
+ * compass points 0/4/8/12 screen the block (a 10-arc covers at least two
+ * neighbouring compass points, so a pixel with no two of them beyond the
+ * barrier on one side is no corner), then with e_k = ring_k - v the largest
+ * 10-arc minimum of e (bright) and of -e (dark) by min / max doubling:
+ * corner(b) <=> arcmax > b, and fast_corner_score_10's barrier search
+ * (b += min_diff until the test fails, fast_10_score.cpp:21-3147) ends at
+ * max(threshold, arcmax - 1).  Bit i of the mask = corner at p + i; arcmax[i]. */
+typedef int16_t f10_i16x16 __attribute__((vector_size(32)));
+typedef uint8_t f10_u8x16 __attribute__((vector_size(16)));
+static inline f10_i16x16 f10_ld(const uint8_t *p) {
+    f10_u8x16 b;
+    memcpy(&b, p, 16);
+    return __builtin_convertvector(b, f10_i16x16);
+}
+static inline int f10_any(f10_i16x16 m) {
+    uint64_t q[4];
+    memcpy(q, &m, 32);
+    return (q[0] | q[1] | q[2] | q[3]) != 0;
+}
+static inline f10_i16x16 f10_min(f10_i16x16 a, f10_i16x16 b) { const f10_i16x16 m = a < b; return (a & m) | (b & ~m); }
+static inline f10_i16x16 f10_max(f10_i16x16 a, f10_i16x16 b) { const f10_i16x16 m = a > b; return (a & m) | (b & ~m); }
+
+static unsigned fast10_test16(const uint8_t *p, const int pix[16], int barrier, int16_t arcmax[16]) {
+    const f10_i16x16 v = f10_ld(p);
+    const f10_i16x16 lo = v - (int16_t)barrier, hi = v + (int16_t)barrier;
+    f10_i16x16 e[16];
+    for (int k = 0; k < 16; k += 4) e[k] = f10_ld(p + pix[k]);
+    const f10_i16x16 b0 = e[0] > hi, b4 = e[4] > hi, b8 = e[8] > hi, b12 = e[12] > hi;
+    const f10_i16x16 d0 = e[0] < lo, d4 = e[4] < lo, d8 = e[8] < lo, d12 = e[12] < lo;
+    const f10_i16x16 scr = (b0 & b4) | (b4 & b8) | (b8 & b12) | (b12 & b0) | (d0 & d4) | (d4 & d8) | (d8 & d12) |
+                           (d12 & d0);
+    if (!f10_any(scr)) return 0u;
+    for (int k = 0; k < 16; k++) {
+        if (k & 3) e[k] = f10_ld(p + pix[k]);
+        e[k] -= v;
+    }
+    f10_i16x16 n2[16], x2[16], n4[16], x4[16], n8[16], x8[16];
+    for (int k = 0; k < 16; k++) { n2[k] = f10_min(e[k], e[(k + 1) & 15]); x2[k] = f10_max(e[k], e[(k + 1) & 15]); }
+    for (int k = 0; k < 16; k++) { n4[k] = f10_min(n2[k], n2[(k + 2) & 15]); x4[k] = f10_max(x2[k], x2[(k + 2) & 15]); }
+    for (int k = 0; k < 16; k++) { n8[k] = f10_min(n4[k], n4[(k + 4) & 15]); x8[k] = f10_max(x4[k], x4[(k + 4) & 15]); }
+    f10_i16x16 bright = f10_min(n8[0], n2[8]), darkmin = f10_max(x8[0], x2[8]);
+    for (int k = 1; k < 16; k++) {
+        bright = f10_max(bright, f10_min(n8[k], n2[(k + 8) & 15]));
+        darkmin = f10_min(darkmin, f10_max(x8[k], x2[(k + 8) & 15]));
+    }
+    const f10_i16x16 am = f10_max(bright, -darkmin);
+    const f10_i16x16 c = (am > (int16_t)barrier) & scr;
+    if (!f10_any(c)) return 0u;
+    unsigned m = 0;
+    for (int i = 0; i < 16; i++) {
+        m |= (unsigned)(c[i] != 0) << i;
+        arcmax[i] = am[i];
+    }
+    return m;
+}
+
+static void ring10_offsets(int stride, int pix[16]) {
+    for (int k = 0; k < 16; k++) pix[k] = kRing[k][0] + kRing[k][1] * stride;
+}
+
+/* 0: the 16-pixel vector test (default), 1: the scalar one (test hook) */
+static int g_fast10_scalar = 0;
+void ygzo_fast10_force_scalar(int on) { g_fast10_scalar = on; }
+
+#if defined(__AVX2__)
+/* The compass screen on 32 pixels at once in unsigned-saturating bytes (the
+ * reference's SSE2 detector screens in bytes too): bit i set when pixel p + i
+ * has two neighbouring compass points both beyond v + b or both beyond v - b.
+ * hi = v +sat b, lo = v -sat b are exact: a saturated bound cannot be passed. */
+static inline uint32_t fast10_screen32(const uint8_t *p, const int pix[16], int barrier) {
+    const __m256i v = _mm256_loadu_si256((const __m256i *)p);
+    const __m256i b = _mm256_set1_epi8((char)barrier);
+    const __m256i hi = _mm256_adds_epu8(v, b), lo = _mm256_subs_epu8(v, b);
+    __m256i B[4], D[4];
+    for (int k = 0; k < 4; k++) {
+        const __m256i e = _mm256_loadu_si256((const __m256i *)(p + pix[4 * k]));
+        B[k] = _mm256_subs_epu8(e, hi);  /* nonzero <=> e > hi */
+        D[k] = _mm256_subs_epu8(lo, e);  /* nonzero <=> e < lo */
+    }
+    __m256i s = _mm256_min_epu8(B[0], B[1]);
+    s = _mm256_max_epu8(s, _mm256_min_epu8(B[1], B[2]));
+    s = _mm256_max_epu8(s, _mm256_min_epu8(B[2], B[3]));
+    s = _mm256_max_epu8(s, _mm256_min_epu8(B[3], B[0]));
+    s = _mm256_max_epu8(s, _mm256_min_epu8(D[0], D[1]));
+    s = _mm256_max_epu8(s, _mm256_min_epu8(D[1], D[2]));
+    s = _mm256_max_epu8(s, _mm256_min_epu8(D[2], D[3]));
+    s = _mm256_max_epu8(s, _mm256_min_epu8(D[3], D[0]));
+    return ~(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(s, _mm256_setzero_si256()));
+}
+#endif
+
+/* corners of rows [y0, y1) x columns [3, w - 3) in raster order; arcmax per corner if am != NULL */
+static int fast10_rows(const uint8_t *img, int w, int y0, int y1, int stride, int barrier, int16_t *xs, int16_t *ys,
+                       int16_t *am, int cap) {
+    int pix[16];
+    ring10_offsets(stride, pix);
+    int n = 0;
+    for (int y = y0; y < y1; y++) {
+        int x = 3;
+        if (!g_fast10_scalar) {
+#if defined(__AVX2__)
+            for (; x + 32 <= w - 3; x += 32) {  /* 32 pixels screened in bytes, survivors' halves tested */
+                const uint8_t *p = img + (size_t)y * stride + x;
+                const uint32_t scr = fast10_screen32(p, pix, barrier);
+                for (int half = 0; half < 2; half++) {
+                    if (!((scr >> (16 * half)) & 0xFFFFu)) continue;
+                    int16_t a[16];
+                    unsigned m = fast10_test16(p + 16 * half, pix, barrier, a);
+                    while (m) {
+                        const int i = __builtin_ctz(m);
+                        m &= m - 1;
+                        if (n < cap) {
+                            xs[n] = (int16_t)(x + 16 * half + i); ys[n] = (int16_t)y;
+                            if (am) am[n] = a[i];
+                        }
+                        n++;
+                    }
+                }
+            }
+#endif
+            for (; x + 16 <= w - 3; x += 16) {  /* ring of lane 15: columns x + 12 .. x + 18 <= w - 1 */
+                int16_t a[16];
+                unsigned m = fast10_test16(img + (size_t)y * stride + x, pix, barrier, a);
+                while (m) {
+                    const int i = __builtin_ctz(m);
+                    m &= m - 1;
+                    if (n < cap) { xs[n] = (int16_t)(x + i); ys[n] = (int16_t)y; if (am) am[n] = a[i]; }
+                    n++;
+                }
+            }
+            if (x < w - 3 && w - 19 >= 3) {  /* the tail: one block ending at column w - 4 */
+                const int xb = w - 19;
+                int16_t a[16];
+                unsigned m = fast10_test16(img + (size_t)y * stride + xb, pix, barrier, a) & (0xFFFFu << (x - xb));
+                while (m) {
+                    const int i = __builtin_ctz(m);
+                    m &= m - 1;
+                    if (n < cap) { xs[n] = (int16_t)(xb + i); ys[n] = (int16_t)y; if (am) am[n] = a[i]; }
+                    n++;
+                }
+                x = w - 3;
+            }
+        }
+        for (; x < w - 3; x++) {
+            const uint8_t *p = img + (size_t)y * stride + x;
+            if (ygzo_fast10_is_corner(p, stride, barrier)) {
+                if (n < cap) {
+                    xs[n] = (int16_t)x; ys[n] = (int16_t)y;
+                    if (am) am[n] = (int16_t)(ygzo_fast10_score(p, stride, barrier) + 1);
+                }
+                n++;
+            }
+        }
+    }
+    return n;
+}
+
 int ygzo_fast10_detect_sse2(const uint8_t *img, int w, int h, int stride, int barrier,
                             int16_t *xs, int16_t *ys, int cap) {
     if (w < 22) return ygzo_fast10_detect_plain(img, w, h, stride, barrier, xs, ys, cap);
     if (h < 7) return 0;
-    int n = 0; /* faster_corner_10_sse.cpp:24-183: rows [3,h-3), cols [3,w-3) */
-    for (int y = 3; y < h - 3; y++)
-        for (int x = 3; x < w - 3; x++)
-            if (ygzo_fast10_is_corner(img + (size_t)y * stride + x, stride, barrier)) {
-                if (n < cap) { xs[n] = (int16_t)x; ys[n] = (int16_t)y; }
-                n++;
-            }
+    /* faster_corner_10_sse.cpp:24-183: rows [3,h-3), cols [3,w-3) */
+    return fast10_rows(img, w, 3, h - 3, stride, barrier, xs, ys, NULL, cap);
+}
+
+/* fast_corner_detect_10_sse2 + fast_corner_score_10 + fast_nonmax_3x3 over one
+ * ROI (the reference library's full FAST-10 pipeline): corners kept by the 3x3
+ * non-maximum suppression (dropped if an 8-neighbour corner scores >= their
+ * own, nonmax_3x3.cpp:17-112), raster order, with their scores.  The NMS reads
+ * a dense score map of the ROI (-1 = no corner) instead of the reference's row
+ * pointers: O(corners), same survivors. */
+int ygzo_fast10_detect_score_nms(const uint8_t *img, int w, int h, int stride, int barrier, int16_t *xs,
+                                 int16_t *ys, int *scores, int cap) {
+    if (w < 22 || h < 7) return -1;
+    /* per-thread scratch kept across calls: the score map stays all -1 between
+     * calls (only the written corners are reset), so a call costs O(corners) on
+     * top of the scan, with no page faults */
+    static __thread int16_t *map = NULL, *cx = NULL;
+    static __thread size_t map_n = 0, c_n = 0;
+    const size_t npx = (size_t)w * h;
+    if (map_n < npx) {
+        free(map);
+        map = (int16_t *)malloc(sizeof(int16_t) * npx);
+        for (size_t i = 0; i < npx; i++) map[i] = -1;
+        map_n = npx;
+    }
+    const size_t ncap = npx / 2 + 16;
+    if (c_n < ncap) {
+        free(cx);
+        cx = (int16_t *)malloc(sizeof(int16_t) * 3 * ncap);
+        c_n = ncap;
+    }
+    int16_t *cy = cx + ncap, *ca = cy + ncap;
+    int nc = fast10_rows(img, w, 3, h - 3, stride, barrier, cx, cy, ca, (int)ncap);
+    if (nc > (int)ncap) nc = (int)ncap;
+    for (int k = 0; k < nc; k++) {
+        const int s = ca[k] - 1 > barrier ? ca[k] - 1 : barrier;
+        ca[k] = (int16_t)s;
+        map[(size_t)cy[k] * w + cx[k]] = (int16_t)s;
+    }
+    int n = 0;
+    for (int k = 0; k < nc; k++) {
+        const int16_t *r = map + (size_t)cy[k] * w + cx[k];
+        const int s = r[0];
+        if (r[-1] >= s || r[1] >= s || r[-w - 1] >= s || r[-w] >= s || r[-w + 1] >= s || r[w - 1] >= s || r[w] >= s ||
+            r[w + 1] >= s)
+            continue;
+        if (n < cap) { xs[n] = cx[k]; ys[n] = cy[k]; scores[n] = s; }
+        n++;
+    }
+    for (int k = 0; k < nc; k++) map[(size_t)cy[k] * w + cx[k]] = -1;
     return n;
 }
 

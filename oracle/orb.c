@@ -675,37 +675,75 @@ static inline int reflect101(int i, int n) {
     return i;
 }
 
+/* The two separable passes on 16-pixel vectors, as OpenCV's SIMD fixed-point
+ * path runs them: the horizontal sums fit uint16 exactly (<= 257 * 255 = 65535),
+ * the vertical sums int32 (<= 257 * 65535 + 32768 < 2^31).  Same integer sums as
+ * the scalar form, so the same bytes.  Per-thread row scratch kept across calls. */
+typedef uint16_t ygzo_u16x16 __attribute__((vector_size(32)));
+typedef int32_t ygzo_i32x16 __attribute__((vector_size(64)));
 void ygzo_gaussian_blur7(const uint8_t *src, int w, int h, int stride, uint8_t *dst,
                          int dstride, int variant) {
     const int *k = variant == YGZO_BLUR_CV3_ROUNDED ? kBlurCV3 : kBlurCV4;
-    /* horizontal pass into int rows: border columns through reflect101, the
-     * interior as a straight 7-tap loop (same sums, vectorisable) */
-    int *rows = (int *)malloc(sizeof(int) * (size_t)w * h);
+    static __thread uint16_t *rows = NULL;
+    static __thread size_t rows_n = 0;
+    const size_t need = (size_t)w * h + 16;
+    if (rows_n < need) {
+        free(rows);
+        rows = (uint16_t *)malloc(sizeof(uint16_t) * need);
+        rows_n = need;
+    }
+    /* horizontal pass: border columns through reflect101, the interior on vectors */
     for (int y = 0; y < h; y++) {
         const uint8_t *s = src + (size_t)y * stride;
-        int *r = rows + (size_t)y * w;
+        uint16_t *r = rows + (size_t)y * w;
         for (int x = 0; x < w; x++) {
             if (x == 3 && w - 3 > 3) x = w - 3;  /* the interior is done below */
             int acc = 0;
             for (int t = 0; t < 7; t++) acc += k[t] * s[reflect101(x + t - 3, w)];
-            r[x] = acc;
+            r[x] = (uint16_t)acc;
         }
-        for (int x = 3; x < w - 3; x++)
-            r[x] = k[0] * s[x - 3] + k[1] * s[x - 2] + k[2] * s[x - 1] + k[3] * s[x] + k[4] * s[x + 1] +
-                   k[5] * s[x + 2] + k[6] * s[x + 3];
+        int x = 3;
+        for (; x + 16 <= w - 3; x += 16) {  /* symmetric kernel: k[t] = k[6 - t] */
+            ygzo_u16x16 px[7];
+            for (int t = 0; t < 7; t++) {
+                ygzo_u8x16 b;
+                memcpy(&b, s + x + t - 3, 16);
+                px[t] = __builtin_convertvector(b, ygzo_u16x16);
+            }
+            const ygzo_u16x16 acc = (px[0] + px[6]) * (uint16_t)k[0] + (px[1] + px[5]) * (uint16_t)k[1] +
+                                    (px[2] + px[4]) * (uint16_t)k[2] + px[3] * (uint16_t)k[3];
+            memcpy(r + x, &acc, 32);
+        }
+        for (; x < w - 3; x++)
+            r[x] = (uint16_t)(k[0] * s[x - 3] + k[1] * s[x - 2] + k[2] * s[x - 1] + k[3] * s[x] + k[4] * s[x + 1] +
+                              k[5] * s[x + 2] + k[6] * s[x + 3]);
     }
     /* vertical pass: 7 row pointers (reflect101 at the top / bottom) */
     for (int y = 0; y < h; y++) {
-        const int *rr[7];
+        const uint16_t *rr[7];
         for (int t = 0; t < 7; t++) rr[t] = rows + (size_t)reflect101(y + t - 3, h) * w;
         uint8_t *o = dst + (size_t)y * dstride;
-        for (int x = 0; x < w; x++) {  /* <= 257 * 255 * 256 + 32768 < 2^31: int32 (vectorises) */
+        int x = 0;
+        for (; x + 16 <= w; x += 16) {
+            ygzo_i32x16 v[7];
+            for (int t = 0; t < 7; t++) {
+                ygzo_u16x16 u;
+                memcpy(&u, rr[t] + x, 32);
+                v[t] = __builtin_convertvector(u, ygzo_i32x16);
+            }
+            ygzo_i32x16 acc = (v[0] + v[6]) * k[0] + (v[1] + v[5]) * k[1] + (v[2] + v[4]) * k[2] + v[3] * k[3];
+            acc = (acc + 32768) >> 16;
+            const ygzo_i32x16 big = acc > 255;  /* CV3's sum-257 kernel can reach 257 (saturate_cast) */
+            acc = (acc & ~big) | (255 & big);
+            const ygzo_u8x16 ob = __builtin_convertvector(acc, ygzo_u8x16);
+            memcpy(o + x, &ob, 16);
+        }
+        for (; x < w; x++) {
             const int acc = k[0] * rr[0][x] + k[1] * rr[1][x] + k[2] * rr[2][x] + k[3] * rr[3][x] +
                             k[4] * rr[4][x] + k[5] * rr[5][x] + k[6] * rr[6][x];
             o[x] = (uint8_t)clampi((acc + 32768) >> 16, 0, 255);
         }
     }
-    free(rows);
 }
 
 /*

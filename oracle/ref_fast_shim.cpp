@@ -34,3 +34,25 @@ extern "C" int ref_fast10_nonmax(const int16_t *xs, const int16_t *ys, const int
     for (size_t i = 0; i < k.size(); i++) keep[i] = k[i];
     return (int)k.size();
 }
+
+// The reference library's whole FAST-10 pipeline (detect_sse2 + score + nonmax_3x3),
+// `reps` times over one ROI, timed here so no Python call overhead is counted:
+// returns the kept-corner count, *sec = mean seconds per pipeline.
+#include <chrono>
+extern "C" int ref_fast10_pipeline_bench(const uint8_t *img, int w, int h, int stride, int barrier, int reps,
+                                         double *sec) {
+    std::vector<fast::fast_xy> c;
+    std::vector<int> s, k;
+    int kept = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < reps; r++) {
+        c.clear();
+        fast::fast_corner_detect_10_sse2(img, w, h, stride, (short)barrier, c);
+        fast::fast_corner_score_10(img, stride, c, barrier, s);
+        fast::fast_nonmax_3x3(c, s, k);
+        kept = (int)k.size();
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    *sec = std::chrono::duration<double>(t1 - t0).count() / (reps > 0 ? reps : 1);
+    return kept;
+}

@@ -118,6 +118,11 @@ int ygzo_fast10_detect_plain(const uint8_t *img, int w, int h, int stride, int b
 /* fast_corner_detect_10_sse2 semantics (faster_corner_10_sse.cpp:189-202). */
 int ygzo_fast10_detect_sse2(const uint8_t *img, int w, int h, int stride, int barrier,
                             int16_t *xs, int16_t *ys, int cap);
+/* detect (SSE2 variant's ROI) + score + 3x3 NMS in one pass: kept corners, raster order */
+int ygzo_fast10_detect_score_nms(const uint8_t *img, int w, int h, int stride, int barrier, int16_t *xs,
+                                 int16_t *ys, int *scores, int cap);
+/* 0: 16-pixel vector FAST-10 test (default), 1: scalar (test hook) */
+void ygzo_fast10_force_scalar(int on);
 int ygzo_fast10_score(const uint8_t *p, int stride, int threshold);
 int ygzo_fast10_nonmax(const int16_t *xs, const int16_t *ys, const int *scores, int n,
                        int *keep);
@@ -224,6 +229,14 @@ void ygzo_search_direct(const ygzo_cam *cam, uint8_t **ref_levels, uint8_t **cur
                         float inv_level_sigma2_1, int n_points, const int *item_ptr, const int *ref_index,
                         const ygzo_kp *kps, const float *pt_ref, const ygzo_se3 *T_cr, const float *px_proj,
                         float border, float *px_out, int *matched);
+/* Tracking::SearchLocalPointsDirect (Tracking.cc:2258-2410) whole: the cache
+ * phase with the 5-px coverage grid, mnCacheHitTh, then the local-map phase. */
+int ygzo_search_local_points_direct(const ygzo_cam *cam, uint8_t **ref_levels, uint8_t **cur_levels, const int *lw,
+                                    const int *lh, int nlevels, const float *scale, const float *inv_scale,
+                                    float inv_level_sigma2_1, int n_cache, int n_local, const int *item_ptr,
+                                    const int *ref_index, const ygzo_kp *kps, const float *pt_ref,
+                                    const ygzo_se3 *T_cr, const float *px_proj, float border, int grid_size,
+                                    int cache_hit_th, float *px_out, int *matched, int *status, int *local_ran);
 
 /* ---------------- stereo (Frame.cc:509-700) ---------------- */
 /* Frame::ComputeStereoMatches (Frame.cc:509-682): left/right pyramids (same

@@ -1229,42 +1229,135 @@ __global__ __launch_bounds__(256) void k_direct_items(const uint8_t *const *__re
     ok_out[i] = (uint8_t)ok;
 }
 
-__global__ __launch_bounds__(256) void k_direct_select(int n_points, const int32_t *__restrict__ item_ptr,
-                                                       const float *__restrict__ px_item,
-                                                       const uint8_t *__restrict__ ok_item, float border, float cols,
-                                                       float rows, float *__restrict__ px_out,
-                                                       int32_t *__restrict__ matched) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_points) return;
-    int m = -1;
-    float u = 0.f, v = 0.f;
+// Tracking::SearchLocalPointsDirect's sequential part (Tracking.cc:2258-2410) in one
+// workgroup: wave 0 replays the cache points in the reference's order against the
+// 5-px coverage grid (an LDS bitmap), 64 points per step: each lane finds its
+// point's first converged in-border item and the two grid cells in parallel, then
+// the wave walks the 64 lanes in order with uniform control flow (readlane + one
+// ballot per point resolves "cell already taken by an earlier success of this
+// step"; earlier steps' marks are already in the bitmap).  The success count
+// decides mnCacheHitTh (:2334-2340); then all 16 waves take the local-map points,
+// which have no grid (:2348-2405).
+__device__ __forceinline__ int direct_first_item(int i, const int32_t *__restrict__ item_ptr,
+                                                 const float *__restrict__ px_item,
+                                                 const uint8_t *__restrict__ ok_item, float border, float cols,
+                                                 float rows, float &u, float &v) {
+    u = 0.f;
+    v = 0.f;
     for (int k = item_ptr[i]; k < item_ptr[i + 1]; k++) {
         if (!ok_item[k]) continue;
         const float x = px_item[2 * k], y = px_item[2 * k + 1];
         if (x < border || y < border || x >= cols - border || y >= rows - border) continue;
-        m = k;
-        u = x;
-        v = y;
-        break;
+        // px_ave = sum(matched_pixels) / size() with exactly one pixel (Tracking.cc:2305-2309)
+        u = x / 1.0f;
+        v = y / 1.0f;
+        return k;
     }
-    // px_ave = sum(matched_pixels) / size() with exactly one pixel (Tracking.cc:2300-2305)
-    px_out[2 * i] = u / 1.0f;
-    px_out[2 * i + 1] = v / 1.0f;
-    matched[i] = m;
+    return -1;
+}
+
+// static_cast<int>(x / grid_size) per axis, k = gy * grid_cols + gx; -2 when k is outside the grid
+__device__ __forceinline__ int direct_cell(float x, float y, int grid_size, int grid_cols, int ncell) {
+    const float gs = (float)grid_size;
+    const int gx = (int)(x / gs), gy = (int)(y / gs);
+    const long k = (long)gy * grid_cols + gx;
+    return (k >= 0 && k < ncell) ? (int)k : -2;
+}
+
+__global__ __launch_bounds__(1024) void k_direct_replay(int n_cache, int n_local, const int32_t *__restrict__ item_ptr,
+                                                        const float *__restrict__ px_item,
+                                                        const uint8_t *__restrict__ ok_item,
+                                                        const float *__restrict__ px_proj, float border, int cols,
+                                                        int rows, int grid_size, int grid_cols, int ncell,
+                                                        int cache_hit_th, float *__restrict__ px_out,
+                                                        int32_t *__restrict__ matched, int32_t *__restrict__ status,
+                                                        int32_t *__restrict__ hdr) {
+    extern __shared__ uint32_t grid[];
+    __shared__ int s_cnt;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int nwords = (ncell + 31) >> 5;
+    for (int w = tid; w < nwords; w += blockDim.x) grid[w] = 0u;
+    __syncthreads();
+    const float fc = (float)cols, fr = (float)rows;
+    if (tid < 64) {
+        int cnt = 0;
+        for (int base = 0; base < n_cache; base += 64) {
+            const int i = base + lane;
+            const bool valid = i < n_cache;
+            float u = 0.f, v = 0.f;
+            int m = -1, c = -2, mk = -1;
+            bool pre = false;
+            if (valid) {
+                m = direct_first_item(i, item_ptr, px_item, ok_item, border, fc, fr, u, v);
+                c = direct_cell(px_proj[2 * i], px_proj[2 * i + 1], grid_size, grid_cols, ncell);
+                if (m >= 0) {
+                    mk = direct_cell(u, v, grid_size, grid_cols, ncell);
+                    if (mk < 0) mk = -1;  // the reference writes outside its grid; never read back here
+                }
+                pre = c >= 0 && ((grid[c >> 5] >> (c & 31)) & 1u);
+            }
+            const int nb = min(64, n_cache - base);
+            bool marked = false;
+            int st = 0;
+            for (int j = 0; j < nb; j++) {
+                const int cj = __builtin_amdgcn_readlane(c, j);
+                const int mj = __builtin_amdgcn_readlane(m, j);
+                const int prej = __builtin_amdgcn_readlane((int)pre, j);
+                const uint64_t hit = __ballot(marked && mk == cj);
+                const bool skip = prej || hit != 0;
+                const int sj = skip ? 2 : (mj >= 0 ? 1 : 0);
+                if (lane == j) {
+                    st = sj;
+                    marked = sj == 1 && mk >= 0;
+                }
+                cnt += sj == 1;
+            }
+            if (marked) atomicOr(&grid[mk >> 5], 1u << (mk & 31));
+            wave_lds_order();
+            if (valid) {
+                const bool ok = st == 1;
+                status[i] = st;
+                matched[i] = ok ? m : -1;
+                px_out[2 * i] = ok ? u : 0.f;
+                px_out[2 * i + 1] = ok ? v : 0.f;
+            }
+        }
+        if (lane == 0) s_cnt = cnt;
+    }
+    __syncthreads();
+    const int cnt = s_cnt;
+    const bool local_ran = !(cnt > cache_hit_th);
+    if (tid == 0) {
+        hdr[0] = cnt;
+        hdr[1] = local_ran ? 1 : 0;
+    }
+    for (int i = n_cache + tid; i < n_cache + n_local; i += blockDim.x) {
+        float u = 0.f, v = 0.f;
+        const int m = local_ran ? direct_first_item(i, item_ptr, px_item, ok_item, border, fc, fr, u, v) : -1;
+        status[i] = local_ran ? (m >= 0 ? 1 : 0) : 3;
+        matched[i] = m;
+        px_out[2 * i] = u;
+        px_out[2 * i + 1] = v;
+    }
 }
 
 hipError_t launch_search_direct(const uint8_t *const *ref_pyrs, const AlignLevels &lv, const uint8_t *cur_pyr,
                                 int nlevels, const float *scale, float inv_sigma2_1, const ygzfe_camera &cam,
-                                int n_points, int n_items, const int32_t *item_ptr, const void *items,
-                                const float *px_proj, float *px_item, uint8_t *ok_item, float border, float *px_out,
-                                int32_t *matched, hipStream_t st) {
-    if (n_points <= 0) return hipSuccess;
+                                int n_cache, int n_local, int n_items, const int32_t *item_ptr, const void *items,
+                                const float *px_proj, float *px_item, uint8_t *ok_item, float border, int grid_size,
+                                int cache_hit_th, float *px_out, int32_t *matched, int32_t *status, int32_t *hdr,
+                                hipStream_t st) {
+    const int n_points = n_cache + n_local;
     if (n_items > 0)
         hipLaunchKernelGGL(k_direct_items, dim3((n_items + 255) / 256), dim3(256), 0, st, ref_pyrs, lv, cur_pyr,
                            nlevels, scale, inv_sigma2_1, cam, n_items, (const DirectItem *)items, px_proj, px_item,
                            ok_item);
-    hipLaunchKernelGGL(k_direct_select, dim3((n_points + 255) / 256), dim3(256), 0, st, n_points, item_ptr, px_item,
-                       ok_item, border, (float)lv.w[0], (float)lv.h[0], px_out, matched);
+    const int grid_cols = lv.w[0] / grid_size, ncell = (lv.h[0] / grid_size) * grid_cols;
+    const size_t lds = (size_t)((ncell + 31) / 32) * 4 + 4;
+    hipLaunchKernelGGL(k_direct_replay, dim3(1), dim3(1024), lds, st, n_cache, n_local, item_ptr, px_item, ok_item,
+                       px_proj, border, lv.w[0], lv.h[0], grid_size, grid_cols, ncell, cache_hit_th, px_out, matched,
+                       status, hdr);
+    (void)n_points;
     return hipGetLastError();
 }
 

@@ -197,7 +197,7 @@ struct ygzfe_extractor {
     int dso_grid = -1;
     // SearchLocalPointsDirect staging: one packed H2D, one packed D2H per call
     DevBuf direct_dev;
-    std::vector<uint8_t> direct_host;
+    HostBuf direct_hin, direct_hout;
     // single-frame latency path: side streams (blur, FAST levels >= 1, octree
     // classes after the first) forked from / joined to `stream`, pinned staging,
     // the packed extraction result (one D2H) and the SparseImgAlign buffers
@@ -207,6 +207,12 @@ struct ygzfe_extractor {
     HostBuf hin, hout, himg;
     hipEvent_t ev_img = nullptr;  // the last image DMA out of himg
     DevBuf res, align_in, align_scratch, align_out;
+    // SparseImgAlign in flight (ygzfe_sparse_align_begin / _end): its own stream,
+    // pinned staging and completion event, so it overlaps the same frame's extraction
+    hipStream_t astream = nullptr;
+    hipEvent_t ev_align_fork = nullptr, ev_align_done = nullptr;
+    HostBuf ahin, ahout;
+    bool align_pending = false;
     bool graph_broken = false;  // stream capture failed once: plain launches
     std::mutex mu;
     int ensure_side() {
@@ -221,6 +227,18 @@ struct ygzfe_extractor {
         for (int i = 0; i < 2; i++) YGZ_HIP(hipEventCreateWithFlags(&ev_oct_join[i], hipEventDisableTiming));
         return YGZFE_OK;
     }
+    int ensure_align_stream() {
+        if (astream) return YGZFE_OK;
+        YGZ_HIP(hipStreamCreateWithFlags(&astream, hipStreamNonBlocking));
+        YGZ_HIP(hipEventCreateWithFlags(&ev_align_fork, hipEventDisableTiming));
+        YGZ_HIP(hipEventCreateWithFlags(&ev_align_done, hipEventDisableTiming));
+        return YGZFE_OK;
+    }
+    // work about to rewrite a pyramid on `st` waits for the alignment reading it
+    int order_after_align(hipStream_t st) {
+        if (align_pending) YGZ_HIP(hipStreamWaitEvent(st, ev_align_done, 0));
+        return YGZFE_OK;
+    }
 };
 
 struct ygzfe_frame {
@@ -231,7 +249,7 @@ struct ygzfe_frame {
     // the captured single-frame extraction (ygzfe_extract, no existing rows)
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
-    const void *gkey[9] = {};
+    const void *gkey[14] = {};
     int grows = 0;
     size_t gcopy = 0;
     void drop_graph() {
@@ -360,6 +378,12 @@ void ygzfe_extractor_destroy(ygzfe_extractor *ex) {
         if (ex->ev_join[i]) (void)hipEventDestroy(ex->ev_join[i]);
     }
     if (ex->ev_fork) (void)hipEventDestroy(ex->ev_fork);
+    if (ex->astream) {
+        (void)hipStreamSynchronize(ex->astream);
+        (void)hipStreamDestroy(ex->astream);
+        (void)hipEventDestroy(ex->ev_align_fork);
+        (void)hipEventDestroy(ex->ev_align_done);
+    }
     if (ex->ev_img) (void)hipEventDestroy(ex->ev_img);
     if (ex->ev_oct_fork) (void)hipEventDestroy(ex->ev_oct_fork);
     for (int i = 0; i < 2; i++)
@@ -462,8 +486,9 @@ int ygzfe_compute_pyramid(ygzfe_extractor *ex, ygzfe_frame *f, const uint8_t *im
     // synchronisation here -- only before the staging is overwritten
     YGZ_TRY(ex->ensure_side());
     const size_t n = (size_t)f->W * f->H;
+    YGZ_HIP(hipEventSynchronize(ex->ev_img));  // the previous DMA out of himg (before it may be reallocated)
+    YGZ_TRY(ex->order_after_align(ex->stream));
     YGZ_TRY(ex->himg.ensure(n));
-    YGZ_HIP(hipEventSynchronize(ex->ev_img));
     uint8_t *h = ex->himg.as<uint8_t>();
     if (stride == f->W) {
         memcpy(h, img, n);
@@ -481,6 +506,7 @@ int ygzfe_compute_pyramid_device(ygzfe_extractor *ex, ygzfe_frame *f, const uint
     if (!ex || !f || !d_img || stride < f->W) { set_error("invalid argument"); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(ex->device));
     hipStream_t st = stream ? (hipStream_t)stream : ex->stream;
+    YGZ_TRY(ex->order_after_align(st));
     YGZ_HIP(hipMemcpy2DAsync(f->pyr.p, f->W, d_img, stride, f->W, f->H, hipMemcpyDeviceToDevice, st));
     YGZ_TRY(pyramid_from_level0(f, st));
     if (!stream) YGZ_HIP(hipStreamSynchronize(st));
@@ -511,6 +537,7 @@ int ygzfe_frame_set_level(ygzfe_frame *f, int level, const uint8_t *src, int src
     if (src_stride < L.w) { set_error("src_stride < level width"); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(f->ex->device));
     YGZ_HIP(hipStreamSynchronize(f->ex->stream));
+    if (f->ex->align_pending) YGZ_HIP(hipEventSynchronize(f->ex->ev_align_done));
     YGZ_HIP(hipMemcpy2D(f->pyr.as<uint8_t>() + L.off, L.w, src, src_stride, L.w, L.h, hipMemcpyHostToDevice));
     return YGZFE_OK;
 }
@@ -601,8 +628,9 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
         // joins and the D2H) is replayed from a HIP graph captured once per frame
         // handle: one submission instead of one host call per launch.  The graph is
         // re-captured when any buffer it names has moved or the copy size changed.
-        const void *key[9] = {pyr, ws.blur.p, ws.cellbuf.p, ws.sel.p, ws.candA.p, ws.candB.p, ex->res.p, ex->hout.p,
-                              ws.ojobs.p};
+        const void *key[14] = {pyr,          ws.blur.p,  ws.cellbuf.p, ws.sel.p,       ws.candA.p,
+                               ws.candB.p,   ex->res.p,  ex->hout.p,   ws.ojobs.p,     ws.cellcnt.p,
+                               ws.selcnt.p,  pd.cells.p, pd.plan.p,    pd.tabs.p};
         static const bool no_graph = getenv("YGZFE_NO_GRAPH") != nullptr;
         bool launched = false;
         if (n_existing == 0 && !no_graph && !ex->graph_broken) {
@@ -1122,10 +1150,10 @@ static AlignLevels levels_of(const Plan &P) {
     return lv;
 }
 
-int ygzfe_sparse_align(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam, const ygzfe_kp *kps,
-                       const float *xyz_ref, const uint8_t *usable, int n, int max_level, int min_level,
-                       const ygzfe_se3 *T_init, ygzfe_align_result *result) {
-    if (!ref || !cur || !cam || !T_init || !result || n < 0 || (n > 0 && (!kps || !xyz_ref || !usable))) {
+int ygzfe_sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam,
+                             const ygzfe_kp *kps, const float *xyz_ref, const uint8_t *usable, int n, int max_level,
+                             int min_level, const ygzfe_se3 *T_init) {
+    if (!ref || !cur || !cam || !T_init || n < 0 || (n > 0 && (!kps || !xyz_ref || !usable))) {
         set_error("invalid argument");
         return YGZFE_EINVAL;
     }
@@ -1135,16 +1163,25 @@ int ygzfe_sparse_align(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygz
         set_error("levels [%d,%d] outside the %d-level pyramid", min_level, max_level, P.nlevels);
         return YGZFE_EINVAL;
     }
-    if (n == 0) {  // SparseImageAlign.cc:24-27
-        memset(result, 0, sizeof(*result));
-        result->T_cur_ref = *T_init;
-        result->chi2 = 1e10f;
-        return YGZFE_OK;
-    }
     ygzfe_extractor *ex = ref->ex;
     YGZ_TRY(ensure_device(ex->device));
     std::lock_guard<std::mutex> lk(ex->mu);
-    hipStream_t st = ex->stream;
+    if (ex->align_pending) { set_error("a SparseImgAlign is already in flight on this extractor"); return YGZFE_ESTATE; }
+    YGZ_TRY(ex->ensure_align_stream());
+    YGZ_TRY(ex->ahout.ensure(sizeof(ygzfe_align_result)));
+    if (n == 0) {  // SparseImageAlign.cc:24-27: no alignment, TCR untouched
+        ygzfe_align_result *r = ex->ahout.as<ygzfe_align_result>();
+        memset(r, 0, sizeof(*r));
+        r->T_cur_ref = *T_init;
+        r->chi2 = 1e10f;
+        YGZ_HIP(hipEventRecord(ex->ev_align_done, ex->astream));
+        ex->align_pending = true;
+        return YGZFE_OK;
+    }
+    hipStream_t st = ex->astream;
+    // after everything queued so far on the extractor stream (the two pyramids)
+    YGZ_HIP(hipEventRecord(ex->ev_align_fork, ex->stream));
+    YGZ_HIP(hipStreamWaitEvent(st, ex->ev_align_fork, 0));
     // one packed H2D from pinned staging: [job][keypoints][xyz][usable] (16-B aligned
     // pieces), cached device buffers, one D2H of the result
     const size_t o_k = align16(sizeof(AlignJob)), o_x = o_k + align16(sizeof(ygzfe_kp) * (size_t)n);
@@ -1153,9 +1190,8 @@ int ygzfe_sparse_align(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygz
     YGZ_TRY(ex->align_in.ensure(in_bytes));
     YGZ_TRY(ex->align_scratch.ensure(sizeof(float) * spj));
     YGZ_TRY(ex->align_out.ensure(sizeof(ygzfe_align_result)));
-    YGZ_TRY(ex->hin.ensure(in_bytes));
-    YGZ_TRY(ex->hout.ensure(sizeof(ygzfe_align_result)));
-    uint8_t *din = ex->align_in.as<uint8_t>(), *hin = ex->hin.as<uint8_t>();
+    YGZ_TRY(ex->ahin.ensure(in_bytes));
+    uint8_t *din = ex->align_in.as<uint8_t>(), *hin = ex->ahin.as<uint8_t>();
     AlignJob job;
     job.ref_pyr = ref->pyr.as<uint8_t>();
     job.cur_pyr = cur->pyr.as<uint8_t>();
@@ -1173,10 +1209,30 @@ int ygzfe_sparse_align(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygz
     YGZ_HIP(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, st));
     YGZ_HIP(launch_sparse_align(levels_of(P), *cam, reinterpret_cast<const AlignJob *>(din), 1,
                                 ex->align_scratch.as<float>(), spj, ex->align_out.as<ygzfe_align_result>(), st, n));
-    YGZ_HIP(hipMemcpyAsync(ex->hout.p, ex->align_out.p, sizeof(*result), hipMemcpyDeviceToHost, st));
-    YGZ_HIP(hipStreamSynchronize(st));
-    memcpy(result, ex->hout.p, sizeof(*result));
+    YGZ_HIP(hipMemcpyAsync(ex->ahout.p, ex->align_out.p, sizeof(ygzfe_align_result), hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipEventRecord(ex->ev_align_done, st));
+    ex->align_pending = true;
     return YGZFE_OK;
+}
+
+int ygzfe_sparse_align_end(const ygzfe_frame *cur, ygzfe_align_result *result) {
+    if (!cur || !result) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    ygzfe_extractor *ex = cur->ex;
+    std::lock_guard<std::mutex> lk(ex->mu);
+    if (!ex->align_pending) { set_error("no SparseImgAlign in flight on this extractor"); return YGZFE_ESTATE; }
+    YGZ_TRY(ensure_device(ex->device));
+    ex->align_pending = false;
+    YGZ_HIP(hipEventSynchronize(ex->ev_align_done));
+    memcpy(result, ex->ahout.p, sizeof(*result));
+    return YGZFE_OK;
+}
+
+int ygzfe_sparse_align(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam, const ygzfe_kp *kps,
+                       const float *xyz_ref, const uint8_t *usable, int n, int max_level, int min_level,
+                       const ygzfe_se3 *T_init, ygzfe_align_result *result) {
+    if (!result) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    YGZ_TRY(ygzfe_sparse_align_begin(ref, cur, cam, kps, xyz_ref, usable, n, max_level, min_level, T_init));
+    return ygzfe_sparse_align_end(cur, result);
 }
 
 }  // extern "C"
@@ -1388,17 +1444,32 @@ extern "C" int ygzfe_find_direct_projection_batch(const ygzfe_frame *const *ref,
     return YGZFE_OK;
 }
 
-extern "C" int ygzfe_search_direct_batch(const ygzfe_frame *const *ref, int n_ref, const ygzfe_frame *cur,
-                                         const ygzfe_camera *cam, int n_points, const int32_t *item_ptr,
-                                         const int32_t *ref_index, const ygzfe_kp *kp_ref, const float *pt_ref,
-                                         const ygzfe_se3 *T_cr, const float *px_proj, float border,
-                                         float *px_out, int32_t *matched_item) {
-    if (!ref || n_ref < 0 || !cur || !cam || n_points < 0 ||
+// SearchLocalPointsDirect (Tracking.cc:2258-2410): items of both phases in one
+// packed H2D from pinned staging, k_direct_items + k_direct_replay, one packed D2H.
+static int search_direct_impl(const ygzfe_frame *const *ref, int n_ref, const ygzfe_frame *cur,
+                              const ygzfe_camera *cam, int n_cache, int n_local, const int32_t *item_ptr,
+                              const int32_t *ref_index, const ygzfe_kp *kp_ref, const float *pt_ref,
+                              const ygzfe_se3 *T_cr, const float *px_proj, float border, int grid_size,
+                              int cache_hit_th, float *px_out, int32_t *matched_item, int32_t *status,
+                              int *cache_success, int *local_ran) {
+    const int n_points = n_cache + n_local;
+    if (!ref || n_ref < 0 || !cur || !cam || n_cache < 0 || n_local < 0 ||
         (n_points > 0 && (!item_ptr || !px_proj || !px_out || !matched_item))) {
         set_error("invalid argument");
         return YGZFE_EINVAL;
     }
-    if (n_points == 0) return YGZFE_OK;
+    if (grid_size <= 0) { set_error("grid_size must be positive"); return YGZFE_EINVAL; }
+    const Plan &P = cur->plan->hp();
+    const long ncell = (long)(P.lv[0].h / grid_size) * (P.lv[0].w / grid_size);
+    if (ncell > kDirectMaxGridCells) {
+        set_error("coverage grid of %ld cells exceeds %d", ncell, kDirectMaxGridCells);
+        return YGZFE_EINVAL;
+    }
+    if (n_points == 0) {
+        if (cache_success) *cache_success = 0;
+        if (local_ran) *local_ran = !(0 > cache_hit_th);
+        return YGZFE_OK;
+    }
     if (item_ptr[0] != 0) { set_error("item_ptr[0] must be 0"); return YGZFE_EINVAL; }
     for (int i = 0; i < n_points; i++)
         if (item_ptr[i + 1] < item_ptr[i]) { set_error("item_ptr not monotone at %d", i); return YGZFE_EINVAL; }
@@ -1406,6 +1477,11 @@ extern "C" int ygzfe_search_direct_batch(const ygzfe_frame *const *ref, int n_re
     if (n_items > 0 && (!ref_index || !kp_ref || !pt_ref || !T_cr)) { set_error("null item array"); return YGZFE_EINVAL; }
     for (int k = 0; k < n_items; k++)
         if (ref_index[k] < 0 || ref_index[k] >= n_ref) { set_error("ref_index[%d] out of range", k); return YGZFE_EINVAL; }
+    for (int k = 0; k < n_items; k++)
+        if (kp_ref[k].octave < 0 || kp_ref[k].octave >= P.nlevels) {
+            set_error("kp_ref[%d].octave %d out of range", k, kp_ref[k].octave);
+            return YGZFE_EINVAL;
+        }
     for (int r = 0; r < n_ref; r++)
         if (!ref[r] || ref[r]->plan != cur->plan) {
             set_error("reference keyframe %d missing or of a different size", r);
@@ -1415,43 +1491,75 @@ extern "C" int ygzfe_search_direct_batch(const ygzfe_frame *const *ref, int n_re
     YGZ_TRY(ensure_device(ex->device));
     std::lock_guard<std::mutex> lk(ex->mu);
     hipStream_t st = ex->stream;
-    const Plan &P = cur->plan->hp();
-    // packed layout: [ref ptrs][scale][item_ptr][px_proj][items] | [px_item][px_out][matched][ok_item]
+    // in: [ref ptrs][scale][item_ptr][px_proj][items]   out: [hdr][px_out][matched][status] | [px_item][ok_item]
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_ptr = 0, o_sc = al(o_ptr + sizeof(void *) * std::max(1, n_ref));
     const size_t o_ip = al(o_sc + 4 * kMaxLevels), o_pp = al(o_ip + 4 * ((size_t)n_points + 1));
     const size_t o_it = al(o_pp + 8 * (size_t)n_points), in_bytes = al(o_it + sizeof(DirectItem) * (size_t)n_items);
-    const size_t o_pxo = 0, o_m = al(o_pxo + 8 * (size_t)n_points), o_pxi = al(o_m + 4 * (size_t)n_points);
-    const size_t o_ok = al(o_pxi + 8 * (size_t)n_items), out_bytes = al(o_ok + (size_t)n_items);
-    std::vector<uint8_t> &h = ex->direct_host;
-    if (h.size() < in_bytes) h.resize(in_bytes);
-    const uint8_t **ptrs = (const uint8_t **)(h.data() + o_ptr);
+    const size_t o_hdr = 0, o_pxo = 16, o_m = o_pxo + 8 * (size_t)n_points, o_st = o_m + 4 * (size_t)n_points;
+    const size_t back_bytes = o_st + 4 * (size_t)n_points;
+    const size_t o_pxi = al(back_bytes), o_ok = al(o_pxi + 8 * (size_t)n_items), out_bytes = al(o_ok + (size_t)n_items);
+    YGZ_TRY(ex->direct_hin.ensure(in_bytes));
+    YGZ_TRY(ex->direct_hout.ensure(back_bytes));
+    uint8_t *h = ex->direct_hin.as<uint8_t>();
+    const uint8_t **ptrs = (const uint8_t **)(h + o_ptr);
     for (int r = 0; r < n_ref; r++) ptrs[r] = ref[r]->pyr.as<uint8_t>();
-    float *sc = (float *)(h.data() + o_sc);
+    float *sc = (float *)(h + o_sc);
     for (int l = 0; l < P.nlevels; l++) sc[l] = P.lv[l].scale;
-    memcpy(h.data() + o_ip, item_ptr, 4 * ((size_t)n_points + 1));
-    memcpy(h.data() + o_pp, px_proj, 8 * (size_t)n_points);
-    DirectItem *it = (DirectItem *)(h.data() + o_it);
-    for (int k = 0; k < n_items; k++) {
-        it[k].kp = kp_ref[k];
-        memcpy(it[k].pt, pt_ref + 3 * (size_t)k, 12);
-        it[k].Tcr = T_cr[k];
-        it[k].ref = ref_index[k];
-    }
+    memcpy(h + o_ip, item_ptr, 4 * ((size_t)n_points + 1));
+    memcpy(h + o_pp, px_proj, 8 * (size_t)n_points);
+    DirectItem *it = (DirectItem *)(h + o_it);
     for (int i = 0; i < n_points; i++)
-        for (int k = item_ptr[i]; k < item_ptr[i + 1]; k++) it[k].point = i;
+        for (int k = item_ptr[i]; k < item_ptr[i + 1]; k++) {
+            it[k].kp = kp_ref[k];
+            memcpy(it[k].pt, pt_ref + 3 * (size_t)k, 12);
+            it[k].Tcr = T_cr[k];
+            it[k].ref = ref_index[k];
+            it[k].point = i;
+            it[k].pad = 0;
+        }
     YGZ_TRY(ex->direct_dev.ensure(in_bytes + out_bytes));
     uint8_t *d = ex->direct_dev.as<uint8_t>(), *dout = d + in_bytes;
-    YGZ_HIP(hipMemcpyAsync(d, h.data(), in_bytes, hipMemcpyHostToDevice, st));
+    YGZ_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st));
     YGZ_HIP(launch_search_direct((const uint8_t *const *)(d + o_ptr), levels_of(P), cur->pyr.as<uint8_t>(),
                                  P.nlevels, (const float *)(d + o_sc), ex->scales.inv_sigma2[1 < P.nlevels ? 1 : 0],
-                                 *cam, n_points, n_items, (const int32_t *)(d + o_ip), d + o_it,
-                                 (const float *)(d + o_pp), (float *)(dout + o_pxi), dout + o_ok, border,
-                                 (float *)(dout + o_pxo), (int32_t *)(dout + o_m), st));
-    YGZ_HIP(hipMemcpyAsync(px_out, dout + o_pxo, 8 * (size_t)n_points, hipMemcpyDeviceToHost, st));
-    YGZ_HIP(hipMemcpyAsync(matched_item, dout + o_m, 4 * (size_t)n_points, hipMemcpyDeviceToHost, st));
+                                 *cam, n_cache, n_local, n_items, (const int32_t *)(d + o_ip), d + o_it,
+                                 (const float *)(d + o_pp), (float *)(dout + o_pxi), dout + o_ok, border, grid_size,
+                                 cache_hit_th, (float *)(dout + o_pxo), (int32_t *)(dout + o_m),
+                                 (int32_t *)(dout + o_st), (int32_t *)(dout + o_hdr), st));
+    uint8_t *hb = ex->direct_hout.as<uint8_t>();
+    YGZ_HIP(hipMemcpyAsync(hb, dout, back_bytes, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipStreamSynchronize(st));
+    memcpy(px_out, hb + o_pxo, 8 * (size_t)n_points);
+    memcpy(matched_item, hb + o_m, 4 * (size_t)n_points);
+    if (status) memcpy(status, hb + o_st, 4 * (size_t)n_points);
+    int32_t hdr[2];
+    memcpy(hdr, hb + o_hdr, 8);
+    if (cache_success) *cache_success = hdr[0];
+    if (local_ran) *local_ran = hdr[1];
     return YGZFE_OK;
+}
+
+extern "C" int ygzfe_search_direct_batch(const ygzfe_frame *const *ref, int n_ref, const ygzfe_frame *cur,
+                                         const ygzfe_camera *cam, int n_points, const int32_t *item_ptr,
+                                         const int32_t *ref_index, const ygzfe_kp *kp_ref, const float *pt_ref,
+                                         const ygzfe_se3 *T_cr, const float *px_proj, float border,
+                                         float *px_out, int32_t *matched_item) {
+    // the local-map loop alone (Tracking.cc:2348-2405): no grid, always runs
+    return search_direct_impl(ref, n_ref, cur, cam, 0, n_points, item_ptr, ref_index, kp_ref, pt_ref, T_cr, px_proj,
+                              border, 5, 0x7fffffff, px_out, matched_item, nullptr, nullptr, nullptr);
+}
+
+extern "C" int ygzfe_search_local_points_direct(const ygzfe_frame *const *ref, int n_ref, const ygzfe_frame *cur,
+                                                const ygzfe_camera *cam, int n_cache, int n_local,
+                                                const int32_t *item_ptr, const int32_t *ref_index,
+                                                const ygzfe_kp *kp_ref, const float *pt_ref, const ygzfe_se3 *T_cr,
+                                                const float *px_proj, float border, int grid_size, int cache_hit_th,
+                                                float *px_out, int32_t *matched_item, int32_t *status,
+                                                int *cache_success, int *local_ran) {
+    return search_direct_impl(ref, n_ref, cur, cam, n_cache, n_local, item_ptr, ref_index, kp_ref, pt_ref, T_cr,
+                              px_proj, border, grid_size, cache_hit_th, px_out, matched_item, status, cache_success,
+                              local_ran);
 }
 
 // --------------------------------------------------------------------------
@@ -1518,8 +1626,8 @@ extern "C" int ygzfe_stereo_matches(const ygzfe_frame *left, const ygzfe_frame *
     const size_t total = al(o_s + 4 * (size_t)nl);
     YGZ_TRY(ex->direct_dev.ensure(total));
     uint8_t *d = ex->direct_dev.as<uint8_t>();
-    std::vector<uint8_t> &h = ex->direct_host;
-    if (h.size() < in_bytes) h.resize(in_bytes);
+    YGZ_TRY(ex->direct_hin.ensure(in_bytes));
+    uint8_t *h = ex->direct_hin.as<uint8_t>();
     StereoJob J;
     J.left_pyr = left->pyr.as<uint8_t>();
     J.right_pyr = right->pyr.as<uint8_t>();
@@ -1532,14 +1640,14 @@ extern "C" int ygzfe_stereo_matches(const ygzfe_frame *left, const ygzfe_frame *
     J.u_right = (float *)(d + o_u);
     J.depth = (float *)(d + o_d);
     J.sad = (int *)(d + o_s);
-    memcpy(h.data() + o_job, &J, sizeof(J));
+    memcpy(h + o_job, &J, sizeof(J));
     const int cnt[2] = {nl, nr};
-    memcpy(h.data() + o_cnt, cnt, 8);
-    memcpy(h.data() + o_kl, kl, sizeof(ygzfe_kp) * (size_t)nl);
-    if (nr) memcpy(h.data() + o_kr, kr, sizeof(ygzfe_kp) * (size_t)nr);
-    memcpy(h.data() + o_dl, dl, 32 * (size_t)nl);
-    if (nr) memcpy(h.data() + o_dr, dr, 32 * (size_t)nr);
-    YGZ_HIP(hipMemcpyAsync(d, h.data(), in_bytes, hipMemcpyHostToDevice, st));
+    memcpy(h + o_cnt, cnt, 8);
+    memcpy(h + o_kl, kl, sizeof(ygzfe_kp) * (size_t)nl);
+    if (nr) memcpy(h + o_kr, kr, sizeof(ygzfe_kp) * (size_t)nr);
+    memcpy(h + o_dl, dl, 32 * (size_t)nl);
+    if (nr) memcpy(h + o_dr, dr, 32 * (size_t)nr);
+    YGZ_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st));
     YGZ_HIP(launch_stereo((const StereoJob *)(d + o_job), 1, nl, stereo_levels_of(P), mb, mbf, st));
     YGZ_HIP(hipMemcpyAsync(u_right, d + o_u, 4 * (size_t)nl, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipMemcpyAsync(depth, d + o_d, 4 * (size_t)nl, hipMemcpyDeviceToHost, st));

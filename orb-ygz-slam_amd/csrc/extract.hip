@@ -835,6 +835,33 @@ __device__ __forceinline__ int block_excl_scan(int v, int *red, int *total) {
     return off + incl - v;
 }
 
+// Runs of equal values across the lanes of a wave (lane order): the run's first
+// lane gets its length, every other lane 0.
+__device__ __forceinline__ int wave_run_length(int t) {
+    const int lane = lane_id();
+    const int prev = __shfl_up(t, 1, 64);
+    const uint64_t heads = __ballot(lane == 0 || prev != t);
+    if (!((heads >> lane) & 1)) return 0;
+    const uint64_t above = lane == 63 ? 0ull : heads >> (lane + 1);
+    return above ? __builtin_ctzll(above) + 1 : 64 - lane;
+}
+
+// The same, with the maximum of v over the run delivered to its first lane.
+__device__ __forceinline__ int wave_run_max(int t, uint32_t v, uint32_t &m) {
+    const int lane = lane_id();
+    const int prev = __shfl_up(t, 1, 64);
+    const uint64_t heads = __ballot(lane == 0 || prev != t);
+    const uint64_t above = lane == 63 ? 0ull : heads >> (lane + 1);
+    const int next = above ? lane + 1 + __builtin_ctzll(above) : 64;  // first lane of the next run
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t w = __shfl_down(v, o, 64);
+        if (lane + o < next) v = v > w ? v : w;
+    }
+    m = v;
+    return ((heads >> lane) & 1) ? next - lane : 0;
+}
+
 __device__ __forceinline__ int oct_quadrant(uint32_t key, uint32_t mid) {
     const int mx = (int)(mid & 0xFFFu), my = (int)((mid >> 12) & 0xFFFu);
     return (key_x(key) < mx ? 0 : 1) + (key_y(key) < my ? 0 : 2);
@@ -862,14 +889,19 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
         S.cq[i][1] = 0u;
     }
     __syncthreads();
-#pragma unroll 4
-    for (int j = tid; j < n; j += NT) {
-        const int i = nid[j];
-        const uint32_t md = S.mid[i];
-        if (md & (1u << 30)) {
-            const int q = oct_quadrant(K[j], md);
-            atomicAdd(&S.cq[i][q >> 1], 1u << ((q & 1) * 16));
+    // Keys come in cell order, so neighbouring lanes mostly hit the same (node,
+    // quadrant) counter: one LDS atomic per run of equal targets, by its first lane,
+    // instead of one same-address atomic per key.
+    for (int j0 = tid - (tid & 63); j0 < n; j0 += NT) {
+        const int j = j0 + (tid & 63);
+        int t = -1;
+        if (j < n) {
+            const int i = nid[j];
+            const uint32_t md = S.mid[i];
+            if (md & (1u << 30)) t = (i << 2) | oct_quadrant(K[j], md);
         }
+        const int run_len = wave_run_length(t);
+        if (run_len > 0 && t >= 0) atomicAdd(&S.cq[t >> 2][(t & 3) >> 1], (uint32_t)run_len << ((t & 1) * 16));
     }
     __syncthreads();
     // b) division order -> E (children created before this node's), Ctot
@@ -906,22 +938,28 @@ __device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, ui
                                    (uint64_t)i;
             nc += tot;
         }
-        int p2 = 1;
-        while (p2 < nc) p2 <<= 1;
-        if (p2 > NC) { overflow = 1; return; }
-        for (int i = nc + tid; i < p2; i += NT) S.sortk[i] = ~0ull;
+        // ascending order by rank: the keys are distinct (creation numbers are), so
+        // rank = number of smaller keys; every lane reads the same sortk[j] (LDS
+        // broadcast) -- one barrier instead of a bitonic network's log^2 stages
         __syncthreads();
-        for (int k = 2; k <= p2; k <<= 1)
-            for (int jj = k >> 1; jj > 0; jj >>= 1) {
-                for (int i = tid; i < p2; i += NT) {
-                    const int ixj = i ^ jj;
-                    if (ixj > i) {
-                        const uint64_t a = S.sortk[i], b = S.sortk[ixj];
-                        if ((a > b) == ((i & k) == 0)) { S.sortk[i] = b; S.sortk[ixj] = a; }
-                    }
-                }
-                __syncthreads();
-            }
+        constexpr int kPer = (NC + NT - 1) / NT;
+        uint64_t mine[kPer];
+        int rk[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; u++) {
+            mine[u] = tid + u * NT < nc ? S.sortk[tid + u * NT] : ~0ull;
+            rk[u] = 0;
+        }
+        for (int j = 0; j < nc; j++) {
+            const uint64_t v = S.sortk[j];
+#pragma unroll
+            for (int u = 0; u < kPer; u++) rk[u] += v < mine[u];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kPer; u++)
+            if (tid + u * NT < nc) S.sortk[rk[u]] = mine[u];
+        __syncthreads();
         // processing order p = 0..nc-1 is sortk[nc-1-p]; cut at the first p with size >= N
         if (tid == 0) S.scal[0] = nc;  // first p reaching N (nc: none)
         __syncthreads();
@@ -1143,8 +1181,14 @@ __device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const
     if (!overflow) {
         for (int i = tid; i < size; i += NT) S.cq[i][0] = 0u;
         __syncthreads();
-        for (int j = tid; j < n; j += NT)
-            atomicMax(&S.cq[nid[j]][0], ((uint32_t)key_score(K[j]) << 24) | (uint32_t)(0xFFFFFF - j));
+        for (int j0 = tid - (tid & 63); j0 < n; j0 += NT) {  // one atomic per run of equal nodes
+            const int j = j0 + (tid & 63);
+            const int t = j < n ? (int)nid[j] : -1;
+            const uint32_t v = j < n ? ((uint32_t)key_score(K[j]) << 24) | (uint32_t)(0xFFFFFF - j) : 0u;
+            uint32_t m;
+            const int run_len = wave_run_max(t, v, m);
+            if (run_len > 0 && t >= 0) atomicMax(&S.cq[t][0], m);
+        }
         __syncthreads();
         if (size > L.sel_cap) overflow = 1;
         for (int i = tid; i < size && i < L.sel_cap; i += NT) out[i] = K[0xFFFFFF - (S.cq[i][0] & 0xFFFFFFu)];

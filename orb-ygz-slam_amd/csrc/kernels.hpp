@@ -160,11 +160,16 @@ struct DirectItem {
     int32_t pad;
 };
 static_assert(sizeof(DirectItem) == 80, "DirectItem layout");
+// n_cache cache points (5-px coverage grid of grid_size, replayed in order) then
+// n_local local-map points (run only if the cache successes <= cache_hit_th);
+// hdr[0] = cache successes, hdr[1] = local phase ran
 hipError_t launch_search_direct(const uint8_t *const *ref_pyrs, const AlignLevels &lv, const uint8_t *cur_pyr,
                                 int nlevels, const float *scale, float inv_sigma2_1, const ygzfe_camera &cam,
-                                int n_points, int n_items, const int32_t *item_ptr, const void *items,
-                                const float *px_proj, float *px_item, uint8_t *ok_item, float border, float *px_out,
-                                int32_t *matched, hipStream_t st);
+                                int n_cache, int n_local, int n_items, const int32_t *item_ptr, const void *items,
+                                const float *px_proj, float *px_item, uint8_t *ok_item, float border, int grid_size,
+                                int cache_hit_th, float *px_out, int32_t *matched, int32_t *status, int32_t *hdr,
+                                hipStream_t st);
+constexpr int kDirectMaxGridCells = 65536 * 8 - 64;  // LDS bitmap of k_direct_replay (<= 64 KB)
 
 // slots.hip: offline sequence mode result slots
 hipError_t launch_pack_slots(const ygzfe_kp *kps, const uint8_t *desc, const int *counts, int kp_cap,

@@ -564,6 +564,36 @@ def search_direct_batch(ref_frames, cur_frame, cam, item_ptr, ref_index, kp_ref,
     return px_out, matched
 
 
+DIRECT_FAILED, DIRECT_MATCHED, DIRECT_GRID_SKIP, DIRECT_NOT_RUN = 0, 1, 2, 3
+
+
+def search_local_points_direct(ref_frames, cur_frame, cam, n_cache, item_ptr, ref_index, kp_ref, pt_ref, T_cr,
+                               px_proj, border=20.0, grid_size=5, cache_hit_th=150):
+    """Tracking::SearchLocalPointsDirect (Tracking.cc:2258-2410) whole: points [0, n_cache) are the
+    cache (5-px coverage grid, replayed in order), the rest the local-map points (searched only
+    when the cache gave <= cache_hit_th successes).  Returns (px_out float32[n,2], matched_item
+    int32[n], status int32[n] (DIRECT_*), cache_success, local_ran)."""
+    refs = (C.c_void_p * max(1, len(ref_frames)))(*[f.h.value for f in ref_frames])
+    item_ptr = np.ascontiguousarray(item_ptr, np.int32)
+    n = len(item_ptr) - 1
+    ref_index = np.ascontiguousarray(ref_index, np.int32)
+    kp_ref = np.ascontiguousarray(kp_ref, KP_DTYPE)
+    pt_ref = np.ascontiguousarray(pt_ref, np.float32).reshape(-1, 3)
+    T_cr = np.ascontiguousarray(T_cr, SE3_DTYPE)
+    px_proj = np.ascontiguousarray(px_proj, np.float32).reshape(-1, 2)
+    px_out = np.zeros((max(n, 0), 2), np.float32)
+    matched = np.zeros(max(n, 0), np.int32)
+    status = np.zeros(max(n, 0), np.int32)
+    cs, lr = C.c_int(), C.c_int()
+    _check(lib().ygzfe_search_local_points_direct(refs, len(ref_frames), cur_frame.h, C.byref(cam), int(n_cache),
+                                                  n - int(n_cache), _p(item_ptr), _p(ref_index), _p(kp_ref),
+                                                  _p(pt_ref), _p(T_cr), _p(px_proj), C.c_float(border), int(grid_size),
+                                                  int(cache_hit_th), _p(px_out), _p(matched), _p(status),
+                                                  C.byref(cs), C.byref(lr)),
+           "search_local_points_direct")
+    return px_out, matched, status, cs.value, bool(lr.value)
+
+
 class Batch:
     """Frames resident in HBM, one launch per stage (the bench / multi-GPU path)."""
 

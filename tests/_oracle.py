@@ -206,6 +206,32 @@ def fast10_scores(img, xs, ys, threshold, x0=0, y0=0):
     return out
 
 
+def fast10_pipeline(img, barrier, x0=0, y0=0, w=None, h=None, scalar=False):
+    """detect_sse2 + score + nonmax_3x3 in one pass (ygzo_fast10_detect_score_nms) -> (xs, ys, scores)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape
+    w = W - x0 if w is None else w
+    h = H - y0 if h is None else h
+    cap = w * h // 2 + 16
+    xs, ys, sc = np.zeros(cap, np.int16), np.zeros(cap, np.int16), np.zeros(cap, np.int32)
+    lib().ygzo_fast10_force_scalar(1 if scalar else 0)
+    try:
+        n = lib().ygzo_fast10_detect_score_nms(C.c_void_p(img.ctypes.data + y0 * W + x0), w, h, W, barrier, _p(xs),
+                                              _p(ys), _p(sc), cap)
+    finally:
+        lib().ygzo_fast10_force_scalar(0)
+    return xs[:n].copy(), ys[:n].copy(), sc[:n].copy()
+
+
+def bench_fast10(img, barrier, x0, y0, w, h, reps=20):
+    """The restated FAST-10 pipeline timed in C -> (kept corners, mean seconds)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    W = img.shape[1]
+    s = C.c_double()
+    n = lib().ygzo_bench_fast10(C.c_void_p(img.ctypes.data + y0 * W + x0), w, h, W, barrier, reps, C.byref(s))
+    return n, s.value
+
+
 def fast10_nonmax(xs, ys, scores):
     xs = np.ascontiguousarray(xs, np.int16)
     ys = np.ascontiguousarray(ys, np.int16)
@@ -293,6 +319,33 @@ def search_direct(orc, kf_levels, cur_levels, cam, item_ptr, ref_index, kps, pt_
                              T, _p(np.ascontiguousarray(px_proj, np.float32)), C.c_float(border), _p(px_out),
                              _p(matched))
     return px_out, matched
+
+
+def search_local_points_direct(orc, kf_levels, cur_levels, cam, n_cache, item_ptr, ref_index, kps, pt_ref, T_cr,
+                               px_proj, border=20.0, grid_size=5, cache_hit_th=150):
+    """Tracking::SearchLocalPointsDirect (Tracking.cc:2258-2410) whole ->
+    (px_out, matched, status, cache_success, local_ran)."""
+    nl = len(cur_levels)
+    flat = [l for lv in kf_levels for l in lv]
+    rp = (C.c_void_p * max(1, len(flat)))(*[l.ctypes.data for l in flat])
+    cp = (C.c_void_p * MAXL)(*[l.ctypes.data for l in cur_levels])
+    lw = (C.c_int * MAXL)(*[l.shape[1] for l in cur_levels])
+    lh = (C.c_int * MAXL)(*[l.shape[0] for l in cur_levels])
+    sc = (C.c_float * MAXL)(*orc.scale.tolist())
+    isc = (C.c_float * MAXL)(*orc.inv_scale.tolist())
+    item_ptr = np.ascontiguousarray(item_ptr, np.int32)
+    n = len(item_ptr) - 1
+    T = (SE3 * max(1, len(T_cr)))(*[se3_from(r["q"], r["t"]) for r in T_cr])
+    px_out = np.zeros((max(n, 0), 2), np.float32)
+    matched = np.zeros(max(n, 0), np.int32)
+    status = np.zeros(max(n, 0), np.int32)
+    lr = C.c_int()
+    cs = lib().ygzo_search_local_points_direct(
+        C.byref(cam), rp, cp, lw, lh, nl, sc, isc, C.c_float(orc.inv_sigma2[1]), int(n_cache), n - int(n_cache),
+        _p(item_ptr), _p(np.ascontiguousarray(ref_index, np.int32)), _p(np.ascontiguousarray(kps, KP_DTYPE)),
+        _p(np.ascontiguousarray(pt_ref, np.float32)), T, _p(np.ascontiguousarray(px_proj, np.float32)),
+        C.c_float(border), int(grid_size), int(cache_hit_th), _p(px_out), _p(matched), _p(status), C.byref(lr))
+    return px_out, matched, status, cs, bool(lr.value)
 
 
 def stereo_matches(orc, left_levels, right_levels, kl, dl, kr, dr, mb, mbf):
@@ -431,6 +484,15 @@ class RefFast:
     @staticmethod
     def available():
         return os.path.exists(REF_FAST_PATH)
+
+    def pipeline_bench(self, img, barrier, x0, y0, w, h, reps=20):
+        """The reference's detect_sse2 + score + nonmax_3x3, timed in C++ -> (kept corners, mean seconds)."""
+        img = np.ascontiguousarray(img, np.uint8)
+        W = img.shape[1]
+        s = C.c_double()
+        n = self.lib.ref_fast10_pipeline_bench(C.c_void_p(img.ctypes.data + y0 * W + x0), w, h, W, barrier, reps,
+                                               C.byref(s))
+        return n, s.value
 
     def detect(self, img, barrier, sse=True, x0=0, y0=0, w=None, h=None, cap=1 << 20):
         img = np.ascontiguousarray(img, np.uint8)

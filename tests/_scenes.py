@@ -110,14 +110,16 @@ def project(cam, q_cw, t_cw, Pw):
     return np.stack([fx * Pc[:, 0] / Pc[:, 2] + cx, fy * Pc[:, 1] / Pc[:, 2] + cy], 1), Pc
 
 
-def direct_scene(seed, n_kf=4, max_obs=5, W=752, H=480, nlevels=4, scale_factor=2.0, n_points=None):
+def direct_scene(seed, n_kf=4, max_obs=5, W=752, H=480, nlevels=4, scale_factor=2.0, n_points=None, cluster=0):
     """SearchLocalPointsDirect inputs (Tracking.cc:2258-2410) on the textured plane.
 
     n_kf keyframes around the origin and a current frame moved by motion(seed).
     Map points = plane points under keyframe 0's pixel grid; each point is observed
     by a random ordered subset (0..max_obs) of the keyframes, its keypoint there =
     the point's projection with a random octave.  px_proj = the projection into the
-    current frame + U(-1.5, 1.5) px (isInFrustum's prediction).  Returns a dict of
+    current frame + U(-1.5, 1.5) px (isInFrustum's prediction).  cluster = k adds k
+    neighbours within +-1.2 px after every grid point (consecutive points then share
+    cells of SearchLocalPointsDirect's 5-px coverage grid).  Returns a dict of
     images, poses and the CSR item arrays of ygzfe.search_direct_batch."""
     rng = np.random.default_rng(1000 + seed)
     sc = PlaneScene(seed, W, H)
@@ -135,6 +137,9 @@ def direct_scene(seed, n_kf=4, max_obs=5, W=752, H=480, nlevels=4, scale_factor=
     uv = np.stack([gx.ravel(), gy.ravel()], 1).astype(np.float64) + rng.uniform(-3, 3, (gx.size, 2))
     if n_points is not None:
         uv = uv[rng.permutation(len(uv))[:n_points]]
+    if cluster:
+        uv = np.concatenate([uv[:, None, :], uv[:, None, :] + rng.uniform(-1.2, 1.2, (len(uv), cluster, 2))],
+                            1).reshape(-1, 2)
     Pw = backproject_plane_np(sc.cam, poses[0], uv)
     n = len(Pw)
     px_cur, _ = project(sc.cam, qc, tc, Pw)

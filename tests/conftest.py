@@ -27,3 +27,15 @@ def gpu():
     if n <= 0:
         pytest.fail("no HIP device visible: -m gpu tests must run on the GPU box (no CPU fallback exists)")
     return ygzfe
+
+
+# headline-path parity first, so a -x stop reports the §8a rows before the §8f ones
+_ORDER = ["test_gpu_extract.py", "test_gpu_extract_split.py", "test_gpu_align.py", "test_gpu_align_batch.py",
+          "test_gpu_match.py", "test_gpu_match_search.py", "test_gpu_dropin.py", "test_gpu_compat.py"]
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def rank(item):
+        name = os.path.basename(str(item.fspath))
+        return _ORDER.index(name) if name in _ORDER else len(_ORDER)
+    items.sort(key=rank)  # stable: file-internal order kept

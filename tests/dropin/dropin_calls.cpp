@@ -14,8 +14,11 @@
 //   Tracking.cc:1662,1674  matcher.SearchByProjection(mCurrentFrame, mvpLocalMapPoints, th, false)
 //   Tracking.cc:1018-1020  matcher.SearchByBoW(mpReferenceKF, mCurrentFrame, vpMapPointMatches)
 //   ORBmatcher.cc:1598-1599 ygz::Align2D(curr->mvImagePyramid[search_level], _patch_with_border, ...)
+//   Tracking.cc:2201        SearchLocalPointsDirect();   (body: compat/dropin/Tracking_direct_gpu.inc)
+//   Tracking.cc:2294        matcher.FindDirectProjection(o.first, &mCurrentFrame, mp, px_curr, level)
 //
 // Prints one line per check; exit 0 and "OK" when every check passes.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -27,6 +30,7 @@
 #include "ORBmatcher.h"
 #include "ORBmatcherGPU.h"
 #include "SparseImageAlign.h"
+#include "TrackingDirectGPU.h"
 #include "ygz_oracle.h"
 
 namespace ygz {
@@ -53,6 +57,38 @@ struct Tracking {
     std::vector<MapPoint *> mvpLocalMapPoints;
     KeyFrame *mpReferenceKF = nullptr;
     int mSensor = System::MONOCULAR;
+    // SearchLocalPointsDirect state (Tracking.h:245-248, 282)
+    set<MapPoint *> mvpDirectMapPointsCache;
+    int mnCacheHitTh = 150;
+    KeyFrame *mpLastKeyFrame = nullptr;
+    std::vector<MapPoint *> mvpNextLocalMapPoints;  // what the UpdateLocalMap stub installs
+    int nUpdateLocalMap = 0;
+    void UpdateLocalMap() {
+        mvpLocalMapPoints = mvpNextLocalMapPoints;
+        nUpdateLocalMap++;
+    }
+    void SearchLocalPointsDirect();
+    void TrackLocalMapDirect() {  // Tracking.cc:2191-2201, the call line verbatim
+        SearchLocalPointsDirect();
+    }
+    // Tracking.cc:2412-2432 verbatim
+    vector<std::pair<KeyFrame *, size_t> >
+    SelectNearestKeyframe(const std::map<KeyFrame *, size_t> &observations, int n) {
+        vector<std::pair<KeyFrame *, size_t> > s;
+        for (auto &o: observations) {
+            if (!o.first->isBad() && o.first != mpLastKeyFrame)
+                s.push_back(make_pair(o.first, o.second));
+        }
+        sort(s.begin(), s.end(),
+             [](const pair<KeyFrame *, size_t> &p1, const pair<KeyFrame *, size_t> &p2) {
+                 return p1.first->mnId > p2.first->mnId;
+             });
+
+        if ((int) s.size() < n)
+            return s;
+        else
+            return vector<std::pair<KeyFrame *, size_t> >(s.begin(), s.begin() + n);
+    }
 
     Tracking(int nFeatures, float fScaleFactor, int nLevels, int fIniThFAST, int fMinThFAST) {
         mpORBextractorLeft = new ORBextractor(nFeatures, fScaleFactor, nLevels, fIniThFAST, fMinThFAST);
@@ -90,6 +126,7 @@ struct Tracking {
         return nmatches;
     }
 };
+#include "Tracking_direct_gpu.inc"
 }  // namespace ygz
 
 using namespace ygz;
@@ -421,6 +458,207 @@ int main() {
         CHECK(tried >= 20 && same == tried && conv > tried / 2,
               "ygz::Align2D(curr->mvImagePyramid[search_level], ...): %d / %d bit-exact with the oracle, %d converged",
               same, tried, conv);
+    }
+
+    // ---------------------------------------------------------------- SearchLocalPointsDirect + FindDirectProjection
+    {
+        // three keyframes of the plane: A = the last frame (identity pose), B and C shifted images
+        // (image shift (dx, dy) <=> T_cw translation (dx Z / fx, dy Z / fy, 0)); C is mpLastKeyFrame,
+        // which SelectNearestKeyframe leaves out
+        const int shifts[3][2] = {{0, 0}, {-1, 1}, {3, 2}};
+        const cv::Mat kim[3] = {im0, synth(W, H, 7u, -1, 1), synth(W, H, 7u, 3, 2)};
+        std::vector<KeyFrame> kfs(3);
+        std::vector<Frame> kframes;
+        kframes.reserve(3);
+        for (int k = 0; k < 3; k++) {
+            kframes.push_back(Frame(kim[k], T.mpORBextractorLeft));
+            kfs[k].mvImagePyramid = kframes[k].mvImagePyramid;  // shared, as KeyFrame.cc:257-260
+            kfs[k].mvScaleFactors = kframes[k].mvScaleFactors;
+            kfs[k].mTcw = SE3f(Eigen::Quaternionf(), Vector3f(shifts[k][0] * Z / Frame::fx, shifts[k][1] * Z / Frame::fy, 0.f));
+            kfs[k].mnId = 10 + k;
+        }
+        T.mpLastKeyFrame = &kfs[2];
+        // map points: the last frame's keypoints on the plane, plus a neighbour 0.6 px away after every
+        // third one (neighbours share cells of the 5-px coverage grid)
+        const Frame &L = T.mLastFrame;
+        std::vector<MapPoint> dm;
+        dm.reserve(2 * L.N);
+        for (int i = 0; i < L.N; i++) {
+            for (int c = 0; c < 1 + (i % 3 == 0); c++) {
+                const cv::KeyPoint &kp = L.mvKeys[i];
+                MapPoint mp;
+                const float u = kp.pt.x + 0.6f * c, v = kp.pt.y - 0.4f * c;
+                mp.mWorldPos = Vector3f((u - Frame::cx) / Frame::fx * Z, (v - Frame::cy) / Frame::fy * Z, Z);
+                mp.mbBad = (dm.size() % 23) == 11;
+                dm.push_back(mp);
+            }
+        }
+        for (size_t j = 0; j < dm.size(); j++) {
+            MapPoint &mp = dm[j];
+            const int oc = (int)(j % 3);
+            for (int k = 0; k < 3; k++) {
+                if (k == 0 && j % 5 == 1) continue;  // observed by B / C only
+                if (k == 1 && j % 4 == 2) continue;
+                const Vector3f pc = kfs[k].mTcw * mp.mWorldPos;
+                cv::KeyPoint kp(cv::Point2f(Frame::fx * pc[0] / pc[2] + Frame::cx, Frame::fy * pc[1] / pc[2] + Frame::cy),
+                                31.f * kfs[k].mvScaleFactors[oc], -1, 0, oc);
+                mp.mObservations[&kfs[k]] = kfs[k].mvKeys.size();
+                kfs[k].mvKeys.push_back(kp);
+            }
+        }
+        // the frame being tracked: no features yet (TrackLocalMapDirect, Tracking.cc:2194), pose = TCR
+        T.mCurrentFrame = Frame(im1, T.mpORBextractorLeft);
+        T.mCurrentFrame.SetPose(TCR);
+        Frame &C = T.mCurrentFrame;
+        const cv::Mat cur_level0 = C.mvImagePyramid[0];
+
+        // expected: the oracle over the same filters and items (ORBmatcher.cc:1577-1582 inputs formed here)
+        uint8_t *cp[YGZO_MAX_LEVELS];
+        for (int l = 0; l < nl; l++) cp[l] = C.mvImagePyramid[l].data;
+        std::vector<uint8_t *> rp(3 * nl);
+        for (int k = 0; k < 3; k++)
+            for (int l = 0; l < nl; l++) rp[k * nl + l] = kfs[k].mvImagePyramid[l].data;
+        ygzo_cam ocam{Frame::fx, Frame::fy, Frame::cx, Frame::cy};
+        struct Want {
+            std::vector<cv::KeyPoint> keys;
+            std::vector<MapPoint *> mps;
+            std::vector<int> from;
+            std::set<MapPoint *> cache;
+            int local_runs = 0;
+        };
+        auto run_oracle_phase = [&](const std::vector<MapPoint *> &pts, int n_cache, int th, Want &w,
+                                    std::vector<int> &status) {
+            std::vector<int32_t> ip(1, 0), ri;
+            std::vector<ygzo_kp> ok;
+            std::vector<float> pt, proj;
+            std::vector<ygzo_se3> tcr;
+            std::vector<long> ids;
+            for (MapPoint *mp : pts) {
+                proj.push_back(mp->mTrackProjX);
+                proj.push_back(mp->mTrackProjY);
+                for (auto &ob : T.SelectNearestKeyframe(mp->GetObservations(), 5)) {
+                    const SE3f pose_ref = ob.first->GetPose();
+                    const Vector3f p = pose_ref * mp->GetWorldPos();
+                    const SE3f Tcr = C.mTcw * pose_ref.inverse();
+                    ri.push_back((int)(ob.first - &kfs[0]));
+                    ok.push_back(*reinterpret_cast<const ygzo_kp *>(&ob.first->mvKeys[ob.second]));
+                    for (int q = 0; q < 3; q++) pt.push_back(p[q]);
+                    tcr.push_back(ygzo_se3{{Tcr.unit_quaternion().x(), Tcr.unit_quaternion().y(),
+                                            Tcr.unit_quaternion().z(), Tcr.unit_quaternion().w()},
+                                           {Tcr.translation()[0], Tcr.translation()[1], Tcr.translation()[2]}});
+                    ids.push_back((long)ob.first->mnId);
+                }
+                ip.push_back((int32_t)ri.size());
+            }
+            const int n = (int)pts.size();
+            std::vector<float> px(2 * n + 2);
+            std::vector<int> m(n + 1);
+            status.assign(n + 1, 0);
+            int ran = 0;
+            const int cs = ygzo_search_local_points_direct(&ocam, rp.data(), cp, lw, lh, nl, o.scale, o.inv_scale,
+                                                           o.inv_sigma2[1], n_cache, n - n_cache, ip.data(), ri.data(),
+                                                           ok.data(), pt.data(), tcr.data(), proj.data(), 20.f, 5, th,
+                                                           px.data(), m.data(), status.data(), &ran);
+            for (int i = 0; i < n; i++)
+                if (status[i] == 1) {
+                    w.keys.push_back(cv::KeyPoint(cv::Point2f(px[2 * i], px[2 * i + 1]), 7, -1, 0, 0));
+                    w.mps.push_back(pts[i]);
+                    w.from.push_back((int)ids[m[i]]);
+                }
+            return cs;
+        };
+        // Tracking.cc:2258-2410 restated over the oracle: cache filters, cache phase, mnCacheHitTh,
+        // UpdateLocalMap, local filters, local phase
+        auto expected = [&](const std::set<MapPoint *> &cache0, const std::vector<MapPoint *> &local, int th) {
+            Want w;
+            w.cache = cache0;
+            std::vector<MapPoint *> pts;
+            for (auto it = w.cache.begin(); it != w.cache.end();) {
+                if ((*it)->isBad() || !C.isInFrustum(*it, 0.5)) { it = w.cache.erase(it); continue; }
+                pts.push_back(*it);
+                ++it;
+            }
+            std::vector<int> st;
+            const int cnt = run_oracle_phase(pts, (int)pts.size(), th, w, st);
+            for (size_t i = 0; i < pts.size(); i++)
+                if (st[i] == 0) w.cache.erase(pts[i]);
+            if (cnt > th) return w;
+            w.local_runs = 1;
+            pts.clear();
+            for (MapPoint *mp : local) {
+                if (w.cache.count(mp) || mp->isBad() || !C.isInFrustum(mp, 0.5)) continue;
+                pts.push_back(mp);
+            }
+            const size_t before = w.mps.size();
+            run_oracle_phase(pts, 0, th, w, st);
+            for (size_t i = before; i < w.mps.size(); i++) w.cache.insert(w.mps[i]);
+            return w;
+        };
+        std::set<MapPoint *> cache0;
+        std::vector<MapPoint *> local;
+        for (size_t j = 0; j < dm.size(); j++) {
+            if (j % 2 == 0) cache0.insert(&dm[j]);
+            local.push_back(&dm[j]);
+        }
+        for (int th : {1 << 30, 150}) {
+            const Want w = expected(cache0, local, th);
+            C.mvKeys.clear();
+            C.mvpMapPoints.clear();
+            C.mvDepth.clear();
+            C.mvbOutlier.clear();
+            C.mvMatchedFrom.clear();
+            C.N = 0;
+            T.mvpDirectMapPointsCache = cache0;
+            T.mvpLocalMapPoints.clear();
+            T.mvpNextLocalMapPoints = local;
+            T.mnCacheHitTh = th;
+            T.nUpdateLocalMap = 0;
+            T.TrackLocalMapDirect();
+            bool same = (size_t)C.N == w.keys.size() && C.mvKeys.size() == w.keys.size() &&
+                        C.mvpMapPoints == w.mps && C.mvMatchedFrom == w.from &&
+                        T.mvpDirectMapPointsCache == w.cache && T.nUpdateLocalMap == w.local_runs &&
+                        (int)C.mvuRight.size() == C.N && C.mvDepth.size() == w.keys.size();
+            for (size_t i = 0; same && i < w.keys.size(); i++)
+                same = C.mvKeys[i].pt.x == w.keys[i].pt.x && C.mvKeys[i].pt.y == w.keys[i].pt.y &&
+                       C.mvKeys[i].size == 7.f && C.mvKeys[i].angle == -1.f;
+            CHECK(same && w.keys.size() > 100,
+                  "SearchLocalPointsDirect() [mnCacheHitTh %d]: %zu points tracked (oracle %zu), local map %s, "
+                  "cache %zu -> %zu", th, C.mvKeys.size(), w.keys.size(), w.local_runs ? "searched" : "skipped",
+                  cache0.size(), T.mvpDirectMapPointsCache.size());
+        }
+
+        // ORBmatcher::FindDirectProjection, one pair at a time, against the oracle
+        ORBmatcher matcher;
+        int tried = 0, same = 0, conv = 0;
+        for (size_t j = 0; j < dm.size() && tried < 40; j += 13) {
+            MapPoint *mp = &dm[j];
+            if (!C.isInFrustum(mp, 0.5)) continue;
+            for (auto &ob : T.SelectNearestKeyframe(mp->GetObservations(), 5)) {
+                Vector2f px_curr(mp->mTrackProjX, mp->mTrackProjY);
+                int level = mp->mnTrackScaleLevel;
+                const bool ok = matcher.FindDirectProjection(ob.first, &T.mCurrentFrame, mp, px_curr, level);
+                const SE3f pose_ref = ob.first->GetPose();
+                const Vector3f p = pose_ref * mp->GetWorldPos();
+                const SE3f Tcr = C.mTcw * pose_ref.inverse();
+                const ygzo_se3 ot{{Tcr.unit_quaternion().x(), Tcr.unit_quaternion().y(), Tcr.unit_quaternion().z(),
+                                   Tcr.unit_quaternion().w()},
+                                  {Tcr.translation()[0], Tcr.translation()[1], Tcr.translation()[2]}};
+                const float pref[3] = {p[0], p[1], p[2]};
+                float opx[2] = {mp->mTrackProjX, mp->mTrackProjY};
+                int osl = 0;
+                const int k = (int)(ob.first - &kfs[0]);
+                const int ook = ygzo_find_direct_projection(
+                    &ocam, &rp[k * nl], lw, lh, cp, lw, lh, nl, o.scale, o.inv_scale, o.inv_sigma2[1], &ot, pref,
+                    reinterpret_cast<const ygzo_kp *>(&ob.first->mvKeys[ob.second]), opx, &osl);
+                tried++;
+                same += (int)ok == ook && level == osl && px_curr[0] == opx[0] && px_curr[1] == opx[1];
+                conv += ok;
+            }
+        }
+        CHECK(tried >= 20 && same == tried && conv > tried / 2,
+              "matcher.FindDirectProjection(ob.first, &mCurrentFrame, mp, px_curr, level): %d / %d bit-exact, "
+              "%d converged", same, tried, conv);
+        (void)cur_level0;
     }
 
     std::printf(fails ? "FAILED %d\n" : "OK\n", fails);

@@ -42,6 +42,7 @@ public:
         mbFeatureExtracted = true;
     }
     void SetPose(const SE3f &Tcw) { mTcw = Tcw; }
+    bool isInFrustum(MapPoint *pMP, float viewingCosLimit);  // defined in the MapPoint.h stub
 
     static float fx, fy, cx, cy, invfx, invfy;
     static float mnMinX, mnMaxX, mnMinY, mnMaxY;
@@ -52,6 +53,7 @@ public:
     cv::Mat mDescriptors, mDescriptorsRight;
     std::vector<MapPoint *> mvpMapPoints;
     std::vector<bool> mvbOutlier;
+    std::vector<int> mvMatchedFrom;
     DBoW2::FeatureVector mFeatVec;
     SE3f mTcw;
     std::vector<cv::Mat> mvImagePyramid;

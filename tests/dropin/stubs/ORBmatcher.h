@@ -1,5 +1,5 @@
 // Test stub of the reference's ORBmatcher.h: the constructor, the members and
-// the declarations of the five tracking-path searches with the reference's
+// the declarations of the five tracking-path searches and FindDirectProjection with the reference's
 // signatures (ORBmatcher.h:38-142).  Written for the test.
 #pragma once
 #include "Common.h"
@@ -20,6 +20,7 @@ public:
     int SearchByBoW(KeyFrame *pKF, Frame &F, std::vector<MapPoint *> &vpMapPointMatches);
     int SearchForInitialization(Frame &F1, Frame &F2, std::vector<cv::Point2f> &vbPrevMatched,
                                 std::vector<int> &vnMatches12, int windowSize = 10);
+    bool FindDirectProjection(KeyFrame *ref, Frame *curr, MapPoint *mp, Vector2f &px_curr, int &search_level);
     static const int TH_LOW;
     static const int TH_HIGH;
     static const int HISTO_LENGTH;

@@ -81,3 +81,23 @@ def test_live_reference_random_frames():
             assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
             sa = ref.scores(img, a[0], a[1], th, x0=3, y0=3)
             assert np.array_equal(sa, O.fast10_scores(img, a[0], a[1], th, x0=3, y0=3))
+
+
+@pytest.mark.parametrize("name", IMAGES)
+@pytest.mark.parametrize("th", THRESHOLDS)
+def test_fast10_vector_pipeline(name, th):
+    """The 16-pixel vector FAST-10 (detect + score + dense-map 3x3 NMS, the CPU baseline's
+    path) == the scalar restatement == the reference library's survivors and scores."""
+    img = image(name)
+    H, W = img.shape
+    xy, sc, keep = FIX[f"{name}/t{th}/s1/xy"], FIX[f"{name}/t{th}/score"], FIX[f"{name}/t{th}/keep"]
+    for scalar in (False, True):
+        xs, ys, s = O.fast10_pipeline(img, th, x0=3, y0=3, w=W - 6, h=H - 6, scalar=scalar)
+        assert np.array_equal(np.stack([xs, ys], 1).astype(np.int16), xy[keep]), (name, th, scalar)
+        assert np.array_equal(s, sc[keep]), (name, th, scalar)
+    O.lib().ygzo_fast10_force_scalar(1)
+    try:
+        xs1, ys1 = O.fast10_detect(img, th, sse=True, x0=3, y0=3, w=W - 6, h=H - 6)
+    finally:
+        O.lib().ygzo_fast10_force_scalar(0)
+    assert np.array_equal(np.stack([xs1, ys1], 1).astype(np.int16), xy)

@@ -279,3 +279,54 @@ def test_bow_oracle_matches_python_restatement(scoring, weighting):
     assert bv.tolist() == vals
     assert fn.tolist() == [n for n in sorted(fv) for _ in fv[n]]
     assert ff.tolist() == [i for n in sorted(fv) for i in fv[n]]
+
+
+def _replay_local_points_direct(first, proj, n_cache, W, H, grid_size, th):
+    """Tracking.cc:2258-2410 in Python over per-point first successes (item, px) or None."""
+    gr, gc = H // grid_size, W // grid_size
+    grid = np.zeros(gr * gc, bool)
+    status, cnt = [], 0
+    for i in range(n_cache):
+        k = int(np.float32(proj[i, 1]) / np.float32(grid_size)) * gc + int(np.float32(proj[i, 0]) / np.float32(grid_size))
+        if 0 <= k < len(grid) and grid[k]:
+            status.append(2)
+            continue
+        if first[i] is None:
+            status.append(0)
+            continue
+        status.append(1)
+        cnt += 1
+        px = first[i][1]
+        k = int(px[1] / np.float32(grid_size)) * gc + int(px[0] / np.float32(grid_size))
+        grid[k] = True
+    ran = not cnt > th
+    for i in range(n_cache, len(proj)):
+        status.append(3 if not ran else (1 if first[i] is not None else 0))
+    return np.array(status), cnt, ran
+
+
+def test_search_local_points_direct_replays_the_grid():
+    """ygzo_search_local_points_direct == the per-point first success (ygzo_search_direct) replayed
+    through Tracking.cc:2258-2410's coverage grid and mnCacheHitTh rule, on clustered points."""
+    import _scenes as S
+    d = S.direct_scene(6, n_kf=2, max_obs=2, n_points=40, cluster=2)
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    kl = [orc.pyramid(im) for im in d["kf_images"]]
+    cl = orc.pyramid(d["cur_image"])
+    cam = O.Cam(*d["scene"].cam)
+    args = (d["item_ptr"], d["ref_index"], d["kps"], d["pt_ref"], d["T_cr"], d["px_proj"])
+    px1, m1 = O.search_direct(orc, kl, cl, cam, *args)
+    first = [(m1[i], px1[i]) if m1[i] >= 0 else None for i in range(len(m1))]
+    n = len(m1)
+    n_cache = (2 * n) // 3
+    for th in (10 ** 6, 3, -1):
+        px, m, st, cs, ran = O.search_local_points_direct(orc, kl, cl, cam, n_cache, *args, cache_hit_th=th)
+        want, wcnt, wran = _replay_local_points_direct(first, d["px_proj"], n_cache, W, H, 5, th)
+        assert np.array_equal(st, want), th
+        assert cs == wcnt and ran == wran
+        ok = st == 1
+        assert np.array_equal(m[ok], m1[ok]) and np.array_equal(px[ok], px1[ok])
+        assert (m[~ok] == -1).all() and (px[~ok] == 0).all()
+    assert (want[:n_cache] == 2).mean() >= 0.1
+    assert ((want[:n_cache] == 1).sum() > 3) and (want[n_cache:] == 3).all()

@@ -212,3 +212,39 @@ def test_search_direct_batch_edges(gpu):
         bad[:] = 7
         gpu.search_direct_batch(kf_fr, cur_fr, cam, d["item_ptr"], bad, d["kps"], d["pt_ref"], d["T_cr"],
                                 d["px_proj"])
+
+
+@pytest.mark.parametrize("seed", [0, 2])
+def test_search_local_points_direct_grid_bitexact(gpu, seed):
+    """Tracking::SearchLocalPointsDirect whole (Tracking.cc:2258-2410): the cache phase with the
+    5-px coverage grid replayed in order (clustered projections: >= 10 % of the cache points are
+    grid-skipped), mnCacheHitTh, then the local-map phase.  matched_item, px, status (hence the
+    mvKeys / mvMatchedFrom order) and the counts bit-exact with the oracle."""
+    d = S.direct_scene(seed, n_kf=4, max_obs=5, cluster=2)
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    ex = gpu.ORBextractor(nf, sf, nl, ini, mn)
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    kf_fr = [ex.ComputePyramid(im) for im in d["kf_images"]]
+    cur_fr = ex.ComputePyramid(d["cur_image"])
+    kl = [orc.pyramid(im) for im in d["kf_images"]]
+    cl = orc.pyramid(d["cur_image"])
+    cam = d["scene"].camera()
+    args = (d["item_ptr"], d["ref_index"], d["kps"], d["pt_ref"], d["T_cr"], d["px_proj"])
+    n = len(d["item_ptr"]) - 1
+    n_cache = (3 * n) // 5
+    seen = set()
+    for th in (10 ** 6, 150, 20):
+        px, m, st, cs, ran = gpu.search_local_points_direct(kf_fr, cur_fr, cam, n_cache, *args, cache_hit_th=th)
+        opx, om, ost, ocs, oran = O.search_local_points_direct(orc, kl, cl, O.Cam(*d["scene"].cam), n_cache, *args,
+                                                               cache_hit_th=th)
+        assert np.array_equal(st, ost), th
+        assert np.array_equal(m, om) and np.array_equal(px, opx), th
+        assert (cs, ran) == (ocs, oran), th
+        seen.add(ran)
+        assert (st[:n_cache] == gpu.DIRECT_GRID_SKIP).mean() >= 0.1
+        assert (st[n_cache:] != gpu.DIRECT_GRID_SKIP).all()
+    assert seen == {True, False}
+    # the local-map-only form is the same replay with no cache points
+    px, m = gpu.search_direct_batch(kf_fr, cur_fr, cam, *args)
+    opx, om, ost, _, _ = O.search_local_points_direct(orc, kl, cl, O.Cam(*d["scene"].cam), 0, *args)
+    assert np.array_equal(m, om) and np.array_equal(px, opx)

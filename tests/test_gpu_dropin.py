@@ -20,5 +20,6 @@ def test_reference_call_sites_compile_and_match_the_oracle(gpu):
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().endswith("OK")
     for line in ("mpAlign->run(&mLastFrame, &mCurrentFrame, TCR)", "DSO_KEYPOINT", "ORBSLAM_KEYPOINT",
-                 "SearchForInitialization", "SearchByBoW", "ygz::Align2D"):
+                 "SearchForInitialization", "SearchByBoW", "ygz::Align2D", "SearchLocalPointsDirect() [mnCacheHitTh 150]",
+                 "SearchLocalPointsDirect() [mnCacheHitTh 1073741824]", "matcher.FindDirectProjection"):
         assert line in r.stdout
