@@ -1077,19 +1077,79 @@ __global__ __launch_bounds__(256) void k_align2d(const uint8_t *__restrict__ img
     conv[i] = (uint8_t)ok;
 }
 
-// One Align2D on a window of a host level (the drop-in Align2D(const cv::Mat&, ...)):
+// One Align2D on a window of a host level (the drop-in Align2D(const cv::Mat&, ...)),
+// by one wave: lane i owns pixel i of the 8x8 patch (its gradient, bilinear
+// sample, residual and the three products), and every lane then folds the 64
+// products of an iteration in the reference's pixel order (LDS broadcast reads),
+// so the sums are the sequential ones of Align.cc:74-96 bit for bit.
 // status 0 / 1 = converged flag, -1 = the window was too small.
-__global__ void k_align2d_window(const uint8_t *__restrict__ win, int stride, int w, int h, int x0, int y0, int ww,
-                                 int wh, const uint8_t *__restrict__ pwb, const uint8_t *__restrict__ p, int n_iter,
-                                 float *__restrict__ px, int *__restrict__ status) {
-    if (threadIdx.x != 0) return;
-    float q[2] = {px[0], px[1]};
-    const int r = align2d_lane(win, stride, w, h, x0, y0, ww, wh, pwb, p, n_iter, q);
-    if (r >= 0) {
-        px[0] = q[0];
-        px[1] = q[1];
+__global__ __launch_bounds__(64) void k_align2d_window(const uint8_t *__restrict__ win, int stride, int w, int h,
+                                                       int x0, int y0, int ww, int wh,
+                                                       const uint8_t *__restrict__ pwb,
+                                                       const uint8_t *__restrict__ p, int n_iter,
+                                                       float *__restrict__ px, int *__restrict__ status) {
+    __shared__ float sj[2][64], sp[3][64];
+    const int lane = threadIdx.x, y = lane >> 3, x = lane & 7;
+    const int hp = 4, step = 10;
+    // reference gradients (Align.cc:37-64): 0.5 * central difference in double, to float
+    const uint8_t *it = pwb + (y + 1) * step + 1 + x;
+    const float J0 = (float)(0.5 * (it[1] - it[-1]));
+    const float J1 = (float)(0.5 * (it[step] - it[-step]));
+    const float refp = (float)p[lane];
+    sj[0][lane] = J0;
+    sj[1][lane] = J1;
+    __syncthreads();
+    float H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 64; i++) {  // H += J J^T in pixel order (Align.cc:58-63)
+        const float J[3] = {sj[0][i], sj[1][i], 1.f};
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) H[r * 3 + c] += J[r] * J[c];
     }
-    status[0] = r;
+    float Hi[9];
+    inverse3(H, Hi);
+    float mean_diff = 0.f, u = px[0], v = px[1];
+    const float min_upd2 = (float)(0.03 * 0.03);
+    int converged = 0, st = 0;
+    for (int iter = 0; iter < n_iter; ++iter) {
+        const int ur = (int)floorf(u), vr = (int)floorf(v);
+        if (ur < hp || vr < hp || ur >= w - hp || vr >= h - hp) break;
+        if (isnan(u) || isnan(v)) { st = -2; break; }  // Align.cc:63-65: false, estimate untouched
+        if (ur - hp < x0 || vr - hp < y0 || ur + hp >= x0 + ww || vr + hp >= y0 + wh) { st = -1; break; }
+        const float sx = u - ur, sy = v - vr;
+        const float wTL = wmul(1.0 - sx, 1.0 - sy), wTR = wmul(sx, 1.0 - sy);
+        const float wBL = wmul(1.0 - sx, sy), wBR = wmul(sx, sy);
+        const uint8_t *q = win + (size_t)(vr + y - hp - y0) * stride + (ur - hp - x0) + x;
+        const float spx = wTL * q[0] + wTR * q[1] + wBL * q[stride] + wBR * q[stride + 1];
+        const float res = spx - refp + mean_diff;
+        __syncthreads();  // the previous iteration's folds are done reading sp
+        sp[0][lane] = res * J0;
+        sp[1][lane] = res * J1;
+        sp[2][lane] = res;
+        __syncthreads();
+        float Jr0 = 0.f, Jr1 = 0.f, Jr2 = 0.f;
+        for (int i = 0; i < 64; i++) {
+            Jr0 -= sp[0][i];
+            Jr1 -= sp[1][i];
+            Jr2 -= sp[2][i];
+        }
+        const float u0 = Hi[0] * Jr0 + Hi[1] * Jr1 + Hi[2] * Jr2;
+        const float u1 = Hi[3] * Jr0 + Hi[4] * Jr1 + Hi[5] * Jr2;
+        const float u2 = Hi[6] * Jr0 + Hi[7] * Jr1 + Hi[8] * Jr2;
+        u += u0;
+        v += u1;
+        mean_diff += u2;
+        if (u0 * u0 + u1 * u1 < min_upd2) { converged = 1; break; }
+    }
+    if (lane == 0) {
+        if (st == 0) {
+            px[0] = u;
+            px[1] = v;
+            st = converged;
+        } else if (st == -2) {
+            st = 0;
+        }
+        status[0] = st;
+    }
 }
 
 hipError_t launch_align2d_window(const uint8_t *win, int stride, int w, int h, int x0, int y0, int ww, int wh,

@@ -122,6 +122,32 @@ struct HostBuf {
 
 static inline size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
 
+// Host entry points without a handle (Hamming, RGB-D depth lookup): one staging
+// area per calling thread and device, kept for the thread's lifetime -- its own
+// non-blocking stream, a device buffer and pinned in / out buffers that only
+// grow -- so a call is one packed H2D, the launches, one packed D2H and one
+// stream synchronisation (no allocation, no device-wide synchronisation).
+struct CallStaging {
+    hipStream_t stream = nullptr;
+    DevBuf dev;
+    HostBuf hin, hout;
+};
+static int call_staging(int device, CallStaging **out) {
+    static thread_local std::map<int, CallStaging *> per_device;  // never freed: lives with the thread
+    CallStaging *&S = per_device[device];
+    if (!S) {
+        S = new CallStaging();
+        if (hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete S;
+            S = nullptr;
+            set_error("hipStreamCreate failed");
+            return YGZFE_EHIP;
+        }
+    }
+    *out = S;
+    return YGZFE_OK;
+}
+
 #define YGZ_TRY(x)                          \
     do {                                    \
         int r_ = (x);                       \
@@ -1080,21 +1106,32 @@ int ygzfe_hamming_best2_device(const uint8_t *d_query, int nq, const uint8_t *d_
 
 int ygzfe_hamming_best2(int device, const uint8_t *query, int nq, const uint8_t *train, int nt, int32_t *best_idx,
                         int32_t *best_dist, int32_t *second_dist) {
-    if (nq < 0 || nt < 0) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    if (nq < 0 || nt < 0 || (nq > 0 && (!query || !best_idx || !best_dist || !second_dist)) || (nt > 0 && !train)) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
     if (nq == 0) return YGZFE_OK;
     YGZ_TRY(ensure_device(device));
-    DevBuf q, t, o;
-    YGZ_TRY(q.ensure((size_t)nq * 32));
-    YGZ_TRY(t.ensure((size_t)(nt > 0 ? nt : 1) * 32));
-    YGZ_TRY(o.ensure((size_t)nq * 12));
-    YGZ_HIP(hipMemcpy(q.p, query, (size_t)nq * 32, hipMemcpyHostToDevice));
-    if (nt > 0) YGZ_HIP(hipMemcpy(t.p, train, (size_t)nt * 32, hipMemcpyHostToDevice));
-    int32_t *bi = o.as<int32_t>(), *bd = bi + nq, *sd = bd + nq;
-    YGZ_HIP(launch_hamming_best2(q.as<uint8_t>(), nq, t.as<uint8_t>(), nt, bi, bd, sd, nullptr));
-    YGZ_HIP(hipDeviceSynchronize());
-    YGZ_HIP(hipMemcpy(best_idx, bi, (size_t)nq * 4, hipMemcpyDeviceToHost));
-    YGZ_HIP(hipMemcpy(best_dist, bd, (size_t)nq * 4, hipMemcpyDeviceToHost));
-    YGZ_HIP(hipMemcpy(second_dist, sd, (size_t)nq * 4, hipMemcpyDeviceToHost));
+    CallStaging *S;
+    YGZ_TRY(call_staging(device, &S));
+    // in: [query][train]  out: [best_idx][best_dist][second_dist]
+    const size_t o_t = align16((size_t)nq * 32), in_bytes = o_t + align16((size_t)(nt > 0 ? nt : 1) * 32);
+    const size_t out_bytes = (size_t)nq * 12;
+    YGZ_TRY(S->hin.ensure(in_bytes));
+    YGZ_TRY(S->hout.ensure(out_bytes));
+    YGZ_TRY(S->dev.ensure(in_bytes + out_bytes));
+    uint8_t *h = S->hin.as<uint8_t>(), *d = S->dev.as<uint8_t>();
+    memcpy(h, query, (size_t)nq * 32);
+    if (nt > 0) memcpy(h + o_t, train, (size_t)nt * 32);
+    YGZ_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, S->stream));
+    int32_t *bi = reinterpret_cast<int32_t *>(d + in_bytes), *bd = bi + nq, *sd = bd + nq;
+    YGZ_HIP(launch_hamming_best2(d, nq, d + o_t, nt, bi, bd, sd, S->stream));
+    YGZ_HIP(hipMemcpyAsync(S->hout.p, bi, out_bytes, hipMemcpyDeviceToHost, S->stream));
+    YGZ_HIP(hipStreamSynchronize(S->stream));
+    const int32_t *ho = S->hout.as<int32_t>();
+    memcpy(best_idx, ho, (size_t)nq * 4);
+    memcpy(best_dist, ho + nq, (size_t)nq * 4);
+    memcpy(second_dist, ho + 2 * (size_t)nq, (size_t)nq * 4);
     return YGZFE_OK;
 }
 
@@ -1104,23 +1141,31 @@ int ygzfe_hamming_csr(int device, const uint8_t *query, int nq, const uint8_t *t
     if (nq == 0) return YGZFE_OK;
     const int nc = row_ptr[nq];
     if (nc == 0) return YGZFE_OK;
+    if (!query || !train || !cand || !dist_out) { set_error("invalid argument"); return YGZFE_EINVAL; }
     for (int k = 0; k < nc; k++)
         if (cand[k] < 0 || cand[k] >= nt) { set_error("candidate index %d out of range", cand[k]); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(device));
-    DevBuf q, t, rp, cd, ds;
-    YGZ_TRY(q.ensure((size_t)nq * 32));
-    YGZ_TRY(t.ensure((size_t)nt * 32));
-    YGZ_TRY(rp.ensure((size_t)(nq + 1) * 4));
-    YGZ_TRY(cd.ensure((size_t)nc * 4));
-    YGZ_TRY(ds.ensure((size_t)nc * 4));
-    YGZ_HIP(hipMemcpy(q.p, query, (size_t)nq * 32, hipMemcpyHostToDevice));
-    YGZ_HIP(hipMemcpy(t.p, train, (size_t)nt * 32, hipMemcpyHostToDevice));
-    YGZ_HIP(hipMemcpy(rp.p, row_ptr, (size_t)(nq + 1) * 4, hipMemcpyHostToDevice));
-    YGZ_HIP(hipMemcpy(cd.p, cand, (size_t)nc * 4, hipMemcpyHostToDevice));
-    YGZ_HIP(launch_hamming_csr(q.as<uint8_t>(), nq, t.as<uint8_t>(), rp.as<int32_t>(), cd.as<int32_t>(),
-                               ds.as<int32_t>(), nullptr));
-    YGZ_HIP(hipDeviceSynchronize());
-    YGZ_HIP(hipMemcpy(dist_out, ds.p, (size_t)nc * 4, hipMemcpyDeviceToHost));
+    CallStaging *S;
+    YGZ_TRY(call_staging(device, &S));
+    // in: [query][train][row_ptr][cand]  out: [dist]
+    const size_t o_t = align16((size_t)nq * 32), o_r = o_t + align16((size_t)nt * 32);
+    const size_t o_c = o_r + align16((size_t)(nq + 1) * 4), in_bytes = o_c + align16((size_t)nc * 4);
+    const size_t out_bytes = (size_t)nc * 4;
+    YGZ_TRY(S->hin.ensure(in_bytes));
+    YGZ_TRY(S->hout.ensure(out_bytes));
+    YGZ_TRY(S->dev.ensure(in_bytes + out_bytes));
+    uint8_t *h = S->hin.as<uint8_t>(), *d = S->dev.as<uint8_t>();
+    memcpy(h, query, (size_t)nq * 32);
+    memcpy(h + o_t, train, (size_t)nt * 32);
+    memcpy(h + o_r, row_ptr, (size_t)(nq + 1) * 4);
+    memcpy(h + o_c, cand, (size_t)nc * 4);
+    YGZ_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, S->stream));
+    int32_t *ds = reinterpret_cast<int32_t *>(d + in_bytes);
+    YGZ_HIP(launch_hamming_csr(d, nq, d + o_t, reinterpret_cast<const int32_t *>(d + o_r),
+                               reinterpret_cast<const int32_t *>(d + o_c), ds, S->stream));
+    YGZ_HIP(hipMemcpyAsync(S->hout.p, ds, out_bytes, hipMemcpyDeviceToHost, S->stream));
+    YGZ_HIP(hipStreamSynchronize(S->stream));
+    memcpy(dist_out, S->hout.p, out_bytes);
     return YGZFE_OK;
 }
 
@@ -1303,20 +1348,26 @@ extern "C" int ygzfe_align2d_batch(const ygzfe_frame *cur, int level, int n, con
     YGZ_TRY(ensure_device(ex->device));
     std::lock_guard<std::mutex> lk(ex->mu);
     hipStream_t st = ex->stream;
-    DevBuf a, b, c, d;
-    YGZ_TRY(a.ensure((size_t)n * 100));
-    YGZ_TRY(b.ensure((size_t)n * 64));
-    YGZ_TRY(c.ensure((size_t)n * 8));
-    YGZ_TRY(d.ensure((size_t)n));
-    YGZ_HIP(hipMemcpyAsync(a.p, patches_with_border, (size_t)n * 100, hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemcpyAsync(b.p, patches, (size_t)n * 64, hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemcpyAsync(c.p, px_io, (size_t)n * 8, hipMemcpyHostToDevice, st));
+    // in: [patches with border][patches][px]  out: [px][converged]
+    const size_t o_p = align16((size_t)n * 100), o_x = o_p + align16((size_t)n * 64), in_bytes = o_x + align16((size_t)n * 8);
+    const size_t out_bytes = (size_t)n * 9;
+    YGZ_TRY(ex->direct_hin.ensure(in_bytes));
+    YGZ_TRY(ex->direct_hout.ensure(out_bytes));
+    YGZ_TRY(ex->direct_dev.ensure(in_bytes + align16(out_bytes)));
+    uint8_t *h = ex->direct_hin.as<uint8_t>(), *d = ex->direct_dev.as<uint8_t>();
+    memcpy(h, patches_with_border, (size_t)n * 100);
+    memcpy(h + o_p, patches, (size_t)n * 64);
+    memcpy(h + o_x, px_io, (size_t)n * 8);
+    YGZ_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st));
+    float *dpx = reinterpret_cast<float *>(d + in_bytes);
+    uint8_t *dconv = d + in_bytes + (size_t)n * 8;
+    YGZ_HIP(hipMemcpyAsync(dpx, d + o_x, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
     const LevelDesc &L = P.lv[level];
-    YGZ_HIP(launch_align2d(cur->pyr.as<uint8_t>() + L.off, L.w, L.h, n, a.as<uint8_t>(), b.as<uint8_t>(), n_iter,
-                           c.as<float>(), d.as<uint8_t>(), st));
-    YGZ_HIP(hipMemcpyAsync(px_io, c.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
-    YGZ_HIP(hipMemcpyAsync(converged, d.p, (size_t)n, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(launch_align2d(cur->pyr.as<uint8_t>() + L.off, L.w, L.h, n, d, d + o_p, n_iter, dpx, dconv, st));
+    YGZ_HIP(hipMemcpyAsync(ex->direct_hout.p, dpx, out_bytes, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipStreamSynchronize(st));
+    memcpy(px_io, ex->direct_hout.p, (size_t)n * 8);
+    memcpy(converged, ex->direct_hout.as<uint8_t>() + (size_t)n * 8, (size_t)n);
     return YGZFE_OK;
 }
 
@@ -1411,36 +1462,41 @@ extern "C" int ygzfe_find_direct_projection_batch(const ygzfe_frame *const *ref,
     std::lock_guard<std::mutex> lk(ex->mu);
     hipStream_t st = ex->stream;
     const Plan &P = cur->plan->hp();
-    std::vector<const uint8_t *> ptrs(nref);
+    // in: [ref ptrs][scale][ref_index][kps][pt][T]  out: [px][level][ok]
+    const size_t o_sc = align16(sizeof(void *) * nref), o_ri = o_sc + align16(sizeof(float) * P.nlevels);
+    const size_t o_kp = o_ri + align16(4 * (size_t)n), o_pt = o_kp + align16(sizeof(ygzfe_kp) * n);
+    const size_t o_T = o_pt + align16(12 * (size_t)n), o_px = o_T + align16(sizeof(ygzfe_se3) * n);
+    const size_t in_bytes = o_px + align16(8 * (size_t)n), out_bytes = (size_t)n * 13;
+    YGZ_TRY(ex->direct_hin.ensure(in_bytes));
+    YGZ_TRY(ex->direct_hout.ensure(out_bytes));
+    YGZ_TRY(ex->direct_dev.ensure(in_bytes + align16(out_bytes)));
+    uint8_t *h = ex->direct_hin.as<uint8_t>(), *d = ex->direct_dev.as<uint8_t>();
+    const uint8_t **ptrs = reinterpret_cast<const uint8_t **>(h);
     for (int r = 0; r < nref; r++) ptrs[r] = ref[r]->pyr.as<uint8_t>();
-    std::vector<float> scale(P.nlevels);
-    for (int l = 0; l < P.nlevels; l++) scale[l] = P.lv[l].scale;
-    DevBuf dptr, dsc, dri, dkp, dpt, dT, dpx, dlv, dok;
-    YGZ_TRY(dptr.ensure(sizeof(void *) * nref));
-    YGZ_TRY(dsc.ensure(sizeof(float) * P.nlevels));
-    YGZ_TRY(dri.ensure(4 * (size_t)n));
-    YGZ_TRY(dkp.ensure(sizeof(ygzfe_kp) * n));
-    YGZ_TRY(dpt.ensure(12 * (size_t)n));
-    YGZ_TRY(dT.ensure(sizeof(ygzfe_se3) * n));
-    YGZ_TRY(dpx.ensure(8 * (size_t)n));
-    YGZ_TRY(dlv.ensure(4 * (size_t)n));
-    YGZ_TRY(dok.ensure((size_t)n));
-    YGZ_HIP(hipMemcpyAsync(dptr.p, ptrs.data(), sizeof(void *) * nref, hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemcpyAsync(dsc.p, scale.data(), sizeof(float) * P.nlevels, hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemcpyAsync(dri.p, ref_index, 4 * (size_t)n, hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemcpyAsync(dkp.p, kp_ref, sizeof(ygzfe_kp) * n, hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemcpyAsync(dpt.p, pt_ref, 12 * (size_t)n, hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemcpyAsync(dT.p, T_cr, sizeof(ygzfe_se3) * n, hipMemcpyHostToDevice, st));
-    YGZ_HIP(hipMemcpyAsync(dpx.p, px_io, 8 * (size_t)n, hipMemcpyHostToDevice, st));
+    float *sc = reinterpret_cast<float *>(h + o_sc);
+    for (int l = 0; l < P.nlevels; l++) sc[l] = P.lv[l].scale;
+    memcpy(h + o_ri, ref_index, 4 * (size_t)n);
+    memcpy(h + o_kp, kp_ref, sizeof(ygzfe_kp) * n);
+    memcpy(h + o_pt, pt_ref, 12 * (size_t)n);
+    memcpy(h + o_T, T_cr, sizeof(ygzfe_se3) * n);
+    memcpy(h + o_px, px_io, 8 * (size_t)n);
+    YGZ_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st));
+    float *dpx = reinterpret_cast<float *>(d + in_bytes);
+    int32_t *dlv = reinterpret_cast<int32_t *>(d + in_bytes + 8 * (size_t)n);
+    uint8_t *dok = d + in_bytes + 12 * (size_t)n;
+    YGZ_HIP(hipMemcpyAsync(dpx, d + o_px, 8 * (size_t)n, hipMemcpyDeviceToDevice, st));
     const AlignLevels lv = levels_of(P);
-    YGZ_HIP(launch_find_direct(dptr.as<const uint8_t *>(), lv, cur->pyr.as<uint8_t>(), lv, P.nlevels,
-                               dsc.as<float>(), ex->scales.inv_sigma2[1 < P.nlevels ? 1 : 0], *cam, n,
-                               dri.as<int32_t>(), dkp.as<ygzfe_kp>(), dpt.as<float>(), dT.as<ygzfe_se3>(),
-                               dpx.as<float>(), dlv.as<int32_t>(), dok.as<uint8_t>(), st));
-    YGZ_HIP(hipMemcpyAsync(px_io, dpx.p, 8 * (size_t)n, hipMemcpyDeviceToHost, st));
-    YGZ_HIP(hipMemcpyAsync(search_level, dlv.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
-    YGZ_HIP(hipMemcpyAsync(ok, dok.p, (size_t)n, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(launch_find_direct(reinterpret_cast<const uint8_t *const *>(d), lv, cur->pyr.as<uint8_t>(), lv, P.nlevels,
+                               reinterpret_cast<const float *>(d + o_sc), ex->scales.inv_sigma2[1 < P.nlevels ? 1 : 0],
+                               *cam, n, reinterpret_cast<const int32_t *>(d + o_ri),
+                               reinterpret_cast<const ygzfe_kp *>(d + o_kp), reinterpret_cast<const float *>(d + o_pt),
+                               reinterpret_cast<const ygzfe_se3 *>(d + o_T), dpx, dlv, dok, st));
+    YGZ_HIP(hipMemcpyAsync(ex->direct_hout.p, dpx, out_bytes, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipStreamSynchronize(st));
+    const uint8_t *ho = ex->direct_hout.as<uint8_t>();
+    memcpy(px_io, ho, 8 * (size_t)n);
+    memcpy(search_level, ho + 8 * (size_t)n, 4 * (size_t)n);
+    memcpy(ok, ho + 12 * (size_t)n, (size_t)n);
     return YGZFE_OK;
 }
 
@@ -1688,18 +1744,25 @@ extern "C" int ygzfe_stereo_from_rgbd(int device, const float *im_depth, int wid
     }
     if (n == 0) return YGZFE_OK;
     YGZ_TRY(ensure_device(device));
-    const size_t img = 4 * (size_t)stride * height;
-    DevBuf di, dk, du, dd;
-    YGZ_TRY(di.ensure(img));
-    YGZ_TRY(dk.ensure(sizeof(ygzfe_kp) * (size_t)n));
-    YGZ_TRY(du.ensure(4 * (size_t)n));
-    YGZ_TRY(dd.ensure(4 * (size_t)n));
-    YGZ_HIP(hipMemcpy(di.p, im_depth, img, hipMemcpyHostToDevice));
-    YGZ_HIP(hipMemcpy(dk.p, kps, sizeof(ygzfe_kp) * (size_t)n, hipMemcpyHostToDevice));
-    YGZ_HIP(launch_stereo_rgbd(di.as<float>(), 0, width, height, stride, dk.as<ygzfe_kp>(), n, nullptr, n, 1, mbf,
-                               du.as<float>(), dd.as<float>(), nullptr));
-    YGZ_HIP(hipMemcpy(u_right, du.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
-    YGZ_HIP(hipMemcpy(depth, dd.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    CallStaging *S;
+    YGZ_TRY(call_staging(device, &S));
+    // in: [depth image][kps]  out: [u_right][depth]
+    const size_t img = 4 * (size_t)stride * height, o_k = align16(img);
+    const size_t in_bytes = o_k + align16(sizeof(ygzfe_kp) * (size_t)n), out_bytes = 8 * (size_t)n;
+    YGZ_TRY(S->hin.ensure(in_bytes));
+    YGZ_TRY(S->hout.ensure(out_bytes));
+    YGZ_TRY(S->dev.ensure(in_bytes + out_bytes));
+    uint8_t *h = S->hin.as<uint8_t>(), *d = S->dev.as<uint8_t>();
+    memcpy(h, im_depth, img);
+    memcpy(h + o_k, kps, sizeof(ygzfe_kp) * (size_t)n);
+    YGZ_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, S->stream));
+    float *du = reinterpret_cast<float *>(d + in_bytes), *dd = du + n;
+    YGZ_HIP(launch_stereo_rgbd(reinterpret_cast<const float *>(d), 0, width, height, stride,
+                               reinterpret_cast<const ygzfe_kp *>(d + o_k), n, nullptr, n, 1, mbf, du, dd, S->stream));
+    YGZ_HIP(hipMemcpyAsync(S->hout.p, du, out_bytes, hipMemcpyDeviceToHost, S->stream));
+    YGZ_HIP(hipStreamSynchronize(S->stream));
+    memcpy(u_right, S->hout.p, 4 * (size_t)n);
+    memcpy(depth, S->hout.as<float>() + n, 4 * (size_t)n);
     return YGZFE_OK;
 }
 
