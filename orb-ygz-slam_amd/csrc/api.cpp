@@ -161,6 +161,7 @@ struct PlanDev {
         YGZ_TRY(plan.ensure(sizeof(Plan)));
         YGZ_TRY(cells.ensure(sizeof(CellDesc) * (host.cells.size() + 1)));
         YGZ_TRY(tabs.ensure(sizeof(int) * host.tabs.size()));
+        host.plan.dtabs = tabs.as<int32_t>();
         YGZ_HIP(hipMemcpy(plan.p, &host.plan, sizeof(Plan), hipMemcpyHostToDevice));
         if (!host.cells.empty())
             YGZ_HIP(hipMemcpy(cells.p, host.cells.data(), sizeof(CellDesc) * host.cells.size(), hipMemcpyHostToDevice));
@@ -186,7 +187,7 @@ static int make_plan(const ygzfe_orb_params &p, int W, int H, std::unique_ptr<Pl
 // extraction scratch for F frames of one plan
 struct Workspace {
     int F = 0, rows = 0;
-    DevBuf blur, cellbuf, cellcnt, candA, candB, sel, selcnt, kps, desc, counts, nexist, err, ojobs;
+    DevBuf blur, cellbuf, cellcnt, candA, candB, sel, selcnt, kps, desc, counts, nexist, err, ojobs, octq;
     DevBuf occ, dso_keys, dso_cnt, dso_total;
     int ensure(const Plan &P, int frames, int rows_needed) {
         F = frames;
@@ -194,8 +195,8 @@ struct Workspace {
         YGZ_TRY(blur.ensure((size_t)F * P.pyr_bytes));
         YGZ_TRY(cellbuf.ensure((size_t)F * P.ncells * P.cell_cap * 4 + 16));
         YGZ_TRY(cellcnt.ensure((size_t)F * P.ncells * 4 + 16));
-        YGZ_TRY(candA.ensure((size_t)F * P.cand_total * 4 + 16));
-        YGZ_TRY(candB.ensure((size_t)F * P.cand_total * 4 + 16));
+        YGZ_TRY(candA.ensure((size_t)F * P.cand_total * 8 + 16));
+        YGZ_TRY(candB.ensure((size_t)F * P.cand_total * 8 + 16));
         YGZ_TRY(sel.ensure((size_t)F * P.sel_total * 4 + 16));
         YGZ_TRY(ojobs.ensure((size_t)F * P.sel_total * 8 + 16));
         YGZ_TRY(selcnt.ensure((size_t)F * P.nlevels * 4 + 128));  // tail: k_orient_desc's 8-int scalar load
@@ -204,6 +205,7 @@ struct Workspace {
         YGZ_TRY(counts.ensure((size_t)F * 4 + 16));
         YGZ_TRY(nexist.ensure((size_t)F * 4 + 16));
         YGZ_TRY(err.ensure(16));
+        YGZ_TRY(octq.ensure(octree_queue_ints(P, F) * sizeof(int)));
         return YGZFE_OK;
     }
 };
@@ -275,7 +277,7 @@ struct ygzfe_frame {
     // the captured single-frame extraction (ygzfe_extract, no existing rows)
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
-    const void *gkey[14] = {};
+    const void *gkey[15] = {};
     int grows = 0;
     size_t gcopy = 0;
     void drop_graph() {
@@ -639,7 +641,8 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
             YGZ_HIP(launch_fast_merged(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(),
                                        ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), 1, st, d_err));
             YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
-                                  ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_err, 1, st,
+                                  ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_err,
+                                  ws.octq.as<int>(), 1, st,
                                   &sd[1], 2, ex->ev_oct_fork, ex->ev_oct_join, true));
             YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_nexist, d_kps, d_count,
                                     rows, ws.ojobs.as<uint2>(), 1, st));
@@ -654,9 +657,9 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
         // joins and the D2H) is replayed from a HIP graph captured once per frame
         // handle: one submission instead of one host call per launch.  The graph is
         // re-captured when any buffer it names has moved or the copy size changed.
-        const void *key[14] = {pyr,          ws.blur.p,  ws.cellbuf.p, ws.sel.p,       ws.candA.p,
+        const void *key[15] = {pyr,          ws.blur.p,  ws.cellbuf.p, ws.sel.p,       ws.candA.p,
                                ws.candB.p,   ex->res.p,  ex->hout.p,   ws.ojobs.p,     ws.cellcnt.p,
-                               ws.selcnt.p,  pd.cells.p, pd.plan.p,    pd.tabs.p};
+                               ws.selcnt.p,  pd.cells.p, pd.plan.p,    pd.tabs.p,      ws.octq.p};
         static const bool no_graph = getenv("YGZFE_NO_GRAPH") != nullptr;
         bool launched = false;
         if (n_existing == 0 && !no_graph && !ex->graph_broken) {
@@ -893,6 +896,7 @@ int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, voi
     t0 = b->begin(st);
     YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
                           ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), ws.err.as<int>(),
+                          ws.octq.as<int>(),
                           n_frames, st, &b->aux[1], 2, b->ev_oct_fork, b->ev_oct_join));
     YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), nullptr, ws.kps.as<ygzfe_kp>(),
                             ws.counts.as<int>(), P.kp_cap, ws.ojobs.as<uint2>(), n_frames, st));

@@ -46,6 +46,9 @@ struct LevelDesc {
     int pyr_tile_begin;
     int fast_roi;        // largest FAST cell ROI side of this level
     int fast_rw, fast_rh;  // largest FAST cell ROI width / height of this level
+    // octree path codes (k_octree_paths): root bits, quadrant depth carried, and the
+    // separable code tables in Plan::dtabs (code = X[x] | Y[y], key coordinates)
+    int oct_rb, oct_dn, oct_xtab, oct_ytab;
 };
 
 struct alignas(16) CellDesc {
@@ -69,6 +72,7 @@ struct Plan {
     int fast_S;               // LDS row stride of a FAST cell ROI (max ROI side, multiple of 4)
     int umax[16];             // IC_Angle circle rows (ORBextractor.cc:453-467)
     LevelDesc lv[kMaxLevels];
+    const int32_t *dtabs;     // device copy of PlanHost::tabs (set at upload)
 };
 
 // --------------------------------------------------------------------------

@@ -1247,6 +1247,813 @@ __global__ __launch_bounds__(NT) void k_octree(const Plan *__restrict__ plan,
     }
 }
 
+// ---------------------------------------------------------------------------
+// Octree distribution by quadrant paths (the kernel in use; k_octree above is the
+// level-synchronous form it replaced, kept for A/B builds with -DYGZ_OCT_LEGACY).
+//
+// A node at depth d is the set of keys that share the first d quadrants of their
+// path from the root column (the division midpoints, ORBextractor.cc:481-482, depend
+// only on the node's bounds, so every key can walk its own path).  With the keys
+// sorted by path code, every node of every depth is a contiguous run, and
+// L_k = depth of the common prefix of sorted keys k-1 and k gives, for all depths at
+// once (main loop, :585-640):
+//   size(d)    = #{k : L_k < d}                      (nodes after pass d)
+//   nexpand(d) = size(d) - #{k : max(L_k, L_k+1) < d} (nodes with > 1 key)
+// so the pass P that ends the main loop follows from two histograms.  The list
+// order after P passes is closed-form: push_front leaves, front to back, the nodes
+// created at depth P, then the singletons created at P-1, P-2, ..., 0; within one
+// creation depth e the order fo_e satisfies fo_0 = root ascending and fo_e =
+// (parent in reverse fo_{e-1}, quadrant descending).  Storing the root field and the
+// odd depths' quadrants complemented makes fo_e the ascending code order for odd e
+// and its reverse for even e.  The final rounds (:641-676) divide the front nodes
+// (those the last pass created) in (key count desc, list position asc) order -- the
+// list position ascends with the std::sort tie-break taken as creation order
+// descending, as in oracle/orb.c -- up to the first division that reaches N.
+// tools/octree_proto.py checks this formulation against oracle/orb.c's list walk.
+
+namespace oct {
+
+// lanes whose db-bit value equals this lane's, among 'valid'
+__device__ __forceinline__ uint64_t match_bits(uint32_t v, int db, uint64_t valid) {
+    uint64_t m = valid;
+    for (int b = 0; b < db; b++) {
+        const bool bit = (v >> b) & 1u;
+        const uint64_t bal = __ballot(bit);
+        m &= bit ? bal : ~bal;
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
+
+template <int NT>
+constexpr int nwaves() { return NT / 64; }
+
+// LDS carve-up.  Sort phase: K | code0 | idx0 | {code1, idx1, hist}.  After the sort
+// (which always ends in buffer 0) the second region holds L and the node lists.
+template <int NC, int NK, int NT>
+struct Layout {
+    static constexpr int kK = 0;
+    static constexpr int kCode0 = kK + 4 * NK;
+    static constexpr int kIdx0 = kCode0 + 4 * NK;
+    static constexpr int kU = (kIdx0 + 2 * NK + 15) & ~15;
+    // sort phase
+    static constexpr int kCode1 = kU;
+    static constexpr int kIdx1 = kCode1 + 4 * NK;
+    static constexpr int kHist = (kIdx1 + 2 * NK + 15) & ~15;
+    static constexpr int kSortEnd = kHist + 4 * 256 * nwaves<NT>();
+    // list phase
+    static constexpr int kNode = kU;                     // u32 [2][NC]: start | len << 16
+    static constexpr int kDep = kNode + 8 * NC;          // u8  [2][NC]: depth | processed << 7
+    static constexpr int kCk = (kDep + 2 * NC + 15) & ~15;  // u32 [NC + 4]: candidate sort keys
+    static constexpr int kCe = kCk + 4 * NC + 16;        // u16 [NC]: children per candidate
+    static constexpr int kCi = kCe + 2 * NC;             // u16 [NC]: inclusive children prefix
+    static constexpr int kHs = kCi + 2 * NC;             // u16 [NC + 2]: sorted position of head r
+    static constexpr int kNgr = kHs + 2 * NC + 4;        // u16 [NC]: list position -> head rank
+    static constexpr int kLc = (kNgr + 2 * NC + 15) & ~15;  // i8 [NK + 1]: L per sorted position (LDS keys)
+    static constexpr int kListEnd = kLc + NK + 16;
+    static constexpr int kBytes = (kSortEnd > kListEnd ? kSortEnd : kListEnd);
+};
+
+struct Scal {
+    int red[16];
+    int wcnt[16][16];  // per wave: per-section head counts (sweep A)
+    int whead[16];     // per wave: heads
+    int hL[16], hM[16];  // histograms of L + 1 and max(L_k, L_k+1) + 1
+    int s[8];
+};
+
+// One pass of an LSD radix sort over the wave-owned segment [s0, s1) (segments in
+// wave order = array order, so each pass is stable): per-wave digit counts by
+// ballot matching, one scan over (digit, wave), then the scatter.
+template <int NT, typename CP, typename IP>
+__device__ __forceinline__ void radix_pass(CP src_c, IP src_i, CP dst_c, IP dst_i, int s0, int s1, int sh,
+                                           int db, uint32_t *hist, Scal &Sc) {
+    constexpr int NW = nwaves<NT>();
+    const int lane = lane_id(), w = threadIdx.x >> 6, nb = 1 << db;
+    uint32_t *hw = hist + w * 256;
+    for (int d = lane; d < nb; d += 64) hw[d] = 0u;
+    for (int k0 = s0; k0 < s1; k0 += 64) {
+        const int k = k0 + lane;
+        const bool v = k < s1;
+        const uint32_t dg = v ? (src_c[k] >> sh) & (uint32_t)(nb - 1) : 0u;
+        const uint64_t peers = match_bits(dg, db, __ballot(v));
+        if (v && (peers & lanes_below()) == 0) hw[dg] += (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    {
+        const int d = threadIdx.x;  // NT >= 256 >= nb
+        int s = 0;
+        if (d < nb)
+            for (int ww = 0; ww < NW; ww++) s += (int)hist[ww * 256 + d];
+        int tot;
+        const int base = block_excl_scan<NT>(d < nb ? s : 0, Sc.red, &tot);
+        if (d < nb) {
+            int run = base;
+            for (int ww = 0; ww < NW; ww++) {
+                const int c = (int)hist[ww * 256 + d];
+                hist[ww * 256 + d] = (uint32_t)run;
+                run += c;
+            }
+        }
+    }
+    __syncthreads();
+    for (int k0 = s0; k0 < s1; k0 += 64) {
+        const int k = k0 + lane;
+        const bool v = k < s1;
+        uint32_t c = 0u, dg = 0u;
+        uint16_t ix = 0;
+        if (v) {
+            c = src_c[k];
+            ix = src_i[k];
+            dg = (c >> sh) & (uint32_t)(nb - 1);
+        }
+        const uint64_t peers = match_bits(dg, db, __ballot(v));
+        const uint32_t base = v ? hw[dg] : 0u;
+        if (v) {
+            const uint64_t below = peers & lanes_below();
+            const uint32_t dst = base + (uint32_t)__popcll(below);
+            dst_c[dst] = c;
+            dst_i[dst] = ix;
+            if (below == 0) hw[dg] = base + (uint32_t)__popcll(peers);
+        }
+    }
+    __syncthreads();
+}
+
+// value of lane ^ J (J < 64): quad_perm for 1 and 2, two bank-masked row shifts
+// for 4 and 8, a row / half-wave swap for 16 and 32
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+    if constexpr (J == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    } else if constexpr (J == 4) {  // banks 0, 2 <- row_shl:4; banks 1, 3 <- row_shr:4
+        const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0x5, false);
+        return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)v, 0x114, 0xF, 0xA, false);
+    } else if constexpr (J == 8) {
+        const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x108, 0xF, 0x3, false);
+        return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)v, 0x118, 0xF, 0xC, false);
+    } else if constexpr (J == 16) {  // {r0, r0, r2, r2} and {r1, r1, r3, r3}
+        const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane_id() & 16) ? p[0] : p[1];
+    } else {  // {lo, lo} and {hi, hi}
+        const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane_id() & 32) ? p[0] : p[1];
+    }
+}
+
+// one bitonic stage (k, J) over a wave's 64 R elements, element e = 64 r + lane:
+// ascending where (e & k) == 0; codes distinct, pads (all ones) only equal to pads.
+// J is a template parameter (the lane exchange pattern), k a runtime value, so the
+// whole sort is a loop over one compiled body per J (~1k instructions in all; a
+// fully unrolled network is ~4k and thrashes the instruction cache beside the
+// other octree classes)
+template <int R, int J>
+__device__ __forceinline__ void bitonic_stage(uint32_t (&S)[R], uint32_t (&I)[R], int k) {
+    const int lane = lane_id();
+    if constexpr (J >= 64) {
+        constexpr int D = J / 64;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (r & D) continue;
+            const bool asc = ((r * 64) & k) == 0;
+            const bool sw = asc ? S[r + D] < S[r] : S[r] < S[r + D];
+            const uint32_t a = S[r], b = S[r + D], ia = I[r], ib = I[r + D];
+            S[r] = sw ? b : a;
+            S[r + D] = sw ? a : b;
+            I[r] = sw ? ib : ia;
+            I[r + D] = sw ? ia : ib;
+        }
+    } else {
+        const bool lower = (lane & J) == 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const bool asc = ((r * 64 + lane) & k) == 0;
+            const uint32_t ps = xor_lane<J>(S[r]), pi = xor_lane<J>(I[r]);
+            const bool take = (lower == asc) ? ps < S[r] : S[r] < ps;
+            S[r] = take ? ps : S[r];
+            I[r] = take ? pi : I[r];
+        }
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void bitonic_sort(uint32_t (&S)[R], uint32_t (&I)[R]) {
+#pragma nounroll
+    for (int k = 2; k <= 64 * R; k <<= 1) {
+#pragma nounroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            switch (j) {
+                case 1: bitonic_stage<R, 1>(S, I, k); break;
+                case 2: bitonic_stage<R, 2>(S, I, k); break;
+                case 4: bitonic_stage<R, 4>(S, I, k); break;
+                case 8: bitonic_stage<R, 8>(S, I, k); break;
+                case 16: bitonic_stage<R, 16>(S, I, k); break;
+                case 32: bitonic_stage<R, 32>(S, I, k); break;
+                case 64: if constexpr (R > 1) bitonic_stage<R, 64>(S, I, k); break;
+                case 128: if constexpr (R > 2) bitonic_stage<R, 128>(S, I, k); break;
+                case 256: if constexpr (R > 4) bitonic_stage<R, 256>(S, I, k); break;
+                case 512: if constexpr (R > 8) bitonic_stage<R, 512>(S, I, k); break;
+                default: break;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ int lcp_depth(uint32_t a, uint32_t b, int rb) {
+    const uint32_t x = a ^ b;
+    if (x == 0u) return 14;  // equal codes: not separated (Dn <= 14: flagged by the caller)
+    const int lz = __clz((int)x);
+    return lz < rb ? -1 : (lz - rb) >> 1;
+}
+
+// K: keys in candidate order; code0/idx0 + code1/idx1: sort buffers; Lc: i8 [n+1]
+template <int NC, int NK, int NT, int RB, typename KP, typename CP, typename IP, typename LP>
+__device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelDesc &L, int l, int f, uint8_t *smem,
+                                     Scal &Sc, const uint32_t *__restrict__ cellbuf,
+                                     const int *__restrict__ cellcnt, KP K, CP code0, IP idx0, CP code1, IP idx1,
+                                     LP Lc, int n, uint32_t *__restrict__ sel, int *__restrict__ selcnt,
+                                     int *__restrict__ err) {
+    using Lay = Layout<NC, NK, NT>;
+    constexpr int NW = nwaves<NT>();
+    const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    if (tid < 16) {  // published by the gather's barriers
+        Sc.hL[tid] = 0;
+        Sc.hM[tid] = 0;
+    }
+    // --- 1. vToDistributeKeys in cell order: every thread places its keys j = tid +
+    //        NT u by branch-free binary searches over the cells' prefix (all steps of all
+    //        its searches interleaved), then issues all their loads together
+    {
+        int *s_pref = reinterpret_cast<int *>(smem + Lay::kHist);
+        int base = 0;
+        for (int cb = 0; cb < L.ncells; cb += NT) {
+            const int c = cb + tid;
+            const int cnt = c < L.ncells ? cellcnt[(size_t)f * plan->ncells + L.cell_begin + c] : 0;
+            int tot;
+            const int ex = block_excl_scan<NT>(cnt, Sc.red, &tot);
+            s_pref[tid] = ex;
+            __syncthreads();
+            const int nch = min(L.ncells - cb, NT);
+            const uint32_t *cs0 = cellbuf + ((size_t)f * plan->ncells + L.cell_begin + cb) * plan->cell_cap;
+            for (int j0 = 0; j0 < tot; j0 += NT * 8) {
+                int cc[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) cc[u] = 0;
+#pragma unroll
+                for (int step = NT / 2; step >= 1; step >>= 1) {
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const int j = j0 + NT * u + tid, q = cc[u] + step;
+                        if (q < nch && s_pref[q] <= j) cc[u] = q;
+                    }
+                }
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int j = j0 + NT * u + tid;
+                    v[u] = j < tot ? cs0[(size_t)cc[u] * plan->cell_cap + (j - s_pref[cc[u]])] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int j = j0 + NT * u + tid;
+                    if (j < tot) K[base + j] = v[u];
+                }
+            }
+            base += tot;
+            __syncthreads();
+        }
+    }
+    if (l == 0) YGZ_BSTAMP_K(3, 3);
+    // --- 2. path codes: root field (complemented) on top, then Dn quadrants of 2 bits,
+    //        odd depths complemented; Dn levels separate any two pixels of the level
+    const int rb = L.oct_rb, Dn = L.oct_dn;  // plan.cpp octree_code_tables
+    const int bits = rb + 2 * Dn;
+    const int passes = (bits + 7) >> 3;
+    const int db = (bits + passes - 1) / passes;
+    const int lowbit = 32 - passes * db;
+    const int *xtab = plan->dtabs + L.oct_xtab, *ytab = plan->dtabs + L.oct_ytab;
+    auto path_code = [&](uint32_t kk) -> uint32_t {
+        return (uint32_t)as_global(xtab)[key_x(kk)] | (uint32_t)as_global(ytab)[key_y(kk)];
+    };
+    const int seg = (((n + NW - 1) / NW) + 63) & ~63;
+    const int s0 = min(n, w * seg), s1 = min(n, s0 + seg);
+    if constexpr (RB > 0) {
+        // --- 3. sort by code (codes are distinct): counting sort on the top BB bits
+        //        (NB = 4 NT buckets; one LDS atomic per key returns its slot), then each
+        //        key's final place = its bucket's start + its rank among the bucket's
+        //        keys (buckets hold a few keys: a depth-5 cell of the quadtree)
+        constexpr int NB = 4 * NT;
+        constexpr int BB = __builtin_ctz(NB);
+        uint32_t *bcnt = reinterpret_cast<uint32_t *>(smem + Lay::kHist);
+        static_assert(NB * 4 <= 4 * 256 * (NT / 64), "bucket counters fit the histogram region");
+#pragma unroll
+        for (int i = 0; i < 4; i++) bcnt[tid * 4 + i] = 0u;
+        __syncthreads();
+        for (int j = tid; j < n; j += NT) {
+            const uint32_t c = path_code(K[j]);
+            code0[j] = c;
+            idx0[j] = (uint16_t)atomicAdd(&bcnt[c >> (32 - BB)], 1u);
+        }
+        __syncthreads();
+        {
+            const uint4 c4 = *reinterpret_cast<const uint4 *>(bcnt + 4 * tid);
+            int tot;
+            const int ex = block_excl_scan<NT>((int)(c4.x + c4.y + c4.z + c4.w), Sc.red, &tot);
+            *reinterpret_cast<uint4 *>(bcnt + 4 * tid) =
+                make_uint4((uint32_t)ex, (uint32_t)ex + c4.x, (uint32_t)ex + c4.x + c4.y,
+                           (uint32_t)ex + c4.x + c4.y + c4.z);
+        }
+        __syncthreads();
+        for (int j = tid; j < n; j += NT) {
+            const uint32_t c = code0[j];
+            const uint32_t p = bcnt[c >> (32 - BB)] + idx0[j];
+            code1[p] = c;
+            idx1[p] = (uint16_t)j;
+        }
+        __syncthreads();
+        for (int p = tid; p < n; p += NT) {
+            const uint32_t c = code1[p];
+            const uint32_t b = c >> (32 - BB);
+            const int st = (int)bcnt[b], en = b + 1 < (uint32_t)NB ? (int)bcnt[b + 1] : n;
+            int rank = 0;
+            for (int q = st; q < en; q++) rank += code1[q] < c;
+            code0[st + rank] = c;
+            idx0[st + rank] = idx1[p];
+        }
+        __syncthreads();
+    } else {
+        {
+            CP c_out = (passes & 1) ? code1 : code0;  // the sort ends in buffer 0
+            IP i_out = (passes & 1) ? idx1 : idx0;
+            for (int j = tid; j < n; j += NT) {
+                c_out[j] = path_code(K[j]);
+                i_out[j] = (uint16_t)j;
+            }
+        }
+        __syncthreads();
+        // --- 3'. (more keys than the LDS holds) LSD radix sort in the global scratch
+        uint32_t *hist = reinterpret_cast<uint32_t *>(smem + Lay::kHist);
+        for (int p = 0; p < passes; p++) {
+            const bool from1 = ((passes - p) & 1) != 0;
+            radix_pass<NT>(from1 ? code1 : code0, from1 ? idx1 : idx0, from1 ? code0 : code1, from1 ? idx0 : idx1,
+                           s0, s1, lowbit + p * db, db, hist, Sc);
+        }
+    }
+    if (l == 0) YGZ_BSTAMP_K(3, 4);
+    // --- 4. L per sorted position and the two histograms.  With the keys in LDS the
+    //        wave's chunks keep L_k and L_k+1 in registers for the sweeps below.
+    constexpr int CH = RB > 0 ? RB : 1;
+    int La[CH], Lb[CH];
+    const int nch = RB > 0 ? RB : (s1 - s0 + 63) / 64;
+    if constexpr (RB > 0) {
+#pragma unroll
+        for (int i = 0; i < CH; i++) {
+            const int k = s0 + 64 * i + lane;
+            La[i] = Lb[i] = -1;
+            if (k < s1) {
+                const uint32_t c = code0[k];
+                if (k > 0) La[i] = lcp_depth(code0[k - 1], c, rb);
+                if (k + 1 < n) Lb[i] = lcp_depth(c, code0[k + 1], rb);
+                if (La[i] >= Dn || (k > 0 && code0[k - 1] == c)) Sc.s[1] = 1;
+                Lc[k] = (int8_t)La[i];
+            }
+        }
+        if (tid == 0) Lc[n] = -1;
+    } else {
+        for (int k = tid; k <= n; k += NT) {
+            int v = -1;
+            if (k > 0 && k < n) {
+                v = lcp_depth(code0[k - 1], code0[k], rb);
+                if (v >= Dn || code0[k - 1] == code0[k]) Sc.s[1] = 1;
+            }
+            Lc[k] = (int8_t)v;
+        }
+        __syncthreads();
+    }
+    auto chunk_ab = [&](int i, int k, int &a, int &b) {
+        if constexpr (RB > 0) {
+            a = La[i];
+            b = Lb[i];
+        } else {
+            a = Lc[k];
+            b = Lc[k + 1];
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < (RB > 0 ? RB : 1 << 30) && i < nch; i++) {
+        const int k = s0 + 64 * i + lane;
+        const bool v = k < s1;
+        int a = 0, m = 0;
+        if (v) {
+            int a0, b0;
+            chunk_ab(i, k, a0, b0);
+            a = a0 + 1;
+            m = (a0 > b0 ? a0 : b0) + 1;
+        }
+        const uint64_t valid = __ballot(v);
+        const uint64_t pa = match_bits((uint32_t)a, 4, valid);
+        if (v && (pa & lanes_below()) == 0) atomicAdd(&Sc.hL[a], __popcll(pa));
+        const uint64_t pm = match_bits((uint32_t)m, 4, valid);
+        if (v && (pm & lanes_below()) == 0) atomicAdd(&Sc.hM[m], __popcll(pm));
+    }
+    __syncthreads();
+    int bad = Sc.s[1];
+    // P: the pass that ends the main loop; final = the final rounds follow
+    const int N = L.budget;
+    int P = 0, final_round = 0;
+    {
+        int cL = Sc.hL[0], cM = Sc.hM[0];
+        int prev = cL;
+        for (int d = 1; d < 16; d++) {
+            cL += Sc.hL[d];
+            cM += Sc.hM[d];
+            P = d;
+            if (cL >= N || cL == prev) break;
+            if (cL + 3 * (cL - cM) > N) { final_round = 1; break; }
+            prev = cL;
+        }
+    }
+    bad |= P >= Dn;
+    // --- 5. the list after P passes: heads (L_k < P), sections e = min(m_k + 1, P)
+    uint32_t *node = reinterpret_cast<uint32_t *>(smem + Lay::kNode);
+    uint8_t *ndep = smem + Lay::kDep;
+    uint16_t *hs = reinterpret_cast<uint16_t *>(smem + Lay::kHs);
+    uint16_t *ngr = reinterpret_cast<uint16_t *>(smem + Lay::kNgr);
+    auto chunk_sec = [&](int i, int k) -> int {
+        int sec = -1;
+        if (k < s1) {
+            int a, b;
+            chunk_ab(i, k, a, b);
+            if (a < P) sec = min((a > b ? a : b) + 1, P);
+        }
+        return sec;
+    };
+    // sweep A: per wave, heads and heads per section (lane e counts section e)
+    {
+        int wc = 0, wh = 0;
+#pragma unroll
+        for (int i = 0; i < (RB > 0 ? RB : 1 << 30) && i < nch; i++) {
+            const int sec = chunk_sec(i, s0 + 64 * i + lane);
+            wh += __popcll(__ballot(sec >= 0));
+            for (int e = 0; e <= P; e++) {
+                const int c = __popcll(__ballot(sec == e));
+                wc += lane == e ? c : 0;
+            }
+        }
+        if (lane < 16) Sc.wcnt[w][lane] = wc;
+        if (lane == 0) Sc.whead[w] = wh;
+    }
+    __syncthreads();
+    // lane e: section e's count, its list base (sections P..0 in descending order)
+    // and this wave's running rank inside it
+    int nheads = 0, hbase = 0, scnt = 0, srun = 0;
+    for (int ww = 0; ww < NW; ww++) {
+        const int h = Sc.whead[ww];
+        hbase += ww < w ? h : 0;
+        nheads += h;
+        const int x = lane < 16 ? Sc.wcnt[ww][lane] : 0;
+        srun += ww < w ? x : 0;
+        scnt += x;
+    }
+    int sbase = 0;  // sum over sections above this lane's
+    {
+        int acc = 0;
+        for (int e = 15; e >= 0; e--) {
+            const int c = __builtin_amdgcn_readlane(scnt, e);
+            sbase = lane == e ? acc : sbase;
+            acc += c;
+        }
+    }
+    const int front0 = __builtin_amdgcn_readlane(scnt, P);
+    int overflow = bad || nheads > NC;
+    if (!overflow) {
+        int hr = hbase;
+#pragma unroll
+        for (int i = 0; i < (RB > 0 ? RB : 1 << 30) && i < nch; i++) {
+            const int k = s0 + 64 * i + lane;
+            const int sec = chunk_sec(i, k);
+            const uint64_t hb = __ballot(sec >= 0);
+            const int gr = hr + __popcll(hb & lanes_below());
+            hr += __popcll(hb);
+            int rank = 0, bse = 0, ce = 0;
+            for (int e = 0; e <= P; e++) {  // e uniform: lane-e values by readlane
+                const uint64_t b = __ballot(sec == e);
+                const int r0 = __builtin_amdgcn_readlane(srun, e);
+                const int b0 = __builtin_amdgcn_readlane(sbase, e), c0 = __builtin_amdgcn_readlane(scnt, e);
+                if (sec == e) {
+                    rank = r0 + __popcll(b & lanes_below());
+                    bse = b0;
+                    ce = c0;
+                }
+                srun += lane == e ? __popcll(b) : 0;
+            }
+            if (sec >= 0) {
+                const int pos = bse + ((sec & 1) ? rank : ce - 1 - rank);
+                hs[gr] = (uint16_t)k;
+                ngr[pos] = (uint16_t)gr;
+                ndep[pos] = (uint8_t)sec;
+            }
+        }
+        if (tid == 0) hs[nheads] = (uint16_t)n;
+    }
+    __syncthreads();
+    int size = nheads;
+    if (!overflow) {
+        for (int p = tid; p < size; p += NT) {
+            const int gr = ngr[p];
+            const int st = hs[gr];
+            node[p] = (uint32_t)st | ((uint32_t)(hs[gr + 1] - st) << 16);
+        }
+    }
+    __syncthreads();
+    if (l == 0) YGZ_BSTAMP_K(3, 5);
+    // --- 6. final rounds
+    int cur = 0, front = front0;
+    uint32_t *ck = reinterpret_cast<uint32_t *>(smem + Lay::kCk);
+    uint16_t *cev = reinterpret_cast<uint16_t *>(smem + Lay::kCe);
+    uint16_t *cin = reinterpret_cast<uint16_t *>(smem + Lay::kCi);
+    int guard = 0;
+    while (final_round && !overflow) {
+        const int prevSize = size;
+        uint32_t *nd = node + cur * NC, *nn = node + (cur ^ 1) * NC;
+        uint8_t *dd = ndep + cur * NC, *dn = ndep + (cur ^ 1) * NC;
+        // candidates: front nodes with > 1 key, key (count desc, position asc)
+        int nc = 0;
+        for (int p0 = 0; p0 < front; p0 += NT) {
+            const int p = p0 + tid;
+            const uint32_t r = p < front ? nd[p] : 0u;
+            const bool cand = p < front && (r >> 16) > 1u;
+            int tot;
+            const int ex = block_excl_scan<NT>(cand ? 1 : 0, Sc.red, &tot);
+            if (cand) ck[nc + ex] = ((0xFFFFu - (r >> 16)) << 16) | (uint32_t)p;
+            nc += tot;
+        }
+        if (tid < 4) ck[nc + tid] = 0xFFFFFFFFu;  // pad to a multiple of 4 (never smaller)
+        __syncthreads();
+        {   // ascending by rank (distinct keys): one barrier, broadcast 16-B reads
+            constexpr int kPer = (NC + NT - 1) / NT;
+            uint32_t mine[kPer];
+            int rk[kPer];
+#pragma unroll
+            for (int u = 0; u < kPer; u++) {
+                mine[u] = tid + u * NT < nc ? ck[tid + u * NT] : 0xFFFFFFFFu;
+                rk[u] = 0;
+            }
+#pragma unroll 2
+            for (int j = 0; j < (w * 64 < nc ? nc : 0); j += 4) {  // waves holding no candidate skip
+                const uint4 v = *reinterpret_cast<const uint4 *>(ck + j);
+#pragma unroll
+                for (int u = 0; u < kPer; u++) rk[u] += (v.x < mine[u]) + (v.y < mine[u]) + (v.z < mine[u]) + (v.w < mine[u]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < kPer; u++)
+                if (tid + u * NT < nc) ck[rk[u]] = mine[u];
+            __syncthreads();
+        }
+        // children per candidate: 1 + #{k in the run : L_k == depth}, four L bytes per
+        // LDS read (exact zero-byte test on L ^ depth)
+        if (tid == 0) Sc.s[0] = nc;
+        for (int c = tid; c < nc; c += NT) {
+            const int p = (int)(ck[c] & 0xFFFFu);
+            const uint32_t r = nd[p];
+            const int st = (int)(r & 0xFFFFu), ln = (int)(r >> 16), dep = dd[p] & 0x7F;
+            int e = 1;
+            if constexpr (RB > 0) {
+                const uint32_t rep = 0x01010101u * (uint32_t)dep;
+                const int k0 = st + 1, k1 = st + ln;  // [k0, k1)
+                for (int a = k0 & ~3; a < k1; a += 4) {
+                    const uint32_t x = *reinterpret_cast<const uint32_t *>(Lc + a) ^ rep;
+                    uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte
+                    const int lo = k0 - a, hi = k1 - a;  // bytes [lo, hi) of this word count
+                    if (lo > 0) z &= 0xFFFFFFFFu << (8 * lo);
+                    if (hi < 4) z &= 0xFFFFFFFFu >> (8 * (4 - hi));
+                    e += __popc(z);
+                }
+            } else {
+                for (int k = st + 1; k < st + ln; k++) e += Lc[k] == dep;
+            }
+            cev[c] = (uint16_t)e;
+        }
+        __syncthreads();
+        // cut: first c with size + sum_{c' <= c} (e - 1) >= N; one scan carries both sums
+        {
+            int carryE = 0, carryD = 0;
+            for (int c0 = 0; c0 < nc; c0 += NT) {
+                const int c = c0 + tid;
+                const int e = c < nc ? (int)cev[c] : 0;
+                int tot;
+                const int ex = block_excl_scan<NT>(c < nc ? (e << 16) | (e - 1) : 0, Sc.red, &tot);
+                const int exE = ex >> 16, exD = ex & 0xFFFF;
+                if (c < nc) {
+                    cin[c] = (uint16_t)(carryE + exE + e);
+                    if (size + carryD + exD + (e - 1) >= N) atomicMin(&Sc.s[0], c);
+                }
+                carryE += tot >> 16;
+                carryD += tot & 0xFFFF;
+            }
+        }
+        __syncthreads();
+        const int cstar = min(Sc.s[0], nc - 1);
+        const int ctot = cstar >= 0 ? (int)cin[cstar] : 0;
+        if (ctot + size - (cstar + 1) > NC) {
+            overflow = 1;
+            break;
+        }
+        // children of the divided nodes: group of c at ctot - cin[c], list-front order
+        for (int c = tid; c <= cstar; c += NT) {
+            const int p = (int)(ck[c] & 0xFFFFu);
+            const uint32_t r = nd[p];
+            const int st = (int)(r & 0xFFFFu), ln = (int)(r >> 16), dep = dd[p] & 0x7F;
+            const int e = cev[c], g0 = ctot - (int)cin[c];
+            const bool fwd = ((dep + 1) & 1) != 0;
+            dd[p] = (uint8_t)(dep | 0x80);
+            int i = 0, cs = st;
+            for (int k = st + 1; k <= st + ln; k++) {
+                if (k == st + ln || Lc[k] == dep) {
+                    const int pos = g0 + (fwd ? i : e - 1 - i);
+                    nn[pos] = (uint32_t)cs | ((uint32_t)(k - cs) << 16);
+                    dn[pos] = (uint8_t)(dep + 1);
+                    cs = k;
+                    i++;
+                }
+            }
+        }
+        __syncthreads();
+        // the other nodes keep their order behind the new front
+        {
+            int carry = 0;
+            for (int p0 = 0; p0 < size; p0 += NT) {
+                const int p = p0 + tid;
+                const bool keep = p < size && !(dd[p] & 0x80);
+                int tot;
+                const int ex = block_excl_scan<NT>(keep ? 1 : 0, Sc.red, &tot);
+                if (keep) {
+                    nn[ctot + carry + ex] = nd[p];
+                    dn[ctot + carry + ex] = dd[p];
+                }
+                carry += tot;
+            }
+        }
+        __syncthreads();
+        size = ctot + size - (cstar + 1);
+        front = ctot;
+        cur ^= 1;
+        if (size >= N || size == prevSize || ++guard > 64) break;
+    }
+    if (l == 0) YGZ_BSTAMP_K(3, 6);
+    // --- 7. retained key per node (first maximum response in candidate order), list order
+    uint32_t *out = sel + (size_t)f * plan->sel_total + L.sel_off;
+    if (size > L.sel_cap) overflow = 1;
+    if (!overflow) {
+        const uint32_t *nd = node + cur * NC;
+        for (int i = tid; i < size; i += NT) {
+            const uint32_t r = nd[i];
+            const int st = (int)(r & 0xFFFFu), ln = (int)(r >> 16);
+            uint32_t best = 0u;
+            for (int k = st; k < st + ln; k++) {
+                const uint32_t ix = idx0[k];
+                const uint32_t v = ((uint32_t)key_score(K[ix]) << 24) | (0xFFFFFFu - ix);
+                best = v > best ? v : best;
+            }
+            out[i] = K[0xFFFFFFu - (best & 0xFFFFFFu)];
+        }
+    }
+    if (tid == 0) {
+        selcnt[(size_t)f * plan->nlevels + l] = overflow ? 0 : size;
+        if (overflow) atomicOr(err, 1);
+    }
+    if (l == 0) YGZ_BSTAMP_K(3, 1);
+    if (l == 0) YGZ_BSTAMP_K(3, 2);
+}
+
+}  // namespace oct
+
+// Work queues between the octree stages of one node-pool class (api.cpp zeroes the
+// counters before each extraction): a task (f << 4 | l) whose level has more
+// candidates than a stage's LDS holds is appended to the next stage's list.
+struct OctQueue {
+    int *cnt_in, *taken_in;
+    const int *list_in;
+    int *cnt_out, *list_out;
+};
+
+// One (frame, level) task with keys, codes and L in LDS (at most NK candidates).
+template <int NC, int NK, int NT>
+__device__ __forceinline__ void octree_task(const Plan *__restrict__ plan, const uint32_t *__restrict__ cellbuf,
+                                            const int *__restrict__ cellcnt, uint32_t *__restrict__ sel,
+                                            int *__restrict__ selcnt, int *__restrict__ err, int f, int l,
+                                            const OctQueue &q, uint8_t *smem, oct::Scal &Sc) {
+    using Lay = oct::Layout<NC, NK, NT>;
+    const int tid = threadIdx.x;
+    if (l == 0) YGZ_BSTAMP_K(3, 0);
+    const LevelDesc &L = plan->lv[l];
+    if (tid == 0) Sc.s[1] = 0;  // "not separated" flag (ordered by the scans' barriers)
+    int part = 0;
+    for (int c = tid; c < L.ncells; c += NT) part += cellcnt[(size_t)f * plan->ncells + L.cell_begin + c];
+    int n;
+    block_excl_scan<NT>(part, Sc.red, &n);
+    if (n > NK) {
+        if (tid == 0) q.list_out[atomicAdd(q.cnt_out, 1)] = (f << 4) | l;
+        return;
+    }
+    uint32_t *K = reinterpret_cast<uint32_t *>(smem + Lay::kK);
+    uint32_t *c0 = reinterpret_cast<uint32_t *>(smem + Lay::kCode0);
+    uint16_t *i0 = reinterpret_cast<uint16_t *>(smem + Lay::kIdx0);
+    uint32_t *c1 = reinterpret_cast<uint32_t *>(smem + Lay::kCode1);
+    uint16_t *i1 = reinterpret_cast<uint16_t *>(smem + Lay::kIdx1);
+    int8_t *Lc = reinterpret_cast<int8_t *>(smem + Lay::kLc);
+    static_assert(NK % NT == 0 && ((NK / NT) & (NK / NT - 1)) == 0, "NK = 64 x waves x a power of two");
+    oct::body<NC, NK, NT, NK / NT>(plan, L, l, f, smem, Sc, cellbuf, cellcnt, K, c0, i0, c1, i1, Lc, n, sel, selcnt,
+                                   err);
+}
+
+// First stage: one workgroup per (frame, level) of the launch group.
+template <int NC, int NK, int NT>
+__global__ __launch_bounds__(NT) void k_octree_paths(const Plan *__restrict__ plan,
+                                                      const uint32_t *__restrict__ cellbuf,
+                                                      const int *__restrict__ cellcnt, uint32_t *__restrict__ sel,
+                                                      int *__restrict__ selcnt, int *__restrict__ err, int level0,
+                                                      OctQueue q) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[oct::Layout<NC, NK, NT>::kBytes];
+    __shared__ oct::Scal Sc;
+    octree_task<NC, NK, NT>(plan, cellbuf, cellcnt, sel, selcnt, err, blockIdx.x, level0 + blockIdx.y, q, smem, Sc);
+}
+
+// Later stages: a persistent grid takes the previous stage's overflow tasks.
+template <int NC, int NK, int NT>
+__global__ __launch_bounds__(NT) void k_octree_paths_q(const Plan *__restrict__ plan,
+                                                        const uint32_t *__restrict__ cellbuf,
+                                                        const int *__restrict__ cellcnt, uint32_t *__restrict__ sel,
+                                                        int *__restrict__ selcnt, int *__restrict__ err, OctQueue q) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[oct::Layout<NC, NK, NT>::kBytes];
+    __shared__ oct::Scal Sc;
+    __shared__ int s_task;
+    const int count = *q.cnt_in;
+    while (true) {
+        __syncthreads();  // the previous task's LDS reads are done
+        if (threadIdx.x == 0) {
+            const int i = atomicAdd(q.taken_in, 1);
+            s_task = i < count ? q.list_in[i] : -1;
+        }
+        __syncthreads();
+        const int t = s_task;
+        if (t < 0) break;
+        octree_task<NC, NK, NT>(plan, cellbuf, cellcnt, sel, selcnt, err, t >> 4, t & 15, q, smem, Sc);
+    }
+}
+
+// Last stage (more keys than any LDS form holds: dense frames only): keys, codes and
+// L in the candidate scratch (8 + 8 B per slot in candA / candB), LSD radix sort.
+template <int NC, int NT>
+__global__ __launch_bounds__(NT) void k_octree_global(const Plan *__restrict__ plan,
+                                                       const uint32_t *__restrict__ cellbuf,
+                                                       const int *__restrict__ cellcnt, uint32_t *__restrict__ candA,
+                                                       uint32_t *__restrict__ candB, uint32_t *__restrict__ sel,
+                                                       int *__restrict__ selcnt, int *__restrict__ err, OctQueue q) {
+    constexpr int NK = NT;  // no keys in LDS; the layout's union region holds the lists
+    using Lay = oct::Layout<NC, NK, NT>;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[Lay::kBytes];
+    __shared__ oct::Scal Sc;
+    __shared__ int s_task;
+    const int tid = threadIdx.x;
+    const int count = *q.cnt_in;
+    while (true) {
+        __syncthreads();
+        if (tid == 0) {
+            const int i = atomicAdd(q.taken_in, 1);
+            s_task = i < count ? q.list_in[i] : -1;
+        }
+        __syncthreads();
+        const int t = s_task;
+        if (t < 0) break;
+        const int f = t >> 4, l = t & 15;
+        const LevelDesc &L = plan->lv[l];
+        if (tid == 0) Sc.s[1] = 0;
+        int part = 0;
+        for (int c = tid; c < L.ncells; c += NT) part += cellcnt[(size_t)f * plan->ncells + L.cell_begin + c];
+        int n;
+        block_excl_scan<NT>(part, Sc.red, &n);
+        if (n > 65535) {  // u16 positions / run lengths
+            if (tid == 0) {
+                selcnt[(size_t)f * plan->nlevels + l] = 0;
+                atomicOr(err, 1);
+            }
+            continue;
+        }
+        const size_t C = (size_t)L.cand_cap;
+        uint32_t *A = candA + 2 * ((size_t)f * plan->cand_total + L.cand_off);
+        uint32_t *B = candB + 2 * ((size_t)f * plan->cand_total + L.cand_off);
+        uint16_t *i0 = reinterpret_cast<uint16_t *>(B + C);
+        // L lives in code1's space once the sort is done with it
+        oct::body<NC, NK, NT, 0>(plan, L, l, f, smem, Sc, cellbuf, cellcnt, A, A + C, i0, B, i0 + C,
+                                 reinterpret_cast<int8_t *>(B), n, sel, selcnt, err);
+    }
+}
+
 
 // ---------------------------------------------------------------------------
 // Orientation (IC_Angle on the unblurred level, ORBextractor.cc:77-101) and
@@ -1316,14 +2123,17 @@ __device__ __forceinline__ int row16_sum(int v) {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 constexpr uint32_t kMagicBits = 0x4B000000u;  // bits of 2^23 (ulp 1 in [2^23, 2^24))
-constexpr int kPatchStride = 64;  // LDS row of a staged keypoint window: 4 x 16 B (window + 16-B misalignment)
-constexpr int kPatchBytes = 37 * kPatchStride;
+// LDS row of a staged keypoint window: the 13 dwords that hold the window's
+// 37 bytes at any 16-B misalignment (o + 37 <= 52).  An odd dword stride puts
+// 32 consecutive rows on 32 different banks (a 64-B stride folds every row onto
+// two bank offsets); rows are 4-B aligned, so they are written as dwords.
+constexpr int kPatchStride = 52;
+// slot per keypoint row: 37 rows, padded to 496 dwords (= 16 mod 32) so that the
+// two keypoints of a 32-lane group read complementary bank sets in the IC pass
+constexpr int kPatchBytes = 1984;
+static_assert(37 * kPatchStride <= kPatchBytes && (kPatchBytes / 4) % 32 == 16, "patch slot");
 
-// byte offset of row r in a swizzled window (Window::store<true>)
-__device__ __forceinline__ uint32_t patch_row_swz(uint32_t r) {
-    return r * kPatchStride + ((r >> 2) << 4);
-}
-static_assert(30 * kPatchStride + (30 >> 2) * 16 + kPatchStride <= kPatchBytes, "swizzled IC window fits the slot");
+__device__ __forceinline__ uint32_t patch_row_swz(uint32_t r) { return r * (uint32_t)kPatchStride; }
 
 // A keypoint window (rows cy-R .. cy-R+NROWS-1) as 4 lanes x 16 B per row, each
 // row the 64 B at ((img + (cy-R+r)*w + cx-R) & ~15): loaded into registers by
@@ -1348,19 +2158,23 @@ struct Window {
             v[k] = as_global(reinterpret_cast<const u32x4 *>(frame + o))[0];
         }
     }
-    // SWZ: row r at 64 r + 16 (r >> 2) (patch_row_swz), so that the 16 rows a
-    // keypoint's lanes read together fall on 16 different bank groups (a 64-B
-    // row stride alone puts rows r, r+4, r+8, ... on the same banks); rows stay
-    // 16-B aligned and never overlap (31 IC rows: 2,096 B <= the 37-row window)
-    template <bool SWZ>
+    // row r at 52 r: lane j of the row's four writes dwords 4j..4j+3 of the
+    // row's aligned 64 B, only the first 13 (lane 3: one)
     __device__ __forceinline__ void store(uint8_t *P, int s) const {
         const int j = s & 3, r0 = s >> 2;
 #pragma unroll
-        for (int k = 0; k + 1 < NK; k++)
-            *reinterpret_cast<u32x4 *>(P + (r0 + 4 * k) * kPatchStride + (SWZ ? 16 * k : 0) + 16 * j) = v[k];
-        if (r0 + 4 * (NK - 1) < NROWS)
-            *reinterpret_cast<u32x4 *>(P + (r0 + 4 * (NK - 1)) * kPatchStride + (SWZ ? 16 * (NK - 1) : 0) +
-                                       16 * j) = v[NK - 1];
+        for (int k = 0; k < NK; k++) {
+            const int r = r0 + 4 * k;
+            if (k + 1 < NK || r < NROWS) {
+                uint32_t *d = reinterpret_cast<uint32_t *>(P + r * kPatchStride + 16 * j);
+                d[0] = v[k].x;
+                if (j < 3) {
+                    d[1] = v[k].y;
+                    d[2] = v[k].z;
+                    d[3] = v[k].w;
+                }
+            }
+        }
         wave_lds_order();
     }
 };
@@ -1430,7 +2244,13 @@ struct IcWindow {
 #pragma unroll
         for (int k = 0; k < 6; k++) {
             const uint32_t ch = (uint32_t)(s + 16 * k), r = ch / 3u, j = ch - 3u * r;
-            if (k < 5 || ch < 93u) *reinterpret_cast<u32x4 *>(P + patch_row_swz(r) + 16u * j) = v[k];
+            if (k < 5 || ch < 93u) {
+                uint32_t *d = reinterpret_cast<uint32_t *>(P + patch_row_swz(r) + 16u * j);
+                d[0] = v[k].x;
+                d[1] = v[k].y;
+                d[2] = v[k].z;
+                d[3] = v[k].w;
+            }
         }
         wave_lds_order();
     }
@@ -1535,11 +2355,11 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     }
     // computeOrbDescriptor (ORBextractor.cc:105-149) on the blurred level
     wave_lds_order();  // IC taps read before the window is replaced
-    wdesc.store<false>(P, s);
+    wdesc.store(P, s);
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float ca, sb;
     glibc_sincosf(angle * factorPI, sb, ca);  // the reference's std::cos(float) / std::sin(float) = glibc cosf / sinf
-    // tap (dy, dx) at P + 64 r + o(r) + 18 + dx with r = 18 + dy, o(r) = (o0 + r w) & 15.
+    // tap (dy, dx) at P + 52 r + o(r) + 18 + dx with r = 18 + dy, o(r) = (o0 + r w) & 15.
     // GET_VALUE's rotation in packed fp32 (the same IEEE products and fused sums
     // as the reference's -O3 -march=native build, oracle/orb.c ygzo_orb_descriptor);
     // cvRound as + 2^23 + K: the sum stays in [2^23, 2^24) (ulp 1) for |v| <= 18.4,
@@ -1547,19 +2367,20 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     //   yb = bits(y + 2^23 + 64)     low bits 46 + r
     //   xb = bits(x + 2^23 + P + 64)
     //   o(r) = ((yb & 15) (w & 15) + c0) & 15 with c0 = (o0 - 46 w) & 15
-    //   address = (yb << 6) + xb + o(r) - kFix  ((yb << 6) leaves 0xC0000000 of the exponent)
+    //   address = mad_u24(yb, 52, xb) + o(r) - kFix  (the low 24 bits of yb are 46 + r: bit 23
+    //   of 2^23's exponent field is 0)
     const uint32_t o0 = (uint32_t)(uintptr_t)fblur + c - 18u * w - 18u;
     const uint32_t w16 = w & 15u;
     const uint32_t Pa = (uint32_t)(uintptr_t)(lds_u8 *)P;
     const uint32_t c0 = (o0 - 46u * w16) & 15u;
     const f32x2 magic = {__uint_as_float(kMagicBits + 64u), __uint_as_float(kMagicBits + Pa + 64u)};
-    constexpr uint32_t kFix = 0xC0000000u + kMagicBits + 46u * 64u + 64u - 18u;
+    constexpr uint32_t kFix = kMagicBits + 46u * (uint32_t)kPatchStride + 64u - 18u;
     const f32x2 rot_a = {sb, ca}, rot_b = {ca, -sb};
     auto tap = [&](float px, float py) -> uint32_t {
         const f32x2 m = (f32x2){py, py} * rot_b;
         const f32x2 yx = __builtin_elementwise_fma((f32x2){px, px}, rot_a, m) + magic;
         const uint32_t yb = __float_as_uint(yx.x), xb = __float_as_uint(yx.y);
-        const uint32_t a = (yb << 6) + xb, o = (yb & 15u) * w16 + c0;
+        const uint32_t a = mad24(yb, (uint32_t)kPatchStride, xb), o = (yb & 15u) * w16 + c0;
         return (uint32_t)*(const lds_u8 *)(uintptr_t)(a + (o & 15u) - kFix);
     };
     uint32_t bits = 0;
@@ -1739,40 +2560,68 @@ static int octree_nc(const LevelDesc &L) {
 #endif
 constexpr int kOctThreads = YGZ_OCT_THREADS;
 
+// queue words per launch group g: counters at octq[8 g ..] (list i: count 2i, taken
+// 2i + 1), lists at octq[kOctQHead + (3 g + i) T], T = frames x levels
+constexpr int kOctQHead = 64;
+size_t octree_queue_ints(const Plan &hp, int nframes) { return kOctQHead + (size_t)12 * nframes * hp.nlevels; }
+
 static hipError_t launch_octree_levels(int nc, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
                                        uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err,
-                                       int nframes, int l0, int nl, hipStream_t st, bool wide) {
+                                       int *octq, int g, int T, int nframes, int l0, int nl, hipStream_t st,
+                                       bool wide) {
     dim3 grid(nframes, nl);
+#ifdef YGZ_OCT_LEGACY
+    (void)octq; (void)g; (void)T;
+#define YGZ_OCT(NC, NK, NT) hipLaunchKernelGGL((k_octree<NC, NK, NT>), grid, dim3(NT), 0, st, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, l0)
     // one frame (the latency path): a workgroup per level has the CU to itself,
     // so the largest class takes 1024 threads (shorter strided loops per pass)
-    if (wide && nc > 512 && nc <= 1024) {
-        hipLaunchKernelGGL((k_octree<1024, 4000, 1024>), grid, dim3(1024), 0, st, dp, cellbuf, cellcnt, candA, candB,
-                           sel, selcnt, err, l0);
-        return hipGetLastError();
-    }
+    if (wide && nc > 512 && nc <= 1024) YGZ_OCT(1024, 4000, 1024);
     // LDS keys: 4000 with NC 1024 (two workgroups per CU), the larger levels' share below
-    if (nc <= 256)
-        hipLaunchKernelGGL((k_octree<256, 1536>), grid, dim3(256), 0, st, dp, cellbuf, cellcnt, candA, candB, sel,
-                           selcnt, err, l0);
-    else if (nc <= 512)
-        hipLaunchKernelGGL((k_octree<512, 3072, kOctThreads>), grid, dim3(kOctThreads), 0, st, dp, cellbuf, cellcnt,
-                           candA, candB, sel, selcnt, err, l0);
-    else if (nc <= 1024)
-        hipLaunchKernelGGL((k_octree<1024, 4000, kOctThreads>), grid, dim3(kOctThreads), 0, st, dp, cellbuf, cellcnt,
-                           candA, candB, sel, selcnt, err, l0);
-    else
-        hipLaunchKernelGGL((k_octree<2048, 4000, kOctThreads>), grid, dim3(kOctThreads), 0, st, dp, cellbuf, cellcnt,
-                           candA, candB, sel, selcnt, err, l0);
+    else if (nc <= 256) YGZ_OCT(256, 1536, 256);
+    else if (nc <= 512) YGZ_OCT(512, 3072, kOctThreads);
+    else if (nc <= 1024) YGZ_OCT(1024, 4000, kOctThreads);
+    else YGZ_OCT(2048, 4000, kOctThreads);
+#undef YGZ_OCT
+#else
+    // stage 0: one workgroup per task, sized for the class's usual candidate count;
+    // stage 1: 4,096 keys in LDS (512 threads); stage 2: 8,192 keys (1,024 threads,
+    // one workgroup per CU); stage 3: the global-scratch form
+    int *cq = octq + 8 * g;
+    int *lists = octq + kOctQHead + (size_t)3 * g * T;
+    const OctQueue q0{nullptr, nullptr, nullptr, cq + 0, lists};
+    const OctQueue q1{cq + 0, cq + 1, lists, cq + 2, lists + T};
+    const OctQueue q2{cq + 2, cq + 3, lists + T, cq + 4, lists + 2 * T};
+    const OctQueue q3{cq + 4, cq + 5, lists + 2 * T, nullptr, nullptr};
+    const int tasks = nframes * nl;
+#define YGZ_OCT(NC, NK, NT)                                                                                           \
+    do {                                                                                                              \
+        hipLaunchKernelGGL((k_octree_paths<NC, NK, NT>), grid, dim3(NT), 0, st, dp, cellbuf, cellcnt, sel, selcnt,     \
+                           err, l0, q0);                                                                              \
+        hipLaunchKernelGGL((k_octree_paths_q<NC, 4096, 512>), dim3(std::min(tasks, 512)), dim3(512), 0, st, dp,       \
+                           cellbuf, cellcnt, sel, selcnt, err, q1);                                                   \
+        hipLaunchKernelGGL((k_octree_paths_q<NC, 8192, 1024>), dim3(std::min(tasks, 256)), dim3(1024), 0, st, dp,     \
+                           cellbuf, cellcnt, sel, selcnt, err, q2);                                                   \
+        hipLaunchKernelGGL((k_octree_global<NC, 512>), dim3(std::min(tasks, 256)), dim3(512), 0, st, dp, cellbuf,     \
+                           cellcnt, candA, candB, sel, selcnt, err, q3);                                              \
+    } while (0)
+    if (wide && nc > 512 && nc <= 1024) YGZ_OCT(1024, 4096, 1024);
+    else if (nc <= 256) YGZ_OCT(256, 1024, 256);
+    else if (nc <= 512) YGZ_OCT(512, 2048, 256);
+    else if (nc <= 1024) YGZ_OCT(1024, 4096, 512);
+    else YGZ_OCT(2048, 4096, 512);
+#undef YGZ_OCT
+#endif
     return hipGetLastError();
 }
 
 // Levels grouped by node-pool class, each group one launch; groups after the
 // first run on the side streams (fork after, join before the caller's next work).
 hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
-                         uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int nframes,
-                         hipStream_t st, const hipStream_t *side, int nside, hipEvent_t fork, const hipEvent_t *join,
-                         bool wide) {
+                         uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int *octq,
+                         int nframes, hipStream_t st, const hipStream_t *side, int nside, hipEvent_t fork,
+                         const hipEvent_t *join, bool wide) {
     int l = 0, g = 0;
+    YGZ_HIPR(hipMemsetAsync(octq, 0, kOctQHead * sizeof(int), st));  // queue counters
     if (side && nside > 0) YGZ_HIPR(hipEventRecord(fork, st));  // before the first group: the groups are independent
     while (l < hp.nlevels) {
         const int nc = octree_nc(hp.lv[l]);
@@ -1783,8 +2632,8 @@ hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf
             s = side[g - 1];
             YGZ_HIPR(hipStreamWaitEvent(s, fork, 0));
         }
-        YGZ_HIPR(launch_octree_levels(nc, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, nframes, l, e - l, s,
-                                      wide));
+        YGZ_HIPR(launch_octree_levels(nc, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, octq, g,
+                                      nframes * hp.nlevels, nframes, l, e - l, s, wide));
         if (s != st) YGZ_HIPR(hipEventRecord(join[g - 1], s));
         l = e;
         g++;

@@ -17,10 +17,12 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
 hipError_t launch_fast_merged(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp,
                               const CellDesc *dcells, uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st,
                               int *clear_flag = nullptr);
+// octq: octree stage queues, octree_queue_ints(hp, nframes) ints (counters zeroed here)
 hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
-                         uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int nframes,
-                         hipStream_t st, const hipStream_t *side = nullptr, int nside = 0, hipEvent_t fork = nullptr,
-                         const hipEvent_t *join = nullptr, bool wide = false);
+                         uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err, int *octq,
+                         int nframes, hipStream_t st, const hipStream_t *side = nullptr, int nside = 0,
+                         hipEvent_t fork = nullptr, const hipEvent_t *join = nullptr, bool wide = false);
+size_t octree_queue_ints(const Plan &hp, int nframes);
 // keypoint rows + per-row orientation jobs (uint2 per selection slot: centre byte offset, w | level << 16)
 hipError_t launch_emit_kps(const Plan &hp, const Plan *dp, const uint32_t *sel, const int *selcnt,
                            const int *n_existing, ygzfe_kp *kps, int *counts, int row_cap, uint2 *ojobs, int nframes,

@@ -56,6 +56,48 @@ void ic_umax(int umax[16]) {
     }
 }
 
+// Path codes of k_octree_paths (extract.hip) as two tables per level: a key's code
+// is X[x] | Y[y].  The x part carries the complemented root column on top; depth d's
+// quadrant (bx | by << 1) goes at bits 30 - rb - 2d.., complemented at odd depths.
+// The division midpoints follow ExtractorNode::DivideNode (ORBextractor.cc:481-482,
+// ceil(half) of the integer extent) and the root columns DistributeOctTree
+// (:537-559, hX in float, x / hX truncated).
+static void octree_code_tables(LevelDesc &L, std::vector<int> *tabs) {
+    const int nIni = L.n_ini, H0 = L.max_by - kMinBorder;
+    const float hX = L.hX;
+    const int rb = nIni > 1 ? 32 - __builtin_clz((unsigned)(nIni - 1)) : 0;
+    const int ext = std::max((int)hX + 1, H0);
+    const int Dn = std::min(32 - __builtin_clz((unsigned)ext) + 2, (32 - rb) >> 1);
+    L.oct_rb = rb;
+    L.oct_dn = Dn;
+    L.oct_xtab = (int)tabs->size();
+    for (int x = 0; x <= L.max_bx - kMinBorder; x++) {
+        int idx = (int)((float)x / hX);
+        idx = idx >= nIni ? nIni - 1 : idx;
+        int x0 = (int)(hX * (float)idx), x1 = (int)(hX * (float)(idx + 1));
+        uint32_t code = rb ? (uint32_t)(nIni - 1 - idx) << (32 - rb) : 0u;
+        for (int d = 1, sh = 32 - rb - 2; d <= Dn; d++, sh -= 2) {
+            const int mx = x0 + ((x1 - x0 + 1) >> 1);
+            const bool bx = x >= mx;
+            (bx ? x0 : x1) = mx;
+            code |= (uint32_t)(bx ^ (d & 1)) << sh;
+        }
+        tabs->push_back((int)code);
+    }
+    L.oct_ytab = (int)tabs->size();
+    for (int y = 0; y <= H0; y++) {
+        int y0 = 0, y1 = H0;
+        uint32_t code = 0u;
+        for (int d = 1, sh = 32 - rb - 2; d <= Dn; d++, sh -= 2) {
+            const int my = y0 + ((y1 - y0 + 1) >> 1);
+            const bool by = y >= my;
+            (by ? y0 : y1) = my;
+            code |= (uint32_t)(by ^ (d & 1)) << (sh + 1);
+        }
+        tabs->push_back((int)code);
+    }
+}
+
 int build_plan(const ygzfe_orb_params &p, int W, int H, PlanHost *ph, char *err, size_t errlen) {
     Plan &P = ph->plan;
     memset(&P, 0, sizeof(P));
@@ -191,6 +233,7 @@ int build_plan(const ygzfe_orb_params &p, int W, int H, PlanHost *ph, char *err,
         }
         L.n_ini = nIni;
         L.hX = (float)(maxBX - minB) / nIni;
+        octree_code_tables(L, &ph->tabs);
         L.sel_cap = std::max(L.budget + 4, 4 * nIni + 4) + 8;
         L.sel_off = sel_total;
         sel_total += L.sel_cap;

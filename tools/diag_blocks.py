@@ -50,13 +50,10 @@ names = ({3: "entry->before loads", 4: "window loads landed (+LDS store)", 5: "I
           7: "descriptor done", 1: "end"} if kern == "1" else
          {3: "ROI staged", 4: "A: 4-point test", 5: "B: segment test", 6: "C: scores",
           7: "D: NMS (+retry)", 1: "end"} if kern == "2" else
-         {3: "gather keys", 4: "initial nodes", 5: "main loop", 1: "retain + end"} if kern == "3" else
+         {3: "gather keys", 4: "codes + radix sort", 5: "L, histograms, list", 6: "final rounds",
+          1: "retain + end"} if kern == "3" else
          {3: "entry .. before the passes", 4: "pass 1", 5: "pass 2", 6: "pass 3", 7: "pass 4",
           1: "later passes + retain + end"})
-if kern == "3":
-    passes = st[:, 6].astype(np.int64)
-    print("octree passes per L0 block: p50 %d p90 %d max %d" % (np.median(passes), np.percentile(passes, 90), passes.max()))
-    st[:, 6] = 0
 prev = st[:, 0]
 for k in (3, 4, 5, 6, 7, 1):
     if k not in names:
