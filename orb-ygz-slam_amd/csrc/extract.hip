@@ -138,6 +138,81 @@ __global__ __launch_bounds__(256) void k_resize_linear(uint8_t *__restrict__ pyr
     pyr[(size_t)f * pitch + D.off + (size_t)y * D.w + x] = (uint8_t)clampi(v, 0, 255);
 }
 
+// Every INTER_LINEAR level from l0 on in one launch, one workgroup per frame (the
+// batch path): level l is formed from level l-1 by the whole workgroup, four output
+// pixels per thread per step, a barrier between levels.  The frame's levels
+// (~1 MB for C4) stay in the CU's L1 / the XCD's L2 between levels.  A thread's four
+// pixels x0..x0+3 need source bytes [sx0, sx3 + 1] of two rows, at most 9 bytes
+// from the dword below sx0: three dword loads per row; same arithmetic as
+// k_resize_linear.
+__device__ __forceinline__ uint32_t pair_at(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t o) {
+    // bytes o, o + 1 (o <= 8) of d2:d1:d0 in the low 16 bits
+    const uint32_t lo = o < 4 ? d0 : (o < 8 ? d1 : d2), hi = o < 4 ? d1 : d2;
+    return __builtin_amdgcn_alignbyte(hi, lo, o & 3u) & 0xFFFFu;
+}
+
+__global__ __launch_bounds__(1024) void k_pyramid_linear_chain(uint8_t *__restrict__ pyr, uint32_t pitch,
+                                                               const Plan *__restrict__ plan,
+                                                               const int *__restrict__ tabs, int l0) {
+    // the level's tables in LDS: x {sx, a0 | a1 << 16} (w <= 2048), y {ya, yb, b0 | b1 << 16} (h <= 2048)
+    __shared__ int2 s_xt[2048];
+    __shared__ int s_yt[3 * 2048];
+    uint8_t *fr = pyr + (size_t)blockIdx.x * pitch;
+    for (int l = l0; l < plan->nlevels; l++) {
+        const LevelDesc &S = plan->lv[l - 1];
+        const LevelDesc &D = plan->lv[l];
+        for (int i = threadIdx.x; i < D.w; i += 1024)
+            s_xt[i] = make_int2(tabs[D.xtab_off + 2 * i], tabs[D.xtab_off + 2 * i + 1]);
+        for (int i = threadIdx.x; i < 3 * D.h; i += 1024) s_yt[i] = tabs[D.ytab_off + i];
+        __syncthreads();  // tables in; level l - 1 complete (workgroup scope: one CU's L1)
+        const int gw = (D.w + 3) >> 2, ng = gw * D.h;
+        const uint8_t *src = fr + S.off;
+        uint8_t *dst = fr + D.off;
+#pragma unroll 2
+        for (int g = threadIdx.x; g < ng; g += 1024) {
+            const int y = g / gw, x0 = (g - y * gw) * 4;
+            const int ya = s_yt[3 * y], yb = s_yt[3 * y + 1], bw = s_yt[3 * y + 2];
+            const int b0 = (int)(int16_t)(bw & 0xFFFF), b1 = (int)(int16_t)(bw >> 16);
+            const int sx0 = s_xt[x0].x;
+            const uint32_t base = (uint32_t)sx0 & ~3u;
+            const uint32_t sa = (uint32_t)((size_t)ya * S.w & 3), sb = (uint32_t)((size_t)yb * S.w & 3);
+            const uint32_t *ra = reinterpret_cast<const uint32_t *>(src + (size_t)ya * S.w + base - sa);
+            const uint32_t *rb = reinterpret_cast<const uint32_t *>(src + (size_t)yb * S.w + base - sb);
+            const uint4 wa = make_uint4(ra[0], ra[1], ra[2], ra[3]);
+            const uint4 wb = make_uint4(rb[0], rb[1], rb[2], rb[3]);
+            uint32_t out = 0u;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int x = x0 + i;
+                const int2 xt = s_xt[x < D.w ? x : x0];
+                const int sx = xt.x;
+                const int a0 = (int)(int16_t)(xt.y & 0xFFFF), a1 = (int)(int16_t)(xt.y >> 16);
+                // byte offsets of sx inside the dword windows of the two rows
+                const uint32_t oa = (uint32_t)(sx - (int)base) + sa, ob = (uint32_t)(sx - (int)base) + sb;
+                const uint32_t pa = oa < 8 ? pair_at(wa.x, wa.y, wa.z, oa) : pair_at(wa.y, wa.z, wa.w, oa - 4);
+                const uint32_t pb = ob < 8 ? pair_at(wb.x, wb.y, wb.z, ob) : pair_at(wb.y, wb.z, wb.w, ob - 4);
+                int r0, r1;
+                if (x < D.xmax) {
+                    r0 = (int)(pa & 0xFF) * a0 + (int)(pa >> 8) * a1;
+                    r1 = (int)(pb & 0xFF) * a0 + (int)(pb >> 8) * a1;
+                } else {
+                    r0 = (int)(pa & 0xFF) * 2048;
+                    r1 = (int)(pb & 0xFF) * 2048;
+                }
+                const int v = (b0 * r0 + b1 * r1 + (1 << 21)) >> 22;
+                out |= (uint32_t)clampi(v, 0, 255) << (8 * i);
+            }
+            uint8_t *o = dst + (size_t)y * D.w + x0;
+            if (x0 + 4 <= D.w && (((uintptr_t)o & 3) == 0)) {
+                *reinterpret_cast<uint32_t *>(o) = out;
+            } else {
+                for (int i = 0; i < 4 && x0 + i < D.w; i++) o[i] = (uint8_t)(out >> (8 * i));
+            }
+        }
+        __syncthreads();  // level l complete and the tables free before the next level
+    }
+}
+
 // ---------------------------------------------------------------------------
 // GaussianBlur 7x7 sigma=2, BORDER_REFLECT_101, 8-bit fixed point:
 //   dst = sat8((sum_v k_v * (sum_h k_h * p) + 2^15) >> 16)
@@ -1289,29 +1364,34 @@ __device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) -
 template <int NT>
 constexpr int nwaves() { return NT / 64; }
 
-// LDS carve-up.  Sort phase: K | code0 | idx0 | {code1, idx1, hist}.  After the sort
-// (which always ends in buffer 0) the second region holds L and the node lists.
-template <int NC, int NK, int NT>
-struct Layout {
-    static constexpr int kK = 0;
-    static constexpr int kCode0 = kK + 4 * NK;
-    static constexpr int kIdx0 = kCode0 + 4 * NK;
-    static constexpr int kU = (kIdx0 + 2 * NK + 15) & ~15;
-    // sort phase
-    static constexpr int kCode1 = kU;
-    static constexpr int kIdx1 = kCode1 + 4 * NK;
-    static constexpr int kHist = (kIdx1 + 2 * NK + 15) & ~15;
-    static constexpr int kSortEnd = kHist + 4 * 256 * nwaves<NT>();
-    // list phase
-    static constexpr int kNode = kU;                     // u32 [2][NC]: start | len << 16
+// LDS of the list phase (from lsm): node lists, final-round scratch, then (kernel
+// k_octree_list only) L of the sorted keys
+template <int NC>
+struct ListLayout {
+    static constexpr int kNode = 0;                      // u32 [2][NC]: start | len << 16
     static constexpr int kDep = kNode + 8 * NC;          // u8  [2][NC]: depth | processed << 7
     static constexpr int kCk = (kDep + 2 * NC + 15) & ~15;  // u32 [NC + 4]: candidate sort keys
     static constexpr int kCe = kCk + 4 * NC + 16;        // u16 [NC]: children per candidate
     static constexpr int kCi = kCe + 2 * NC;             // u16 [NC]: inclusive children prefix
     static constexpr int kHs = kCi + 2 * NC;             // u16 [NC + 2]: sorted position of head r
     static constexpr int kNgr = kHs + 2 * NC + 4;        // u16 [NC]: list position -> head rank
-    static constexpr int kLc = (kNgr + 2 * NC + 15) & ~15;  // i8 [NK + 1]: L per sorted position (LDS keys)
-    static constexpr int kListEnd = kLc + NK + 16;
+    static constexpr int kLc = (kNgr + 2 * NC + 15) & ~15;
+    static constexpr int bytes(int nl) { return kLc + nl + 16; }
+};
+
+// LDS of the sort phase: K | code0 | idx0 | {code1, idx1, hist}; the list phase of the
+// global-scratch form uses the region from kU
+template <int NC, int NK, int NT>
+struct Layout {
+    static constexpr int kK = 0;
+    static constexpr int kCode0 = kK + 4 * NK;
+    static constexpr int kIdx0 = kCode0 + 4 * NK;
+    static constexpr int kU = (kIdx0 + 2 * NK + 15) & ~15;
+    static constexpr int kCode1 = kU;
+    static constexpr int kIdx1 = kCode1 + 4 * NK;
+    static constexpr int kHist = (kIdx1 + 2 * NK + 15) & ~15;
+    static constexpr int kSortEnd = kHist + 4 * 256 * nwaves<NT>();
+    static constexpr int kListEnd = kU + ListLayout<NC>::bytes(0);
     static constexpr int kBytes = (kSortEnd > kListEnd ? kSortEnd : kListEnd);
 };
 
@@ -1469,20 +1549,18 @@ __device__ __forceinline__ int lcp_depth(uint32_t a, uint32_t b, int rb) {
     return lz < rb ? -1 : (lz - rb) >> 1;
 }
 
-// K: keys in candidate order; code0/idx0 + code1/idx1: sort buffers; Lc: i8 [n+1]
+// Sort phase of one (frame, level): the keys in candidate order into K, sorted by
+// path code (code0 / idx0: codes and candidate indices in sorted order), L of the
+// sorted keys into Lc (i8 [n + 1]); Sc.s[1] = keys not separated (never, for
+// distinct pixels).  code1 / idx1: sort scratch.
 template <int NC, int NK, int NT, int RB, typename KP, typename CP, typename IP, typename LP>
-__device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelDesc &L, int l, int f, uint8_t *smem,
-                                     Scal &Sc, const uint32_t *__restrict__ cellbuf,
-                                     const int *__restrict__ cellcnt, KP K, CP code0, IP idx0, CP code1, IP idx1,
-                                     LP Lc, int n, uint32_t *__restrict__ sel, int *__restrict__ selcnt,
-                                     int *__restrict__ err) {
+__device__ __forceinline__ void body_sort(const Plan *__restrict__ plan, const LevelDesc &L, int l, int f,
+                                          uint8_t *smem, Scal &Sc, const uint32_t *__restrict__ cellbuf,
+                                          const int *__restrict__ cellcnt, KP K, CP code0, IP idx0, CP code1,
+                                          IP idx1, LP Lc, int n) {
     using Lay = Layout<NC, NK, NT>;
     constexpr int NW = nwaves<NT>();
     const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    if (tid < 16) {  // published by the gather's barriers
-        Sc.hL[tid] = 0;
-        Sc.hM[tid] = 0;
-    }
     // --- 1. vToDistributeKeys in cell order: every thread places its keys j = tid +
     //        NT u by branch-free binary searches over the cells' prefix (all steps of all
     //        its searches interleaved), then issues all their loads together
@@ -1603,47 +1681,47 @@ __device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelD
         }
     }
     if (l == 0) YGZ_BSTAMP_K(3, 4);
-    // --- 4. L per sorted position and the two histograms.  With the keys in LDS the
-    //        wave's chunks keep L_k and L_k+1 in registers for the sweeps below.
-    constexpr int CH = RB > 0 ? RB : 1;
-    int La[CH], Lb[CH];
-    const int nch = RB > 0 ? RB : (s1 - s0 + 63) / 64;
-    if constexpr (RB > 0) {
-#pragma unroll
-        for (int i = 0; i < CH; i++) {
-            const int k = s0 + 64 * i + lane;
-            La[i] = Lb[i] = -1;
-            if (k < s1) {
-                const uint32_t c = code0[k];
-                if (k > 0) La[i] = lcp_depth(code0[k - 1], c, rb);
-                if (k + 1 < n) Lb[i] = lcp_depth(c, code0[k + 1], rb);
-                if (La[i] >= Dn || (k > 0 && code0[k - 1] == c)) Sc.s[1] = 1;
-                Lc[k] = (int8_t)La[i];
-            }
+    // --- 4. L_k = depth of the common prefix of sorted keys k-1 and k (-1: root differs)
+    for (int k = tid; k <= n; k += NT) {
+        int v = -1;
+        if (k > 0 && k < n) {
+            const uint32_t a = code0[k - 1], c = code0[k];
+            v = lcp_depth(a, c, rb);
+            if (v >= Dn || a == c) Sc.s[1] = 1;
         }
-        if (tid == 0) Lc[n] = -1;
-    } else {
-        for (int k = tid; k <= n; k += NT) {
-            int v = -1;
-            if (k > 0 && k < n) {
-                v = lcp_depth(code0[k - 1], code0[k], rb);
-                if (v >= Dn || code0[k - 1] == code0[k]) Sc.s[1] = 1;
-            }
-            Lc[k] = (int8_t)v;
-        }
-        __syncthreads();
+        Lc[k] = (int8_t)v;
     }
+    __syncthreads();
+}
+
+// List phase of one (frame, level) after the sort: the main loop's pass count and
+// list from the histograms of L, the final rounds, the retained keys.  Lc: L of the
+// sorted keys (i8 [n + 1]); key_at(k) -> {key, candidate index} of sorted key k;
+// lsm: ListLayout<NC> (L not in it).
+template <int NC, int NT, typename LP, typename KF>
+__device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const LevelDesc &L, int l, int f,
+                                          uint8_t *lsm, Scal &Sc, LP Lc, int n, int bad, KF key_at,
+                                          uint32_t *__restrict__ sel, int *__restrict__ selcnt,
+                                          int *__restrict__ err) {
+    using Lay = ListLayout<NC>;
+    constexpr int NW = nwaves<NT>();
+    const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const int Dn = L.oct_dn;
+    const int seg = (((n + NW - 1) / NW) + 63) & ~63;
+    const int s0 = min(n, w * seg), s1 = min(n, s0 + seg);
+    const int nch = (s1 - s0 + 63) / 64;
+    if (tid < 16) {
+        Sc.hL[tid] = 0;
+        Sc.hM[tid] = 0;
+    }
+    __syncthreads();
     auto chunk_ab = [&](int i, int k, int &a, int &b) {
-        if constexpr (RB > 0) {
-            a = La[i];
-            b = Lb[i];
-        } else {
-            a = Lc[k];
-            b = Lc[k + 1];
-        }
+        (void)i;
+        a = Lc[k];
+        b = Lc[k + 1];
     };
 #pragma unroll
-    for (int i = 0; i < (RB > 0 ? RB : 1 << 30) && i < nch; i++) {
+    for (int i = 0; i < nch; i++) {
         const int k = s0 + 64 * i + lane;
         const bool v = k < s1;
         int a = 0, m = 0;
@@ -1660,7 +1738,6 @@ __device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelD
         if (v && (pm & lanes_below()) == 0) atomicAdd(&Sc.hM[m], __popcll(pm));
     }
     __syncthreads();
-    int bad = Sc.s[1];
     // P: the pass that ends the main loop; final = the final rounds follow
     const int N = L.budget;
     int P = 0, final_round = 0;
@@ -1678,10 +1755,10 @@ __device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelD
     }
     bad |= P >= Dn;
     // --- 5. the list after P passes: heads (L_k < P), sections e = min(m_k + 1, P)
-    uint32_t *node = reinterpret_cast<uint32_t *>(smem + Lay::kNode);
-    uint8_t *ndep = smem + Lay::kDep;
-    uint16_t *hs = reinterpret_cast<uint16_t *>(smem + Lay::kHs);
-    uint16_t *ngr = reinterpret_cast<uint16_t *>(smem + Lay::kNgr);
+    uint32_t *node = reinterpret_cast<uint32_t *>(lsm + Lay::kNode);
+    uint8_t *ndep = lsm + Lay::kDep;
+    uint16_t *hs = reinterpret_cast<uint16_t *>(lsm + Lay::kHs);
+    uint16_t *ngr = reinterpret_cast<uint16_t *>(lsm + Lay::kNgr);
     auto chunk_sec = [&](int i, int k) -> int {
         int sec = -1;
         if (k < s1) {
@@ -1691,66 +1768,75 @@ __device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelD
         }
         return sec;
     };
-    // sweep A: per wave, heads and heads per section (lane e counts section e)
+    // sweep A: per wave, heads per section (lanes matched on their section; the run's
+    // leader adds its count)
+    if (tid < 16 * NW) (&Sc.wcnt[0][0])[tid] = 0;
+    __syncthreads();
     {
-        int wc = 0, wh = 0;
+        int wh = 0;
 #pragma unroll
-        for (int i = 0; i < (RB > 0 ? RB : 1 << 30) && i < nch; i++) {
+        for (int i = 0; i < nch; i++) {
             const int sec = chunk_sec(i, s0 + 64 * i + lane);
-            wh += __popcll(__ballot(sec >= 0));
-            for (int e = 0; e <= P; e++) {
-                const int c = __popcll(__ballot(sec == e));
-                wc += lane == e ? c : 0;
-            }
+            const uint64_t hb = __ballot(sec >= 0);
+            wh += __popcll(hb);
+            const uint64_t peers = match_bits((uint32_t)(sec + 1), 4, hb);
+            if (sec >= 0 && (peers & lanes_below()) == 0) Sc.wcnt[w][sec] += __popcll(peers);
         }
-        if (lane < 16) Sc.wcnt[w][lane] = wc;
         if (lane == 0) Sc.whead[w] = wh;
     }
     __syncthreads();
-    // lane e: section e's count, its list base (sections P..0 in descending order)
-    // and this wave's running rank inside it
-    int nheads = 0, hbase = 0, scnt = 0, srun = 0;
+    // section e (e <= P): its count, its list base (sections P..0 descending), and this
+    // wave's running rank inside it (LDS, per wave)
+    int nheads = 0, hbase = 0;
     for (int ww = 0; ww < NW; ww++) {
         const int h = Sc.whead[ww];
         hbase += ww < w ? h : 0;
         nheads += h;
-        const int x = lane < 16 ? Sc.wcnt[ww][lane] : 0;
-        srun += ww < w ? x : 0;
-        scnt += x;
     }
-    int sbase = 0;  // sum over sections above this lane's
+    int front0 = 0;
     {
-        int acc = 0;
+        int scnt = 0, srun = 0;
+        if (lane < 16)
+            for (int ww = 0; ww < NW; ww++) {
+                const int x = Sc.wcnt[ww][lane];
+                srun += ww < w ? x : 0;
+                scnt += x;
+            }
+        int acc = 0, sbase = 0;
         for (int e = 15; e >= 0; e--) {
             const int c = __builtin_amdgcn_readlane(scnt, e);
             sbase = lane == e ? acc : sbase;
             acc += c;
         }
+        front0 = __builtin_amdgcn_readlane(scnt, P);
+        __syncthreads();  // every wave has read wcnt
+        if (lane < 16) {
+            Sc.wcnt[w][lane] = srun;  // now: this wave's running rank in section lane
+            if (w == 0) {
+                Sc.hL[lane] = sbase;  // reused: section base / count
+                Sc.hM[lane] = scnt;
+            }
+        }
+        __syncthreads();
     }
-    const int front0 = __builtin_amdgcn_readlane(scnt, P);
     int overflow = bad || nheads > NC;
     if (!overflow) {
         int hr = hbase;
 #pragma unroll
-        for (int i = 0; i < (RB > 0 ? RB : 1 << 30) && i < nch; i++) {
+        for (int i = 0; i < nch; i++) {
             const int k = s0 + 64 * i + lane;
             const int sec = chunk_sec(i, k);
             const uint64_t hb = __ballot(sec >= 0);
             const int gr = hr + __popcll(hb & lanes_below());
             hr += __popcll(hb);
-            int rank = 0, bse = 0, ce = 0;
-            for (int e = 0; e <= P; e++) {  // e uniform: lane-e values by readlane
-                const uint64_t b = __ballot(sec == e);
-                const int r0 = __builtin_amdgcn_readlane(srun, e);
-                const int b0 = __builtin_amdgcn_readlane(sbase, e), c0 = __builtin_amdgcn_readlane(scnt, e);
-                if (sec == e) {
-                    rank = r0 + __popcll(b & lanes_below());
-                    bse = b0;
-                    ce = c0;
-                }
-                srun += lane == e ? __popcll(b) : 0;
-            }
+            const uint64_t peers = match_bits((uint32_t)(sec + 1), 4, hb);
+            const int q = sec < 0 ? 0 : sec;
+            const int r0 = Sc.wcnt[w][q];
             if (sec >= 0) {
+                const uint64_t below = peers & lanes_below();
+                const int rank = r0 + __popcll(below);
+                if (below == 0) Sc.wcnt[w][q] = r0 + __popcll(peers);
+                const int bse = Sc.hL[q], ce = Sc.hM[q];
                 const int pos = bse + ((sec & 1) ? rank : ce - 1 - rank);
                 hs[gr] = (uint16_t)k;
                 ngr[pos] = (uint16_t)gr;
@@ -1772,9 +1858,9 @@ __device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelD
     if (l == 0) YGZ_BSTAMP_K(3, 5);
     // --- 6. final rounds
     int cur = 0, front = front0;
-    uint32_t *ck = reinterpret_cast<uint32_t *>(smem + Lay::kCk);
-    uint16_t *cev = reinterpret_cast<uint16_t *>(smem + Lay::kCe);
-    uint16_t *cin = reinterpret_cast<uint16_t *>(smem + Lay::kCi);
+    uint32_t *ck = reinterpret_cast<uint32_t *>(lsm + Lay::kCk);
+    uint16_t *cev = reinterpret_cast<uint16_t *>(lsm + Lay::kCe);
+    uint16_t *cin = reinterpret_cast<uint16_t *>(lsm + Lay::kCi);
     int guard = 0;
     while (final_round && !overflow) {
         const int prevSize = size;
@@ -1802,11 +1888,14 @@ __device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelD
                 mine[u] = tid + u * NT < nc ? ck[tid + u * NT] : 0xFFFFFFFFu;
                 rk[u] = 0;
             }
-#pragma unroll 2
-            for (int j = 0; j < (w * 64 < nc ? nc : 0); j += 4) {  // waves holding no candidate skip
-                const uint4 v = *reinterpret_cast<const uint4 *>(ck + j);
 #pragma unroll
-                for (int u = 0; u < kPer; u++) rk[u] += (v.x < mine[u]) + (v.y < mine[u]) + (v.z < mine[u]) + (v.w < mine[u]);
+            for (int u = 0; u < kPer; u++) {
+                if (u * NT + w * 64 >= nc) break;  // wave-uniform: slots past the candidates skip
+#pragma unroll 2
+                for (int j = 0; j < nc; j += 4) {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(ck + j);
+                    rk[u] += (v.x < mine[u]) + (v.y < mine[u]) + (v.z < mine[u]) + (v.w < mine[u]);
+                }
             }
             __syncthreads();
 #pragma unroll
@@ -1822,7 +1911,7 @@ __device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelD
             const uint32_t r = nd[p];
             const int st = (int)(r & 0xFFFFu), ln = (int)(r >> 16), dep = dd[p] & 0x7F;
             int e = 1;
-            if constexpr (RB > 0) {
+            if constexpr (true) {
                 const uint32_t rep = 0x01010101u * (uint32_t)dep;
                 const int k0 = st + 1, k1 = st + ln;  // [k0, k1)
                 for (int a = k0 & ~3; a < k1; a += 4) {
@@ -1833,8 +1922,6 @@ __device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelD
                     if (hi < 4) z &= 0xFFFFFFFFu >> (8 * (4 - hi));
                     e += __popc(z);
                 }
-            } else {
-                for (int k = st + 1; k < st + ln; k++) e += Lc[k] == dep;
             }
             cev[c] = (uint16_t)e;
         }
@@ -1913,13 +2000,15 @@ __device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelD
         for (int i = tid; i < size; i += NT) {
             const uint32_t r = nd[i];
             const int st = (int)(r & 0xFFFFu), ln = (int)(r >> 16);
-            uint32_t best = 0u;
+            uint32_t best = 0u, bkey = 0u;
             for (int k = st; k < st + ln; k++) {
-                const uint32_t ix = idx0[k];
-                const uint32_t v = ((uint32_t)key_score(K[ix]) << 24) | (0xFFFFFFu - ix);
+                uint32_t kv, ix;
+                key_at(k, kv, ix);
+                const uint32_t v = ((uint32_t)key_score(kv) << 24) | (0xFFFFFFu - ix);
+                bkey = v > best ? kv : bkey;
                 best = v > best ? v : best;
             }
-            out[i] = K[0xFFFFFFu - (best & 0xFFFFFFu)];
+            out[i] = bkey;
         }
     }
     if (tid == 0) {
@@ -1932,8 +2021,8 @@ __device__ __forceinline__ void body(const Plan *__restrict__ plan, const LevelD
 
 }  // namespace oct
 
-// Work queues between the octree stages of one node-pool class (api.cpp zeroes the
-// counters before each extraction): a task (f << 4 | l) whose level has more
+// Work queues between the octree sort stages of one node-pool class (api.cpp zeroes
+// the counters before each extraction): a task (f << 4 | l) whose level has more
 // candidates than a stage's LDS holds is appended to the next stage's list.
 struct OctQueue {
     int *cnt_in, *taken_in;
@@ -1941,12 +2030,28 @@ struct OctQueue {
     int *cnt_out, *list_out;
 };
 
-// One (frame, level) task with keys, codes and L in LDS (at most NK candidates).
+// Sorted-key scratch of a task in the candidate scratch: sorted keys Ks (u32 [C],
+// candA), their candidate indices Is (u16 [C], candB) and L (i8 [C + 1], candB + 4 C).
+struct OctScratch {
+    uint32_t *Ks;
+    uint16_t *Is;
+    int8_t *Lg;
+    __device__ OctScratch(const Plan *plan, const LevelDesc &L, uint32_t *candA, uint32_t *candB, int f) {
+        const size_t slot = 2 * ((size_t)f * plan->cand_total + L.cand_off), C = (size_t)L.cand_cap;
+        Ks = candA + slot;
+        Is = reinterpret_cast<uint16_t *>(candB + slot);
+        Lg = reinterpret_cast<int8_t *>(candB + slot + C);
+    }
+};
+
+// Sort stage of one (frame, level) with keys, codes and indices in LDS (at most NK
+// candidates): sorted keys, indices and L to the scratch, hdr = n + 1 | bad << 30
+// (0: the task went on to a later stage).
 template <int NC, int NK, int NT>
-__device__ __forceinline__ void octree_task(const Plan *__restrict__ plan, const uint32_t *__restrict__ cellbuf,
-                                            const int *__restrict__ cellcnt, uint32_t *__restrict__ sel,
-                                            int *__restrict__ selcnt, int *__restrict__ err, int f, int l,
-                                            const OctQueue &q, uint8_t *smem, oct::Scal &Sc) {
+__device__ __forceinline__ void octree_sort_task(const Plan *__restrict__ plan, const uint32_t *__restrict__ cellbuf,
+                                                 const int *__restrict__ cellcnt, uint32_t *__restrict__ candA,
+                                                 uint32_t *__restrict__ candB, int *__restrict__ hdr, int f, int l,
+                                                 const OctQueue &q, uint8_t *smem, oct::Scal &Sc) {
     using Lay = oct::Layout<NC, NK, NT>;
     const int tid = threadIdx.x;
     if (l == 0) YGZ_BSTAMP_K(3, 0);
@@ -1956,8 +2061,12 @@ __device__ __forceinline__ void octree_task(const Plan *__restrict__ plan, const
     for (int c = tid; c < L.ncells; c += NT) part += cellcnt[(size_t)f * plan->ncells + L.cell_begin + c];
     int n;
     block_excl_scan<NT>(part, Sc.red, &n);
+    const size_t t = (size_t)f * plan->nlevels + l;
     if (n > NK) {
-        if (tid == 0) q.list_out[atomicAdd(q.cnt_out, 1)] = (f << 4) | l;
+        if (tid == 0) {
+            hdr[t] = 0;
+            q.list_out[atomicAdd(q.cnt_out, 1)] = (f << 4) | l;
+        }
         return;
     }
     uint32_t *K = reinterpret_cast<uint32_t *>(smem + Lay::kK);
@@ -1965,30 +2074,35 @@ __device__ __forceinline__ void octree_task(const Plan *__restrict__ plan, const
     uint16_t *i0 = reinterpret_cast<uint16_t *>(smem + Lay::kIdx0);
     uint32_t *c1 = reinterpret_cast<uint32_t *>(smem + Lay::kCode1);
     uint16_t *i1 = reinterpret_cast<uint16_t *>(smem + Lay::kIdx1);
-    int8_t *Lc = reinterpret_cast<int8_t *>(smem + Lay::kLc);
     static_assert(NK % NT == 0 && ((NK / NT) & (NK / NT - 1)) == 0, "NK = 64 x waves x a power of two");
-    oct::body<NC, NK, NT, NK / NT>(plan, L, l, f, smem, Sc, cellbuf, cellcnt, K, c0, i0, c1, i1, Lc, n, sel, selcnt,
-                                   err);
+    const OctScratch o(plan, L, candA, candB, f);
+    oct::body_sort<NC, NK, NT, NK / NT>(plan, L, l, f, smem, Sc, cellbuf, cellcnt, K, c0, i0, c1, i1, o.Lg, n);
+    for (int k = tid; k < n; k += NT) {
+        const uint16_t ix = i0[k];
+        o.Ks[k] = K[ix];
+        o.Is[k] = ix;
+    }
+    if (tid == 0) hdr[t] = (n + 1) | (Sc.s[1] << 30);
 }
 
-// First stage: one workgroup per (frame, level) of the launch group.
+// First sort stage: one workgroup per (frame, level) of the launch group.
 template <int NC, int NK, int NT>
-__global__ __launch_bounds__(NT) void k_octree_paths(const Plan *__restrict__ plan,
-                                                      const uint32_t *__restrict__ cellbuf,
-                                                      const int *__restrict__ cellcnt, uint32_t *__restrict__ sel,
-                                                      int *__restrict__ selcnt, int *__restrict__ err, int level0,
-                                                      OctQueue q) {
+__global__ __launch_bounds__(NT) void k_octree_sort(const Plan *__restrict__ plan, const uint32_t *__restrict__ cellbuf,
+                                                     const int *__restrict__ cellcnt, uint32_t *__restrict__ candA,
+                                                     uint32_t *__restrict__ candB, int *__restrict__ hdr, int level0,
+                                                     OctQueue q) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[oct::Layout<NC, NK, NT>::kBytes];
     __shared__ oct::Scal Sc;
-    octree_task<NC, NK, NT>(plan, cellbuf, cellcnt, sel, selcnt, err, blockIdx.x, level0 + blockIdx.y, q, smem, Sc);
+    octree_sort_task<NC, NK, NT>(plan, cellbuf, cellcnt, candA, candB, hdr, blockIdx.x, level0 + blockIdx.y, q, smem,
+                                 Sc);
 }
 
-// Later stages: a persistent grid takes the previous stage's overflow tasks.
+// Later sort stages: a persistent grid takes the previous stage's overflow tasks.
 template <int NC, int NK, int NT>
-__global__ __launch_bounds__(NT) void k_octree_paths_q(const Plan *__restrict__ plan,
-                                                        const uint32_t *__restrict__ cellbuf,
-                                                        const int *__restrict__ cellcnt, uint32_t *__restrict__ sel,
-                                                        int *__restrict__ selcnt, int *__restrict__ err, OctQueue q) {
+__global__ __launch_bounds__(NT) void k_octree_sort_q(const Plan *__restrict__ plan,
+                                                       const uint32_t *__restrict__ cellbuf,
+                                                       const int *__restrict__ cellcnt, uint32_t *__restrict__ candA,
+                                                       uint32_t *__restrict__ candB, int *__restrict__ hdr, OctQueue q) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[oct::Layout<NC, NK, NT>::kBytes];
     __shared__ oct::Scal Sc;
     __shared__ int s_task;
@@ -2002,12 +2116,40 @@ __global__ __launch_bounds__(NT) void k_octree_paths_q(const Plan *__restrict__ 
         __syncthreads();
         const int t = s_task;
         if (t < 0) break;
-        octree_task<NC, NK, NT>(plan, cellbuf, cellcnt, sel, selcnt, err, t >> 4, t & 15, q, smem, Sc);
+        octree_sort_task<NC, NK, NT>(plan, cellbuf, cellcnt, candA, candB, hdr, t >> 4, t & 15, q, smem, Sc);
     }
 }
 
+// List phase of every sorted task of the launch group: L staged into LDS, the node
+// lists in LDS (~31 KB at NC 1024: five workgroups per CU where the sort holds two).
+template <int NC, int NT>
+__global__ __launch_bounds__(NT) void k_octree_list(const Plan *__restrict__ plan, uint32_t *__restrict__ candA,
+                                                     uint32_t *__restrict__ candB, const int *__restrict__ hdr,
+                                                     uint32_t *__restrict__ sel, int *__restrict__ selcnt,
+                                                     int *__restrict__ err, int level0) {
+    using Lay = oct::ListLayout<NC>;
+    __shared__ __attribute__((aligned(16))) uint8_t lsm[Lay::bytes(8192 + 4)];
+    __shared__ oct::Scal Sc;
+    const int f = blockIdx.x, l = level0 + blockIdx.y, tid = threadIdx.x;
+    const int h = hdr[(size_t)f * plan->nlevels + l];
+    if (h == 0) return;  // left to the global-scratch stage
+    const int n = (h & 0x3FFFFFFF) - 1, bad = (h >> 30) & 1;
+    const LevelDesc &L = plan->lv[l];
+    const OctScratch o(plan, L, candA, candB, f);
+    int8_t *Lc = reinterpret_cast<int8_t *>(lsm + Lay::kLc);
+    for (int i = tid; i <= n >> 2; i += NT)
+        reinterpret_cast<uint32_t *>(Lc)[i] = as_global(reinterpret_cast<const uint32_t *>(o.Lg))[i];
+    // (body_list's first barrier publishes L)
+    auto key_at = [&](int k, uint32_t &kv, uint32_t &ix) {
+        kv = as_global(o.Ks)[k];
+        ix = as_global(o.Is)[k];
+    };
+    oct::body_list<NC, NT>(plan, L, l, f, lsm, Sc, Lc, n, bad, key_at, sel, selcnt, err);
+}
+
 // Last stage (more keys than any LDS form holds: dense frames only): keys, codes and
-// L in the candidate scratch (8 + 8 B per slot in candA / candB), LSD radix sort.
+// L in the candidate scratch (8 + 8 B per slot in candA / candB), LSD radix sort, then
+// the list phase, in one workgroup.
 template <int NC, int NT>
 __global__ __launch_bounds__(NT) void k_octree_global(const Plan *__restrict__ plan,
                                                        const uint32_t *__restrict__ cellbuf,
@@ -2048,9 +2190,13 @@ __global__ __launch_bounds__(NT) void k_octree_global(const Plan *__restrict__ p
         uint32_t *A = candA + 2 * ((size_t)f * plan->cand_total + L.cand_off);
         uint32_t *B = candB + 2 * ((size_t)f * plan->cand_total + L.cand_off);
         uint16_t *i0 = reinterpret_cast<uint16_t *>(B + C);
-        // L lives in code1's space once the sort is done with it
-        oct::body<NC, NK, NT, 0>(plan, L, l, f, smem, Sc, cellbuf, cellcnt, A, A + C, i0, B, i0 + C,
-                                 reinterpret_cast<int8_t *>(B), n, sel, selcnt, err);
+        int8_t *Lg = reinterpret_cast<int8_t *>(B);  // L in code1's space once the sort is done with it
+        oct::body_sort<NC, NK, NT, 0>(plan, L, l, f, smem, Sc, cellbuf, cellcnt, A, A + C, i0, B, i0 + C, Lg, n);
+        auto key_at = [&](int k, uint32_t &kv, uint32_t &ix) {
+            ix = i0[k];
+            kv = A[ix];
+        };
+        oct::body_list<NC, NT>(plan, L, l, f, smem + Lay::kU, Sc, Lg, n, Sc.s[1], key_at, sel, selcnt, err);
     }
 }
 
@@ -2468,6 +2614,17 @@ hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Pl
         else if (K == 2) hipLaunchKernelGGL(k_pyramid_area_chain<2>, grid, dim3(256), 0, st, pyr, pitch, dp);
         else hipLaunchKernelGGL(k_pyramid_area_chain<1>, grid, dim3(256), 0, st, pyr, pitch, dp);
     }
+    // a batch whose remaining levels are all INTER_LINEAR: one launch, a workgroup per
+    // frame (a handful of frames keep the per-level launches, which spread each
+    // level over the whole GPU)
+    bool all_linear = K + 1 < hp.nlevels;
+    for (int l = K + 1; l < hp.nlevels; l++)  // (four pixels span at most 16 source bytes up to 1.5 x)
+        all_linear = all_linear && hp.lv[l].resize_mode == 2 && 2 * hp.lv[l - 1].w <= 3 * hp.lv[l].w &&
+                     hp.lv[l].w <= 2048 && hp.lv[l].h <= 2048;
+    if (all_linear && nframes >= 64) {
+        hipLaunchKernelGGL(k_pyramid_linear_chain, dim3(nframes), dim3(1024), 0, st, pyr, pitch, dp, dtabs, K + 1);
+        return hipGetLastError();
+    }
     for (int l = K + 1; l < hp.nlevels; l++) {
         const LevelDesc &D = hp.lv[l];
         dim3 grid((D.w + 63) / 64, (D.h + 3) / 4, nframes);
@@ -2561,9 +2718,10 @@ static int octree_nc(const LevelDesc &L) {
 constexpr int kOctThreads = YGZ_OCT_THREADS;
 
 // queue words per launch group g: counters at octq[8 g ..] (list i: count 2i, taken
-// 2i + 1), lists at octq[kOctQHead + (3 g + i) T], T = frames x levels
+// 2i + 1), lists at octq[kOctQHead + (3 g + i) T], T = frames x levels; then the
+// per-task sort headers at octq[kOctQHead + 12 T + f levels + l]
 constexpr int kOctQHead = 64;
-size_t octree_queue_ints(const Plan &hp, int nframes) { return kOctQHead + (size_t)12 * nframes * hp.nlevels; }
+size_t octree_queue_ints(const Plan &hp, int nframes) { return kOctQHead + (size_t)13 * nframes * hp.nlevels; }
 
 static hipError_t launch_octree_levels(int nc, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
                                        uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err,
@@ -2583,33 +2741,56 @@ static hipError_t launch_octree_levels(int nc, const Plan *dp, const uint32_t *c
     else YGZ_OCT(2048, 4000, kOctThreads);
 #undef YGZ_OCT
 #else
-    // stage 0: one workgroup per task, sized for the class's usual candidate count;
-    // stage 1: 4,096 keys in LDS (512 threads); stage 2: 8,192 keys (1,024 threads,
-    // one workgroup per CU); stage 3: the global-scratch form
+    // sort stage 0: one workgroup per task, sized for the class's usual candidate count
+    // (wide = one frame: 8,192 keys at once); stage 1: 4,096 keys in LDS (512 threads);
+    // stage 2: 8,192 keys (1,024 threads, one workgroup per CU); stage 3: the
+    // global-scratch form (sort + list); then the list phase of every LDS-sorted task
     int *cq = octq + 8 * g;
     int *lists = octq + kOctQHead + (size_t)3 * g * T;
+    int *hdr = octq + kOctQHead + (size_t)12 * T;
     const OctQueue q0{nullptr, nullptr, nullptr, cq + 0, lists};
     const OctQueue q1{cq + 0, cq + 1, lists, cq + 2, lists + T};
     const OctQueue q2{cq + 2, cq + 3, lists + T, cq + 4, lists + 2 * T};
     const OctQueue q3{cq + 4, cq + 5, lists + 2 * T, nullptr, nullptr};
     const int tasks = nframes * nl;
-#define YGZ_OCT(NC, NK, NT)                                                                                           \
-    do {                                                                                                              \
-        hipLaunchKernelGGL((k_octree_paths<NC, NK, NT>), grid, dim3(NT), 0, st, dp, cellbuf, cellcnt, sel, selcnt,     \
-                           err, l0, q0);                                                                              \
-        hipLaunchKernelGGL((k_octree_paths_q<NC, 4096, 512>), dim3(std::min(tasks, 512)), dim3(512), 0, st, dp,       \
-                           cellbuf, cellcnt, sel, selcnt, err, q1);                                                   \
-        hipLaunchKernelGGL((k_octree_paths_q<NC, 8192, 1024>), dim3(std::min(tasks, 256)), dim3(1024), 0, st, dp,     \
-                           cellbuf, cellcnt, sel, selcnt, err, q2);                                                   \
-        hipLaunchKernelGGL((k_octree_global<NC, 512>), dim3(std::min(tasks, 256)), dim3(512), 0, st, dp, cellbuf,     \
-                           cellcnt, candA, candB, sel, selcnt, err, q3);                                              \
+#define YGZ_OCT_SORT0(NC, NK, NT)                                                                                 \
+    hipLaunchKernelGGL((k_octree_sort<NC, NK, NT>), grid, dim3(NT), 0, st, dp, cellbuf, cellcnt, candA, candB, hdr, \
+                       l0, q0)
+#define YGZ_OCT_REST(NC, Q1)                                                                                      \
+    do {                                                                                                          \
+        if (Q1)                                                                                                   \
+            hipLaunchKernelGGL((k_octree_sort_q<NC, 4096, 512>), dim3(std::min(tasks, 512)), dim3(512), 0, st, dp, \
+                               cellbuf, cellcnt, candA, candB, hdr, q1);                                          \
+        hipLaunchKernelGGL((k_octree_sort_q<NC, 8192, 1024>), dim3(std::min(tasks, NC >= 1024 ? 256 : 64)),      \
+                           dim3(1024), 0, st, dp,                                                                 \
+                           cellbuf, cellcnt, candA, candB, hdr, Q1 ? q2 : q1);                                    \
+        hipLaunchKernelGGL((k_octree_global<NC, 512>), dim3(std::min(tasks, 64)), dim3(512), 0, st, dp, cellbuf,  \
+                           cellcnt, candA, candB, sel, selcnt, err, Q1 ? q3 : q2);                                \
+        hipLaunchKernelGGL((k_octree_list<NC, 256>), grid, dim3(256), 0, st, dp, candA, candB, hdr, sel, selcnt,  \
+                           err, l0);                                                                              \
     } while (0)
-    if (wide && nc > 512 && nc <= 1024) YGZ_OCT(1024, 4096, 1024);
-    else if (nc <= 256) YGZ_OCT(256, 1024, 256);
-    else if (nc <= 512) YGZ_OCT(512, 2048, 256);
-    else if (nc <= 1024) YGZ_OCT(1024, 4096, 512);
-    else YGZ_OCT(2048, 4096, 512);
-#undef YGZ_OCT
+    if (wide && nc <= 1024) {
+        YGZ_OCT_SORT0(1024, 8192, 1024);
+        // stage 0 overflows to list 0, which the global stage reads as its input
+        hipLaunchKernelGGL((k_octree_global<1024, 512>), dim3(std::min(tasks, 256)), dim3(512), 0, st, dp, cellbuf,
+                           cellcnt, candA, candB, sel, selcnt, err, q1);
+        hipLaunchKernelGGL((k_octree_list<1024, 1024>), grid, dim3(1024), 0, st, dp, candA, candB, hdr, sel, selcnt,
+                           err, l0);
+    } else if (nc <= 256) {
+        YGZ_OCT_SORT0(256, 1024, 256);
+        YGZ_OCT_REST(256, true);
+    } else if (nc <= 512) {
+        YGZ_OCT_SORT0(512, 4096, 512);
+        YGZ_OCT_REST(512, false);
+    } else if (nc <= 1024) {
+        YGZ_OCT_SORT0(1024, 4096, 512);
+        YGZ_OCT_REST(1024, false);
+    } else {
+        YGZ_OCT_SORT0(2048, 4096, 512);
+        YGZ_OCT_REST(2048, false);
+    }
+#undef YGZ_OCT_SORT0
+#undef YGZ_OCT_REST
 #endif
     return hipGetLastError();
 }
@@ -2622,6 +2803,13 @@ hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf
                          const hipEvent_t *join, bool wide) {
     int l = 0, g = 0;
     YGZ_HIPR(hipMemsetAsync(octq, 0, kOctQHead * sizeof(int), st));  // queue counters
+    if (wide) {  // one frame: every level in one launch chain when the node pools allow
+        int ncmax = 0;
+        for (int k = 0; k < hp.nlevels; k++) ncmax = std::max(ncmax, octree_nc(hp.lv[k]));
+        if (ncmax <= 1024)
+            return launch_octree_levels(1024, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, octq, 0,
+                                        nframes * hp.nlevels, nframes, 0, hp.nlevels, st, true);
+    }
     if (side && nside > 0) YGZ_HIPR(hipEventRecord(fork, st));  // before the first group: the groups are independent
     while (l < hp.nlevels) {
         const int nc = octree_nc(hp.lv[l]);

@@ -127,6 +127,34 @@ def test_batch_matches_single(gpu):
         assert np.array_equal(dg, dr)
 
 
+@pytest.mark.parametrize("cfg,size", [("C4", (640, 480)), ("C1", (641, 479))])
+def test_batch_linear_pyramid_chain(gpu, cfg, size):
+    """A batch of >= 64 frames forms its INTER_LINEAR levels in one launch (a workgroup
+    per frame, k_pyramid_linear_chain): every level of every frame equals the oracle's
+    cv::resize chain (ORBextractor.cc:1129-1150), odd sizes included; keypoints of a
+    few frames too."""
+    W, H = size
+    _, _, nf, sf, nl, ini, mn = S.CONFIGS[cfg]
+    F = 64
+    base = [S.frame(s, W, H) for s in range(4)]
+    frames = np.stack([np.roll(base[i % 4], 3 * i, axis=1) for i in range(F)])
+    b = gpu.Batch((nf, sf, nl, ini, mn, 0), 0, W, H, F)
+    b.upload(frames)
+    b.extract(F)
+    b.check()
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    for i in (0, 1, 37, F - 1):
+        lv = orc.pyramid(frames[i])
+        for l in range(nl):
+            got = b.read_level(i, l)
+            assert np.array_equal(got, lv[l]), f"frame {i} level {l}"
+    for i in (0, F - 1):
+        kg, dg = b.result(i)
+        kr, dr = orc.extract(orc.pyramid(frames[i]))
+        assert_kps_equal(kg, kr, f"{cfg} batch frame {i}")
+        assert np.array_equal(dg, dr)
+
+
 def test_featureless_frame(gpu):
     """Edge case: a flat image has no FAST corners -> empty result, no hang."""
     W, H, ex, orc = make(gpu, "C2")
