@@ -77,10 +77,15 @@ def parse():
                     help="split: blur + descriptors + Hamming on a side stream beside FAST / octree, "
                          "SparseImgAlign after them; overlap: SparseImgAlign beside orient + Hamming too; "
                          "serial: every stage on one stream")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="process each rank's shard in this many chunks (each its own batch), gathering a "
+                         "chunk's result slots on a communication stream while the next chunk computes "
+                         "(default: 4 when N > 1, else 1 = one batch)")
     ap.add_argument("--no-undistort", action="store_true", help="skip the undistort-remap side measurement")
     ap.add_argument("--no-stage-timing", action="store_true", help="no per-stage hipEvents in the timed region")
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2-transform side measurement")
     ap.add_argument("--no-stereo", action="store_true", help="skip the stereo-matching side measurement")
+    ap.add_argument("--no-a11", action="store_true", help="skip the tracking-path searches line (row a11)")
     ap.add_argument("--no-direct", action="store_true", help="skip the SearchLocalPointsDirect side measurement")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (TUM 640x480, 2000 features) throughput line")
     ap.add_argument("--latency-frames", type=int, default=200,
@@ -257,16 +262,88 @@ def main():
         stream.wait_stream(side)  # the slots need the descriptors
         pack_and_gather(timed_gather)
 
+    # ------------------------------------------------ chunked schedule (default for N > 1)
+    # The shard in n_chunks batches bound to consecutive slices of the same device
+    # buffers (each with the frame before it, for its first align pair: that frame is
+    # extracted twice, identically).  Chunk c's slots are packed into rows [c R, ..)
+    # and gathered to rank 0 on `comm` while chunk c + 1 computes on `stream`, so only
+    # the last chunk's gather is exposed (ygzfe.dist.chunk_rows / chunk_frames;
+    # tests/test_cpu_dist.py checks the layout under gloo).
+    n_chunks = args.chunks if args.chunks > 0 else (4 if world > 1 else 1)
+    chunks = []
+    comm = None
+    if n_chunks > 1:
+        maxlen_c, Rc = D.chunk_rows(n_seq, world, n_chunks)
+        slots = torch.zeros((n_chunks * Rc, S_b), dtype=torch.uint8, device=dev)
+        comm = torch.cuda.Stream(dev)
+        for c in range(n_chunks):
+            s_c, e_c, hc, nc = D.chunk_frames(n_own, h, c, Rc)
+            bt = None
+            if nc > 0:
+                bt = ygzfe.Batch((nf, sf, nl, ini, mn, 0), local, W, H, max(e_c - s_c, 2))
+                bt.bind(pyramids=pyr_t.data_ptr() + s_c * batch.frame_pitch, kps=kps_t[s_c:].data_ptr(),
+                        counts=counts_t[s_c:].data_ptr())
+            bufs = [torch.empty((Rc, S_b), dtype=torch.uint8, device=dev) for _ in range(world)] \
+                if (rank == 0 and world > 1) else None
+            chunks.append((s_c, e_c - s_c, hc, nc, bt, bufs, c * Rc))
+
+    def step_chunked(timed_gather=False):
+        for c, (s_c, L_c, hc, nc, bt, bufs, row0) in enumerate(chunks):
+            if nc > 0:
+                Pc = L_c - 1
+                bt.extract(L_c, sptr)
+                if Pc > 0:
+                    bt.match(Pc, cur_idx.data_ptr(), ref_idx.data_ptr(), bi[s_c:].data_ptr(), bd[s_c:].data_ptr(),
+                             sd[s_c:].data_ptr(), sptr)
+                    if not args.no_align:
+                        ygzfe.plane_points_device(kps_t[s_c:].data_ptr(), cap, Pc, cam, r3_t[s_c:].data_ptr(),
+                                                  cz_t[s_c:].data_ptr(), S.PLANE_Z, xyz[s_c:].data_ptr(), sptr)
+                        bt.sparse_align(Pc, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz[s_c:].data_ptr(),
+                                        usable[s_c:].data_ptr(), camera, 3, 1, T_init[s_c:].data_ptr(),
+                                        out[s_c:].data_ptr(), sptr)
+                bt.pack_slots(hc, nc, out[s_c:].data_ptr() if (Pc > 0 and not args.no_align) else 0, b0 + row0,
+                              slots[row0:].data_ptr(), S_b, sptr)
+            if world > 1:
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                comm.wait_event(ev)
+                with torch.cuda.stream(comm):
+                    if timed_gather:
+                        e0_, e1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0_.record(comm)
+                    dist.gather(slots[row0:row0 + Rc], bufs, dst=0)
+                    if timed_gather:
+                        e1_.record(comm)
+                        gather_ms.append((e0_, e1_))
+        if world > 1:
+            stream.wait_stream(comm)
+
+    batches = [ch[4] for ch in chunks if ch[4] is not None] if chunks else [batch]
+    F_ext = sum(ch[1] for ch in chunks if ch[3] > 0) if chunks else F
+
+    def check_all():
+        for bt in batches:
+            bt.check()
+
+    def timing_all(enable):
+        acc = {}
+        for bt in batches:
+            for k, v in bt.timing(enable).items():
+                acc[k] = acc.get(k, 0.0) + v
+        return acc
+
+    if chunks:
+        step = step_chunked  # noqa: F811 (the chunked schedule replaces the one-batch step)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    batch.check()
+    check_all()
     if world > 1:
         dist.barrier()
-    batch.timing(False)  # `value`: no per-stage events inside the timed region
+    timing_all(False)  # `value`: no per-stage events inside the timed region
     run = step
     graph_ok = False
-    if args.graph and world == 1:
+    if args.graph and world == 1 and not chunks:
         # one step captured as a HIP graph (every launch of the library, its
         # fork/join events and the side streams), replayed per step
         try:
@@ -293,20 +370,20 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    batch.check()
+    check_all()
     elapsed = D.max_over_ranks(elapsed, dev)
     # roofline: the same K steps again with hipEvents around every stage launch
     # (a stage event between two kernels adds ~10 us of dispatch gap, so they
     # stay out of the throughput run)
     stage_ms = {}
     if not args.no_stage_timing:
-        batch.timing(True)
+        timing_all(True)
         torch.cuda.synchronize(dev)
         for _ in range(args.steps):
             step(timed_gather=True)
         torch.cuda.synchronize(dev)
-        stage_ms = batch.timing(False)
-        batch.check()
+        stage_ms = timing_all(False)
+        check_all()
         if gather_ms:
             stage_ms["rccl_gather"] = float(np.mean([a.elapsed_time(b) for a, b in gather_ms]))
         if world > 1:
@@ -318,8 +395,13 @@ def main():
     # ------------------------------------------------ results check: rank 0 holds every frame's slot
     seq_check = None
     if rank == 0:
-        full = torch.cat([gg[:D.shard(n_seq, r, world)[1] - D.shard(n_seq, r, world)[0]]
-                          for r, gg in enumerate(gathered)]) if world > 1 else slots[:n_own]
+        if world > 1 and chunks:
+            full = D.assemble_chunks([ch[5] for ch in chunks], n_seq, world)
+        elif world > 1:
+            full = torch.cat([gg[:D.shard(n_seq, r, world)[1] - D.shard(n_seq, r, world)[0]]
+                              for r, gg in enumerate(gathered)])
+        else:
+            full = slots[:n_own]
         hdr = full[:, :64].contiguous().view(torch.int32).cpu().numpy()
         seq_check = {"frames_at_root": int(full.shape[0]),
                      "frame_index_ok": bool(np.array_equal(hdr[:, 10], np.arange(n_seq))),
@@ -332,18 +414,25 @@ def main():
     nvis = out[:max(P, 1), 7].contiguous().view(torch.int32).cpu().numpy() if P > 0 else np.zeros(1, np.int32)
     plan = ygzfe.orb_plan(nf, sf, nl, ini, mn, W, H)
     areas = [w * hh for w, hh in plan["sizes"]]
-    cand, selk = batch.stats(F)  # per-level totals over the F frames of the last extract
+    if chunks:  # per-level totals over every chunk batch's last extract (lead frames included)
+        cand = selk = 0
+        for ch in chunks:
+            if ch[3] > 0:
+                cc_, ss_ = ch[4].stats(ch[1])
+                cand, selk = cand + cc_, selk + ss_
+    else:
+        cand, selk = batch.stats(F)  # per-level totals over the F frames of the last extract
     N = float(counts.mean())
     nv = float(nvis.mean())
     ncells_tot = int(sum(plan["ncells"]))
     # algorithmic bytes per launch (per step, F frames): each intermediate crosses
     # HBM once written and once read
     alg = {
-        "pyramid": F * sum(areas[l - 1] + areas[l] for l in range(1, nl)),
-        "blur7": F * 2 * sum(areas),
-        "fast9_cells": F * sum(a for a, c in zip(areas, plan["ncells"]) if c > 0) + 4 * int(cand.sum())
-        + 4 * F * ncells_tot,
-        "octree": 4 * int(cand.sum()) + 4 * F * ncells_tot + 4 * int(selk.sum()),
+        "pyramid": F_ext * sum(areas[l - 1] + areas[l] for l in range(1, nl)),
+        "blur7": F_ext * 2 * sum(areas),
+        "fast9_cells": F_ext * sum(a for a, c in zip(areas, plan["ncells"]) if c > 0) + 4 * int(cand.sum())
+        + 4 * F_ext * ncells_tot,
+        "octree": 4 * int(cand.sum()) + 4 * F_ext * ncells_tot + 4 * int(selk.sum()),
         "orient_rbrief": int(counts.sum()) * (961 + 512 + 4 + 60),
         "hamming_best2": int(sum(32 * (counts[i + 1] + counts[i]) + 12 * counts[i + 1] for i in range(P))),
         "sparse_align": int(P * (3 * nv * (36 + 10 * 25) + 12 * nv + 96)),
@@ -368,7 +457,7 @@ def main():
             traffic = tj["per_step"][dom]["traffic_bytes"]
     roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic, "valu_frac": valu_frac,
-            "avg_launch_ms": round(dom_ms, 4), "alg_bytes_per_launch": int(alg[dom]), "frames_per_launch": F,
+            "avg_launch_ms": round(dom_ms, 4), "alg_bytes_per_launch": int(alg[dom]), "frames_per_launch": F_ext,
             "stages_ms": {k: round(v, 4) for k, v in stage_ms.items()},
             "stages_gbps": {k: round(alg[k] / (stage_ms[k] * 1e-3) / 1e9, 1) for k in alg if stage_ms.get(k, 0) > 0}}
     # whole pipeline, SURVEY §8d model: (B_extract + B_align) per frame x fps
@@ -424,6 +513,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_direct:
         direct_line = direct_leg(S, args.cpu_sample > 0)
 
+    # ------------------------------------------------ §8(a) row a11: the tracking-path searches
+    a11_line = None
+    if rank == 0 and world == 1 and not args.no_a11:
+        a11_line = tracking_search_leg(S, args.cpu_sample > 0)
+
     # ------------------------------------------------ §8(f) rank 3: stereo matching
     stereo_line = None
     if rank == 0 and world == 1 and not args.no_stereo:
@@ -473,15 +567,16 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded textured-plane renders on the device, EuRoC intrinsics; no dataset)",
             "config": {"workload": wl, "sequence_frames": n_seq, "frames_per_gpu": n_own,
-                       "frames_extracted_per_gpu": F, "image": f"{W}x{H}", "nfeatures": nf, "scale_factor": sf,
+                       "frames_extracted_per_gpu": F_ext, "chunks": n_chunks, "image": f"{W}x{H}", "nfeatures": nf, "scale_factor": sf,
                        "nlevels": nl, "fast_th": [ini, mn], "align_pairs_per_gpu": P,
                        "mean_keypoints": round(N, 1), "mean_align_visible": round(nv, 1),
                        "mean_fast_candidates": round(float(cand.sum()) / F, 1),
                        "mean_fast_candidates_per_level": [round(float(c) / F, 1) for c in cand],
                        "mean_keypoints_per_level": [round(float(c) / F, 1) for c in selk],
                        "parallelism": f"frame-sharded x{world} (contiguous shards + 1-frame halo)",
-                       "collective": "RCCL gather of result slots to rank 0 (torch.distributed.gather)"
-                       if world > 1 else "none (N=1: rank 0 is the root)",
+                       "collective": (f"RCCL gather of result slots to rank 0 (torch.distributed.gather), "
+                                      f"{n_chunks} chunk(s), each gathered on a communication stream while the "
+                                      f"next chunk computes") if world > 1 else "none (N=1: rank 0 is the root)",
                        "schedule": args.schedule, "hip_graph": graph_ok},
             "roofline": roof,
             "pipeline_gbps_model": round(pipeline_gbps, 2),
@@ -490,6 +585,7 @@ def main():
             "cpu_baseline": cpu,
             "latency": lat,
             "c4_batched": c4_line,
+            "tracking_searches": a11_line,
             "next_rows": {"undistort_remap": und_line, "search_local_points_direct": direct_line,
                           "stereo_matches": stereo_line, "dbow2_transform": bow_line},
         }
@@ -755,6 +851,54 @@ def stereo_leg(S, dev, with_cpu, n_pairs=64, reps=20):
             tc.append(time.perf_counter() - t0)
         line["cpu_port_ms_per_pair"] = round(float(np.median(tc)) * 1e3, 4)
         line["cpu_cores"] = 1
+    return line
+
+
+def tracking_search_leg(S, with_cpu, reps=50):
+    """Row a11 per frame, the way Tracking calls it: the current frame's keypoints and
+    descriptors uploaded once (ORBmatcher_gpu.inc's set_frame), then
+    SearchByProjection(CurrentFrame, LastFrame, th 7, checkOri) (ORBmatcher.cc:1218-1350,
+    TrackWithMotionModel) and SearchByProjection(F, vpLocalMapPoints, th 3, nnratio 0.8)
+    (ORBmatcher.cc:43-126, SearchLocalPoints) on a C2 frame pair; host C ABI (the calls the
+    drop-in header makes), median over `reps` frames.  CPU: oracle/match.c's literal
+    restatement of the same loops, 1 thread."""
+    import ygzfe
+    p = S.match_pair("C2", 0)
+    bnd = (0.0, float(p["W"]), 0.0, float(p["H"]))
+    Q1, qd1, ur, bl1 = S.projection_queries(p, 0, th=7.0, level_mode="mixed")
+    Q2, qd2, _, bl2 = S.projection_queries(p, 10, th=3.0 * 2.5, level_mode="band")
+    mf = ygzfe.MatchFrame(0)
+
+    def gpu_frame():
+        cur = mf.set(p["k1"], p["d1"], ur, bnd)
+        g1, n1 = ygzfe.search_projection_best(cur, Q1, qd1, bl1, 100, True)
+        g2, n2 = ygzfe.search_projection_ratio(cur, Q2, qd2, bl2, 0.8)
+        return n1, n2
+
+    for _ in range(3):
+        gpu_frame()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        n1, n2 = gpu_frame()
+        ts.append(time.perf_counter() - t0)
+    line = {"frame_keypoints": int(len(p["k1"])), "last_frame_queries": int(len(Q1)),
+            "local_map_queries": int(len(Q2)), "matches_last_frame": int(n1), "matches_local_map": int(n2),
+            "median_ms": round(float(np.median(ts)) * 1e3, 4),
+            "path": "host C ABI per frame: frame upload + grid, SearchByProjection(F, LastF, checkOri) + "
+                    "SearchByProjection(F, localMPs, nnratio 0.8), results on the host"}
+    if with_cpu:
+        import _oracle as O
+        tc = []
+        for _ in range(10):
+            t0 = time.perf_counter()
+            mfr = O.mframe(p["k1"], p["d1"], ur, bnd)
+            O.search_projection_best(mfr, Q1, qd1, bl1, 100, True)
+            O.search_projection_ratio(mfr, Q2, qd2, bl2, 0.8)
+            tc.append(time.perf_counter() - t0)
+        line["cpu_port_ms"] = round(float(np.median(tc)) * 1e3, 4)
+        line["cpu_cores"] = 1
+        line["speedup_vs_cpu_port"] = round(line["cpu_port_ms"] / line["median_ms"], 2)
     return line
 
 

@@ -964,12 +964,21 @@ int ygzfe_diag_stage_ms(ygzfe_batch *b, int stage, int n_frames, int reps, int b
     return YGZFE_OK;
 }
 
+// Host reads of extraction outputs: the batch stream (uploads, own launches) and the
+// last extraction's end event (its descriptor pass, after every other stage joined)
+// instead of a device-wide synchronisation that would also wait for unrelated streams.
+// An extraction captured into a caller's graph is the caller's to synchronise.
+static int batch_wait(ygzfe_batch *b) {
+    YGZ_HIP(hipStreamSynchronize(b->stream));
+    if (b->desc_pending) YGZ_HIP(hipEventSynchronize(b->ev_desc_done));
+    return YGZFE_OK;
+}
+
 int ygzfe_batch_check(ygzfe_batch *b) {
     if (!b) { set_error("null batch"); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(b->device));
     int herr = 0;
-    YGZ_HIP(hipStreamSynchronize(b->stream));
-    YGZ_HIP(hipDeviceSynchronize());
+    YGZ_TRY(batch_wait(b));
     YGZ_HIP(hipMemcpy(&herr, b->ws.err.p, sizeof(int), hipMemcpyDeviceToHost));
     if (herr) { set_error("octree node pool overflow"); return YGZFE_EINVAL; }
     return YGZFE_OK;
@@ -978,7 +987,7 @@ int ygzfe_batch_check(ygzfe_batch *b) {
 int ygzfe_batch_result(ygzfe_batch *b, int frame, ygzfe_kp *kps, int cap, uint8_t *desc, int *n_out) {
     if (!b || frame < 0 || frame >= b->maxF || !n_out) { set_error("invalid argument"); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(b->device));
-    YGZ_HIP(hipDeviceSynchronize());
+    YGZ_TRY(batch_wait(b));
     const Plan &P = b->plan->hp();
     int n = 0;
     YGZ_HIP(hipMemcpy(&n, b->ws.counts.as<int>() + frame, sizeof(int), hipMemcpyDeviceToHost));
@@ -1021,7 +1030,7 @@ int ygzfe_batch_read_level(ygzfe_batch *b, int frame, int level, int blurred, ui
     const DevBuf &src = blurred ? b->ws.blur : b->pyr;
     if (!src.p) { set_error("no %s buffer yet (run ygzfe_batch_extract first)", blurred ? "blurred" : "pyramid"); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(b->device));
-    YGZ_HIP(hipDeviceSynchronize());  // extract may have run on a caller stream + side streams
+    YGZ_TRY(batch_wait(b));  // extract may have run on a caller stream + side streams
     YGZ_HIP(hipMemcpy2D(dst, dst_stride, (const uint8_t *)src.p + (size_t)frame * P.pyr_bytes + L.off, L.w, L.w, L.h,
                         hipMemcpyDeviceToHost));
     return YGZFE_OK;
@@ -1031,7 +1040,7 @@ int ygzfe_batch_stats(ygzfe_batch *b, int n_frames, int64_t *candidates, int64_t
     if (!b || n_frames < 0 || n_frames > b->maxF) { set_error("invalid argument"); return YGZFE_EINVAL; }
     const Plan &P = b->plan->hp();
     YGZ_TRY(ensure_device(b->device));
-    YGZ_HIP(hipDeviceSynchronize());  // extract may have run on a caller stream + side streams
+    YGZ_TRY(batch_wait(b));  // extract may have run on a caller stream + side streams
     for (int l = 0; l < P.nlevels; l++) {
         if (candidates) candidates[l] = 0;
         if (selected) selected[l] = 0;
@@ -2431,7 +2440,7 @@ extern "C" int ygzfe_match_frame_from_batch(ygzfe_match_frame *f, ygzfe_batch *b
     if (f->device != b->device) { set_error("match frame and batch on different devices"); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(f->device));
     const Plan &P = b->plan->hp();
-    YGZ_HIP(hipDeviceSynchronize());  // the batch's extraction may run on caller streams
+    YGZ_TRY(batch_wait(b));  // the batch's extraction may run on caller streams
     int n = 0;
     YGZ_HIP(hipMemcpy(&n, b->ws.counts.as<int>() + frame, sizeof(int), hipMemcpyDeviceToHost));
     f->n = n;

@@ -117,6 +117,55 @@ def gather_slots(local_slots, n_frames, rank, world, device=None):
     return torch.cat(parts, 0)
 
 
+def chunk_rows(n_frames, world, n_chunks):
+    """Row layout of the chunked gather: every rank pads its shard to maxlen =
+    ceil(n_frames / world) slot rows, cut into n_chunks pieces of R rows (the last may
+    run past maxlen: those rows are padding).  Chunk c of every rank is rows
+    [c R, (c + 1) R); the same R on every rank keeps each chunk's gather uniform."""
+    maxlen = -(-n_frames // world)
+    R = -(-maxlen // max(1, n_chunks))
+    return maxlen, R
+
+
+def chunk_frames(n_own, h, c, R):
+    """Local frames of chunk c of a rank owning n_own frames from local index h: the
+    batch range [s, e) (the frame before the chunk included, for its first align pair),
+    the own frames' offset in that range, and how many there are."""
+    a = h + min(c * R, n_own)
+    e = h + min((c + 1) * R, n_own)
+    s = a - 1 if a > 0 else a
+    return s, e, a - s, e - a
+
+
+def assemble_chunks(chunk_bufs, n_frames, world):
+    """Rank 0: chunk_bufs[c][r] = rank r's rows of chunk c -> [n_frames, S] in global
+    frame order (each rank's rows concatenated over chunks, cut to its shard)."""
+    import torch
+    parts = []
+    for r in range(world):
+        b, e = shard(n_frames, r, world)
+        parts.append(torch.cat([cb[r] for cb in chunk_bufs], 0)[:e - b])
+    return torch.cat(parts, 0)
+
+
+def gather_slots_chunked(local_slots, n_frames, rank, world, n_chunks, device=None):
+    """gather_slots as n_chunks gathers of R rows each (the bench issues each one on
+    a communication stream as soon as its chunk is packed, overlapping the next
+    chunk's compute).  Returns [n_frames, S] on rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    S = local_slots.shape[1]
+    maxlen, R = chunk_rows(n_frames, world, n_chunks)
+    pad = torch.zeros((n_chunks * R, S), dtype=torch.uint8, device=device or local_slots.device)
+    pad[:local_slots.shape[0]] = local_slots
+    bufs = []
+    for c in range(n_chunks):
+        cb = [torch.empty((R, S), dtype=torch.uint8, device=pad.device) for _ in range(world)] if rank == 0 else None
+        dist.gather(pad[c * R:(c + 1) * R], cb, dst=0)
+        bufs.append(cb)
+    return assemble_chunks(bufs, n_frames, world) if rank == 0 else None
+
+
 def max_over_ranks(seconds, device=None):
     """The bench's wall time: the slowest rank's (all_reduce MAX of one float64)."""
     import torch

@@ -93,6 +93,55 @@ def test_gloo_world2_gather_and_timing(n_frames):
     assert not D.unpack_slot(full[0], cap, ygzfe.KP_DTYPE)["has_align"]
 
 
+def _chunk_worker(rank, world, port, n_frames, cap, n_chunks, ret):
+    """bench.py's chunked schedule on CPU: the shard processed in n_chunks batches (each
+    with the frame before it, for its first align pair); chunk c's slots packed into
+    rows [c R, c R + own) and gathered to rank 0 before chunk c + 1 is processed."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b, e = D.shard(n_frames, rank, world)
+    hb, he = D.with_halo(b, e)
+    h, n_own = b - hb, e - b
+    maxlen, R = D.chunk_rows(n_frames, world, n_chunks)
+    S = D.slot_bytes(cap)
+    pad = torch.zeros((n_chunks * R, S), dtype=torch.uint8)
+    bufs, covered = [], []
+    for c in range(n_chunks):
+        s0, e0, hc, nc = D.chunk_frames(n_own, h, c, R)
+        if nc > 0:
+            frames = list(range(hb + s0 + hc, hb + s0 + hc + nc))  # global frames this chunk owns
+            covered += frames
+            counts, kps, desc, align = fake_results(frames, cap)
+            pad[c * R:c * R + nc] = torch.from_numpy(D.pack_slots(counts, kps, desc, align, global_first=frames[0]))
+            assert s0 + hc - 1 >= 0 or frames[0] == 0  # the pair (first - 1, first) is inside the batch
+        cb = [torch.empty((R, S), dtype=torch.uint8) for _ in range(world)] if rank == 0 else None
+        dist.gather(pad[c * R:(c + 1) * R], cb, dst=0)
+        bufs.append(cb)
+    assert covered == list(range(b, e))
+    via_helper = D.gather_slots_chunked(pad[:n_own], n_frames, rank, world, n_chunks)
+    if rank == 0:
+        ret["full"] = D.assemble_chunks(bufs, n_frames, world).numpy()
+        ret["helper"] = via_helper.numpy()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_frames,n_chunks", [(2, 16, 4), (2, 9, 3), (3, 17, 4), (2, 5, 4)])
+def test_gloo_chunked_gather_equals_single_rank(world, n_frames, n_chunks):
+    """The overlapped (chunked) gather of bench.py --gpus N: every frame lands once, in
+    order, with its own slot, whatever the shard / chunk split (uneven shards, chunks
+    longer than a shard, empty trailing chunks)."""
+    cap = 5
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_chunk_worker, args=(world, free_port(), n_frames, cap, n_chunks, ret), nprocs=world, join=True)
+    counts, kps, desc, align = fake_results(list(range(n_frames)), cap)
+    want = D.pack_slots(counts, kps, desc, align)
+    assert np.array_equal(ret["full"], want)
+    assert np.array_equal(ret["helper"], want)
+
+
 # ---------------------------------------------------------------- real extractor output
 # The C5 pipeline per rank (bench.py): extract the shard plus its one-frame halo,
 # align every pair (k-1, k) of the shard, pack the slots, gather to rank 0 -- here
