@@ -54,6 +54,16 @@ static int ensure_device(int device) {
     return YGZFE_OK;
 }
 
+// Graph capture vs. teardown across threads: a thread capturing its extraction
+// graph must not overlap another thread's hipFree / stream / graph destruction (the
+// runtime's capture bookkeeping is process-wide; tests/test_gpu_concurrency.py hit it
+// with two extractors on two threads, Frame.cc:728-731).  Capture takes ~0.1 ms once
+// per frame handle; teardown is rare: one lock for both.
+static std::recursive_mutex &graph_mutex() {
+    static std::recursive_mutex mu;
+    return mu;
+}
+
 struct DevBuf {
     void *p = nullptr;
     size_t n = 0;
@@ -63,7 +73,10 @@ struct DevBuf {
     DevBuf &operator=(const DevBuf &) = delete;
     ~DevBuf() { release(); }
     void release() {
-        if (p && owned) (void)hipFree(p);
+        if (p && owned) {
+            std::lock_guard<std::recursive_mutex> lk(graph_mutex());  // not during another thread's capture
+            (void)hipFree(p);
+        }
         p = nullptr;
         n = 0;
         owned = true;
@@ -73,6 +86,7 @@ struct DevBuf {
         if (!owned && p && n >= bytes) return YGZFE_OK;
         release();
         if (bytes == 0) bytes = 16;
+        std::lock_guard<std::recursive_mutex> lk(graph_mutex());
         if (hipMalloc(&p, bytes) != hipSuccess) {
             p = nullptr;
             set_error("hipMalloc(%zu) failed", bytes);
@@ -399,6 +413,7 @@ int ygzfe_extractor_create(const ygzfe_orb_params *p, int device, ygzfe_extracto
 
 void ygzfe_extractor_destroy(ygzfe_extractor *ex) {
     if (!ex) return;
+    std::lock_guard<std::recursive_mutex> lk(graph_mutex());
     (void)hipSetDevice(ex->device);
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
     for (int i = 0; i < 3; i++) {
@@ -493,6 +508,7 @@ int ygzfe_frame_create(ygzfe_extractor *ex, int width, int height, ygzfe_frame *
 
 void ygzfe_frame_destroy(ygzfe_frame *f) {
     if (!f) return;
+    std::lock_guard<std::recursive_mutex> lk(graph_mutex());
     (void)hipSetDevice(f->ex->device);
     (void)hipStreamSynchronize(f->ex->stream);
     delete f;
@@ -664,6 +680,7 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
         bool launched = false;
         if (n_existing == 0 && !no_graph && !ex->graph_broken) {
             if (!f->gexec || memcmp(f->gkey, key, sizeof(key)) != 0 || f->grows != rows || f->gcopy != copy) {
+                std::lock_guard<std::recursive_mutex> lk(graph_mutex());
                 f->drop_graph();
                 bool ok = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess;
                 const int rc = ok ? enqueue() : YGZFE_EHIP;
@@ -792,6 +809,7 @@ int ygzfe_batch_create(const ygzfe_orb_params *p, int device, int width, int hei
 
 void ygzfe_batch_destroy(ygzfe_batch *b) {
     if (!b) return;
+    std::lock_guard<std::recursive_mutex> lk(graph_mutex());
     (void)hipSetDevice(b->device);
     (void)hipStreamSynchronize(b->stream);
     (void)b->collect();
@@ -2256,9 +2274,11 @@ struct ygzfe_match_frame {
     DevBuf kps, desc, uright, cell;
     std::vector<ygzfe_kp> host_kps;  // angles / octaves / positions the host-side query building reads
     int last_rescans = 0;            // queries of the last search whose top-K list the skips exhausted
-    // per-call staging
+    // per-call staging: page-locked, one DMA per direction; ev_in = the last H2D out of
+    // hin / hset (the next call refills them only after it)
     DevBuf in, out, scratch;
-    std::vector<uint8_t> hin, hout;
+    HostBuf hin, hout, hset;
+    hipEvent_t ev_in = nullptr, ev_set = nullptr;
 };
 
 namespace {
@@ -2282,7 +2302,7 @@ int match_frame_finish(ygzfe_match_frame *f, const ygzfe_bounds *bounds) {
     YGZ_TRY(f->cell.ensure(sizeof(int32_t) * (size_t)std::max(f->n, 1)));
     YGZ_HIP(launch_match_cells(f->kps.as<ygzfe_kp>(), f->n, bounds->min_x, bounds->min_y, f->inv_w, f->inv_h,
                                f->cell.as<int32_t>(), f->stream));
-    YGZ_HIP(hipStreamSynchronize(f->stream));
+    // no synchronisation: every search runs on f->stream after the grid
     return YGZFE_OK;
 }
 
@@ -2336,8 +2356,9 @@ int run_match(MatchCall &c) {
     YGZ_TRY(f->in.ensure(ai.off));
     YGZ_TRY(f->out.ensure(ao.off));
     uint8_t *din = f->in.as<uint8_t>(), *dout = f->out.as<uint8_t>();
-    f->hin.resize(ai.off);
-    uint8_t *h = f->hin.data();
+    if (f->ev_in) YGZ_HIP(hipEventSynchronize(f->ev_in));  // the previous H2D out of hin
+    YGZ_TRY(f->hin.ensure(ai.off));
+    uint8_t *h = f->hin.as<uint8_t>();
     MatchJob J;
     memset(&J, 0, sizeof(J));
     J.kps = f->kps.as<ygzfe_kp>();
@@ -2370,15 +2391,18 @@ int run_match(MatchCall &c) {
     if (c.cand_host && c.n_cand) memcpy(h + o_c, c.cand_host, sizeof(int32_t) * c.n_cand);
     if (c.blocked_host && n) memcpy(h + o_bl, c.blocked_host, (size_t)n);
     YGZ_HIP(hipMemcpyAsync(din, h, ai.off, hipMemcpyHostToDevice, st));
+    if (!f->ev_in) YGZ_HIP(hipEventCreateWithFlags(&f->ev_in, hipEventDisableTiming));
+    YGZ_HIP(hipEventRecord(f->ev_in, st));
     YGZ_HIP(launch_match(reinterpret_cast<const MatchJob *>(din + o_job), 1, nq, n, c.mode, c.th_dist, c.check_ori,
                          c.nnratio, st));
-    f->hout.resize(out_bytes);
-    YGZ_HIP(hipMemcpyAsync(f->hout.data(), dout, out_bytes, hipMemcpyDeviceToHost, st));
+    YGZ_TRY(f->hout.ensure(out_bytes));
+    YGZ_HIP(hipMemcpyAsync(f->hout.p, dout, out_bytes, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipStreamSynchronize(st));
-    if (c.train_out && n) memcpy(c.train_out, f->hout.data() + o_tout, sizeof(int32_t) * n);
-    if (c.query_out && nq) memcpy(c.query_out, f->hout.data() + o_qout, sizeof(int32_t) * nq);
-    memcpy(&c.nmatches, f->hout.data() + o_nm, sizeof(int32_t));
-    memcpy(&f->last_rescans, f->hout.data() + o_nm + 4, sizeof(int32_t));
+    const uint8_t *ho = f->hout.as<uint8_t>();
+    if (c.train_out && n) memcpy(c.train_out, ho + o_tout, sizeof(int32_t) * n);
+    if (c.query_out && nq) memcpy(c.query_out, ho + o_qout, sizeof(int32_t) * nq);
+    memcpy(&c.nmatches, ho + o_nm, sizeof(int32_t));
+    memcpy(&f->last_rescans, ho + o_nm + 4, sizeof(int32_t));
     return YGZFE_OK;
 }
 
@@ -2398,6 +2422,8 @@ extern "C" void ygzfe_match_frame_destroy(ygzfe_match_frame *f) {
     if (!f) return;
     (void)hipSetDevice(f->device);
     if (f->stream) (void)hipStreamSynchronize(f->stream), (void)hipStreamDestroy(f->stream);
+    if (f->ev_in) (void)hipEventDestroy(f->ev_in);
+    if (f->ev_set) (void)hipEventDestroy(f->ev_set);
     delete f;
 }
 
@@ -2422,14 +2448,21 @@ extern "C" int ygzfe_match_frame_set(ygzfe_match_frame *f, const ygzfe_kp *kps, 
     f->host_kps.assign(kps, kps + n);
     YGZ_TRY(f->kps.ensure(sizeof(ygzfe_kp) * (size_t)std::max(n, 1)));
     YGZ_TRY(f->desc.ensure((size_t)32 * std::max(n, 1)));
-    if (n) {
-        YGZ_HIP(hipMemcpyAsync(f->kps.p, kps, sizeof(ygzfe_kp) * n, hipMemcpyHostToDevice, f->stream));
-        YGZ_HIP(hipMemcpyAsync(f->desc.p, desc, (size_t)32 * n, hipMemcpyHostToDevice, f->stream));
-    }
     f->has_uright = u_right != nullptr;
-    if (u_right) {
-        YGZ_TRY(f->uright.ensure(sizeof(float) * (size_t)std::max(n, 1)));
-        if (n) YGZ_HIP(hipMemcpyAsync(f->uright.p, u_right, sizeof(float) * n, hipMemcpyHostToDevice, f->stream));
+    if (u_right) YGZ_TRY(f->uright.ensure(sizeof(float) * (size_t)std::max(n, 1)));
+    if (n) {  // keypoints, descriptors (and u_right) through page-locked staging: async DMAs
+        const size_t kb = sizeof(ygzfe_kp) * (size_t)n, db = (size_t)32 * n, ub = u_right ? sizeof(float) * n : 0;
+        if (f->ev_set) YGZ_HIP(hipEventSynchronize(f->ev_set));  // the previous frame's DMA out of hset
+        YGZ_TRY(f->hset.ensure(kb + db + ub));
+        uint8_t *hs = f->hset.as<uint8_t>();
+        memcpy(hs, kps, kb);
+        memcpy(hs + kb, desc, db);
+        if (ub) memcpy(hs + kb + db, u_right, ub);
+        YGZ_HIP(hipMemcpyAsync(f->kps.p, hs, kb, hipMemcpyHostToDevice, f->stream));
+        YGZ_HIP(hipMemcpyAsync(f->desc.p, hs + kb, db, hipMemcpyHostToDevice, f->stream));
+        if (ub) YGZ_HIP(hipMemcpyAsync(f->uright.p, hs + kb + db, ub, hipMemcpyHostToDevice, f->stream));
+        if (!f->ev_set) YGZ_HIP(hipEventCreateWithFlags(&f->ev_set, hipEventDisableTiming));
+        YGZ_HIP(hipEventRecord(f->ev_set, f->stream));
     }
     return match_frame_finish(f, bounds);
 }

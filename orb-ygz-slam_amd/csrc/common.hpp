@@ -88,6 +88,14 @@ template <class T>
 __device__ __forceinline__ gptr_t<T> as_global(const T *p) {
     return (gptr_t<T>)p;
 }
+// ... and for stores: global_store_* (vmcnt only) instead of flat_store_*, which an
+// LDS wait (lgkmcnt) would otherwise also wait on
+template <class T>
+using gmut_t = __attribute__((address_space(1))) T *;
+template <class T>
+__device__ __forceinline__ gmut_t<T> as_global_mut(T *p) {
+    return (gmut_t<T>)p;
+}
 // a * b + c on 24-bit operands (v_mad_u32_u24, full rate); inline asm so the
 // compiler cannot widen it into a quarter-rate v_mad_u64_u32
 __device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {

@@ -124,10 +124,14 @@ __device__ __forceinline__ uint32_t window_order(const MatchJob &J, const Window
     return ((uint32_t)(ix * kGridRows + iy) << 16) | (uint32_t)j;  // GetFeaturesInArea order
 }
 
-// key = dist << 52 | order << 20 | train index
-__device__ __forceinline__ uint64_t make_key(int dist, uint32_t order, int j) {
-    return ((uint64_t)dist << 52) | ((uint64_t)order << 20) | (uint64_t)j;
+// key = dist << 52 | order << 20 | octave << 16 | train index (n <= 65535).  The
+// candidate order is unique within a query, so the octave bits never decide a
+// comparison; they spare the serial replay a dependent load per ratio test.
+__device__ __forceinline__ uint64_t make_key(int dist, uint32_t order, int j, int octave) {
+    return ((uint64_t)dist << 52) | ((uint64_t)order << 20) | ((uint64_t)(octave & 15) << 16) | (uint64_t)j;
 }
+__device__ __forceinline__ int key_train(uint64_t k) { return (int)(k & 0xFFFF); }
+__device__ __forceinline__ int key_octave(uint64_t k) { return (int)((k >> 16) & 15); }
 
 template <class Pred>
 __device__ __forceinline__ void scan_query(const MatchJob &J, int q, const ygzfe_match_query &Q, const uint32_t qd[8],
@@ -140,7 +144,7 @@ __device__ __forceinline__ void scan_query(const MatchJob &J, int q, const ygzfe
         const int dist = hamming32(qd, J.desc + (size_t)j * 32);
         if (skip(j, dist)) return;
         count++;
-        uint64_t key = make_key(dist, order, j);
+        uint64_t key = make_key(dist, order, j, J.kps[j].octave);
 #pragma unroll
         for (int k = 0; k < kTopK; k++) {  // sorted insertion, branch-free
             const uint64_t lo = key < L[k] ? key : L[k], hi = key < L[k] ? L[k] : key;
@@ -242,26 +246,57 @@ __device__ __forceinline__ int rot_bin(float aq, float at) {
     return min(max(bin, 0), 63);
 }
 
+// LDS of k_match_replay: blocked [n], INIT's distance / match arrays, then (when the
+// total stays under 64 KB) the train keypoints' angles and octaves
+__host__ __device__ __forceinline__ size_t replay_lds_base(int n, int mode) {
+    return (size_t)((n + 15) & ~15) + (mode == YGZFE_MATCH_INIT ? 4 * (size_t)((n + 7) & ~7) : 0);
+}
+__host__ __device__ __forceinline__ bool staged_kp_fits(int n, int mode) {
+    return replay_lds_base(n, mode) + 5 * (size_t)((n + 3) & ~3) + 64 <= 65536;
+}
+
 __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict__ jobs, int mode, int th_dist,
-                                                     int check_ori, float nnratio) {
+                                                     int check_ori, float nnratio, int stage_kv) {
     extern __shared__ uint8_t lds[];
-    const MatchJob &J = jobs[blockIdx.x];
+    // the job's fields in registers: the loop's global stores could otherwise alias the
+    // job record and force a reload of every field (a scalar-load latency per query)
+    const MatchJob J = jobs[blockIdx.x];
+    const auto g_train_out = as_global_mut(J.train_out), g_query_out = as_global_mut(J.query_out);
+    const auto g_pushes = as_global_mut(J.pushes), g_nmatches = as_global_mut(J.nmatches);
+    const auto g_q = as_global(J.q);
+    const auto g_ncand = as_global(J.ncand);
+    const auto g_topk = as_global(J.topk);
+    const auto g_kps = as_global(J.kps);
+    const auto g_blocked0 = as_global(J.blocked0);
+    const auto g_qid = as_global(J.qid);
     const int lane = threadIdx.x;
     const int n = J.n_train;
     __shared__ int rot_count[64];
     uint8_t *blocked = lds;                                            // [n]
     uint16_t *mdist = reinterpret_cast<uint16_t *>(lds + ((n + 15) & ~15));  // INIT: vMatchedDistance (0xFFFF = INT_MAX)
     int16_t *m21 = reinterpret_cast<int16_t *>(mdist + ((n + 7) & ~7));      // INIT: vnMatches21
+    // the train keypoints' octave and angle the per-query decisions read (LDS when it
+    // fits: the replay is a serial chain, a global load per query is its latency)
+    const size_t kv_off = ((n + 15) & ~15) + (mode == YGZFE_MATCH_INIT ? 4 * (size_t)((n + 7) & ~7) : 0);
+    const bool kv_lds = stage_kv != 0;  // allocated for the launch's largest n (>= this job's)
+    float *s_ang = reinterpret_cast<float *>(lds + kv_off);
+    uint8_t *s_oct = lds + kv_off + 4 * (size_t)((n + 3) & ~3);
     for (int j = lane; j < n; j += 64) {
-        blocked[j] = J.blocked0 ? J.blocked0[j] : 0;
-        if (J.train_out) J.train_out[j] = -1;
+        blocked[j] = J.blocked0 ? g_blocked0[j] : 0;
+        if (J.train_out) g_train_out[j] = -1;
         if (mode == YGZFE_MATCH_INIT) {
             mdist[j] = 0xFFFF;
             m21[j] = -1;
         }
+        if (kv_lds) {
+            s_ang[j] = g_kps[j].angle;
+            s_oct[j] = (uint8_t)g_kps[j].octave;
+        }
     }
+    auto oct_of = [&](int j) -> int { return kv_lds ? (int)s_oct[j] : g_kps[j].octave; };
+    auto ang_of = [&](int j) -> float { return kv_lds ? s_ang[j] : g_kps[j].angle; };
     if (mode == YGZFE_MATCH_INIT)
-        for (int i = lane; i < J.nq; i += 64) J.query_out[i] = -1;
+        for (int i = lane; i < J.nq; i += 64) g_query_out[i] = -1;
     rot_count[lane] = 0;
     __syncthreads();
     int nmatches = 0, npush = 0, rescans = 0;
@@ -271,39 +306,83 @@ __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict_
         if (mode == YGZFE_MATCH_INIT) return (int)mdist[j] <= dist;  // vMatchedDistance[i2] <= dist (0xFFFF: INT_MAX)
         return blocked[j] != 0;
     };
-    // prefetch of the next query's entries
-    uint64_t E = ~0ull;
-    int cnt = 0;
-    ygzfe_match_query Q;
-    if (J.nq > 0) {
-        Q = J.q[0];
-        cnt = J.ncand[0];
-        if (lane < kTopK) E = J.topk[lane];
-    }
-    for (int q = 0; q < J.nq; q++) {
-        const ygzfe_match_query cq = Q;
-        const uint64_t cE = E;
-        const int ccnt = cnt;
-        if (q + 1 < J.nq) {
-            Q = J.q[q + 1];
-            cnt = J.ncand[q + 1];
-            E = lane < kTopK ? J.topk[(size_t)(q + 1) * kTopK + lane] : ~0ull;
+    // Queries staged 64 at a time (lane i loads query b + i: flags, angle, candidate
+    // count, top-K entries), double-buffered in LDS: the serial chain below then pays
+    // LDS latencies only, the next block's global loads landing meanwhile.
+    __shared__ uint64_t s_qe[2][64 * kTopK];
+    struct Blk {
+        int flags, cnt;
+        float angle;
+        uint64_t e[kTopK];
+    };
+    auto load_blk = [&](int b0) -> Blk {
+        Blk r;
+        const int q = b0 + lane;
+        r.flags = 0;
+        r.cnt = 0;
+        r.angle = 0.f;
+#pragma unroll
+        for (int k = 0; k < kTopK; k++) r.e[k] = ~0ull;
+        if (q < J.nq) {
+            r.flags = g_q[q].flags;
+            r.angle = g_q[q].angle;
+            r.cnt = g_ncand[q];
+            typedef unsigned v4u __attribute__((ext_vector_type(4)));
+            const auto t = (gptr_t<v4u>)(J.topk + (size_t)q * kTopK);
+#pragma unroll
+            for (int k = 0; k < kTopK / 2; k++) {
+                const v4u v = t[k];
+                r.e[2 * k] = ((uint64_t)v.y << 32) | v.x;
+                r.e[2 * k + 1] = ((uint64_t)v.w << 32) | v.z;
+            }
         }
-        if (!(cq.flags & YGZFE_MQ_VALID) || ccnt == 0) continue;
+        return r;
+    };
+    auto store_blk = [&](int buf, const Blk &r) {
+#pragma unroll
+        for (int k = 0; k < kTopK; k++) s_qe[buf][lane * kTopK + k] = r.e[k];
+        wave_lds_order();
+    };
+    Blk cur;
+    if (J.nq > 0) {
+        cur = load_blk(0);
+        store_blk(0, cur);
+    }
+    for (int qb = 0; qb < J.nq; qb += 64) {
+        const int buf = (qb >> 6) & 1;
+        const bool more = qb + 64 < J.nq;
+        Blk nxt;
+        if (more) nxt = load_blk(qb + 64);  // in flight during this block
+        const int qe = min(J.nq, qb + 64);
+        // flags / counts / angles of the block by readlane (lane t holds query qb + t's);
+        // the top-K entries by LDS reads issued one query ahead
+        uint64_t Enext = lane < kTopK ? s_qe[buf][lane] : ~0ull;
+    for (int q = qb; q < qe; q++) {
+        const int t = q - qb;
+        const uint64_t cE = Enext;
+        if (q + 1 < qe) Enext = lane < kTopK ? s_qe[buf][(t + 1) * kTopK + lane] : ~0ull;
+        const int cflags = __builtin_amdgcn_readlane(cur.flags, t), ccnt = __builtin_amdgcn_readlane(cur.cnt, t);
+        if (!(cflags & YGZFE_MQ_VALID) || ccnt == 0) continue;
+        const float cangle = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur.angle), t));
         const int nk = min(ccnt, kTopK);
-        int dist_l = (int)(cE >> 52), j_l = (int)(cE & 0xFFFFF);
+        int dist_l = (int)(cE >> 52), j_l = key_train(cE);
         const bool ok = lane < nk && !skip(j_l, dist_l);
         const uint64_t bal = __ballot(ok);
         uint64_t best = ~0ull, second = ~0ull;
+        auto lane_key = [&](int from) -> uint64_t {  // uniform lane index: no LDS round trip
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cE, from);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cE >> 32), from);
+            return ((uint64_t)hi << 32) | lo;
+        };
         if (__popcll(bal) >= need || ccnt <= kTopK) {
             if (bal) {
-                const int b0 = __builtin_ctzll(bal);
-                best = __shfl(cE, b0, 64);
+                best = lane_key(__builtin_ctzll(bal));
                 const uint64_t rest = bal & (bal - 1);
-                if (rest) second = __shfl(cE, __builtin_ctzll(rest), 64);
+                if (rest) second = lane_key(__builtin_ctzll(rest));
             }
         } else {  // the skips used up the K entries: re-scan this query under the current state
             rescans++;
+            const ygzfe_match_query cq = J.q[q];
             uint32_t qd[8];
             load_qdesc(J, q, qd);
             uint64_t L[kTopK];
@@ -314,22 +393,22 @@ __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict_
             second = wave_min_u64(L[0]);
         }
         const bool has1 = best != ~0ull, has2 = second != ~0ull;
-        const int bj = (int)(best & 0xFFFFF), bd = has1 ? (int)(best >> 52) : 256;
-        const int sj = (int)(second & 0xFFFFF), sdist = has2 ? (int)(second >> 52) : 256;
-        const int id = J.qid ? J.qid[q] : q;
+        const int bj = key_train(best), bd = has1 ? (int)(best >> 52) : 256;
+        const int sj = key_train(second), sdist = has2 ? (int)(second >> 52) : 256;
+        const int id = J.qid ? g_qid[q] : q;
         int push_id = -1;
         if (mode == YGZFE_MATCH_BEST) {
             if (has1 && bd <= th_dist) {
-                if (lane == 0) J.train_out[bj] = q;
-                blocked[bj] = (cq.flags & YGZFE_MQ_BLOCKS) ? 1 : 0;
+                if (lane == 0) g_train_out[bj] = q;
+                blocked[bj] = (cflags & YGZFE_MQ_BLOCKS) ? 1 : 0;
                 nmatches++;
                 push_id = bj;
             }
         } else if (mode == YGZFE_MATCH_RATIO) {
-            const int bl = has1 ? J.kps[bj].octave : -1, sl = has2 ? J.kps[sj].octave : -1;
+            const int bl = has1 ? key_octave(best) : -1, sl = has2 ? key_octave(second) : -1;
             if (has1 && bd <= 100 && !(bl == sl && bd > nnratio * sdist)) {
-                if (lane == 0) J.train_out[bj] = q;
-                blocked[bj] = (cq.flags & YGZFE_MQ_BLOCKS) ? 1 : 0;
+                if (lane == 0) g_train_out[bj] = q;
+                blocked[bj] = (cflags & YGZFE_MQ_BLOCKS) ? 1 : 0;
                 nmatches++;
             }
         } else if (mode == YGZFE_MATCH_INIT) {
@@ -337,10 +416,10 @@ __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict_
             if (has1 && bdi <= 50 && bdi < (float)sdi * nnratio) {
                 const int old = m21[bj];
                 if (old >= 0) {
-                    if (lane == 0) J.query_out[old] = -1;
+                    if (lane == 0) g_query_out[old] = -1;
                     nmatches--;
                 }
-                if (lane == 0) J.query_out[q] = bj;
+                if (lane == 0) g_query_out[q] = bj;
                 m21[bj] = (int16_t)q;
                 mdist[bj] = (uint16_t)bdi;
                 nmatches++;
@@ -348,47 +427,51 @@ __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict_
             }
         } else {  // BOW
             if (has1 && bd <= 50 && (float)bd < nnratio * (float)sdist) {
-                if (lane == 0) J.train_out[bj] = id;
+                if (lane == 0) g_train_out[bj] = id;
                 blocked[bj] = 1;
                 nmatches++;
                 push_id = bj;
             }
         }
-        if (push_id >= 0 && check_ori && mode != YGZFE_MATCH_RATIO) {
-            const int bin = rot_bin(cq.angle, J.kps[bj].angle);
-            if (lane == 0) {
-                rot_count[bin]++;
-                J.pushes[npush] = (bin << 24) | push_id;
-            }
+        if (push_id >= 0 && check_ori && mode != YGZFE_MATCH_RATIO) {  // histogram counted after the loop
+            const int bin = rot_bin(cangle, ang_of(bj));
+            if (lane == 0) g_pushes[npush] = (bin << 24) | push_id;
             npush++;
         }
         wave_lds_order();  // the LDS state updates precede the next query's reads (one wave: DS ops in order)
     }
+        if (more) {
+            store_blk(buf ^ 1, nxt);
+            cur = nxt;
+        }
+    }
     if (check_ori && mode != YGZFE_MATCH_RATIO && npush > 0) {
         __threadfence_block();
+        __syncthreads();  // the pushes are visible to every lane
+        for (int p = lane; p < npush; p += 64) atomicAdd(&rot_count[g_pushes[p] >> 24], 1);
         __syncthreads();
         int i1, i2, i3;
         three_maxima(rot_count, i1, i2, i3);
         int removed = 0;
         for (int p = lane; p < npush; p += 64) {
-            const int v = J.pushes[p], bin = v >> 24, pid = v & 0xFFFFFF;
+            const int v = g_pushes[p], bin = v >> 24, pid = v & 0xFFFFFF;
             if (bin == i1 || bin == i2 || bin == i3) continue;
             if (mode == YGZFE_MATCH_BEST) {
-                J.train_out[pid] = -2;
+                g_train_out[pid] = -2;
                 removed++;
             } else if (mode == YGZFE_MATCH_BOW) {
-                J.train_out[pid] = -1;
+                g_train_out[pid] = -1;
                 removed++;
-            } else if (J.query_out[pid] >= 0) {  // INIT
-                J.query_out[pid] = -1;
+            } else if (g_query_out[pid] >= 0) {  // INIT
+                g_query_out[pid] = -1;
                 removed++;
             }
         }
         nmatches -= wave_sum_i(removed);
     }
     if (lane == 0) {
-        J.nmatches[0] = nmatches;
-        J.nmatches[1] = rescans;  // diagnostics: queries whose top-K list the skips exhausted
+        g_nmatches[0] = nmatches;
+        g_nmatches[1] = rescans;  // diagnostics: queries whose top-K list the skips exhausted
     }
 }
 
@@ -397,9 +480,10 @@ hipError_t launch_match(const MatchJob *d_jobs, int njobs, int max_q, int max_tr
     if (njobs <= 0) return hipSuccess;
     if (max_q > 0)
         hipLaunchKernelGGL(k_match_topk, dim3((max_q + 3) / 4, njobs), dim3(256), 0, st, d_jobs, max_q);
-    const size_t lds = (size_t)((max_train + 15) & ~15) +
-                       (mode == YGZFE_MATCH_INIT ? 2 * (size_t)((max_train + 7) & ~7) * 2 : 0) + 64;
-    hipLaunchKernelGGL(k_match_replay, dim3(njobs), dim3(64), lds, st, d_jobs, mode, th_dist, check_ori, nnratio);
+    const size_t lds = replay_lds_base(max_train, mode) +
+                       (staged_kp_fits(max_train, mode) ? 5 * (size_t)((max_train + 3) & ~3) : 0) + 64;
+    hipLaunchKernelGGL(k_match_replay, dim3(njobs), dim3(64), lds, st, d_jobs, mode, th_dist, check_ori, nnratio,
+                       (int)staged_kp_fits(max_train, mode));
     return hipGetLastError();
 }
 
