@@ -49,6 +49,14 @@ static int ensure_device(int device) {
     std::lock_guard<std::mutex> lk(mu);
     if (device < 64 && !uploaded[device]) {
         YGZ_HIP(upload_pattern(kPatternHost));
+        uint32_t fails[2] = {0, 0};
+        YGZ_HIP(run_arith_guard(fails));
+        if (fails[0] || fails[1]) {
+            set_error("arithmetic guard failed on device %d (f16 ordering: %u, cvRound: %u mismatches): the "
+                      "library was built with flags that break its bit-exact paths (fast-math, denormal flush)",
+                      device, fails[0], fails[1]);
+            return YGZFE_EHIP;
+        }
         uploaded[device] = true;
     }
     return YGZFE_OK;
@@ -2274,6 +2282,7 @@ struct ygzfe_match_frame {
     DevBuf kps, desc, uright, cell;
     std::vector<ygzfe_kp> host_kps;  // angles / octaves / positions the host-side query building reads
     int last_rescans = 0;            // queries of the last search whose top-K list the skips exhausted
+    int last_passes = -1;            // parallel-resolve passes of the last search (-1: serial replay)
     // per-call staging: page-locked, one DMA per direction; ev_in = the last H2D out of
     // hin / hset (the next call refills them only after it)
     DevBuf in, out, scratch;
@@ -2284,6 +2293,7 @@ struct ygzfe_match_frame {
 namespace {
 
 constexpr int kMatchTopK = 8;  // match.hip kTopK
+constexpr int kMatchResolvePasses = 32;  // k_match_resolve pass budget before the serial replay
 
 struct Arena {
     size_t off = 0;
@@ -2348,7 +2358,7 @@ int run_match(MatchCall &c) {
     Arena ao;
     const size_t o_tout = ao.take(sizeof(int32_t) * (size_t)std::max(n, 1));
     const size_t o_qout = ao.take(sizeof(int32_t) * (size_t)std::max(nq, 1));
-    const size_t o_nm = ao.take(2 * sizeof(int32_t));
+    const size_t o_nm = ao.take(4 * sizeof(int32_t));
     const size_t out_bytes = ao.off;
     const size_t o_topk = ao.take(sizeof(uint64_t) * kMatchTopK * (size_t)std::max(nq, 1));
     const size_t o_ncand = ao.take(sizeof(int32_t) * (size_t)std::max(nq, 1));
@@ -2393,8 +2403,11 @@ int run_match(MatchCall &c) {
     YGZ_HIP(hipMemcpyAsync(din, h, ai.off, hipMemcpyHostToDevice, st));
     if (!f->ev_in) YGZ_HIP(hipEventCreateWithFlags(&f->ev_in, hipEventDisableTiming));
     YGZ_HIP(hipEventRecord(f->ev_in, st));
+    // YGZFE_MATCH_PASSES: the parallel resolve's pass budget (0 = serial replay; tests force both)
+    const char *ev = getenv("YGZFE_MATCH_PASSES");
+    const int max_passes = ev ? atoi(ev) : kMatchResolvePasses;
     YGZ_HIP(launch_match(reinterpret_cast<const MatchJob *>(din + o_job), 1, nq, n, c.mode, c.th_dist, c.check_ori,
-                         c.nnratio, st));
+                         c.nnratio, max_passes, st));
     YGZ_TRY(f->hout.ensure(out_bytes));
     YGZ_HIP(hipMemcpyAsync(f->hout.p, dout, out_bytes, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipStreamSynchronize(st));
@@ -2403,6 +2416,7 @@ int run_match(MatchCall &c) {
     if (c.query_out && nq) memcpy(c.query_out, ho + o_qout, sizeof(int32_t) * nq);
     memcpy(&c.nmatches, ho + o_nm, sizeof(int32_t));
     memcpy(&f->last_rescans, ho + o_nm + 4, sizeof(int32_t));
+    memcpy(&f->last_passes, ho + o_nm + 8, sizeof(int32_t));
     return YGZFE_OK;
 }
 
@@ -2430,6 +2444,12 @@ extern "C" void ygzfe_match_frame_destroy(ygzfe_match_frame *f) {
 extern "C" int ygzfe_match_frame_stats(const ygzfe_match_frame *f, int *rescans) {
     if (!f || !rescans) { set_error("invalid argument"); return YGZFE_EINVAL; }
     *rescans = f->last_rescans;
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_match_frame_resolve_stats(const ygzfe_match_frame *f, int *passes) {
+    if (!f || !passes) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    *passes = f->last_passes;
     return YGZFE_OK;
 }
 

@@ -2582,6 +2582,42 @@ static int device_cus() {
     return n;
 }
 
+// Arithmetic guard, run once per device before the first call (api.cpp
+// ensure_device): the two bit-level tricks the kernels rest on, evaluated with this
+// translation unit's own flags and helpers, so a build or mode change that breaks them
+// (fast-math, f16 denormal flushing, a rounding mode other than nearest-even) fails
+// every call instead of shifting corners or descriptor bits silently.
+//   fails[0]: k_fast_cells' f16 ordering — bytes 0..255 as f16 bit patterns (+0 and
+//             subnormals) must min / max exactly like the integers (hmin3 / hmax3);
+//   fails[1]: k_orient_desc's cvRound — bits(v + 2^23 + 64) - bits(2^23 + 64) must be
+//             round-half-even(v) over the taps' range |v| <= 18.4, incl. every .5.
+__global__ __launch_bounds__(256) void k_arith_guard(uint32_t *__restrict__ fails) {
+    const int a = blockIdx.x, b = threadIdx.x;
+    const h16x2 ha = as_h16x2((uint32_t)a | ((uint32_t)b << 16)), hb = as_h16x2((uint32_t)b | ((uint32_t)a << 16));
+    const uint32_t mn = as_u32(hmin3(ha, hb, hb)), mx = as_u32(hmax3(ha, ha, hb));
+    const uint32_t lo = (uint32_t)min(a, b), hi = (uint32_t)max(a, b);
+    if (mn != (lo | (lo << 16)) || mx != (hi | (hi << 16))) atomicAdd(&fails[0], 1u);
+    if (a < 160) {  // v = (a - 80) / 4 + b / 1024: quarters, halves, and values between
+        const float v = (float)(a - 80) * 0.25f + (float)b * (1.0f / 1024.0f);
+        const float magic = __uint_as_float(kMagicBits + 64u);
+        const int got = (int)(__float_as_uint(v + magic) - (kMagicBits + 64u));
+        if (got != (int)__builtin_rintf(v)) atomicAdd(&fails[1], 1u);
+    }
+}
+
+hipError_t run_arith_guard(uint32_t host_fails[2]) {
+    uint32_t *d = nullptr;
+    hipError_t e = hipMalloc(&d, 2 * sizeof(uint32_t));
+    if (e != hipSuccess) return e;
+    if ((e = hipMemset(d, 0, 2 * sizeof(uint32_t))) == hipSuccess) {
+        hipLaunchKernelGGL(k_arith_guard, dim3(256), dim3(256), 0, 0, d);
+        if ((e = hipGetLastError()) == hipSuccess)
+            e = hipMemcpy(host_fails, d, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(d);
+    return e;
+}
+
 hipError_t upload_pattern(const int *pat) {
     int8_t p8[1024];
     for (int i = 0; i < 1024; i++) p8[i] = (int8_t)pat[i];

@@ -6,6 +6,7 @@ namespace ygzfe {
 
 // extract.hip
 hipError_t upload_pattern(const int *pat);
+hipError_t run_arith_guard(uint32_t host_fails[2]);  // extract.hip k_arith_guard
 hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const int *dtabs,
                           int nframes, hipStream_t st);
 hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
@@ -73,12 +74,13 @@ struct MatchJob {
     int32_t *train_out;         // [n_train]
     int32_t *query_out;         // INIT: vnMatches12 [nq]
     int32_t *pushes;            // [nq] rotation-histogram pushes
-    int32_t *nmatches;          // [1]
+    int32_t *nmatches;          // [4]: matches, rescans, resolve passes (-1: serial replay), spare
 };
 hipError_t launch_match_cells(const ygzfe_kp *kps, int n, float min_x, float min_y, float inv_w, float inv_h,
                               int32_t *cell, hipStream_t st);
+// max_passes: the parallel resolve's pass budget (0: serial replay only)
 hipError_t launch_match(const MatchJob *d_jobs, int njobs, int max_q, int max_train, int mode, int th_dist,
-                        int check_ori, float nnratio, hipStream_t st);
+                        int check_ori, float nnratio, int max_passes, hipStream_t st);
 
 // align.hip
 struct AlignLevels {

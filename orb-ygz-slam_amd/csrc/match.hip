@@ -255,12 +255,269 @@ __host__ __device__ __forceinline__ bool staged_kp_fits(int n, int mode) {
     return replay_lds_base(n, mode) + 5 * (size_t)((n + 3) & ~3) + 64 <= 65536;
 }
 
+// ---------------------------------------------------------------------------
+// k_match_resolve: the same sequential result, found in parallel.
+//
+// A query's decision depends on the state its candidates are in when the
+// reference's loop reaches it, and that state is written only by earlier
+// queries' matches: train keypoint j is skipped by query q iff the LAST query
+// p < q that matched j set it (BEST / RATIO: p's MapPoint has observations —
+// the test `mvpMapPoints[i2]->Observations() > 0`, ORBmatcher.cc:1290-1292 /
+// :76-78; BoW: always, `vpMapPointMatches[realIdxF]` set, :210-211), else its
+// initial state.  So decisions d_q = f_q(d_0 .. d_{q-1}) with f_q strictly
+// causal, and the iteration d^{k+1}_q = f_q(d^k) (every query re-decided
+// against the previous pass's decisions, all at once) has exactly one fixed
+// point, the sequential result, reached after at most (longest chain of
+// queries whose decisions feed each other) + 1 passes (4-5 on the test scenes).
+// A pass: the matched queries are linked per train keypoint in LDS (atomic
+// exchange into head[j]); each query walks its top-K entries in order and, for
+// each, the entry's list for the latest chooser before it.  A pass that changes
+// no decision ends the loop.
+//
+// A query whose skips exhaust its top-K entries of a longer candidate list needs
+// its whole candidate list under the current state (the serial path's re-scan).
+// Once the passes settle with such queries present, the train keypoints are
+// bucketed by grid cell in LDS (counting sort) and the passes continue with
+// those queries scanning their GetFeaturesInArea cells (or BoW node list) in
+// their own thread.  If the pass budget runs out the status word hands the job
+// to k_match_replay (the serial replay from scratch); otherwise the outputs are
+// written here and k_match_replay exits on entry.
+// ---------------------------------------------------------------------------
+constexpr int kResolveThreads = 1024;
+constexpr int kGridCells = kGridCols * kGridRows;  // 3072 = 3 per thread
+static_assert(kGridCells == 3 * kResolveThreads, "cell scan: 3 cells per thread");
+__host__ __device__ __forceinline__ size_t resolve_lds_bytes(int n, int nq) {
+    return 4 * (size_t)n + 8 * (size_t)nq + 4 * (size_t)kGridCells + 2 * (size_t)((n + 1) & ~1) +
+           (size_t)((nq + 3) & ~3);
+}
+
+__global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJob *__restrict__ jobs, int mode,
+                                                                   int th_dist, int check_ori, float nnratio,
+                                                                   int max_passes) {
+    extern __shared__ uint8_t lds[];
+    const MatchJob J = jobs[blockIdx.x];
+    const int tid = threadIdx.x, n = J.n_train, nq = J.nq;
+    int32_t *head = reinterpret_cast<int32_t *>(lds);       // [n]  latest linked chooser of j
+    int32_t *link = head + n;                               // [nq] next chooser of the same j
+    int32_t *choice = link + nq;                            // [nq] matched train index, -1 none, -2 re-scan
+    int32_t *cend = choice + nq;                            // [cells] end of each cell's keypoints in sidx
+    uint16_t *sidx = reinterpret_cast<uint16_t *>(cend + kGridCells);             // [n] keypoints by cell
+    uint8_t *qbl = reinterpret_cast<uint8_t *>(sidx + ((n + 1) & ~1));            // [nq] q's match blocks
+    __shared__ int s_rot[kHisto + 2];
+    __shared__ int s_sum[16];
+    const auto g_topk = as_global(J.topk);
+    const auto g_ncand = as_global(J.ncand);
+    const auto g_q = as_global(J.q);
+    const auto g_blocked0 = as_global(J.blocked0);
+    const auto g_kps = as_global(J.kps);
+    const int need = mode == YGZFE_MATCH_BEST ? 1 : 2;
+    for (int q = tid; q < nq; q += kResolveThreads) {
+        choice[q] = -1;
+        qbl[q] = mode == YGZFE_MATCH_BOW ? 1 : ((g_q[q].flags & YGZFE_MQ_BLOCKS) ? 1 : 0);
+    }
+    for (int j = tid; j < n; j += kResolveThreads) head[j] = -1;
+    // the state query q sees keypoint j in: set by the latest chooser before q
+    auto blocked_at = [&](int j, int q) -> bool {
+        int last = -1;
+        for (int p = head[j]; p >= 0; p = link[p])
+            if (p < q && p > last) last = p;
+        return last >= 0 ? qbl[last] != 0 : (J.blocked0 ? g_blocked0[j] != 0 : false);
+    };
+    // the serial path's re-scan, in one thread: the whole candidate list under the state
+    auto rescan = [&](int q, uint64_t &best, uint64_t &second) {
+        const ygzfe_match_query Q = J.q[q];
+        uint32_t qd[8];
+        load_qdesc(J, q, qd);
+        best = second = ~0ull;
+        auto consider = [&](int j, uint32_t order) {
+            if (blocked_at(j, q)) return;
+            const uint64_t key = make_key(hamming32(qd, J.desc + (size_t)j * 32), order, j, g_kps[j].octave);
+            if (key < best) {
+                second = best;
+                best = key;
+            } else if (key < second) {
+                second = key;
+            }
+        };
+        if (J.cand_ptr) {
+            const int b = J.cand_ptr[2 * q], e = J.cand_ptr[2 * q + 1];
+            for (int p = b; p < e; p++) consider(J.cand[p], (uint32_t)(p - b));
+        } else {
+            const Window w = make_window(J, Q);
+            for (int ix = w.cx0; ix <= w.cx1; ix++)
+                for (int iy = w.cy0; iy <= w.cy1; iy++) {
+                    const int c = ix * kGridRows + iy;
+                    for (int t = c ? cend[c - 1] : 0; t < cend[c]; t++) {
+                        const int j = sidx[t];
+                        const uint32_t o = window_order(J, w, Q, j);
+                        if (o != ~0u) consider(j, o);
+                    }
+                }
+        }
+    };
+    // query q's decision against the chooser lists of the previous pass
+    auto decide = [&](int q, bool full) -> int {
+        const int flags = g_q[q].flags, cnt = g_ncand[q];
+        if (!(flags & YGZFE_MQ_VALID) || cnt == 0) return -1;
+        const int nk = min(cnt, kTopK);
+        uint64_t best = ~0ull, second = ~0ull;
+        int found = 0;
+        for (int k = 0; k < nk && found < need; k++) {
+            const uint64_t e = g_topk[(size_t)q * kTopK + k];
+            if (blocked_at(key_train(e), q)) continue;
+            if (found == 0) best = e;
+            else second = e;
+            found++;
+        }
+        if (found < need && cnt > kTopK) {
+            if (!full) return -2;
+            rescan(q, best, second);
+        }
+        const bool has1 = best != ~0ull, has2 = second != ~0ull;
+        const int bd = has1 ? (int)(best >> 52) : 256, sdist = has2 ? (int)(second >> 52) : 256;
+        bool ok;
+        if (mode == YGZFE_MATCH_BEST) {
+            ok = has1 && bd <= th_dist;
+        } else if (mode == YGZFE_MATCH_RATIO) {
+            const int bl = has1 ? key_octave(best) : -1, sl = has2 ? key_octave(second) : -1;
+            ok = has1 && bd <= 100 && !(bl == sl && bd > nnratio * sdist);
+        } else {  // BOW
+            ok = has1 && bd <= 50 && (float)bd < nnratio * (float)sdist;
+        }
+        return ok ? key_train(best) : -1;
+    };
+    // keypoints bucketed by cell (cell-major ix * rows + iy), for the re-scans
+    auto build_cells = [&]() {
+        for (int c = tid; c < kGridCells; c += kResolveThreads) cend[c] = 0;
+        __syncthreads();
+        for (int j = tid; j < n; j += kResolveThreads) {
+            const int c = J.cell[j];
+            if (c >= 0) atomicAdd(&cend[(c >> 8) * kGridRows + (c & 0xFF)], 1);
+        }
+        __syncthreads();
+        const int c0 = 3 * tid;
+        const int a0 = cend[c0], a1 = cend[c0 + 1], a2 = cend[c0 + 2], sum = a0 + a1 + a2;
+        const int lane = tid & 63, wv = tid >> 6;
+        int incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) s_sum[wv] = incl;
+        __syncthreads();
+        int base = 0;
+        for (int k = 0; k < wv; k++) base += s_sum[k];
+        const int start = base + incl - sum;  // exclusive start of cell c0
+        cend[c0] = start;                     // starts for now; the scatter advances them to ends
+        cend[c0 + 1] = start + a0;
+        cend[c0 + 2] = start + a0 + a1;
+        __syncthreads();
+        for (int j = tid; j < n; j += kResolveThreads) {
+            const int c = J.cell[j];
+            if (c >= 0) sidx[atomicAdd(&cend[(c >> 8) * kGridRows + (c & 0xFF)], 1)] = (uint16_t)j;
+        }
+        __syncthreads();
+    };
+    __syncthreads();
+    int pass = 0;
+    bool converged = false, full = false;
+    while (pass < max_passes) {
+        if (pass > 0) {  // link the previous pass's matches per keypoint
+            for (int j = tid; j < n; j += kResolveThreads) head[j] = -1;
+            __syncthreads();
+            for (int q = tid; q < nq; q += kResolveThreads) {
+                const int c = choice[q];
+                if (c >= 0) link[q] = atomicExch(&head[c], q);
+            }
+            __syncthreads();
+        }
+        int changed = 0, pending = 0;
+        for (int q = tid; q < nq; q += kResolveThreads) {
+            const int c = decide(q, full);
+            changed |= c != choice[q];
+            pending |= c == -2;
+            choice[q] = c;  // lists are not rebuilt until the next pass: no reader sees this
+        }
+        pass++;
+        if (!__syncthreads_or(changed)) {
+            if (!__syncthreads_or(pending)) {
+                converged = true;
+                break;
+            }
+            build_cells();  // settled with re-scans outstanding: the next passes do them
+            full = true;
+        }
+    }
+    if (!converged) {
+        if (tid == 0) as_global_mut(J.nmatches)[2] = -1;  // k_match_replay takes the job
+        return;
+    }
+    // outputs: train_out[j] = the last query that matched j
+    const auto g_train_out = as_global_mut(J.train_out);
+    const auto g_qid = as_global(J.qid);
+    for (int j = tid; j < n; j += kResolveThreads) {
+        int last = -1;
+        for (int p = head[j]; p >= 0; p = link[p]) last = max(last, p);
+        if (J.train_out) g_train_out[j] = last < 0 ? -1 : (mode == YGZFE_MATCH_BOW && J.qid ? g_qid[last] : last);
+    }
+    if (tid < kHisto + 2) s_rot[tid] = 0;
+    __syncthreads();
+    int matched = 0, nrescan = 0;
+    const bool ori = check_ori && mode != YGZFE_MATCH_RATIO;
+    for (int q = tid; q < nq; q += kResolveThreads) {
+        const int c = choice[q];
+        if (c < 0) continue;
+        matched++;
+        if (ori) atomicAdd(&s_rot[rot_bin(g_q[q].angle, g_kps[c].angle)], 1);
+    }
+    __syncthreads();
+    int removed = 0;
+    if (ori) {
+        int i1, i2, i3;
+        three_maxima(s_rot, i1, i2, i3);
+        for (int q = tid; q < nq; q += kResolveThreads) {
+            const int c = choice[q];
+            if (c < 0) continue;
+            const int bin = rot_bin(g_q[q].angle, g_kps[c].angle);
+            if (bin == i1 || bin == i2 || bin == i3) continue;
+            if (J.train_out) g_train_out[c] = mode == YGZFE_MATCH_BEST ? -2 : -1;
+            removed++;
+        }
+    }
+    if (full)  // diagnostics: the queries whose top-K list the final state exhausts
+        for (int q = tid; q < nq; q += kResolveThreads) {
+            const int cnt = g_ncand[q];
+            if (!(g_q[q].flags & YGZFE_MQ_VALID) || cnt <= kTopK) continue;
+            int found = 0;
+            for (int k = 0; k < kTopK && found < need; k++)
+                found += !blocked_at(key_train(g_topk[(size_t)q * kTopK + k]), q);
+            nrescan += found < need;
+        }
+    const int net = wave_sum_i(matched - removed), nr = wave_sum_i(nrescan);
+    __syncthreads();  // s_sum reused
+    if ((tid & 63) == 0) s_sum[tid >> 6] = net | (nr << 20);
+    __syncthreads();
+    if (tid == 0) {
+        int tot = 0, totr = 0;
+        for (int k = 0; k < kResolveThreads / 64; k++) {
+            tot += s_sum[k] & 0xFFFFF;
+            totr += s_sum[k] >> 20;
+        }
+        const auto g_nm = as_global_mut(J.nmatches);
+        g_nm[0] = tot;
+        g_nm[1] = totr;
+        g_nm[2] = pass;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict__ jobs, int mode, int th_dist,
-                                                     int check_ori, float nnratio, int stage_kv) {
+                                                     int check_ori, float nnratio, int stage_kv, int resolved_first) {
     extern __shared__ uint8_t lds[];
     // the job's fields in registers: the loop's global stores could otherwise alias the
     // job record and force a reload of every field (a scalar-load latency per query)
     const MatchJob J = jobs[blockIdx.x];
+    if (resolved_first && as_global(J.nmatches)[2] >= 0) return;  // k_match_resolve wrote the outputs
     const auto g_train_out = as_global_mut(J.train_out), g_query_out = as_global_mut(J.query_out);
     const auto g_pushes = as_global_mut(J.pushes), g_nmatches = as_global_mut(J.nmatches);
     const auto g_q = as_global(J.q);
@@ -472,18 +729,25 @@ __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict_
     if (lane == 0) {
         g_nmatches[0] = nmatches;
         g_nmatches[1] = rescans;  // diagnostics: queries whose top-K list the skips exhausted
+        g_nmatches[2] = -1;       // the serial replay decided
     }
 }
 
 hipError_t launch_match(const MatchJob *d_jobs, int njobs, int max_q, int max_train, int mode, int th_dist,
-                        int check_ori, float nnratio, hipStream_t st) {
+                        int check_ori, float nnratio, int max_passes, hipStream_t st) {
     if (njobs <= 0) return hipSuccess;
     if (max_q > 0)
         hipLaunchKernelGGL(k_match_topk, dim3((max_q + 3) / 4, njobs), dim3(256), 0, st, d_jobs, max_q);
+    // INIT's skip state is a distance, and a re-match unmatches the previous query: serial only
+    const size_t rl = resolve_lds_bytes(max_train, max_q);
+    const bool resolve = max_passes > 0 && mode != YGZFE_MATCH_INIT && rl <= 65536;
+    if (resolve)
+        hipLaunchKernelGGL(k_match_resolve, dim3(njobs), dim3(kResolveThreads), rl, st, d_jobs, mode, th_dist,
+                           check_ori, nnratio, max_passes);
     const size_t lds = replay_lds_base(max_train, mode) +
                        (staged_kp_fits(max_train, mode) ? 5 * (size_t)((max_train + 3) & ~3) : 0) + 64;
     hipLaunchKernelGGL(k_match_replay, dim3(njobs), dim3(64), lds, st, d_jobs, mode, th_dist, check_ori, nnratio,
-                       (int)staged_kp_fits(max_train, mode));
+                       (int)staged_kp_fits(max_train, mode), (int)resolve);
     return hipGetLastError();
 }
 

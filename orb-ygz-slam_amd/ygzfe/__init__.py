@@ -357,6 +357,12 @@ class MatchFrame:
         _check(lib().ygzfe_match_frame_stats(self.h, C.byref(r)), "match_frame_stats")
         return r.value
 
+    def resolve_passes(self):
+        """Parallel-resolve passes of the last search (-1: the serial replay decided)."""
+        r = C.c_int()
+        _check(lib().ygzfe_match_frame_resolve_stats(self.h, C.byref(r)), "match_frame_resolve_stats")
+        return r.value
+
     def from_batch(self, batch, frame, bounds=(0.0, 752.0, 0.0, 480.0)):
         b = Bounds(*[float(x) for x in bounds])
         _check(lib().ygzfe_match_frame_from_batch(self.h, batch.h, frame, C.byref(b)), "match_frame_from_batch")

@@ -9,7 +9,13 @@ literal restatement of the reference loops (oracle/match.c), bit-exact on every 
 
 C2 (EuRoC 752x480, 1000 features) and C4 (TUM 640x480, 2000 features) frame pairs, rotation
 check on and off, plus dense windows where the sequential skips exhaust the GPU's per-query
-top-K list (the re-scan path)."""
+top-K list (the re-scan path).
+
+Every test runs twice: with the parallel resolve (k_match_resolve, the default) and with
+the serial replay alone (YGZFE_MATCH_PASSES=0); test_resolve_pass_budget covers the
+hand-over when the pass budget runs out."""
+import os
+
 import numpy as np
 import pytest
 
@@ -19,6 +25,20 @@ import _scenes as S
 pytestmark = pytest.mark.gpu
 
 PAIRS = {}
+
+
+@pytest.fixture(autouse=True, params=["resolve", "serial"])
+def decide(request):
+    old = os.environ.get("YGZFE_MATCH_PASSES")
+    if request.param == "serial":
+        os.environ["YGZFE_MATCH_PASSES"] = "0"
+    else:
+        os.environ.pop("YGZFE_MATCH_PASSES", None)
+    yield request.param
+    if old is None:
+        os.environ.pop("YGZFE_MATCH_PASSES", None)
+    else:
+        os.environ["YGZFE_MATCH_PASSES"] = old
 
 
 def pair(cfg, seed):
@@ -37,7 +57,7 @@ def gpu_frame(gpu, kps, desc, ur, p):
 
 @pytest.mark.parametrize("cfg,seed", [("C2", 0), ("C2", 1), ("C4", 2)])
 @pytest.mark.parametrize("check_ori", [True, False])
-def test_search_by_projection_last_frame(gpu, cfg, seed, check_ori):
+def test_search_by_projection_last_frame(gpu, cfg, seed, check_ori, decide):
     p = pair(cfg, seed)
     for th, lm in ((7.0, "mixed"), (15.0, "band"), (14.0, "none")):
         Q, qd, ur, bl = S.projection_queries(p, seed, th=th, level_mode=lm)
@@ -46,6 +66,7 @@ def test_search_by_projection_last_frame(gpu, cfg, seed, check_ori):
         want, wn = O.search_projection_best(O.mframe(p["k1"], p["d1"], ur, bounds(p)), Q, qd, bl, 100, check_ori)
         assert gn == wn and np.array_equal(got, want), (th, lm, gn, wn, np.flatnonzero(got != want)[:10])
         assert wn > 50  # the scene really matches
+        assert (cur.resolve_passes() >= 1) == (decide == "resolve")  # the path under test decided
 
 
 @pytest.mark.parametrize("check_ori", [True, False])
@@ -63,7 +84,7 @@ def test_search_by_projection_keyframe_relocalisation(gpu, check_ori):
 
 
 @pytest.mark.parametrize("cfg,seed", [("C2", 1), ("C4", 2)])
-def test_search_by_projection_local_map_ratio(gpu, cfg, seed):
+def test_search_by_projection_local_map_ratio(gpu, cfg, seed, decide):
     p = pair(cfg, seed)
     for nnratio, lm in ((0.8, "band"), (0.6, "mixed"), (1.0, "none")):
         Q, qd, ur, bl = S.projection_queries(p, seed + 10, th=3.0 * 2.5, level_mode=lm)
@@ -72,6 +93,7 @@ def test_search_by_projection_local_map_ratio(gpu, cfg, seed):
         want, wn = O.search_projection_ratio(O.mframe(p["k1"], p["d1"], ur, bounds(p)), Q, qd, bl, nnratio)
         assert gn == wn and np.array_equal(got, want), (nnratio, lm)
         assert wn > 30
+        assert (F.resolve_passes() >= 1) == (decide == "resolve")
 
 
 @pytest.mark.parametrize("cfg,seed", [("C2", 0), ("C4", 2)])
@@ -96,7 +118,7 @@ def test_search_for_initialization(gpu, cfg, seed, check_ori, window):
 
 @pytest.mark.parametrize("check_ori", [True, False])
 @pytest.mark.parametrize("n_nodes", [40, 400])
-def test_search_by_bow(gpu, check_ori, n_nodes):
+def test_search_by_bow(gpu, check_ori, n_nodes, decide):
     """Tracking.cc:1018-1020 ORBmatcher(0.7, false) and :1847 (0.75, true)."""
     p = pair("C2", 1)
     rng = np.random.default_rng(n_nodes)
@@ -114,6 +136,7 @@ def test_search_by_bow(gpu, check_ori, n_nodes):
                                    O.mframe(p["k1"], p["d1"], None, bounds(p)), usable, fv0, fv1, nnratio, check_ori)
         assert gn == wn and np.array_equal(got, want), nnratio
         assert wn > 10
+        assert (F.resolve_passes() >= 1) == (decide == "resolve")
 
 
 def sub_fv(fv, keep):
@@ -160,3 +183,24 @@ def test_empty_inputs(gpu):
     Q, qd, _, _ = S.projection_queries(p, 1)
     got, gn = gpu.search_projection_best(none, Q, qd, None, 100, True)
     assert gn == 0 and len(got) == 0
+
+
+def test_resolve_pass_budget(gpu, decide):
+    """Budgets of 1..3 passes: when the chains of dependent decisions are longer, the
+    resolve hands the job to the serial replay (passes -1); the result never changes."""
+    if decide == "serial":
+        pytest.skip("budget sweep runs once")
+    p = pair("C2", 0)
+    Q, qd, ur, bl = S.projection_queries(p, 4, th=15.0, level_mode="none", blocks_frac=1.0)
+    cur = gpu_frame(gpu, p["k1"], p["d1"], ur, p)
+    want, wn = O.search_projection_best(O.mframe(p["k1"], p["d1"], ur, bounds(p)), Q, qd, bl, 100, True)
+    seen = set()
+    try:
+        for budget in ("1", "2", "3", "64"):
+            os.environ["YGZFE_MATCH_PASSES"] = budget
+            got, gn = gpu.search_projection_best(cur, Q, qd, bl, 100, True)
+            assert gn == wn and np.array_equal(got, want), budget
+            seen.add(cur.resolve_passes() >= 1)
+    finally:
+        os.environ.pop("YGZFE_MATCH_PASSES", None)
+    assert seen == {True, False}  # both the hand-over and the resolved path ran
