@@ -238,8 +238,8 @@ int ygzfe_match_frame_set(ygzfe_match_frame *f, const ygzfe_kp *kps, const uint8
  * sequential skips exhausted their K best candidates (the result never depends on it). */
 int ygzfe_match_frame_stats(const ygzfe_match_frame *f, int *rescans);
 /* Passes the parallel resolve of the last search took to reach the sequential
- * result (-1: the serial replay decided; environment YGZFE_MATCH_PASSES sets the
- * pass budget, 0 = serial replay only).  Results are identical either way. */
+ * result (-1: the serial replay decided: SearchForInitialization, > 4096 queries,
+ * or environment YGZFE_MATCH_PASSES=0).  Results are identical either way. */
 int ygzfe_match_frame_resolve_stats(const ygzfe_match_frame *f, int *passes);
 /* The same from frame `frame` of a batch (device-to-device copy of its rows). */
 int ygzfe_match_frame_from_batch(ygzfe_match_frame *f, ygzfe_batch *b, int frame, const ygzfe_bounds *bounds);

@@ -2292,8 +2292,7 @@ struct ygzfe_match_frame {
 
 namespace {
 
-constexpr int kMatchTopK = 8;  // match.hip kTopK
-constexpr int kMatchResolvePasses = 32;  // k_match_resolve pass budget before the serial replay
+constexpr int kMatchTopK = 32;  // match.hip kTopList (J.topk stride)
 
 struct Arena {
     size_t off = 0;
@@ -2403,9 +2402,9 @@ int run_match(MatchCall &c) {
     YGZ_HIP(hipMemcpyAsync(din, h, ai.off, hipMemcpyHostToDevice, st));
     if (!f->ev_in) YGZ_HIP(hipEventCreateWithFlags(&f->ev_in, hipEventDisableTiming));
     YGZ_HIP(hipEventRecord(f->ev_in, st));
-    // YGZFE_MATCH_PASSES: the parallel resolve's pass budget (0 = serial replay; tests force both)
+    // YGZFE_MATCH_PASSES=0 selects the serial replay (tests run both paths)
     const char *ev = getenv("YGZFE_MATCH_PASSES");
-    const int max_passes = ev ? atoi(ev) : kMatchResolvePasses;
+    const int max_passes = ev ? atoi(ev) : 1;
     YGZ_HIP(launch_match(reinterpret_cast<const MatchJob *>(din + o_job), 1, nq, n, c.mode, c.th_dist, c.check_ori,
                          c.nnratio, max_passes, st));
     YGZ_TRY(f->hout.ensure(out_bytes));
@@ -2417,6 +2416,11 @@ int run_match(MatchCall &c) {
     memcpy(&c.nmatches, ho + o_nm, sizeof(int32_t));
     memcpy(&f->last_rescans, ho + o_nm + 4, sizeof(int32_t));
     memcpy(&f->last_passes, ho + o_nm + 8, sizeof(int32_t));
+    if (max_passes > 0 && f->last_passes < 0 && c.mode != YGZFE_MATCH_INIT && nq > 0 && nq <= 4096 &&
+        resolve_fits(n, nq)) {
+        set_error("match resolve did not reach its fixed point within nq + 2 passes (internal error)");
+        return YGZFE_EHIP;
+    }
     return YGZFE_OK;
 }
 

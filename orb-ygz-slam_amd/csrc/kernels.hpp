@@ -78,7 +78,9 @@ struct MatchJob {
 };
 hipError_t launch_match_cells(const ygzfe_kp *kps, int n, float min_x, float min_y, float inv_w, float inv_h,
                               int32_t *cell, hipStream_t st);
-// max_passes: the parallel resolve's pass budget (0: serial replay only)
+// max_passes: 0 = serial replay only (k_match_replay); otherwise the parallel resolve
+// (k_match_resolve) wherever resolve_fits, INIT always serial
+bool resolve_fits(int n_train, int nq);
 hipError_t launch_match(const MatchJob *d_jobs, int njobs, int max_q, int max_train, int mode, int th_dist,
                         int check_ori, float nnratio, int max_passes, hipStream_t st);
 

@@ -33,8 +33,19 @@
 
 namespace ygzfe {
 
+#ifdef YGZ_STAMPS  // diagnostic build: this file's kernels stamp into their own buffer
+__device__ unsigned long long g_mstamps[1 << 20];
+#define g_bstamps g_mstamps
+extern "C" int ygzfe_diag_match_stamps(unsigned long long *out, int n) {
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mstamps), sizeof(unsigned long long) * (size_t)n);
+    return 0;
+}
+#endif
+
 constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS / ROWS (Frame.h:27-28)
-constexpr int kTopK = 8;
+constexpr int kTopK = 8;      // per-lane list, and the entries the decisions keep in registers
+constexpr int kTopList = 32;  // entries k_match_topk lists per query (J.topk stride)
 constexpr int kHisto = 30;                       // ORBmatcher::HISTO_LENGTH (ORBmatcher.cc:38)
 
 // Frame::PosInGrid (Frame.cc:483-493): std::round(float), cell -1 when outside
@@ -173,18 +184,32 @@ __device__ __forceinline__ void load_qdesc(const MatchJob &J, int q, uint32_t qd
     qd[4] = b.x; qd[5] = b.y; qd[6] = b.z; qd[7] = b.w;
 }
 
-// wave-merge of the lanes' sorted lists: the K smallest keys, ascending, in lanes 0..K-1
-__device__ __forceinline__ uint64_t merge_topk(uint64_t L[kTopK]) {
+// wave-merge of the lanes' sorted lists: the smallest keys, ascending, in lanes
+// 0..V-1.  Each lane holds its kTopK best; the merge pops up to kTopList keys and
+// stops after popping the last held key of a lane that had more candidates (the
+// next key could be that lane's unseen one), so the first V keys are exactly the
+// V best.  V >= min(count, kTopK) always.
+__device__ __forceinline__ uint64_t merge_topk(uint64_t L[kTopK], int lane_count, int &V) {
     const int lane = threadIdx.x & 63;
     uint64_t mine = ~0ull;
-#pragma unroll
-    for (int e = 0; e < kTopK; e++) {
+    int popped = 0;
+    V = kTopList;
+    for (int e = 0; e < kTopList; e++) {
         const uint64_t m = wave_min_u64(L[0]);
+        if (m == ~0ull) {
+            V = e;
+            break;
+        }
         if (lane == e) mine = m;
-        if (L[0] == m && m != ~0ull) {  // keys are unique: one lane pops
+        if (L[0] == m) {  // keys are unique: one lane pops
 #pragma unroll
             for (int k = 0; k + 1 < kTopK; k++) L[k] = L[k + 1];
             L[kTopK - 1] = ~0ull;
+            popped++;
+        }
+        if (__ballot(popped == kTopK && lane_count > kTopK)) {
+            V = e + 1;
+            break;
         }
     }
     return mine;
@@ -205,10 +230,11 @@ __global__ __launch_bounds__(256) void k_match_topk(const MatchJob *__restrict__
     uint64_t L[kTopK];
     int count;
     scan_query(J, q, Q, qd, [](int, int) { return false; }, L, count);
-    count = wave_sum_i(count);
-    const uint64_t mine = merge_topk(L);
-    if (lane < kTopK) J.topk[(size_t)q * kTopK + lane] = mine;
-    if (lane == 0) J.ncand[q] = count;
+    const int total = wave_sum_i(count);
+    int V;
+    const uint64_t mine = merge_topk(L, count, V);
+    if (lane < kTopList) J.topk[(size_t)q * kTopList + lane] = mine;
+    if (lane == 0) J.ncand[q] = total | (V << 24);  // candidates | listed entries << 24
 }
 
 // ComputeThreeMaxima (ORBmatcher.cc:1471-1502)
@@ -255,269 +281,15 @@ __host__ __device__ __forceinline__ bool staged_kp_fits(int n, int mode) {
     return replay_lds_base(n, mode) + 5 * (size_t)((n + 3) & ~3) + 64 <= 65536;
 }
 
-// ---------------------------------------------------------------------------
-// k_match_resolve: the same sequential result, found in parallel.
-//
-// A query's decision depends on the state its candidates are in when the
-// reference's loop reaches it, and that state is written only by earlier
-// queries' matches: train keypoint j is skipped by query q iff the LAST query
-// p < q that matched j set it (BEST / RATIO: p's MapPoint has observations —
-// the test `mvpMapPoints[i2]->Observations() > 0`, ORBmatcher.cc:1290-1292 /
-// :76-78; BoW: always, `vpMapPointMatches[realIdxF]` set, :210-211), else its
-// initial state.  So decisions d_q = f_q(d_0 .. d_{q-1}) with f_q strictly
-// causal, and the iteration d^{k+1}_q = f_q(d^k) (every query re-decided
-// against the previous pass's decisions, all at once) has exactly one fixed
-// point, the sequential result, reached after at most (longest chain of
-// queries whose decisions feed each other) + 1 passes (4-5 on the test scenes).
-// A pass: the matched queries are linked per train keypoint in LDS (atomic
-// exchange into head[j]); each query walks its top-K entries in order and, for
-// each, the entry's list for the latest chooser before it.  A pass that changes
-// no decision ends the loop.
-//
-// A query whose skips exhaust its top-K entries of a longer candidate list needs
-// its whole candidate list under the current state (the serial path's re-scan).
-// Once the passes settle with such queries present, the train keypoints are
-// bucketed by grid cell in LDS (counting sort) and the passes continue with
-// those queries scanning their GetFeaturesInArea cells (or BoW node list) in
-// their own thread.  If the pass budget runs out the status word hands the job
-// to k_match_replay (the serial replay from scratch); otherwise the outputs are
-// written here and k_match_replay exits on entry.
-// ---------------------------------------------------------------------------
-constexpr int kResolveThreads = 1024;
-constexpr int kGridCells = kGridCols * kGridRows;  // 3072 = 3 per thread
-static_assert(kGridCells == 3 * kResolveThreads, "cell scan: 3 cells per thread");
-__host__ __device__ __forceinline__ size_t resolve_lds_bytes(int n, int nq) {
-    return 4 * (size_t)n + 8 * (size_t)nq + 4 * (size_t)kGridCells + 2 * (size_t)((n + 1) & ~1) +
-           (size_t)((nq + 3) & ~3);
+// The serial replay, run by ONE wave (k_match_replay: INIT, jobs the resolve's LDS
+// cannot hold, or YGZFE_MATCH_PASSES=0).
+__device__ __forceinline__ void wave_sync() {
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
 }
 
-__global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJob *__restrict__ jobs, int mode,
-                                                                   int th_dist, int check_ori, float nnratio,
-                                                                   int max_passes) {
-    extern __shared__ uint8_t lds[];
-    const MatchJob J = jobs[blockIdx.x];
-    const int tid = threadIdx.x, n = J.n_train, nq = J.nq;
-    int32_t *head = reinterpret_cast<int32_t *>(lds);       // [n]  latest linked chooser of j
-    int32_t *link = head + n;                               // [nq] next chooser of the same j
-    int32_t *choice = link + nq;                            // [nq] matched train index, -1 none, -2 re-scan
-    int32_t *cend = choice + nq;                            // [cells] end of each cell's keypoints in sidx
-    uint16_t *sidx = reinterpret_cast<uint16_t *>(cend + kGridCells);             // [n] keypoints by cell
-    uint8_t *qbl = reinterpret_cast<uint8_t *>(sidx + ((n + 1) & ~1));            // [nq] q's match blocks
-    __shared__ int s_rot[kHisto + 2];
-    __shared__ int s_sum[16];
-    const auto g_topk = as_global(J.topk);
-    const auto g_ncand = as_global(J.ncand);
-    const auto g_q = as_global(J.q);
-    const auto g_blocked0 = as_global(J.blocked0);
-    const auto g_kps = as_global(J.kps);
-    const int need = mode == YGZFE_MATCH_BEST ? 1 : 2;
-    for (int q = tid; q < nq; q += kResolveThreads) {
-        choice[q] = -1;
-        qbl[q] = mode == YGZFE_MATCH_BOW ? 1 : ((g_q[q].flags & YGZFE_MQ_BLOCKS) ? 1 : 0);
-    }
-    for (int j = tid; j < n; j += kResolveThreads) head[j] = -1;
-    // the state query q sees keypoint j in: set by the latest chooser before q
-    auto blocked_at = [&](int j, int q) -> bool {
-        int last = -1;
-        for (int p = head[j]; p >= 0; p = link[p])
-            if (p < q && p > last) last = p;
-        return last >= 0 ? qbl[last] != 0 : (J.blocked0 ? g_blocked0[j] != 0 : false);
-    };
-    // the serial path's re-scan, in one thread: the whole candidate list under the state
-    auto rescan = [&](int q, uint64_t &best, uint64_t &second) {
-        const ygzfe_match_query Q = J.q[q];
-        uint32_t qd[8];
-        load_qdesc(J, q, qd);
-        best = second = ~0ull;
-        auto consider = [&](int j, uint32_t order) {
-            if (blocked_at(j, q)) return;
-            const uint64_t key = make_key(hamming32(qd, J.desc + (size_t)j * 32), order, j, g_kps[j].octave);
-            if (key < best) {
-                second = best;
-                best = key;
-            } else if (key < second) {
-                second = key;
-            }
-        };
-        if (J.cand_ptr) {
-            const int b = J.cand_ptr[2 * q], e = J.cand_ptr[2 * q + 1];
-            for (int p = b; p < e; p++) consider(J.cand[p], (uint32_t)(p - b));
-        } else {
-            const Window w = make_window(J, Q);
-            for (int ix = w.cx0; ix <= w.cx1; ix++)
-                for (int iy = w.cy0; iy <= w.cy1; iy++) {
-                    const int c = ix * kGridRows + iy;
-                    for (int t = c ? cend[c - 1] : 0; t < cend[c]; t++) {
-                        const int j = sidx[t];
-                        const uint32_t o = window_order(J, w, Q, j);
-                        if (o != ~0u) consider(j, o);
-                    }
-                }
-        }
-    };
-    // query q's decision against the chooser lists of the previous pass
-    auto decide = [&](int q, bool full) -> int {
-        const int flags = g_q[q].flags, cnt = g_ncand[q];
-        if (!(flags & YGZFE_MQ_VALID) || cnt == 0) return -1;
-        const int nk = min(cnt, kTopK);
-        uint64_t best = ~0ull, second = ~0ull;
-        int found = 0;
-        for (int k = 0; k < nk && found < need; k++) {
-            const uint64_t e = g_topk[(size_t)q * kTopK + k];
-            if (blocked_at(key_train(e), q)) continue;
-            if (found == 0) best = e;
-            else second = e;
-            found++;
-        }
-        if (found < need && cnt > kTopK) {
-            if (!full) return -2;
-            rescan(q, best, second);
-        }
-        const bool has1 = best != ~0ull, has2 = second != ~0ull;
-        const int bd = has1 ? (int)(best >> 52) : 256, sdist = has2 ? (int)(second >> 52) : 256;
-        bool ok;
-        if (mode == YGZFE_MATCH_BEST) {
-            ok = has1 && bd <= th_dist;
-        } else if (mode == YGZFE_MATCH_RATIO) {
-            const int bl = has1 ? key_octave(best) : -1, sl = has2 ? key_octave(second) : -1;
-            ok = has1 && bd <= 100 && !(bl == sl && bd > nnratio * sdist);
-        } else {  // BOW
-            ok = has1 && bd <= 50 && (float)bd < nnratio * (float)sdist;
-        }
-        return ok ? key_train(best) : -1;
-    };
-    // keypoints bucketed by cell (cell-major ix * rows + iy), for the re-scans
-    auto build_cells = [&]() {
-        for (int c = tid; c < kGridCells; c += kResolveThreads) cend[c] = 0;
-        __syncthreads();
-        for (int j = tid; j < n; j += kResolveThreads) {
-            const int c = J.cell[j];
-            if (c >= 0) atomicAdd(&cend[(c >> 8) * kGridRows + (c & 0xFF)], 1);
-        }
-        __syncthreads();
-        const int c0 = 3 * tid;
-        const int a0 = cend[c0], a1 = cend[c0 + 1], a2 = cend[c0 + 2], sum = a0 + a1 + a2;
-        const int lane = tid & 63, wv = tid >> 6;
-        int incl = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += v;
-        }
-        if (lane == 63) s_sum[wv] = incl;
-        __syncthreads();
-        int base = 0;
-        for (int k = 0; k < wv; k++) base += s_sum[k];
-        const int start = base + incl - sum;  // exclusive start of cell c0
-        cend[c0] = start;                     // starts for now; the scatter advances them to ends
-        cend[c0 + 1] = start + a0;
-        cend[c0 + 2] = start + a0 + a1;
-        __syncthreads();
-        for (int j = tid; j < n; j += kResolveThreads) {
-            const int c = J.cell[j];
-            if (c >= 0) sidx[atomicAdd(&cend[(c >> 8) * kGridRows + (c & 0xFF)], 1)] = (uint16_t)j;
-        }
-        __syncthreads();
-    };
-    __syncthreads();
-    int pass = 0;
-    bool converged = false, full = false;
-    while (pass < max_passes) {
-        if (pass > 0) {  // link the previous pass's matches per keypoint
-            for (int j = tid; j < n; j += kResolveThreads) head[j] = -1;
-            __syncthreads();
-            for (int q = tid; q < nq; q += kResolveThreads) {
-                const int c = choice[q];
-                if (c >= 0) link[q] = atomicExch(&head[c], q);
-            }
-            __syncthreads();
-        }
-        int changed = 0, pending = 0;
-        for (int q = tid; q < nq; q += kResolveThreads) {
-            const int c = decide(q, full);
-            changed |= c != choice[q];
-            pending |= c == -2;
-            choice[q] = c;  // lists are not rebuilt until the next pass: no reader sees this
-        }
-        pass++;
-        if (!__syncthreads_or(changed)) {
-            if (!__syncthreads_or(pending)) {
-                converged = true;
-                break;
-            }
-            build_cells();  // settled with re-scans outstanding: the next passes do them
-            full = true;
-        }
-    }
-    if (!converged) {
-        if (tid == 0) as_global_mut(J.nmatches)[2] = -1;  // k_match_replay takes the job
-        return;
-    }
-    // outputs: train_out[j] = the last query that matched j
-    const auto g_train_out = as_global_mut(J.train_out);
-    const auto g_qid = as_global(J.qid);
-    for (int j = tid; j < n; j += kResolveThreads) {
-        int last = -1;
-        for (int p = head[j]; p >= 0; p = link[p]) last = max(last, p);
-        if (J.train_out) g_train_out[j] = last < 0 ? -1 : (mode == YGZFE_MATCH_BOW && J.qid ? g_qid[last] : last);
-    }
-    if (tid < kHisto + 2) s_rot[tid] = 0;
-    __syncthreads();
-    int matched = 0, nrescan = 0;
-    const bool ori = check_ori && mode != YGZFE_MATCH_RATIO;
-    for (int q = tid; q < nq; q += kResolveThreads) {
-        const int c = choice[q];
-        if (c < 0) continue;
-        matched++;
-        if (ori) atomicAdd(&s_rot[rot_bin(g_q[q].angle, g_kps[c].angle)], 1);
-    }
-    __syncthreads();
-    int removed = 0;
-    if (ori) {
-        int i1, i2, i3;
-        three_maxima(s_rot, i1, i2, i3);
-        for (int q = tid; q < nq; q += kResolveThreads) {
-            const int c = choice[q];
-            if (c < 0) continue;
-            const int bin = rot_bin(g_q[q].angle, g_kps[c].angle);
-            if (bin == i1 || bin == i2 || bin == i3) continue;
-            if (J.train_out) g_train_out[c] = mode == YGZFE_MATCH_BEST ? -2 : -1;
-            removed++;
-        }
-    }
-    if (full)  // diagnostics: the queries whose top-K list the final state exhausts
-        for (int q = tid; q < nq; q += kResolveThreads) {
-            const int cnt = g_ncand[q];
-            if (!(g_q[q].flags & YGZFE_MQ_VALID) || cnt <= kTopK) continue;
-            int found = 0;
-            for (int k = 0; k < kTopK && found < need; k++)
-                found += !blocked_at(key_train(g_topk[(size_t)q * kTopK + k]), q);
-            nrescan += found < need;
-        }
-    const int net = wave_sum_i(matched - removed), nr = wave_sum_i(nrescan);
-    __syncthreads();  // s_sum reused
-    if ((tid & 63) == 0) s_sum[tid >> 6] = net | (nr << 20);
-    __syncthreads();
-    if (tid == 0) {
-        int tot = 0, totr = 0;
-        for (int k = 0; k < kResolveThreads / 64; k++) {
-            tot += s_sum[k] & 0xFFFFF;
-            totr += s_sum[k] >> 20;
-        }
-        const auto g_nm = as_global_mut(J.nmatches);
-        g_nm[0] = tot;
-        g_nm[1] = totr;
-        g_nm[2] = pass;
-    }
-}
-
-__global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict__ jobs, int mode, int th_dist,
-                                                     int check_ori, float nnratio, int stage_kv, int resolved_first) {
-    extern __shared__ uint8_t lds[];
-    // the job's fields in registers: the loop's global stores could otherwise alias the
-    // job record and force a reload of every field (a scalar-load latency per query)
-    const MatchJob J = jobs[blockIdx.x];
-    if (resolved_first && as_global(J.nmatches)[2] >= 0) return;  // k_match_resolve wrote the outputs
+__device__ __forceinline__ void replay_serial(const MatchJob &J, uint8_t *lds, int mode, int th_dist, int check_ori,
+                                           float nnratio, int stage_kv) {
     const auto g_train_out = as_global_mut(J.train_out), g_query_out = as_global_mut(J.query_out);
     const auto g_pushes = as_global_mut(J.pushes), g_nmatches = as_global_mut(J.nmatches);
     const auto g_q = as_global(J.q);
@@ -526,7 +298,7 @@ __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict_
     const auto g_kps = as_global(J.kps);
     const auto g_blocked0 = as_global(J.blocked0);
     const auto g_qid = as_global(J.qid);
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int n = J.n_train;
     __shared__ int rot_count[64];
     uint8_t *blocked = lds;                                            // [n]
@@ -555,7 +327,7 @@ __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict_
     if (mode == YGZFE_MATCH_INIT)
         for (int i = lane; i < J.nq; i += 64) g_query_out[i] = -1;
     rot_count[lane] = 0;
-    __syncthreads();
+    wave_sync();
     int nmatches = 0, npush = 0, rescans = 0;
     const int need = mode == YGZFE_MATCH_BEST ? 1 : 2;
     // skip test of the reference's scan against the current state
@@ -583,9 +355,9 @@ __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict_
         if (q < J.nq) {
             r.flags = g_q[q].flags;
             r.angle = g_q[q].angle;
-            r.cnt = g_ncand[q];
+            r.cnt = g_ncand[q] & 0xFFFFFF;
             typedef unsigned v4u __attribute__((ext_vector_type(4)));
-            const auto t = (gptr_t<v4u>)(J.topk + (size_t)q * kTopK);
+            const auto t = (gptr_t<v4u>)(J.topk + (size_t)q * kTopList);
 #pragma unroll
             for (int k = 0; k < kTopK / 2; k++) {
                 const v4u v = t[k];
@@ -703,10 +475,9 @@ __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict_
         }
     }
     if (check_ori && mode != YGZFE_MATCH_RATIO && npush > 0) {
-        __threadfence_block();
-        __syncthreads();  // the pushes are visible to every lane
+        wave_sync();  // the pushes are visible to every lane
         for (int p = lane; p < npush; p += 64) atomicAdd(&rot_count[g_pushes[p] >> 24], 1);
-        __syncthreads();
+        wave_sync();
         int i1, i2, i3;
         three_maxima(rot_count, i1, i2, i3);
         int removed = 0;
@@ -733,21 +504,428 @@ __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict_
     }
 }
 
+__global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict__ jobs, int mode, int th_dist,
+                                                     int check_ori, float nnratio, int stage_kv) {
+    extern __shared__ uint8_t lds[];
+    // the job's fields in registers: the loop's global stores could otherwise alias the
+    // job record and force a reload of every field (a scalar-load latency per query)
+    const MatchJob J = jobs[blockIdx.x];
+    replay_serial(J, lds, mode, th_dist, check_ori, nnratio, stage_kv);
+}
+
+// ---------------------------------------------------------------------------
+// k_match_resolve<R>: the same sequential result, found in parallel.
+//
+// A query's decision depends on the state its candidates are in when the
+// reference's loop reaches it, and that state is written only by earlier
+// queries' matches: train keypoint j is skipped by query q iff the LAST query
+// p < q that matched j set it (BEST / RATIO: p's MapPoint has observations —
+// the test `mvpMapPoints[i2]->Observations() > 0`, ORBmatcher.cc:1290-1292 /
+// :76-78; BoW: always, `vpMapPointMatches[realIdxF]` set, :210-211), else its
+// initial state.  So decisions d_q = f_q(d_0 .. d_{q-1}) with f_q strictly
+// causal, and the iteration d^{k+1}_q = f_q(d^k) (every query re-decided
+// against the previous pass's decisions, all at once) has exactly one fixed
+// point, the sequential result, reached after at most (longest chain of
+// queries whose decisions feed each other) + 1 passes (4-13 on the test scenes).
+//
+// A pass: the matched queries are linked per train keypoint in LDS (atomic
+// exchange into head[j]); each thread re-decides its R queries from their top-K
+// entries (held in registers across passes, 4 B each), walking each entry's
+// list for the latest chooser before the query.  A query whose skips exhaust
+// the top-K entries of a longer candidate list (the serial path's re-scan) goes
+// to a list that the 16 waves then work through, one query per wave: lanes over
+// the query's GetFeaturesInArea cells (keypoints bucketed by cell in LDS on
+// first need) or BoW node list, Hamming + state per candidate, a wave min for
+// the best two.  A pass that changes no decision ends the loop.
+// ---------------------------------------------------------------------------
+constexpr int kResolveThreads = 1024, kResolveWaves = kResolveThreads / 64;
+constexpr int kGridCells = kGridCols * kGridRows;  // 3072 = 3 per thread
+static_assert(kGridCells == 3 * kResolveThreads, "cell scan: 3 cells per thread");
+constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
+constexpr uint16_t kChoiceNone = 0xFFFF, kChoicePending = 0xFFFE;
+
+// LDS of the resolve: heads i32[2][n] | link i16[nq] | choice u16[nq] | rq i16[nq] |
+// cell end u16[cells] | keypoints by cell u16[n] | q blocks u8[nq] | initial state u8[n]
+__host__ __device__ __forceinline__ size_t resolve_lds_bytes(int n, int nq) {
+    const size_t n2 = (size_t)((n + 1) & ~1), q2 = (size_t)((nq + 1) & ~1);
+    return 8 * n2 + 6 * q2 + 2 * (size_t)kGridCells + 2 * n2 + q2 + n2;
+}
+__host__ __device__ __forceinline__ size_t replay_lds_bytes(int n, int mode) {
+    return replay_lds_base(n, mode) + (staged_kp_fits(n, mode) ? 5 * (size_t)((n + 3) & ~3) : 0) + 64;
+}
+
+// entry = dist << 20 | octave << 16 | train index (from a top-K key)
+__device__ __forceinline__ uint32_t entry_of(uint64_t key) {
+    return key == ~0ull ? kNoEntry : (uint32_t)((key >> 52) << 20) | (uint32_t)(key & 0xFFFFF);
+}
+
+template <int R>
+__global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJob *__restrict__ jobs, int mode,
+                                                                   int th_dist, int check_ori, float nnratio,
+                                                                   int max_passes) {
+    extern __shared__ uint8_t lds[];
+    YGZ_BSTAMP_K(5, 0);
+    const MatchJob J = jobs[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, n = J.n_train, nq = J.nq;
+    const size_t n2 = (size_t)((n + 1) & ~1), q2 = (size_t)((nq + 1) & ~1);
+    // pass k links into heads[k & 1]; the other buffer (read by pass k - 1) is cleared meanwhile
+    int32_t *heads = reinterpret_cast<int32_t *>(lds);       // [2][n] latest linked chooser of j
+    int16_t *link = reinterpret_cast<int16_t *>(heads + 2 * n2);  // [nq] next chooser of the same j
+    uint16_t *choice = reinterpret_cast<uint16_t *>(link + q2);   // [nq] matched train index / none
+    int16_t *rq = reinterpret_cast<int16_t *>(choice + q2);  // [nq] this pass's re-scan queries
+    uint16_t *cend = reinterpret_cast<uint16_t *>(rq + q2);  // [cells] end of each cell in sidx
+    uint16_t *sidx = cend + kGridCells;                      // [n] keypoints by cell
+    uint8_t *qbl = reinterpret_cast<uint8_t *>(sidx + n2);   // [nq] a match by q blocks its keypoint
+    uint8_t *bl0 = qbl + q2;                                 // [n]  initial skip state
+    __shared__ int s_rot[kHisto + 2];
+    __shared__ int s_sum[kResolveWaves];
+    __shared__ int s_nrq[2], s_chg[2];  // per pass parity: pass k resets pass k + 1's
+    const auto g_ncand = as_global(J.ncand);
+    const auto g_q = as_global(J.q);
+    const auto g_blocked0 = as_global(J.blocked0);
+    const auto g_kps = as_global(J.kps);
+    const auto g_cell = as_global(J.cell);
+    const auto g_topk = as_global(J.topk);
+    const int need = mode == YGZFE_MATCH_BEST ? 1 : 2;
+    // the thread's queries q = tid + 1024 r: candidate count (-1: not valid), listed
+    // entries, angle, and the first kTopK entries
+    int qcnt[R], qlist[R];
+    float qang[R];
+    uint32_t E[R][kTopK];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int q = tid + kResolveThreads * r;
+        qcnt[r] = -1;
+        qlist[r] = 0;
+        qang[r] = 0.f;
+        if (q < nq) {
+            const int flags = g_q[q].flags;
+            const int nc = g_ncand[q];
+            qang[r] = g_q[q].angle;
+            qcnt[r] = (flags & YGZFE_MQ_VALID) ? (nc & 0xFFFFFF) : -1;
+            qlist[r] = nc >> 24;
+            typedef unsigned v4u __attribute__((ext_vector_type(4)));
+            const auto t = (gptr_t<v4u>)(J.topk + (size_t)q * kTopList);
+#pragma unroll
+            for (int k = 0; k < kTopK / 2; k++) {
+                const v4u v = t[k];
+                E[r][2 * k] = entry_of(((uint64_t)v.y << 32) | v.x);
+                E[r][2 * k + 1] = entry_of(((uint64_t)v.w << 32) | v.z);
+            }
+            choice[q] = kChoiceNone;
+            qbl[q] = mode == YGZFE_MATCH_BOW ? 1 : ((flags & YGZFE_MQ_BLOCKS) ? 1 : 0);
+        }
+    }
+    for (int j = tid; j < n; j += kResolveThreads) {
+        heads[j] = -1;
+        heads[n2 + j] = -1;
+        bl0[j] = J.blocked0 ? g_blocked0[j] : 0;
+    }
+    if (tid == 0) s_nrq[0] = s_nrq[1] = s_chg[0] = s_chg[1] = 0;
+    // the state query q sees keypoint j in: set by the latest chooser before q
+    const int32_t *head = heads;
+    auto blocked_at = [&](int j, int q) -> bool {
+        int last = -1;
+        for (int p = head[j]; p >= 0; p = link[p])
+            if (p < q && p > last) last = p;
+        return (last >= 0 ? qbl[last] : bl0[j]) != 0;
+    };
+    auto rule = [&](uint32_t best, uint32_t second) -> int {  // the mode's acceptance test
+        const bool has1 = best != kNoEntry, has2 = second != kNoEntry;
+        const int bd = has1 ? (int)(best >> 20) : 256, sdist = has2 ? (int)(second >> 20) : 256;
+        bool ok;
+        if (mode == YGZFE_MATCH_BEST) {
+            ok = has1 && bd <= th_dist;
+        } else if (mode == YGZFE_MATCH_RATIO) {
+            const int bl = has1 ? (int)((best >> 16) & 15) : -1, sl = has2 ? (int)((second >> 16) & 15) : -1;
+            ok = has1 && bd <= 100 && !(bl == sl && bd > nnratio * sdist);
+        } else {  // BOW
+            ok = has1 && bd <= 50 && (float)bd < nnratio * (float)sdist;
+        }
+        return ok ? (int)(best & 0xFFFF) : kChoiceNone;
+    };
+    bool cells_built = false;
+    auto build_cells = [&]() {  // counting sort of the keypoints by cell (cell-major ix * rows + iy)
+        for (int c = tid; c < kGridCells; c += kResolveThreads) cend[c] = 0;
+        __syncthreads();
+        for (int j = tid; j < n; j += kResolveThreads) {
+            const int c = g_cell[j];
+            if (c >= 0) atomicAdd(reinterpret_cast<uint32_t *>(cend) + (((c >> 8) * kGridRows + (c & 0xFF)) >> 1),
+                                  ((((c >> 8) * kGridRows + (c & 0xFF)) & 1) ? 0x10000u : 1u));
+        }
+        __syncthreads();
+        const int c0 = 3 * tid;
+        const int a0 = cend[c0], a1 = cend[c0 + 1], a2 = cend[c0 + 2], sum = a0 + a1 + a2;
+        int incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) s_sum[wv] = incl;
+        __syncthreads();
+        int base = 0;
+        for (int k = 0; k < wv; k++) base += s_sum[k];
+        const int start = base + incl - sum;  // exclusive start of cell c0
+        cend[c0] = (uint16_t)(start + a0);     // ends
+        cend[c0 + 1] = (uint16_t)(start + a0 + a1);
+        cend[c0 + 2] = (uint16_t)(start + sum);
+        __syncthreads();
+        for (int j = tid; j < n; j += kResolveThreads) {  // scatter from each cell's end down
+            const int c = g_cell[j];
+            if (c < 0) continue;
+            const int cc = (c >> 8) * kGridRows + (c & 0xFF);
+            const uint32_t sh = (cc & 1) ? 16 : 0;
+            const uint32_t old = atomicSub(reinterpret_cast<uint32_t *>(cend) + (cc >> 1), 1u << sh);
+            sidx[((old >> sh) & 0xFFFF) - 1] = (uint16_t)j;
+        }
+        __syncthreads();
+        // the scatter took every end down to its start: restore the ends
+        cend[c0] = (uint16_t)(start + a0);
+        cend[c0 + 1] = (uint16_t)(start + a0 + a1);
+        cend[c0 + 2] = (uint16_t)(start + sum);
+        __syncthreads();
+    };
+    // the serial path's re-scan by one wave: every candidate under the current state
+    auto wave_rescan = [&](int q) -> int {
+        const ygzfe_match_query Q = J.q[q];
+        uint32_t qd[8];
+        load_qdesc(J, q, qd);
+        uint64_t b1 = ~0ull, b2 = ~0ull;
+        auto consider = [&](int j, uint32_t order) {
+            if (blocked_at(j, q)) return;
+            const uint64_t key = make_key(hamming32(qd, J.desc + (size_t)j * 32), order, j, g_kps[j].octave);
+            if (key < b1) {
+                b2 = b1;
+                b1 = key;
+            } else if (key < b2) {
+                b2 = key;
+            }
+        };
+        if (J.cand_ptr) {
+            const int b = J.cand_ptr[2 * q], e = J.cand_ptr[2 * q + 1];
+            for (int p = b + lane; p < e; p += 64) consider(J.cand[p], (uint32_t)(p - b));
+        } else {
+            const Window w = make_window(J, Q);
+            const int ncx = w.cx1 - w.cx0 + 1, ncy = w.cy1 - w.cy0 + 1;
+            const int ncell = w.cx0 <= w.cx1 ? ncx * ncy : 0;
+            for (int cb = 0; cb < ncell; cb += 64) {  // 64 window cells at a time
+                int lo = 0, cnt = 0;
+                if (cb + lane < ncell) {
+                    const int k = cb + lane;
+                    const int c = (w.cx0 + k / ncy) * kGridRows + (w.cy0 + k % ncy);
+                    lo = c ? cend[c - 1] : 0;
+                    cnt = cend[c] - lo;
+                }
+                int incl = cnt;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int v = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += v;
+                }
+                const int total = __shfl(incl, 63, 64);
+                for (int e0 = 0; e0 < total; e0 += 64) {
+                    const int e = e0 + lane;
+                    // the lane holding e's cell: the first whose inclusive count exceeds e
+                    int src = 0;
+#pragma unroll
+                    for (int step = 32; step >= 1; step >>= 1) {
+                        const int probe = src + step - 1;
+                        if (__shfl(incl, probe, 64) <= e) src += step;
+                    }
+                    const int s_lo = __shfl(lo, src, 64), s_incl = __shfl(incl, src, 64), s_cnt = __shfl(cnt, src, 64);
+                    if (e < total) {
+                        const int j = sidx[s_lo + e - (s_incl - s_cnt)];
+                        const uint32_t o = window_order(J, w, Q, j);
+                        if (o != ~0u) consider(j, o);
+                    }
+                }
+            }
+        }
+        const uint64_t best = wave_min_u64(b1);
+        if (b1 == best) b1 = b2;  // keys are unique: one lane pops
+        const uint64_t second = wave_min_u64(b1);
+        return rule(entry_of(best), entry_of(second));
+    };
+    __syncthreads();
+    YGZ_BSTAMP_K(5, 1);
+    int pass = 0;
+    bool converged = false;
+    // the fixed point is reached within nq + 1 passes (query k is final after pass k + 1);
+    // max_passes only bounds a broken invariant, reported as status -1
+    while (pass < max_passes) {
+        const int b = pass & 1;
+        int32_t *hb = heads + (b ? n2 : 0), *ho = heads + (b ? 0 : n2);
+        head = hb;
+        if (pass > 0) {  // link the previous pass's matches per keypoint (hb was cleared last pass)
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int q = tid + kResolveThreads * r;
+                if (q < nq) {
+                    const int c = choice[q];
+                    if (c != kChoiceNone) link[q] = (int16_t)atomicExch(&hb[c], q);
+                }
+            }
+            __syncthreads();
+            if (pass == 1) YGZ_BSTAMP_K(5, 6);
+        }
+        for (int j = tid; j < n; j += kResolveThreads) ho[j] = -1;  // next pass's lists
+        int changed = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int q = tid + kResolveThreads * r;
+            if (qcnt[r] <= 0) continue;  // invalid, past nq, or no candidate: never matches
+            uint32_t best = kNoEntry, second = kNoEntry;
+            int found = 0;
+            const int nk = min(qlist[r], kTopK);
+#pragma unroll
+            for (int k = 0; k < kTopK; k++) {
+                if (k >= nk || found >= need) break;
+                const uint32_t e = E[r][k];
+                if (blocked_at((int)(e & 0xFFFF), q)) continue;
+                if (found == 0) best = e;
+                else second = e;
+                found++;
+            }
+            for (int k = kTopK; k < qlist[r] && found < need; k++) {  // the listed entries past the registers
+                const uint32_t e = entry_of(g_topk[(size_t)q * kTopList + k]);
+                if (blocked_at((int)(e & 0xFFFF), q)) continue;
+                if (found == 0) best = e;
+                else second = e;
+                found++;
+            }
+            if (found < need && qcnt[r] > qlist[r]) {
+                rq[atomicAdd(&s_nrq[b], 1)] = (int16_t)q;  // decided below by a wave
+                continue;
+            }
+            const int c = rule(best, second);
+            changed |= c != choice[q];
+            choice[q] = (uint16_t)c;  // lists are not rebuilt until the next pass: no reader sees this
+        }
+        if (changed) s_chg[b] = 1;
+        __syncthreads();
+        if (pass == 1) YGZ_BSTAMP_K(5, 7);
+        const int nrq = s_nrq[b];
+        if (nrq > 0) {
+            if (!cells_built && !J.cand_ptr) build_cells();
+            cells_built = true;
+            changed = 0;
+            for (int i = wv; i < nrq; i += kResolveWaves) {
+                const int q = rq[i];
+                const int c = wave_rescan(q);
+                if (lane == 0) {
+                    changed |= c != choice[q];
+                    choice[q] = (uint16_t)c;
+                }
+            }
+            if (changed) s_chg[b] = 1;
+            __syncthreads();
+        }
+        pass++;
+        if (pass == 1) YGZ_BSTAMP_K(5, 3);
+        const bool any = s_chg[b] != 0;
+        // the parity-(b ^ 1) flags were last read in the previous pass, before this pass's
+        // first barrier; the next pass writes them only after its link barrier
+        if (tid == 0) s_chg[b ^ 1] = s_nrq[b ^ 1] = 0;
+        if (!any) {
+            converged = true;
+            break;
+        }
+    }
+    YGZ_BSTAMP_K(5, 4);
+    if (!converged) {
+        if (tid == 0) as_global_mut(J.nmatches)[2] = -1;  // the host reports the error
+        return;
+    }
+    // outputs: train_out[j] = the last query that matched j (the final lists)
+    const auto g_train_out = as_global_mut(J.train_out);
+    const auto g_qid = as_global(J.qid);
+    for (int j = tid; j < n; j += kResolveThreads) {
+        int last = -1;
+        for (int p = head[j]; p >= 0; p = link[p]) last = max(last, p);
+        if (J.train_out) g_train_out[j] = last < 0 ? -1 : (mode == YGZFE_MATCH_BOW && J.qid ? g_qid[last] : last);
+    }
+    if (tid < kHisto + 2) s_rot[tid] = 0;
+    __syncthreads();
+    const bool ori = check_ori && mode != YGZFE_MATCH_RATIO;
+    int matched = 0, bins[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int q = tid + kResolveThreads * r;
+        bins[r] = -1;
+        if (q >= nq) continue;
+        const int c = choice[q];
+        if (c == kChoiceNone) continue;
+        matched++;
+        if (ori) {
+            bins[r] = rot_bin(qang[r], g_kps[c].angle);
+            atomicAdd(&s_rot[bins[r]], 1);
+        }
+    }
+    __syncthreads();
+    int removed = 0;
+    if (ori) {
+        int i1, i2, i3;
+        three_maxima(s_rot, i1, i2, i3);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int bin = bins[r];
+            if (bin < 0 || bin == i1 || bin == i2 || bin == i3) continue;
+            const int c = choice[tid + kResolveThreads * r];
+            if (J.train_out) g_train_out[c] = mode == YGZFE_MATCH_BEST ? -2 : -1;
+            removed++;
+        }
+    }
+    // diagnostics: queries whose top-K list the final state exhausts (the serial path's re-scans)
+    int nrescan = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int q = tid + kResolveThreads * r;
+        if (qcnt[r] <= kTopK) continue;
+        int found = 0;
+#pragma unroll
+        for (int k = 0; k < kTopK; k++) found += !blocked_at((int)(E[r][k] & 0xFFFF), q);
+        nrescan += found < need;
+    }
+    const int net = wave_sum_i(matched - removed), nr = wave_sum_i(nrescan);
+    if (lane == 0) s_sum[wv] = net | (nr << 20);
+    __syncthreads();
+    if (tid == 0) {
+        int tot = 0, totr = 0;
+        for (int k = 0; k < kResolveWaves; k++) {
+            tot += s_sum[k] & 0xFFFFF;
+            totr += s_sum[k] >> 20;
+        }
+        const auto g_nm = as_global_mut(J.nmatches);
+        g_nm[0] = tot;
+        g_nm[1] = totr;
+        g_nm[2] = pass;
+    }
+    YGZ_BSTAMP_K(5, 5);
+}
+
+bool resolve_fits(int n_train, int nq) {
+    return nq <= 4 * kResolveThreads && n_train <= 65533 && resolve_lds_bytes(n_train, nq) <= 65536;
+}
+
 hipError_t launch_match(const MatchJob *d_jobs, int njobs, int max_q, int max_train, int mode, int th_dist,
                         int check_ori, float nnratio, int max_passes, hipStream_t st) {
     if (njobs <= 0) return hipSuccess;
     if (max_q > 0)
         hipLaunchKernelGGL(k_match_topk, dim3((max_q + 3) / 4, njobs), dim3(256), 0, st, d_jobs, max_q);
-    // INIT's skip state is a distance, and a re-match unmatches the previous query: serial only
+    const int stage_kv = (int)staged_kp_fits(max_train, mode);
+    const size_t ser = replay_lds_bytes(max_train, mode);
+    // INIT's skip state is a distance and a re-match unmatches the previous query: serial only
+    const int R = max_q <= kResolveThreads ? 1 : max_q <= 2 * kResolveThreads ? 2 : max_q <= 4 * kResolveThreads ? 4 : 0;
     const size_t rl = resolve_lds_bytes(max_train, max_q);
-    const bool resolve = max_passes > 0 && mode != YGZFE_MATCH_INIT && rl <= 65536;
-    if (resolve)
-        hipLaunchKernelGGL(k_match_resolve, dim3(njobs), dim3(kResolveThreads), rl, st, d_jobs, mode, th_dist,
-                           check_ori, nnratio, max_passes);
-    const size_t lds = replay_lds_base(max_train, mode) +
-                       (staged_kp_fits(max_train, mode) ? 5 * (size_t)((max_train + 3) & ~3) : 0) + 64;
-    hipLaunchKernelGGL(k_match_replay, dim3(njobs), dim3(64), lds, st, d_jobs, mode, th_dist, check_ori, nnratio,
-                       (int)staged_kp_fits(max_train, mode), (int)resolve);
+    if (max_passes > 0 && mode != YGZFE_MATCH_INIT && R > 0 && resolve_fits(max_train, max_q)) {
+        auto k = R == 1 ? k_match_resolve<1> : R == 2 ? k_match_resolve<2> : k_match_resolve<4>;
+        hipLaunchKernelGGL(k, dim3(njobs), dim3(kResolveThreads), rl, st, d_jobs, mode, th_dist, check_ori, nnratio,
+                           max_q + 2);
+    } else {
+        hipLaunchKernelGGL(k_match_replay, dim3(njobs), dim3(64), ser, st, d_jobs, mode, th_dist, check_ori, nnratio,
+                           stage_kv);
+    }
     return hipGetLastError();
 }
 

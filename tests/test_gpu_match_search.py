@@ -12,8 +12,8 @@ check on and off, plus dense windows where the sequential skips exhaust the GPU'
 top-K list (the re-scan path).
 
 Every test runs twice: with the parallel resolve (k_match_resolve, the default) and with
-the serial replay alone (YGZFE_MATCH_PASSES=0); test_resolve_pass_budget covers the
-hand-over when the pass budget runs out."""
+the serial replay alone (YGZFE_MATCH_PASSES=0); test_resolve_long_chains drives the resolve
+through long dependency chains."""
 import os
 
 import numpy as np
@@ -185,22 +185,18 @@ def test_empty_inputs(gpu):
     assert gn == 0 and len(got) == 0
 
 
-def test_resolve_pass_budget(gpu, decide):
-    """Budgets of 1..3 passes: when the chains of dependent decisions are longer, the
-    resolve hands the job to the serial replay (passes -1); the result never changes."""
-    if decide == "serial":
-        pytest.skip("budget sweep runs once")
+def test_resolve_long_chains(gpu, decide):
+    """Every query blocking and windows of 40 px: each query's best candidates are taken by
+    the ones before it, so decisions feed each other in long chains (many resolve passes,
+    re-scans in most passes); the result equals the oracle's and the serial replay's."""
     p = pair("C2", 0)
-    Q, qd, ur, bl = S.projection_queries(p, 4, th=15.0, level_mode="none", blocks_frac=1.0)
-    cur = gpu_frame(gpu, p["k1"], p["d1"], ur, p)
-    want, wn = O.search_projection_best(O.mframe(p["k1"], p["d1"], ur, bounds(p)), Q, qd, bl, 100, True)
-    seen = set()
-    try:
-        for budget in ("1", "2", "3", "64"):
-            os.environ["YGZFE_MATCH_PASSES"] = budget
-            got, gn = gpu.search_projection_best(cur, Q, qd, bl, 100, True)
-            assert gn == wn and np.array_equal(got, want), budget
-            seen.add(cur.resolve_passes() >= 1)
-    finally:
-        os.environ.pop("YGZFE_MATCH_PASSES", None)
-    assert seen == {True, False}  # both the hand-over and the resolved path ran
+    Q, qd, ur, bl = S.projection_queries(p, 9, th=40.0, level_mode="none", blocks_frac=1.0, stereo_frac=0.0,
+                                         valid_frac=1.0, flip_bits=40)
+    cur = gpu_frame(gpu, p["k1"], p["d1"], None, p)
+    got, gn = gpu.search_projection_best(cur, Q, qd, None, 100, True)
+    want, wn = O.search_projection_best(O.mframe(p["k1"], p["d1"], None, bounds(p)), Q, qd, None, 100, True)
+    assert gn == wn and np.array_equal(got, want)
+    if decide == "resolve":
+        assert cur.resolve_passes() > 8, cur.resolve_passes()
+    else:
+        assert cur.resolve_passes() == -1
