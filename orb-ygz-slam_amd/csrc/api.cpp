@@ -1735,7 +1735,6 @@ extern "C" int ygzfe_stereo_matches(const ygzfe_frame *left, const ygzfe_frame *
     J.u_right = (float *)(d + o_u);
     J.depth = (float *)(d + o_d);
     J.sad = (int *)(d + o_s);
-    memcpy(h + o_job, &J, sizeof(J));
     const int cnt[2] = {nl, nr};
     memcpy(h + o_cnt, cnt, 8);
     memcpy(h + o_kl, kl, sizeof(ygzfe_kp) * (size_t)nl);
@@ -2293,6 +2292,7 @@ struct ygzfe_match_frame {
 namespace {
 
 constexpr int kMatchTopK = 32;  // match.hip kTopList (J.topk stride)
+constexpr int kMatchCells = 64 * 48;  // FRAME_GRID_COLS x ROWS
 
 struct Arena {
     size_t off = 0;
@@ -2308,9 +2308,11 @@ int match_frame_finish(ygzfe_match_frame *f, const ygzfe_bounds *bounds) {
     // Frame.cc:296-297
     f->inv_w = (float)64 / (float)(bounds->max_x - bounds->min_x);
     f->inv_h = (float)48 / (float)(bounds->max_y - bounds->min_y);
-    YGZ_TRY(f->cell.ensure(sizeof(int32_t) * (size_t)std::max(f->n, 1)));
+    // cell[n] | cell ends [64 * 48] | keypoints by cell u16[n]
+    YGZ_TRY(f->cell.ensure(sizeof(int32_t) * ((size_t)f->n + kMatchCells) + sizeof(uint16_t) * (size_t)f->n + 16));
     YGZ_HIP(launch_match_cells(f->kps.as<ygzfe_kp>(), f->n, bounds->min_x, bounds->min_y, f->inv_w, f->inv_h,
-                               f->cell.as<int32_t>(), f->stream));
+                               f->cell.as<int32_t>(), f->cell.as<int32_t>() + f->n,
+                               reinterpret_cast<uint16_t *>(f->cell.as<int32_t>() + f->n + kMatchCells), f->stream));
     // no synchronisation: every search runs on f->stream after the grid
     return YGZFE_OK;
 }
@@ -2346,7 +2348,6 @@ int run_match(MatchCall &c) {
     hipStream_t st = f->stream;
     // device input layout
     Arena ai;
-    const size_t o_job = ai.take(sizeof(MatchJob));
     const size_t o_q = ai.take(sizeof(ygzfe_match_query) * (size_t)std::max(nq, 1));
     const size_t o_qd = c.qdesc_host ? ai.take((size_t)32 * std::max(c.n_qdesc, 1)) : 0;
     const size_t o_qid = c.qid.empty() ? 0 : ai.take(sizeof(int32_t) * c.qid.size());
@@ -2362,18 +2363,24 @@ int run_match(MatchCall &c) {
     const size_t o_topk = ao.take(sizeof(uint64_t) * kMatchTopK * (size_t)std::max(nq, 1));
     const size_t o_ncand = ao.take(sizeof(int32_t) * (size_t)std::max(nq, 1));
     const size_t o_push = ao.take(sizeof(int32_t) * (size_t)std::max(nq, 1));
-    YGZ_TRY(f->in.ensure(ai.off));
+    const size_t o_qang = ao.take(sizeof(float) * (size_t)std::max(nq, 1));
     YGZ_TRY(f->out.ensure(ao.off));
-    uint8_t *din = f->in.as<uint8_t>(), *dout = f->out.as<uint8_t>();
-    if (f->ev_in) YGZ_HIP(hipEventSynchronize(f->ev_in));  // the previous H2D out of hin
+    uint8_t *dout = f->out.as<uint8_t>();
+    // The inputs stay in page-locked host memory that the kernels read directly (one
+    // pass in k_match_topk, which copies what the decisions need into HBM): no H2D
+    // copy and no copy-to-kernel dependency on the stream.  The previous call
+    // synchronised its stream, so the staging is free.
     YGZ_TRY(f->hin.ensure(ai.off));
-    uint8_t *h = f->hin.as<uint8_t>();
+    uint8_t *h = f->hin.as<uint8_t>(), *din = nullptr;
+    YGZ_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&din), h, 0));
     MatchJob J;
     memset(&J, 0, sizeof(J));
     J.kps = f->kps.as<ygzfe_kp>();
     J.desc = f->desc.as<uint8_t>();
     J.u_right = f->has_uright ? f->uright.as<float>() : nullptr;
     J.cell = f->cell.as<int32_t>();
+    J.cend = J.cell + n;
+    J.cidx = reinterpret_cast<const uint16_t *>(J.cend + kMatchCells);
     J.n_train = n;
     J.min_x = f->bounds.min_x;
     J.min_y = f->bounds.min_y;
@@ -2388,27 +2395,30 @@ int run_match(MatchCall &c) {
     J.blocked0 = c.blocked_host ? din + o_bl : nullptr;
     J.topk = reinterpret_cast<uint64_t *>(dout + o_topk);
     J.ncand = reinterpret_cast<int32_t *>(dout + o_ncand);
+    J.qangle = reinterpret_cast<float *>(dout + o_qang);
     J.train_out = reinterpret_cast<int32_t *>(dout + o_tout);
     J.query_out = reinterpret_cast<int32_t *>(dout + o_qout);
     J.pushes = reinterpret_cast<int32_t *>(dout + o_push);
     J.nmatches = reinterpret_cast<int32_t *>(dout + o_nm);
-    memcpy(h + o_job, &J, sizeof(J));
     if (nq) memcpy(h + o_q, c.q.data(), sizeof(ygzfe_match_query) * nq);
     if (c.qdesc_host && c.n_qdesc) memcpy(h + o_qd, c.qdesc_host, (size_t)32 * c.n_qdesc);
     if (!c.qid.empty()) memcpy(h + o_qid, c.qid.data(), sizeof(int32_t) * c.qid.size());
     if (!c.cand_ptr.empty()) memcpy(h + o_cp, c.cand_ptr.data(), sizeof(int32_t) * c.cand_ptr.size());
     if (c.cand_host && c.n_cand) memcpy(h + o_c, c.cand_host, sizeof(int32_t) * c.n_cand);
     if (c.blocked_host && n) memcpy(h + o_bl, c.blocked_host, (size_t)n);
-    YGZ_HIP(hipMemcpyAsync(din, h, ai.off, hipMemcpyHostToDevice, st));
-    if (!f->ev_in) YGZ_HIP(hipEventCreateWithFlags(&f->ev_in, hipEventDisableTiming));
-    YGZ_HIP(hipEventRecord(f->ev_in, st));
     // YGZFE_MATCH_PASSES=0 selects the serial replay (tests run both paths)
     const char *ev = getenv("YGZFE_MATCH_PASSES");
     const int max_passes = ev ? atoi(ev) : 1;
-    YGZ_HIP(launch_match(reinterpret_cast<const MatchJob *>(din + o_job), 1, nq, n, c.mode, c.th_dist, c.check_ori,
-                         c.nnratio, max_passes, st));
     YGZ_TRY(f->hout.ensure(out_bytes));
-    YGZ_HIP(hipMemcpyAsync(f->hout.p, dout, out_bytes, hipMemcpyDeviceToHost, st));
+    const bool direct = match_resolves(n, nq, c.mode, max_passes);
+    if (direct) {  // k_match_resolve writes each output once, straight into page-locked host memory
+        uint8_t *hod = nullptr;
+        YGZ_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&hod), f->hout.p, 0));
+        J.train_out = reinterpret_cast<int32_t *>(hod + o_tout);
+        J.nmatches = reinterpret_cast<int32_t *>(hod + o_nm);
+    }
+    YGZ_HIP(launch_match(J, c.mode, c.th_dist, c.check_ori, c.nnratio, max_passes, st));
+    if (!direct) YGZ_HIP(hipMemcpyAsync(f->hout.p, dout, out_bytes, hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipStreamSynchronize(st));
     const uint8_t *ho = f->hout.as<uint8_t>();
     if (c.train_out && n) memcpy(c.train_out, ho + o_tout, sizeof(int32_t) * n);

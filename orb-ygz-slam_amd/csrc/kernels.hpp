@@ -58,6 +58,8 @@ struct MatchJob {
     const uint8_t *desc;
     const float *u_right;       // mvuRight or null
     const int32_t *cell;        // PosInGrid: ix << 8 | iy, -1 outside (k_match_cells)
+    const int32_t *cend;        // [64 * 48] end of cell ix * 48 + iy in cidx (Frame::mGrid as an index)
+    const uint16_t *cidx;       // [n] keypoints by cell
     int n_train;
     float min_x, min_y, inv_w, inv_h;
     // queries in the reference's order
@@ -70,19 +72,21 @@ struct MatchJob {
     const uint8_t *blocked0;    // initial skip state per train keypoint, or null
     // scratch / outputs
     uint64_t *topk;             // [nq][kTopK]
-    int32_t *ncand;             // [nq]
+    int32_t *ncand;             // [nq] candidates | valid / blocks bits | listed entries << 24 (k_match_topk)
+    float *qangle;              // [nq] query angles (k_match_topk copies them from the query records)
     int32_t *train_out;         // [n_train]
     int32_t *query_out;         // INIT: vnMatches12 [nq]
     int32_t *pushes;            // [nq] rotation-histogram pushes
     int32_t *nmatches;          // [4]: matches, rescans, resolve passes (-1: serial replay), spare
 };
 hipError_t launch_match_cells(const ygzfe_kp *kps, int n, float min_x, float min_y, float inv_w, float inv_h,
-                              int32_t *cell, hipStream_t st);
+                              int32_t *cell, int32_t *cend, uint16_t *cidx, hipStream_t st);
 // max_passes: 0 = serial replay only (k_match_replay); otherwise the parallel resolve
 // (k_match_resolve) wherever resolve_fits, INIT always serial
 bool resolve_fits(int n_train, int nq);
-hipError_t launch_match(const MatchJob *d_jobs, int njobs, int max_q, int max_train, int mode, int th_dist,
-                        int check_ori, float nnratio, int max_passes, hipStream_t st);
+bool match_resolves(int n_train, int nq, int mode, int max_passes);  // launch_match takes k_match_resolve
+hipError_t launch_match(const MatchJob &J, int mode, int th_dist, int check_ori, float nnratio, int max_passes,
+                        hipStream_t st);
 
 // align.hip
 struct AlignLevels {

@@ -46,24 +46,66 @@ extern "C" int ygzfe_diag_match_stamps(unsigned long long *out, int n) {
 constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS / ROWS (Frame.h:27-28)
 constexpr int kTopK = 8;      // per-lane list, and the entries the decisions keep in registers
 constexpr int kTopList = 32;  // entries k_match_topk lists per query (J.topk stride)
+// J.ncand[q] as k_match_topk writes it: candidates (bits 0-15) | valid | blocks | listed entries << 24
+constexpr int kInfoValid = 1 << 22, kInfoBlocks = 1 << 23;
 constexpr int kHisto = 30;                       // ORBmatcher::HISTO_LENGTH (ORBmatcher.cc:38)
 
-// Frame::PosInGrid (Frame.cc:483-493): std::round(float), cell -1 when outside
-__global__ __launch_bounds__(256) void k_match_cells(const ygzfe_kp *__restrict__ kps, int n, float min_x,
-                                                     float min_y, float inv_w, float inv_h,
-                                                     int32_t *__restrict__ cell) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const int px = (int)__builtin_roundf((kps[i].x - min_x) * inv_w);
-    const int py = (int)__builtin_roundf((kps[i].y - min_y) * inv_h);
-    cell[i] = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : (px << 8) | py;
+// Frame::PosInGrid (Frame.cc:483-493): std::round(float), cell -1 when outside; and
+// the grid as an index (Frame::mGrid, Frame.cc:412-422): the keypoints bucketed by
+// cell (cell-major ix * rows + iy), cend[c] = end of cell c in cidx.  One workgroup,
+// counting sort in LDS; the order inside a cell is immaterial (candidates are ranked
+// by their (distance, cell, index) keys).
+constexpr int kGridCells = kGridCols * kGridRows;  // 3072
+__global__ __launch_bounds__(1024) void k_match_cells(const ygzfe_kp *__restrict__ kps, int n, float min_x,
+                                                      float min_y, float inv_w, float inv_h,
+                                                      int32_t *__restrict__ cell, int32_t *__restrict__ cend,
+                                                      uint16_t *__restrict__ cidx) {
+    __shared__ int cnt[kGridCells];
+    __shared__ int s_sum[16];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    auto cell_of = [&](int i) -> int {
+        const int px = (int)__builtin_roundf((kps[i].x - min_x) * inv_w);
+        const int py = (int)__builtin_roundf((kps[i].y - min_y) * inv_h);
+        return (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : (px << 8) | py;
+    };
+    for (int c = tid; c < kGridCells; c += 1024) cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const int c = cell_of(i);
+        cell[i] = c;
+        if (c >= 0) atomicAdd(&cnt[(c >> 8) * kGridRows + (c & 0xFF)], 1);
+    }
+    __syncthreads();
+    const int c0 = 3 * tid;
+    const int a0 = cnt[c0], a1 = cnt[c0 + 1], a2 = cnt[c0 + 2], sum = a0 + a1 + a2;
+    int incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) s_sum[wv] = incl;
+    __syncthreads();
+    int base = 0;
+    for (int k = 0; k < wv; k++) base += s_sum[k];
+    const int e0 = base + incl - sum + a0, e1 = e0 + a1, e2 = e1 + a2;  // ends of cells c0 .. c0 + 2
+    cend[c0] = e0;
+    cend[c0 + 1] = e1;
+    cend[c0 + 2] = e2;
+    cnt[c0] = e0;
+    cnt[c0 + 1] = e1;
+    cnt[c0 + 2] = e2;
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {  // each cell filled from its end down
+        const int c = cell_of(i);
+        if (c >= 0) cidx[atomicSub(&cnt[(c >> 8) * kGridRows + (c & 0xFF)], 1) - 1] = (uint16_t)i;
+    }
 }
 
 hipError_t launch_match_cells(const ygzfe_kp *kps, int n, float min_x, float min_y, float inv_w, float inv_h,
-                              int32_t *cell, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_match_cells, dim3((n + 255) / 256), dim3(256), 0, st, kps, n, min_x, min_y, inv_w, inv_h,
-                       cell);
+                              int32_t *cell, int32_t *cend, uint16_t *cidx, hipStream_t st) {
+    hipLaunchKernelGGL(k_match_cells, dim3(1), dim3(1024), 0, st, kps, n, min_x, min_y, inv_w, inv_h, cell, cend,
+                       cidx);
     return hipGetLastError();
 }
 
@@ -113,14 +155,10 @@ __device__ __forceinline__ Window make_window(const MatchJob &J, const ygzfe_mat
     return w;
 }
 
-// Is train keypoint j in the query's candidate list (window + level + stereo)?
-// Returns its candidate-order key (cell-major, then index) or ~0.
-__device__ __forceinline__ uint32_t window_order(const MatchJob &J, const Window &w, const ygzfe_match_query &q,
-                                                 int j) {
-    const int c = J.cell[j];
-    if (c < 0) return ~0u;
-    const int ix = c >> 8, iy = c & 0xFF;
-    if (ix < w.cx0 || ix > w.cx1 || iy < w.cy0 || iy > w.cy1) return ~0u;
+// Is train keypoint j of cell (ix, iy) in the query's candidate list (window +
+// level + stereo)?  Returns its candidate-order key (cell-major, then index) or ~0.
+__device__ __forceinline__ uint32_t window_accept(const MatchJob &J, const Window &w, const ygzfe_match_query &q,
+                                                  int j, int c) {
     const ygzfe_kp &kp = J.kps[j];
     if (w.check_levels) {
         if (kp.octave < w.min_level) return ~0u;
@@ -132,7 +170,41 @@ __device__ __forceinline__ uint32_t window_order(const MatchJob &J, const Window
         const float er = fabsf(q.u_right - J.u_right[j]);
         if (er > q.radius) return ~0u;
     }
-    return ((uint32_t)(ix * kGridRows + iy) << 16) | (uint32_t)j;  // GetFeaturesInArea order
+    return ((uint32_t)c << 16) | (uint32_t)j;  // GetFeaturesInArea order
+}
+
+// The window's cells' keypoints spread over the wave's lanes (64 cells at a time,
+// their index ranges concatenated): fn(j, c) on each lane holding one.
+template <class F>
+__device__ __forceinline__ void for_window(const MatchJob &J, const Window &w, F fn) {
+    const int lane = threadIdx.x & 63;
+    if (w.cx0 > w.cx1) return;
+    const int ncy = w.cy1 - w.cy0 + 1, ncell = (w.cx1 - w.cx0 + 1) * ncy;
+    for (int cb = 0; cb < ncell; cb += 64) {
+        int lo = 0, cnt = 0, c = 0;
+        if (cb + lane < ncell) {
+            const int k = cb + lane;
+            c = (w.cx0 + k / ncy) * kGridRows + (w.cy0 + k % ncy);
+            lo = c ? J.cend[c - 1] : 0;
+            cnt = J.cend[c] - lo;
+        }
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        const int total = __shfl(incl, 63, 64);
+        for (int e0 = 0; e0 < total; e0 += 64) {
+            const int e = e0 + lane;
+            int src = 0;  // the lane holding e's cell: the first whose inclusive count exceeds e
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1)
+                if (__shfl(incl, src + step - 1, 64) <= e) src += step;
+            const int s_lo = __shfl(lo, src, 64), s_ex = __shfl(incl - cnt, src, 64), s_c = __shfl(c, src, 64);
+            if (e < total) fn((int)J.cidx[s_lo + e - s_ex], s_c);
+        }
+    }
 }
 
 // key = dist << 52 | order << 20 | octave << 16 | train index (n <= 65535).  The
@@ -168,11 +240,10 @@ __device__ __forceinline__ void scan_query(const MatchJob &J, int q, const ygzfe
         for (int p = b + lane; p < e; p += 64) consider(J.cand[p], (uint32_t)(p - b));
     } else {
         const Window w = make_window(J, Q);
-        if (w.cx0 <= w.cx1)
-            for (int j = lane; j < J.n_train; j += 64) {
-                const uint32_t o = window_order(J, w, Q, j);
-                if (o != ~0u) consider(j, o);
-            }
+        for_window(J, w, [&](int j, int c) {
+            const uint32_t o = window_accept(J, w, Q, j, c);
+            if (o != ~0u) consider(j, o);
+        });
     }
 }
 
@@ -184,57 +255,56 @@ __device__ __forceinline__ void load_qdesc(const MatchJob &J, int q, uint32_t qd
     qd[4] = b.x; qd[5] = b.y; qd[6] = b.z; qd[7] = b.w;
 }
 
-// wave-merge of the lanes' sorted lists: the smallest keys, ascending, in lanes
-// 0..V-1.  Each lane holds its kTopK best; the merge pops up to kTopList keys and
-// stops after popping the last held key of a lane that had more candidates (the
-// next key could be that lane's unseen one), so the first V keys are exactly the
-// V best.  V >= min(count, kTopK) always.
-__device__ __forceinline__ uint64_t merge_topk(uint64_t L[kTopK], int lane_count, int &V) {
-    const int lane = threadIdx.x & 63;
-    uint64_t mine = ~0ull;
-    int popped = 0;
-    V = kTopList;
-    for (int e = 0; e < kTopList; e++) {
-        const uint64_t m = wave_min_u64(L[0]);
-        if (m == ~0ull) {
-            V = e;
-            break;
-        }
-        if (lane == e) mine = m;
-        if (L[0] == m) {  // keys are unique: one lane pops
-#pragma unroll
-            for (int k = 0; k + 1 < kTopK; k++) L[k] = L[k + 1];
-            L[kTopK - 1] = ~0ull;
-            popped++;
-        }
-        if (__ballot(popped == kTopK && lane_count > kTopK)) {
-            V = e + 1;
-            break;
-        }
-    }
-    return mine;
-}
-
-__global__ __launch_bounds__(256) void k_match_topk(const MatchJob *__restrict__ jobs, int max_q) {
-    const MatchJob &J = jobs[blockIdx.y];
-    const int q = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+// k_match_topk: one wave per query, all queries at once.  Lanes collect the
+// window's candidates (the frame's cell index, for_window) keeping their kTopK
+// smallest keys; the kept keys go to LDS and each is ranked by counting the
+// smaller ones (broadcast reads, no cross-lane reductions).  The first V ranks are
+// exact: V counts the kept keys up to the smallest kTopK-th key of a lane that
+// dropped candidates (its dropped ones are larger), capped at kTopList.
+constexpr int kTopkWaves = 4;
+__global__ __launch_bounds__(64 * kTopkWaves) void k_match_topk(const MatchJob J) {
+    __shared__ uint64_t s_keys[kTopkWaves][64 * kTopK];
+    const int q = __builtin_amdgcn_readfirstlane(blockIdx.x * kTopkWaves + (threadIdx.x >> 6));
     if (q >= J.nq) return;
     const int lane = threadIdx.x & 63;
-    const ygzfe_match_query Q = J.q[q];
+    uint64_t *K = s_keys[threadIdx.x >> 6];
+    const ygzfe_match_query Q = J.q[q];  // the query records may live in host memory (read once here)
     if (!(Q.flags & YGZFE_MQ_VALID)) {
         if (lane == 0) J.ncand[q] = 0;
         return;
     }
+    if (lane == 0) J.qangle[q] = Q.angle;
     uint32_t qd[8];
     load_qdesc(J, q, qd);
     uint64_t L[kTopK];
     int count;
     scan_query(J, q, Q, qd, [](int, int) { return false; }, L, count);
-    const int total = wave_sum_i(count);
-    int V;
-    const uint64_t mine = merge_topk(L, count, V);
-    if (lane < kTopList) J.topk[(size_t)q * kTopList + lane] = mine;
-    if (lane == 0) J.ncand[q] = total | (V << 24);  // candidates | listed entries << 24
+    const int kept = min(count, kTopK);
+    int off = kept;  // exclusive prefix of the kept counts
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(off, o, 64);
+        if (lane >= o) off += v;
+    }
+    const int T = __shfl(off, 63, 64), total = wave_sum_i(count);
+    off -= kept;
+#pragma unroll
+    for (int k = 0; k < kTopK; k++)
+        if (k < kept) K[off + k] = L[k];
+    uint64_t thr = ~0ull;  // keys above the smallest dropped-lane bound are not exact
+    if (__ballot(count > kTopK)) thr = wave_min_u64(count > kTopK ? L[kTopK - 1] : ~0ull);
+    wave_lds_order();
+    int V = 0;
+    for (int t0 = 0; t0 < T; t0 += 64) {
+        const int t = t0 + lane;
+        const uint64_t mine = t < T ? K[t] : ~0ull;
+        int rank = 0;
+        for (int u = 0; u < T; u++) rank += K[u] < mine;
+        if (t < T && mine <= thr && rank < kTopList) J.topk[(size_t)q * kTopList + rank] = mine;
+        V += __popcll(__ballot(t < T && mine <= thr));
+    }
+    V = min(V, kTopList);
+    if (lane == 0) J.ncand[q] = total | kInfoValid | ((Q.flags & YGZFE_MQ_BLOCKS) ? kInfoBlocks : 0) | (V << 24);
 }
 
 // ComputeThreeMaxima (ORBmatcher.cc:1471-1502)
@@ -292,7 +362,6 @@ __device__ __forceinline__ void replay_serial(const MatchJob &J, uint8_t *lds, i
                                            float nnratio, int stage_kv) {
     const auto g_train_out = as_global_mut(J.train_out), g_query_out = as_global_mut(J.query_out);
     const auto g_pushes = as_global_mut(J.pushes), g_nmatches = as_global_mut(J.nmatches);
-    const auto g_q = as_global(J.q);
     const auto g_ncand = as_global(J.ncand);
     const auto g_topk = as_global(J.topk);
     const auto g_kps = as_global(J.kps);
@@ -353,9 +422,10 @@ __device__ __forceinline__ void replay_serial(const MatchJob &J, uint8_t *lds, i
 #pragma unroll
         for (int k = 0; k < kTopK; k++) r.e[k] = ~0ull;
         if (q < J.nq) {
-            r.flags = g_q[q].flags;
-            r.angle = g_q[q].angle;
-            r.cnt = g_ncand[q] & 0xFFFFFF;
+            const int info = g_ncand[q];
+            r.flags = (info & kInfoValid ? YGZFE_MQ_VALID : 0) | (info & kInfoBlocks ? YGZFE_MQ_BLOCKS : 0);
+            r.angle = J.qangle[q];
+            r.cnt = info & 0xFFFF;
             typedef unsigned v4u __attribute__((ext_vector_type(4)));
             const auto t = (gptr_t<v4u>)(J.topk + (size_t)q * kTopList);
 #pragma unroll
@@ -504,12 +574,9 @@ __device__ __forceinline__ void replay_serial(const MatchJob &J, uint8_t *lds, i
     }
 }
 
-__global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict__ jobs, int mode, int th_dist,
-                                                     int check_ori, float nnratio, int stage_kv) {
+__global__ __launch_bounds__(64) void k_match_replay(const MatchJob J, int mode, int th_dist, int check_ori,
+                                                     float nnratio, int stage_kv) {
     extern __shared__ uint8_t lds[];
-    // the job's fields in registers: the loop's global stores could otherwise alias the
-    // job record and force a reload of every field (a scalar-load latency per query)
-    const MatchJob J = jobs[blockIdx.x];
     replay_serial(J, lds, mode, th_dist, check_ori, nnratio, stage_kv);
 }
 
@@ -539,16 +606,15 @@ __global__ __launch_bounds__(64) void k_match_replay(const MatchJob *__restrict_
 // the best two.  A pass that changes no decision ends the loop.
 // ---------------------------------------------------------------------------
 constexpr int kResolveThreads = 1024, kResolveWaves = kResolveThreads / 64;
-constexpr int kGridCells = kGridCols * kGridRows;  // 3072 = 3 per thread
 static_assert(kGridCells == 3 * kResolveThreads, "cell scan: 3 cells per thread");
 constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
 constexpr uint16_t kChoiceNone = 0xFFFF, kChoicePending = 0xFFFE;
 
-// LDS of the resolve: heads i32[2][n] | link i16[nq] | choice u16[nq] | rq i16[nq] |
-// cell end u16[cells] | keypoints by cell u16[n] | q blocks u8[nq] | initial state u8[n]
+// LDS of the resolve: heads i32[2][n] | train angles f32[n] | link i16[nq] | choice u16[nq] |
+// rq i16[nq] | q blocks u8[nq] | initial state u8[n]
 __host__ __device__ __forceinline__ size_t resolve_lds_bytes(int n, int nq) {
     const size_t n2 = (size_t)((n + 1) & ~1), q2 = (size_t)((nq + 1) & ~1);
-    return 8 * n2 + 6 * q2 + 2 * (size_t)kGridCells + 2 * n2 + q2 + n2;
+    return 12 * n2 + 6 * q2 + q2 + n2;
 }
 __host__ __device__ __forceinline__ size_t replay_lds_bytes(int n, int mode) {
     return replay_lds_base(n, mode) + (staged_kp_fits(n, mode) ? 5 * (size_t)((n + 3) & ~3) : 0) + 64;
@@ -560,31 +626,26 @@ __device__ __forceinline__ uint32_t entry_of(uint64_t key) {
 }
 
 template <int R>
-__global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJob *__restrict__ jobs, int mode,
-                                                                   int th_dist, int check_ori, float nnratio,
-                                                                   int max_passes) {
+__global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJob J, int mode, int th_dist,
+                                                                   int check_ori, float nnratio, int max_passes) {
     extern __shared__ uint8_t lds[];
     YGZ_BSTAMP_K(5, 0);
-    const MatchJob J = jobs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, n = J.n_train, nq = J.nq;
     const size_t n2 = (size_t)((n + 1) & ~1), q2 = (size_t)((nq + 1) & ~1);
     // pass k links into heads[k & 1]; the other buffer (read by pass k - 1) is cleared meanwhile
     int32_t *heads = reinterpret_cast<int32_t *>(lds);       // [2][n] latest linked chooser of j
-    int16_t *link = reinterpret_cast<int16_t *>(heads + 2 * n2);  // [nq] next chooser of the same j
+    float *tang = reinterpret_cast<float *>(heads + 2 * n2);  // [n]  train keypoint angles (rotation check)
+    int16_t *link = reinterpret_cast<int16_t *>(tang + n2);  // [nq] next chooser of the same j
     uint16_t *choice = reinterpret_cast<uint16_t *>(link + q2);   // [nq] matched train index / none
     int16_t *rq = reinterpret_cast<int16_t *>(choice + q2);  // [nq] this pass's re-scan queries
-    uint16_t *cend = reinterpret_cast<uint16_t *>(rq + q2);  // [cells] end of each cell in sidx
-    uint16_t *sidx = cend + kGridCells;                      // [n] keypoints by cell
-    uint8_t *qbl = reinterpret_cast<uint8_t *>(sidx + n2);   // [nq] a match by q blocks its keypoint
+    uint8_t *qbl = reinterpret_cast<uint8_t *>(rq + q2);     // [nq] a match by q blocks its keypoint
     uint8_t *bl0 = qbl + q2;                                 // [n]  initial skip state
     __shared__ int s_rot[kHisto + 2];
     __shared__ int s_sum[kResolveWaves];
     __shared__ int s_nrq[2], s_chg[2];  // per pass parity: pass k resets pass k + 1's
     const auto g_ncand = as_global(J.ncand);
-    const auto g_q = as_global(J.q);
     const auto g_blocked0 = as_global(J.blocked0);
     const auto g_kps = as_global(J.kps);
-    const auto g_cell = as_global(J.cell);
     const auto g_topk = as_global(J.topk);
     const int need = mode == YGZFE_MATCH_BEST ? 1 : 2;
     // the thread's queries q = tid + 1024 r: candidate count (-1: not valid), listed
@@ -599,11 +660,10 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
         qlist[r] = 0;
         qang[r] = 0.f;
         if (q < nq) {
-            const int flags = g_q[q].flags;
             const int nc = g_ncand[q];
-            qang[r] = g_q[q].angle;
-            qcnt[r] = (flags & YGZFE_MQ_VALID) ? (nc & 0xFFFFFF) : -1;
-            qlist[r] = nc >> 24;
+            qang[r] = J.qangle[q];
+            qcnt[r] = (nc & kInfoValid) ? (nc & 0xFFFF) : -1;
+            qlist[r] = (uint32_t)nc >> 24;
             typedef unsigned v4u __attribute__((ext_vector_type(4)));
             const auto t = (gptr_t<v4u>)(J.topk + (size_t)q * kTopList);
 #pragma unroll
@@ -613,15 +673,18 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
                 E[r][2 * k + 1] = entry_of(((uint64_t)v.w << 32) | v.z);
             }
             choice[q] = kChoiceNone;
-            qbl[q] = mode == YGZFE_MATCH_BOW ? 1 : ((flags & YGZFE_MQ_BLOCKS) ? 1 : 0);
+            qbl[q] = mode == YGZFE_MATCH_BOW ? 1 : ((nc & kInfoBlocks) ? 1 : 0);
         }
     }
+    const bool ori = check_ori && mode != YGZFE_MATCH_RATIO;
     for (int j = tid; j < n; j += kResolveThreads) {
         heads[j] = -1;
         heads[n2 + j] = -1;
         bl0[j] = J.blocked0 ? g_blocked0[j] : 0;
+        if (ori) tang[j] = g_kps[j].angle;
     }
     if (tid == 0) s_nrq[0] = s_nrq[1] = s_chg[0] = s_chg[1] = 0;
+    if (tid < kHisto + 2) s_rot[tid] = 0;
     // the state query q sees keypoint j in: set by the latest chooser before q
     const int32_t *head = heads;
     auto blocked_at = [&](int j, int q) -> bool {
@@ -629,6 +692,27 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
         for (int p = head[j]; p >= 0; p = link[p])
             if (p < q && p > last) last = p;
         return (last >= 0 ? qbl[last] : bl0[j]) != 0;
+    };
+    // blocked entries among the first nk register entries of query (r, q), as a bit mask:
+    // every entry's head and initial state read at once, list walks only where linked
+    auto blocked_mask = [&](const uint32_t (&e)[kTopK], int nk, int q) -> uint32_t {
+        int hk[kTopK];
+        uint8_t b0[kTopK];
+#pragma unroll
+        for (int k = 0; k < kTopK; k++) {
+            const int j = (int)(e[k] & 0xFFFF);
+            hk[k] = k < nk ? head[j] : -1;
+            b0[k] = k < nk ? bl0[j] : 0;
+        }
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < kTopK; k++) {
+            int last = -1;
+            for (int p = hk[k]; p >= 0; p = link[p])
+                if (p < q && p > last) last = p;
+            m |= (uint32_t)((last >= 0 ? qbl[last] : b0[k]) != 0) << k;
+        }
+        return m;
     };
     auto rule = [&](uint32_t best, uint32_t second) -> int {  // the mode's acceptance test
         const bool has1 = best != kNoEntry, has2 = second != kNoEntry;
@@ -643,48 +727,6 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
             ok = has1 && bd <= 50 && (float)bd < nnratio * (float)sdist;
         }
         return ok ? (int)(best & 0xFFFF) : kChoiceNone;
-    };
-    bool cells_built = false;
-    auto build_cells = [&]() {  // counting sort of the keypoints by cell (cell-major ix * rows + iy)
-        for (int c = tid; c < kGridCells; c += kResolveThreads) cend[c] = 0;
-        __syncthreads();
-        for (int j = tid; j < n; j += kResolveThreads) {
-            const int c = g_cell[j];
-            if (c >= 0) atomicAdd(reinterpret_cast<uint32_t *>(cend) + (((c >> 8) * kGridRows + (c & 0xFF)) >> 1),
-                                  ((((c >> 8) * kGridRows + (c & 0xFF)) & 1) ? 0x10000u : 1u));
-        }
-        __syncthreads();
-        const int c0 = 3 * tid;
-        const int a0 = cend[c0], a1 = cend[c0 + 1], a2 = cend[c0 + 2], sum = a0 + a1 + a2;
-        int incl = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += v;
-        }
-        if (lane == 63) s_sum[wv] = incl;
-        __syncthreads();
-        int base = 0;
-        for (int k = 0; k < wv; k++) base += s_sum[k];
-        const int start = base + incl - sum;  // exclusive start of cell c0
-        cend[c0] = (uint16_t)(start + a0);     // ends
-        cend[c0 + 1] = (uint16_t)(start + a0 + a1);
-        cend[c0 + 2] = (uint16_t)(start + sum);
-        __syncthreads();
-        for (int j = tid; j < n; j += kResolveThreads) {  // scatter from each cell's end down
-            const int c = g_cell[j];
-            if (c < 0) continue;
-            const int cc = (c >> 8) * kGridRows + (c & 0xFF);
-            const uint32_t sh = (cc & 1) ? 16 : 0;
-            const uint32_t old = atomicSub(reinterpret_cast<uint32_t *>(cend) + (cc >> 1), 1u << sh);
-            sidx[((old >> sh) & 0xFFFF) - 1] = (uint16_t)j;
-        }
-        __syncthreads();
-        // the scatter took every end down to its start: restore the ends
-        cend[c0] = (uint16_t)(start + a0);
-        cend[c0 + 1] = (uint16_t)(start + a0 + a1);
-        cend[c0 + 2] = (uint16_t)(start + sum);
-        __syncthreads();
     };
     // the serial path's re-scan by one wave: every candidate under the current state
     auto wave_rescan = [&](int q) -> int {
@@ -707,40 +749,10 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
             for (int p = b + lane; p < e; p += 64) consider(J.cand[p], (uint32_t)(p - b));
         } else {
             const Window w = make_window(J, Q);
-            const int ncx = w.cx1 - w.cx0 + 1, ncy = w.cy1 - w.cy0 + 1;
-            const int ncell = w.cx0 <= w.cx1 ? ncx * ncy : 0;
-            for (int cb = 0; cb < ncell; cb += 64) {  // 64 window cells at a time
-                int lo = 0, cnt = 0;
-                if (cb + lane < ncell) {
-                    const int k = cb + lane;
-                    const int c = (w.cx0 + k / ncy) * kGridRows + (w.cy0 + k % ncy);
-                    lo = c ? cend[c - 1] : 0;
-                    cnt = cend[c] - lo;
-                }
-                int incl = cnt;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int v = __shfl_up(incl, o, 64);
-                    if (lane >= o) incl += v;
-                }
-                const int total = __shfl(incl, 63, 64);
-                for (int e0 = 0; e0 < total; e0 += 64) {
-                    const int e = e0 + lane;
-                    // the lane holding e's cell: the first whose inclusive count exceeds e
-                    int src = 0;
-#pragma unroll
-                    for (int step = 32; step >= 1; step >>= 1) {
-                        const int probe = src + step - 1;
-                        if (__shfl(incl, probe, 64) <= e) src += step;
-                    }
-                    const int s_lo = __shfl(lo, src, 64), s_incl = __shfl(incl, src, 64), s_cnt = __shfl(cnt, src, 64);
-                    if (e < total) {
-                        const int j = sidx[s_lo + e - (s_incl - s_cnt)];
-                        const uint32_t o = window_order(J, w, Q, j);
-                        if (o != ~0u) consider(j, o);
-                    }
-                }
-            }
+            for_window(J, w, [&](int j, int c) {
+                const uint32_t o = window_accept(J, w, Q, j, c);
+                if (o != ~0u) consider(j, o);
+            });
         }
         const uint64_t best = wave_min_u64(b1);
         if (b1 == best) b1 = b2;  // keys are unique: one lane pops
@@ -779,7 +791,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
             int found = 0;
             const int nk = min(qlist[r], kTopK);
 #pragma unroll
-            for (int k = 0; k < kTopK; k++) {
+            for (int k = 0; k < kTopK; k++) {  // in order, stopping at the decision (fewest instructions)
                 if (k >= nk || found >= need) break;
                 const uint32_t e = E[r][k];
                 if (blocked_at((int)(e & 0xFFFF), q)) continue;
@@ -807,8 +819,6 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
         if (pass == 1) YGZ_BSTAMP_K(5, 7);
         const int nrq = s_nrq[b];
         if (nrq > 0) {
-            if (!cells_built && !J.cand_ptr) build_cells();
-            cells_built = true;
             changed = 0;
             for (int i = wv; i < nrq; i += kResolveWaves) {
                 const int q = rq[i];
@@ -837,17 +847,9 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
         if (tid == 0) as_global_mut(J.nmatches)[2] = -1;  // the host reports the error
         return;
     }
-    // outputs: train_out[j] = the last query that matched j (the final lists)
-    const auto g_train_out = as_global_mut(J.train_out);
-    const auto g_qid = as_global(J.qid);
-    for (int j = tid; j < n; j += kResolveThreads) {
-        int last = -1;
-        for (int p = head[j]; p >= 0; p = link[p]) last = max(last, p);
-        if (J.train_out) g_train_out[j] = last < 0 ? -1 : (mode == YGZFE_MATCH_BOW && J.qid ? g_qid[last] : last);
-    }
-    if (tid < kHisto + 2) s_rot[tid] = 0;
-    __syncthreads();
-    const bool ori = check_ori && mode != YGZFE_MATCH_RATIO;
+    // outputs, each written once (J.train_out / J.nmatches may be page-locked host memory):
+    // the rotation check's removals are marked in the spare head buffer first
+    int32_t *removed_at = head == heads ? heads + n2 : heads;  // all -1 (cleared in the last pass)
     int matched = 0, bins[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -858,7 +860,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
         if (c == kChoiceNone) continue;
         matched++;
         if (ori) {
-            bins[r] = rot_bin(qang[r], g_kps[c].angle);
+            bins[r] = rot_bin(qang[r], tang[c]);
             atomicAdd(&s_rot[bins[r]], 1);
         }
     }
@@ -871,8 +873,7 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
         for (int r = 0; r < R; r++) {
             const int bin = bins[r];
             if (bin < 0 || bin == i1 || bin == i2 || bin == i3) continue;
-            const int c = choice[tid + kResolveThreads * r];
-            if (J.train_out) g_train_out[c] = mode == YGZFE_MATCH_BEST ? -2 : -1;
+            removed_at[choice[tid + kResolveThreads * r]] = 1;
             removed++;
         }
     }
@@ -882,14 +883,22 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
     for (int r = 0; r < R; r++) {
         const int q = tid + kResolveThreads * r;
         if (qcnt[r] <= kTopK) continue;
-        int found = 0;
-#pragma unroll
-        for (int k = 0; k < kTopK; k++) found += !blocked_at((int)(E[r][k] & 0xFFFF), q);
-        nrescan += found < need;
+        nrescan += __popc(~blocked_mask(E[r], kTopK, q) & 0xFFu) < need;
     }
     const int net = wave_sum_i(matched - removed), nr = wave_sum_i(nrescan);
     if (lane == 0) s_sum[wv] = net | (nr << 20);
     __syncthreads();
+    // train_out[j]: the last query that matched j (the final lists), -2 / -1 where removed
+    const auto g_train_out = as_global_mut(J.train_out);
+    const auto g_qid = as_global(J.qid);
+    if (J.train_out)
+        for (int j = tid; j < n; j += kResolveThreads) {
+            int last = -1;
+            for (int p = head[j]; p >= 0; p = link[p]) last = max(last, p);
+            int v = last < 0 ? -1 : (mode == YGZFE_MATCH_BOW && J.qid ? g_qid[last] : last);
+            if (removed_at[j] >= 0) v = mode == YGZFE_MATCH_BEST ? -2 : -1;
+            g_train_out[j] = v;
+        }
     if (tid == 0) {
         int tot = 0, totr = 0;
         for (int k = 0; k < kResolveWaves; k++) {
@@ -904,27 +913,29 @@ __global__ __launch_bounds__(kResolveThreads) void k_match_resolve(const MatchJo
     YGZ_BSTAMP_K(5, 5);
 }
 
+bool match_resolves(int n_train, int nq, int mode, int max_passes) {
+    return max_passes > 0 && mode != YGZFE_MATCH_INIT && resolve_fits(n_train, nq);
+}
+
 bool resolve_fits(int n_train, int nq) {
     return nq <= 4 * kResolveThreads && n_train <= 65533 && resolve_lds_bytes(n_train, nq) <= 65536;
 }
 
-hipError_t launch_match(const MatchJob *d_jobs, int njobs, int max_q, int max_train, int mode, int th_dist,
-                        int check_ori, float nnratio, int max_passes, hipStream_t st) {
-    if (njobs <= 0) return hipSuccess;
-    if (max_q > 0)
-        hipLaunchKernelGGL(k_match_topk, dim3((max_q + 3) / 4, njobs), dim3(256), 0, st, d_jobs, max_q);
-    const int stage_kv = (int)staged_kp_fits(max_train, mode);
-    const size_t ser = replay_lds_bytes(max_train, mode);
+hipError_t launch_match(const MatchJob &J, int mode, int th_dist, int check_ori, float nnratio, int max_passes,
+                        hipStream_t st) {
+    if (J.nq > 0)
+        hipLaunchKernelGGL(k_match_topk, dim3((J.nq + kTopkWaves - 1) / kTopkWaves), dim3(64 * kTopkWaves), 0, st, J);
+    const int n = J.n_train, nq = J.nq;
+    const int stage_kv = (int)staged_kp_fits(n, mode);
     // INIT's skip state is a distance and a re-match unmatches the previous query: serial only
-    const int R = max_q <= kResolveThreads ? 1 : max_q <= 2 * kResolveThreads ? 2 : max_q <= 4 * kResolveThreads ? 4 : 0;
-    const size_t rl = resolve_lds_bytes(max_train, max_q);
-    if (max_passes > 0 && mode != YGZFE_MATCH_INIT && R > 0 && resolve_fits(max_train, max_q)) {
+    const int R = nq <= kResolveThreads ? 1 : nq <= 2 * kResolveThreads ? 2 : 4;
+    if (match_resolves(n, nq, mode, max_passes)) {
         auto k = R == 1 ? k_match_resolve<1> : R == 2 ? k_match_resolve<2> : k_match_resolve<4>;
-        hipLaunchKernelGGL(k, dim3(njobs), dim3(kResolveThreads), rl, st, d_jobs, mode, th_dist, check_ori, nnratio,
-                           max_q + 2);
+        hipLaunchKernelGGL(k, dim3(1), dim3(kResolveThreads), resolve_lds_bytes(n, nq), st, J, mode, th_dist,
+                           check_ori, nnratio, nq + 2);
     } else {
-        hipLaunchKernelGGL(k_match_replay, dim3(njobs), dim3(64), ser, st, d_jobs, mode, th_dist, check_ori, nnratio,
-                           stage_kv);
+        hipLaunchKernelGGL(k_match_replay, dim3(1), dim3(64), replay_lds_bytes(n, mode), st, J, mode, th_dist,
+                           check_ori, nnratio, stage_kv);
     }
     return hipGetLastError();
 }
