@@ -1735,6 +1735,7 @@ extern "C" int ygzfe_stereo_matches(const ygzfe_frame *left, const ygzfe_frame *
     J.u_right = (float *)(d + o_u);
     J.depth = (float *)(d + o_d);
     J.sad = (int *)(d + o_s);
+    memcpy(h + o_job, &J, sizeof(J));
     const int cnt[2] = {nl, nr};
     memcpy(h + o_cnt, cnt, 8);
     memcpy(h + o_kl, kl, sizeof(ygzfe_kp) * (size_t)nl);
