@@ -279,6 +279,9 @@ struct ygzfe_extractor {
     }
     int ensure_align_stream() {
         if (astream) return YGZFE_OK;
+        // Normal priority, created on first use.  Measured alternatives (tools/run_lat_ab.sh):
+        // the greatest / least priority, a dedicated queue (full CU mask) and creating the
+        // extractor's streams eagerly all ran the single-frame path 15-30 % slower.
         YGZ_HIP(hipStreamCreateWithFlags(&astream, hipStreamNonBlocking));
         YGZ_HIP(hipEventCreateWithFlags(&ev_align_fork, hipEventDisableTiming));
         YGZ_HIP(hipEventCreateWithFlags(&ev_align_done, hipEventDisableTiming));
