@@ -2692,6 +2692,12 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
         int S = fast_stride(L.fast_rw), R = fast_stride(L.fast_rh);
         if (!(S == 40 && R <= 56) && S != R) S = R = std::max(S, R);  // other shapes: square slices
         if (R < S) R = S;
+        // ROIs up to 36 x 40 (C2 level 0): a 36-byte row stride brings the slice to 4.9 KB,
+        // 8 workgroups (8 waves / SIMD) per CU instead of 7
+#ifndef YGZ_FAST36
+#define YGZ_FAST36 1
+#endif
+        if (YGZ_FAST36 && L.fast_rw <= 36 && L.fast_rh <= 40) S = 36, R = 40;
         const size_t lds = fast_cells_lds_bytes(S, R);
         const int cb = L.cell_begin, ce = L.cell_begin + L.ncells;
         const dim3 grid((L.ncells + kFastWaves - 1) / kFastWaves, nframes);
@@ -2699,7 +2705,8 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
         const hipStream_t st = (l == 0 || !lvl_streams || n_lvl_streams <= 0) ? st0
                                                                                 : lvl_streams[(l - 1) % n_lvl_streams];
 #define YGZ_FAST(SS, RR) hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce, l, nullptr)
-        if (S == 40 && R == 40) YGZ_FAST(40, 40);
+        if (S == 36 && R == 40) YGZ_FAST(36, 40);
+        else if (S == 40 && R == 40) YGZ_FAST(40, 40);
         else if (S == 40 && R == 48) YGZ_FAST(40, 48);
         else if (S == 40 && R == 56) YGZ_FAST(40, 56);
         else if (S == 48) YGZ_FAST(48, 48);
