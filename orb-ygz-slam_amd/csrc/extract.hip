@@ -2411,25 +2411,38 @@ struct IcWindow {
 // address) & 15 of LDS row r); every tap is an LDS byte read.  Octree
 // keypoints sit >= 19 px inside the level, so the 31x31 IC window and the
 // 37x37 rotated-pattern window never leave it.
-__global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__ pyr,
+#ifndef YGZ_ORIENT_V2
+#define YGZ_ORIENT_V2 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_orient_desc(const uint8_t *__restrict__ pyr,
                                                      const uint8_t *__restrict__ blur, uint32_t pitch,
                                                      const Plan *__restrict__ plan, const uint2 *__restrict__ ojobs,
                                                      const int *__restrict__ n_existing,
                                                      ygzfe_kp *__restrict__ kps, uint8_t *__restrict__ desc,
                                                      int row_cap) {
     __shared__ uint8_t s_patch[16][kPatchBytes];  // one 37x37 window per keypoint row
+#if YGZ_ORIENT_V2
+    // the pattern (c_pattern, 1 KB) staged once per workgroup; the IC row weights are
+    // formed in registers from umax, so the workgroup's LDS is 32 KB (5 per CU)
+    __shared__ uint4 s_const[64];
+#else
     // the IC row weights (c_icw, 1 KB) and the pattern (c_pattern, 1 KB), staged
     // once per workgroup instead of 8 vector loads per lane: the stage is bound by
     // the vector-memory address path, and 16 rows share them
     __shared__ uint4 s_const[128];
+#endif
     int bx, f;
     swizzled_block_2d(bx, f);  // one frame's keypoints on one XCD: window lines shared in its L2
     const int lane = threadIdx.x & 63, s = lane & 15;
     const int idx = bx * 16 + (threadIdx.x >> 4);
     uint4 cst = make_uint4(0u, 0u, 0u, 0u);
+#if YGZ_ORIENT_V2
+    if (threadIdx.x < 64) cst = reinterpret_cast<const uint4 *>(c_pattern)[threadIdx.x];
+#else
     if (threadIdx.x < 128)
         cst = threadIdx.x < 64 ? reinterpret_cast<const uint4 *>(c_icw)[threadIdx.x]
                                : reinterpret_cast<const uint4 *>(c_pattern)[threadIdx.x - 64];
+#endif
     const int sel_total = plan->sel_total;
     uint2 job = make_uint2(kOrientNone, 0u);
     if (idx < sel_total) job = ojobs[(size_t)f * sel_total + idx];
@@ -2443,6 +2456,31 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     uint8_t *P = s_patch[threadIdx.x >> 4];
     IcWindow wic;
     Window<18, 37> wdesc;
+#if YGZ_ORIENT_V2
+    wic.load(fimg, w, c, s);  // the rBRIEF window follows once the IC window is in LDS
+    if (threadIdx.x < 64) s_const[threadIdx.x] = cst;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    wave_lds_order();
+    if (!active) return;  // whole rows leave together
+    // IC row weights of lane s's rows (|v| = s + 1; lane 15 the centre row): byte b of
+    // the 32 is 1 / b where |b - 15| <= umax[|v|] (the disc), else 0 -- c_icw's values
+    uint32_t W0[8], W1[8];
+    {
+        const int um = plan->umax[s == 15 ? 0 : s + 1];
+        const uint32_t M = (uint32_t)((2ull << (15 + um)) - (1ull << (15 - um)));  // bytes 15-um .. 15+um
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            W0[k] = (((M >> (4 * k)) & 15u) * 0x00204081u) & 0x01010101u;
+            W1[k] = (W0[k] * 0xFFu) & (0x03020100u + 0x04040404u * (uint32_t)k);
+        }
+    }
+    const int ne = n_existing ? n_existing[f] : 0;
+    float angle;
+    {
+        wic.store(P, s);
+        wdesc.load(fblur, w, c, s);  // in flight during the IC sums
+#else
     wic.load(fimg, w, c, s);  // both windows in flight before the first wait
     wdesc.load(fblur, w, c, s);
     // publish the constants: LDS writes retired, then a bare s_barrier (a
@@ -2465,6 +2503,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
     float angle;
     {
         wic.store(P, s);
+        const uint32_t W0[8] = {wq[0].x, wq[0].y, wq[0].z, wq[0].w, wq[1].x, wq[1].y, wq[1].z, wq[1].w};
+        const uint32_t W1[8] = {wq[2].x, wq[2].y, wq[2].z, wq[2].w, wq[3].x, wq[3].y, wq[3].z, wq[3].w};
+#endif
         // IC_Angle (ORBextractor.cc:77-101): lane s takes the window rows 15 +- (s+1)
         // (lane 15 the centre row).  Per row, with I the 31 row bytes (32nd
         // weighted 0): S0 = sum of I over the disc (dot4 with the 0/1 weights),
@@ -2472,8 +2513,6 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
         // m01 += v (S0(+v) - S0(-v)), m10 += S1 - 15 S0.  Integer sums: the
         // moments equal the reference's exactly.
         const uint32_t o0 = (uint32_t)(uintptr_t)fimg + c - 15u * w - 15u;
-        const uint32_t W0[8] = {wq[0].x, wq[0].y, wq[0].z, wq[0].w, wq[1].x, wq[1].y, wq[1].z, wq[1].w};
-        const uint32_t W1[8] = {wq[2].x, wq[2].y, wq[2].z, wq[2].w, wq[3].x, wq[3].y, wq[3].z, wq[3].w};
         auto row_sums = [&](int r, uint32_t &s0, uint32_t &s1) {
             const uint32_t o = mad24((uint32_t)r, w, o0) & 15u;  // window start inside LDS row r
             const uint32_t *d = reinterpret_cast<const uint32_t *>(P + patch_row_swz((uint32_t)r) + (o & ~3u));
@@ -2500,6 +2539,14 @@ __global__ __launch_bounds__(256) void k_orient_desc(const uint8_t *__restrict__
         angle = fast_atan2_deg((float)m01, (float)m10);
     }
     // computeOrbDescriptor (ORBextractor.cc:105-149) on the blurred level
+#if YGZ_ORIENT_V2
+    int4 pat[4];  // 16 pairs x (x0, y0, x1, y1) int8 (read after the IC pass: fewer live registers there)
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint4 u = s_const[s * 4 + q];
+        pat[q] = make_int4((int)u.x, (int)u.y, (int)u.z, (int)u.w);
+    }
+#endif
     wave_lds_order();  // IC taps read before the window is replaced
     wdesc.store(P, s);
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
