@@ -86,6 +86,7 @@ def parse():
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2-transform side measurement")
     ap.add_argument("--no-stereo", action="store_true", help="skip the stereo-matching side measurement")
     ap.add_argument("--no-a11", action="store_true", help="skip the tracking-path searches line (row a11)")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in call-site timing line")
     ap.add_argument("--no-direct", action="store_true", help="skip the SearchLocalPointsDirect side measurement")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (TUM 640x480, 2000 features) throughput line")
     ap.add_argument("--latency-frames", type=int, default=200,
@@ -543,6 +544,12 @@ def main():
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu = cpu_baseline(frames, r3[:n_host], cz[:n_host], S, args, sc)
 
+    # the drop-in headers (compat/dropin) timed through the reference's own call sites
+    # (tests/dropin/dropin_calls --time), beside the oracle's loops: part of the CPU-baseline
+    # leg, since that program also runs the oracle (as its checker and as the CPU side)
+    dropin = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and not args.no_dropin:
+        dropin = dropin_leg()
     if lat is not None and cpu is not None:
         cpu_lat = cpu["ms_pyramid"] + cpu["ms_extract"] + cpu["ms_align"]
         lat["cpu_port_ms"] = round(cpu_lat, 3)
@@ -586,12 +593,42 @@ def main():
             "latency": lat,
             "c4_batched": c4_line,
             "tracking_searches": a11_line,
+            "dropin_call_sites": dropin,
             "next_rows": {"undistort_remap": und_line, "search_local_points_direct": direct_line,
                           "stereo_matches": stereo_line, "dbow2_transform": bow_line},
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dropin_leg():
+    """The drop-in C++ headers through the reference's own call sites (Frame.cc:327-348,
+    Tracking.cc:1156-1171, 1662-1674, 2171): tests/dropin/dropin_calls built and run with
+    --time.  Each line: median ms per call through the drop-in (host cv::Mat / Frame /
+    MapPoint in, results written back into the Frame) and the oracle's literal loops
+    (1 thread).  None when the program cannot be built here."""
+    import subprocess
+    root = os.path.dirname(os.path.abspath(__file__))
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(root, "compat"), "dropin"], check=True, timeout=240,
+                       capture_output=True)
+        r = subprocess.run([os.path.join(root, "compat", "build", "dropin_calls"), "--time"], capture_output=True,
+                           text=True, timeout=240)
+    except Exception as e:  # noqa: BLE001 -- reported, never fatal to the bench line
+        return {"error": repr(e)[:200]}
+    out = {"parity": "ok" if r.returncode == 0 else f"FAILED (rc {r.returncode})"}
+    for ln in r.stdout.splitlines():
+        f = ln.split()
+        if len(f) >= 6 and f[0] == "TIMING" and f[2] == "dropin_ms":
+            d = {"dropin_ms": float(f[3]), "oracle_ms": float(f[5])}
+            d["speedup_vs_cpu_port"] = round(d["oracle_ms"] / d["dropin_ms"], 2) if d["dropin_ms"] > 0 else None
+            if len(f) >= 8:
+                d[f[6]] = int(f[7])
+            out[f[1]] = d
+    out["path"] = ("compat/dropin headers (ORBextractor.h, SparseImageAlign.h, ORBmatcherGPU.h) under the "
+                   "reference's call sites, libygzfe.so underneath; CPU side: the oracle, 1 thread")
+    return out
 
 
 def plane_xyz(S, pose, kps, cam):

@@ -262,6 +262,7 @@ struct ygzfe_extractor {
     hipStream_t astream = nullptr;
     hipEvent_t ev_align_fork = nullptr, ev_align_done = nullptr;
     HostBuf ahin, ahout;
+    HostBuf hlvl;  // page-locked staging of ygzfe_frame_level / _set_level (pageable 2-D copies are row by row)
     bool align_pending = false;
     bool graph_broken = false;  // stream capture failed once: plain launches
     std::mutex mu;
@@ -577,9 +578,22 @@ int ygzfe_frame_level(const ygzfe_frame *f, int level, int *w, int *h, uint8_t *
     if (h) *h = L.h;
     if (dst) {
         if (dst_stride < L.w) { set_error("dst_stride < level width"); return YGZFE_EINVAL; }
-        YGZ_TRY(ensure_device(f->ex->device));
-        YGZ_HIP(hipStreamSynchronize(f->ex->stream));
-        YGZ_HIP(hipMemcpy2D(dst, dst_stride, f->pyr.as<uint8_t>() + L.off, L.w, L.w, L.h, hipMemcpyDeviceToHost));
+        ygzfe_extractor *ex = f->ex;
+        YGZ_TRY(ensure_device(ex->device));
+        std::lock_guard<std::mutex> lk(ex->mu);
+        // one contiguous DMA into page-locked staging, ordered after the frame's work on
+        // ex->stream, then the row copy on the host
+        const size_t n = (size_t)L.w * L.h;
+        YGZ_HIP(hipStreamSynchronize(ex->stream));  // the staging's previous use, the pyramid's writers
+        YGZ_TRY(ex->hlvl.ensure(n));
+        YGZ_HIP(hipMemcpyAsync(ex->hlvl.p, f->pyr.as<uint8_t>() + L.off, n, hipMemcpyDeviceToHost, ex->stream));
+        YGZ_HIP(hipStreamSynchronize(ex->stream));
+        const uint8_t *hs = ex->hlvl.as<uint8_t>();
+        if (dst_stride == L.w) {
+            memcpy(dst, hs, n);
+        } else {
+            for (int y = 0; y < L.h; y++) memcpy(dst + (size_t)y * dst_stride, hs + (size_t)y * L.w, (size_t)L.w);
+        }
     }
     return YGZFE_OK;
 }
@@ -590,10 +604,21 @@ int ygzfe_frame_set_level(ygzfe_frame *f, int level, const uint8_t *src, int src
     if (level < 0 || level >= P.nlevels) { set_error("level %d out of range", level); return YGZFE_EINVAL; }
     const LevelDesc &L = P.lv[level];
     if (src_stride < L.w) { set_error("src_stride < level width"); return YGZFE_EINVAL; }
-    YGZ_TRY(ensure_device(f->ex->device));
-    YGZ_HIP(hipStreamSynchronize(f->ex->stream));
-    if (f->ex->align_pending) YGZ_HIP(hipEventSynchronize(f->ex->ev_align_done));
-    YGZ_HIP(hipMemcpy2D(f->pyr.as<uint8_t>() + L.off, L.w, src, src_stride, L.w, L.h, hipMemcpyHostToDevice));
+    ygzfe_extractor *ex = f->ex;
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    YGZ_HIP(hipStreamSynchronize(ex->stream));  // the staging's previous use
+    if (ex->align_pending) YGZ_HIP(hipEventSynchronize(ex->ev_align_done));  // an alignment reading this pyramid
+    const size_t n = (size_t)L.w * L.h;
+    YGZ_TRY(ex->hlvl.ensure(n));
+    uint8_t *hs = ex->hlvl.as<uint8_t>();
+    if (src_stride == L.w) {
+        memcpy(hs, src, n);
+    } else {
+        for (int y = 0; y < L.h; y++) memcpy(hs + (size_t)y * L.w, src + (size_t)y * src_stride, (size_t)L.w);
+    }
+    YGZ_HIP(hipMemcpyAsync(f->pyr.as<uint8_t>() + L.off, hs, n, hipMemcpyHostToDevice, ex->stream));
+    YGZ_HIP(hipStreamSynchronize(ex->stream));  // the level is in place when the call returns, as before
     return YGZFE_OK;
 }
 

@@ -19,6 +19,7 @@
 //
 // Prints one line per check; exit 0 and "OK" when every check passes.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -159,6 +160,21 @@ static cv::Mat synth(int W, int H, unsigned seed, int dx, int dy) {
     return img;
 }
 
+// median wall time (ms) of `reps` calls of fn(): the drop-in path as a Tracking thread sees
+// it (bench.py's dropin leg reads the TIMING lines)
+template <class Fn>
+static double median_ms(int reps, Fn fn) {
+    std::vector<double> t;
+    for (int i = 0; i < reps; i++) {
+        const auto t0 = std::chrono::steady_clock::now();
+        fn();
+        t.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+static bool g_timing = false;
+
 static ygzo_mframe mframe(const Frame &F, bool uright) {
     ygzo_mframe f;
     f.kps = reinterpret_cast<const ygzo_kp *>(F.mvKeys.data());
@@ -172,7 +188,8 @@ static ygzo_mframe mframe(const Frame &F, bool uright) {
     return f;
 }
 
-int main() {
+int main(int argc, char **argv) {
+    g_timing = argc > 1 && std::strcmp(argv[1], "--time") == 0;
     const int W = 752, H = 480, nl = 4;
     Frame::fx = 458.654f;
     Frame::fy = 457.296f;
@@ -284,6 +301,36 @@ int main() {
         const auto I = T.mpAlign->getFisherInformation();
         CHECK(std::fabs(I(0, 0) - ao.H[0] / (float)(5e-4 * 255 * 255)) <= 1e-3f * std::fabs(I(0, 0)) + 1e-3f,
               "getFisherInformation() = H / 32.5125: %.4g", I(0, 0));
+        if (g_timing) {
+            SE3f Tx;
+            const double ga = median_ms(30, [&] { T.SparseAlign(Tx); });
+            const double ca = median_ms(10, [&] {
+                ygzo_sparse_align(rp, cp, lw, lh, o.inv_scale, &cam,
+                                  reinterpret_cast<const ygzo_kp *>(T.mLastFrame.mvKeys.data()), xyz.data(), us.data(),
+                                  T.mLastFrame.N, nl - 1, 1, &T0, &ao);
+            });
+            std::printf("TIMING sparse_align dropin_ms %.4f oracle_ms %.4f\n", ga, ca);
+            // Frame(im, extractor) + ExtractFeatures: the pyramid and the ORB extraction as Frame.cc:327-348
+            // runs them (cv::Mat image on the host, mvKeys / mDescriptors back on the host)
+            // steady state: the drop-in's pyramid pool holds 96 device frames, each created
+            // (and its extraction graph captured) on first use; Tracking streams past that
+            auto one = [&] {
+                Frame Fx(im1, T.mpORBextractorLeft);
+                Fx.ExtractFeatures();
+            };
+            for (int i = 0; i < dropin::PyramidPool::capacity() + 4; i++) one();
+            const double ge = median_ms(30, one);
+            const double gp = median_ms(30, [&] { T.mpORBextractorLeft->ComputePyramid(im1); });
+            const double gf = median_ms(30, [&] { Frame Fx(im1, T.mpORBextractorLeft); });
+            std::printf("TIMING extract_parts pyramid_ms %.4f frame_ctor_ms %.4f\n", gp, gf);
+            std::vector<ygzo_kp> ok_(4096);
+            std::vector<uint8_t> od(4096 * 32);
+            const double ce = median_ms(10, [&] {
+                ygzo_compute_pyramid(&o, im1.data, W, H, W, lp);
+                ygzo_extract_orbslam(&o, lp, lw, lh, nullptr, 0, ok_.data(), od.data(), 4096);
+            });
+            std::printf("TIMING extract dropin_ms %.4f oracle_ms %.4f\n", ge, ce);
+        }
     }
 
     // ---------------------------------------------------------------- SearchByProjection(F, LastF)
@@ -326,6 +373,18 @@ int main() {
         }
         CHECK(same, "matcher.SearchByProjection(mCurrentFrame, mLastFrame, th, MONOCULAR): %d matches (oracle %d)",
               nmatches, wn);
+        if (g_timing) {
+            const double g = median_ms(50, [&] {
+                for (int i = 0; i < C.N; i++) C.mvpMapPoints[i] = nullptr;
+                T.MotionModel(15);
+            });
+            const double c = median_ms(50, [&] {
+                ygzo_search_projection_best(&mf, q.data(), qd.data(), (int)q.size(), blocked.data(), 100, 1,
+                                            want.data());
+            });
+            std::printf("TIMING search_by_projection_last_frame dropin_ms %.4f oracle_ms %.4f queries %zu\n", g, c,
+                        q.size());
+        }
     }
 
     // ---------------------------------------------------------------- SearchByProjection(F, local map points)
@@ -363,6 +422,17 @@ int main() {
         for (int i = 0; i < C.N && same; i++)
             same = C.mvpMapPoints[i] == (want[i] >= 0 ? T.mvpLocalMapPoints[want[i]] : nullptr);
         CHECK(same, "matcher.SearchByProjection(mCurrentFrame, mvpLocalMapPoints, th, false): %d (oracle %d)", cnt, wn);
+        if (g_timing) {
+            const double g = median_ms(50, [&] {
+                for (int i = 0; i < C.N; i++) C.mvpMapPoints[i] = nullptr;
+                T.LocalPoints(3);
+            });
+            const double c = median_ms(50, [&] {
+                ygzo_search_projection_ratio(&mf, q.data(), qd.data(), (int)q.size(), nullptr, 0.8f, want.data());
+            });
+            std::printf("TIMING search_by_projection_local_map dropin_ms %.4f oracle_ms %.4f queries %zu\n", g, c,
+                        q.size());
+        }
     }
 
     // ---------------------------------------------------------------- SearchForInitialization
