@@ -695,6 +695,26 @@ int main(int argc, char **argv) {
                   "SearchLocalPointsDirect() [mnCacheHitTh %d]: %zu points tracked (oracle %zu), local map %s, "
                   "cache %zu -> %zu", th, C.mvKeys.size(), w.keys.size(), w.local_runs ? "searched" : "skipped",
                   cache0.size(), T.mvpDirectMapPointsCache.size());
+            if (g_timing && th == 150) {
+                auto run = [&] {
+                    C.mvKeys.clear();
+                    C.mvpMapPoints.clear();
+                    C.mvDepth.clear();
+                    C.mvbOutlier.clear();
+                    C.mvMatchedFrom.clear();
+                    C.N = 0;
+                    T.mvpDirectMapPointsCache = cache0;
+                    T.mvpLocalMapPoints.clear();
+                    T.mvpNextLocalMapPoints = local;
+                    T.mnCacheHitTh = th;
+                    T.nUpdateLocalMap = 0;
+                    T.TrackLocalMapDirect();
+                };
+                const double g = median_ms(30, run);
+                const double c = median_ms(5, [&] { (void)expected(cache0, local, th); });
+                std::printf("TIMING search_local_points_direct dropin_ms %.4f oracle_ms %.4f points %zu\n", g, c,
+                            local.size() + cache0.size());
+            }
         }
 
         // ORBmatcher::FindDirectProjection, one pair at a time, against the oracle
