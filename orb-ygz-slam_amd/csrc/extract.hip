@@ -2806,6 +2806,10 @@ static int octree_nc(const LevelDesc &L) {
 #define YGZ_OCT_THREADS 512
 #endif
 constexpr int kOctThreads = YGZ_OCT_THREADS;
+#ifndef YGZ_OCT_LIST_THREADS
+#define YGZ_OCT_LIST_THREADS 256  // k_octree_list workgroup of the batched classes
+#endif
+constexpr int kOctListThreads = YGZ_OCT_LIST_THREADS;
 
 // queue words per launch group g: counters at octq[8 g ..] (list i: count 2i, taken
 // 2i + 1), lists at octq[kOctQHead + (3 g + i) T], T = frames x levels; then the
@@ -2856,8 +2860,8 @@ static hipError_t launch_octree_levels(int nc, const Plan *dp, const uint32_t *c
                            cellbuf, cellcnt, candA, candB, hdr, Q1 ? q2 : q1);                                    \
         hipLaunchKernelGGL((k_octree_global<NC, 512>), dim3(std::min(tasks, 64)), dim3(512), 0, st, dp, cellbuf,  \
                            cellcnt, candA, candB, sel, selcnt, err, Q1 ? q3 : q2);                                \
-        hipLaunchKernelGGL((k_octree_list<NC, 256>), grid, dim3(256), 0, st, dp, candA, candB, hdr, sel, selcnt,  \
-                           err, l0);                                                                              \
+        hipLaunchKernelGGL((k_octree_list<NC, kOctListThreads>), grid, dim3(kOctListThreads), 0, st, dp, candA,   \
+                           candB, hdr, sel, selcnt, err, l0);                                                     \
     } while (0)
     if (wide && nc <= 1024) {
         YGZ_OCT_SORT0(1024, 8192, 1024);
