@@ -73,10 +73,11 @@ def parse():
     ap.add_argument("--no-align", action="store_true")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture one step into a HIP graph and replay it (measured: same throughput as eager launches)")
-    ap.add_argument("--schedule", choices=["split", "overlap", "serial"], default="serial",
+    ap.add_argument("--schedule", choices=["split", "overlap", "tail", "serial"], default="serial",
                     help="split: blur + descriptors + Hamming on a side stream beside FAST / octree, "
                          "SparseImgAlign after them; overlap: SparseImgAlign beside orient + Hamming too; "
-                         "serial: every stage on one stream")
+                         "tail: the extraction on one stream, then Hamming on a side stream beside "
+                         "SparseImgAlign; serial: every stage on one stream")
     ap.add_argument("--chunks", type=int, default=0,
                     help="process each rank's shard in this many chunks (each its own batch), gathering a "
                          "chunk's result slots on a communication stream while the next chunk computes "
@@ -241,9 +242,27 @@ def main():
                                    camera, 3, 1, T_init.data_ptr(), out.data_ptr(), sptr)
         pack_and_gather(timed_gather)
 
+    def step_tail(timed_gather=False):
+        # extraction in stage order on `stream` (each extraction kernel has the GPU to
+        # itself), then Hamming (descriptors) on `side` beside SparseImgAlign (pyramids +
+        # rows) on `stream`
+        batch.extract(F, sptr)
+        side.wait_stream(stream)
+        batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(),
+                    side.cuda_stream)
+        if not args.no_align:
+            ygzfe.plane_points_device(kps_t.data_ptr(), cap, P, cam, r3_t.data_ptr(), cz_t.data_ptr(), S.PLANE_Z,
+                                      xyz.data_ptr(), sptr)
+            batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(), camera,
+                               3, 1, T_init.data_ptr(), out.data_ptr(), sptr)
+        stream.wait_stream(side)  # the slots need the match results' descriptors in place
+        pack_and_gather(timed_gather)
+
     def step(timed_gather=False):
         if args.schedule == "serial" or P == 0:
             return step_serial(timed_gather)
+        if args.schedule == "tail":
+            return step_tail(timed_gather)
         # keypoint rows on `stream`, blur + descriptors on `side` (the blur runs
         # beside FAST); Hamming (descriptors only) follows on `side`
         side.wait_stream(stream)
