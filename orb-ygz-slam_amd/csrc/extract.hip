@@ -591,6 +591,9 @@ struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI 
 #if defined(__FAST_MATH__)
 #error "k_fast_cells orders ring bytes as f16 subnormals: build without fast-math (denormals kept)"
 #endif
+#ifndef YGZ_FAST_A2
+#define YGZ_FAST_A2 0  // two row chunks per step: measured equal (0.614 vs 0.617 ms / 1024)
+#endif
 template <int S>
 __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, const CellDesc &cd, uint8_t *img,
                                                uint8_t *sc, uint16_t *list, uint32_t *__restrict__ out,
@@ -617,8 +620,8 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
 #pragma unroll
             for (int k = 0; k < 4; k++) colmask |= (uint32_t)(4 * j + k < iw) << k;
             const s16x2 t2 = {(short)th, (short)th};
-            for (int y0 = 0; y0 < ih; y0 += rpc) {
-                const int y = y0 + rr;  // interior row; its pixels are ROI (4j+3+k, y+3)
+            // the screen of the lane's 4 pixels in interior row y (bit k: pixel 4j + k survives)
+            auto screen = [&](int y) -> uint32_t {
                 const uint32_t *rt = reinterpret_cast<const uint32_t *>(img + y * S) + j;
                 const uint32_t *rc = reinterpret_cast<const uint32_t *>(img + (y + 3) * S) + j;
                 const uint32_t *rb = reinterpret_cast<const uint32_t *>(img + (y + 6) * S) + j;
@@ -646,9 +649,12 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                     const s16x2 m = __builtin_elementwise_max(__builtin_bit_cast(s16x2, bv) - v, v - __builtin_bit_cast(s16x2, dv));
                     sg[hlf] = as_u32(t2 - m);
                 }
-                uint32_t m = ((sg[0] >> 15) & 1u) | (((sg[1] >> 15) & 1u) << 1) | (((sg[0] >> 31) & 1u) << 2) |
-                             (((sg[1] >> 31) & 1u) << 3);
-                m &= y < ih ? colmask : 0u;
+                const uint32_t m = ((sg[0] >> 15) & 1u) | (((sg[1] >> 15) & 1u) << 1) | (((sg[0] >> 31) & 1u) << 2) |
+                                   (((sg[1] >> 31) & 1u) << 3);
+                return m & (y < ih ? colmask : 0u);
+            };
+            // survivors appended in raster order (lanes are row-major, bits in column order)
+            auto compact = [&](uint32_t m, int y) {
                 const uint64_t M0 = __ballot(m & 1u), M1 = __ballot(m & 2u), M2 = __ballot(m & 4u), M3 = __ballot(m & 8u);
                 int pos = na + popc_below(M0) + popc_below(M1) + popc_below(M2) + popc_below(M3);
                 const uint32_t ey = (uint32_t)(y + 3) << 8;
@@ -656,7 +662,18 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                 for (int k = 0; k < 4; k++)
                     if ((m >> k) & 1u) list[pos++] = (uint16_t)(ey | (uint32_t)(4 * j + k + 3));
                 na += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
+            };
+#if YGZ_FAST_A2
+            // two row chunks per step: the second chunk's LDS reads are in flight while the
+            // first is screened (rows past ih screen out through colmask)
+            for (int y0 = 0; y0 < ih; y0 += 2 * rpc) {
+                const uint32_t ma = screen(y0 + rr), mb = screen(y0 + rpc + rr);
+                compact(ma, y0 + rr);
+                if (y0 + rpc < ih) compact(mb, y0 + rpc + rr);
             }
+#else
+            for (int y0 = 0; y0 < ih; y0 += rpc) compact(screen(y0 + rr), y0 + rr);
+#endif
         }
         if (S == 40 && pass == 0) YGZ_BSTAMP_K(2, 4);
 #if defined(YGZ_FAST_STOP) && YGZ_FAST_STOP <= 1  // timing experiment only (never in the product build)
