@@ -244,6 +244,9 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 #define YGZ_BLUR_AHEAD 10  // rows in flight per wave
 #endif
 constexpr int kBlurAhead = YGZ_BLUR_AHEAD;
+#ifndef YGZ_BLUR_ROLLED
+#define YGZ_BLUR_ROLLED 0  // rolled by the prefetch period: 88 -> 33 KB of code, but 2 % slower
+#endif
 
 __device__ __forceinline__ void blur_hsum(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t o,
                                           uint32_t ka, uint32_t kb, uint32_t h[4]) {
@@ -343,10 +346,22 @@ __device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ s
     const bool store_lane = x < w;
     uint32_t prv[4] = {0u, 0u, 0u, 0u};  // row sums of the previous row
     uint32_t pr[5][4];                   // pr[m]: (row n-5+m-1, row n-5+m) packed, m = 0..4
+#if YGZ_BLUR_ROLLED
+    // rows in blocks of kBlurAhead (the prefetch ring's period): the body is unrolled
+    // only that far, so the kernel stays inside the instruction cache
+    for (int r0 = 0; r0 < kBlurRows + 6; r0 += kBlurAhead)
+#pragma unroll
+    for (int i = 0; i < kBlurAhead; i++) {
+        const int r = r0 + i;
+        if (r >= kBlurRows + 6) break;
+        Row cur = buf[i];
+        if (r + kBlurAhead < kBlurRows + 6) fetch(r + kBlurAhead, buf[i]);
+#else
 #pragma unroll
     for (int r = 0; r < kBlurRows + 6; r++) {
         Row cur = buf[r % kBlurAhead];
         if (r + kBlurAhead < kBlurRows + 6) fetch(r + kBlurAhead, buf[r % kBlurAhead]);
+#endif
         uint32_t am1 = (uint32_t)__builtin_amdgcn_update_dpp((int)cur.halo, (int)cur.a, 0x138, 0xF, 0xF, false);
         if (right_edge) {
             if (fix_r) cur.a = __builtin_amdgcn_perm(cur.a, am1, 0x03000102u);
@@ -448,10 +463,20 @@ __global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(const uint8_t *__re
         for (int r = 0; r < kBlurAhead; r++) fetch(r, buf[r]);
         const bool active = x < w;
         uint32_t ring[7][4];
+#if YGZ_BLUR_ROLLED
+        for (int r0 = 0; r0 < kBlurRows + 6; r0 += kBlurAhead)
+#pragma unroll
+        for (int i = 0; i < kBlurAhead; i++) {
+            const int r = r0 + i;
+            if (r >= kBlurRows + 6) break;
+            const BlurRow cur = buf[i];
+            if (r + kBlurAhead < kBlurRows + 6) fetch(r + kBlurAhead, buf[i]);
+#else
 #pragma unroll
         for (int r = 0; r < kBlurRows + 6; r++) {
             const BlurRow cur = buf[r % kBlurAhead];
             if (r + kBlurAhead < kBlurRows + 6) fetch(r + kBlurAhead, buf[r % kBlurAhead]);
+#endif
             // A[l-1], A[l], A[l+1], A[l+2] (row dwords around the lane's own)
             const uint32_t hl = __builtin_amdgcn_readlane(cur.halo, 0);
             const uint32_t hr1 = __builtin_amdgcn_readlane(cur.halo, 1), hr2 = __builtin_amdgcn_readlane(cur.halo, 2);
@@ -1476,87 +1501,6 @@ __device__ __forceinline__ void radix_pass(CP src_c, IP src_i, CP dst_c, IP dst_
         }
     }
     __syncthreads();
-}
-
-// value of lane ^ J (J < 64): quad_perm for 1 and 2, two bank-masked row shifts
-// for 4 and 8, a row / half-wave swap for 16 and 32
-template <int J>
-__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
-    if constexpr (J == 1) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
-    } else if constexpr (J == 2) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
-    } else if constexpr (J == 4) {  // banks 0, 2 <- row_shl:4; banks 1, 3 <- row_shr:4
-        const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0x5, false);
-        return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)v, 0x114, 0xF, 0xA, false);
-    } else if constexpr (J == 8) {
-        const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x108, 0xF, 0x3, false);
-        return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)v, 0x118, 0xF, 0xC, false);
-    } else if constexpr (J == 16) {  // {r0, r0, r2, r2} and {r1, r1, r3, r3}
-        const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-        return (lane_id() & 16) ? p[0] : p[1];
-    } else {  // {lo, lo} and {hi, hi}
-        const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-        return (lane_id() & 32) ? p[0] : p[1];
-    }
-}
-
-// one bitonic stage (k, J) over a wave's 64 R elements, element e = 64 r + lane:
-// ascending where (e & k) == 0; codes distinct, pads (all ones) only equal to pads.
-// J is a template parameter (the lane exchange pattern), k a runtime value, so the
-// whole sort is a loop over one compiled body per J (~1k instructions in all; a
-// fully unrolled network is ~4k and thrashes the instruction cache beside the
-// other octree classes)
-template <int R, int J>
-__device__ __forceinline__ void bitonic_stage(uint32_t (&S)[R], uint32_t (&I)[R], int k) {
-    const int lane = lane_id();
-    if constexpr (J >= 64) {
-        constexpr int D = J / 64;
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            if (r & D) continue;
-            const bool asc = ((r * 64) & k) == 0;
-            const bool sw = asc ? S[r + D] < S[r] : S[r] < S[r + D];
-            const uint32_t a = S[r], b = S[r + D], ia = I[r], ib = I[r + D];
-            S[r] = sw ? b : a;
-            S[r + D] = sw ? a : b;
-            I[r] = sw ? ib : ia;
-            I[r + D] = sw ? ia : ib;
-        }
-    } else {
-        const bool lower = (lane & J) == 0;
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const bool asc = ((r * 64 + lane) & k) == 0;
-            const uint32_t ps = xor_lane<J>(S[r]), pi = xor_lane<J>(I[r]);
-            const bool take = (lower == asc) ? ps < S[r] : S[r] < ps;
-            S[r] = take ? ps : S[r];
-            I[r] = take ? pi : I[r];
-        }
-    }
-}
-
-template <int R>
-__device__ __forceinline__ void bitonic_sort(uint32_t (&S)[R], uint32_t (&I)[R]) {
-#pragma nounroll
-    for (int k = 2; k <= 64 * R; k <<= 1) {
-#pragma nounroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            switch (j) {
-                case 1: bitonic_stage<R, 1>(S, I, k); break;
-                case 2: bitonic_stage<R, 2>(S, I, k); break;
-                case 4: bitonic_stage<R, 4>(S, I, k); break;
-                case 8: bitonic_stage<R, 8>(S, I, k); break;
-                case 16: bitonic_stage<R, 16>(S, I, k); break;
-                case 32: bitonic_stage<R, 32>(S, I, k); break;
-                case 64: if constexpr (R > 1) bitonic_stage<R, 64>(S, I, k); break;
-                case 128: if constexpr (R > 2) bitonic_stage<R, 128>(S, I, k); break;
-                case 256: if constexpr (R > 4) bitonic_stage<R, 256>(S, I, k); break;
-                case 512: if constexpr (R > 8) bitonic_stage<R, 512>(S, I, k); break;
-                default: break;
-            }
-        }
-    }
 }
 
 __device__ __forceinline__ int lcp_depth(uint32_t a, uint32_t b, int rb) {
