@@ -172,6 +172,45 @@ static inline uint32_t fast10_screen32(const uint8_t *p, const int pix[16], int 
     s = _mm256_max_epu8(s, _mm256_min_epu8(D[3], D[0]));
     return ~(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(s, _mm256_setzero_si256()));
 }
+
+/* The segment test and arcmax of 32 screened pixels in unsigned-saturating
+ * bytes: bright margins b_k = ring_k -sat v, dark d_k = v -sat ring_k, the
+ * largest 10-arc minimum of each by min doubling (2, 4, 8, then + 2).  The
+ * saturation clamps arcmax at 0, and a corner needs arcmax > barrier >= 0, so
+ * the corners and their arcmax are the int16 test's exactly (half the lanes'
+ * work of fast10_test16 per pixel).  Bit i = corner at p + i; am[i] = arcmax. */
+static inline uint32_t fast10_test32(const uint8_t *p, const int pix[16], int barrier, uint8_t am[32]) {
+    const __m256i v = _mm256_loadu_si256((const __m256i *)p);
+    __m256i b2[16], d2[16];
+    {
+        __m256i b[16], d[16];
+        for (int k = 0; k < 16; k++) {
+            const __m256i e = _mm256_loadu_si256((const __m256i *)(p + pix[k]));
+            b[k] = _mm256_subs_epu8(e, v);
+            d[k] = _mm256_subs_epu8(v, e);
+        }
+        for (int k = 0; k < 16; k++) {
+            b2[k] = _mm256_min_epu8(b[k], b[(k + 1) & 15]);
+            d2[k] = _mm256_min_epu8(d[k], d[(k + 1) & 15]);
+        }
+    }
+    __m256i best = _mm256_setzero_si256();
+    {
+        __m256i b4[16], d4[16];
+        for (int k = 0; k < 16; k++) {
+            b4[k] = _mm256_min_epu8(b2[k], b2[(k + 2) & 15]);
+            d4[k] = _mm256_min_epu8(d2[k], d2[(k + 2) & 15]);
+        }
+        for (int k = 0; k < 16; k++) {
+            const __m256i b10 = _mm256_min_epu8(_mm256_min_epu8(b4[k], b4[(k + 4) & 15]), b2[(k + 8) & 15]);
+            const __m256i d10 = _mm256_min_epu8(_mm256_min_epu8(d4[k], d4[(k + 4) & 15]), d2[(k + 8) & 15]);
+            best = _mm256_max_epu8(best, _mm256_max_epu8(b10, d10));
+        }
+    }
+    _mm256_storeu_si256((__m256i *)am, best);
+    const __m256i over = _mm256_subs_epu8(best, _mm256_set1_epi8((char)barrier)); /* nonzero <=> am > barrier */
+    return ~(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(over, _mm256_setzero_si256()));
+}
 #endif
 
 /* corners of rows [y0, y1) x columns [3, w - 3) in raster order; arcmax per corner if am != NULL */
@@ -184,22 +223,20 @@ static int fast10_rows(const uint8_t *img, int w, int y0, int y1, int stride, in
         int x = 3;
         if (!g_fast10_scalar) {
 #if defined(__AVX2__)
-            for (; x + 32 <= w - 3; x += 32) {  /* 32 pixels screened in bytes, survivors' halves tested */
+            for (; x + 32 <= w - 3; x += 32) {  /* 32 pixels screened, then tested, in bytes */
                 const uint8_t *p = img + (size_t)y * stride + x;
                 const uint32_t scr = fast10_screen32(p, pix, barrier);
-                for (int half = 0; half < 2; half++) {
-                    if (!((scr >> (16 * half)) & 0xFFFFu)) continue;
-                    int16_t a[16];
-                    unsigned m = fast10_test16(p + 16 * half, pix, barrier, a);
-                    while (m) {
-                        const int i = __builtin_ctz(m);
-                        m &= m - 1;
-                        if (n < cap) {
-                            xs[n] = (int16_t)(x + 16 * half + i); ys[n] = (int16_t)y;
-                            if (am) am[n] = a[i];
-                        }
-                        n++;
+                if (!scr) continue;
+                uint8_t a[32];
+                uint32_t m = fast10_test32(p, pix, barrier, a) & scr;
+                while (m) {
+                    const int i = __builtin_ctz(m);
+                    m &= m - 1;
+                    if (n < cap) {
+                        xs[n] = (int16_t)(x + i); ys[n] = (int16_t)y;
+                        if (am) am[n] = a[i];
                     }
+                    n++;
                 }
             }
 #endif
