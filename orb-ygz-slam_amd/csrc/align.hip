@@ -1152,6 +1152,24 @@ __global__ __launch_bounds__(64) void k_align2d_window(const uint8_t *__restrict
     }
 }
 
+// Stream placement probe: one lane waits `us` microseconds on the 100 MHz
+// real-time counter (bounded: it always ends), then exits; k_empty does nothing.
+__global__ void k_hold_us(int us) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime(), ticks = (uint64_t)us * 100u;
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+__global__ void k_empty() {}
+
+hipError_t launch_hold_us(int us, hipStream_t st) {
+    hipLaunchKernelGGL(k_hold_us, dim3(1), dim3(64), 0, st, us);
+    return hipGetLastError();
+}
+hipError_t launch_empty(hipStream_t st) {
+    hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st);
+    return hipGetLastError();
+}
+
 hipError_t launch_align2d_window(const uint8_t *win, int stride, int w, int h, int x0, int y0, int ww, int wh,
                                  const uint8_t *pwb, const uint8_t *p, int n_iter, float *px, int *status,
                                  hipStream_t st) {

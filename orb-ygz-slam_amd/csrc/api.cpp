@@ -9,6 +9,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -278,16 +280,68 @@ struct ygzfe_extractor {
         for (int i = 0; i < 2; i++) YGZ_HIP(hipEventCreateWithFlags(&ev_oct_join[i], hipEventDisableTiming));
         return YGZFE_OK;
     }
+    // Does work on `cand` run beside work on `stream`?  `stream` is held for 2 ms by
+    // one lane; an empty kernel on `cand` must finish inside the hold.  A stream that
+    // shares the hardware queue of `stream` waits for the hold instead.
+    int probe_beside(hipStream_t cand, bool &beside) {
+        beside = false;
+        YGZ_HIP(launch_empty(cand));  // the candidate's queue acquired, both streams idle
+        YGZ_HIP(hipStreamSynchronize(cand));
+        YGZ_HIP(hipStreamSynchronize(stream));
+        hipEvent_t ea = nullptr, eb = nullptr;
+        hipError_t e = hipEventCreateWithFlags(&ea, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&eb, hipEventDisableTiming);
+        if (e == hipSuccess) e = launch_hold_us(2000, stream);
+        if (e == hipSuccess) e = hipEventRecord(ea, stream);
+        if (e == hipSuccess) e = launch_empty(cand);
+        if (e == hipSuccess) e = hipEventRecord(eb, cand);
+        if (e == hipSuccess) {
+            const auto t0 = std::chrono::steady_clock::now();
+            while (hipEventQuery(eb) == hipErrorNotReady &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(50)) {
+            }
+            beside = hipEventQuery(eb) == hipSuccess && hipEventQuery(ea) == hipErrorNotReady;
+        }
+        (void)hipStreamSynchronize(stream);
+        (void)hipStreamSynchronize(cand);
+        if (ea) (void)hipEventDestroy(ea);
+        if (eb) (void)hipEventDestroy(eb);
+        if (e != hipSuccess) { set_error("align stream probe: %s", hipGetErrorString(e)); return YGZFE_EHIP; }
+        return YGZFE_OK;
+    }
     int ensure_align_stream() {
         if (astream) return YGZFE_OK;
         // Normal priority, created on first use.  Measured alternatives (tools/run_lat_ab.sh):
         // the greatest / least priority, a dedicated queue (full CU mask) and creating the
         // extractor's streams eagerly all ran the single-frame path 15-30 % slower.
-        YGZ_HIP(hipStreamCreateWithFlags(&astream, hipStreamNonBlocking));
+        // Streams beyond GPU_MAX_HW_QUEUES share hardware queues, and an align stream on the
+        // extraction stream's queue runs after the extraction instead of beside it (0.28
+        // instead of 0.16 ms per frame).  So each candidate is probed; a
+        // rejected one stays alive until the choice is made (the next stream then lands on
+        // another queue).  YGZFE_ALIGN_PROBE=0 keeps the first stream unprobed.
         YGZ_HIP(hipEventCreateWithFlags(&ev_align_fork, hipEventDisableTiming));
         YGZ_HIP(hipEventCreateWithFlags(&ev_align_done, hipEventDisableTiming));
-        return YGZFE_OK;
+        const char *pe = getenv("YGZFE_ALIGN_PROBE");
+        const bool probe = !(pe && pe[0] == '0');
+        std::vector<hipStream_t> rejected;
+        int rc = YGZFE_OK;
+        for (int attempt = 0; rc == YGZFE_OK && !astream; attempt++) {
+            hipStream_t s = nullptr;
+            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+                set_error("hipStreamCreate failed");
+                rc = YGZFE_EHIP;
+                break;
+            }
+            bool beside = true;
+            if (probe && attempt < 4) rc = probe_beside(s, beside);
+            if (rc == YGZFE_OK && beside) astream = s;
+            else rejected.push_back(s);
+            align_probe_attempts = attempt + 1;
+        }
+        for (hipStream_t s : rejected) (void)hipStreamDestroy(s);
+        return rc;
     }
+    int align_probe_attempts = 0;
     // work about to rewrite a pyramid on `st` waits for the alignment reading it
     int order_after_align(hipStream_t st) {
         if (align_pending) YGZ_HIP(hipStreamWaitEvent(st, ev_align_done, 0));

@@ -619,6 +619,9 @@ struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI 
 #ifndef YGZ_FAST_A2
 #define YGZ_FAST_A2 0  // two row chunks per step: measured equal (0.614 vs 0.617 ms / 1024)
 #endif
+#ifndef YGZ_FAST_C3
+#define YGZ_FAST_C3 0  // phase-A compaction by the survivor count's 3 bits (experiment)
+#endif
 template <int S>
 __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, const CellDesc &cd, uint8_t *img,
                                                uint8_t *sc, uint16_t *list, uint32_t *__restrict__ out,
@@ -680,13 +683,21 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             };
             // survivors appended in raster order (lanes are row-major, bits in column order)
             auto compact = [&](uint32_t m, int y) {
+#if YGZ_FAST_C3
+                // the lane's survivor count (0..4) by its three bits: 3 ballots instead of 4
+                const uint32_t cn = __builtin_popcount(m);
+                const uint64_t C0 = __ballot(cn & 1u), C1 = __ballot(cn & 2u), C2 = __ballot(cn & 4u);
+                int pos = na + popc_below(C0) + 2 * popc_below(C1) + 4 * popc_below(C2);
+                na += __popcll(C0) + 2 * __popcll(C1) + 4 * __popcll(C2);
+#else
                 const uint64_t M0 = __ballot(m & 1u), M1 = __ballot(m & 2u), M2 = __ballot(m & 4u), M3 = __ballot(m & 8u);
                 int pos = na + popc_below(M0) + popc_below(M1) + popc_below(M2) + popc_below(M3);
+                na += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
+#endif
                 const uint32_t ey = (uint32_t)(y + 3) << 8;
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     if ((m >> k) & 1u) list[pos++] = (uint16_t)(ey | (uint32_t)(4 * j + k + 3));
-                na += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
             };
 #if YGZ_FAST_A2
             // two row chunks per step: the second chunk's LDS reads are in flight while the

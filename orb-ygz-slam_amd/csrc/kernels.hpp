@@ -107,6 +107,10 @@ hipError_t launch_sparse_align(const AlignLevels &lv, const ygzfe_camera &cam, c
                                int njobs, float *scratch, size_t scratch_per_job, ygzfe_align_result *out,
                                hipStream_t st, int max_n);
 size_t sparse_align_scratch_floats(int n);
+// stream placement probe (ensure_align_stream): a kernel that holds its stream for
+// `us` microseconds of wall clock, and an empty one
+hipError_t launch_hold_us(int us, hipStream_t st);
+hipError_t launch_empty(hipStream_t st);
 hipError_t launch_align2d(const uint8_t *img, int w, int h, int n, const uint8_t *pwb, const uint8_t *p,
                           int n_iter, float *px, uint8_t *conv, hipStream_t st);
 hipError_t launch_align2d_window(const uint8_t *win, int stride, int w, int h, int x0, int y0, int ww, int wh,
