@@ -581,30 +581,38 @@ __device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
 // them with v_alignbyte into one ds_write_b32 (commit).  NI loads per lane.
 // Loads are buffer loads on the frame's level (wave-uniform descriptor, 32-bit
 // lane offsets, one 24-bit multiply-add per row; reads past the level return 0).
+// YGZ_FAST_SHIFT = 1: every ROI row is staged one byte to the right (LDS byte c + 1
+// of the row holds ROI column c), so the dword holding interior pixels 4j..4j+3
+// (ROI columns 4j+3..4j+6) is aligned: phase A reads 5 dwords per 4 pixels
+// instead of 7.  Needs S >= ROI width + 1.
+#ifndef YGZ_FAST_SHIFT
+#define YGZ_FAST_SHIFT 0
+#endif
 template <int S, int R>
 struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI height)
     static constexpr int DW = S / 4, RPI = 64 / DW, NI = (R + RPI - 1) / RPI;
     uint32_t lo[NI], hi[NI];
     __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, uint32_t off0, int w, int rw, int rh, int lane) {
-        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + 3) / 4;
+        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + YGZ_FAST_SHIFT + 3) / 4;
 #pragma unroll
         for (int k = 0; k < NI; k++) {
             const int r = k * RPI + rlane;
             lo[k] = hi[k] = 0u;
             if (rlane < RPI && r < rh && dw < ndw) {
-                const uint32_t o = (mad24((uint32_t)r, (uint32_t)w, off0) & ~3u) + 4u * (uint32_t)dw;
+                // (a row start at level offset 0 wraps below 0 when shifted: that dword reads 0)
+                const uint32_t o = ((mad24((uint32_t)r, (uint32_t)w, off0) - YGZ_FAST_SHIFT) & ~3u) + 4u * (uint32_t)dw;
                 lo[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0);
                 hi[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4u, 0, 0);
             }
         }
     }
     __device__ __forceinline__ void commit(uint8_t *img, uint32_t off0, int w, int rw, int rh, int lane) const {
-        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + 3) / 4;
+        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + YGZ_FAST_SHIFT + 3) / 4;
 #pragma unroll
         for (int k = 0; k < NI; k++) {
             const int r = k * RPI + rlane;
             if (rlane < RPI && r < rh && dw < ndw) {
-                const uint32_t sh = mad24((uint32_t)r, (uint32_t)w, off0) & 3u;
+                const uint32_t sh = (mad24((uint32_t)r, (uint32_t)w, off0) - YGZ_FAST_SHIFT) & 3u;
                 reinterpret_cast<uint32_t *>(img + r * S)[dw] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh);
             }
         }
@@ -650,6 +658,19 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             const s16x2 t2 = {(short)th, (short)th};
             // the screen of the lane's 4 pixels in interior row y (bit k: pixel 4j + k survives)
             auto screen = [&](int y) -> uint32_t {
+#if YGZ_FAST_SHIFT
+                // rows staged one byte right: pixels 4j..4j+3 are the aligned dword j + 1
+                const uint8_t *al = img - 1;
+                const uint32_t *rt = reinterpret_cast<const uint32_t *>(al + y * S) + j;
+                const uint32_t *rc = reinterpret_cast<const uint32_t *>(al + (y + 3) * S) + j;
+                const uint32_t *rb = reinterpret_cast<const uint32_t *>(al + (y + 6) * S) + j;
+                const uint32_t D0 = rc[0], D1 = rc[1], D2 = rc[2];
+                const uint32_t C = D1;                                       // x .. x+3
+                const uint32_t Lw = __builtin_amdgcn_alignbyte(D1, D0, 1);  // x-3 .. x
+                const uint32_t Rw = __builtin_amdgcn_alignbyte(D2, D1, 3);  // x+3 .. x+6
+                const uint32_t Tw = rt[1];
+                const uint32_t Bw = rb[1];
+#else
                 const uint32_t *rt = reinterpret_cast<const uint32_t *>(img + y * S) + j;
                 const uint32_t *rc = reinterpret_cast<const uint32_t *>(img + (y + 3) * S) + j;
                 const uint32_t *rb = reinterpret_cast<const uint32_t *>(img + (y + 6) * S) + j;
@@ -659,6 +680,7 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                 const uint32_t Rw = __builtin_amdgcn_alignbyte(D2, D1, 2);  // x+3 .. x+6
                 const uint32_t Tw = __builtin_amdgcn_alignbyte(rt[1], rt[0], 3);
                 const uint32_t Bw = __builtin_amdgcn_alignbyte(rb[1], rb[0], 3);
+#endif
                 uint32_t sg[2];
 #pragma unroll
                 for (int hlf = 0; hlf < 2; hlf++) {
@@ -880,7 +902,7 @@ __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu
     if (lane == 0) cellcnt[(size_t)f * plan->ncells + c] = img[lane * 7] == 255 ? 1 : 0;  // keep the staging live
     return;
 #endif
-    fast_cell_item<S>(plan, cd, img, sc, list, cellbuf + ((size_t)f * plan->ncells + c) * plan->cell_cap,
+    fast_cell_item<S>(plan, cd, img + YGZ_FAST_SHIFT, sc, list, cellbuf + ((size_t)f * plan->ncells + c) * plan->cell_cap,
                       cellcnt + (size_t)f * plan->ncells + c, lane);
     if (S == 40) YGZ_BSTAMP_K(2, 1);
     if (S == 40) YGZ_BSTAMP_K(2, 2);
@@ -2708,7 +2730,7 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
         if (L.ncells == 0) continue;
         // row stride S >= the widest ROI, row capacity R >= the tallest (LDS per
         // wave ~ 2 S R: C2 levels 1-2 have 38-px-wide, 41/50-px-tall ROIs)
-        int S = fast_stride(L.fast_rw), R = fast_stride(L.fast_rh);
+        int S = fast_stride(L.fast_rw + YGZ_FAST_SHIFT), R = fast_stride(L.fast_rh);
         if (!(S == 40 && R <= 56) && S != R) S = R = std::max(S, R);  // other shapes: square slices
         if (R < S) R = S;
         // ROIs up to 36 x 40 (C2 level 0): a 36-byte row stride brings the slice to 4.9 KB,
@@ -2716,7 +2738,7 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
 #ifndef YGZ_FAST36
 #define YGZ_FAST36 1
 #endif
-        if (YGZ_FAST36 && L.fast_rw <= 36 && L.fast_rh <= 40) S = 36, R = 40;
+        if (YGZ_FAST36 && L.fast_rw + YGZ_FAST_SHIFT <= 36 && L.fast_rh <= 40) S = 36, R = 40;
         const size_t lds = fast_cells_lds_bytes(S, R);
         const int cb = L.cell_begin, ce = L.cell_begin + L.ncells;
         const dim3 grid((L.ncells + kFastWaves - 1) / kFastWaves, nframes);
@@ -2747,7 +2769,7 @@ hipError_t launch_fast_merged(const uint8_t *pyr, uint32_t pitch, const Plan &hp
     int S = 40, R = 40;
     for (int l = 0; l < hp.nlevels; l++) {
         if (hp.lv[l].ncells == 0) continue;
-        S = std::max(S, fast_stride(hp.lv[l].fast_rw));
+        S = std::max(S, fast_stride(hp.lv[l].fast_rw + YGZ_FAST_SHIFT));
         R = std::max(R, fast_stride(hp.lv[l].fast_rh));
     }
     if (!(S == 40 && R <= 56)) S = R = std::max(S, R);
