@@ -588,6 +588,12 @@ __device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
 #ifndef YGZ_FAST_SHIFT
 #define YGZ_FAST_SHIFT 0
 #endif
+// a wave's LDS slice (16-B aligned): ROI tile S*R, score map, pixel list.  Shifted, the
+// interior is at most S - 7 wide and the score map R - 2 rows (see the zeroing in
+// fast_cell_item), so C2 level 0 fits a (40, 38) slice of 5,072 B: 8 workgroups per CU
+__host__ __device__ constexpr int fast_slice_bytes(int S, int R) {
+    return (S * R + S * (R - (YGZ_FAST_SHIFT ? 2 : 0)) + 2 * (S - 6 - YGZ_FAST_SHIFT) * (R - 6) + 15) / 16 * 16;
+}
 template <int S, int R>
 struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI height)
     static constexpr int DW = S / 4, RPI = 64 / DW, NI = (R + RPI - 1) / RPI;
@@ -642,8 +648,11 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
         {
             uint4 *z = reinterpret_cast<uint4 *>(sc);
             const uint4 zero = {0u, 0u, 0u, 0u};
-            for (int i = lane; i < (rh * S) / 16; i += 64) z[i] = zero;
-            for (int i = ((rh * S) / 16) * 16 + lane; i < rh * S; i += 64) sc[i] = 0;
+            // corners sit on rows <= rh - 4, so their NMS windows end at row rh - 3
+            constexpr int kZr = YGZ_FAST_SHIFT ? 2 : 0;  // the shifted layout's score map: R - 2 rows
+            const int nz = (rh - kZr) * S;
+            for (int i = lane; i < nz / 16; i += 64) z[i] = zero;
+            for (int i = (nz / 16) * 16 + lane; i < nz; i += 64) sc[i] = 0;
         }
         // A: 4 pixels per lane, byte pairs as packed u16 / i16 halves; the test
         //    is (T|B) & (L|R) beyond the threshold for either polarity.
@@ -853,7 +862,7 @@ __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu
     const CellDesc *__restrict__ cells, uint32_t *__restrict__ cellbuf, int *__restrict__ cellcnt, int cell_begin,
     int cell_end, int level, int *__restrict__ clear_flag) {
     extern __shared__ uint8_t s_dyn[];
-    constexpr int slice = (2 * S * R + 2 * (S - 6) * (R - 6) + 15) / 16 * 16;  // 16-B aligned slices
+    constexpr int slice = fast_slice_bytes(S, R);
     // wave-uniform cell index: the CellDesc and the level record come by scalar
     // loads (vector loads here put two dependent global round trips in front of
     // the ROI loads)
@@ -883,7 +892,7 @@ __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu
     if (c >= cell_end) return;
     uint8_t *img = s_dyn + wave * slice;
     uint8_t *sc = img + S * R;
-    uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * R);
+    uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * (R - (YGZ_FAST_SHIFT ? 2 : 0)));
     const CellDesc cd = scalar_load(cells + c);
     // one launch per level: the level record loads beside cd, not after it;
     // level < 0 (one launch over every level's cells): the cell's own level
@@ -915,7 +924,7 @@ static int fast_stride(int roi) {
 }
 
 static size_t fast_cells_lds_bytes(int S, int R) {
-    return kFastWaves * (size_t)((2 * S * R + 2 * (S - 6) * (R - 6) + 15) / 16 * 16);
+    return kFastWaves * (size_t)fast_slice_bytes(S, R);
 }
 
 // ---------------------------------------------------------------------------
@@ -2739,6 +2748,7 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
 #define YGZ_FAST36 1
 #endif
         if (YGZ_FAST36 && L.fast_rw + YGZ_FAST_SHIFT <= 36 && L.fast_rh <= 40) S = 36, R = 40;
+        if (YGZ_FAST_SHIFT && S == 40 && R == 40 && L.fast_rh <= 38) R = 38;  // the shifted C2 level 0
         const size_t lds = fast_cells_lds_bytes(S, R);
         const int cb = L.cell_begin, ce = L.cell_begin + L.ncells;
         const dim3 grid((L.ncells + kFastWaves - 1) / kFastWaves, nframes);
@@ -2747,6 +2757,9 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
                                                                                 : lvl_streams[(l - 1) % n_lvl_streams];
 #define YGZ_FAST(SS, RR) hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce, l, nullptr)
         if (S == 36 && R == 40) YGZ_FAST(36, 40);
+#if YGZ_FAST_SHIFT
+        else if (S == 40 && R == 38) YGZ_FAST(40, 38);
+#endif
         else if (S == 40 && R == 40) YGZ_FAST(40, 40);
         else if (S == 40 && R == 48) YGZ_FAST(40, 48);
         else if (S == 40 && R == 56) YGZ_FAST(40, 56);
