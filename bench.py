@@ -47,15 +47,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-SWEEP = 240  # frames per sweep of the synthetic trajectory
-C5_FRAMES = 3682 + 3040 + 2700 + 2033 + 2273  # EuRoC MH01..MH05 (Examples/Monocular/EuRoC_TimeStamps)
-XI = np.array([0.012, -0.006, 0.009, 0.0025, -0.002, 0.0015], np.float32)  # per-frame motion (v, w)
-
-
-def sweep_index(g):
-    """Trajectory position of global frame g: 0..SWEEP and back (triangle wave)."""
-    k = g % (2 * SWEEP)
-    return k if k <= SWEEP else 2 * SWEEP - k
+from ygzfe.sequence import C5_FRAMES, XI, C5Shard, sweep_index  # noqa: E402
 
 
 def parse():
@@ -151,209 +143,25 @@ def main():
 
     W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
     n_seq = (args.frames or C5_FRAMES) if args.workload == "c5" else world * args.batch
-    b0, e0 = D.shard(n_seq, rank, world)       # this rank's frames (global indices)
-    hb, he = D.with_halo(b0, e0)               # + the halo frame whose pair (b0-1, b0) this rank aligns
-    h = b0 - hb
-    F = he - hb                                # frames extracted locally
-    n_own = e0 - b0
-    P = F - 1                                  # align / match pairs (ref p -> cur p+1)
-    maxlen = -(-n_seq // world)
-    cam = ygzfe.EUROC_CAM
-    sc = S.PlaneScene(11, W, H)
-    poses = [ygzfe.trajectory_pose(sweep_index(g), XI) for g in range(hb, he)]
-
-    batch = ygzfe.Batch((nf, sf, nl, ini, mn, 0), local, W, H, max(F, 2))
-    cap = batch.kp_cap
-    # a real stream shared by torch and ygzfe: torch's default stream is the
-    # legacy null stream (handle 0), which ygzfe reads as "the handle's own
-    # stream" and which does not order against ygzfe's non-blocking streams
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
-    sptr = stream.cuda_stream
-    kps_t = torch.empty((max(F, 2), cap, 7), dtype=torch.float32, device=dev)
-    counts_t = torch.zeros(max(F, 2), dtype=torch.int32, device=dev)
-    pyr_t = torch.zeros(max(F, 2) * batch.frame_pitch, dtype=torch.uint8, device=dev)
-    batch.bind(pyramids=pyr_t.data_ptr(), kps=kps_t.data_ptr(), counts=counts_t.data_ptr())
-
-    # the sequence rendered on the device straight into the level-0 slots
-    t_r = time.time()
-    tex_d = torch.from_numpy(sc.tex).to(dev)
-    q_d = torch.from_numpy(np.stack([q for q, _ in poses])).to(dev)
-    t_d = torch.from_numpy(np.stack([t for _, t in poses])).to(dev)
-    seeds_d = torch.arange(hb, he, dtype=torch.int64, device=dev)
-    ygzfe.render_plane_device(tex_d.data_ptr(), S.TEX_W, S.TEX_H, S.TEXEL, S.PLANE_Z, cam, q_d.data_ptr(),
-                              t_d.data_ptr(), seeds_d.data_ptr(), F, W, H, pyr_t.data_ptr(), batch.frame_pitch,
-                              noise_amp=2, stream=sptr)
-    torch.cuda.synchronize(dev)
-    render_s = time.time() - t_r
-    del tex_d
-
-    ref_idx = torch.arange(0, max(P, 1), dtype=torch.int32, device=dev)
-    cur_idx = ref_idx + 1
-    bi = torch.empty((max(P, 1), cap), dtype=torch.int32, device=dev)
-    bd = torch.empty_like(bi)
-    sd = torch.empty_like(bi)
-    xyz = torch.empty((max(P, 1), cap, 3), dtype=torch.float32, device=dev)
-    usable = torch.ones((max(P, 1), cap), dtype=torch.uint8, device=dev)
-    T_init = torch.zeros((max(P, 1), 7), dtype=torch.float32, device=dev)
-    T_init[:, 3] = 1.0
-    out = torch.zeros((max(P, 1), 45), dtype=torch.float32, device=dev)
-    # plane Z_w = 3 in each reference camera: X_c = lam * d_c, lam = (Z - C_z) / (r3 . d_c)
-    r3 = np.zeros((F, 3), np.float32)
-    cz = np.zeros(F, np.float32)
-    for i, (q, t) in enumerate(poses):
-        qi, ti = S.se3_inv(q.astype(np.float64), t.astype(np.float64))
-        R_wc = np.array([S.quat_rot(qi, e) for e in np.eye(3)]).T
-        r3[i] = R_wc[2]
-        cz[i] = ti[2]
-    r3_t = torch.from_numpy(r3).to(dev)
-    cz_t = torch.from_numpy(cz).to(dev)
-    camera = ygzfe.Camera(*cam)
-    # result slots: this rank's own frames, padded to the longest shard for the gather
-    S_b = ygzfe.slot_bytes(cap)
-    slots = torch.zeros((maxlen, S_b), dtype=torch.uint8, device=dev)
-    gathered = [torch.empty_like(slots) for _ in range(world)] if (rank == 0 and world > 1) else None
-    gather_ms = []
-
-    side = torch.cuda.Stream(dev)  # Hamming (descriptors only) runs beside SparseImgAlign (pyramids + kps)
-
-    def pack_and_gather(timed_gather=False):
-        # no align record when align did not run (P == 0 or --no-align): has_align stays 0
-        batch.pack_slots(h, n_own, out.data_ptr() if (P > 0 and not args.no_align) else 0, b0, slots.data_ptr(), S_b,
-                         sptr)
-        if world > 1:
-            if timed_gather:
-                e0_, e1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0_.record(stream)
-            dist.gather(slots, gathered, dst=0)
-            if timed_gather:
-                e1_.record(stream)
-                gather_ms.append((e0_, e1_))
-
-    def step_serial(timed_gather=False):
-        batch.extract(F, sptr)
-        if P > 0:
-            batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(),
-                        sptr)
-            if not args.no_align:
-                ygzfe.plane_points_device(kps_t.data_ptr(), cap, P, cam, r3_t.data_ptr(), cz_t.data_ptr(),
-                                          S.PLANE_Z, xyz.data_ptr(), sptr)
-                batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(),
-                                   camera, 3, 1, T_init.data_ptr(), out.data_ptr(), sptr)
-        pack_and_gather(timed_gather)
-
-    def step_tail(timed_gather=False):
-        # extraction in stage order on `stream` (each extraction kernel has the GPU to
-        # itself), then Hamming (descriptors) on `side` beside SparseImgAlign (pyramids +
-        # rows) on `stream`
-        batch.extract(F, sptr)
-        side.wait_stream(stream)
-        batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(),
-                    side.cuda_stream)
-        if not args.no_align:
-            ygzfe.plane_points_device(kps_t.data_ptr(), cap, P, cam, r3_t.data_ptr(), cz_t.data_ptr(), S.PLANE_Z,
-                                      xyz.data_ptr(), sptr)
-            batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(), camera,
-                               3, 1, T_init.data_ptr(), out.data_ptr(), sptr)
-        stream.wait_stream(side)  # the slots need the match results' descriptors in place
-        pack_and_gather(timed_gather)
-
-    def step(timed_gather=False):
-        if args.schedule == "serial" or P == 0:
-            return step_serial(timed_gather)
-        if args.schedule == "tail":
-            return step_tail(timed_gather)
-        # keypoint rows on `stream`, blur + descriptors on `side` (the blur runs
-        # beside FAST); Hamming (descriptors only) follows on `side`
-        side.wait_stream(stream)
-        batch.extract_split(F, sptr, side.cuda_stream)
-        batch.match(P, cur_idx.data_ptr(), ref_idx.data_ptr(), bi.data_ptr(), bd.data_ptr(), sd.data_ptr(),
-                    side.cuda_stream)
-        if not args.no_align:
-            ygzfe.plane_points_device(kps_t.data_ptr(), cap, P, cam, r3_t.data_ptr(), cz_t.data_ptr(), S.PLANE_Z,
-                                      xyz.data_ptr(), sptr)
-            if args.schedule == "split":
-                # a SparseImgAlign workgroup takes a whole CU (1024 threads x 128 VGPRs,
-                # 148 KB LDS): beside orient/Hamming it waits for free CUs and the
-                # overlap costs more than it hides, so it runs after them
-                stream.wait_stream(side)
-            batch.sparse_align(P, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz.data_ptr(), usable.data_ptr(), camera,
-                               3, 1, T_init.data_ptr(), out.data_ptr(), sptr)
-        stream.wait_stream(side)  # the slots need the descriptors
-        pack_and_gather(timed_gather)
-
-    # ------------------------------------------------ chunked schedule (default for N > 1)
-    # The shard in n_chunks batches bound to consecutive slices of the same device
-    # buffers (each with the frame before it, for its first align pair: that frame is
-    # extracted twice, identically).  Chunk c's slots are packed into rows [c R, ..)
-    # and gathered to rank 0 on `comm` while chunk c + 1 computes on `stream`, so only
-    # the last chunk's gather is exposed (ygzfe.dist.chunk_rows / chunk_frames;
-    # tests/test_cpu_dist.py checks the layout under gloo).
     n_chunks = args.chunks if args.chunks > 0 else (4 if world > 1 else 1)
-    chunks = []
-    comm = None
-    if n_chunks > 1:
-        maxlen_c, Rc = D.chunk_rows(n_seq, world, n_chunks)
-        slots = torch.zeros((n_chunks * Rc, S_b), dtype=torch.uint8, device=dev)
-        comm = torch.cuda.Stream(dev)
-        for c in range(n_chunks):
-            s_c, e_c, hc, nc = D.chunk_frames(n_own, h, c, Rc)
-            bt = None
-            if nc > 0:
-                bt = ygzfe.Batch((nf, sf, nl, ini, mn, 0), local, W, H, max(e_c - s_c, 2))
-                bt.bind(pyramids=pyr_t.data_ptr() + s_c * batch.frame_pitch, kps=kps_t[s_c:].data_ptr(),
-                        counts=counts_t[s_c:].data_ptr())
-            bufs = [torch.empty((Rc, S_b), dtype=torch.uint8, device=dev) for _ in range(world)] \
-                if (rank == 0 and world > 1) else None
-            chunks.append((s_c, e_c - s_c, hc, nc, bt, bufs, c * Rc))
+    t_r = time.time()
+    # the rank's whole C5 job (ygzfe/sequence.py; tests/test_gpu_c5.py runs the same object)
+    shard = C5Shard(n_seq, rank, world, dev, chunks=n_chunks, schedule=args.schedule, align=not args.no_align,
+                    scenes=S)
+    render_s = time.time() - t_r
+    torch.cuda.set_stream(shard.stream)
+    stream, sptr = shard.stream, shard.sptr
+    batch, cap = shard.batch, shard.cap
+    b0, h, F, n_own, P = shard.b0, shard.h, shard.F, shard.n_own, shard.P
+    poses, sc, r3, cz = shard.poses, shard.sc, shard.r3, shard.cz
+    pyr_t, counts_t, out = shard.pyr_t, shard.counts_t, shard.out
+    chunks, batches, F_ext = shard.chunks, shard.batches, shard.F_ext
+    S_b = shard.slot_bytes
+    gather_ms = shard.gather_ms
+    step = shard.step
+    check_all = shard.check
+    timing_all = shard.timing
 
-    def step_chunked(timed_gather=False):
-        for c, (s_c, L_c, hc, nc, bt, bufs, row0) in enumerate(chunks):
-            if nc > 0:
-                Pc = L_c - 1
-                bt.extract(L_c, sptr)
-                if Pc > 0:
-                    bt.match(Pc, cur_idx.data_ptr(), ref_idx.data_ptr(), bi[s_c:].data_ptr(), bd[s_c:].data_ptr(),
-                             sd[s_c:].data_ptr(), sptr)
-                    if not args.no_align:
-                        ygzfe.plane_points_device(kps_t[s_c:].data_ptr(), cap, Pc, cam, r3_t[s_c:].data_ptr(),
-                                                  cz_t[s_c:].data_ptr(), S.PLANE_Z, xyz[s_c:].data_ptr(), sptr)
-                        bt.sparse_align(Pc, ref_idx.data_ptr(), cur_idx.data_ptr(), xyz[s_c:].data_ptr(),
-                                        usable[s_c:].data_ptr(), camera, 3, 1, T_init[s_c:].data_ptr(),
-                                        out[s_c:].data_ptr(), sptr)
-                bt.pack_slots(hc, nc, out[s_c:].data_ptr() if (Pc > 0 and not args.no_align) else 0, b0 + row0,
-                              slots[row0:].data_ptr(), S_b, sptr)
-            if world > 1:
-                ev = torch.cuda.Event()
-                ev.record(stream)
-                comm.wait_event(ev)
-                with torch.cuda.stream(comm):
-                    if timed_gather:
-                        e0_, e1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        e0_.record(comm)
-                    dist.gather(slots[row0:row0 + Rc], bufs, dst=0)
-                    if timed_gather:
-                        e1_.record(comm)
-                        gather_ms.append((e0_, e1_))
-        if world > 1:
-            stream.wait_stream(comm)
-
-    batches = [ch[4] for ch in chunks if ch[4] is not None] if chunks else [batch]
-    F_ext = sum(ch[1] for ch in chunks if ch[3] > 0) if chunks else F
-
-    def check_all():
-        for bt in batches:
-            bt.check()
-
-    def timing_all(enable):
-        acc = {}
-        for bt in batches:
-            for k, v in bt.timing(enable).items():
-                acc[k] = acc.get(k, 0.0) + v
-        return acc
-
-    if chunks:
-        step = step_chunked  # noqa: F811 (the chunked schedule replaces the one-batch step)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -415,13 +223,7 @@ def main():
     # ------------------------------------------------ results check: rank 0 holds every frame's slot
     seq_check = None
     if rank == 0:
-        if world > 1 and chunks:
-            full = D.assemble_chunks([ch[5] for ch in chunks], n_seq, world)
-        elif world > 1:
-            full = torch.cat([gg[:D.shard(n_seq, r, world)[1] - D.shard(n_seq, r, world)[0]]
-                              for r, gg in enumerate(gathered)])
-        else:
-            full = slots[:n_own]
+        full = shard.root_slots()
         hdr = full[:, :64].contiguous().view(torch.int32).cpu().numpy()
         seq_check = {"frames_at_root": int(full.shape[0]),
                      "frame_index_ok": bool(np.array_equal(hdr[:, 10], np.arange(n_seq))),
@@ -464,10 +266,10 @@ def main():
     dom_ms = stage_ms[dom]
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
     traffic = valu_frac = None
-    tpath = os.path.join(ROOT, "profiles", "r02_traffic.json")
-    if not os.path.exists(tpath):
-        tpath = os.path.join(ROOT, "profiles", "r01_traffic.json")
-    if os.path.exists(tpath):  # PMC FETCH_SIZE x2 + WRITE_SIZE of the same kernel (tools/run_pmc.sh)
+    # the newest round's PMC pass (profiles/rNN_traffic.json)
+    tcands = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_traffic.json"))
+    tpath = os.path.join(ROOT, "profiles", tcands[-1]) if tcands else ""
+    if tpath and os.path.exists(tpath):  # PMC FETCH_SIZE x2 + WRITE_SIZE of the same kernel (tools/run_pmc.sh)
         tj = json.load(open(tpath))
         per = tj.get("per_frame", {}).get(dom)
         if per is not None:  # scaled to this launch's frame count
@@ -719,11 +521,14 @@ def latency_leg(frames, poses, sc, S, n_timed, warm=10):
             pk = kps[cur][:n_out.value].copy()
             prev = (pk, plane_xyz(S, poses[i], pk, sc.cam), np.ones(len(pk), np.uint8))
         out[mode] = (np.array(ts) * 1e3, np.array(te) * 1e3)
+    att, passed = C.c_int(), C.c_int()
+    ygzfe._check(L.ygzfe_extractor_align_probe(ex.h, C.byref(att), C.byref(passed)), "align_probe")
     ts, te = out["overlap"]
     ss, se = out["serial"]
     return {"frames": len(ts), "median_ms": round(float(np.median(ts)), 4), "p90_ms": round(float(np.percentile(ts, 90)), 4),
             "median_extract_ms": round(float(np.median(te)), 4),
             "median_align_wait_ms": round(float(np.median(ts - te)), 4),
+            "align_stream_probe": {"streams_created": att.value, "passed": passed.value},
             "serial": {"median_ms": round(float(np.median(ss)), 4),
                        "median_extract_ms": round(float(np.median(se)), 4),
                        "median_align_ms": round(float(np.median(ss - se)), 4)},

@@ -14,9 +14,17 @@
 // Gauss-Newton iterations each (iterations[], :38-43; n_iter is ignored as
 // there), return n_meas_ / 16.  getFisherInformation() = H_ / (float)(5e-4 *
 // 255 * 255) (:51-55).
+//
+// Method: NLLSSolver::optimize dispatches on method_ (NLSSolver_impl.hpp:8-13) to
+// Gauss-Newton or Levenberg-Marquardt (:95 ff).  The GPU kernel implements the
+// Gauss-Newton path Tracking uses (Tracking.cc:284 keeps the default).  An instance
+// constructed with LevenbergMarquardt refuses to run: run() logs once to stderr and
+// returns 0 (the reference's "no alignment" result, SparseImageAlign.cc:24-27)
+// instead of silently computing a different estimate.
 #ifndef YGZ_SPARSE_IMAGE_ALIGN_
 #define YGZ_SPARSE_IMAGE_ALIGN_
 
+#include <cstdio>
 #include <type_traits>
 #include <vector>
 
@@ -27,13 +35,12 @@ namespace ygz {
 
 class SparseImgAlign {
 public:
-    enum Method { GaussNewton, LevenbergMarquardt };  // NLLSSolver's methods; GN is the one run()
+    enum Method { GaussNewton, LevenbergMarquardt };  // NLLSSolver's methods (NLSSolver.h:40-43)
 
     SparseImgAlign(int n_levels, int min_level, int n_iter = 10, Method method = GaussNewton, bool display = false,
                    bool verbose = false)
-        : max_level_(n_levels), min_level_(min_level) {
+        : max_level_(n_levels), min_level_(min_level), method_(method) {
         (void)n_iter;  // iterations[] overrides it per level (SparseImageAlign.cc:38-43)
-        (void)method;
         (void)display;
         (void)verbose;
         for (int i = 0; i < 36; i++) H_[i] = 0.f;
@@ -41,6 +48,15 @@ public:
 
     template <class FrameT, class SE3T>
     size_t run(FrameT *ref_frame, FrameT *cur_frame, SE3T &TCR) {
+        if (method_ != GaussNewton) {  // NLSSolver_impl.hpp:8-13: only the GN path is on the GPU
+            static bool logged = false;
+            if (!logged) {
+                logged = true;
+                fprintf(stderr, "ygzfe SparseImgAlign: Method LevenbergMarquardt is not implemented on the GPU; "
+                                "run() returns 0 (construct with GaussNewton, as Tracking.cc:284 does)\n");
+            }
+            return 0;
+        }
         if (ref_frame->mvKeys.empty()) return 0;  // SparseImageAlign.cc:24-27
         const SE3T T_cur_from_ref = cur_frame->mTcw * ref_frame->mTcw.inverse();
         const int n = ref_frame->N;
@@ -100,6 +116,7 @@ public:
 
 protected:
     int max_level_, min_level_;
+    Method method_;
     float H_[36];
 };
 

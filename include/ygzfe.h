@@ -318,6 +318,11 @@ int ygzfe_sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, con
                              const ygzfe_kp *kps, const float *xyz_ref, const uint8_t *usable, int n,
                              int max_level, int min_level, const ygzfe_se3 *T_init);
 int ygzfe_sparse_align_end(const ygzfe_frame *cur, ygzfe_align_result *result);
+/* The align stream's hardware-queue placement probe, for audit: streams
+ * the probe created (0 before the first alignment) and whether the chosen one passed
+ * the probe (1), was taken unprobed (0: probe off, 4 rejections or its 150 ms spent),
+ * or no stream exists yet (-1). */
+int ygzfe_extractor_align_probe(ygzfe_extractor *ex, int *attempts, int *passed);
 
 /* Batched: pair p aligns frame ref_idx[p] -> cur_idx[p] of a batch, with the
  * ref frame's batch keypoints (level-0 px); d_xyz_ref [n_pairs][kp_cap][3] and
@@ -326,6 +331,18 @@ int ygzfe_batch_sparse_align(ygzfe_batch *b, int n_pairs, const int32_t *d_ref_i
                              const int32_t *d_cur_idx, const float *d_xyz_ref, const uint8_t *d_usable,
                              const ygzfe_camera *cam, int max_level, int min_level,
                              const ygzfe_se3 *d_T_init, ygzfe_align_result *d_out, void *stream);
+
+/* Thirdparty/fast's FAST-10 detector over n_roi ROIs of a host image, the segment
+ * test the DSO_KEYPOINT cells run (ORBextractor.cc:1328-1340):
+ *   variant 0: fast_corner_detect_10 (fast_10.cpp:8-3154), every pixel of the ROI;
+ *   variant 1: fast_corner_detect_10_sse2 (faster_corner_10_sse.cpp:24-202), rows
+ *              [3, h-3) x cols [3, w-3); the plain scan when w < 22.
+ * rois = (x0, y0, w, h) per ROI; every tested pixel's radius-3 ring must lie in
+ * the image (EINVAL otherwise: the reference reads out of bounds there).  Corners
+ * in the reference's order (raster), ROI-relative like its fast_xy: xy[r][cap][2];
+ * counts[r] = corners found (ECAP if any exceeds cap; the first cap are written). */
+int ygzfe_fast10_detect(int device, const uint8_t *img, int width, int height, int stride, const int32_t *rois,
+                        int n_roi, int barrier, int variant, int16_t *xy, int cap, int32_t *counts);
 
 /* ------------------------------------------------------------------------ */
 /* Align2D / FindDirectProjection (Align.h:20-26, ORBmatcher.cc:1573-1602)   */

@@ -15,6 +15,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels.hpp"
@@ -146,31 +147,59 @@ struct HostBuf {
 
 static inline size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
 
-// Host entry points without a handle (Hamming, RGB-D depth lookup): one staging
-// area per calling thread and device, kept for the thread's lifetime -- its own
-// non-blocking stream, a device buffer and pinned in / out buffers that only
-// grow -- so a call is one packed H2D, the launches, one packed D2H and one
-// stream synchronisation (no allocation, no device-wide synchronisation).
+// Host entry points without a handle (Hamming, RGB-D depth lookup, Align2D on a host
+// image, FAST-10 ROIs): a call leases a staging area from a process-wide pool per
+// device -- its own non-blocking stream, a device buffer and pinned in / out buffers
+// that only grow -- and returns it when the call ends, so a call is one packed H2D,
+// the launches, one packed D2H and one stream synchronisation (no allocation, no
+// device-wide synchronisation).  The pool holds as many areas as calls ever ran at
+// once, whatever the number of threads that come and go (no per-thread leak).
 struct CallStaging {
     hipStream_t stream = nullptr;
     DevBuf dev;
     HostBuf hin, hout;
 };
-static int call_staging(int device, CallStaging **out) {
-    static thread_local std::map<int, CallStaging *> per_device;  // never freed: lives with the thread
-    CallStaging *&S = per_device[device];
-    if (!S) {
-        S = new CallStaging();
-        if (hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) != hipSuccess) {
-            delete S;
-            S = nullptr;
+static std::mutex &staging_mutex() {
+    static std::mutex mu;
+    return mu;
+}
+static std::map<int, std::vector<CallStaging *>> &staging_free() {
+    static auto *pool = new std::map<int, std::vector<CallStaging *>>();  // lives with the process
+    return *pool;
+}
+struct StagingLease {
+    CallStaging *s = nullptr;
+    int device = -1;
+    StagingLease() = default;
+    StagingLease(const StagingLease &) = delete;
+    StagingLease &operator=(const StagingLease &) = delete;
+    ~StagingLease() {
+        if (!s) return;
+        std::lock_guard<std::mutex> lk(staging_mutex());
+        staging_free()[device].push_back(s);
+    }
+    CallStaging *operator->() const { return s; }
+    int acquire(int dev) {
+        device = dev;
+        {
+            std::lock_guard<std::mutex> lk(staging_mutex());
+            std::vector<CallStaging *> &fl = staging_free()[dev];
+            if (!fl.empty()) {
+                s = fl.back();
+                fl.pop_back();
+                return YGZFE_OK;
+            }
+        }
+        CallStaging *n = new CallStaging();
+        if (hipStreamCreateWithFlags(&n->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete n;
             set_error("hipStreamCreate failed");
             return YGZFE_EHIP;
         }
+        s = n;
+        return YGZFE_OK;
     }
-    *out = S;
-    return YGZFE_OK;
-}
+};
 
 #define YGZ_TRY(x)                          \
     do {                                    \
@@ -298,8 +327,8 @@ struct ygzfe_extractor {
         if (e == hipSuccess) {
             const auto t0 = std::chrono::steady_clock::now();
             while (hipEventQuery(eb) == hipErrorNotReady &&
-                   std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(50)) {
-            }
+                   std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(50))
+                std::this_thread::yield();
             beside = hipEventQuery(eb) == hipSuccess && hipEventQuery(ea) == hipErrorNotReady;
         }
         (void)hipStreamSynchronize(stream);
@@ -325,6 +354,9 @@ struct ygzfe_extractor {
         const bool probe = !(pe && pe[0] == '0');
         std::vector<hipStream_t> rejected;
         int rc = YGZFE_OK;
+        // at most 4 probes and 150 ms in all (another thread's work on the GPU can make
+        // good candidates fail); then the next stream is taken unprobed
+        const auto t_start = std::chrono::steady_clock::now();
         for (int attempt = 0; rc == YGZFE_OK && !astream; attempt++) {
             hipStream_t s = nullptr;
             if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
@@ -333,15 +365,22 @@ struct ygzfe_extractor {
                 break;
             }
             bool beside = true;
-            if (probe && attempt < 4) rc = probe_beside(s, beside);
-            if (rc == YGZFE_OK && beside) astream = s;
-            else rejected.push_back(s);
+            const bool in_budget = std::chrono::steady_clock::now() - t_start < std::chrono::milliseconds(150);
+            const bool probed = probe && attempt < 4 && in_budget;
+            if (probed) rc = probe_beside(s, beside);
+            if (rc == YGZFE_OK && beside) {
+                astream = s;
+                align_probe_beside = probed ? 1 : 0;
+            } else {
+                rejected.push_back(s);
+            }
             align_probe_attempts = attempt + 1;
         }
         for (hipStream_t s : rejected) (void)hipStreamDestroy(s);
         return rc;
     }
-    int align_probe_attempts = 0;
+    int align_probe_attempts = 0;  // streams created by the placement probe (0: no align yet)
+    int align_probe_beside = -1;   // 1: the align stream passed the probe; 0: taken unprobed
     // work about to rewrite a pyramid on `st` waits for the alignment reading it
     int order_after_align(hipStream_t st) {
         if (align_pending) YGZ_HIP(hipStreamWaitEvent(st, ev_align_done, 0));
@@ -574,9 +613,15 @@ int ygzfe_frame_create(ygzfe_extractor *ex, int width, int height, ygzfe_frame *
 
 void ygzfe_frame_destroy(ygzfe_frame *f) {
     if (!f) return;
-    std::lock_guard<std::recursive_mutex> lk(graph_mutex());
     (void)hipSetDevice(f->ex->device);
-    (void)hipStreamSynchronize(f->ex->stream);
+    {
+        // an alignment in flight (ygzfe_sparse_align_begin, on ex->astream) may read this
+        // frame's pyramid: wait for it (its result stays staged for _end)
+        std::lock_guard<std::mutex> lk(f->ex->mu);
+        if (f->ex->align_pending) (void)hipEventSynchronize(f->ex->ev_align_done);
+        (void)hipStreamSynchronize(f->ex->stream);
+    }
+    std::lock_guard<std::recursive_mutex> lk(graph_mutex());
     delete f;
 }
 
@@ -1233,8 +1278,8 @@ int ygzfe_hamming_best2(int device, const uint8_t *query, int nq, const uint8_t 
     }
     if (nq == 0) return YGZFE_OK;
     YGZ_TRY(ensure_device(device));
-    CallStaging *S;
-    YGZ_TRY(call_staging(device, &S));
+    StagingLease S;
+    YGZ_TRY(S.acquire(device));
     // in: [query][train]  out: [best_idx][best_dist][second_dist]
     const size_t o_t = align16((size_t)nq * 32), in_bytes = o_t + align16((size_t)(nt > 0 ? nt : 1) * 32);
     const size_t out_bytes = (size_t)nq * 12;
@@ -1266,8 +1311,8 @@ int ygzfe_hamming_csr(int device, const uint8_t *query, int nq, const uint8_t *t
     for (int k = 0; k < nc; k++)
         if (cand[k] < 0 || cand[k] >= nt) { set_error("candidate index %d out of range", cand[k]); return YGZFE_EINVAL; }
     YGZ_TRY(ensure_device(device));
-    CallStaging *S;
-    YGZ_TRY(call_staging(device, &S));
+    StagingLease S;
+    YGZ_TRY(S.acquire(device));
     // in: [query][train][row_ptr][cand]  out: [dist]
     const size_t o_t = align16((size_t)nq * 32), o_r = o_t + align16((size_t)nt * 32);
     const size_t o_c = o_r + align16((size_t)(nq + 1) * 4), in_bytes = o_c + align16((size_t)nc * 4);
@@ -1378,6 +1423,14 @@ int ygzfe_sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, con
     YGZ_HIP(hipMemcpyAsync(ex->ahout.p, ex->align_out.p, sizeof(ygzfe_align_result), hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipEventRecord(ex->ev_align_done, st));
     ex->align_pending = true;
+    return YGZFE_OK;
+}
+
+int ygzfe_extractor_align_probe(ygzfe_extractor *ex, int *attempts, int *passed) {
+    if (!ex) { set_error("invalid argument"); return YGZFE_EINVAL; }
+    std::lock_guard<std::mutex> lk(ex->mu);
+    if (attempts) *attempts = ex->align_probe_attempts;
+    if (passed) *passed = ex->align_probe_beside;
     return YGZFE_OK;
 }
 
@@ -1492,16 +1545,61 @@ extern "C" int ygzfe_align2d_batch(const ygzfe_frame *cur, int level, int n, con
     return YGZFE_OK;
 }
 
+// FAST-10 (Thirdparty/fast) over host-image ROIs: the whole image and the ROI table
+// go up in one DMA, one workgroup per ROI, the corner lists come back in one.
+extern "C" int ygzfe_fast10_detect(int device, const uint8_t *img, int width, int height, int stride,
+                                   const int32_t *rois, int n_roi, int barrier, int variant, int16_t *xy, int cap,
+                                   int32_t *counts) {
+    if (!img || width <= 0 || height <= 0 || stride < width || n_roi < 0 || (n_roi > 0 && (!rois || !counts)) ||
+        cap < 0 || (cap > 0 && !xy) || (variant != 0 && variant != 1) || barrier < 0) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    for (int r = 0; r < n_roi; r++) {
+        const int x0 = rois[4 * r], y0 = rois[4 * r + 1], w = rois[4 * r + 2], h = rois[4 * r + 3];
+        if (w < 0 || h < 0) { set_error("roi %d: negative size", r); return YGZFE_EINVAL; }
+        // the tested pixels (the whole ROI for the plain scan, its [3, -3) interior for SSE2
+        // when w >= 22) with their radius-3 rings
+        const int in = (variant == 1 && w >= 22) ? 3 : 0;
+        if (w - 2 * in <= 0 || h - 2 * in <= 0) continue;
+        if (x0 + in - 3 < 0 || y0 + in - 3 < 0 || x0 + w - in + 3 > width || y0 + h - in + 3 > height) {
+            set_error("roi %d (%d, %d, %d, %d): the segment test would read outside the %dx%d image", r, x0, y0, w,
+                      h, width, height);
+            return YGZFE_EINVAL;
+        }
+    }
+    if (n_roi == 0) return YGZFE_OK;
+    YGZ_TRY(ensure_device(device));
+    StagingLease S;
+    YGZ_TRY(S.acquire(device));
+    // in: [image][rois]  out: [counts][xy]
+    const size_t img_b = (size_t)stride * height, o_r = align16(img_b), in_bytes = o_r + align16((size_t)n_roi * 16);
+    const size_t o_xy = align16((size_t)n_roi * 4), out_bytes = o_xy + (size_t)n_roi * cap * 4;
+    YGZ_TRY(S->hin.ensure(in_bytes));
+    YGZ_TRY(S->hout.ensure(out_bytes));
+    YGZ_TRY(S->dev.ensure(in_bytes + out_bytes));
+    uint8_t *h = S->hin.as<uint8_t>(), *d = S->dev.as<uint8_t>();
+    memcpy(h, img, img_b);
+    memcpy(h + o_r, rois, (size_t)n_roi * 16);
+    YGZ_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, S->stream));
+    int32_t *dc = reinterpret_cast<int32_t *>(d + in_bytes);
+    int16_t *dxy = reinterpret_cast<int16_t *>(d + in_bytes + o_xy);
+    YGZ_HIP(launch_fast10_rois(d, stride, reinterpret_cast<const int *>(d + o_r), n_roi, barrier, variant, dxy, cap,
+                               dc, S->stream));
+    YGZ_HIP(hipMemcpyAsync(S->hout.p, dc, out_bytes, hipMemcpyDeviceToHost, S->stream));
+    YGZ_HIP(hipStreamSynchronize(S->stream));
+    memcpy(counts, S->hout.p, (size_t)n_roi * 4);
+    if (cap > 0) memcpy(xy, S->hout.as<uint8_t>() + o_xy, (size_t)n_roi * cap * 4);
+    for (int r = 0; r < n_roi; r++)
+        if (counts[r] > cap) {
+            set_error("roi %d: %d corners > cap %d", r, counts[r], cap);
+            return YGZFE_ECAP;
+        }
+    return YGZFE_OK;
+}
+
 // Align2D(const cv::Mat& cur_img, ...) on a host image: the 48 x 48 window around
 // the estimate goes up (the whole image only when the iterations walk out of it).
-namespace {
-struct Align2DStaging {
-    int device = -1;
-    hipStream_t stream = nullptr;
-    DevBuf buf;
-};
-}  // namespace
-
 extern "C" int ygzfe_align2d_image(int device, const uint8_t *img, int w, int h, int stride,
                                    const uint8_t *patch_with_border, const uint8_t *patch, int n_iter, float *px,
                                    uint8_t *converged) {
@@ -1510,14 +1608,8 @@ extern "C" int ygzfe_align2d_image(int device, const uint8_t *img, int w, int h,
         return YGZFE_EINVAL;
     }
     YGZ_TRY(ensure_device(device));
-    // one staging area per thread and device, kept for the process lifetime
-    static thread_local std::map<int, Align2DStaging *> staging;
-    Align2DStaging *&S = staging[device];
-    if (!S) {
-        S = new Align2DStaging();
-        S->device = device;
-        YGZ_HIP(hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking));
-    }
+    StagingLease S;
+    YGZ_TRY(S.acquire(device));
     hipStream_t st = S->stream;
     const size_t small = 256;  // pwb 100 | p 64 | px 8 | status 4
     uint8_t host_small[small];
@@ -1537,8 +1629,8 @@ extern "C" int ygzfe_align2d_image(int device, const uint8_t *img, int w, int h,
             ww = std::min(cu + half, w) - x0;
             wh = std::min(cv + half, h) - y0;
         }
-        YGZ_TRY(S->buf.ensure(small + (size_t)ww * wh));
-        uint8_t *d = S->buf.as<uint8_t>();
+        YGZ_TRY(S->dev.ensure(small + (size_t)ww * wh));
+        uint8_t *d = S->dev.as<uint8_t>();
         YGZ_HIP(hipMemcpyAsync(d, host_small, 172, hipMemcpyHostToDevice, st));
         YGZ_HIP(hipMemcpy2DAsync(d + small, ww, img + (size_t)y0 * stride + x0, stride, ww, wh,
                                  hipMemcpyHostToDevice, st));
@@ -1865,8 +1957,8 @@ extern "C" int ygzfe_stereo_from_rgbd(int device, const float *im_depth, int wid
     }
     if (n == 0) return YGZFE_OK;
     YGZ_TRY(ensure_device(device));
-    CallStaging *S;
-    YGZ_TRY(call_staging(device, &S));
+    StagingLease S;
+    YGZ_TRY(S.acquire(device));
     // in: [depth image][kps]  out: [u_right][depth]
     const size_t img = 4 * (size_t)stride * height, o_k = align16(img);
     const size_t in_bytes = o_k + align16(sizeof(ygzfe_kp) * (size_t)n), out_bytes = 8 * (size_t)n;
@@ -2370,6 +2462,10 @@ struct ygzfe_match_frame {
     DevBuf in, out, scratch;
     HostBuf hin, hout, hset;
     hipEvent_t ev_in = nullptr, ev_set = nullptr;
+    // recorded on `stream` once the frame's keypoints, descriptors and grid are on the
+    // device: a search on another frame's stream that reads this frame's descriptors as
+    // its queries (SearchForInitialization, SearchByBoW) waits for it
+    hipEvent_t ev_ready = nullptr;
 };
 
 namespace {
@@ -2396,7 +2492,10 @@ int match_frame_finish(ygzfe_match_frame *f, const ygzfe_bounds *bounds) {
     YGZ_HIP(launch_match_cells(f->kps.as<ygzfe_kp>(), f->n, bounds->min_x, bounds->min_y, f->inv_w, f->inv_h,
                                f->cell.as<int32_t>(), f->cell.as<int32_t>() + f->n,
                                reinterpret_cast<uint16_t *>(f->cell.as<int32_t>() + f->n + kMatchCells), f->stream));
-    // no synchronisation: every search runs on f->stream after the grid
+    // no host synchronisation: a search on this frame runs on f->stream after the grid;
+    // one that reads this frame's descriptors from another stream waits on ev_ready
+    if (!f->ev_ready) YGZ_HIP(hipEventCreateWithFlags(&f->ev_ready, hipEventDisableTiming));
+    YGZ_HIP(hipEventRecord(f->ev_ready, f->stream));
     return YGZFE_OK;
 }
 
@@ -2407,6 +2506,7 @@ struct MatchCall {
     std::vector<ygzfe_match_query> q;
     const uint8_t *qdesc_host = nullptr;  // [n_qdesc][32] (host) or
     const uint8_t *qdesc_dev = nullptr;   // device descriptors (INIT / BoW: a match frame's)
+    const ygzfe_match_frame *qframe = nullptr;  // the match frame that owns qdesc_dev
     int n_qdesc = 0;
     std::vector<int32_t> qid, cand_ptr;
     const int32_t *cand_host = nullptr;
@@ -2429,6 +2529,8 @@ int run_match(MatchCall &c) {
     }
     YGZ_TRY(ensure_device(f->device));
     hipStream_t st = f->stream;
+    // query descriptors of another match frame: uploaded on that frame's stream
+    if (c.qframe && c.qframe != f && c.qframe->ev_ready) YGZ_HIP(hipStreamWaitEvent(st, c.qframe->ev_ready, 0));
     // device input layout
     Arena ai;
     const size_t o_q = ai.take(sizeof(ygzfe_match_query) * (size_t)std::max(nq, 1));
@@ -2535,6 +2637,7 @@ extern "C" void ygzfe_match_frame_destroy(ygzfe_match_frame *f) {
     if (f->stream) (void)hipStreamSynchronize(f->stream), (void)hipStreamDestroy(f->stream);
     if (f->ev_in) (void)hipEventDestroy(f->ev_in);
     if (f->ev_set) (void)hipEventDestroy(f->ev_set);
+    if (f->ev_ready) (void)hipEventDestroy(f->ev_ready);
     delete f;
 }
 
@@ -2570,6 +2673,10 @@ extern "C" int ygzfe_match_frame_set(ygzfe_match_frame *f, const ygzfe_kp *kps, 
     if (n) {  // keypoints, descriptors (and u_right) through page-locked staging: async DMAs
         const size_t kb = sizeof(ygzfe_kp) * (size_t)n, db = (size_t)32 * n, ub = u_right ? sizeof(float) * n : 0;
         if (f->ev_set) YGZ_HIP(hipEventSynchronize(f->ev_set));  // the previous frame's DMA out of hset
+        // test hook (tests/test_gpu_match_search.py): hold this frame's stream before its
+        // upload, so a search on another frame's stream that skipped the ev_ready wait
+        // would read descriptors that are not there yet
+        if (const char *hold = getenv("YGZFE_DEBUG_SET_HOLD_US")) YGZ_HIP(launch_hold_us(atoi(hold), f->stream));
         YGZ_TRY(f->hset.ensure(kb + db + ub));
         uint8_t *hs = f->hset.as<uint8_t>();
         memcpy(hs, kps, kb);
@@ -2605,7 +2712,11 @@ extern "C" int ygzfe_match_frame_from_batch(ygzfe_match_frame *f, ygzfe_batch *b
         YGZ_HIP(hipMemcpyAsync(f->host_kps.data(), f->kps.p, sizeof(ygzfe_kp) * n, hipMemcpyDeviceToHost, f->stream));
     }
     f->has_uright = false;
-    return match_frame_finish(f, bounds);
+    YGZ_TRY(match_frame_finish(f, bounds));
+    // host_kps (read by the host when this frame is a SearchForInitialization / BoW query
+    // frame) arrives by the async D2H above
+    YGZ_HIP(hipStreamSynchronize(f->stream));
+    return YGZFE_OK;
 }
 
 extern "C" int ygzfe_search_projection_best(ygzfe_match_frame *cur, const ygzfe_match_query *q, const uint8_t *q_desc,
@@ -2676,6 +2787,7 @@ extern "C" int ygzfe_search_for_initialization(ygzfe_match_frame *F1, ygzfe_matc
         Q.flags = kp.octave > 0 ? 0 : YGZFE_MQ_VALID;
     }
     c.qdesc_dev = F1->desc.as<uint8_t>();
+    c.qframe = F1;
     c.mode = YGZFE_MATCH_INIT;
     c.nnratio = nnratio;
     c.check_ori = check_ori;
@@ -2737,6 +2849,7 @@ extern "C" int ygzfe_search_by_bow(ygzfe_match_frame *kf, ygzfe_match_frame *F, 
     c.n_cand = n_cand;
     if (c.cand_ptr.empty()) c.cand_ptr.assign(2, 0);  // BoW mode even with no query
     c.qdesc_dev = kf->desc.as<uint8_t>();
+    c.qframe = kf;
     c.mode = YGZFE_MATCH_BOW;
     c.nnratio = nnratio;
     c.check_ori = check_ori;

@@ -217,4 +217,64 @@ hipError_t launch_dso_finish2(const uint32_t *keys, const int *cnt, int ncells, 
     return hipGetLastError();
 }
 
+// Thirdparty/fast's fast_corner_detect_10 / _sse2 over caller ROIs (roi = x0, y0, w, h),
+// the same segment test (fast10_corner) the DSO cells run.  Scan region per ROI:
+// plain (variant 0) every pixel of the ROI (fast_10.cpp:35-42); SSE2 (variant 1)
+// rows [3, h-3) x cols [3, w-3), a plain scan when w < 22 and nothing when h < 7
+// (faster_corner_10_sse.cpp:24-202).  One 256-thread workgroup per ROI walks the
+// region in raster order and appends corners in that order (the reference's
+// vector order); counts may exceed cap (only the first cap are written).
+__global__ __launch_bounds__(256) void k_fast10_rois(const uint8_t *__restrict__ img, int stride,
+                                                     const int *__restrict__ rois, int barrier, int variant,
+                                                     int16_t *__restrict__ out_xy, int cap,
+                                                     int *__restrict__ counts) {
+    __shared__ int s_wave[4];
+    const int r = blockIdx.x;
+    const int x0 = rois[4 * r], y0 = rois[4 * r + 1], w = rois[4 * r + 2], h = rois[4 * r + 3];
+    int lo_x = 0, hi_x = w, lo_y = 0, hi_y = h;
+    if (variant == 1 && w >= 22) {
+        lo_x = 3, hi_x = w - 3, lo_y = 3, hi_y = h - 3;
+        if (h < 7) hi_y = lo_y;
+    }
+    const int span = hi_x > lo_x ? hi_x - lo_x : 0;
+    const int rows = hi_y > lo_y ? hi_y - lo_y : 0;
+    const int total = span * rows;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int base = 0;
+    for (int i0 = 0; i0 < total; i0 += 256) {
+        const int i = i0 + threadIdx.x;
+        int cx = 0, cy = 0;
+        bool c = false;
+        if (i < total) {
+            cy = lo_y + i / span;
+            cx = lo_x + i % span;
+            c = fast10_corner(img + (size_t)(y0 + cy) * stride + (x0 + cx), stride, barrier);
+        }
+        const uint64_t m = __ballot(c);
+        if (lane == 0) s_wave[wv] = __popcll(m);
+        __syncthreads();
+        int before = 0;
+        for (int k = 0; k < wv; k++) before += s_wave[k];
+        const int n_blk = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+        if (c) {
+            const int pos = base + before + __popcll(m & ((1ull << lane) - 1ull));
+            if (pos < cap) {
+                out_xy[((size_t)r * cap + pos) * 2] = (int16_t)cx;
+                out_xy[((size_t)r * cap + pos) * 2 + 1] = (int16_t)cy;
+            }
+        }
+        base += n_blk;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) counts[r] = base;
+}
+
+hipError_t launch_fast10_rois(const uint8_t *img, int stride, const int *rois, int n_rois, int barrier,
+                              int variant, int16_t *out_xy, int cap, int *counts, hipStream_t st) {
+    if (n_rois <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fast10_rois, dim3(n_rois), dim3(256), 0, st, img, stride, rois, barrier, variant, out_xy,
+                       cap, counts);
+    return hipGetLastError();
+}
+
 }  // namespace ygzfe

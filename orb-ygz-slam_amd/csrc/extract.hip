@@ -4,7 +4,7 @@
 // pyramid          ORBextractor.cc:1129-1150               k_resize_area2 / k_resize_linear
 // blur 7x7 s=2     ORBextractor.cc:1079-1084               k_blur7
 // FAST-9 per cell  ORBextractor.cc:747-781 (+cv::FAST)     k_fast_cells
-// octree           ORBextractor.cc:533-723, 783-798        k_octree<NODE_CAP>
+// octree           ORBextractor.cc:533-723, 783-798        k_octree_sort / k_octree_list
 // angle + rBRIEF   ORBextractor.cc:77-149, 1101-1125       k_orient_desc / k_desc_existing
 //
 // Everything is batched over frames (grid.z / grid.y = frame) so one launch per
@@ -244,9 +244,6 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 #define YGZ_BLUR_AHEAD 10  // rows in flight per wave
 #endif
 constexpr int kBlurAhead = YGZ_BLUR_AHEAD;
-#ifndef YGZ_BLUR_ROLLED
-#define YGZ_BLUR_ROLLED 0  // rolled by the prefetch period: 88 -> 33 KB of code, but 2 % slower
-#endif
 
 __device__ __forceinline__ void blur_hsum(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t o,
                                           uint32_t ka, uint32_t kb, uint32_t h[4]) {
@@ -346,22 +343,10 @@ __device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ s
     const bool store_lane = x < w;
     uint32_t prv[4] = {0u, 0u, 0u, 0u};  // row sums of the previous row
     uint32_t pr[5][4];                   // pr[m]: (row n-5+m-1, row n-5+m) packed, m = 0..4
-#if YGZ_BLUR_ROLLED
-    // rows in blocks of kBlurAhead (the prefetch ring's period): the body is unrolled
-    // only that far, so the kernel stays inside the instruction cache
-    for (int r0 = 0; r0 < kBlurRows + 6; r0 += kBlurAhead)
-#pragma unroll
-    for (int i = 0; i < kBlurAhead; i++) {
-        const int r = r0 + i;
-        if (r >= kBlurRows + 6) break;
-        Row cur = buf[i];
-        if (r + kBlurAhead < kBlurRows + 6) fetch(r + kBlurAhead, buf[i]);
-#else
 #pragma unroll
     for (int r = 0; r < kBlurRows + 6; r++) {
         Row cur = buf[r % kBlurAhead];
         if (r + kBlurAhead < kBlurRows + 6) fetch(r + kBlurAhead, buf[r % kBlurAhead]);
-#endif
         uint32_t am1 = (uint32_t)__builtin_amdgcn_update_dpp((int)cur.halo, (int)cur.a, 0x138, 0xF, 0xF, false);
         if (right_edge) {
             if (fix_r) cur.a = __builtin_amdgcn_perm(cur.a, am1, 0x03000102u);
@@ -463,20 +448,10 @@ __global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(const uint8_t *__re
         for (int r = 0; r < kBlurAhead; r++) fetch(r, buf[r]);
         const bool active = x < w;
         uint32_t ring[7][4];
-#if YGZ_BLUR_ROLLED
-        for (int r0 = 0; r0 < kBlurRows + 6; r0 += kBlurAhead)
-#pragma unroll
-        for (int i = 0; i < kBlurAhead; i++) {
-            const int r = r0 + i;
-            if (r >= kBlurRows + 6) break;
-            const BlurRow cur = buf[i];
-            if (r + kBlurAhead < kBlurRows + 6) fetch(r + kBlurAhead, buf[i]);
-#else
 #pragma unroll
         for (int r = 0; r < kBlurRows + 6; r++) {
             const BlurRow cur = buf[r % kBlurAhead];
             if (r + kBlurAhead < kBlurRows + 6) fetch(r + kBlurAhead, buf[r % kBlurAhead]);
-#endif
             // A[l-1], A[l], A[l+1], A[l+2] (row dwords around the lane's own)
             const uint32_t hl = __builtin_amdgcn_readlane(cur.halo, 0);
             const uint32_t hr1 = __builtin_amdgcn_readlane(cur.halo, 1), hr2 = __builtin_amdgcn_readlane(cur.halo, 2);
@@ -928,38 +903,7 @@ static size_t fast_cells_lds_bytes(int S, int R) {
 }
 
 // ---------------------------------------------------------------------------
-// Octree distribution (DistributeOctTree, ORBextractor.cc:533-723 with
-// ExtractorNode::DivideNode :479-531), one 256-thread workgroup per
-// (frame, level), level-synchronous.
-//
-// The reference walks a std::list and divides one node at a time, pushing the
-// non-empty children (n1..n4) to the front.  One walk of the main loop (:593-635)
-// therefore yields   [children of the last divided node, n4..n1] ... [children of
-// the first divided node, n4..n1] ++ [undivided nodes in their old order],
-// and the children are created (= the std::sort pointer tie-break, :656, taken
-// as creation order like oracle/orb.c) in division order, n1..n4.  The same
-// holds for one round of the final loop (:648-672), whose division order is the
-// (size, creation) descending sort and which stops at the first division that
-// makes size >= N: a prefix sum over the sorted candidates finds that cut.
-// So every pass is: quadrant histogram of the keys of the dividing nodes (LDS
-// atomics), prefix sums over nodes for the new list positions and creation
-// numbers, then every key relabels itself with its new node's list position.
-// Keys never move: a node's keys are the keys carrying its label, in candidate
-// order, so the retained key (:700-716, first maximum response) is the
-// max of (score << 24 | (0xFFFFFF - candidate index)).
-
-template <int NC>
-struct OctLds {
-    uint64_t bnd[2][NC];  // x0 | y0 << 16 | x1 << 32 | y1 << 48, list order
-    uint32_t cnt[2][NC];
-    uint32_t seq[2][NC];  // creation number; bit 31: created with > 1 key by the last pass
-    uint32_t cq[NC][2];   // quadrant key counts (u16 pairs); best key at the end
-    uint32_t mid[NC];     // mx | my << 12 | hist << 30 | div << 31
-    uint32_t remap[NC];   // div << 31 | non-empty quadrant mask << 16 | position
-    uint64_t sortk[NC];   // final-round candidates: cnt << 48 | seq << 16 | node
-    int red[16];
-    int scal[8];
-};
+// Wave / workgroup scans shared by the octree kernels below.
 
 // Inclusive wave scan on DPP: Hillis-Steele inside each 16-lane row
 // (row_shr:1,2,4,8; lanes shifted in from outside the row add 0), then
@@ -994,421 +938,9 @@ __device__ __forceinline__ int block_excl_scan(int v, int *red, int *total) {
     return off + incl - v;
 }
 
-// Runs of equal values across the lanes of a wave (lane order): the run's first
-// lane gets its length, every other lane 0.
-__device__ __forceinline__ int wave_run_length(int t) {
-    const int lane = lane_id();
-    const int prev = __shfl_up(t, 1, 64);
-    const uint64_t heads = __ballot(lane == 0 || prev != t);
-    if (!((heads >> lane) & 1)) return 0;
-    const uint64_t above = lane == 63 ? 0ull : heads >> (lane + 1);
-    return above ? __builtin_ctzll(above) + 1 : 64 - lane;
-}
-
-// The same, with the maximum of v over the run delivered to its first lane.
-__device__ __forceinline__ int wave_run_max(int t, uint32_t v, uint32_t &m) {
-    const int lane = lane_id();
-    const int prev = __shfl_up(t, 1, 64);
-    const uint64_t heads = __ballot(lane == 0 || prev != t);
-    const uint64_t above = lane == 63 ? 0ull : heads >> (lane + 1);
-    const int next = above ? lane + 1 + __builtin_ctzll(above) : 64;  // first lane of the next run
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t w = __shfl_down(v, o, 64);
-        if (lane + o < next) v = v > w ? v : w;
-    }
-    m = v;
-    return ((heads >> lane) & 1) ? next - lane : 0;
-}
-
-__device__ __forceinline__ int oct_quadrant(uint32_t key, uint32_t mid) {
-    const int mx = (int)(mid & 0xFFFu), my = (int)((mid >> 12) & 0xFFFu);
-    return (key_x(key) < mx ? 0 : 1) + (key_y(key) < my ? 0 : 2);
-}
-
-__device__ __forceinline__ int quad_count(const uint32_t c[2], int q) {
-    return (int)((c[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu);
-}
-
-template <int NC, int NT>
-__device__ __forceinline__ void octree_pass(OctLds<NC> &S, const uint32_t *K, uint16_t *nid, int n, int N,
-                                            bool final_round, int &cur, int &size, int &seqc, int &nexpand,
-                                            int &overflow) {
-    const int tid = threadIdx.x;
-    // a) which nodes get their keys histogrammed: dividing nodes (main loop) or
-    //    the final-round candidates (vSizeAndPointerToNode of the last pass)
-    for (int i = tid; i < size; i += NT) {
-        const uint64_t b = S.bnd[cur][i];
-        const int x0 = (int)(b & 0xFFFF), y0 = (int)((b >> 16) & 0xFFFF);
-        const int x1 = (int)((b >> 32) & 0xFFFF), y1 = (int)(b >> 48);
-        const int mx = x0 + (int)ceilf((float)(x1 - x0) / 2), my = y0 + (int)ceilf((float)(y1 - y0) / 2);
-        const bool hist = final_round ? (S.seq[cur][i] >> 31) != 0 : S.cnt[cur][i] > 1;
-        S.mid[i] = (uint32_t)mx | ((uint32_t)my << 12) | ((uint32_t)hist << 30) | ((uint32_t)(hist && !final_round) << 31);
-        S.cq[i][0] = 0u;
-        S.cq[i][1] = 0u;
-    }
-    __syncthreads();
-    // Keys come in cell order, so neighbouring lanes mostly hit the same (node,
-    // quadrant) counter: one LDS atomic per run of equal targets, by its first lane,
-    // instead of one same-address atomic per key.
-    for (int j0 = tid - (tid & 63); j0 < n; j0 += NT) {
-        const int j = j0 + (tid & 63);
-        int t = -1;
-        if (j < n) {
-            const int i = nid[j];
-            const uint32_t md = S.mid[i];
-            if (md & (1u << 30)) t = (i << 2) | oct_quadrant(K[j], md);
-        }
-        const int run_len = wave_run_length(t);
-        if (run_len > 0 && t >= 0) atomicAdd(&S.cq[t >> 2][(t & 3) >> 1], (uint32_t)run_len << ((t & 1) * 16));
-    }
-    __syncthreads();
-    // b) division order -> E (children created before this node's), Ctot
-    int ctot = 0;
-    if (!final_round) {
-        int carry = 0;
-        for (int i0 = 0; i0 < size; i0 += NT) {
-            const int i = i0 + tid;
-            int e = 0;
-            bool div = false;
-            if (i < size) {
-                div = (S.mid[i] >> 31) != 0;
-                if (div) {
-                    const uint32_t c[2] = {S.cq[i][0], S.cq[i][1]};
-                    e = (quad_count(c, 0) > 0) + (quad_count(c, 1) > 0) + (quad_count(c, 2) > 0) + (quad_count(c, 3) > 0);
-                }
-            }
-            int tot;
-            const int ex = block_excl_scan<NT>(e, S.red, &tot);
-            if (div) S.remap[i] = (uint32_t)(carry + ex);
-            carry += tot;
-        }
-        ctot = carry;
-    } else {
-        // candidates, list order -> sortk, then ascending sort; division order is descending
-        int nc = 0;
-        for (int i0 = 0; i0 < size; i0 += NT) {
-            const int i = i0 + tid;
-            const bool cand = i < size && (S.mid[i] & (1u << 30));
-            int tot;
-            const int ex = block_excl_scan<NT>(cand ? 1 : 0, S.red, &tot);
-            if (cand)
-                S.sortk[nc + ex] = ((uint64_t)S.cnt[cur][i] << 48) | ((uint64_t)(S.seq[cur][i] & 0x7FFFFFFFu) << 16) |
-                                   (uint64_t)i;
-            nc += tot;
-        }
-        // ascending order by rank: the keys are distinct (creation numbers are), so
-        // rank = number of smaller keys; every lane reads the same sortk[j] (LDS
-        // broadcast) -- one barrier instead of a bitonic network's log^2 stages
-        __syncthreads();
-        constexpr int kPer = (NC + NT - 1) / NT;
-        uint64_t mine[kPer];
-        int rk[kPer];
-#pragma unroll
-        for (int u = 0; u < kPer; u++) {
-            mine[u] = tid + u * NT < nc ? S.sortk[tid + u * NT] : ~0ull;
-            rk[u] = 0;
-        }
-        for (int j = 0; j < nc; j++) {
-            const uint64_t v = S.sortk[j];
-#pragma unroll
-            for (int u = 0; u < kPer; u++) rk[u] += v < mine[u];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < kPer; u++)
-            if (tid + u * NT < nc) S.sortk[rk[u]] = mine[u];
-        __syncthreads();
-        // processing order p = 0..nc-1 is sortk[nc-1-p]; cut at the first p with size >= N
-        if (tid == 0) S.scal[0] = nc;  // first p reaching N (nc: none)
-        __syncthreads();
-        int carryE = 0, carryD = 0;
-        for (int p0 = 0; p0 < nc; p0 += NT) {
-            const int p = p0 + tid;
-            int e = 0;
-            int i = 0;
-            if (p < nc) {
-                i = (int)(S.sortk[nc - 1 - p] & 0xFFFF);
-                const uint32_t c[2] = {S.cq[i][0], S.cq[i][1]};
-                e = (quad_count(c, 0) > 0) + (quad_count(c, 1) > 0) + (quad_count(c, 2) > 0) + (quad_count(c, 3) > 0);
-            }
-            int totE, totD;
-            const int exE = block_excl_scan<NT>(e, S.red, &totE);
-            const int exD = block_excl_scan<NT>(p < nc ? e - 1 : 0, S.red, &totD);
-            if (p < nc) {
-                S.remap[i] = (uint32_t)(carryE + exE);
-                if (size + carryD + exD + (e - 1) >= N) atomicMin(&S.scal[0], p);
-            }
-            carryE += totE;
-            carryD += totD;
-        }
-        __syncthreads();
-        const int pstar = min(S.scal[0], nc - 1);  // last dividing position
-        for (int p = tid; p <= pstar; p += NT) {
-            const int i = (int)(S.sortk[nc - 1 - p] & 0xFFFF);
-            S.mid[i] |= 1u << 31;
-        }
-        __syncthreads();
-        if (pstar >= 0 && tid == 0) {
-            const int i = (int)(S.sortk[nc - 1 - pstar] & 0xFFFF);
-            const uint32_t c[2] = {S.cq[i][0], S.cq[i][1]};
-            const int e = (quad_count(c, 0) > 0) + (quad_count(c, 1) > 0) + (quad_count(c, 2) > 0) + (quad_count(c, 3) > 0);
-            S.scal[1] = (int)S.remap[i] + e;
-        } else if (tid == 0) {
-            S.scal[1] = 0;
-        }
-        __syncthreads();
-        ctot = S.scal[1];
-    }
-    // c) positions: divided -> child block at ctot - E - e (reverse division order);
-    //    undivided -> ctot + rank in list order.  New records into the other buffer.
-    const int nxt = cur ^ 1;
-    int carryK = 0, nexp = 0;
-    for (int i0 = 0; i0 < size; i0 += NT) {
-        const int i = i0 + tid;
-        const bool valid = i < size;
-        const bool div = valid && (S.mid[i] >> 31);
-        int tot;
-        const int ex = block_excl_scan<NT>(valid && !div ? 1 : 0, S.red, &tot);
-        if (valid) {
-            if (div) {
-                const uint32_t c[2] = {S.cq[i][0], S.cq[i][1]};
-                int cc[4], mask = 0, e = 0;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    cc[q] = quad_count(c, q);
-                    mask |= (cc[q] > 0) << q;
-                    e += cc[q] > 0;
-                }
-                const int E = (int)S.remap[i];
-                const int start = ctot - E - e;
-                S.remap[i] = (1u << 31) | ((uint32_t)mask << 16) | (uint32_t)start;
-                const uint64_t b = S.bnd[cur][i];
-                const uint32_t x0 = (uint32_t)(b & 0xFFFF), y0 = (uint32_t)((b >> 16) & 0xFFFF);
-                const uint32_t x1 = (uint32_t)((b >> 32) & 0xFFFF), y1 = (uint32_t)(b >> 48);
-                const uint32_t md = S.mid[i];
-                const uint32_t mx = md & 0xFFFu, my = (md >> 12) & 0xFFFu;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (cc[q] == 0) continue;
-                    const int pos = start + __popc((uint32_t)mask >> (q + 1));
-                    if (pos >= NC) { overflow = 1; continue; }
-                    const uint64_t cx0 = (q & 1) ? mx : x0, cx1 = (q & 1) ? x1 : mx;
-                    const uint64_t cy0 = (q & 2) ? my : y0, cy1 = (q & 2) ? y1 : my;
-                    S.bnd[nxt][pos] = cx0 | (cy0 << 16) | (cx1 << 32) | (cy1 << 48);
-                    S.cnt[nxt][pos] = (uint32_t)cc[q];
-                    S.seq[nxt][pos] = (uint32_t)(seqc + E + __popc((uint32_t)mask & ((1u << q) - 1))) |
-                                      ((uint32_t)(cc[q] > 1) << 31);
-                    nexp += cc[q] > 1;
-                }
-            } else {
-                const int pos = ctot + carryK + ex;
-                S.remap[i] = (uint32_t)pos;
-                if (pos >= NC) {
-                    overflow = 1;
-                } else {
-                    S.bnd[nxt][pos] = S.bnd[cur][i];
-                    S.cnt[nxt][pos] = S.cnt[cur][i];
-                    S.seq[nxt][pos] = S.seq[cur][i] & 0x7FFFFFFFu;
-                }
-            }
-        }
-        carryK += tot;
-    }
-    int totx;  // expanders | overflow flags << 24, block-uniform; also orders the writes before the sweep
-    block_excl_scan<NT>(nexp | (overflow << 24), S.red, &totx);
-    overflow = totx >> 24 ? 1 : 0;
-    totx &= 0xFFFFFF;
-    // d) every key takes its node's new list position
-#pragma unroll 4
-    for (int j = tid; j < n; j += NT) {
-        const int i = nid[j];
-        const uint32_t r = S.remap[i];
-        if (r >> 31) {
-            const int q = oct_quadrant(K[j], S.mid[i]);
-            nid[j] = (uint16_t)((r & 0xFFFFu) + __popc(((r >> 16) & 15u) >> (q + 1)));
-        } else {
-            nid[j] = (uint16_t)(r & 0xFFFFu);
-        }
-    }
-    cur = nxt;
-    size = ctot + carryK;
-    seqc += ctot;
-    nexpand = totx;
-    if (size > NC) overflow = 1;
-    __syncthreads();
-}
-
-template <int NC, int NT>
-__device__ __forceinline__ void octree_body(const Plan *__restrict__ plan, const LevelDesc &L, int l, int f,
-                                            OctLds<NC> &S, const uint32_t *__restrict__ cellbuf,
-                                            const int *__restrict__ cellcnt, int *s_pref, uint32_t *K,
-                                            uint16_t *nid, int n, uint32_t *__restrict__ sel,
-                                            int *__restrict__ selcnt, int *__restrict__ err) {
-    const int tid = threadIdx.x;
-    // 1. vToDistributeKeys in cell order: 256 cells per chunk, key index -> cell by
-    //    binary search over the chunk's exclusive prefix
-    {
-        int base = 0;
-        for (int cb = 0; cb < L.ncells; cb += NT) {
-            const int c = cb + tid;
-            const int cnt = c < L.ncells ? cellcnt[(size_t)f * plan->ncells + L.cell_begin + c] : 0;
-            int tot;
-            s_pref[tid] = block_excl_scan<NT>(cnt, S.red, &tot);
-            __syncthreads();
-            const int nch = min(L.ncells - cb, NT);
-            const uint32_t *cs0 = cellbuf + ((size_t)f * plan->ncells + L.cell_begin + cb) * plan->cell_cap;
-            for (int j0 = 0; j0 < tot; j0 += NT * 8) {  // 8 independent key loads in flight per thread
-                uint32_t v[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int j = j0 + NT * u + tid;
-                    v[u] = 0u;
-                    if (j < tot) {
-                        int lo = 0, hi = nch - 1;
-                        while (lo < hi) {
-                            const int md = (lo + hi + 1) >> 1;
-                            if (s_pref[md] <= j) lo = md; else hi = md - 1;
-                        }
-                        v[u] = cs0[(size_t)lo * plan->cell_cap + (j - s_pref[lo])];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int j = j0 + NT * u + tid;
-                    if (j < tot) K[base + j] = v[u];
-                }
-            }
-            base += tot;
-            __syncthreads();
-        }
-    }
-    if (l == 0) YGZ_BSTAMP_K(3, 3);
-    // 2. initial nodes (:535-580): columns of width hX, push_back order, empty ones erased
-    const int nIni = L.n_ini;
-    const float hX = L.hX;
-    const int H0 = L.max_by - kMinBorder;
-    if (tid < 8) S.scal[tid] = 0;
-    __syncthreads();
-    for (int j = tid; j < n; j += NT) {
-        int idx = (int)((float)key_x(K[j]) / hX);
-        idx = idx >= nIni ? nIni - 1 : idx;
-        nid[j] = (uint16_t)idx;
-        atomicAdd(&S.scal[idx], 1);
-    }
-    __syncthreads();
-    int size = 0;
-    for (int i = 0; i < nIni; i++) {
-        const int c = S.scal[i];
-        if (c > 0) {
-            if (tid == 0) {
-                const uint64_t x0 = (uint32_t)(int)(hX * (float)i), x1 = (uint32_t)(int)(hX * (float)(i + 1));
-                S.bnd[0][size] = x0 | (x1 << 32) | ((uint64_t)H0 << 48);
-                S.cnt[0][size] = (uint32_t)c;
-                S.seq[0][size] = (uint32_t)i;
-            }
-            if (tid == 0) S.remap[i] = (uint32_t)size;
-            size++;
-        }
-    }
-    __syncthreads();
-    for (int j = tid; j < n; j += NT) nid[j] = (uint16_t)S.remap[nid[j]];
-    __syncthreads();
-    if (l == 0) YGZ_BSTAMP_K(3, 4);
-    // 3. main loop (:585-680)
-    const int N = L.budget;
-    int cur = 0, seqc = nIni, overflow = 0, nexpand = 0, guard = 0;
-    bool final_round = false;
-    if (l == 0) YGZ_BSTAMP_K(4, 3);
-    while (true) {
-        const int prev = size;
-        octree_pass<NC, NT>(S, K, nid, n, N, final_round, cur, size, seqc, nexpand, overflow);
-        if (l == 0 && guard < 4) {  // diagnostic build (STAMPK=4): the first four passes
-            if (guard == 0) YGZ_BSTAMP_K(4, 4);
-            if (guard == 1) YGZ_BSTAMP_K(4, 5);
-            if (guard == 2) YGZ_BSTAMP_K(4, 6);
-            if (guard == 3) YGZ_BSTAMP_K(4, 7);
-        }
-        if (overflow || ++guard > 4096) { overflow = 1; break; }
-        if (size >= N || size == prev) break;
-        if (!final_round && size + nexpand * 3 > N) final_round = true;
-    }
-    if (l == 0) YGZ_BSTAMP_K(3, 5);
-    if (l == 0) YGZ_BVAL_K(3, 6, guard);
-    // 4. retained key per node, list order
-    uint32_t *out = sel + (size_t)f * plan->sel_total + L.sel_off;
-    if (!overflow) {
-        for (int i = tid; i < size; i += NT) S.cq[i][0] = 0u;
-        __syncthreads();
-        for (int j0 = tid - (tid & 63); j0 < n; j0 += NT) {  // one atomic per run of equal nodes
-            const int j = j0 + (tid & 63);
-            const int t = j < n ? (int)nid[j] : -1;
-            const uint32_t v = j < n ? ((uint32_t)key_score(K[j]) << 24) | (uint32_t)(0xFFFFFF - j) : 0u;
-            uint32_t m;
-            const int run_len = wave_run_max(t, v, m);
-            if (run_len > 0 && t >= 0) atomicMax(&S.cq[t][0], m);
-        }
-        __syncthreads();
-        if (size > L.sel_cap) overflow = 1;
-        for (int i = tid; i < size && i < L.sel_cap; i += NT) out[i] = K[0xFFFFFF - (S.cq[i][0] & 0xFFFFFFu)];
-    }
-    if (tid == 0) {
-        selcnt[(size_t)f * plan->nlevels + l] = overflow ? 0 : min(size, L.sel_cap);
-        if (overflow) atomicOr(err, 1);
-    }
-    if (l == 0) YGZ_BSTAMP_K(3, 1);
-    if (l == 0) YGZ_BSTAMP_K(3, 2);
-    if (l == 0) YGZ_BSTAMP_K(4, 1);
-    if (l == 0) YGZ_BSTAMP_K(4, 2);
-}
-
-// Keys and labels in LDS when the level has at most kOctLdsKeys candidates
-// (the common case), else in the global scratch; the node lists always in LDS.
-// 4000 keeps the NC=1024 workgroup under 80 KiB: two workgroups per CU.
-constexpr int kOctLdsKeys = 4000;
-
-// One launch per level (or a group of levels, l = level0 + blockIdx.y) so that
-// the node pool NC and the LDS key capacity NK fit that level's budget: the
-// small levels' workgroups then need a fraction of level 0's LDS and many fit
-// per CU.
-template <int NC, int NK, int NT = 256>
-__global__ __launch_bounds__(NT) void k_octree(const Plan *__restrict__ plan,
-                                                const uint32_t *__restrict__ cellbuf,
-                                                const int *__restrict__ cellcnt,
-                                                uint32_t *__restrict__ candA, uint32_t *__restrict__ candB,
-                                                uint32_t *__restrict__ sel, int *__restrict__ selcnt,
-                                                int *__restrict__ err, int level0) {
-    __shared__ OctLds<NC> S;
-    __shared__ uint32_t sK[NK];
-    __shared__ uint16_t sNid[NK];
-    int *s_pref = reinterpret_cast<int *>(S.sortk);  // gather prefix; sortk is free until the final rounds
-    const int f = blockIdx.x, l = level0 + blockIdx.y, tid = threadIdx.x;
-    if (l == 0) YGZ_BSTAMP_K(3, 0);
-    if (l == 0) YGZ_BSTAMP_K(4, 0);
-    const LevelDesc &L = plan->lv[l];
-    int part = 0;
-    for (int c = tid; c < L.ncells; c += NT) part += cellcnt[(size_t)f * plan->ncells + L.cell_begin + c];
-    int n;
-    block_excl_scan<NT>(part, S.red, &n);
-    if (n > 65535) {  // u16 labels / quadrant counts
-        if (tid == 0) {
-            selcnt[(size_t)f * plan->nlevels + l] = 0;
-            atomicOr(err, 1);
-        }
-        return;
-    }
-    if (n <= NK) {
-        octree_body<NC, NT>(plan, L, l, f, S, cellbuf, cellcnt, s_pref, sK, sNid, n, sel, selcnt, err);
-    } else {
-        uint32_t *K = candA + (size_t)f * plan->cand_total + L.cand_off;
-        uint16_t *nid = reinterpret_cast<uint16_t *>(candB + (size_t)f * plan->cand_total + L.cand_off);
-        octree_body<NC, NT>(plan, L, l, f, S, cellbuf, cellcnt, s_pref, K, nid, n, sel, selcnt, err);
-    }
-}
-
 // ---------------------------------------------------------------------------
-// Octree distribution by quadrant paths (the kernel in use; k_octree above is the
-// level-synchronous form it replaced, kept for A/B builds with -DYGZ_OCT_LEGACY).
+// Octree distribution by quadrant paths (DistributeOctTree, ORBextractor.cc:533-723
+// with ExtractorNode::DivideNode :479-531).
 //
 // A node at depth d is the set of keys that share the first d quadrants of their
 // path from the root column (the division midpoints, ORBextractor.cc:481-482, depend
@@ -2818,37 +2350,39 @@ constexpr int kOctThreads = YGZ_OCT_THREADS;
 #endif
 constexpr int kOctListThreads = YGZ_OCT_LIST_THREADS;
 
-// queue words per launch group g: counters at octq[8 g ..] (list i: count 2i, taken
-// 2i + 1), lists at octq[kOctQHead + (3 g + i) T], T = frames x levels; then the
-// per-task sort headers at octq[kOctQHead + 12 T + f levels + l]
-constexpr int kOctQHead = 64;
-size_t octree_queue_ints(const Plan &hp, int nframes) { return kOctQHead + (size_t)13 * nframes * hp.nlevels; }
+// launch groups: runs of consecutive levels with one node-pool class (the class
+// sequence can go back up, e.g. when the last level's remainder budget or a flipped
+// n_ini moves it, so a plan may hold up to nlevels groups)
+static int octree_groups(const Plan &hp) {
+    int G = 0;
+    for (int l = 0; l < hp.nlevels; G++) {
+        const int nc = octree_nc(hp.lv[l]);
+        while (l < hp.nlevels && octree_nc(hp.lv[l]) == nc) l++;
+    }
+    return G;
+}
+// queue words: 8 counters per launch group g at octq[8 g ..] (list i: count 2i, taken
+// 2i + 1) in a head of max(64, 8 G) words; then 3 lists per group at
+// octq[head + (3 g + i) T], T = frames x levels; then the per-task sort headers at
+// octq[head + 3 G T + f levels + l]
+static size_t oct_head(int G) { return (size_t)std::max(64, 8 * G); }
+size_t octree_queue_ints(const Plan &hp, int nframes) {
+    const int G = octree_groups(hp);
+    return oct_head(G) + (size_t)(3 * G + 1) * nframes * hp.nlevels;
+}
 
 static hipError_t launch_octree_levels(int nc, const Plan *dp, const uint32_t *cellbuf, const int *cellcnt,
                                        uint32_t *candA, uint32_t *candB, uint32_t *sel, int *selcnt, int *err,
-                                       int *octq, int g, int T, int nframes, int l0, int nl, hipStream_t st,
-                                       bool wide) {
+                                       int *octq, int g, int G, int T, int nframes, int l0, int nl,
+                                       hipStream_t st, bool wide) {
     dim3 grid(nframes, nl);
-#ifdef YGZ_OCT_LEGACY
-    (void)octq; (void)g; (void)T;
-#define YGZ_OCT(NC, NK, NT) hipLaunchKernelGGL((k_octree<NC, NK, NT>), grid, dim3(NT), 0, st, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, l0)
-    // one frame (the latency path): a workgroup per level has the CU to itself,
-    // so the largest class takes 1024 threads (shorter strided loops per pass)
-    if (wide && nc > 512 && nc <= 1024) YGZ_OCT(1024, 4000, 1024);
-    // LDS keys: 4000 with NC 1024 (two workgroups per CU), the larger levels' share below
-    else if (nc <= 256) YGZ_OCT(256, 1536, 256);
-    else if (nc <= 512) YGZ_OCT(512, 3072, kOctThreads);
-    else if (nc <= 1024) YGZ_OCT(1024, 4000, kOctThreads);
-    else YGZ_OCT(2048, 4000, kOctThreads);
-#undef YGZ_OCT
-#else
     // sort stage 0: one workgroup per task, sized for the class's usual candidate count
     // (wide = one frame: 8,192 keys at once); stage 1: 4,096 keys in LDS (512 threads);
     // stage 2: 8,192 keys (1,024 threads, one workgroup per CU); stage 3: the
     // global-scratch form (sort + list); then the list phase of every LDS-sorted task
     int *cq = octq + 8 * g;
-    int *lists = octq + kOctQHead + (size_t)3 * g * T;
-    int *hdr = octq + kOctQHead + (size_t)12 * T;
+    int *lists = octq + oct_head(G) + (size_t)3 * g * T;
+    int *hdr = octq + oct_head(G) + (size_t)3 * G * T;
     const OctQueue q0{nullptr, nullptr, nullptr, cq + 0, lists};
     const OctQueue q1{cq + 0, cq + 1, lists, cq + 2, lists + T};
     const OctQueue q2{cq + 2, cq + 3, lists + T, cq + 4, lists + 2 * T};
@@ -2892,7 +2426,6 @@ static hipError_t launch_octree_levels(int nc, const Plan *dp, const uint32_t *c
     }
 #undef YGZ_OCT_SORT0
 #undef YGZ_OCT_REST
-#endif
     return hipGetLastError();
 }
 
@@ -2903,12 +2436,13 @@ hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf
                          int nframes, hipStream_t st, const hipStream_t *side, int nside, hipEvent_t fork,
                          const hipEvent_t *join, bool wide) {
     int l = 0, g = 0;
-    YGZ_HIPR(hipMemsetAsync(octq, 0, kOctQHead * sizeof(int), st));  // queue counters
+    const int G = octree_groups(hp);
+    YGZ_HIPR(hipMemsetAsync(octq, 0, oct_head(G) * sizeof(int), st));  // queue counters
     if (wide) {  // one frame: every level in one launch chain when the node pools allow
         int ncmax = 0;
         for (int k = 0; k < hp.nlevels; k++) ncmax = std::max(ncmax, octree_nc(hp.lv[k]));
         if (ncmax <= 1024)
-            return launch_octree_levels(1024, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, octq, 0,
+            return launch_octree_levels(1024, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, octq, 0, G,
                                         nframes * hp.nlevels, nframes, 0, hp.nlevels, st, true);
     }
     if (side && nside > 0) YGZ_HIPR(hipEventRecord(fork, st));  // before the first group: the groups are independent
@@ -2921,7 +2455,7 @@ hipError_t launch_octree(const Plan &hp, const Plan *dp, const uint32_t *cellbuf
             s = side[g - 1];
             YGZ_HIPR(hipStreamWaitEvent(s, fork, 0));
         }
-        YGZ_HIPR(launch_octree_levels(nc, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, octq, g,
+        YGZ_HIPR(launch_octree_levels(nc, dp, cellbuf, cellcnt, candA, candB, sel, selcnt, err, octq, g, G,
                                       nframes * hp.nlevels, nframes, l, e - l, s, wide));
         if (s != st) YGZ_HIPR(hipEventRecord(join[g - 1], s));
         l = e;

@@ -35,6 +35,8 @@ hipError_t launch_desc_existing(const uint8_t *pyr, const uint8_t *blur, const P
                                 uint8_t *desc, int n, int recompute_angle, hipStream_t st);
 
 // dso.hip
+hipError_t launch_fast10_rois(const uint8_t *img, int stride, const int *rois, int n_rois, int barrier,
+                              int variant, int16_t *out_xy, int cap, int *counts, hipStream_t st);
 hipError_t launch_dso_occupancy(const ygzfe_kp *kps, int n, uint8_t *occ, int w, int h, hipStream_t st);
 hipError_t launch_dso_pass(const uint8_t *img, int w, int h, int g, const uint8_t *occ, uint32_t *keys, int *cnt,
                            hipStream_t st);

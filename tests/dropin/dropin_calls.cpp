@@ -298,6 +298,12 @@ int main(int argc, char **argv) {
         CHECK(ret == (size_t)ao.n_visible && err <= 1e-4f && ret > 100,
               "mpAlign->run(&mLastFrame, &mCurrentFrame, TCR): visible %zu (oracle %d), |dT| %.2e, t (%.4f %.4f) "
               "expected ~(%.4f %.4f)", ret, ao.n_visible, err, TCR.translation()[0], TCR.translation()[1], tx, ty);
+        {  // NLSSolver_impl.hpp:8-13: the GPU runs only Gauss-Newton; LM is refused (returns 0)
+            ygz::SparseImgAlign lm(nl - 1, 1, 10, ygz::SparseImgAlign::LevenbergMarquardt);
+            SE3f Tlm;
+            CHECK(lm.run(&T.mLastFrame, &T.mCurrentFrame, Tlm) == 0,
+                  "SparseImgAlign(.., LevenbergMarquardt).run() refused (returns 0, logs once)");
+        }
         const auto I = T.mpAlign->getFisherInformation();
         CHECK(std::fabs(I(0, 0) - ao.H[0] / (float)(5e-4 * 255 * 255)) <= 1e-3f * std::fabs(I(0, 0)) + 1e-3f,
               "getFisherInformation() = H / 32.5125: %.4g", I(0, 0));

@@ -139,6 +139,36 @@ def test_search_by_bow(gpu, check_ori, n_nodes, decide):
         assert (F.resolve_passes() >= 1) == (decide == "resolve")
 
 
+@pytest.mark.parametrize("mode", ["init", "bow"])
+def test_query_frame_upload_in_flight(gpu, mode, decide):
+    """SearchForInitialization / SearchByBoW read the query frame's descriptors on the device
+    from the train frame's stream.  The query frame is set (async upload on its own stream)
+    with that stream held for 20 ms (YGZFE_DEBUG_SET_HOLD_US) and the search starts at once:
+    it must wait for the upload (ev_ready) and still equal the oracle."""
+    p = pair("C2", 0)
+    F2 = gpu_frame(gpu, p["k1"], p["d1"], None, p)
+    os.environ["YGZFE_DEBUG_SET_HOLD_US"] = "20000"
+    try:
+        F1 = gpu_frame(gpu, p["k0"], p["d0"], None, p)  # fresh device buffers, upload held
+    finally:
+        os.environ.pop("YGZFE_DEBUG_SET_HOLD_US", None)
+    if mode == "init":
+        rng = np.random.default_rng(3)
+        prev = (np.stack([p["k0"]["x"], p["k0"]["y"]], 1) + rng.uniform(-2, 2, (len(p["k0"]), 2))).astype(np.float32)
+        got, gn, _ = gpu.search_for_initialization(F1, F2, prev, 100, 0.9, True)
+        want, wn, _ = O.search_for_initialization(O.mframe(p["k0"], p["d0"], None, bounds(p)),
+                                                  O.mframe(p["k1"], p["d1"], None, bounds(p)), prev, 100, 0.9, True)
+    else:
+        usable = np.ones(len(p["k0"]), np.uint8)
+        fv0 = S.feature_vector(p["d0"], 40, 0)
+        fv1 = S.feature_vector(p["d1"], 40, 0)
+        got, gn = gpu.search_by_bow(F1, F2, usable, fv0, fv1, 0.75, True)
+        want, wn = O.search_by_bow(O.mframe(p["k0"], p["d0"], None, bounds(p)),
+                                   O.mframe(p["k1"], p["d1"], None, bounds(p)), usable, fv0, fv1, 0.75, True)
+    assert gn == wn and np.array_equal(got, want)
+    assert wn > 10
+
+
 def sub_fv(fv, keep):
     nodes, ptr, feats = fv
     nn, pp, ff = [], [0], []
