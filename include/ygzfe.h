@@ -483,6 +483,16 @@ int ygzfe_undistort_maps(const ygzfe_undistort *u, int16_t *map1, uint16_t *map2
 /* remap n device images (pitch between images, row stride inside one) */
 int ygzfe_undistort_apply_device(const ygzfe_undistort *u, const uint8_t *d_src, size_t src_pitch, int src_stride,
                                  uint8_t *d_dst, size_t dst_pitch, int dst_stride, int n_images, void *stream);
+/* The RGB-D depth image's undistortion (Frame.cc:799-804): the same maps, cv::remap
+ * INTER_LINEAR on CV_32F (float weight table, BORDER_CONSTANT 0), n_images images of
+ * src_stride / dst_stride floats per row, src_pitch / dst_pitch floats apart. */
+int ygzfe_undistort_apply_f32_device(const ygzfe_undistort *u, const float *d_src, size_t src_pitch, int src_stride,
+                                     float *d_dst, size_t dst_pitch, int dst_stride, int n_images, void *stream);
+/* One host image in, its undistorted copy out (the drop-in Frame::ComputeImagePyramid's
+ * remaps of mImGray / mImRight, Frame.cc:786-797, and of mImDepth, :799-804); strides in
+ * elements. */
+int ygzfe_undistort_image(const ygzfe_undistort *u, const uint8_t *src, int src_stride, uint8_t *dst, int dst_stride);
+int ygzfe_undistort_depth(const ygzfe_undistort *u, const float *src, int src_stride, float *dst, int dst_stride);
 /* ComputeImagePyramid with undistortion: remap(img) -> level 0, then levels */
 int ygzfe_compute_pyramid_undistorted(ygzfe_extractor *ex, ygzfe_frame *f, ygzfe_undistort *u, const uint8_t *img,
                                       int stride);

@@ -111,3 +111,40 @@ void ygzo_remap_linear(const uint8_t *src, int W, int H, int sstride, const int1
             dst[(size_t)y * dstride + x] = (uint8_t)(val < 0 ? 0 : (val > 255 ? 255 : val));
         }
 }
+
+/* remapBilinear<Cast<float, float>, RemapNoVec, float> with BORDER_CONSTANT
+ * (borderValue 0): the RGB-D depth image's undistortion (Frame.cc:799-804, the
+ * same CV_16SC2 maps).  remap() takes the float weight table for every depth but
+ * CV_8U (imgwarp.cpp: fixpt = depth == CV_8U); initInterTab2D's float entries are
+ * c_y[k1] * c_x[k2] with c = (1 - t/32, t/32), exact in float.  The sum is
+ * S00 w0 + S01 w1 + S10 w2 + S11 w3, left to right in float (no FMA contraction:
+ * the scalar path of OpenCV's baseline x86-64 build; built -ffp-contract=off). */
+void ygzo_remap_linear_f32(const float *src, int W, int H, int sstride, const int16_t *map1, const uint16_t *map2,
+                           int DW, int DH, float *dst, int dstride) {
+    for (int y = 0; y < DH; y++)
+        for (int x = 0; x < DW; x++) {
+            const int sx = map1[2 * ((size_t)y * DW + x)], sy = map1[2 * ((size_t)y * DW + x) + 1];
+            const int f = map2[(size_t)y * DW + x];
+            const int tx = f & (INTER_TAB_SIZE - 1), ty = f >> INTER_BITS;
+            const float cx0 = 1.f - (float)tx * (1.f / INTER_TAB_SIZE), cx1 = (float)tx * (1.f / INTER_TAB_SIZE);
+            const float cy0 = 1.f - (float)ty * (1.f / INTER_TAB_SIZE), cy1 = (float)ty * (1.f / INTER_TAB_SIZE);
+            const float w0 = cy0 * cx0, w1 = cy0 * cx1, w2 = cy1 * cx0, w3 = cy1 * cx1;
+            float v0, v1, v2, v3;
+            if ((unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1)) {
+                const float *S = src + (size_t)sy * sstride + sx;
+                v0 = S[0]; v1 = S[1]; v2 = S[sstride]; v3 = S[sstride + 1];
+            } else if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
+                dst[(size_t)y * dstride + x] = 0.f;
+                continue;
+            } else {
+                const int x0 = sx, x1 = sx + 1, y0 = sy, y1 = sy + 1;
+                const int ok_x0 = x0 >= 0 && x0 < W, ok_x1 = x1 >= 0 && x1 < W;
+                const int ok_y0 = y0 >= 0 && y0 < H, ok_y1 = y1 >= 0 && y1 < H;
+                v0 = ok_x0 && ok_y0 ? src[(size_t)y0 * sstride + x0] : 0.f;
+                v1 = ok_x1 && ok_y0 ? src[(size_t)y0 * sstride + x1] : 0.f;
+                v2 = ok_x0 && ok_y1 ? src[(size_t)y1 * sstride + x0] : 0.f;
+                v3 = ok_x1 && ok_y1 ? src[(size_t)y1 * sstride + x1] : 0.f;
+            }
+            dst[(size_t)y * dstride + x] = v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3;
+        }
+}

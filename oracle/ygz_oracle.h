@@ -275,6 +275,9 @@ void ygzo_undistort_map(const float cam[4], const float *dist, int ndist, int W,
 /* cv::remap(src, dst, map1, map2, INTER_LINEAR), BORDER_CONSTANT 0 */
 void ygzo_remap_linear(const uint8_t *src, int W, int H, int sstride, const int16_t *map1, const uint16_t *map2,
                        int DW, int DH, uint8_t *dst, int dstride);
+/* the same remap for CV_32F (Frame.cc:799-804, RGB-D depth): float weight table */
+void ygzo_remap_linear_f32(const float *src, int W, int H, int sstride, const int16_t *map1, const uint16_t *map2,
+                           int DW, int DH, float *dst, int dstride);
 
 /* ---------------- CPU baseline driver (oracle/bench.c, bench.py's cpu_baseline) ---------------- */
 typedef struct ygzo_bench_stats {

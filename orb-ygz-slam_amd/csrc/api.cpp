@@ -2380,6 +2380,66 @@ extern "C" int ygzfe_undistort_apply_device(const ygzfe_undistort *u, const uint
     return YGZFE_OK;
 }
 
+extern "C" int ygzfe_undistort_apply_f32_device(const ygzfe_undistort *u, const float *d_src, size_t src_pitch,
+                                                int src_stride, float *d_dst, size_t dst_pitch, int dst_stride,
+                                                int n_images, void *stream) {
+    if (!u || n_images < 0 || (n_images > 0 && (!d_src || !d_dst)) || src_stride < u->W || dst_stride < u->W ||
+        (n_images > 1 && (src_pitch < (size_t)src_stride * u->H || dst_pitch < (size_t)dst_stride * u->H)) ||
+        n_images > 65535) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    if (n_images == 0) return YGZFE_OK;
+    YGZ_TRY(ensure_device(u->device));
+    hipStream_t st = stream ? (hipStream_t)stream : u->stream;
+    YGZ_HIP(launch_remap_f32(d_src, src_pitch, u->W, u->H, src_stride, u->map1.as<int16_t>(), u->map2.as<uint16_t>(),
+                             d_dst, dst_pitch, dst_stride, n_images, st));
+    if (!stream) YGZ_HIP(hipStreamSynchronize(st));
+    return YGZFE_OK;
+}
+
+// host image in, host image out: one H2D, the remap, one D2H (leased staging)
+static int undistort_host(const ygzfe_undistort *u, const void *src, int src_stride, void *dst, int dst_stride,
+                          int esize) {
+    if (!u || !src || !dst || src_stride < u->W || dst_stride < u->W) {
+        set_error("invalid argument");
+        return YGZFE_EINVAL;
+    }
+    YGZ_TRY(ensure_device(u->device));
+    StagingLease S;
+    YGZ_TRY(S.acquire(u->device));
+    const size_t row = (size_t)u->W * esize, img = row * u->H, o_d = align16(img);
+    YGZ_TRY(S->hin.ensure(img));
+    YGZ_TRY(S->hout.ensure(img));
+    YGZ_TRY(S->dev.ensure(o_d + img));
+    uint8_t *h = S->hin.as<uint8_t>(), *d = S->dev.as<uint8_t>();
+    for (int y = 0; y < u->H; y++)
+        memcpy(h + (size_t)y * row, static_cast<const uint8_t *>(src) + (size_t)y * src_stride * esize, row);
+    YGZ_HIP(hipMemcpyAsync(d, h, img, hipMemcpyHostToDevice, S->stream));
+    if (esize == 4)
+        YGZ_HIP(launch_remap_f32(reinterpret_cast<const float *>(d), 0, u->W, u->H, u->W, u->map1.as<int16_t>(),
+                                 u->map2.as<uint16_t>(), reinterpret_cast<float *>(d + o_d), 0, u->W, 1, S->stream));
+    else
+        YGZ_HIP(launch_remap_linear(d, 0, u->W, u->H, u->W, u->map1.as<int16_t>(), u->map2.as<uint16_t>(), u->boxes.p,
+                                    u->max_box, u->any_large, d + o_d, 0, u->W, 1, S->stream));
+    YGZ_HIP(hipMemcpyAsync(S->hout.p, d + o_d, img, hipMemcpyDeviceToHost, S->stream));
+    YGZ_HIP(hipStreamSynchronize(S->stream));
+    for (int y = 0; y < u->H; y++)
+        memcpy(static_cast<uint8_t *>(dst) + (size_t)y * dst_stride * esize, S->hout.as<uint8_t>() + (size_t)y * row,
+               row);
+    return YGZFE_OK;
+}
+
+extern "C" int ygzfe_undistort_image(const ygzfe_undistort *u, const uint8_t *src, int src_stride, uint8_t *dst,
+                                     int dst_stride) {
+    return undistort_host(u, src, src_stride, dst, dst_stride, 1);
+}
+
+extern "C" int ygzfe_undistort_depth(const ygzfe_undistort *u, const float *src, int src_stride, float *dst,
+                                     int dst_stride) {
+    return undistort_host(u, src, src_stride, dst, dst_stride, 4);
+}
+
 extern "C" int ygzfe_compute_pyramid_undistorted(ygzfe_extractor *ex, ygzfe_frame *f, ygzfe_undistort *u,
                                                  const uint8_t *img, int stride) {
     if (!ex || !f || !u || !img || stride < f->W) { set_error("invalid argument"); return YGZFE_EINVAL; }

@@ -192,6 +192,9 @@ hipError_t launch_pack_slots(const ygzfe_kp *kps, const uint8_t *desc, const int
                              const ygzfe_align_result *align, int frame_begin, int n_frames, int global_first,
                              uint8_t *slots, size_t slot_pitch, hipStream_t st);
 
+hipError_t launch_remap_f32(const float *src, size_t src_pitch, int W, int H, int sstride, const int16_t *map1,
+                            const uint16_t *map2, float *dst, size_t dst_pitch, int dstride, int n_images,
+                            hipStream_t st);
 hipError_t launch_undistort_map(const float cam[4], const float *dist, int ndist, int W, int H, int16_t *map1,
                                 uint16_t *map2, hipStream_t st);
 int remap_tiles(int W, int H);  // entries of the per-tile source-box table (16 B each: x0, y0, w, h)

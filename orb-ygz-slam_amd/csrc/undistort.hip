@@ -329,6 +329,58 @@ static void inv3(const double a[9], double b[9]) {
     b[8] = (a[0] * a[4] - a[1] * a[3]) * d;
 }
 
+// The RGB-D depth image's undistortion (Frame.cc:799-804): the same maps, remap on
+// CV_32F.  remapBilinear<Cast<float, float>> takes the float weight table
+// (c_y * c_x, c = (1 - t/32, t/32), exact) and sums S00 w0 + S01 w1 + S10 w2 + S11 w3
+// left to right in float (no contraction: -ffp-contract=off), BORDER_CONSTANT 0;
+// oracle/undistort.c ygzo_remap_linear_f32.  One thread per output pixel, images
+// along grid.y (map reads coalesced, the 2x2 taps cache-local: the map is smooth).
+__global__ __launch_bounds__(256) void k_remap_f32(const float *__restrict__ src, size_t src_pitch, int W, int H,
+                                                   int sstride, const int16_t *__restrict__ map1,
+                                                   const uint16_t *__restrict__ map2, float *__restrict__ dst,
+                                                   size_t dst_pitch, int dstride) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= W || y >= H) return;
+    const float *S0 = src + (size_t)blockIdx.z * src_pitch;
+    const size_t o = (size_t)y * W + x;
+    const uint32_t xy = reinterpret_cast<const uint32_t *>(map1)[o];
+    const int sx = (int16_t)(xy & 0xFFFFu), sy = (int16_t)(xy >> 16);
+    const int f = map2[o];
+    const int tx = f & 31, ty = f >> 5;
+    const float cx0 = 1.f - (float)tx * (1.f / 32), cx1 = (float)tx * (1.f / 32);
+    const float cy0 = 1.f - (float)ty * (1.f / 32), cy1 = (float)ty * (1.f / 32);
+    const float w0 = cy0 * cx0, w1 = cy0 * cx1, w2 = cy1 * cx0, w3 = cy1 * cx1;
+    float v0, v1, v2, v3, r;
+    if ((unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1)) {
+        const float *S = S0 + (size_t)sy * sstride + sx;
+        v0 = S[0];
+        v1 = S[1];
+        v2 = S[sstride];
+        v3 = S[sstride + 1];
+        r = v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3;
+    } else if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
+        r = 0.f;
+    } else {
+        const bool ok_x0 = sx >= 0 && sx < W, ok_x1 = sx + 1 >= 0 && sx + 1 < W;
+        const bool ok_y0 = sy >= 0 && sy < H, ok_y1 = sy + 1 >= 0 && sy + 1 < H;
+        v0 = ok_x0 && ok_y0 ? S0[(size_t)sy * sstride + sx] : 0.f;
+        v1 = ok_x1 && ok_y0 ? S0[(size_t)sy * sstride + sx + 1] : 0.f;
+        v2 = ok_x0 && ok_y1 ? S0[(size_t)(sy + 1) * sstride + sx] : 0.f;
+        v3 = ok_x1 && ok_y1 ? S0[(size_t)(sy + 1) * sstride + sx + 1] : 0.f;
+        r = v0 * w0 + v1 * w1 + v2 * w2 + v3 * w3;
+    }
+    dst[(size_t)blockIdx.z * dst_pitch + (size_t)y * dstride + x] = r;
+}
+
+hipError_t launch_remap_f32(const float *src, size_t src_pitch, int W, int H, int sstride, const int16_t *map1,
+                            const uint16_t *map2, float *dst, size_t dst_pitch, int dstride, int n_images,
+                            hipStream_t st) {
+    if (n_images <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_remap_f32, dim3((W + 63) / 64, (H + 3) / 4, n_images), dim3(256), 0, st, src, src_pitch, W,
+                       H, sstride, map1, map2, dst, dst_pitch, dstride);
+    return hipGetLastError();
+}
+
 hipError_t launch_undistort_map(const float cam[4], const float *dist, int ndist, int W, int H, int16_t *map1,
                                 uint16_t *map2, hipStream_t st) {
     UndistortParams P;

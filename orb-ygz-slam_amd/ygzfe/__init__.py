@@ -286,6 +286,26 @@ class Undistort:
                                                   C.c_void_p(d_dst), C.c_size_t(dst_pitch), dst_stride, n_images,
                                                   C.c_void_p(stream)), "undistort_apply")
 
+    def apply_f32_device(self, d_src, src_pitch, src_stride, d_dst, dst_pitch, dst_stride, n_images, stream=None):
+        """remap of n CV_32F device images (pitch / stride in floats): Frame.cc:799-804."""
+        _check(lib().ygzfe_undistort_apply_f32_device(self.h, C.c_void_p(d_src), C.c_size_t(src_pitch), src_stride,
+                                                      C.c_void_p(d_dst), C.c_size_t(dst_pitch), dst_stride, n_images,
+                                                      C.c_void_p(stream)), "undistort_apply_f32")
+
+    def remap_image(self, image):
+        """cv::remap(mImGray / mImRight, ..., INTER_LINEAR) on a host u8 image (Frame.cc:786-797)."""
+        image = np.ascontiguousarray(image, np.uint8)
+        out = np.zeros_like(image)
+        _check(lib().ygzfe_undistort_image(self.h, _p(image), image.shape[1], _p(out), out.shape[1]), "undistort_image")
+        return out
+
+    def remap_depth(self, depth):
+        """cv::remap(mImDepth, ..., INTER_LINEAR) on a host CV_32F depth image (Frame.cc:799-804)."""
+        depth = np.ascontiguousarray(depth, np.float32)
+        out = np.zeros_like(depth)
+        _check(lib().ygzfe_undistort_depth(self.h, _p(depth), depth.shape[1], _p(out), out.shape[1]), "undistort_depth")
+        return out
+
     def ComputePyramid(self, extractor, image, frame=None):
         """ComputeImagePyramid with mDistCoef != 0: remap(image) -> level 0 -> levels."""
         image = np.ascontiguousarray(image, np.uint8)

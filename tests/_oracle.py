@@ -262,6 +262,17 @@ def remap_linear(src, map1, map2):
     return out
 
 
+def remap_linear_f32(src, map1, map2):
+    """remap(src, map1, map2, INTER_LINEAR, BORDER_CONSTANT 0) for CV_32F (the RGB-D depth image)."""
+    src = np.ascontiguousarray(src, np.float32)
+    H, W = src.shape
+    DH, DW = map2.shape
+    out = np.zeros((DH, DW), np.float32)
+    lib().ygzo_remap_linear_f32(_p(src), W, H, W, _p(np.ascontiguousarray(map1)), _p(np.ascontiguousarray(map2)),
+                                DW, DH, _p(out), DW)
+    return out
+
+
 def hamming_best2(q, t):
     q = np.ascontiguousarray(q, np.uint8)
     t = np.ascontiguousarray(t, np.uint8)

@@ -43,6 +43,7 @@ const int ORBmatcher::HISTO_LENGTH = 30;
 float Frame::fx, Frame::fy, Frame::cx, Frame::cy, Frame::invfx, Frame::invfy;
 float Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY, Frame::mnMaxY;
 long unsigned int Frame::nNextId = 0;
+bool Frame::mbNeedUndistort = false;
 
 struct System {
     enum eSensor { MONOCULAR = 0, STEREO = 1, RGBD = 2 };
@@ -186,6 +187,218 @@ static ygzo_mframe mframe(const Frame &F, bool uright) {
     f.min_y = Frame::mnMinY;
     f.max_y = Frame::mnMaxY;
     return f;
+}
+
+// Frame.cc:495-500, 509-700, 773-813 through the drop-in bodies (compat/dropin/Frame_gpu.inc),
+// each against the oracle: the TUM1 (C4) RGB-D frame undistorted (gray + CV_32F depth), its
+// depths; a rectified EuRoC stereo pair's ComputeStereoMatches; ComputeBoW on a vocabulary
+// bound with gpu::BindVocabulary.
+static void frame_rows() {
+    // TUM1.yaml:8-17 (C4): K, k1 k2 p1 p2 k3 -> Frame::mbNeedUndistort (Tracking.cc:171-204)
+    const int W = 640, H = 480, nl = 8;
+    Eigen::Matrix3f K;
+    K(0, 0) = 517.306408f;
+    K(1, 1) = 516.469215f;
+    K(0, 2) = 318.643040f;
+    K(1, 2) = 255.313989f;
+    K(2, 2) = 1.f;
+    cv::Mat D(5, 1, CV_32F);
+    const float dist[5] = {0.262383f, -0.953104f, -0.005358f, 0.002628f, 1.163314f};
+    std::memcpy(D.data, dist, sizeof(dist));
+    const float cam4[4] = {K(0, 0), K(1, 1), K(0, 2), K(1, 2)};
+    std::vector<int16_t> m1((size_t)2 * W * H);
+    std::vector<uint16_t> m2((size_t)W * H);
+    ygzo_undistort_map(cam4, dist, 5, W, H, m1.data(), m2.data());
+    const cv::Mat gray = synth(W, H, 11u, 0, 0);
+    cv::Mat depth(H, W, CV_32F);
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {  // TUM-like: uint16 / 5000, holes
+            const unsigned h = (((unsigned)x * 73856093u) ^ ((unsigned)y * 19349663u)) % 97u;
+            const int raw = h < 5 ? 0 : (int)(5000.f * (0.8f + 0.002f * x + 0.003f * y + 0.25f * ((x / 97 + y / 71) % 3)));
+            depth.ptr<float>(y)[x] = (float)raw * (1.0f / 5000);
+        }
+    ORBextractor ex4(2000, 1.2f, nl, 20, 7);  // TUM1.yaml (C4)
+    const bool saved = Frame::mbNeedUndistort;
+    Frame::mbNeedUndistort = true;
+    Frame F(gray, cv::Mat(), depth, Frame::RGBD, &ex4, nullptr, nullptr, K, D, 40.0f);
+    {
+        std::vector<uint8_t> ug((size_t)W * H);
+        ygzo_remap_linear(gray.data, W, H, W, m1.data(), m2.data(), W, H, ug.data(), W);
+        std::vector<float> ud((size_t)W * H);
+        ygzo_remap_linear_f32(depth.ptr<float>(0), W, H, W, m1.data(), m2.data(), W, H, ud.data(), W);
+        const bool g_ok = F.mImGray.cols == W && std::memcmp(F.mImGray.data, ug.data(), ug.size()) == 0;
+        const bool d_ok = F.mImDepth.cols == W && std::memcmp(F.mImDepth.data, ud.data(), ud.size() * 4) == 0;
+        ygzo_orb o4;
+        ygzo_orb_init(&o4, 2000, 1.2f, nl, 20, 7, 0);
+        int lw[YGZO_MAX_LEVELS], lh[YGZO_MAX_LEVELS];
+        ygzo_level_sizes(&o4, W, H, lw, lh);
+        std::vector<std::vector<uint8_t>> lv(nl);
+        uint8_t *lp[YGZO_MAX_LEVELS];
+        for (int l = 0; l < nl; l++) {
+            lv[l].resize((size_t)lw[l] * lh[l]);
+            lp[l] = lv[l].data();
+        }
+        ygzo_compute_pyramid(&o4, ug.data(), W, H, W, lp);
+        bool p_ok = (int)F.mvImagePyramid.size() == nl;
+        for (int l = 0; l < nl && p_ok; l++)
+            p_ok = std::memcmp(F.mvImagePyramid[l].data, lp[l], lv[l].size()) == 0;
+        CHECK(g_ok && d_ok && p_ok, "Frame::ComputeImagePyramid (RGB-D, TUM1 distortion): remap(mImGray) %s, "
+              "remap(mImDepth) CV_32F %s, pyramid %s == oracle", g_ok ? "ok" : "differs", d_ok ? "ok" : "differs",
+              p_ok ? "ok" : "differs");
+        if (g_timing) {
+            const double gm = median_ms(20, [&] {
+                Frame Fx(gray, cv::Mat(), depth, Frame::RGBD, &ex4, nullptr, nullptr, K, D, 40.0f);
+            });
+            const double cm = median_ms(5, [&] {
+                ygzo_remap_linear(gray.data, W, H, W, m1.data(), m2.data(), W, H, ug.data(), W);
+                ygzo_remap_linear_f32(depth.ptr<float>(0), W, H, W, m1.data(), m2.data(), W, H, ud.data(), W);
+                ygzo_compute_pyramid(&o4, ug.data(), W, H, W, lp);
+            });
+            std::printf("TIMING frame_undistort_pyramid_rgbd dropin_ms %.4f oracle_ms %.4f\n", gm, cm);
+        }
+        // ExtractFeatures, RGB-D branch (Frame.cc:737-750): ExtractORB(0), then ComputeStereoFromRGBD(mImDepth)
+        F.ExtractORB(0, F.mImGray);
+        F.N = (int)F.mvKeys.size();
+        F.ComputeStereoFromRGBD(F.mImDepth);
+        std::vector<float> our(F.N), odp(F.N);
+        ygzo_stereo_from_rgbd(ud.data(), W, H, W, reinterpret_cast<const ygzo_kp *>(F.mvKeys.data()), F.N, 40.0f,
+                              our.data(), odp.data());
+        int with_depth = 0;
+        for (int i = 0; i < F.N; i++) with_depth += F.mvDepth[i] > 0;
+        const bool s_ok = F.N > 500 && (int)F.mvDepth.size() == F.N &&
+                          std::memcmp(F.mvDepth.data(), odp.data(), 4 * (size_t)F.N) == 0 &&
+                          std::memcmp(F.mvuRight.data(), our.data(), 4 * (size_t)F.N) == 0;
+        CHECK(s_ok && with_depth > F.N / 2, "Frame::ComputeStereoFromRGBD(mImDepth) on the undistorted depth: %d "
+              "keypoints, %d depths == oracle", F.N, with_depth);
+    }
+    Frame::mbNeedUndistort = saved;
+
+    // ---------------- ComputeStereoMatches: a rectified EuRoC pair (right = left moved 6 px)
+    {
+        const int Ws = 752, Hs = 480, ns = 4;
+        Eigen::Matrix3f Ks;
+        Ks(0, 0) = 458.654f;
+        Ks(1, 1) = 457.296f;
+        Ks(0, 2) = 367.215f;
+        Ks(1, 2) = 248.375f;
+        Ks(2, 2) = 1.f;
+        const cv::Mat L = synth(Ws, Hs, 21u, 0, 0), R = synth(Ws, Hs, 21u, -6, 0);
+        ORBextractor exl(1000, 2.0f, ns, 20, 7), exr(1000, 2.0f, ns, 20, 7);
+        const float bf = 0.11f * Ks(0, 0);  // EuRoC.yaml Camera.bf
+        Frame S(L, R, cv::Mat(), Frame::Stereo, &exl, &exr, nullptr, Ks, cv::Mat(), bf);
+        S.ExtractORB(0, S.mImGray);
+        S.ExtractORB(1, S.mImRight);
+        S.N = (int)S.mvKeys.size();
+        S.ComputeStereoMatches();
+        ygzo_orb os;
+        ygzo_orb_init(&os, 1000, 2.0f, ns, 20, 7, 0);
+        int lw[YGZO_MAX_LEVELS], lh[YGZO_MAX_LEVELS];
+        ygzo_level_sizes(&os, Ws, Hs, lw, lh);
+        std::vector<std::vector<uint8_t>> ll(ns), rl(ns);
+        uint8_t *lp[YGZO_MAX_LEVELS], *rp[YGZO_MAX_LEVELS];
+        for (int l = 0; l < ns; l++) {
+            ll[l].resize((size_t)lw[l] * lh[l]);
+            rl[l].resize((size_t)lw[l] * lh[l]);
+            lp[l] = ll[l].data();
+            rp[l] = rl[l].data();
+        }
+        ygzo_compute_pyramid(&os, L.data, Ws, Hs, Ws, lp);
+        ygzo_compute_pyramid(&os, R.data, Ws, Hs, Ws, rp);
+        const int nr = (int)S.mvKeysRight.size();
+        std::vector<float> our(S.N), odp(S.N);
+        ygzo_stereo_matches(lp, rp, lw, lh, ns, os.scale, os.inv_scale,
+                            reinterpret_cast<const ygzo_kp *>(S.mvKeys.data()), S.mDescriptors.data, S.N,
+                            reinterpret_cast<const ygzo_kp *>(S.mvKeysRight.data()), S.mDescriptorsRight.data, nr,
+                            S.mb, S.mbf, our.data(), odp.data(), nullptr);
+        int with_depth = 0;
+        for (int i = 0; i < S.N; i++) with_depth += S.mvDepth[i] > 0;
+        const bool ok = S.N > 300 && nr > 300 && std::memcmp(S.mvDepth.data(), odp.data(), 4 * (size_t)S.N) == 0 &&
+                        std::memcmp(S.mvuRight.data(), our.data(), 4 * (size_t)S.N) == 0;
+        CHECK(ok && with_depth > S.N / 4, "Frame::ComputeStereoMatches(): %d left / %d right keypoints, %d depths "
+              "== oracle", S.N, nr, with_depth);
+        if (g_timing) {
+            const double gm = median_ms(20, [&] { S.ComputeStereoMatches(); });
+            const double cm = median_ms(5, [&] {
+                ygzo_stereo_matches(lp, rp, lw, lh, ns, os.scale, os.inv_scale,
+                                    reinterpret_cast<const ygzo_kp *>(S.mvKeys.data()), S.mDescriptors.data, S.N,
+                                    reinterpret_cast<const ygzo_kp *>(S.mvKeysRight.data()), S.mDescriptorsRight.data,
+                                    nr, S.mb, S.mbf, our.data(), odp.data(), nullptr);
+            });
+            std::printf("TIMING compute_stereo_matches dropin_ms %.4f oracle_ms %.4f\n", gm, cm);
+        }
+
+        // ---------------- ComputeBoW: a k = 10, L = 3 vocabulary bound to the Frame's ORBVocabulary
+        const int k = 10, Lv = 3;
+        std::vector<int32_t> parent(1, -1);
+        std::vector<uint8_t> leaf(1, 0);
+        int lvl_begin = 0, lvl_end = 1;
+        for (int d = 1; d <= Lv; d++) {
+            for (int p = lvl_begin; p < lvl_end; p++)
+                for (int c = 0; c < k; c++) {
+                    parent.push_back(p);
+                    leaf.push_back(d == Lv);
+                }
+            lvl_begin = lvl_end;
+            lvl_end = (int)parent.size();
+        }
+        const int nn = (int)parent.size();
+        std::vector<uint8_t> vdesc((size_t)nn * 32);
+        std::vector<double> wgt(nn);
+        unsigned sd = 12345u;
+        for (int i = 0; i < nn; i++) {
+            // a child is its parent's descriptor with a few bits flipped: a real-looking tree
+            for (int b = 0; b < 32; b++) vdesc[(size_t)32 * i + b] = i ? vdesc[(size_t)32 * parent[i] + b] : 0;
+            if (i == 0) continue;
+            for (int f = 0; f < 24; f++) {
+                sd = sd * 1664525u + 1013904223u;
+                vdesc[(size_t)32 * i + ((sd >> 8) & 31)] ^= (uint8_t)(1u << ((sd >> 16) & 7));
+            }
+            for (int b = 0; b < 32 && parent[i] == 0; b++) {  // level-1 centres: random
+                sd = sd * 1664525u + 1013904223u;
+                vdesc[(size_t)32 * i + b] = (uint8_t)(sd >> 24);
+            }
+            wgt[i] = 0.5 + (double)((sd >> 4) % 1000) / 400.0;
+        }
+        ygzfe_vocab *gv = nullptr;
+        const int rc = ygzfe_vocab_create(dropin::device(), k, Lv, 0, 0, nn, parent.data(), leaf.data(), vdesc.data(),
+                                          wgt.data(), &gv);
+        ygzo_vocab *ov = ygzo_vocab_create(k, Lv, 0, 0, nn, parent.data(), leaf.data(), vdesc.data(), wgt.data());
+        static int voc_token;  // stands for the System's ORBVocabulary object
+        gpu::BindVocabulary(&voc_token, gv);
+        S.mpORBvocabulary = reinterpret_cast<ORBVocabulary *>(&voc_token);
+        S.ComputeBoW();
+        std::vector<int32_t> ow(S.N), ofn(S.N), off(S.N);
+        std::vector<double> oval(S.N);
+        int onw = 0, onf = 0;
+        ygzo_compute_bow(ov, S.mDescriptors.data, S.N, 4, ow.data(), oval.data(), &onw, ofn.data(), off.data(), &onf);
+        bool b_ok = rc == YGZFE_OK && (int)S.mBowVec.size() == onw && onw > 20;
+        int i = 0;
+        for (auto &e : S.mBowVec) {
+            b_ok = b_ok && i < onw && (int)e.first == ow[i] && e.second == oval[i];
+            i++;
+        }
+        int j = 0;
+        for (auto &e : S.mFeatVec)
+            for (unsigned f : e.second) {
+                b_ok = b_ok && j < onf && (int)e.first == ofn[j] && (int)f == off[j];
+                j++;
+            }
+        b_ok = b_ok && j == onf;
+        CHECK(b_ok, "Frame::ComputeBoW(): BowVector %d words, FeatureVector %d entries == oracle (bound vocabulary, "
+              "%d nodes)", (int)S.mBowVec.size(), j, nn);
+        if (g_timing) {
+            const double gm = median_ms(20, [&] {
+                S.mBowVec.clear();
+                S.ComputeBoW();
+            });
+            const double cm = median_ms(5, [&] {
+                ygzo_compute_bow(ov, S.mDescriptors.data, S.N, 4, ow.data(), oval.data(), &onw, ofn.data(),
+                                 off.data(), &onf);
+            });
+            std::printf("TIMING compute_bow dropin_ms %.4f oracle_ms %.4f\n", gm, cm);
+        }
+        ygzo_vocab_destroy(ov);
+    }
 }
 
 int main(int argc, char **argv) {
@@ -756,6 +969,9 @@ int main(int argc, char **argv) {
               "%d converged", same, tried, conv);
         (void)cur_level0;
     }
+
+    // ---------------------------------------------------------------- Frame.cc's §8f rows (Frame_gpu.inc)
+    frame_rows();
 
     std::printf(fails ? "FAILED %d\n" : "OK\n", fails);
     return fails ? 1 : 0;

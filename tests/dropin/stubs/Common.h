@@ -36,6 +36,8 @@ struct Vector3f {
 
 struct Matrix3f {
     float m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    float &operator()(int r, int c) { return m[3 * r + c]; }
+    float operator()(int r, int c) const { return m[3 * r + c]; }
     Vector3f operator*(const Vector3f &p) const {
         return Vector3f(m[0] * p[0] + m[1] * p[1] + m[2] * p[2], m[3] * p[0] + m[4] * p[1] + m[5] * p[2],
                         m[6] * p[0] + m[7] * p[1] + m[8] * p[2]);
@@ -115,9 +117,16 @@ struct SE3f {
 }  // namespace Sophus
 
 namespace DBoW2 {
+typedef unsigned int WordId;
+typedef double WordValue;
 typedef unsigned int NodeId;
 typedef std::map<NodeId, std::vector<unsigned int>> FeatureVector;
+typedef std::map<WordId, WordValue> BowVector;
 }  // namespace DBoW2
+
+namespace ygz {
+class ORBVocabulary;  // TemplatedVocabulary<FORB::TDescriptor, FORB> (ORBVocabulary.h): only its address is used
+}  // namespace ygz
 
 namespace ygz {
 using namespace std;

@@ -1,10 +1,12 @@
 // Test stub of the reference's Frame (Frame.h): the members the hot-path call
-// sites read, and the two member functions whose bodies hold the call sites
-// verbatim (Frame::ExtractORB Frame.cc:332-348, Frame::ComputeImagePyramid
-// Frame.cc:807-813).  Written for the test; the drop-in ORBextractor.h comes
+// sites read, Frame::ExtractORB with its call sites verbatim (Frame.cc:332-348),
+// and ComputeImagePyramid / ComputeStereoMatches / ComputeStereoFromRGBD /
+// ComputeBoW with the drop-in bodies (compat/dropin/Frame_gpu.inc), as Frame.cc
+// would include them.  Written for the test; the drop-in ORBextractor.h comes
 // first on the include path, as it would in the reference build.
 #pragma once
 #include "Common.h"
+#include "FrameGPU.h"
 #include "ORBextractor.h"
 
 namespace ygz {
@@ -15,6 +17,7 @@ class MapPoint;
 
 class Frame {
 public:
+    typedef enum { Monocular = 0, Stereo, RGBD } SensorType;  // Frame.h:38-41
     Frame() {}
     Frame(const cv::Mat &imGray, ORBextractor *extractor) : mpORBextractorLeft(extractor), mImGray(imGray.clone()) {
         mnId = nNextId++;
@@ -30,8 +33,27 @@ public:
         ComputeImagePyramid();
     }
 
+    // the stereo / RGB-D constructors' parts that reach the §8f rows (Frame.cc:181-236):
+    // members set, then ComputeImagePyramid (undistortion of every image included)
+    Frame(const cv::Mat &imLeft, const cv::Mat &imRight, const cv::Mat &imDepth, SensorType sensor,
+          ORBextractor *extractorLeft, ORBextractor *extractorRight, ORBVocabulary *voc, const Eigen::Matrix3f &K,
+          const cv::Mat &distCoef, float bf)
+        : mbf(bf), mpORBvocabulary(voc), mK(K), mDistCoef(distCoef.clone()), mSensor(sensor),
+          mImDepth(imDepth.clone()), mpORBextractorLeft(extractorLeft), mpORBextractorRight(extractorRight),
+          mImGray(imLeft.clone()), mImRight(imRight.clone()) {
+        mnId = nNextId++;
+        mb = mbf / K(0, 0);
+        mnScaleLevels = mpORBextractorLeft->GetLevels();
+        mvScaleFactors = mpORBextractorLeft->GetScaleFactors();
+        mvInvScaleFactors = mpORBextractorLeft->GetInverseScaleFactors();
+        ComputeImagePyramid();
+    }
+
     void ExtractORB(int flag, const cv::Mat &im);
     void ComputeImagePyramid();
+    void ComputeStereoMatches();
+    void ComputeStereoFromRGBD(const cv::Mat &imDepth);
+    void ComputeBoW();
     void ExtractFeatures() {  // the parts of Frame.cc:717-771 the searches depend on
         ExtractORB(0, mImGray);
         N = mvKeys.size();
@@ -55,6 +77,13 @@ public:
     std::vector<bool> mvbOutlier;
     std::vector<int> mvMatchedFrom;
     DBoW2::FeatureVector mFeatVec;
+    DBoW2::BowVector mBowVec;
+    ORBVocabulary *mpORBvocabulary = nullptr;
+    Eigen::Matrix3f mK;
+    cv::Mat mDistCoef;
+    static bool mbNeedUndistort;
+    SensorType mSensor = Monocular;
+    cv::Mat mImDepth;
     SE3f mTcw;
     std::vector<cv::Mat> mvImagePyramid;
     int mnScaleLevels = 0;
@@ -81,13 +110,6 @@ inline void Frame::ExtractORB(int flag, const cv::Mat &im) {
         }
 }
 
-// Frame.cc:807-813 verbatim (the undistortion before it is out of this test)
-inline void Frame::ComputeImagePyramid() {
-        mpORBextractorLeft->ComputePyramid(mImGray);
-
-        mvImagePyramid.resize(mpORBextractorLeft->GetLevels());
-        for (int l = 0; l < mpORBextractorLeft->GetLevels(); l++) {
-            mvImagePyramid[l] = mpORBextractorLeft->mvImagePyramid[l].clone();
-        }
-}
+// Frame.cc:495-500, 509-700, 773-813: the drop-in bodies
+#include "Frame_gpu.inc"
 }  // namespace ygz

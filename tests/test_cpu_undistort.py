@@ -97,3 +97,45 @@ def test_remap_fully_outside_is_zero():
     m1[..., 1] = 3
     out = O.remap_linear(img, m1, np.full((H, W), 16, np.uint16))
     assert (out == 100).all()
+
+
+def _remap_f32_numpy(src, m1, m2):
+    """A second, vectorised restatement of remapBilinear<float> (BORDER_CONSTANT 0): the
+    float weights c_y * c_x, summed S00 w0 + S01 w1 + S10 w2 + S11 w3 in float32."""
+    H, W = src.shape
+    sx, sy = m1[..., 0].astype(np.int64), m1[..., 1].astype(np.int64)
+    tx, ty = (m2 & 31).astype(np.float32), (m2 >> 5).astype(np.float32)
+    f32 = np.float32
+    cx1, cy1 = tx * f32(1 / 32), ty * f32(1 / 32)
+    cx0, cy0 = f32(1) - cx1, f32(1) - cy1
+    w = [cy0 * cx0, cy0 * cx1, cy1 * cx0, cy1 * cx1]
+
+    def tap(x, y):
+        ok = (x >= 0) & (x < W) & (y >= 0) & (y < H)
+        return np.where(ok, src[np.clip(y, 0, H - 1), np.clip(x, 0, W - 1)], f32(0)).astype(np.float32)
+
+    v = [tap(sx, sy), tap(sx + 1, sy), tap(sx, sy + 1), tap(sx + 1, sy + 1)]
+    out = ((v[0] * w[0] + v[1] * w[1]).astype(np.float32) + v[2] * w[2]).astype(np.float32) + v[3] * w[3]
+    outside = (sx >= W) | (sx + 1 < 0) | (sy >= H) | (sy + 1 < 0)
+    return np.where(outside, f32(0), out.astype(np.float32)).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", ["tum1", "odd", "wild"])
+def test_remap_f32_matches_numpy_restatement(name):
+    """Frame.cc:799-804 (the RGB-D depth remap): the C restatement equals an independent
+    vectorised one bit for bit, including the BORDER_CONSTANT edge taps."""
+    cam, dist, (W, H) = CAM.ALL[name]
+    m1, m2 = O.undistort_map(cam, dist, W, H)
+    rng = np.random.default_rng(3)
+    src = (rng.random((H, W)) * 4.0).astype(np.float32)
+    src[rng.random((H, W)) < 0.05] = 0.0
+    got = O.remap_linear_f32(src, m1, m2)
+    want = _remap_f32_numpy(src, m1, m2)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_remap_f32_zero_distortion_is_copy():
+    cam, _, (W, H) = CAM.TUM1
+    m1, m2 = O.undistort_map(cam, (), W, H)
+    src = np.random.default_rng(5).random((H, W)).astype(np.float32)
+    assert np.array_equal(O.remap_linear_f32(src, m1, m2), src)

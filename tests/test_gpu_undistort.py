@@ -135,3 +135,70 @@ def test_size_mismatch_fails_loudly(gpu):
         b.upload_undistorted(und, np.zeros((1, 480, 752), np.uint8))
     with pytest.raises(gpu.YgzfeError):
         gpu.Undistort(cam, np.zeros(13, np.float32), 64, 64)
+
+
+def _depth_image(seed, W, H):
+    """TUM-like CV_32F depth (Tracking.cc GrabImageRGBD: uint16 / 5000 -> metres): a tilted
+    plane with steps, holes (0 = no depth) and a few large values."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    d = (0.8 + 0.002 * xx + 0.003 * yy + 0.25 * ((xx // 97 + yy // 71) % 3)).astype(np.float32)
+    raw = np.round(d * 5000).astype(np.uint16)
+    raw[rng.random((H, W)) < 0.05] = 0
+    raw[rng.random((H, W)) < 0.001] = 65535
+    return (raw.astype(np.float32) * np.float32(1.0 / 5000)).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", sorted(CAM.ALL))
+def test_remap_depth_f32_bitexact(gpu, name):
+    """Frame.cc:799-804 (RGB-D): remap(mImDepth, map1, map2, INTER_LINEAR) on CV_32F, host in / out
+    and batched on the device, bit-exact against the oracle's float remapBilinear."""
+    import torch
+    cam, dist, (W, H) = CAM.ALL[name]
+    und = gpu.Undistort(cam, dist, W, H)
+    m1, m2 = O.undistort_map(cam, dist, W, H)
+    depths = [_depth_image(s, W, H) for s in range(3)]
+    for d in depths[:1]:
+        got = und.remap_depth(d)
+        ref = O.remap_linear_f32(d, m1, m2)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), \
+            f"{np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))} px differ"
+        assert (ref > 0).mean() > 0.5
+    src = torch.from_numpy(np.stack(depths)).cuda()
+    pitch = W * H + 16
+    dst = torch.full((3, pitch), -1.0, dtype=torch.float32, device="cuda")
+    und.apply_f32_device(src.data_ptr(), W * H, W, dst.data_ptr(), pitch, W, 3)
+    out = dst.cpu().numpy()
+    for i, d in enumerate(depths):
+        ref = O.remap_linear_f32(d, m1, m2)
+        assert np.array_equal(out[i, :W * H].reshape(H, W).view(np.uint32), ref.view(np.uint32)), f"image {i}"
+        assert (out[i, W * H:] == -1.0).all(), "wrote past the image"
+
+
+def test_remap_image_host_bitexact(gpu):
+    """The u8 host-in / host-out remap the drop-in Frame::ComputeImagePyramid uses (Frame.cc:786-797)."""
+    for name in ("tum1", "odd"):
+        cam, dist, (W, H) = CAM.ALL[name]
+        und = gpu.Undistort(cam, dist, W, H)
+        m1, m2 = O.undistort_map(cam, dist, W, H)
+        img = S.frame(4, W, H)
+        assert np.array_equal(und.remap_image(img), O.remap_linear(img, m1, m2)), name
+
+
+def test_rgbd_depth_undistorted_then_stereo(gpu):
+    """The C4 (TUM1, distorted) RGB-D path: depth undistorted (Frame.cc:799-804) then
+    ComputeStereoFromRGBD (:684-700) at the undistorted keypoints, both against the oracle."""
+    cam, dist, (W, H) = CAM.TUM1
+    und = gpu.Undistort(cam, dist, W, H)
+    m1, m2 = O.undistort_map(cam, dist, W, H)
+    _, _, nf, sf, nl, ini, mn = S.CONFIGS["C4"]
+    img = und.remap_image(S.frame(9, W, H))
+    ex = gpu.ORBextractor(nf, sf, nl, ini, mn, device=0)
+    kps, _ = ex.extract(ex.ComputePyramid(img))
+    depth = _depth_image(9, W, H)
+    dg = und.remap_depth(depth)
+    ur, dp = gpu.stereo_from_rgbd(dg, kps, 40.0)
+    dref = O.remap_linear_f32(depth, m1, m2)
+    rur, rdp = O.stereo_from_rgbd(dref, kps, 40.0)
+    assert np.array_equal(dp, rdp) and np.array_equal(ur, rur)
+    assert (dp > 0).mean() > 0.5
