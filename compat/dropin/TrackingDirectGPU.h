@@ -39,7 +39,13 @@ inline ygzfe_se3 to_se3(const SE3 &T) {
 // with their candidate observations (SelectNearestKeyframe order, <= 5 keyframes).
 class DirectBatch {
 public:
+    DirectBatch() = default;
+    DirectBatch(const DirectBatch &) = delete;
+    DirectBatch &operator=(const DirectBatch &) = delete;
+    ~DirectBatch() { release(); }
+
     void clear() {
+        release();
         item_ptr_.assign(1, 0);
         ref_index_.clear();
         kps_.clear();
@@ -88,12 +94,12 @@ public:
         ygzfe_frame *cf = dropin::PyramidPool::instance().find_or_upload(cur.mvImagePyramid);
         if (!cf) return fail("the current frame pyramid could not be placed on the device");
         const ygzfe_camera cam{FrameT::fx, FrameT::fy, FrameT::cx, FrameT::cy};
-        if (ygzfe_search_local_points_direct(refs_.data(), (int)refs_.size(), cf, &cam, n_cache, n - n_cache,
-                                             item_ptr_.data(), ref_index_.data(), kps_.data(), pt_ref_.data(),
-                                             T_cr_.data(), px_proj_.data(), border, grid_size, cache_hit_th,
-                                             px_out_.data(), matched_.data(), status_.data(), &cache_success_,
-                                             &local_ran_) != YGZFE_OK)
-            return fail(ygzfe_last_error());
+        const int rc = ygzfe_search_local_points_direct(
+            refs_.data(), (int)refs_.size(), cf, &cam, n_cache, n - n_cache, item_ptr_.data(), ref_index_.data(),
+            kps_.data(), pt_ref_.data(), T_cr_.data(), px_proj_.data(), border, grid_size, cache_hit_th,
+            px_out_.data(), matched_.data(), status_.data(), &cache_success_, &local_ran_);
+        release();  // the call has read the keyframe pyramids
+        if (rc != YGZFE_OK) return fail(ygzfe_last_error());
         return true;
     }
 
@@ -108,14 +114,23 @@ private:
     int slot_of(KeyFrameT *ref) {
         auto it = slot_.find((const void *)ref);
         if (it != slot_.end()) return it->second;
-        // every keyframe of the call must stay resident until the call (and the current frame's lookup)
-        if ((int)refs_.size() + 2 > dropin::PyramidPool::capacity()) ok_ = false;
+        // every keyframe of the call stays resident until the call: pinned in the pool,
+        // which grows past its soft capacity for a large local map instead of failing
         ygzfe_frame *f = dropin::PyramidPool::instance().find_or_upload(ref->mvImagePyramid);
-        if (!f) ok_ = false;
+        if (!f) {
+            ok_ = false;
+        } else {
+            dropin::PyramidPool::instance().pin(f, 1);
+            pinned_.push_back(f);
+        }
         const int s = (int)refs_.size();
         refs_.push_back(f);
         slot_[(const void *)ref] = s;
         return s;
+    }
+    void release() {
+        for (const ygzfe_frame *f : pinned_) dropin::PyramidPool::instance().pin(f, -1);
+        pinned_.clear();
     }
     bool fail(const char *why) {
         dropin::log_once("SearchLocalPointsDirect", why);
@@ -126,7 +141,7 @@ private:
     std::vector<float> pt_ref_, px_proj_, px_out_;
     std::vector<ygzfe_se3> T_cr_;
     std::vector<long> kf_id_;
-    std::vector<const ygzfe_frame *> refs_;
+    std::vector<const ygzfe_frame *> refs_, pinned_;
     std::map<const void *, int> slot_;
     int cache_success_ = 0, local_ran_ = 1;
     bool ok_ = true;

@@ -13,10 +13,11 @@
 //
 // Device pyramids: Frame::ComputeImagePyramid computes the pyramid through the
 // extractor (ComputePyramid, then clones mvImagePyramid, Frame.cc:807-813).
-// The extractor leaves the device copy in a small process-wide pool keyed by
-// the level-0 bytes; a later call that receives the Frame's (cloned) host
-// pyramid finds it there after one memcmp of level 0, and uploads the host
-// levels only when the pool has no copy (a Frame built some other way).
+// The extractor leaves the device copy in a process-wide pool; a later call that
+// receives the Frame's (cloned) host pyramid finds it by its level-0 pointer and
+// a content fingerprint (one full compare of level 0 the first time a pointer is
+// seen), and uploads the host levels only when the pool has no copy (a Frame
+// built some other way).
 #ifndef YGZFE_DROPIN_H_
 #define YGZFE_DROPIN_H_
 
@@ -29,6 +30,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "ygzfe.h"
@@ -64,54 +66,83 @@ public:
     }
 
     // The device pyramid of `img` (level 0, w x h, row stride) computed by `ex`;
-    // the returned frame stays valid until kCapacity newer pyramids have been made.
+    // the returned frame stays valid until soft_capacity() newer pyramids have been made
+    // (unless pinned).
     ygzfe_frame *compute(ygzfe_extractor *ex, int nlevels, const uint8_t *img, int w, int h, size_t stride) {
         std::lock_guard<std::mutex> lk(mu_);
-        Entry &e = slot(ex, nlevels, w, h);
-        if (!e.f) return nullptr;
-        e.level0.resize((size_t)w * h);
-        for (int y = 0; y < h; y++) std::memcpy(&e.level0[(size_t)y * w], img + (size_t)y * stride, (size_t)w);
-        if (ygzfe_compute_pyramid(ex, e.f, e.level0.data(), w) != YGZFE_OK) {
-            e.level0.clear();
+        Entry *e = slot(ex, nlevels, w, h);
+        if (!e || !e->f) return nullptr;
+        e->level0.resize((size_t)w * h);
+        for (int y = 0; y < h; y++) std::memcpy(&e->level0[(size_t)y * w], img + (size_t)y * stride, (size_t)w);
+        if (ygzfe_compute_pyramid(ex, e->f, e->level0.data(), w) != YGZFE_OK) {
+            e->level0.clear();
             return nullptr;
         }
-        return e.f;
+        set_fp(e, fingerprint(e->level0.data(), w, h, (size_t)w));
+        return e->f;
     }
 
     // The device copy of a host pyramid (levels[l]: .data / .cols / .rows / .step).
-    // An entry whose level 0 last came from the same host pointer is checked
-    // first (a KeyFrame shares its Frame's pyramid, KeyFrame.cc:257-260, so a
-    // keyframe is found on its first entry); every hit is confirmed by a full
-    // compare of level 0, so a reused host buffer never returns a stale pyramid.
+    // Lookup by the host level-0 pointer, guarded by a content fingerprint (18 whole
+    // rows and 2,048 bytes spread over level 0, hashed: ~3 us), so a hit costs no full
+    // compare.  A pointer seen for the first time is matched to an entry with the same
+    // fingerprint by one full compare of level 0 (once per host pyramid: a Frame clones
+    // the extractor's levels, Frame.cc:812; a KeyFrame shares its Frame's, KeyFrame.cc:
+    // 257-260), so a reused host buffer never returns a stale pyramid unless new
+    // content matched every sampled byte of the old.
     template <class MatVec>
     ygzfe_frame *find_or_upload(const MatVec &levels) {
-        if (levels.empty()) return nullptr;
-        const int w = levels[0].cols, h = levels[0].rows;
+        if (levels.empty() || !levels[0].data) return nullptr;
+        const int w = levels[0].cols, h = levels[0].rows, nl = (int)levels.size();
         const uint8_t *key = levels[0].data;
+        const size_t stride = (size_t)levels[0].step[0];
+        const uint64_t fp = fingerprint(key, w, h, stride);
         std::lock_guard<std::mutex> lk(mu_);
-        for (int pass = 0; pass < 2; pass++)
-            for (auto it = lru_.begin(); it != lru_.end(); ++it) {
-                if ((pass == 0) != (it->host_ptr == key)) continue;
-                if (it->w == w && it->h == h && it->nlevels == (int)levels.size() && same_level0(*it, levels[0])) {
-                    it->host_ptr = key;
-                    lru_.splice(lru_.begin(), lru_, it);
-                    return lru_.front().f;
-                }
+        auto ip = by_ptr_.find(key);
+        if (ip != by_ptr_.end()) {
+            Entry *e = ip->second;
+            if (e->fp == fp && e->w == w && e->h == h && e->nlevels == nl) return touch(e)->f;
+            by_ptr_.erase(ip);  // the buffer holds other content now
+            e->host_ptr = nullptr;
+        }
+        auto range = by_fp_.equal_range(fp);
+        for (auto it = range.first; it != range.second; ++it) {
+            Entry *e = it->second;
+            if (e->w == w && e->h == h && e->nlevels == nl && same_level0(*e, key, stride)) {
+                bind_ptr(e, key);
+                return touch(e)->f;
             }
+        }
         if (!ex_) return nullptr;  // no extractor yet: nothing defines the level geometry
-        Entry &e = slot(ex_, (int)levels.size(), w, h);
-        if (!e.f) return nullptr;
-        for (int l = 0; l < (int)levels.size(); l++)
-            if (ygzfe_frame_set_level(e.f, l, levels[l].data, (int)levels[l].step[0]) != YGZFE_OK) return nullptr;
-        e.level0.resize((size_t)w * h);
-        for (int y = 0; y < h; y++)
-            std::memcpy(&e.level0[(size_t)y * w], levels[0].data + (size_t)y * levels[0].step[0], (size_t)w);
-        e.host_ptr = key;
-        return e.f;
+        Entry *e = slot(ex_, nl, w, h);
+        if (!e || !e->f) return nullptr;
+        for (int l = 0; l < nl; l++)
+            if (ygzfe_frame_set_level(e->f, l, levels[l].data, (int)levels[l].step[0]) != YGZFE_OK) return nullptr;
+        e->level0.resize((size_t)w * h);
+        for (int y = 0; y < h; y++) std::memcpy(&e->level0[(size_t)y * w], key + (size_t)y * stride, (size_t)w);
+        set_fp(e, fp);
+        bind_ptr(e, key);
+        return e->f;
     }
 
-    // pyramids a caller may hold at once (a newer lookup can recycle an older entry)
-    static int capacity() { return kCapacity; }
+    // Entries a caller needs together (a SearchLocalPointsDirect phase's keyframes)
+    // are pinned: they are never recycled, and the pool grows past its soft capacity
+    // rather than fail when every entry is pinned.
+    void pin(const ygzfe_frame *f, int delta) {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (Entry &e : lru_)
+            if (e.f == f) {
+                e.pins += delta;
+                return;
+            }
+    }
+
+    // pyramids a caller may hold unpinned at once (a newer lookup can recycle an older entry)
+    static int soft_capacity() { return kCapacity; }
+    int size() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return (int)lru_.size();
+    }
 
     // the extractor whose level geometry uploads use (the latest one constructed)
     void set_extractor(ygzfe_extractor *ex, int nlevels) {
@@ -123,6 +154,7 @@ public:
         std::lock_guard<std::mutex> lk(mu_);
         for (auto it = lru_.begin(); it != lru_.end();)
             if (it->ex == ex) {
+                unindex(&*it);
                 ygzfe_frame_destroy(it->f);
                 it = lru_.erase(it);
             } else {
@@ -132,32 +164,105 @@ public:
     }
 
 private:
-    // a local map's keyframes (SearchLocalPointsDirect: <= 5 per map point, the
-    // local keyframe set is capped at 80, Tracking.cc UpdateLocalKeyFrames) plus the
-    // frames in flight: 96 pyramids of 752 x 480 are ~46 MB of HBM
+    // a local map's keyframes plus the frames in flight: 96 pyramids of 752 x 480 are
+    // ~46 MB of HBM; pinned entries may take the pool past it
     static constexpr int kCapacity = 96;
     struct Entry {
         ygzfe_extractor *ex = nullptr;
         ygzfe_frame *f = nullptr;
-        int w = 0, h = 0, nlevels = 0;
+        int w = 0, h = 0, nlevels = 0, pins = 0;
         const uint8_t *host_ptr = nullptr;  // the host level 0 this content was last seen at
+        uint64_t fp = 0;
+        bool has_fp = false;
         std::vector<uint8_t> level0;
+        std::list<Entry>::iterator self;  // its own position in lru_ (list iterators are stable)
     };
-    template <class Mat>
-    static bool same_level0(const Entry &e, const Mat &m) {
+    static uint64_t mix(uint64_t h, uint64_t v) {
+        h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+        return h * 0xBF58476D1CE4E5B9ull;
+    }
+    // 18 whole rows (first, last, 16 spread) + 2,048 bytes on a stride coprime to the width
+    static uint64_t fingerprint(const uint8_t *p, int w, int h, size_t stride) {
+        uint64_t f = mix((uint64_t)w, (uint64_t)h);
+        if (w <= 0 || h <= 0) return f;
+        for (int k = 0; k < 18; k++) {
+            const int y = k == 0 ? 0 : (k == 17 ? h - 1 : (int)((long)k * h / 17));
+            const uint8_t *r = p + (size_t)y * stride;
+            uint64_t acc = 0;
+            int x = 0;
+            for (; x + 8 <= w; x += 8) {
+                uint64_t v;
+                std::memcpy(&v, r + x, 8);
+                acc = mix(acc, v);
+            }
+            for (; x < w; x++) acc = mix(acc, r[x]);
+            f = mix(f, acc);
+        }
+        const size_t n = (size_t)w * h, step = n / 2048 + 1;
+        size_t i = 7 % n;
+        for (int k = 0; k < 2048; k++, i = (i + step * 2 + 1) % n) f = mix(f, p[(i / w) * stride + i % w]);
+        return f;
+    }
+    bool same_level0(const Entry &e, const uint8_t *p, size_t stride) const {
         if (e.level0.size() != (size_t)e.w * e.h) return false;
         for (int y = 0; y < e.h; y++)
-            if (std::memcmp(&e.level0[(size_t)y * e.w], m.data + (size_t)y * m.step[0], (size_t)e.w) != 0) return false;
+            if (std::memcmp(&e.level0[(size_t)y * e.w], p + (size_t)y * stride, (size_t)e.w) != 0) return false;
         return true;
     }
-    // a free (least recently used) entry for a w x h pyramid of `ex`, moved to the front
-    Entry &slot(ygzfe_extractor *ex, int nlevels, int w, int h) {
-        if ((int)lru_.size() >= kCapacity) {
-            lru_.splice(lru_.begin(), lru_, std::prev(lru_.end()));
+    Entry *touch(Entry *e) {
+        lru_.splice(lru_.begin(), lru_, e->self);
+        return e;
+    }
+    void unindex(Entry *e) {
+        if (e->host_ptr) {
+            auto ip = by_ptr_.find(e->host_ptr);
+            if (ip != by_ptr_.end() && ip->second == e) by_ptr_.erase(ip);
+            e->host_ptr = nullptr;
+        }
+        if (e->has_fp) {
+            auto range = by_fp_.equal_range(e->fp);
+            for (auto it = range.first; it != range.second; ++it)
+                if (it->second == e) {
+                    by_fp_.erase(it);
+                    break;
+                }
+            e->has_fp = false;
+        }
+    }
+    void set_fp(Entry *e, uint64_t fp) {
+        e->fp = fp;
+        e->has_fp = true;
+        by_fp_.insert(std::make_pair(fp, e));
+    }
+    void bind_ptr(Entry *e, const uint8_t *key) {
+        if (e->host_ptr && e->host_ptr != key) {
+            auto ip = by_ptr_.find(e->host_ptr);
+            if (ip != by_ptr_.end() && ip->second == e) by_ptr_.erase(ip);
+        }
+        auto ip = by_ptr_.find(key);
+        if (ip != by_ptr_.end() && ip->second != e) ip->second->host_ptr = nullptr;
+        by_ptr_[key] = e;
+        e->host_ptr = key;
+    }
+    // a free (least recently used, unpinned) entry for a w x h pyramid of `ex`, at the front
+    Entry *slot(ygzfe_extractor *ex, int nlevels, int w, int h) {
+        auto victim = lru_.end();
+        if ((int)lru_.size() >= kCapacity)
+            for (auto it = lru_.end(); it != lru_.begin();) {
+                --it;
+                if (it->pins == 0) {
+                    victim = it;
+                    break;
+                }
+            }
+        if (victim != lru_.end()) {
+            lru_.splice(lru_.begin(), lru_, victim);
         } else {
             lru_.emplace_front();
         }
         Entry &e = lru_.front();
+        e.self = lru_.begin();
+        unindex(&e);
         if (!e.f || e.ex != ex || e.w != w || e.h != h) {
             ygzfe_frame_destroy(e.f);
             e.f = nullptr;
@@ -167,12 +272,14 @@ private:
         e.w = w;
         e.h = h;
         e.nlevels = nlevels;
-        e.host_ptr = nullptr;
+        e.pins = 0;
         e.level0.clear();
-        return e;
+        return &e;
     }
     std::mutex mu_;
     std::list<Entry> lru_;
+    std::unordered_map<const uint8_t *, Entry *> by_ptr_;
+    std::unordered_multimap<uint64_t, Entry *> by_fp_;
     ygzfe_extractor *ex_ = nullptr;
     int nlevels_ = 0;
 };

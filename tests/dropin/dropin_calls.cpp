@@ -537,7 +537,7 @@ int main(int argc, char **argv) {
                 Frame Fx(im1, T.mpORBextractorLeft);
                 Fx.ExtractFeatures();
             };
-            for (int i = 0; i < dropin::PyramidPool::capacity() + 4; i++) one();
+            for (int i = 0; i < dropin::PyramidPool::soft_capacity() + 4; i++) one();
             const double ge = median_ms(30, one);
             const double gp = median_ms(30, [&] { T.mpORBextractorLeft->ComputePyramid(im1); });
             const double gf = median_ms(30, [&] { Frame Fx(im1, T.mpORBextractorLeft); });
@@ -750,27 +750,37 @@ int main(int argc, char **argv) {
     }
 
     // ---------------------------------------------------------------- SearchLocalPointsDirect + FindDirectProjection
-    {
-        // three keyframes of the plane: A = the last frame (identity pose), B and C shifted images
-        // (image shift (dx, dy) <=> T_cw translation (dx Z / fx, dy Z / fy, 0)); C is mpLastKeyFrame,
-        // which SelectNearestKeyframe leaves out
-        const int shifts[3][2] = {{0, 0}, {-1, 1}, {3, 2}};
-        const cv::Mat kim[3] = {im0, synth(W, H, 7u, -1, 1), synth(W, H, 7u, 3, 2)};
-        std::vector<KeyFrame> kfs(3);
-        std::vector<Frame> kframes;
-        kframes.reserve(3);
-        for (int k = 0; k < 3; k++) {
-            kframes.push_back(Frame(kim[k], T.mpORBextractorLeft));
+    // NK keyframes of the plane: A = the last frame (identity pose), B, C, ... shifted images
+    // (image shift (dx, dy) <=> T_cw translation (dx Z / fx, dy Z / fy, 0)); C is mpLastKeyFrame,
+    // which SelectNearestKeyframe leaves out.  NK = 100 first: a local map larger than the
+    // pyramid pool's soft capacity (96), whose keyframes a phase pins; then NK = 3, whose state
+    // the FindDirectProjection checks below reuse.
+    std::vector<KeyFrame> kfs;
+    std::vector<Frame> kframes;
+    std::vector<MapPoint> dm;
+    std::vector<uint8_t *> rp;
+    for (const int NK : {100, 3}) {
+        kfs.clear();
+        kframes.clear();
+        kfs.resize(NK);
+        kframes.reserve(NK);
+        auto shift = [](int k, int c) {
+            static const int s3[3][2] = {{0, 0}, {-1, 1}, {3, 2}};
+            return k < 3 ? s3[k][c] : (c == 0 ? (k * 5) % 9 - 4 : (k * 3) % 7 - 3);
+        };
+        for (int k = 0; k < NK; k++) {
+            const cv::Mat kim = k == 0 ? im0 : synth(W, H, 7u, shift(k, 0), shift(k, 1));
+            kframes.push_back(Frame(kim, T.mpORBextractorLeft));
             kfs[k].mvImagePyramid = kframes[k].mvImagePyramid;  // shared, as KeyFrame.cc:257-260
             kfs[k].mvScaleFactors = kframes[k].mvScaleFactors;
-            kfs[k].mTcw = SE3f(Eigen::Quaternionf(), Vector3f(shifts[k][0] * Z / Frame::fx, shifts[k][1] * Z / Frame::fy, 0.f));
+            kfs[k].mTcw = SE3f(Eigen::Quaternionf(), Vector3f(shift(k, 0) * Z / Frame::fx, shift(k, 1) * Z / Frame::fy, 0.f));
             kfs[k].mnId = 10 + k;
         }
         T.mpLastKeyFrame = &kfs[2];
         // map points: the last frame's keypoints on the plane, plus a neighbour 0.6 px away after every
         // third one (neighbours share cells of the 5-px coverage grid)
         const Frame &L = T.mLastFrame;
-        std::vector<MapPoint> dm;
+        dm.clear();
         dm.reserve(2 * L.N);
         for (int i = 0; i < L.N; i++) {
             for (int c = 0; c < 1 + (i % 3 == 0); c++) {
@@ -785,9 +795,10 @@ int main(int argc, char **argv) {
         for (size_t j = 0; j < dm.size(); j++) {
             MapPoint &mp = dm[j];
             const int oc = (int)(j % 3);
-            for (int k = 0; k < 3; k++) {
+            for (int k = 0; k < NK; k++) {
                 if (k == 0 && j % 5 == 1) continue;  // observed by B / C only
                 if (k == 1 && j % 4 == 2) continue;
+                if (k >= 3 && (j + 7 * (size_t)k) % 17 != 0) continue;  // NK = 100: ~6 more keyframes per point
                 const Vector3f pc = kfs[k].mTcw * mp.mWorldPos;
                 cv::KeyPoint kp(cv::Point2f(Frame::fx * pc[0] / pc[2] + Frame::cx, Frame::fy * pc[1] / pc[2] + Frame::cy),
                                 31.f * kfs[k].mvScaleFactors[oc], -1, 0, oc);
@@ -804,8 +815,8 @@ int main(int argc, char **argv) {
         // expected: the oracle over the same filters and items (ORBmatcher.cc:1577-1582 inputs formed here)
         uint8_t *cp[YGZO_MAX_LEVELS];
         for (int l = 0; l < nl; l++) cp[l] = C.mvImagePyramid[l].data;
-        std::vector<uint8_t *> rp(3 * nl);
-        for (int k = 0; k < 3; k++)
+        rp.assign((size_t)NK * nl, nullptr);
+        for (int k = 0; k < NK; k++)
             for (int l = 0; l < nl; l++) rp[k * nl + l] = kfs[k].mvImagePyramid[l].data;
         ygzo_cam ocam{Frame::fx, Frame::fy, Frame::cx, Frame::cy};
         struct Want {
@@ -911,10 +922,14 @@ int main(int argc, char **argv) {
                 same = C.mvKeys[i].pt.x == w.keys[i].pt.x && C.mvKeys[i].pt.y == w.keys[i].pt.y &&
                        C.mvKeys[i].size == 7.f && C.mvKeys[i].angle == -1.f;
             CHECK(same && w.keys.size() > 100,
-                  "SearchLocalPointsDirect() [mnCacheHitTh %d]: %zu points tracked (oracle %zu), local map %s, "
-                  "cache %zu -> %zu", th, C.mvKeys.size(), w.keys.size(), w.local_runs ? "searched" : "skipped",
-                  cache0.size(), T.mvpDirectMapPointsCache.size());
-            if (g_timing && th == 150) {
+                  "SearchLocalPointsDirect() [%d keyframes, mnCacheHitTh %d]: %zu points tracked (oracle %zu), local "
+                  "map %s, cache %zu -> %zu", NK, th, C.mvKeys.size(), w.keys.size(),
+                  w.local_runs ? "searched" : "skipped", cache0.size(), T.mvpDirectMapPointsCache.size());
+            if (NK > dropin::PyramidPool::soft_capacity() && th == 150)
+                CHECK(dropin::PyramidPool::instance().size() > dropin::PyramidPool::soft_capacity(),
+                      "  the pyramid pool grew past its soft capacity for the pinned keyframes: %d entries",
+                      dropin::PyramidPool::instance().size());
+            if (g_timing && th == 150 && NK == 3) {
                 auto run = [&] {
                     C.mvKeys.clear();
                     C.mvpMapPoints.clear();
@@ -935,6 +950,7 @@ int main(int argc, char **argv) {
                             local.size() + cache0.size());
             }
         }
+        if (NK == 3) {
 
         // ORBmatcher::FindDirectProjection, one pair at a time, against the oracle
         ORBmatcher matcher;
@@ -968,6 +984,7 @@ int main(int argc, char **argv) {
               "matcher.FindDirectProjection(ob.first, &mCurrentFrame, mp, px_curr, level): %d / %d bit-exact, "
               "%d converged", same, tried, conv);
         (void)cur_level0;
+        }
     }
 
     // ---------------------------------------------------------------- Frame.cc's §8f rows (Frame_gpu.inc)
