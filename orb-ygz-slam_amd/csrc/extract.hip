@@ -510,9 +510,8 @@ __global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(const uint8_t *__re
 }
 
 // ---------------------------------------------------------------------------
-// FAST-9/16 + cornerScore<16> + 3x3 non-max suppression inside one cell ROI
-// (ORBextractor.cc:747-781).  One 256-thread workgroup per (cell, frame).
-
+// FAST-9/16 + cornerScore<16> + 3x3 non-max suppression inside each cell ROI
+// (ORBextractor.cc:747-781).
 
 // Ring taps on a ROI tile of row stride S (compile time, so every ring tap is
 // an immediate ds_read offset from q = centre - 3S - 3).
@@ -541,59 +540,44 @@ __device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
     return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
 
-// One wave per cell (four per 256-thread workgroup), each with a dynamic-LDS
-// slice: ROI tile S*S, score map S*S, pixel list 2*(S-6)^2.  Per threshold:
-//   A  every interior pixel: 4-point necessary test -- a 9-arc holds a
-//      neighbouring pair of the compass points 0/4/8/12, i.e.
-//      (p0|p8) & (p4|p12) -- 4 pixels per lane on packed i16 pairs;
-//      survivors compacted (ballot + mbcnt) into the list
-//   B  survivors: full segment test, corners compacted in place
-//   C  corners: score into the map
-//   D  corners: strict 3x3 non-max suppression, survivors -> cell list
-// Every list keeps raster order, so the output order is cv::FAST's.
-// ROI staging: lane = (row offset, dword) with S/4 dwords per LDS row; each
-// lane reads the two aligned dwords around its 4 bytes (issue) and realigns
-// them with v_alignbyte into one ds_write_b32 (commit).  NI loads per lane.
-// Loads are buffer loads on the frame's level (wave-uniform descriptor, 32-bit
-// lane offsets, one 24-bit multiply-add per row; reads past the level return 0).
-// YGZ_FAST_SHIFT = 1: every ROI row is staged one byte to the right (LDS byte c + 1
-// of the row holds ROI column c), so the dword holding interior pixels 4j..4j+3
-// (ROI columns 4j+3..4j+6) is aligned: phase A reads 5 dwords per 4 pixels
-// instead of 7.  Needs S >= ROI width + 1.
-#ifndef YGZ_FAST_SHIFT
-#define YGZ_FAST_SHIFT 0
-#endif
-// a wave's LDS slice (16-B aligned): ROI tile S*R, score map, pixel list.  Shifted, the
-// interior is at most S - 7 wide and the score map R - 2 rows (see the zeroing in
-// fast_cell_item), so C2 level 0 fits a (40, 38) slice of 5,072 B: 8 workgroups per CU
+// Two FAST paths share the segment test below:
+//   k_fast_strips (every launch): one wave per strip -- <= 8 consecutive cells of one
+//     cell row -- stages the strip's band (the cells' ROI rows, 256 columns) in LDS once,
+//     screens every interior pixel from aligned row dwords with the column neighbours
+//     from the adjacent lanes (DPP), then runs the segment test + cornerScore on the
+//     survivors, NMS inside each cell and the per-cell lists;
+//   fast_cell_item (a cell's minThFAST retry, and a strip whose survivor or corner lists
+//     would overflow): one cell ROI staged in LDS, phases A-D below.
+// Both give cv::FAST's corners, scores and order per cell (ORBextractor.cc:747-781).
+
+// a wave's per-cell LDS slice (16-B aligned): ROI tile S*R, score map S*R, pixel list
 __host__ __device__ constexpr int fast_slice_bytes(int S, int R) {
-    return (S * R + S * (R - (YGZ_FAST_SHIFT ? 2 : 0)) + 2 * (S - 6 - YGZ_FAST_SHIFT) * (R - 6) + 15) / 16 * 16;
+    return (S * R + S * R + 2 * (S - 6) * (R - 6) + 15) / 16 * 16;
 }
 template <int S, int R>
 struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI height)
     static constexpr int DW = S / 4, RPI = 64 / DW, NI = (R + RPI - 1) / RPI;
     uint32_t lo[NI], hi[NI];
     __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, uint32_t off0, int w, int rw, int rh, int lane) {
-        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + YGZ_FAST_SHIFT + 3) / 4;
+        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + 3) / 4;
 #pragma unroll
         for (int k = 0; k < NI; k++) {
             const int r = k * RPI + rlane;
             lo[k] = hi[k] = 0u;
             if (rlane < RPI && r < rh && dw < ndw) {
-                // (a row start at level offset 0 wraps below 0 when shifted: that dword reads 0)
-                const uint32_t o = ((mad24((uint32_t)r, (uint32_t)w, off0) - YGZ_FAST_SHIFT) & ~3u) + 4u * (uint32_t)dw;
+                const uint32_t o = (mad24((uint32_t)r, (uint32_t)w, off0) & ~3u) + 4u * (uint32_t)dw;
                 lo[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0);
                 hi[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4u, 0, 0);
             }
         }
     }
     __device__ __forceinline__ void commit(uint8_t *img, uint32_t off0, int w, int rw, int rh, int lane) const {
-        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + YGZ_FAST_SHIFT + 3) / 4;
+        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + 3) / 4;
 #pragma unroll
         for (int k = 0; k < NI; k++) {
             const int r = k * RPI + rlane;
             if (rlane < RPI && r < rh && dw < ndw) {
-                const uint32_t sh = (mad24((uint32_t)r, (uint32_t)w, off0) - YGZ_FAST_SHIFT) & 3u;
+                const uint32_t sh = mad24((uint32_t)r, (uint32_t)w, off0) & 3u;
                 reinterpret_cast<uint32_t *>(img + r * S)[dw] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh);
             }
         }
@@ -601,36 +585,108 @@ struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI 
     }
 };
 
-// One (cell, frame) item on a wave whose ROI is already in LDS: phases A-D (+ retry).
 #if defined(__FAST_MATH__)
-#error "k_fast_cells orders ring bytes as f16 subnormals: build without fast-math (denormals kept)"
+#error "the FAST kernels order ring bytes as f16 subnormals: build without fast-math (denormals kept)"
 #endif
-#ifndef YGZ_FAST_A2
-#define YGZ_FAST_A2 0  // two row chunks per step: measured equal (0.614 vs 0.617 ms / 1024)
-#endif
-#ifndef YGZ_FAST_C3
-#define YGZ_FAST_C3 0  // phase-A compaction by the survivor count's 3 bits (experiment)
-#endif
+
+// The 4-point necessary test of 4 pixels (the bytes of C) at threshold th: a 9-arc
+// holds a neighbouring pair of the compass points 0/4/8/12, so a corner has
+// (T|B) & (L|R) beyond the threshold on one side.  T / B / Lw / Rw: the dwords of the
+// pixels 3 up / 3 down / 3 left / 3 right.  Bit k: pixel k survives.
+__device__ __forceinline__ uint32_t fast_screen4(uint32_t T, uint32_t B, uint32_t Lw, uint32_t Rw, uint32_t C,
+                                                 int th) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const s16x2 t2 = {(short)th, (short)th};
+    uint32_t sg[2];
+#pragma unroll
+    for (int hlf = 0; hlf < 2; hlf++) {
+        // bright: (T|B) & (L|R) above v+t <=> min(max(T,B), max(L,R)) - v > t;
+        // dark:   (T|B) & (L|R) below v-t <=> v - max(min(T,B), min(L,R)) > t;
+        // sign of t - max(both) marks the survivors (v_pk_max/min_u16, bytes < 256)
+        const uint32_t sel = hlf ? 0x0C030C01u : 0x0C020C00u;  // bytes 1,3 / 0,2 -> u16 lanes
+        const u16x2 dT = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(T, T, sel));
+        const u16x2 dB = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(B, B, sel));
+        const u16x2 dL = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Lw, Lw, sel));
+        const u16x2 dR = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Rw, Rw, sel));
+        const u16x2 bv = __builtin_elementwise_min(__builtin_elementwise_max(dT, dB), __builtin_elementwise_max(dL, dR));
+        const u16x2 dv = __builtin_elementwise_max(__builtin_elementwise_min(dT, dB), __builtin_elementwise_min(dL, dR));
+        const s16x2 v = as_s16x2(__builtin_amdgcn_perm(C, C, sel));
+        const s16x2 m = __builtin_elementwise_max(__builtin_bit_cast(s16x2, bv) - v, v - __builtin_bit_cast(s16x2, dv));
+        sg[hlf] = as_u32(t2 - m);
+    }
+    return ((sg[0] >> 15) & 1u) | (((sg[1] >> 15) & 1u) << 1) | (((sg[0] >> 31) & 1u) << 2) |
+           (((sg[1] >> 31) & 1u) << 3);
+}
+
+// Segment test and score of two survivors at once (entries e = row << 8 | col on a
+// tile of row stride S), as packed pairs: with e[k] = r_k - v,
+//   arcmax = max(max_k min(e[k..k+8]), max_k min(-e[k..k+8]))
+// corner (FAST_t<16>: 9 contiguous ring pixels all > v+t or all < v-t) <=> arcmax > t,
+// and then cornerScore<16> = max(t, arcmax) - 1 = arcmax - 1.  The min / max run on
+// v_pk_minimum3_f16 / v_pk_maximum3_f16 over the ring bytes taken as f16 bit
+// patterns (+0 and subnormals, ordered like the integers and selected exactly with f16
+// denormals kept), and min / max commute with "- v".
+template <int S>
+__device__ __forceinline__ s16x2 fast_arcmax2(const uint8_t *img, uint32_t e0, uint32_t e1) {
+    // ring bases q = centre - 3S - 3: every tap an immediate, non-negative ds_read offset
+    uint32_t b0 = ((e0 >> 8) - 3) * S + (e0 & 0xFFu) - 3, b1 = ((e1 >> 8) - 3) * S + (e1 & 0xFFu) - 3;
+    asm("" : "+v"(b0), "+v"(b1));  // taps off q (not off the centre): immediate offsets only
+    const uint8_t *q0 = img + b0, *q1 = img + b1;
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    auto pair = [&](int o) {  // both survivors' bytes as the u16 halves
+        u16x2 p;
+        p.x = q0[o];
+        p.y = q1[o];
+        return __builtin_bit_cast(uint32_t, p);
+    };
+    const s16x2 vb = as_s16x2(pair(Ring<S>::kCentre));
+    h16x2 e[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) e[k] = as_h16x2(pair(Ring<S>::off(k)));
+    h16x2 w3[16];
+    // bright: max_k min(e[k..k+8]) = max_k min3(w3[k], w3[k+3], w3[k+6]), w3 = min of 3
+#pragma unroll
+    for (int k = 0; k < 16; k++) w3[k] = hmin3(e[k], e[(k + 1) & 15], e[(k + 2) & 15]);
+    h16x2 b9[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) b9[k] = hmin3(w3[k], w3[(k + 3) & 15], w3[(k + 6) & 15]);
+    const h16x2 bright = hmax3(hmax3(hmax3(b9[0], b9[1], b9[2]), hmax3(b9[3], b9[4], b9[5]), hmax3(b9[6], b9[7], b9[8])),
+                               hmax3(b9[9], b9[10], b9[11]), hmax3(hmax3(b9[12], b9[13], b9[14]), b9[15], b9[15]));
+    // dark: max_k min(-e[k..k+8]) = -(min_k max(e[k..k+8]))
+#pragma unroll
+    for (int k = 0; k < 16; k++) w3[k] = hmax3(e[k], e[(k + 1) & 15], e[(k + 2) & 15]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) b9[k] = hmax3(w3[k], w3[(k + 3) & 15], w3[(k + 6) & 15]);
+    const h16x2 darkmin = hmin3(hmin3(hmin3(b9[0], b9[1], b9[2]), hmin3(b9[3], b9[4], b9[5]), hmin3(b9[6], b9[7], b9[8])),
+                                hmin3(b9[9], b9[10], b9[11]), hmin3(hmin3(b9[12], b9[13], b9[14]), b9[15], b9[15]));
+    const s16x2 bi = as_s16x2(as_u32(bright)) - vb, di = vb - as_s16x2(as_u32(darkmin));
+    return __builtin_elementwise_max(bi, di);
+}
+
+// One (cell, frame) item on a wave whose ROI is already in LDS (row stride S), from
+// threshold pass pass0 (0: iniThFAST then the minThFAST retry; 1: minThFAST only):
+//   A  every interior pixel: the 4-point screen, 4 pixels per lane; survivors
+//      compacted (ballot + mbcnt) into the list in raster order
+//   BC survivors: segment test + score, corners compacted in place, scores into the map
+//   D  corners: strict 3x3 non-max suppression, survivors -> the cell's list
+// and the retry at minThFAST when no corner survives (ORBextractor.cc:765-770).
 template <int S>
 __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, const CellDesc &cd, uint8_t *img,
                                                uint8_t *sc, uint16_t *list, uint32_t *__restrict__ out,
-                                               int *__restrict__ cnt_out, int lane) {
+                                               int *__restrict__ cnt_out, int lane, int pass0) {
     const int rw = cd.rw, rh = cd.rh;
     const int iw = rw - 6, ih = rh - 6;
     int total = 0;
-    for (int pass = 0; pass < 2; pass++) {
+    for (int pass = pass0; pass < 2; pass++) {
         const int th = pass == 0 ? plan->ini_th : plan->min_th;
         {
             uint4 *z = reinterpret_cast<uint4 *>(sc);
             const uint4 zero = {0u, 0u, 0u, 0u};
-            // corners sit on rows <= rh - 4, so their NMS windows end at row rh - 3
-            constexpr int kZr = YGZ_FAST_SHIFT ? 2 : 0;  // the shifted layout's score map: R - 2 rows
-            const int nz = (rh - kZr) * S;
+            const int nz = rh * S;
             for (int i = lane; i < nz / 16; i += 64) z[i] = zero;
             for (int i = (nz / 16) * 16 + lane; i < nz; i += 64) sc[i] = 0;
         }
-        // A: 4 pixels per lane, byte pairs as packed u16 / i16 halves; the test
-        //    is (T|B) & (L|R) beyond the threshold for either polarity.
+        // A: 4 pixels per lane
         int na = 0;
         if (iw > 0 && ih > 0) {
             const int lpr = iw <= 32 ? 8 : (iw <= 64 ? 16 : 32);  // lanes per row (4 px each)
@@ -639,159 +695,46 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             uint32_t colmask = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) colmask |= (uint32_t)(4 * j + k < iw) << k;
-            const s16x2 t2 = {(short)th, (short)th};
-            // the screen of the lane's 4 pixels in interior row y (bit k: pixel 4j + k survives)
-            auto screen = [&](int y) -> uint32_t {
-#if YGZ_FAST_SHIFT
-                // rows staged one byte right: pixels 4j..4j+3 are the aligned dword j + 1
-                const uint8_t *al = img - 1;
-                const uint32_t *rt = reinterpret_cast<const uint32_t *>(al + y * S) + j;
-                const uint32_t *rc = reinterpret_cast<const uint32_t *>(al + (y + 3) * S) + j;
-                const uint32_t *rb = reinterpret_cast<const uint32_t *>(al + (y + 6) * S) + j;
-                const uint32_t D0 = rc[0], D1 = rc[1], D2 = rc[2];
-                const uint32_t C = D1;                                       // x .. x+3
-                const uint32_t Lw = __builtin_amdgcn_alignbyte(D1, D0, 1);  // x-3 .. x
-                const uint32_t Rw = __builtin_amdgcn_alignbyte(D2, D1, 3);  // x+3 .. x+6
-                const uint32_t Tw = rt[1];
-                const uint32_t Bw = rb[1];
-#else
+            for (int y0 = 0; y0 < ih; y0 += rpc) {
+                const int y = y0 + rr;
                 const uint32_t *rt = reinterpret_cast<const uint32_t *>(img + y * S) + j;
                 const uint32_t *rc = reinterpret_cast<const uint32_t *>(img + (y + 3) * S) + j;
                 const uint32_t *rb = reinterpret_cast<const uint32_t *>(img + (y + 6) * S) + j;
                 const uint32_t D0 = rc[0], D1 = rc[1], D2 = rc[2];
                 const uint32_t C = __builtin_amdgcn_alignbyte(D1, D0, 3);   // x .. x+3
-                const uint32_t Lw = D0;                                      // x-3 .. x
                 const uint32_t Rw = __builtin_amdgcn_alignbyte(D2, D1, 2);  // x+3 .. x+6
                 const uint32_t Tw = __builtin_amdgcn_alignbyte(rt[1], rt[0], 3);
                 const uint32_t Bw = __builtin_amdgcn_alignbyte(rb[1], rb[0], 3);
-#endif
-                uint32_t sg[2];
-#pragma unroll
-                for (int hlf = 0; hlf < 2; hlf++) {
-                    // bright: (T|B) & (L|R) above v+t <=> min(max(T,B), max(L,R)) - v > t;
-                    // dark:   (T|B) & (L|R) below v-t <=> v - max(min(T,B), min(L,R)) > t;
-                    // sign of t - max(both) marks the survivors (v_pk_max/min_u16, bytes < 256)
-                    const uint32_t sel = hlf ? 0x0C030C01u : 0x0C020C00u;  // bytes 1,3 / 0,2 -> u16 lanes
-                    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-                    const u16x2 dT = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Tw, Tw, sel));
-                    const u16x2 dB = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Bw, Bw, sel));
-                    const u16x2 dL = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Lw, Lw, sel));
-                    const u16x2 dR = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Rw, Rw, sel));
-                    const u16x2 bv = __builtin_elementwise_min(__builtin_elementwise_max(dT, dB), __builtin_elementwise_max(dL, dR));
-                    const u16x2 dv = __builtin_elementwise_max(__builtin_elementwise_min(dT, dB), __builtin_elementwise_min(dL, dR));
-                    const s16x2 v = as_s16x2(__builtin_amdgcn_perm(C, C, sel));
-                    const s16x2 m = __builtin_elementwise_max(__builtin_bit_cast(s16x2, bv) - v, v - __builtin_bit_cast(s16x2, dv));
-                    sg[hlf] = as_u32(t2 - m);
-                }
-                const uint32_t m = ((sg[0] >> 15) & 1u) | (((sg[1] >> 15) & 1u) << 1) | (((sg[0] >> 31) & 1u) << 2) |
-                                   (((sg[1] >> 31) & 1u) << 3);
-                return m & (y < ih ? colmask : 0u);
-            };
-            // survivors appended in raster order (lanes are row-major, bits in column order)
-            auto compact = [&](uint32_t m, int y) {
-#if YGZ_FAST_C3
-                // the lane's survivor count (0..4) by its three bits: 3 ballots instead of 4
-                const uint32_t cn = __builtin_popcount(m);
-                const uint64_t C0 = __ballot(cn & 1u), C1 = __ballot(cn & 2u), C2 = __ballot(cn & 4u);
-                int pos = na + popc_below(C0) + 2 * popc_below(C1) + 4 * popc_below(C2);
-                na += __popcll(C0) + 2 * __popcll(C1) + 4 * __popcll(C2);
-#else
+                const uint32_t m = fast_screen4(Tw, Bw, D0, Rw, C, th) & (y < ih ? colmask : 0u);
+                // survivors appended in raster order (lanes are row-major, bits in column order)
                 const uint64_t M0 = __ballot(m & 1u), M1 = __ballot(m & 2u), M2 = __ballot(m & 4u), M3 = __ballot(m & 8u);
                 int pos = na + popc_below(M0) + popc_below(M1) + popc_below(M2) + popc_below(M3);
                 na += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
-#endif
                 const uint32_t ey = (uint32_t)(y + 3) << 8;
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     if ((m >> k) & 1u) list[pos++] = (uint16_t)(ey | (uint32_t)(4 * j + k + 3));
-            };
-#if YGZ_FAST_A2
-            // two row chunks per step: the second chunk's LDS reads are in flight while the
-            // first is screened (rows past ih screen out through colmask)
-            for (int y0 = 0; y0 < ih; y0 += 2 * rpc) {
-                const uint32_t ma = screen(y0 + rr), mb = screen(y0 + rpc + rr);
-                compact(ma, y0 + rr);
-                if (y0 + rpc < ih) compact(mb, y0 + rpc + rr);
             }
-#else
-            for (int y0 = 0; y0 < ih; y0 += rpc) compact(screen(y0 + rr), y0 + rr);
-#endif
         }
-        if (S == 40 && pass == 0) YGZ_BSTAMP_K(2, 4);
-#if defined(YGZ_FAST_STOP) && YGZ_FAST_STOP <= 1  // timing experiment only (never in the product build)
-        if (lane == 0) *cnt_out = 0;
-        return;
-#endif
-        // BC: segment test and score in one pass, two survivors per lane as packed
-        //     pairs (low half list[i], high half list[i+1]), e[k] = r_k - v:
-        //       arcmax = max(max_k min(e[k..k+8]), max_k min(-e[k..k+8]))
-        //     corner (FAST_t<16>: 9 contiguous ring pixels all > v+t or all < v-t)
-        //     <=> arcmax > t, and then cornerScore<16> = max(t, arcmax) - 1 =
-        //     arcmax - 1, written to the score map.  Corners are compacted in place
-        //     in raster order (writes never pass the read front).
-        //     The min / max run on v_pk_minimum3_f16 / v_pk_maximum3_f16 over the
-        //     ring bytes r as f16 bit patterns (+0 and subnormals, ordered like the
-        //     integers and selected exactly with f16 denormals kept), and
-        //     min / max commute with "- v": e.g. max_k min(e[..]) = max_k min(r[..]) - v.
+        // BC: two survivors per lane (low half list[i], high half list[i+1]); corners
+        // compacted in place in raster order (writes never pass the read front)
         int nc = 0;
         for (int i0 = 0; i0 < na; i0 += 128) {
             const int i = i0 + 2 * lane;
             const uint32_t pr = reinterpret_cast<const uint32_t *>(list)[i >> 1];  // list[i], list[i+1]
             const bool v0 = i < na, v1 = i + 1 < na;
             const uint32_t e0 = v0 ? (pr & 0xFFFFu) : 0x0303u, e1 = v1 ? (pr >> 16) : 0x0303u;
-            // ring bases q = centre - 3S - 3: every tap an immediate, non-negative ds_read offset
-            uint32_t b0 = ((e0 >> 8) - 3) * S + (e0 & 0xFFu) - 3, b1 = ((e1 >> 8) - 3) * S + (e1 & 0xFFu) - 3;
-            const uint32_t o0 = b0 + Ring<S>::kCentre, o1 = b1 + Ring<S>::kCentre;
-            asm("" : "+v"(b0), "+v"(b1));  // taps off q (not off the centre): immediate offsets only
-            const uint8_t *q0 = img + b0, *q1 = img + b1;
-            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-            auto pair = [&](int o) {  // both survivors' bytes as the u16 halves
-                u16x2 p;
-                p.x = q0[o];
-                p.y = q1[o];
-                return __builtin_bit_cast(uint32_t, p);
-            };
-            // the ring bytes themselves as f16 bit patterns (0..255: +0 and subnormals,
-            // ordered like the integers; the kernels keep f16 denormals): min / max
-            // commute with "- v", so v is subtracted once at the end
-            const s16x2 vb = as_s16x2(pair(Ring<S>::kCentre));
-            h16x2 e[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) e[k] = as_h16x2(pair(Ring<S>::off(k)));
-            h16x2 w3[16];
-            // bright: max_k min(e[k..k+8]) = max_k min3(w3[k], w3[k+3], w3[k+6]), w3 = min of 3
-#pragma unroll
-            for (int k = 0; k < 16; k++) w3[k] = hmin3(e[k], e[(k + 1) & 15], e[(k + 2) & 15]);
-            h16x2 b9[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) b9[k] = hmin3(w3[k], w3[(k + 3) & 15], w3[(k + 6) & 15]);
-            const h16x2 bright = hmax3(hmax3(hmax3(b9[0], b9[1], b9[2]), hmax3(b9[3], b9[4], b9[5]), hmax3(b9[6], b9[7], b9[8])),
-                                       hmax3(b9[9], b9[10], b9[11]), hmax3(hmax3(b9[12], b9[13], b9[14]), b9[15], b9[15]));
-            // dark: max_k min(-e[k..k+8]) = -(min_k max(e[k..k+8]))
-#pragma unroll
-            for (int k = 0; k < 16; k++) w3[k] = hmax3(e[k], e[(k + 1) & 15], e[(k + 2) & 15]);
-#pragma unroll
-            for (int k = 0; k < 16; k++) b9[k] = hmax3(w3[k], w3[(k + 3) & 15], w3[(k + 6) & 15]);
-            const h16x2 darkmin = hmin3(hmin3(hmin3(b9[0], b9[1], b9[2]), hmin3(b9[3], b9[4], b9[5]), hmin3(b9[6], b9[7], b9[8])),
-                                        hmin3(b9[9], b9[10], b9[11]), hmin3(hmin3(b9[12], b9[13], b9[14]), b9[15], b9[15]));
-            const s16x2 bi = as_s16x2(as_u32(bright)) - vb, di = vb - as_s16x2(as_u32(darkmin));
-            const s16x2 am = __builtin_elementwise_max(bi, di);
+            const s16x2 am = fast_arcmax2<S>(img, e0, e1);
             const bool c0 = v0 && am.x > th, c1 = v1 && am.y > th;
-            if (c0) sc[o0] = (uint8_t)(am.x - 1);
-            if (c1) sc[o1] = (uint8_t)(am.y - 1);
+            if (c0) sc[(e0 >> 8) * S + (e0 & 0xFFu)] = (uint8_t)(am.x - 1);
+            if (c1) sc[(e1 >> 8) * S + (e1 & 0xFFu)] = (uint8_t)(am.y - 1);
             const uint64_t M0 = __ballot(c0), M1 = __ballot(c1);
             const int pos = nc + popc_below(M0) + popc_below(M1);
             if (c0) list[pos] = (uint16_t)e0;
             if (c1) list[pos + (c0 ? 1 : 0)] = (uint16_t)e1;
             nc += __popcll(M0) + __popcll(M1);
         }
-        if (S == 40 && pass == 0) YGZ_BSTAMP_K(2, 5);
-#if defined(YGZ_FAST_STOP) && YGZ_FAST_STOP <= 3
-        if (lane == 0) *cnt_out = 0;
-        return;
-#endif
         wave_lds_order();
-        if (S == 40 && pass == 0) YGZ_BSTAMP_K(2, 6);
         // D: strict 3x3 NMS over the corner list
         for (int i0 = 0; i0 < nc; i0 += 64) {
             const int i = i0 + lane;
@@ -817,89 +760,270 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
         }
         if (total > 0) break;
     }
-    if (S == 40) YGZ_BSTAMP_K(2, 7);
     if (lane == 0) *cnt_out = min(total, plan->cell_cap);
 }
 
-// One wave per (cell, frame) item (four per 256-thread workgroup), each with a
-// dynamic-LDS slice: ROI tile S*S, score map S*S, pixel list 2*(S-6)^2.
-// (A persistent variant -- a resident-sized grid walking item ranges with the
-// next ROI prefetched -- measured slower: item costs vary with texture, and
-// the waves per CU, not the dispatch, bound the throughput.)
-#ifndef YGZ_FAST_WAVES_EU
-#define YGZ_FAST_WAVES_EU 6  // waves per SIMD the FAST kernels are register-limited to
-#endif
-constexpr int kFastWaves = 4;  // cells (waves) per workgroup (8 measured slower: a block holds its LDS until its slowest cell ends)
+// ---------------------------------------------------------------------------
+// k_fast_strips: one wave per (strip, frame).
+//
+// Per strip (plan.cpp: <= 8 cells of one cell row, ROI columns inside a 256-byte
+// window from a multiple of 4; the cells' ROIs share the band's rows):
+//   1  the band's rows are read once (one coalesced dword per lane per row, 8 rows in
+//      flight) into LDS at a 260-byte stride (rows shift one bank);
+//   2  as soon as row r + 3 is in, row r is screened at iniThFAST: T / C / B are aligned
+//      LDS dwords, the 3-left / 3-right dwords come from the neighbouring lanes (DPP
+//      wave shifts, v_alignbyte); survivors in band raster order into a u16 list;
+//   3  segment test + score on the survivors (fast_arcmax2), corners kept with their
+//      arcmax in a u32 list (raster order);
+//   4  the band is zeroed and becomes the score map (arcmax at the corners); strict
+//      3x3 NMS per corner where the neighbours in another cell count as 0 -- cv::FAST
+//      on the cell's ROI sees 0 outside its [3, w - 3) interior -- so a corner is kept
+//      iff arcmax > every in-cell neighbour's arcmax (scores = arcmax - 1);
+//   5  kept corners appended to their cell's list in raster order (ranks by ballots on
+//      the 3-bit cell index), counts per cell in LDS;
+//   6  a cell with no kept corner reruns at minThFAST through fast_cell_item (its ROI
+//      staged into the now free LDS); a strip whose survivor or corner list would
+//      overflow runs every cell through fast_cell_item (both thresholds).
+constexpr int kStripStride = 260;      // band row stride (65 dwords)
+constexpr int kStripCap = 1024;        // screen survivors per strip
+constexpr int kStripCornerCap = 512;   // corners per strip
+constexpr int kStripPF = 8;            // band rows in flight
+__host__ __device__ constexpr int strip_band_bytes(int rh) { return (rh * kStripStride + 15) / 16 * 16; }
+__host__ __device__ constexpr int strip_main_bytes(int rh, int S, int R) {
+    return strip_band_bytes(rh) + 2 * kStripCap + 4 * kStripCornerCap > fast_slice_bytes(S, R)
+               ? strip_band_bytes(rh) + 2 * kStripCap + 4 * kStripCornerCap
+               : fast_slice_bytes(S, R);
+}
+struct StripRec {
+    int xy, rl, tx, c0, nc, col, pad0, pad1;
+};
 
 template <int S, int R>
-__global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(YGZ_FAST_WAVES_EU))) void k_fast_cells(
+__global__ __launch_bounds__(64) void k_fast_strips(const uint8_t *__restrict__ pyr, uint32_t pitch,
+                                                    const Plan *__restrict__ plan,
+                                                    const CellDesc *__restrict__ cells, uint32_t *__restrict__ cellbuf,
+                                                    int *__restrict__ cellcnt, int level, int band_rows,
+                                                    int *__restrict__ clear_flag) {
+    extern __shared__ uint8_t s_dyn[];
+    const int lane = threadIdx.x;
+    const int f = blockIdx.y;
+    int l = level, sl = blockIdx.x;
+    if (l < 0) {  // one launch over every level's strips: the strip's level
+        l = 0;
+        while (sl >= plan->lv[l].nstrips) sl -= plan->lv[l].nstrips, l++;
+    }
+    if (clear_flag && blockIdx.x == 0 && f == 0 && lane == 0) *clear_flag = 0;  // the octree's overflow flag
+    const LevelDesc &L = plan->lv[l];
+    const StripRec sr = scalar_load(reinterpret_cast<const StripRec *>(plan->dtabs + L.strip_off + kStripInts * sl));
+    const int xs = sr.xy & 0xFFFF, y0 = sr.xy >> 16, rh = sr.rl & 0xFFFF;
+    const int tx0 = sr.tx & 0xFFFF, tx1 = sr.tx >> 16, c0 = sr.c0, nc = sr.nc;
+    const int main_bytes = strip_main_bytes(band_rows, S, R);
+    uint8_t *band = s_dyn;
+    uint16_t *list = reinterpret_cast<uint16_t *>(s_dyn + strip_band_bytes(band_rows));
+    uint32_t *corners = reinterpret_cast<uint32_t *>(list + kStripCap);
+    uint8_t *ctab = s_dyn + main_bytes;
+    int *cnt = reinterpret_cast<int *>(ctab + 256);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(pyr + (size_t)f * pitch + L.off), 0, (int)((uint32_t)L.w * (uint32_t)L.h), 0x00020000);
+    const int th = plan->ini_th;
+    // the column table (cell of each window column, its edges; 0xFF = not tested)
+    const uint32_t tab = as_global(plan->dtabs)[sr.col + lane];
+    reinterpret_cast<uint32_t *>(ctab)[lane] = tab;
+    if (lane < kStripMaxCells) cnt[lane] = 0;
+    uint32_t colmask = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) colmask |= (uint32_t)(((tab >> (8 * k)) & 0xFFu) != 0xFFu) << k;
+    (void)tx0;
+    (void)tx1;
+
+    // 1 + 2: band rows in, each row screened once the row three below it is in
+    const bool aligned = (L.w & 3) == 0;
+    const uint32_t w = (uint32_t)L.w;
+    uint32_t blo[kStripPF], bhi[kStripPF];
+    auto issue = [&](int r, uint32_t &lo, uint32_t &hi) {
+        const uint32_t o = ((uint32_t)(y0 + r) * w + (uint32_t)xs) & ~3u;
+        lo = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4u * (uint32_t)lane, 0, 0);
+        hi = aligned ? 0u : __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4u * (uint32_t)lane + 4u, 0, 0);
+    };
+#pragma unroll
+    for (int i = 0; i < kStripPF; i++)
+        if (i < rh) issue(i, blo[i], bhi[i]);
+    int na = 0;
+    bool ovf = false;
+    const uint32_t *bw = reinterpret_cast<const uint32_t *>(band);
+    for (int r0 = 0; r0 < rh; r0 += kStripPF) {
+#pragma unroll
+        for (int i = 0; i < kStripPF; i++) {
+            const int r = r0 + i;
+            if (r >= rh) break;
+            const uint32_t sh = ((uint32_t)(y0 + r) * w + (uint32_t)xs) & 3u;
+            const uint32_t v = aligned ? blo[i] : __builtin_amdgcn_alignbyte(bhi[i], blo[i], sh);
+            if (r + kStripPF < rh) issue(r + kStripPF, blo[i], bhi[i]);
+            reinterpret_cast<uint32_t *>(band + r * kStripStride)[lane] = v;
+            if (r >= 6) {
+                const int rc = r - 3;
+                const uint32_t T = bw[(rc - 3) * (kStripStride / 4) + lane];
+                const uint32_t Cc = bw[rc * (kStripStride / 4) + lane];
+                const uint32_t B = v;
+                const uint32_t Cp = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Cc, 0x138, 0xF, 0xF, false);  // lane - 1
+                const uint32_t Cn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Cc, 0x130, 0xF, 0xF, false);  // lane + 1
+                const uint32_t Lw = __builtin_amdgcn_alignbyte(Cc, Cp, 1);  // x-3 .. x
+                const uint32_t Rw = __builtin_amdgcn_alignbyte(Cn, Cc, 3);  // x+3 .. x+6
+                const uint32_t m = fast_screen4(T, B, Lw, Rw, Cc, th) & colmask;
+                const uint64_t M0 = __ballot(m & 1u), M1 = __ballot(m & 2u), M2 = __ballot(m & 4u), M3 = __ballot(m & 8u);
+                const int n = __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
+                if (na + n > kStripCap) ovf = true;
+                if (!ovf) {
+                    int pos = na + popc_below(M0) + popc_below(M1) + popc_below(M2) + popc_below(M3);
+                    const uint32_t ey = (uint32_t)rc << 8;
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if ((m >> k) & 1u) list[pos++] = (uint16_t)(ey | (uint32_t)(4 * lane + k));
+                    na += n;
+                }
+            }
+        }
+    }
+    wave_lds_order();
+
+    // 3: segment test + score on the survivors, two per lane
+    int ncorn = 0;
+    if (!ovf) {
+        for (int i0 = 0; i0 < na; i0 += 128) {
+            const int i = i0 + 2 * lane;
+            const uint32_t pr = reinterpret_cast<const uint32_t *>(list)[i >> 1];
+            const bool v0 = i < na, v1 = i + 1 < na;
+            const uint32_t e0 = v0 ? (pr & 0xFFFFu) : 0x0303u, e1 = v1 ? (pr >> 16) : 0x0303u;
+            const s16x2 am = fast_arcmax2<kStripStride>(band, e0, e1);
+            const bool k0 = v0 && am.x > th, k1 = v1 && am.y > th;
+            const uint64_t M0 = __ballot(k0), M1 = __ballot(k1);
+            const int n = __popcll(M0) + __popcll(M1);
+            if (ncorn + n > kStripCornerCap) {
+                ovf = true;
+                break;
+            }
+            const int pos = ncorn + popc_below(M0) + popc_below(M1);
+            if (k0) corners[pos] = ((uint32_t)am.x << 16) | e0;
+            if (k1) corners[pos + (k0 ? 1 : 0)] = ((uint32_t)am.y << 16) | e1;
+            ncorn += n;
+        }
+    }
+    wave_lds_order();
+
+    if (!ovf) {
+        // 4: the band becomes the score map
+        {
+            uint4 *z = reinterpret_cast<uint4 *>(band);
+            const uint4 zero = {0u, 0u, 0u, 0u};
+            for (int i = lane; i < strip_band_bytes(rh) / 16; i += 64) z[i] = zero;
+        }
+        wave_lds_order();
+        for (int i = lane; i < ncorn; i += 64) {
+            const uint32_t e = corners[i];
+            band[((e >> 8) & 0xFFu) * kStripStride + (e & 0xFFu)] = (uint8_t)(e >> 16);
+        }
+        wave_lds_order();
+        // 5: NMS inside each cell; kept corners -> their cell's list in raster order
+        const int cap = plan->cell_cap;
+        uint32_t *fbuf = cellbuf + ((size_t)f * plan->ncells + c0) * cap;
+        for (int i0 = 0; i0 < ncorn; i0 += 64) {
+            const int i = i0 + lane;
+            bool keep = false;
+            uint32_t e = 0, k = 0;
+            if (i < ncorn) {
+                e = corners[i];
+                const uint32_t x = e & 0xFFu, y = (e >> 8) & 0xFFu, am = e >> 16;
+                const uint32_t tb = ctab[x];
+                k = tb & 7u;
+                const uint8_t *r = band + (y - 1) * kStripStride + (x - 1);
+                const uint32_t lm = max(max((uint32_t)r[0], (uint32_t)r[kStripStride]), (uint32_t)r[2 * kStripStride]);
+                const uint32_t rm = max(max((uint32_t)r[2], (uint32_t)r[kStripStride + 2]), (uint32_t)r[2 * kStripStride + 2]);
+                const uint32_t mm = max((uint32_t)r[1], (uint32_t)r[2 * kStripStride + 1]);
+                const uint32_t nb = max(max((tb & 16u) ? 0u : lm, (tb & 32u) ? 0u : rm), mm);
+                keep = am > nb;
+            }
+            const uint64_t K = __ballot(keep);
+            const uint64_t B0 = __ballot(keep && (k & 1u)), B1 = __ballot(keep && (k & 2u)), B2 = __ballot(keep && (k & 4u));
+            if (keep) {
+                const uint64_t eq = K & ((k & 1u) ? B0 : ~B0) & ((k & 2u) ? B1 : ~B1) & ((k & 4u) ? B2 : ~B2);
+                const int pos = cnt[k] + popc_below(eq);
+                if (pos < cap) {
+                    const uint32_t x = e & 0xFFu, y = (e >> 8) & 0xFFu;
+                    fbuf[(size_t)k * cap + pos] = pack_key(xs + (int)x - kMinBorder, y0 + (int)y - kMinBorder,
+                                                           (int)(e >> 16) - 1);
+                }
+                if ((eq >> lane) == 1ull) cnt[k] = pos + 1;  // the cell's last lane in this batch
+            }
+            wave_lds_order();
+        }
+    }
+    wave_lds_order();
+
+    // 6: counts; the minThFAST retry of cells without a kept corner (all cells on overflow)
+    const int mine = lane < nc ? cnt[lane] : 1;
+    const uint64_t all = nc >= 64 ? ~0ull : ((1ull << nc) - 1ull);
+    uint64_t redo = ovf ? all : (__ballot(lane < nc && mine == 0) & all);
+    if (lane < nc && !((redo >> lane) & 1ull))
+        cellcnt[(size_t)f * plan->ncells + c0 + lane] = min(mine, plan->cell_cap);
+    redo = __builtin_amdgcn_readfirstlane((uint32_t)redo) | ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(redo >> 32)) << 32);
+    while (redo) {
+        const int k = __builtin_ctzll(redo);
+        redo &= redo - 1;
+        const CellDesc cd = scalar_load(cells + c0 + k);
+        uint8_t *img = s_dyn;
+        uint8_t *sc = img + S * R;
+        uint16_t *clist = reinterpret_cast<uint16_t *>(sc + S * R);
+        const uint32_t off0 = (uint32_t)cd.y0 * (uint32_t)L.w + (uint32_t)cd.x0;
+        wave_lds_order();
+        {
+            RoiStage<S, R> st;
+            st.issue(rs, off0, L.w, cd.rw, cd.rh, lane);
+            st.commit(img, off0, L.w, cd.rw, cd.rh, lane);
+        }
+        fast_cell_item<S>(plan, cd, img, sc, clist, cellbuf + ((size_t)f * plan->ncells + c0 + k) * plan->cell_cap,
+                          cellcnt + (size_t)f * plan->ncells + c0 + k, lane, ovf ? 0 : 1);
+    }
+}
+
+// per-level ROI slice for the retry path: the level's largest cell ROI, row stride a
+// multiple of 4 (>= 36), rows rounded up to 8 (>= 40)
+static void fast_slice_shape(int rw, int rh, int &S, int &R) {
+    S = rw <= 36 ? 36 : ((rw + 7) / 8) * 8;
+    R = std::max(40, ((rh + 7) / 8) * 8);
+}
+static size_t fast_strips_lds_bytes(int band_rows, int S, int R) {
+    return (size_t)strip_main_bytes(band_rows, S, R) + 256 + 64;
+}
+
+// The per-cell path as a whole launch (one wave per (cell, frame), four per workgroup):
+// the A/B reference for k_fast_strips (YGZFE_FAST_CELLS=1 selects it).
+constexpr int kFastWaves = 4;
+template <int S, int R>
+__global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(6))) void k_fast_cells(
     const uint8_t *__restrict__ pyr, uint32_t pitch, const Plan *__restrict__ plan,
     const CellDesc *__restrict__ cells, uint32_t *__restrict__ cellbuf, int *__restrict__ cellcnt, int cell_begin,
     int cell_end, int level, int *__restrict__ clear_flag) {
     extern __shared__ uint8_t s_dyn[];
     constexpr int slice = fast_slice_bytes(S, R);
-    // wave-uniform cell index: the CellDesc and the level record come by scalar
-    // loads (vector loads here put two dependent global round trips in front of
-    // the ROI loads)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-// Block order (a speed / traffic choice only; results never depend on it):
-// 0 = plain, 1 = contiguous ranges per XCD (a frame's cells on one L2: HBM reads
-// 0.87x the levels' bytes but 13 % slower), 2 (default) = runs of 4 consecutive
-// blocks per XCD (1.29x instead of 2.07x, +1 % time)
-#ifndef YGZ_FAST_XCD
-#define YGZ_FAST_XCD 2
-#endif
-#if YGZ_FAST_XCD == 1
-    int bx, f;
-    swizzled_block_2d(bx, f);  // contiguous block ranges per XCD
-#elif YGZ_FAST_XCD == 2
-    // runs of 4 consecutive blocks (16 cells) per XCD: neighbouring cells' ROI
-    // halos come from one L2 (block b runs on XCD b % 8)
-    const int orig = blockIdx.x + gridDim.x * blockIdx.y, nwg = gridDim.x * gridDim.y;
-    int lid = ((orig >> 5) << 5) + ((orig & 7) << 2) + ((orig >> 3) & 3);
-    if ((orig | 31) >= nwg) lid = orig;  // the ragged tail keeps the plain order
-    const int bx = lid % gridDim.x, f = lid / gridDim.x;
-#else
-    const int bx = blockIdx.x, f = blockIdx.y;
-#endif
-    const int c = cell_begin + bx * kFastWaves + wave;
-    if (clear_flag && c == cell_begin && f == 0 && lane == 0) *clear_flag = 0;  // the octree's overflow flag
+    const int c = cell_begin + blockIdx.x * kFastWaves + wave, f = blockIdx.y;
+    if (clear_flag && c == cell_begin && f == 0 && lane == 0) *clear_flag = 0;
     if (c >= cell_end) return;
     uint8_t *img = s_dyn + wave * slice;
     uint8_t *sc = img + S * R;
-    uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * (R - (YGZ_FAST_SHIFT ? 2 : 0)));
+    uint16_t *list = reinterpret_cast<uint16_t *>(sc + S * R);
     const CellDesc cd = scalar_load(cells + c);
-    // one launch per level: the level record loads beside cd, not after it;
-    // level < 0 (one launch over every level's cells): the cell's own level
     const LevelDesc &L = plan->lv[level >= 0 ? level : cd.level];
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(pyr + (size_t)f * pitch + L.off), 0, (int)((uint32_t)L.w * (uint32_t)L.h), 0x00020000);
-    const uint32_t off0 = (uint32_t)cd.y0 * (uint32_t)L.w + (uint32_t)cd.x0;  // ROI origin in the level
-    if (S == 40) YGZ_BSTAMP_K(2, 0);
+    const uint32_t off0 = (uint32_t)cd.y0 * (uint32_t)L.w + (uint32_t)cd.x0;
     {
         RoiStage<S, R> st;
         st.issue(rs, off0, L.w, cd.rw, cd.rh, lane);
         st.commit(img, off0, L.w, cd.rw, cd.rh, lane);
     }
-    if (S == 40) YGZ_BSTAMP_K(2, 3);
-#if defined(YGZ_FAST_STOP) && YGZ_FAST_STOP <= 0
-    if (lane == 0) cellcnt[(size_t)f * plan->ncells + c] = img[lane * 7] == 255 ? 1 : 0;  // keep the staging live
-    return;
-#endif
-    fast_cell_item<S>(plan, cd, img + YGZ_FAST_SHIFT, sc, list, cellbuf + ((size_t)f * plan->ncells + c) * plan->cell_cap,
-                      cellcnt + (size_t)f * plan->ncells + c, lane);
-    if (S == 40) YGZ_BSTAMP_K(2, 1);
-    if (S == 40) YGZ_BSTAMP_K(2, 2);
-}
-
-// per-level ROI stride: the level's largest cell ROI rounded up to 8 (>= 40)
-static int fast_stride(int roi) {
-    const int S = ((roi + 7) / 8) * 8;
-    return S < 40 ? 40 : S;
-}
-
-static size_t fast_cells_lds_bytes(int S, int R) {
-    return kFastWaves * (size_t)fast_slice_bytes(S, R);
+    fast_cell_item<S>(plan, cd, img, sc, list, cellbuf + ((size_t)f * plan->ncells + c) * plan->cell_cap,
+                      cellcnt + (size_t)f * plan->ncells + c, lane, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -2260,75 +2384,91 @@ hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const 
     return hipGetLastError();
 }
 
+// the (S, R) instance of the per-cell slice for ROIs up to rw x rh
+static void fast_shape_pick(int rw, int rh, int &S, int &R) {
+    fast_slice_shape(rw, rh, S, R);
+    if (S == 36 && R > 40) S = 40;
+    if (!((S == 36 && R == 40) || (S == 40 && R <= 56))) S = R = std::max(S, R);
+}
+#define YGZ_FAST_SHAPES(X) X(36, 40) X(40, 40) X(40, 48) X(40, 56) X(48, 48) X(56, 56) X(64, 64) X(72, 72)
+
+// YGZFE_FAST_CELLS=1: the per-cell kernel instead of the strips (A/B reference)
+static bool fast_cells_path() {
+    static const bool on = getenv("YGZFE_FAST_CELLS") != nullptr && getenv("YGZFE_FAST_CELLS")[0] == '1';
+    return on;
+}
+
 hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const CellDesc *dcells,
                        uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st0, const hipStream_t *lvl_streams,
                        int n_lvl_streams) {
     if (hp.ncells == 0) return hipSuccess;
-    // one launch per level, each with its own compile-time ROI stride (LDS per
-    // wave ~ 2 S^2: the small-cell levels keep 7 workgroups per CU)
+    // one launch per level: the level's band height and ROI shape size the LDS
     for (int l = 0; l < hp.nlevels; l++) {
         const LevelDesc &L = hp.lv[l];
         if (L.ncells == 0) continue;
-        // row stride S >= the widest ROI, row capacity R >= the tallest (LDS per
-        // wave ~ 2 S R: C2 levels 1-2 have 38-px-wide, 41/50-px-tall ROIs)
-        int S = fast_stride(L.fast_rw + YGZ_FAST_SHIFT), R = fast_stride(L.fast_rh);
-        if (!(S == 40 && R <= 56) && S != R) S = R = std::max(S, R);  // other shapes: square slices
-        if (R < S) R = S;
-        // ROIs up to 36 x 40 (C2 level 0): a 36-byte row stride brings the slice to 4.9 KB,
-        // 8 workgroups (8 waves / SIMD) per CU instead of 7
-#ifndef YGZ_FAST36
-#define YGZ_FAST36 1
-#endif
-        if (YGZ_FAST36 && L.fast_rw + YGZ_FAST_SHIFT <= 36 && L.fast_rh <= 40) S = 36, R = 40;
-        if (YGZ_FAST_SHIFT && S == 40 && R == 40 && L.fast_rh <= 38) R = 38;  // the shifted C2 level 0
-        const size_t lds = fast_cells_lds_bytes(S, R);
-        const int cb = L.cell_begin, ce = L.cell_begin + L.ncells;
-        const dim3 grid((L.ncells + kFastWaves - 1) / kFastWaves, nframes);
+        int S, R;
+        fast_shape_pick(L.fast_rw, L.fast_rh, S, R);
         // level 0 on the caller's stream, the others spread over the given side streams
         const hipStream_t st = (l == 0 || !lvl_streams || n_lvl_streams <= 0) ? st0
                                                                                 : lvl_streams[(l - 1) % n_lvl_streams];
-#define YGZ_FAST(SS, RR) hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, cb, ce, l, nullptr)
-        if (S == 36 && R == 40) YGZ_FAST(36, 40);
-#if YGZ_FAST_SHIFT
-        else if (S == 40 && R == 38) YGZ_FAST(40, 38);
-#endif
-        else if (S == 40 && R == 40) YGZ_FAST(40, 40);
-        else if (S == 40 && R == 48) YGZ_FAST(40, 48);
-        else if (S == 40 && R == 56) YGZ_FAST(40, 56);
-        else if (S == 48) YGZ_FAST(48, 48);
-        else if (S == 56) YGZ_FAST(56, 56);
-        else if (S == 64) YGZ_FAST(64, 64);
-        else YGZ_FAST(72, 72);
+        if (fast_cells_path()) {
+            const size_t lds = kFastWaves * (size_t)fast_slice_bytes(S, R);
+            const dim3 grid((L.ncells + kFastWaves - 1) / kFastWaves, nframes);
+#define YGZ_FAST(SS, RR)                                                                                        \
+    if (S == SS && R == RR)                                                                                     \
+        hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, \
+                           cellbuf, cellcnt, L.cell_begin, L.cell_begin + L.ncells, l, nullptr);
+            YGZ_FAST_SHAPES(YGZ_FAST)
 #undef YGZ_FAST
+        } else {
+            const size_t lds = fast_strips_lds_bytes(L.fast_rh, S, R);
+            const dim3 grid(L.nstrips, nframes);
+#define YGZ_FAST(SS, RR)                                                                                           \
+    if (S == SS && R == RR)                                                                                        \
+        hipLaunchKernelGGL((k_fast_strips<SS, RR>), grid, dim3(64), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, \
+                           l, L.fast_rh, nullptr);
+            YGZ_FAST_SHAPES(YGZ_FAST)
+#undef YGZ_FAST
+        }
     }
     return hipGetLastError();
 }
 
-// Every level's cells in ONE launch (the single-frame path: one frame's 412
-// C2 cells fill the GPU anyway, and three dependent launches cost three
-// dispatch gaps): the LDS slice of the largest ROI of any level.
+// Every level's strips in ONE launch (the single-frame path: one frame's strips
+// fill the GPU anyway, and three dependent launches cost three dispatch gaps):
+// the LDS of the tallest band and the largest ROI of any level.
 hipError_t launch_fast_merged(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp,
                               const CellDesc *dcells, uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st,
                               int *clear_flag) {
     if (hp.ncells == 0) return hipSuccess;
-    int S = 40, R = 40;
+    int rw = 0, rh = 0, nstrips = 0;
     for (int l = 0; l < hp.nlevels; l++) {
         if (hp.lv[l].ncells == 0) continue;
-        S = std::max(S, fast_stride(hp.lv[l].fast_rw + YGZ_FAST_SHIFT));
-        R = std::max(R, fast_stride(hp.lv[l].fast_rh));
+        rw = std::max(rw, hp.lv[l].fast_rw);
+        rh = std::max(rh, hp.lv[l].fast_rh);
+        nstrips += hp.lv[l].nstrips;
     }
-    if (!(S == 40 && R <= 56)) S = R = std::max(S, R);
-    const size_t lds = fast_cells_lds_bytes(S, R);
-    const dim3 grid((hp.ncells + kFastWaves - 1) / kFastWaves, nframes);
-#define YGZ_FAST(SS, RR) hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, 0, hp.ncells, -1, clear_flag)
-    if (S == 40 && R == 40) YGZ_FAST(40, 40);
-    else if (S == 40 && R == 48) YGZ_FAST(40, 48);
-    else if (S == 40 && R == 56) YGZ_FAST(40, 56);
-    else if (S == 48) YGZ_FAST(48, 48);
-    else if (S == 56) YGZ_FAST(56, 56);
-    else if (S == 64) YGZ_FAST(64, 64);
-    else YGZ_FAST(72, 72);
+    int S, R;
+    fast_shape_pick(rw, rh, S, R);
+    if (fast_cells_path()) {
+        const size_t lds = kFastWaves * (size_t)fast_slice_bytes(S, R);
+        const dim3 grid((hp.ncells + kFastWaves - 1) / kFastWaves, nframes);
+#define YGZ_FAST(SS, RR)                                                                                        \
+    if (S == SS && R == RR)                                                                                     \
+        hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, \
+                           cellbuf, cellcnt, 0, hp.ncells, -1, clear_flag);
+        YGZ_FAST_SHAPES(YGZ_FAST)
 #undef YGZ_FAST
+    } else {
+        const size_t lds = fast_strips_lds_bytes(rh, S, R);
+        const dim3 grid(nstrips, nframes);
+#define YGZ_FAST(SS, RR)                                                                                           \
+    if (S == SS && R == RR)                                                                                        \
+        hipLaunchKernelGGL((k_fast_strips<SS, RR>), grid, dim3(64), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, \
+                           -1, rh, clear_flag);
+        YGZ_FAST_SHAPES(YGZ_FAST)
+#undef YGZ_FAST
+    }
     return hipGetLastError();
 }
 

@@ -752,14 +752,14 @@ int main(int argc, char **argv) {
     // ---------------------------------------------------------------- SearchLocalPointsDirect + FindDirectProjection
     // NK keyframes of the plane: A = the last frame (identity pose), B, C, ... shifted images
     // (image shift (dx, dy) <=> T_cw translation (dx Z / fx, dy Z / fy, 0)); C is mpLastKeyFrame,
-    // which SelectNearestKeyframe leaves out.  NK = 100 first: a local map larger than the
+    // which SelectNearestKeyframe leaves out.  NK = 130 first: a local map larger than the
     // pyramid pool's soft capacity (96), whose keyframes a phase pins; then NK = 3, whose state
     // the FindDirectProjection checks below reuse.
     std::vector<KeyFrame> kfs;
     std::vector<Frame> kframes;
     std::vector<MapPoint> dm;
     std::vector<uint8_t *> rp;
-    for (const int NK : {100, 3}) {
+    for (const int NK : {130, 3}) {
         kfs.clear();
         kframes.clear();
         kfs.resize(NK);
@@ -798,7 +798,7 @@ int main(int argc, char **argv) {
             for (int k = 0; k < NK; k++) {
                 if (k == 0 && j % 5 == 1) continue;  // observed by B / C only
                 if (k == 1 && j % 4 == 2) continue;
-                if (k >= 3 && (j + 7 * (size_t)k) % 17 != 0) continue;  // NK = 100: ~6 more keyframes per point
+                if (k >= 3 && (j + 7 * (size_t)k) % 26 != 0) continue;  // NK = 130: 5 more keyframes per point
                 const Vector3f pc = kfs[k].mTcw * mp.mWorldPos;
                 cv::KeyPoint kp(cv::Point2f(Frame::fx * pc[0] / pc[2] + Frame::cx, Frame::fy * pc[1] / pc[2] + Frame::cy),
                                 31.f * kfs[k].mvScaleFactors[oc], -1, 0, oc);
