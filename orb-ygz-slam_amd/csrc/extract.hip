@@ -510,6 +510,42 @@ __global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(const uint8_t *__re
 }
 
 // ---------------------------------------------------------------------------
+// Wave / workgroup scans (FAST strips, octree).
+
+// Inclusive wave scan on DPP: Hillis-Steele inside each 16-lane row
+// (row_shr:1,2,4,8; lanes shifted in from outside the row add 0), then
+// row_bcast:15 / row_bcast:31 carry rows 0-1 / 0-2 into the rows above.
+// Six DPP adds instead of six LDS-routed shuffles.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// exclusive scan over the 256 threads of the block; *total = block sum
+template <int NT>
+__device__ __forceinline__ int block_excl_scan(int v, int *red, int *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int incl = wave_incl_scan(v);
+    if (lane == 63) red[w] = incl;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) {
+        const int r = red[i];
+        off += i < w ? r : 0;
+        tot += r;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + incl - v;
+}
+
+// ---------------------------------------------------------------------------
 // FAST-9/16 + cornerScore<16> + 3x3 non-max suppression inside each cell ROI
 // (ORBextractor.cc:747-781).
 
@@ -772,7 +808,9 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
 //      flight) into LDS at a 260-byte stride (rows shift one bank);
 //   2  as soon as row r + 3 is in, row r is screened at iniThFAST: T / C / B are aligned
 //      LDS dwords, the 3-left / 3-right dwords come from the neighbouring lanes (DPP
-//      wave shifts, v_alignbyte); survivors in band raster order into a u16 list;
+//      wave shifts, v_alignbyte); a lane with survivors appends one packet (row, lane,
+//      4-bit mask: one ballot per row), and the packets expand into a u16 survivor
+//      list in band raster order (a wave scan per 64 packets);
 //   3  segment test + score on the survivors (fast_arcmax2), corners kept with their
 //      arcmax in a u32 list (raster order);
 //   4  the band is zeroed and becomes the score map (arcmax at the corners); strict
@@ -848,8 +886,9 @@ __global__ __launch_bounds__(64) void k_fast_strips(const uint8_t *__restrict__ 
 #pragma unroll
     for (int i = 0; i < kStripPF; i++)
         if (i < rh) issue(i, blo[i], bhi[i]);
-    int na = 0;
+    int npk = 0;
     bool ovf = false;
+    uint32_t *packets = corners;  // the corner list's memory until the survivors are expanded
     const uint32_t *bw = reinterpret_cast<const uint32_t *>(band);
     for (int r0 = 0; r0 < rh; r0 += kStripPF) {
 #pragma unroll
@@ -870,18 +909,39 @@ __global__ __launch_bounds__(64) void k_fast_strips(const uint8_t *__restrict__ 
                 const uint32_t Lw = __builtin_amdgcn_alignbyte(Cc, Cp, 1);  // x-3 .. x
                 const uint32_t Rw = __builtin_amdgcn_alignbyte(Cn, Cc, 3);  // x+3 .. x+6
                 const uint32_t m = fast_screen4(T, B, Lw, Rw, Cc, th) & colmask;
-                const uint64_t M0 = __ballot(m & 1u), M1 = __ballot(m & 2u), M2 = __ballot(m & 4u), M3 = __ballot(m & 8u);
-                const int n = __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
-                if (na + n > kStripCap) ovf = true;
-                if (!ovf) {
-                    int pos = na + popc_below(M0) + popc_below(M1) + popc_below(M2) + popc_below(M3);
-                    const uint32_t ey = (uint32_t)rc << 8;
-#pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        if ((m >> k) & 1u) list[pos++] = (uint16_t)(ey | (uint32_t)(4 * lane + k));
-                    na += n;
+                // one packet (row, lane, 4-bit mask) per lane with a survivor, in lane order
+                const uint64_t P = __ballot(m != 0u);
+                if (P) {
+                    const int n = __popcll(P);
+                    if (npk + n > kStripCornerCap) ovf = true;
+                    if (!ovf) {
+                        if (m) packets[npk + popc_below(P)] = ((uint32_t)rc << 12) | ((uint32_t)lane << 4) | m;
+                        npk += n;
+                    }
                 }
             }
+        }
+    }
+    wave_lds_order();
+    // packets -> survivors (u16 row << 8 | column) in band raster order
+    int na = 0;
+    if (!ovf) {
+        for (int p0 = 0; p0 < npk; p0 += 64) {
+            const int p = p0 + lane;
+            const uint32_t pk = p < npk ? packets[p] : 0u;
+            const int c = __popcll(pk & 0xFu);
+            const int incl = wave_incl_scan(c);
+            const int tot = __builtin_amdgcn_readlane(incl, 63);
+            if (na + tot > kStripCap) {
+                ovf = true;
+                break;
+            }
+            int pos = na + incl - c;
+            const uint32_t e = ((pk >> 12) << 8) | (((pk >> 4) & 63u) << 2);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if ((pk >> k) & 1u) list[pos++] = (uint16_t)(e + k);
+            na += tot;
         }
     }
     wave_lds_order();
@@ -1026,41 +1086,6 @@ __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu
                       cellcnt + (size_t)f * plan->ncells + c, lane, 0);
 }
 
-// ---------------------------------------------------------------------------
-// Wave / workgroup scans shared by the octree kernels below.
-
-// Inclusive wave scan on DPP: Hillis-Steele inside each 16-lane row
-// (row_shr:1,2,4,8; lanes shifted in from outside the row add 0), then
-// row_bcast:15 / row_bcast:31 carry rows 0-1 / 0-2 into the rows above.
-// Six DPP adds instead of six LDS-routed shuffles.
-__device__ __forceinline__ int wave_incl_scan(int v) {
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-    return v;
-}
-
-// exclusive scan over the 256 threads of the block; *total = block sum
-template <int NT>
-__device__ __forceinline__ int block_excl_scan(int v, int *red, int *total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int incl = wave_incl_scan(v);
-    if (lane == 63) red[w] = incl;
-    __syncthreads();
-    int off = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < NT / 64; i++) {
-        const int r = red[i];
-        off += i < w ? r : 0;
-        tot += r;
-    }
-    __syncthreads();
-    *total = tot;
-    return off + incl - v;
-}
 
 // ---------------------------------------------------------------------------
 // Octree distribution by quadrant paths (DistributeOctTree, ORBextractor.cc:533-723

@@ -798,7 +798,7 @@ int main(int argc, char **argv) {
             for (int k = 0; k < NK; k++) {
                 if (k == 0 && j % 5 == 1) continue;  // observed by B / C only
                 if (k == 1 && j % 4 == 2) continue;
-                if (k >= 3 && (j + 7 * (size_t)k) % 26 != 0) continue;  // NK = 130: 5 more keyframes per point
+                if (k >= 3 && (j / 2 + 7 * (size_t)k) % 26 != 0) continue;  // NK = 130: 5 more keyframes per point
                 const Vector3f pc = kfs[k].mTcw * mp.mWorldPos;
                 cv::KeyPoint kp(cv::Point2f(Frame::fx * pc[0] / pc[2] + Frame::cx, Frame::fy * pc[1] / pc[2] + Frame::cy),
                                 31.f * kfs[k].mvScaleFactors[oc], -1, 0, oc);
