@@ -118,6 +118,7 @@ private:
         // which grows past its soft capacity for a large local map instead of failing
         ygzfe_frame *f = dropin::PyramidPool::instance().find_or_upload(ref->mvImagePyramid);
         if (!f) {
+            if (ok_) dropin::log_once("SearchLocalPointsDirect: keyframe pyramid", dropin::PyramidPool::instance().why().c_str());
             ok_ = false;
         } else {
             dropin::PyramidPool::instance().pin(f, 1);

@@ -31,6 +31,7 @@
 #include <set>
 #include <string>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "ygzfe.h"
@@ -92,7 +93,10 @@ public:
     // content matched every sampled byte of the old.
     template <class MatVec>
     ygzfe_frame *find_or_upload(const MatVec &levels) {
-        if (levels.empty() || !levels[0].data) return nullptr;
+        if (levels.empty() || !levels[0].data) {
+            std::lock_guard<std::mutex> lk(mu_);
+            return failed("empty mvImagePyramid");
+        }
         const int w = levels[0].cols, h = levels[0].rows, nl = (int)levels.size();
         const uint8_t *key = levels[0].data;
         const size_t stride = (size_t)levels[0].step[0];
@@ -113,11 +117,15 @@ public:
                 return touch(e)->f;
             }
         }
-        if (!ex_) return nullptr;  // no extractor yet: nothing defines the level geometry
-        Entry *e = slot(ex_, nl, w, h);
-        if (!e || !e->f) return nullptr;
+        ygzfe_extractor *ex = nullptr;
+        for (auto it = live_.rbegin(); it != live_.rend() && !ex; ++it)
+            if (it->second == nl) ex = it->first;
+        if (!ex) return failed("no live ORBextractor with this pyramid's level count defines the level geometry");
+        Entry *e = slot(ex, nl, w, h);
+        if (!e || !e->f) return failed(last_error());
         for (int l = 0; l < nl; l++)
-            if (ygzfe_frame_set_level(e->f, l, levels[l].data, (int)levels[l].step[0]) != YGZFE_OK) return nullptr;
+            if (ygzfe_frame_set_level(e->f, l, levels[l].data, (int)levels[l].step[0]) != YGZFE_OK)
+                return failed(last_error());
         e->level0.resize((size_t)w * h);
         for (int y = 0; y < h; y++) std::memcpy(&e->level0[(size_t)y * w], key + (size_t)y * stride, (size_t)w);
         set_fp(e, fp);
@@ -137,6 +145,12 @@ public:
             }
     }
 
+    // why the last lookup returned no pyramid
+    std::string why() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return why_;
+    }
+
     // pyramids a caller may hold unpinned at once (a newer lookup can recycle an older entry)
     static int soft_capacity() { return kCapacity; }
     int size() {
@@ -144,11 +158,12 @@ public:
         return (int)lru_.size();
     }
 
-    // the extractor whose level geometry uploads use (the latest one constructed)
+    // the extractors whose level geometry uploads use: the latest live one with the
+    // pyramid's level count (a destroyed extractor -- e.g. Tracking's mpIniORBextractor
+    // after initialization -- hands over to the one constructed before it)
     void set_extractor(ygzfe_extractor *ex, int nlevels) {
         std::lock_guard<std::mutex> lk(mu_);
-        ex_ = ex;
-        nlevels_ = nlevels;
+        live_.push_back(std::make_pair(ex, nlevels));
     }
     void forget_extractor(ygzfe_extractor *ex) {
         std::lock_guard<std::mutex> lk(mu_);
@@ -160,7 +175,8 @@ public:
             } else {
                 ++it;
             }
-        if (ex_ == ex) ex_ = nullptr;
+        for (auto it = live_.begin(); it != live_.end();)
+            it = it->first == ex ? live_.erase(it) : it + 1;
     }
 
 private:
@@ -276,12 +292,16 @@ private:
         e.level0.clear();
         return &e;
     }
+    ygzfe_frame *failed(const char *why) {
+        why_ = why ? why : "";
+        return nullptr;
+    }
     std::mutex mu_;
+    std::string why_;
     std::list<Entry> lru_;
     std::unordered_map<const uint8_t *, Entry *> by_ptr_;
     std::unordered_multimap<uint64_t, Entry *> by_fp_;
-    ygzfe_extractor *ex_ = nullptr;
-    int nlevels_ = 0;
+    std::vector<std::pair<ygzfe_extractor *, int>> live_;  // (extractor, nlevels), construction order
 };
 
 // cv::KeyPoint has the 28-byte ygzfe_kp layout (pt.x, pt.y, size, angle, response, octave, class_id)

@@ -3,10 +3,9 @@
 //  * k_sparse_align: SparseImgAlign::run (SparseImageAlign.cc:20-49) with
 //    precomputeReferencePatches (:57-128), computeResiduals (:130-231), the
 //    Gauss-Newton loop of NLSSolver_impl.hpp:18-91, LDLT solve (:233-238) and
-//    T <- T * exp(-x) (:240-244).  One 256-thread workgroup per frame pair runs
-//    every level and iteration; the (feature, pixel) residual terms are spread
-//    over the workgroup and H / Jres / chi2 are reduced with wave shuffles +
-//    LDS.  The reduction order differs from the reference's sequential sum,
+//    T <- T * exp(-x) (:240-244).  One 1024-thread workgroup per frame pair runs
+//    every level and iteration (wave 0 solves, waves 1..15 own one feature per
+//    lane); H / Jres / chi2 are reduced with DPP wave steps + one LDS pass.  The reduction order differs from the reference's sequential sum,
 //    so poses agree within 1e-4, not bitwise.
 //  * k_align2d: Align2D (Align.cc:8-105), one lane per patch, sequential float
 //    order as the reference -> bit-exact with oracle/.
@@ -595,7 +594,11 @@ __device__ __attribute__((noinline)) void sparse_align_generic(const AlignLevels
 // Sx = sum gx*res, Sy = sum gy*res, Sxx, Sxy, Syy (same algebra, different
 // float association than the reference's per-pixel sums -> 1e-4 pose parity).
 // The per-feature sums are reduced by transposing DPP / permlane steps
-// (wave_reduce8 / wave_reduce32) and one LDS pass over the waves.
+// (wave_reduce8 / wave_reduce32) and one LDS pass over the waves.  H is the
+// level's visible-feature sum less the features projected out of bounds in the
+// iteration (SparseImageAlign.cc:160-163 skips them): their H_f is recomputed from
+// the level's moments Sxx, Sxy, Syy kept in registers and summed per wave, so LDS
+// holds only the reference patches (61 KB).
 #ifdef YGZ_STAMPS
 // diagnostic build only (lib/libygzfe_diag.so): solver-wave timestamps of block 0
 __device__ unsigned long long g_stamps[4096];
@@ -694,10 +697,8 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
     }
     __shared__ float s_part[NW][32];
     __shared__ float s_patch[16][NF];  // ref_patch_cache_ of the owned features (column = feature)
-    __shared__ float s_Hf[21][NF];     // per-feature H contribution of the level (upper triangle)
-    __shared__ float s_Hvis[21];       // sum of s_Hf over the level's features
-    __shared__ uint16_t s_out[NF];     // features projected out of bounds this iteration
-    __shared__ int s_nout;
+    __shared__ float s_Hvis[21];       // the level's H over its visible features
+    __shared__ float s_opart[NW][24];  // per-wave H of the features projected out of bounds this iteration
     __shared__ SE3 s_T, s_old;
     __shared__ float s_chi2, s_Hpk[21];  // H of the last iteration, upper triangle row-major
     __shared__ int s_stop, s_break, s_nmeas;
@@ -711,7 +712,6 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
         s_stop = 0;
         s_nmeas = 0;
         s_break = 0;
-        s_nout = 0;
         for (int i = 0; i < 21; i++) s_Hpk[i] = 0.f;
     }
     __syncthreads();
@@ -720,7 +720,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
         // ---------------- solver wave: reduce partials, LDLT, T <- T exp(-x) (NLSSolver_impl.hpp:18-91)
         for (int level = job.max_level; level >= job.min_level; level--) {
             if (tid == 0) s_old = s_T;
-            __syncthreads();  // L0: level start, s_part = per-wave sums of s_Hf
+            __syncthreads();  // L0: level start, s_part = per-wave sums of the features' H
             YGZ_STAMP(1);
             if (lane < 21) {
                 float r = 0.f;
@@ -746,19 +746,11 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                 if (lane < 29) {
                     if (lane < 8) {
                         r = pk8;
-                    } else {  // H = H_vis - sum of the out-of-bounds features' H_f
-                        const int k = lane - 8, nout = s_nout;
+                    } else {  // H = H_vis - sum of the out-of-bounds features' H_f (per-wave sums)
+                        const int k = lane - 8;
                         float o = 0.f;
-                        int i = 0;
-                        for (; i + 4 <= nout; i += 4) {  // independent LDS reads, same summation order
-                            const int a0 = s_out[i], a1 = s_out[i + 1], a2 = s_out[i + 2], a3 = s_out[i + 3];
-                            const float v0 = s_Hf[k][a0], v1 = s_Hf[k][a1], v2 = s_Hf[k][a2], v3 = s_Hf[k][a3];
-                            o += v0;
-                            o += v1;
-                            o += v2;
-                            o += v3;
-                        }
-                        for (; i < nout; i++) o += s_Hf[k][s_out[i]];
+#pragma unroll
+                        for (int w = 1; w < NW; w++) o += s_opart[w][k];
                         r = s_Hvis[k] - o;
                         s_Hpk[k] = r;  // H of this iteration (the result's Fisher information)
                     }
@@ -768,10 +760,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                     float x[6];
                     const int nmeas = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 7));
                     const float new_chi2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 6)) / (float)nmeas;
-                    if (lane == 0) {
-                        s_nout = 0;
-                        s_nmeas = nmeas;
-                    }
+                    if (lane == 0) s_nmeas = nmeas;
                     YGZ_STAMP(7);
                     ldlt_solve6_nopiv(r, x);
                     YGZ_STAMP(8);
@@ -836,6 +825,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
     float gx[16], gy[16];
 #pragma unroll
     for (int p = 0; p < 16; p++) { gx[p] = 0.f; gy[p] = 0.f; s_patch[p][f] = 0.f; }
+    float Sxx = 0.f, Sxy = 0.f, Syy = 0.f;  // the level's gradient moments (H_f of an out-of-bounds feature)
     for (int level = job.max_level; level >= job.min_level; level--) {
         const int W = lv.w[level], H = lv.h[level];
         const float scale = lv.inv_scale[level];
@@ -893,7 +883,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
             for (int p = 0; p < 16; p++) { gx[p] = 0.f; gy[p] = 0.f; }
         }
         {
-            float Sxx = 0.f, Sxy = 0.f, Syy = 0.f;
+            Sxx = 0.f, Sxy = 0.f, Syy = 0.f;
 #pragma unroll
             for (int p = 0; p < 16; p++) { Sxx += gx[p] * gx[p]; Sxy += gx[p] * gy[p]; Syy += gy[p] * gy[p]; }
             const float fs2 = fs * fs;
@@ -908,7 +898,6 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                     const float hrc = fj[r] * fj[c] * Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * Sxy +
                                       fj[6 + r] * fj[6 + c] * Syy;
                     hv[m] = (own && vis) ? hrc * fs2 : 0.f;
-                    if (own) s_Hf[m][f] = hv[m];
                     m++;
                 }
 #pragma unroll
@@ -922,6 +911,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
             float acc[8];
 #pragma unroll
             for (int k = 0; k < 8; k++) acc[k] = 0.f;
+            bool out_now = false;
             if (own && vis) {
                 // The residual loop runs in fused multiply-adds and projects with
                 // one reciprocal of z: rounding-level differences from the
@@ -937,7 +927,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                 const float v = __builtin_fmaf(cam.fy * pc3[1], izc, cam.cy) * scale;
                 const int ui = (int)floorf(u), vi = (int)floorf(v);
                 if (ui < 0 || vi < 0 || ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H) {
-                    s_out[atomicAdd(&s_nout, 1)] = (uint16_t)f;
+                    out_now = true;
                 } else {
                     const float su = u - ui, sv = v - vi;
                     const float wtl = wmulf(1.f - su, 1.f - sv), wtr = wmulf(su, 1.f - sv);
@@ -974,6 +964,28 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
             {
                 const float t = wave_reduce8(acc, lane);
                 if ((lane & 7) == 0) s_part[wave][lane >> 3] = t;
+            }
+            // H_f of the features projected out of bounds, summed per wave (usually none)
+            if (__ballot(out_now)) {
+                float fj[12];
+                jacob_xyz2cam_fresh(X, Y, Z, fj);
+                const float fs2 = fs * fs;
+                float hv[32];
+                int m = 0;
+#pragma unroll
+                for (int r = 0; r < 6; r++)
+#pragma unroll
+                    for (int c = r; c < 6; c++) {
+                        const float hrc = fj[r] * fj[c] * Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * Sxy +
+                                          fj[6 + r] * fj[6 + c] * Syy;
+                        hv[m++] = out_now ? hrc * fs2 : 0.f;
+                    }
+#pragma unroll
+                for (int k = 21; k < 32; k++) hv[k] = 0.f;
+                const float t = wave_reduce32(hv, lane);
+                if ((lane & 1) == 0 && (lane >> 1) < 21) s_opart[wave][lane >> 1] = t;
+            } else if (lane < 21) {
+                s_opart[wave][lane] = 0.f;
             }
             __syncthreads();  // A
             __syncthreads();  // B

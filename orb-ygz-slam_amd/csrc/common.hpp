@@ -49,21 +49,7 @@ struct LevelDesc {
     // octree path codes (k_octree_paths): root bits, quadrant depth carried, and the
     // separable code tables in Plan::dtabs (code = X[x] | Y[y], key coordinates)
     int oct_rb, oct_dn, oct_xtab, oct_ytab;
-    // FAST strips (k_fast_strips): nstrips records of kStripInts ints at Plan::dtabs + strip_off
-    int strip_off, nstrips;
 };
-
-// A FAST strip: <= 8 consecutive cells of one cell row whose ROI columns fit one
-// 256-byte window that starts at a multiple of 4 (plan.cpp); k_fast_strips runs one
-// wave over it.  Ints in Plan::dtabs:
-//   [0] xs | y0 << 16   window's first level column, band (ROI) top row
-//   [1] rh | level << 16  band rows
-//   [2] tx0 | tx1 << 16   tested columns [tx0, tx1), window-relative
-//   [3] c0                first cell (plan index), [4] nc cells
-//   [5] column table: int offset in dtabs of 256 bytes, byte x = the cell (0..7) of
-//       window column x | first column of its cell << 4 | last << 5, 0xFF untested
-constexpr int kStripInts = 8;
-constexpr int kStripMaxCells = 8;
 
 struct alignas(16) CellDesc {
     int16_t x0, y0, rw, rh;   // ROI origin / size in level pixels

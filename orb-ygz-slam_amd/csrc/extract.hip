@@ -510,7 +510,7 @@ __global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(const uint8_t *__re
 }
 
 // ---------------------------------------------------------------------------
-// Wave / workgroup scans (FAST strips, octree).
+// Wave / workgroup scans (octree).
 
 // Inclusive wave scan on DPP: Hillis-Steele inside each 16-lane row
 // (row_shr:1,2,4,8; lanes shifted in from outside the row add 0), then
@@ -576,15 +576,9 @@ __device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
     return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
 
-// Two FAST paths share the segment test below:
-//   k_fast_strips (every launch): one wave per strip -- <= 8 consecutive cells of one
-//     cell row -- stages the strip's band (the cells' ROI rows, 256 columns) in LDS once,
-//     screens every interior pixel from aligned row dwords with the column neighbours
-//     from the adjacent lanes (DPP), then runs the segment test + cornerScore on the
-//     survivors, NMS inside each cell and the per-cell lists;
-//   fast_cell_item (a cell's minThFAST retry, and a strip whose survivor or corner lists
-//     would overflow): one cell ROI staged in LDS, phases A-D below.
-// Both give cv::FAST's corners, scores and order per cell (ORBextractor.cc:747-781).
+// FAST-9 per cell (k_fast_cells): one cell ROI staged in LDS, phases A-D of
+// fast_cell_item give cv::FAST's corners, scores and order per cell
+// (ORBextractor.cc:747-781).
 
 // a wave's per-cell LDS slice (16-B aligned): ROI tile S*R, score map S*R, pixel list
 __host__ __device__ constexpr int fast_slice_bytes(int S, int R) {
@@ -799,264 +793,15 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
     if (lane == 0) *cnt_out = min(total, plan->cell_cap);
 }
 
-// ---------------------------------------------------------------------------
-// k_fast_strips: one wave per (strip, frame).
-//
-// Per strip (plan.cpp: <= 8 cells of one cell row, ROI columns inside a 256-byte
-// window from a multiple of 4; the cells' ROIs share the band's rows):
-//   1  the band's rows are read once (one coalesced dword per lane per row, 8 rows in
-//      flight) into LDS at a 260-byte stride (rows shift one bank);
-//   2  as soon as row r + 3 is in, row r is screened at iniThFAST: T / C / B are aligned
-//      LDS dwords, the 3-left / 3-right dwords come from the neighbouring lanes (DPP
-//      wave shifts, v_alignbyte); a lane with survivors appends one packet (row, lane,
-//      4-bit mask: one ballot per row), and the packets expand into a u16 survivor
-//      list in band raster order (a wave scan per 64 packets);
-//   3  segment test + score on the survivors (fast_arcmax2), corners kept with their
-//      arcmax in a u32 list (raster order);
-//   4  the band is zeroed and becomes the score map (arcmax at the corners); strict
-//      3x3 NMS per corner where the neighbours in another cell count as 0 -- cv::FAST
-//      on the cell's ROI sees 0 outside its [3, w - 3) interior -- so a corner is kept
-//      iff arcmax > every in-cell neighbour's arcmax (scores = arcmax - 1);
-//   5  kept corners appended to their cell's list in raster order (ranks by ballots on
-//      the 3-bit cell index), counts per cell in LDS;
-//   6  a cell with no kept corner reruns at minThFAST through fast_cell_item (its ROI
-//      staged into the now free LDS); a strip whose survivor or corner list would
-//      overflow runs every cell through fast_cell_item (both thresholds).
-constexpr int kStripStride = 260;      // band row stride (65 dwords)
-constexpr int kStripCap = 1024;        // screen survivors per strip
-constexpr int kStripCornerCap = 512;   // corners per strip
-constexpr int kStripPF = 8;            // band rows in flight
-__host__ __device__ constexpr int strip_band_bytes(int rh) { return (rh * kStripStride + 15) / 16 * 16; }
-__host__ __device__ constexpr int strip_main_bytes(int rh, int S, int R) {
-    return strip_band_bytes(rh) + 2 * kStripCap + 4 * kStripCornerCap > fast_slice_bytes(S, R)
-               ? strip_band_bytes(rh) + 2 * kStripCap + 4 * kStripCornerCap
-               : fast_slice_bytes(S, R);
-}
-struct StripRec {
-    int xy, rl, tx, c0, nc, col, pad0, pad1;
-};
-
-template <int S, int R>
-__global__ __launch_bounds__(64) void k_fast_strips(const uint8_t *__restrict__ pyr, uint32_t pitch,
-                                                    const Plan *__restrict__ plan,
-                                                    const CellDesc *__restrict__ cells, uint32_t *__restrict__ cellbuf,
-                                                    int *__restrict__ cellcnt, int level, int band_rows,
-                                                    int *__restrict__ clear_flag) {
-    extern __shared__ uint8_t s_dyn[];
-    const int lane = threadIdx.x;
-    const int f = blockIdx.y;
-    int l = level, sl = blockIdx.x;
-    if (l < 0) {  // one launch over every level's strips: the strip's level
-        l = 0;
-        while (sl >= plan->lv[l].nstrips) sl -= plan->lv[l].nstrips, l++;
-    }
-    if (clear_flag && blockIdx.x == 0 && f == 0 && lane == 0) *clear_flag = 0;  // the octree's overflow flag
-    const LevelDesc &L = plan->lv[l];
-    const StripRec sr = scalar_load(reinterpret_cast<const StripRec *>(plan->dtabs + L.strip_off + kStripInts * sl));
-    const int xs = sr.xy & 0xFFFF, y0 = sr.xy >> 16, rh = sr.rl & 0xFFFF;
-    const int tx0 = sr.tx & 0xFFFF, tx1 = sr.tx >> 16, c0 = sr.c0, nc = sr.nc;
-    const int main_bytes = strip_main_bytes(band_rows, S, R);
-    uint8_t *band = s_dyn;
-    uint16_t *list = reinterpret_cast<uint16_t *>(s_dyn + strip_band_bytes(band_rows));
-    uint32_t *corners = reinterpret_cast<uint32_t *>(list + kStripCap);
-    uint8_t *ctab = s_dyn + main_bytes;
-    int *cnt = reinterpret_cast<int *>(ctab + 256);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(pyr + (size_t)f * pitch + L.off), 0, (int)((uint32_t)L.w * (uint32_t)L.h), 0x00020000);
-    const int th = plan->ini_th;
-    // the column table (cell of each window column, its edges; 0xFF = not tested)
-    const uint32_t tab = as_global(plan->dtabs)[sr.col + lane];
-    reinterpret_cast<uint32_t *>(ctab)[lane] = tab;
-    if (lane < kStripMaxCells) cnt[lane] = 0;
-    uint32_t colmask = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) colmask |= (uint32_t)(((tab >> (8 * k)) & 0xFFu) != 0xFFu) << k;
-    (void)tx0;
-    (void)tx1;
-
-    // 1 + 2: band rows in, each row screened once the row three below it is in
-    const bool aligned = (L.w & 3) == 0;
-    const uint32_t w = (uint32_t)L.w;
-    uint32_t blo[kStripPF], bhi[kStripPF];
-    auto issue = [&](int r, uint32_t &lo, uint32_t &hi) {
-        const uint32_t o = ((uint32_t)(y0 + r) * w + (uint32_t)xs) & ~3u;
-        lo = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4u * (uint32_t)lane, 0, 0);
-        hi = aligned ? 0u : __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4u * (uint32_t)lane + 4u, 0, 0);
-    };
-#pragma unroll
-    for (int i = 0; i < kStripPF; i++)
-        if (i < rh) issue(i, blo[i], bhi[i]);
-    int npk = 0;
-    bool ovf = false;
-    uint32_t *packets = corners;  // the corner list's memory until the survivors are expanded
-    const uint32_t *bw = reinterpret_cast<const uint32_t *>(band);
-    for (int r0 = 0; r0 < rh; r0 += kStripPF) {
-#pragma unroll
-        for (int i = 0; i < kStripPF; i++) {
-            const int r = r0 + i;
-            if (r >= rh) break;
-            const uint32_t sh = ((uint32_t)(y0 + r) * w + (uint32_t)xs) & 3u;
-            const uint32_t v = aligned ? blo[i] : __builtin_amdgcn_alignbyte(bhi[i], blo[i], sh);
-            if (r + kStripPF < rh) issue(r + kStripPF, blo[i], bhi[i]);
-            reinterpret_cast<uint32_t *>(band + r * kStripStride)[lane] = v;
-            if (r >= 6) {
-                const int rc = r - 3;
-                const uint32_t T = bw[(rc - 3) * (kStripStride / 4) + lane];
-                const uint32_t Cc = bw[rc * (kStripStride / 4) + lane];
-                const uint32_t B = v;
-                const uint32_t Cp = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Cc, 0x138, 0xF, 0xF, false);  // lane - 1
-                const uint32_t Cn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Cc, 0x130, 0xF, 0xF, false);  // lane + 1
-                const uint32_t Lw = __builtin_amdgcn_alignbyte(Cc, Cp, 1);  // x-3 .. x
-                const uint32_t Rw = __builtin_amdgcn_alignbyte(Cn, Cc, 3);  // x+3 .. x+6
-                const uint32_t m = fast_screen4(T, B, Lw, Rw, Cc, th) & colmask;
-                // one packet (row, lane, 4-bit mask) per lane with a survivor, in lane order
-                const uint64_t P = __ballot(m != 0u);
-                if (P) {
-                    const int n = __popcll(P);
-                    if (npk + n > kStripCornerCap) ovf = true;
-                    if (!ovf) {
-                        if (m) packets[npk + popc_below(P)] = ((uint32_t)rc << 12) | ((uint32_t)lane << 4) | m;
-                        npk += n;
-                    }
-                }
-            }
-        }
-    }
-    wave_lds_order();
-    // packets -> survivors (u16 row << 8 | column) in band raster order
-    int na = 0;
-    if (!ovf) {
-        for (int p0 = 0; p0 < npk; p0 += 64) {
-            const int p = p0 + lane;
-            const uint32_t pk = p < npk ? packets[p] : 0u;
-            const int c = __popcll(pk & 0xFu);
-            const int incl = wave_incl_scan(c);
-            const int tot = __builtin_amdgcn_readlane(incl, 63);
-            if (na + tot > kStripCap) {
-                ovf = true;
-                break;
-            }
-            int pos = na + incl - c;
-            const uint32_t e = ((pk >> 12) << 8) | (((pk >> 4) & 63u) << 2);
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                if ((pk >> k) & 1u) list[pos++] = (uint16_t)(e + k);
-            na += tot;
-        }
-    }
-    wave_lds_order();
-
-    // 3: segment test + score on the survivors, two per lane
-    int ncorn = 0;
-    if (!ovf) {
-        for (int i0 = 0; i0 < na; i0 += 128) {
-            const int i = i0 + 2 * lane;
-            const uint32_t pr = reinterpret_cast<const uint32_t *>(list)[i >> 1];
-            const bool v0 = i < na, v1 = i + 1 < na;
-            const uint32_t e0 = v0 ? (pr & 0xFFFFu) : 0x0303u, e1 = v1 ? (pr >> 16) : 0x0303u;
-            const s16x2 am = fast_arcmax2<kStripStride>(band, e0, e1);
-            const bool k0 = v0 && am.x > th, k1 = v1 && am.y > th;
-            const uint64_t M0 = __ballot(k0), M1 = __ballot(k1);
-            const int n = __popcll(M0) + __popcll(M1);
-            if (ncorn + n > kStripCornerCap) {
-                ovf = true;
-                break;
-            }
-            const int pos = ncorn + popc_below(M0) + popc_below(M1);
-            if (k0) corners[pos] = ((uint32_t)am.x << 16) | e0;
-            if (k1) corners[pos + (k0 ? 1 : 0)] = ((uint32_t)am.y << 16) | e1;
-            ncorn += n;
-        }
-    }
-    wave_lds_order();
-
-    if (!ovf) {
-        // 4: the band becomes the score map
-        {
-            uint4 *z = reinterpret_cast<uint4 *>(band);
-            const uint4 zero = {0u, 0u, 0u, 0u};
-            for (int i = lane; i < strip_band_bytes(rh) / 16; i += 64) z[i] = zero;
-        }
-        wave_lds_order();
-        for (int i = lane; i < ncorn; i += 64) {
-            const uint32_t e = corners[i];
-            band[((e >> 8) & 0xFFu) * kStripStride + (e & 0xFFu)] = (uint8_t)(e >> 16);
-        }
-        wave_lds_order();
-        // 5: NMS inside each cell; kept corners -> their cell's list in raster order
-        const int cap = plan->cell_cap;
-        uint32_t *fbuf = cellbuf + ((size_t)f * plan->ncells + c0) * cap;
-        for (int i0 = 0; i0 < ncorn; i0 += 64) {
-            const int i = i0 + lane;
-            bool keep = false;
-            uint32_t e = 0, k = 0;
-            if (i < ncorn) {
-                e = corners[i];
-                const uint32_t x = e & 0xFFu, y = (e >> 8) & 0xFFu, am = e >> 16;
-                const uint32_t tb = ctab[x];
-                k = tb & 7u;
-                const uint8_t *r = band + (y - 1) * kStripStride + (x - 1);
-                const uint32_t lm = max(max((uint32_t)r[0], (uint32_t)r[kStripStride]), (uint32_t)r[2 * kStripStride]);
-                const uint32_t rm = max(max((uint32_t)r[2], (uint32_t)r[kStripStride + 2]), (uint32_t)r[2 * kStripStride + 2]);
-                const uint32_t mm = max((uint32_t)r[1], (uint32_t)r[2 * kStripStride + 1]);
-                const uint32_t nb = max(max((tb & 16u) ? 0u : lm, (tb & 32u) ? 0u : rm), mm);
-                keep = am > nb;
-            }
-            const uint64_t K = __ballot(keep);
-            const uint64_t B0 = __ballot(keep && (k & 1u)), B1 = __ballot(keep && (k & 2u)), B2 = __ballot(keep && (k & 4u));
-            if (keep) {
-                const uint64_t eq = K & ((k & 1u) ? B0 : ~B0) & ((k & 2u) ? B1 : ~B1) & ((k & 4u) ? B2 : ~B2);
-                const int pos = cnt[k] + popc_below(eq);
-                if (pos < cap) {
-                    const uint32_t x = e & 0xFFu, y = (e >> 8) & 0xFFu;
-                    fbuf[(size_t)k * cap + pos] = pack_key(xs + (int)x - kMinBorder, y0 + (int)y - kMinBorder,
-                                                           (int)(e >> 16) - 1);
-                }
-                if ((eq >> lane) == 1ull) cnt[k] = pos + 1;  // the cell's last lane in this batch
-            }
-            wave_lds_order();
-        }
-    }
-    wave_lds_order();
-
-    // 6: counts; the minThFAST retry of cells without a kept corner (all cells on overflow)
-    const int mine = lane < nc ? cnt[lane] : 1;
-    const uint64_t all = nc >= 64 ? ~0ull : ((1ull << nc) - 1ull);
-    uint64_t redo = ovf ? all : (__ballot(lane < nc && mine == 0) & all);
-    if (lane < nc && !((redo >> lane) & 1ull))
-        cellcnt[(size_t)f * plan->ncells + c0 + lane] = min(mine, plan->cell_cap);
-    redo = __builtin_amdgcn_readfirstlane((uint32_t)redo) | ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(redo >> 32)) << 32);
-    while (redo) {
-        const int k = __builtin_ctzll(redo);
-        redo &= redo - 1;
-        const CellDesc cd = scalar_load(cells + c0 + k);
-        uint8_t *img = s_dyn;
-        uint8_t *sc = img + S * R;
-        uint16_t *clist = reinterpret_cast<uint16_t *>(sc + S * R);
-        const uint32_t off0 = (uint32_t)cd.y0 * (uint32_t)L.w + (uint32_t)cd.x0;
-        wave_lds_order();
-        {
-            RoiStage<S, R> st;
-            st.issue(rs, off0, L.w, cd.rw, cd.rh, lane);
-            st.commit(img, off0, L.w, cd.rw, cd.rh, lane);
-        }
-        fast_cell_item<S>(plan, cd, img, sc, clist, cellbuf + ((size_t)f * plan->ncells + c0 + k) * plan->cell_cap,
-                          cellcnt + (size_t)f * plan->ncells + c0 + k, lane, ovf ? 0 : 1);
-    }
-}
-
-// per-level ROI slice for the retry path: the level's largest cell ROI, row stride a
-// multiple of 4 (>= 36), rows rounded up to 8 (>= 40)
+// per-level ROI slice: the level's largest cell ROI, row stride a multiple of 4
+// (>= 36), rows rounded up to 8 (>= 40)
 static void fast_slice_shape(int rw, int rh, int &S, int &R) {
     S = rw <= 36 ? 36 : ((rw + 7) / 8) * 8;
     R = std::max(40, ((rh + 7) / 8) * 8);
 }
-static size_t fast_strips_lds_bytes(int band_rows, int S, int R) {
-    return (size_t)strip_main_bytes(band_rows, S, R) + 256 + 64;
-}
 
-// The per-cell path as a whole launch (one wave per (cell, frame), four per workgroup):
-// the A/B reference for k_fast_strips (YGZFE_FAST_CELLS=1 selects it).
+// One wave per (cell, frame), four per workgroup: the cell's ROI staged into the
+// wave's LDS slice, then fast_cell_item.
 constexpr int kFastWaves = 4;
 template <int S, int R>
 __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(6))) void k_fast_cells(
@@ -2417,17 +2162,11 @@ static void fast_shape_pick(int rw, int rh, int &S, int &R) {
 }
 #define YGZ_FAST_SHAPES(X) X(36, 40) X(40, 40) X(40, 48) X(40, 56) X(48, 48) X(56, 56) X(64, 64) X(72, 72)
 
-// YGZFE_FAST_CELLS=1: the per-cell kernel instead of the strips (A/B reference)
-static bool fast_cells_path() {
-    static const bool on = getenv("YGZFE_FAST_CELLS") != nullptr && getenv("YGZFE_FAST_CELLS")[0] == '1';
-    return on;
-}
-
 hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const CellDesc *dcells,
                        uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st0, const hipStream_t *lvl_streams,
                        int n_lvl_streams) {
     if (hp.ncells == 0) return hipSuccess;
-    // one launch per level: the level's band height and ROI shape size the LDS
+    // one launch per level: the level's ROI shape sizes the LDS slices
     for (int l = 0; l < hp.nlevels; l++) {
         const LevelDesc &L = hp.lv[l];
         if (L.ncells == 0) continue;
@@ -2436,64 +2175,41 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
         // level 0 on the caller's stream, the others spread over the given side streams
         const hipStream_t st = (l == 0 || !lvl_streams || n_lvl_streams <= 0) ? st0
                                                                                 : lvl_streams[(l - 1) % n_lvl_streams];
-        if (fast_cells_path()) {
-            const size_t lds = kFastWaves * (size_t)fast_slice_bytes(S, R);
-            const dim3 grid((L.ncells + kFastWaves - 1) / kFastWaves, nframes);
+        const size_t lds = kFastWaves * (size_t)fast_slice_bytes(S, R);
+        const dim3 grid((L.ncells + kFastWaves - 1) / kFastWaves, nframes);
 #define YGZ_FAST(SS, RR)                                                                                        \
     if (S == SS && R == RR)                                                                                     \
         hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, \
                            cellbuf, cellcnt, L.cell_begin, L.cell_begin + L.ncells, l, nullptr);
-            YGZ_FAST_SHAPES(YGZ_FAST)
+        YGZ_FAST_SHAPES(YGZ_FAST)
 #undef YGZ_FAST
-        } else {
-            const size_t lds = fast_strips_lds_bytes(L.fast_rh, S, R);
-            const dim3 grid(L.nstrips, nframes);
-#define YGZ_FAST(SS, RR)                                                                                           \
-    if (S == SS && R == RR)                                                                                        \
-        hipLaunchKernelGGL((k_fast_strips<SS, RR>), grid, dim3(64), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, \
-                           l, L.fast_rh, nullptr);
-            YGZ_FAST_SHAPES(YGZ_FAST)
-#undef YGZ_FAST
-        }
     }
     return hipGetLastError();
 }
 
-// Every level's strips in ONE launch (the single-frame path: one frame's strips
-// fill the GPU anyway, and three dependent launches cost three dispatch gaps):
-// the LDS of the tallest band and the largest ROI of any level.
+// Every level's cells in ONE launch (the single-frame path: one frame's cells fill
+// the GPU anyway, and three dependent launches cost three dispatch gaps): the
+// slices of the largest ROI of any level.
 hipError_t launch_fast_merged(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp,
                               const CellDesc *dcells, uint32_t *cellbuf, int *cellcnt, int nframes, hipStream_t st,
                               int *clear_flag) {
     if (hp.ncells == 0) return hipSuccess;
-    int rw = 0, rh = 0, nstrips = 0;
+    int rw = 0, rh = 0;
     for (int l = 0; l < hp.nlevels; l++) {
         if (hp.lv[l].ncells == 0) continue;
         rw = std::max(rw, hp.lv[l].fast_rw);
         rh = std::max(rh, hp.lv[l].fast_rh);
-        nstrips += hp.lv[l].nstrips;
     }
     int S, R;
     fast_shape_pick(rw, rh, S, R);
-    if (fast_cells_path()) {
-        const size_t lds = kFastWaves * (size_t)fast_slice_bytes(S, R);
-        const dim3 grid((hp.ncells + kFastWaves - 1) / kFastWaves, nframes);
+    const size_t lds = kFastWaves * (size_t)fast_slice_bytes(S, R);
+    const dim3 grid((hp.ncells + kFastWaves - 1) / kFastWaves, nframes);
 #define YGZ_FAST(SS, RR)                                                                                        \
     if (S == SS && R == RR)                                                                                     \
         hipLaunchKernelGGL((k_fast_cells<SS, RR>), grid, dim3(64 * kFastWaves), lds, st, pyr, pitch, dp, dcells, \
                            cellbuf, cellcnt, 0, hp.ncells, -1, clear_flag);
-        YGZ_FAST_SHAPES(YGZ_FAST)
+    YGZ_FAST_SHAPES(YGZ_FAST)
 #undef YGZ_FAST
-    } else {
-        const size_t lds = fast_strips_lds_bytes(rh, S, R);
-        const dim3 grid(nstrips, nframes);
-#define YGZ_FAST(SS, RR)                                                                                           \
-    if (S == SS && R == RR)                                                                                        \
-        hipLaunchKernelGGL((k_fast_strips<SS, RR>), grid, dim3(64), lds, st, pyr, pitch, dp, dcells, cellbuf, cellcnt, \
-                           -1, rh, clear_flag);
-        YGZ_FAST_SHAPES(YGZ_FAST)
-#undef YGZ_FAST
-    }
     return hipGetLastError();
 }
 

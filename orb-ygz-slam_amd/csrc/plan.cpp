@@ -224,45 +224,6 @@ int build_plan(const ygzfe_orb_params &p, int W, int H, PlanHost *ph, char *err,
             }
         }
         L.ncells = (int)ph->cells.size() - L.cell_begin;
-        // FAST strips: each cell row cut into runs of <= 8 cells whose ROI columns fit a
-        // 256-byte window from a multiple of 4 (one wave: 64 lanes x 4 columns)
-        {
-            std::vector<int> recs, tabs;
-            const int c_end = L.cell_begin + L.ncells;
-            for (int j = L.cell_begin; j < c_end;) {
-                const CellDesc &a = ph->cells[j];
-                const int xs = a.x0 & ~3;
-                int k = j;
-                while (k < c_end && k - j < kStripMaxCells && ph->cells[k].y0 == a.y0 &&
-                       ph->cells[k].x0 + ph->cells[k].rw - xs <= 256)
-                    k++;
-                const CellDesc &b = ph->cells[k - 1];
-                const int tx0 = a.x0 + 3 - xs, tx1 = b.x0 + b.rw - 3 - xs;
-                int rec[kStripInts] = {xs | (a.y0 << 16), a.rh | (l << 16), tx0 | (tx1 << 16), j, k - j, 0, 0, 0};
-                rec[5] = (int)tabs.size();  // made absolute below
-                uint8_t col[256];
-                memset(col, 0xFF, sizeof(col));
-                for (int c = j; c < k; c++) {
-                    const CellDesc &cd = ph->cells[c];
-                    const int c0 = cd.x0 + 3 - xs, c1 = cd.x0 + cd.rw - 3 - xs;  // tested columns of cell c
-                    for (int x = c0; x < c1; x++)
-                        col[x] = (uint8_t)((c - j) | (x == c0 ? 16 : 0) | (x == c1 - 1 ? 32 : 0));
-                }
-                for (int q = 0; q < 64; q++) {
-                    int v;
-                    memcpy(&v, col + 4 * q, 4);
-                    tabs.push_back(v);
-                }
-                recs.insert(recs.end(), rec, rec + kStripInts);
-                j = k;
-            }
-            L.nstrips = (int)recs.size() / kStripInts;
-            L.strip_off = (int)ph->tabs.size();
-            const int tab_base = L.strip_off + (int)recs.size();
-            for (int s = 0; s < L.nstrips; s++) recs[s * kStripInts + 5] += tab_base;
-            ph->tabs.insert(ph->tabs.end(), recs.begin(), recs.end());
-            ph->tabs.insert(ph->tabs.end(), tabs.begin(), tabs.end());
-        }
         // DistributeOctTree initial nodes (ORBextractor.cc:537-539)
         int nIni = (int)roundf((float)(maxBX - minB) / (maxBY - minB));
         if (nIni < 1) nIni = 1;

@@ -769,7 +769,8 @@ int main(int argc, char **argv) {
             return k < 3 ? s3[k][c] : (c == 0 ? (k * 5) % 9 - 4 : (k * 3) % 7 - 3);
         };
         for (int k = 0; k < NK; k++) {
-            const cv::Mat kim = k == 0 ? im0 : synth(W, H, 7u, shift(k, 0), shift(k, 1));
+            cv::Mat kim = k == 0 ? im0 : synth(W, H, 7u, shift(k, 0), shift(k, 1));
+            if (k >= 3) kim.data[k] ^= 0x5A;  // row 0 (no window reaches it): every keyframe's pyramid distinct
             kframes.push_back(Frame(kim, T.mpORBextractorLeft));
             kfs[k].mvImagePyramid = kframes[k].mvImagePyramid;  // shared, as KeyFrame.cc:257-260
             kfs[k].mvScaleFactors = kframes[k].mvScaleFactors;

@@ -20,6 +20,9 @@ def test_reference_call_sites_compile_and_match_the_oracle(gpu):
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().endswith("OK")
     for line in ("mpAlign->run(&mLastFrame, &mCurrentFrame, TCR)", "DSO_KEYPOINT", "ORBSLAM_KEYPOINT",
-                 "SearchForInitialization", "SearchByBoW", "ygz::Align2D", "SearchLocalPointsDirect() [mnCacheHitTh 150]",
-                 "SearchLocalPointsDirect() [mnCacheHitTh 1073741824]", "matcher.FindDirectProjection"):
+                 "SearchForInitialization", "SearchByBoW", "ygz::Align2D", "SearchLocalPointsDirect() [3 keyframes, mnCacheHitTh 150]",
+                 "SearchLocalPointsDirect() [3 keyframes, mnCacheHitTh 1073741824]",
+                 "SearchLocalPointsDirect() [130 keyframes, mnCacheHitTh 150]",
+                 "the pyramid pool grew past its soft capacity", "matcher.FindDirectProjection",
+                 "Frame::ComputeStereoMatches()", "Frame::ComputeBoW()", "remap(mImDepth) CV_32F"):
         assert line in r.stdout

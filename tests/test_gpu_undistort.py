@@ -163,7 +163,8 @@ def test_remap_depth_f32_bitexact(gpu, name):
         ref = O.remap_linear_f32(d, m1, m2)
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), \
             f"{np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))} px differ"
-        assert (ref > 0).mean() > 0.5
+        # the "wild" model maps most of the frame outside the source (BORDER_CONSTANT 0)
+        assert (ref > 0).mean() > (0.2 if name == "wild" else 0.5)
     src = torch.from_numpy(np.stack(depths)).cuda()
     pitch = W * H + 16
     dst = torch.full((3, pitch), -1.0, dtype=torch.float32, device="cuda")
