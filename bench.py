@@ -444,8 +444,8 @@ def dropin_leg():
         if len(f) >= 6 and f[0] == "TIMING" and f[2] == "dropin_ms":
             d = {"dropin_ms": float(f[3]), "oracle_ms": float(f[5])}
             d["speedup_vs_cpu_port"] = round(d["oracle_ms"] / d["dropin_ms"], 2) if d["dropin_ms"] > 0 else None
-            if len(f) >= 8:
-                d[f[6]] = int(f[7])
+            for k in range(6, len(f) - 1, 2):  # extra "name value" pairs (counts, time splits)
+                d[f[k]] = int(f[k + 1]) if f[k + 1].isdigit() else float(f[k + 1])
             out[f[1]] = d
     out["path"] = ("compat/dropin headers (ORBextractor.h, SparseImageAlign.h, ORBmatcherGPU.h) under the "
                    "reference's call sites, libygzfe.so underneath; CPU side: the oracle, 1 thread")

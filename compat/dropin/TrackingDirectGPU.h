@@ -14,7 +14,11 @@
 #ifndef YGZFE_TRACKING_DIRECT_GPU_H_
 #define YGZFE_TRACKING_DIRECT_GPU_H_
 
+#include <chrono>
 #include <map>
+#include <memory>
+#include <type_traits>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -33,6 +37,21 @@ inline ygzfe_se3 to_se3(const SE3 &T) {
     o.q[3] = T.unit_quaternion().w();
     for (int k = 0; k < 3; k++) o.t[k] = T.translation()[k];
     return o;
+}
+
+// Where a SearchLocalPointsDirect's time goes (read by tests/dropin/dropin_calls --time):
+// pyramid-pool lookups, and the C-ABI calls (H2D, kernels, D2H); the rest is the
+// reference's host loops (filters, SelectNearestKeyframe, item set-up, results).
+struct DirectStats {
+    double pool_ms = 0, call_ms = 0;
+    long calls = 0;
+};
+inline DirectStats &direct_stats() {
+    static DirectStats s;
+    return s;
+}
+inline double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 // One phase of SearchLocalPointsDirect: the points in the reference's loop order
@@ -55,6 +74,8 @@ public:
         kf_id_.clear();
         refs_.clear();
         slot_.clear();
+        slot_tcr_.clear();
+        slot_pose_.clear();
         ok_ = true;
     }
 
@@ -65,16 +86,17 @@ public:
     void add_point(MapPointT *mp, const std::vector<std::pair<KeyFrameT *, size_t>> &obs_sorted, FrameT &cur) {
         px_proj_.push_back(mp->mTrackProjX);
         px_proj_.push_back(mp->mTrackProjY);
+        const auto pw = mp->GetWorldPos();
         for (auto &o : obs_sorted) {
             KeyFrameT *ref = o.first;
-            const int slot = slot_of(ref);
-            const auto pose_ref = ref->GetPose();
-            const auto pt_ref = pose_ref * mp->GetWorldPos();
-            const auto TCR = cur.mTcw * pose_ref.inverse();
+            // the keyframe's pose and TCR once per phase (a snapshot, as one GetPose() call)
+            const int slot = slot_of(ref, cur);
+            const auto &pose_ref = slot_pose<KeyFrameT>(slot);
+            const auto pt_ref = pose_ref * pw;
             ref_index_.push_back(slot);
             kps_.push_back(*dropin::as_kp(&ref->mvKeys[o.second]));
             for (int k = 0; k < 3; k++) pt_ref_.push_back(pt_ref[k]);
-            T_cr_.push_back(to_se3(TCR));
+            T_cr_.push_back(slot_tcr_[slot]);
             kf_id_.push_back((long)ref->mnId);
         }
         item_ptr_.push_back((int32_t)ref_index_.size());
@@ -91,13 +113,18 @@ public:
         cache_success_ = 0;
         local_ran_ = 1;
         if (!ok_) return fail("a keyframe pyramid could not be placed on the device");
+        auto t0 = std::chrono::steady_clock::now();
         ygzfe_frame *cf = dropin::PyramidPool::instance().find_or_upload(cur.mvImagePyramid);
+        direct_stats().pool_ms += ms_since(t0);
         if (!cf) return fail("the current frame pyramid could not be placed on the device");
         const ygzfe_camera cam{FrameT::fx, FrameT::fy, FrameT::cx, FrameT::cy};
+        t0 = std::chrono::steady_clock::now();
         const int rc = ygzfe_search_local_points_direct(
             refs_.data(), (int)refs_.size(), cf, &cam, n_cache, n - n_cache, item_ptr_.data(), ref_index_.data(),
             kps_.data(), pt_ref_.data(), T_cr_.data(), px_proj_.data(), border, grid_size, cache_hit_th,
             px_out_.data(), matched_.data(), status_.data(), &cache_success_, &local_ran_);
+        direct_stats().call_ms += ms_since(t0);
+        direct_stats().calls++;
         release();  // the call has read the keyframe pyramids
         if (rc != YGZFE_OK) return fail(ygzfe_last_error());
         return true;
@@ -111,12 +138,25 @@ public:
 
 private:
     template <class KeyFrameT>
-    int slot_of(KeyFrameT *ref) {
+    using Pose = typename std::decay<decltype(std::declval<KeyFrameT &>().GetPose())>::type;
+    template <class KeyFrameT>
+    const Pose<KeyFrameT> &slot_pose(int slot) const {
+        return *static_cast<const Pose<KeyFrameT> *>(slot_pose_[slot].get());
+    }
+    template <class KeyFrameT, class FrameT>
+    int slot_of(KeyFrameT *ref, FrameT &cur) {
         auto it = slot_.find((const void *)ref);
         if (it != slot_.end()) return it->second;
+        {
+            auto *pose = new Pose<KeyFrameT>(ref->GetPose());
+            slot_tcr_.push_back(to_se3(cur.mTcw * pose->inverse()));  // TCR (ORBmatcher.cc:1577-1582)
+            slot_pose_.emplace_back(pose, [](const void *q) { delete static_cast<const Pose<KeyFrameT> *>(q); });
+        }
         // every keyframe of the call stays resident until the call: pinned in the pool,
         // which grows past its soft capacity for a large local map instead of failing
+        const auto t0 = std::chrono::steady_clock::now();
         ygzfe_frame *f = dropin::PyramidPool::instance().find_or_upload(ref->mvImagePyramid);
+        direct_stats().pool_ms += ms_since(t0);
         if (!f) {
             if (ok_) dropin::log_once("SearchLocalPointsDirect: keyframe pyramid", dropin::PyramidPool::instance().why().c_str());
             ok_ = false;
@@ -143,7 +183,9 @@ private:
     std::vector<ygzfe_se3> T_cr_;
     std::vector<long> kf_id_;
     std::vector<const ygzfe_frame *> refs_, pinned_;
-    std::map<const void *, int> slot_;
+    std::unordered_map<const void *, int> slot_;
+    std::vector<ygzfe_se3> slot_tcr_;
+    std::vector<std::shared_ptr<const void>> slot_pose_;  // the keyframe poses, type-erased
     int cache_success_ = 0, local_ran_ = 1;
     bool ok_ = true;
 };

@@ -84,8 +84,8 @@ public:
     }
 
     // The device copy of a host pyramid (levels[l]: .data / .cols / .rows / .step).
-    // Lookup by the host level-0 pointer, guarded by a content fingerprint (18 whole
-    // rows and 2,048 bytes spread over level 0, hashed: ~3 us), so a hit costs no full
+    // Lookup by the host level-0 pointer, guarded by a content fingerprint (8 whole
+    // rows and 512 bytes spread over level 0, hashed), so a hit costs no full
     // compare.  A pointer seen for the first time is matched to an entry with the same
     // fingerprint by one full compare of level 0 (once per host pyramid: a Frame clones
     // the extractor's levels, Frame.cc:812; a KeyFrame shares its Frame's, KeyFrame.cc:
@@ -138,11 +138,8 @@ public:
     // rather than fail when every entry is pinned.
     void pin(const ygzfe_frame *f, int delta) {
         std::lock_guard<std::mutex> lk(mu_);
-        for (Entry &e : lru_)
-            if (e.f == f) {
-                e.pins += delta;
-                return;
-            }
+        auto it = by_frame_.find(f);
+        if (it != by_frame_.end()) it->second->pins += delta;
     }
 
     // why the last lookup returned no pyramid
@@ -170,6 +167,7 @@ public:
         for (auto it = lru_.begin(); it != lru_.end();)
             if (it->ex == ex) {
                 unindex(&*it);
+                by_frame_.erase(it->f);
                 ygzfe_frame_destroy(it->f);
                 it = lru_.erase(it);
             } else {
@@ -197,12 +195,12 @@ private:
         h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
         return h * 0xBF58476D1CE4E5B9ull;
     }
-    // 18 whole rows (first, last, 16 spread) + 2,048 bytes on a stride coprime to the width
+    // 8 whole rows (first, last, 6 spread) + 512 bytes on a stride coprime to the width
     static uint64_t fingerprint(const uint8_t *p, int w, int h, size_t stride) {
         uint64_t f = mix((uint64_t)w, (uint64_t)h);
         if (w <= 0 || h <= 0) return f;
-        for (int k = 0; k < 18; k++) {
-            const int y = k == 0 ? 0 : (k == 17 ? h - 1 : (int)((long)k * h / 17));
+        for (int k = 0; k < 8; k++) {
+            const int y = k == 0 ? 0 : (k == 7 ? h - 1 : (int)((long)k * h / 7));
             const uint8_t *r = p + (size_t)y * stride;
             uint64_t acc = 0;
             int x = 0;
@@ -214,9 +212,9 @@ private:
             for (; x < w; x++) acc = mix(acc, r[x]);
             f = mix(f, acc);
         }
-        const size_t n = (size_t)w * h, step = n / 2048 + 1;
+        const size_t n = (size_t)w * h, step = n / 512 + 1;
         size_t i = 7 % n;
-        for (int k = 0; k < 2048; k++, i = (i + step * 2 + 1) % n) f = mix(f, p[(i / w) * stride + i % w]);
+        for (int k = 0; k < 512; k++, i = (i + step * 2 + 1) % n) f = mix(f, p[(i / w) * stride + i % w]);
         return f;
     }
     bool same_level0(const Entry &e, const uint8_t *p, size_t stride) const {
@@ -260,17 +258,24 @@ private:
         by_ptr_[key] = e;
         e->host_ptr = key;
     }
-    // a free (least recently used, unpinned) entry for a w x h pyramid of `ex`, at the front
+    // a free (least recently used, unpinned) entry for a w x h pyramid of `ex`, at the front:
+    // the least recently used one of the same geometry if there is one (its device
+    // pyramid is reused; another geometry's costs a hipFree + hipMalloc), else the LRU
     Entry *slot(ygzfe_extractor *ex, int nlevels, int w, int h) {
         auto victim = lru_.end();
-        if ((int)lru_.size() >= kCapacity)
+        if ((int)lru_.size() >= kCapacity) {
             for (auto it = lru_.end(); it != lru_.begin();) {
                 --it;
-                if (it->pins == 0) {
+                if (it->pins == 0 && it->f && it->ex == ex && it->w == w && it->h == h) {
                     victim = it;
                     break;
                 }
             }
+            for (auto it = lru_.end(); victim == lru_.end() && it != lru_.begin();) {
+                --it;
+                if (it->pins == 0) victim = it;
+            }
+        }
         if (victim != lru_.end()) {
             lru_.splice(lru_.begin(), lru_, victim);
         } else {
@@ -280,9 +285,11 @@ private:
         e.self = lru_.begin();
         unindex(&e);
         if (!e.f || e.ex != ex || e.w != w || e.h != h) {
+            by_frame_.erase(e.f);
             ygzfe_frame_destroy(e.f);
             e.f = nullptr;
             if (ygzfe_frame_create(ex, w, h, &e.f) != YGZFE_OK) e.f = nullptr;
+            if (e.f) by_frame_[e.f] = &e;
         }
         e.ex = ex;
         e.w = w;
@@ -301,6 +308,7 @@ private:
     std::list<Entry> lru_;
     std::unordered_map<const uint8_t *, Entry *> by_ptr_;
     std::unordered_multimap<uint64_t, Entry *> by_fp_;
+    std::unordered_map<const ygzfe_frame *, Entry *> by_frame_;  // pin() lookups
     std::vector<std::pair<ygzfe_extractor *, int>> live_;  // (extractor, nlevels), construction order
 };
 

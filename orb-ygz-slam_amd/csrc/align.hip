@@ -684,6 +684,323 @@ __device__ __forceinline__ float wave_reduce8(float (&v)[8], int lane) {
     return t + YGZ_DPP(t, 0xB1, 0xF);
 }
 
+// ---- pieces of the register kernel: per-pair LDS state, solver-wave steps, and the
+// feature threads' level set-up and residual passes
+
+// the per-pair LDS state: partial sums per wave, the level's H over the visible
+// features, per-wave H of the features out of bounds this iteration, pose, last H
+template <int NW>
+struct AlignPairLds {
+    float part[NW][32];
+    float Hvis[21];
+    float opart[NW][24];
+    SE3 T, old;
+    float chi2, Hpk[21];  // H of the last iteration, upper triangle row-major
+    int stop, brk, nmeas;
+};
+
+template <int NW>
+__device__ __forceinline__ void align_pair_init(AlignPairLds<NW> &P, const AlignJob &job) {
+    for (int i = 0; i < 4; i++) P.T.q[i] = job.T_init.q[i];
+    for (int i = 0; i < 3; i++) P.T.t[i] = job.T_init.t[i];
+    P.chi2 = 1e10f;
+    P.stop = 0;
+    P.nmeas = 0;
+    P.brk = 0;
+    for (int i = 0; i < 21; i++) P.Hpk[i] = 0.f;
+}
+
+template <int NW>
+__device__ __forceinline__ void align_pair_result(const AlignPairLds<NW> &P, ygzfe_align_result *out) {
+    ygzfe_align_result res;
+    for (int i = 0; i < 4; i++) res.T_cur_ref.q[i] = P.T.q[i];
+    for (int i = 0; i < 3; i++) res.T_cur_ref.t[i] = P.T.t[i];
+    res.n_visible = P.nmeas / kPA;
+    res.chi2 = P.chi2;
+    for (int rr = 0, m = 0; rr < 6; rr++)
+        for (int c = rr; c < 6; c++, m++) { res.H[rr * 6 + c] = P.Hpk[m]; res.H[c * 6 + rr] = P.Hpk[m]; }
+    *out = res;
+}
+
+// level start, solver wave: H_vis = the waves' partial sums of the visible features' H
+template <int NW>
+__device__ __forceinline__ void align_sum_hvis(AlignPairLds<NW> &P, int lane) {
+    if (lane < 21) {
+        float r = 0.f;
+        for (int w = 1; w < NW; w++) r += P.part[w][lane];
+        P.Hvis[lane] = r;
+    }
+}
+
+// one Gauss-Newton step, solver wave (NLSSolver_impl.hpp:18-91): reduce the
+// partials, H = H_vis - sum of the out-of-bounds features' H_f, LDLT, rollback or
+// T <- T exp(-x); P.brk set when the level's loop ends
+template <int NW>
+__device__ __forceinline__ void align_solver_step(AlignPairLds<NW> &P, int it, int lane) {
+    // Jres[6], chi2, n_meas over waves 1..NW-1: lane 8g + k adds waves
+    // 2g+1, 2g+2 of value k, then the 8 groups are folded by cross-lane adds
+    float pk8;
+    {
+        const int k8 = lane & 7, w1 = 2 * (lane >> 3) + 1, w2 = w1 + 1;
+        pk8 = (w1 < NW ? P.part[w1][k8] : 0.f) + (w2 < NW ? P.part[w2][k8] : 0.f);
+        pk8 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(pk8), 0x128, 0xF, 0xF, false));
+        pk8 += __shfl_xor(pk8, 16, 64);
+        pk8 += __shfl_xor(pk8, 32, 64);
+    }
+    float r = 0.f;
+    if (lane < 29) {
+        if (lane < 8) {
+            r = pk8;
+        } else {  // per-wave sums of the out-of-bounds features' H_f
+            const int k = lane - 8;
+            float o = 0.f;
+#pragma unroll
+            for (int w = 1; w < NW; w++) o += P.opart[w][k];
+            r = P.Hvis[k] - o;
+            P.Hpk[k] = r;  // H of this iteration (the result's Fisher information)
+        }
+    }
+    YGZ_STAMP(6);
+    float x[6];
+    const int nmeas = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 7));
+    const float new_chi2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 6)) / (float)nmeas;
+    if (lane == 0) P.nmeas = nmeas;
+    YGZ_STAMP(7);
+    ldlt_solve6_nopiv(r, x);
+    YGZ_STAMP(8);
+    const bool stop = P.stop || isnan(x[0]);
+    const bool rollback = (it > 0 && (double)new_chi2 > 1.2 * (double)P.chi2) || stop;
+    if (rollback) {
+        if (lane == 0) {
+            P.stop = stop ? 1 : 0;
+            P.T = P.old;
+            P.brk = 1;
+        }
+    } else {
+        float mx[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) mx[k] = -x[k];
+        SE3 E, Tn;
+        se3_exp_wave(mx, E);
+        const SE3 Tc = P.T;
+        se3_mul_fast(Tc, E, Tn);
+        YGZ_STAMP(10);
+        float nm = -1.f;
+#pragma unroll
+        for (int k = 0; k < 6; k++) nm = fabsf(x[k]) > nm ? fabsf(x[k]) : nm;
+        if (lane == 0) {
+            P.old = Tc;
+            P.T = Tn;
+            P.chi2 = new_chi2;
+            P.brk = nm <= 0.000001f ? 1 : 0;
+        }
+    }
+}
+
+// one reference feature owned by a thread of the feature waves
+struct AlignFeat {
+    float X, Y, Z, kx, ky;
+    bool own, usable, vis;
+    float gx[16], gy[16];
+    float Sxx, Sxy, Syy;  // the level's gradient moments (H_f of an out-of-bounds feature)
+};
+
+__device__ __forceinline__ void align_feat_load(AlignFeat &F, const AlignJob &job, int f) {
+    F.own = f < job.n;
+    F.X = 0.f; F.Y = 0.f; F.Z = 1.f; F.kx = 0.f; F.ky = 0.f;
+    F.usable = false;
+    F.vis = false;
+    if (F.own) {
+        F.X = job.xyz[3 * f]; F.Y = job.xyz[3 * f + 1]; F.Z = job.xyz[3 * f + 2];
+        F.usable = job.usable[f] != 0;
+        F.kx = job.kps[f].x; F.ky = job.kps[f].y;
+    }
+#pragma unroll
+    for (int p = 0; p < 16; p++) { F.gx[p] = 0.f; F.gy[p] = 0.f; }
+    F.Sxx = F.Sxy = F.Syy = 0.f;
+}
+
+// precomputeReferencePatches (SparseImageAlign.cc:57-128) for the thread's feature at
+// `level`: its patch column of s_patch, gradients and moments; the wave's partial
+// sums of the visible features' H into part[wave]
+template <int NF, int NW>
+__device__ __forceinline__ void align_feat_precompute(AlignFeat &F, const AlignLevels &lv, const ygzfe_camera &cam,
+                                                      const uint8_t *ref_pyr, int level, float (*s_patch)[NF], int f,
+                                                      float (*part)[32], int wave, int lane) {
+    const int border = 3;
+    const int W = lv.w[level], H = lv.h[level];
+    const float scale = lv.inv_scale[level];
+    const float fs = cam.fx * scale;
+    const uint8_t *rimg = ref_pyr + lv.off[level];
+    bool here = false;
+    if (F.own && F.usable) {
+        const float u_ref = F.kx * scale, v_ref = F.ky * scale;
+        const int ui = (int)floorf(u_ref), vi = (int)floorf(v_ref);
+        here = !(ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H);
+        if (here) {
+            F.vis = true;  // visible_fts_ is never reset between levels (SparseImageAlign.cc:34,81)
+            const float su = u_ref - ui, sv = v_ref - vi;
+            const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
+            const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
+            // 7x7 window: rows vi-3..vi+3, cols ui-3..ui+3; R[y][x] = ref(vi-3+y, ui-3+x),
+            // kept as packed bytes (all 7 rows in flight at once)
+            const uint8_t *base = rimg + (size_t)(vi - 3) * W + (ui - 3);
+            uint32_t R[7][2];
+#pragma unroll
+            for (int y = 0; y < 7; y++) load_row_packed<7>(base + (size_t)y * W, R[y]);
+            auto rpx = [&](int y, int x) -> float { return (float)((R[y][x >> 2] >> (8 * (x & 3))) & 0xFFu); };
+            // J[y][x]: the bilinear sample at (x + su, y + sv) of the window; the
+            // reference's patch and central differences are entries of J:
+            // patch = J[py+1][px+1], gx = (J[py+1][px+2] - J[py+1][px]) / 2,
+            // gy = (J[py+2][px+1] - J[py][px+1]) / 2 -- the same expressions
+            // as SparseImageAlign.cc:98-125, each evaluated once
+            float J0[6], J1[6], J2[6];
+            auto jrow = [&](int y, float (&o)[6]) {
+#pragma unroll
+                for (int x = 0; x < 6; x++)
+                    o[x] = wtl * rpx(y, x) + wtr * rpx(y, x + 1) + wbl * rpx(y + 1, x) + wbr * rpx(y + 1, x + 1);
+            };
+            jrow(0, J0);
+            jrow(1, J1);
+#pragma unroll
+            for (int py = 0; py < 4; py++) {
+                jrow(py + 2, J2);  // rows py, py+1, py+2 in J0, J1, J2
+#pragma unroll
+                for (int px = 0; px < 4; px++) {
+                    const int pi = py * 4 + px;
+                    s_patch[pi][f] = J1[px + 1];
+                    F.gx[pi] = 0.5f * (J1[px + 2] - J1[px]);
+                    F.gy[pi] = 0.5f * (J2[px + 1] - J0[px + 1]);
+                }
+#pragma unroll
+                for (int x = 0; x < 6; x++) { J0[x] = J1[x]; J1[x] = J2[x]; }
+            }
+        }
+    }
+    if (!here) {  // jacobian_cache_.setZero() per level; the stale ref patch stays
+#pragma unroll
+        for (int p = 0; p < 16; p++) { F.gx[p] = 0.f; F.gy[p] = 0.f; }
+    }
+    F.Sxx = 0.f, F.Sxy = 0.f, F.Syy = 0.f;
+#pragma unroll
+    for (int p = 0; p < 16; p++) { F.Sxx += F.gx[p] * F.gx[p]; F.Sxy += F.gx[p] * F.gy[p]; F.Syy += F.gy[p] * F.gy[p]; }
+    const float fs2 = fs * fs;
+    float fj[12];
+    jacob_xyz2cam_fresh(F.X, F.Y, F.Z, fj);
+    float hv[32];
+    int m = 0;
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int c = r; c < 6; c++) {
+            const float hrc = fj[r] * fj[c] * F.Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * F.Sxy +
+                              fj[6 + r] * fj[6 + c] * F.Syy;
+            hv[m] = (F.own && F.vis) ? hrc * fs2 : 0.f;
+            m++;
+        }
+#pragma unroll
+    for (int k = 21; k < 32; k++) hv[k] = 0.f;
+    const float t = wave_reduce32(hv, lane);
+    if ((lane & 1) == 0 && (lane >> 1) < 21) part[wave][lane >> 1] = t;
+}
+
+// computeResiduals (SparseImageAlign.cc:130-231) for the thread's feature at pose T:
+// the wave's partial Jres / chi2 / count into part[wave], and the per-wave H of the
+// features projected out of bounds (usually none) into opart[wave]
+template <int NF, int NW>
+__device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const SE3 &T, const AlignLevels &lv,
+                                                    const ygzfe_camera &cam, const uint8_t *cur_pyr, int level,
+                                                    const float (*s_patch)[NF], int f, float (*part)[32],
+                                                    float (*opart)[24], int wave, int lane) {
+    const int border = 3;
+    const int W = lv.w[level], H = lv.h[level];
+    const float scale = lv.inv_scale[level];
+    const float fs = cam.fx * scale;
+    const uint8_t *cimg = cur_pyr + lv.off[level];
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc[k] = 0.f;
+    bool out_now = false;
+    if (F.own && F.vis) {
+        // The residual loop runs in fused multiply-adds and projects with
+        // one reciprocal of z: rounding-level differences from the
+        // reference's separate products, inside the 1e-4 pose parity of
+        // SparseImgAlign (the Jacobian and the bilinear weights keep the
+        // reference's values: jacob_xyz2cam_ff, wmulf)
+        const float P3[3] = {F.X, F.Y, F.Z};
+        float pc3[3];
+        se3_act(T, P3, pc3);
+        const float izc = 1.0f / pc3[2];
+        const float u = __builtin_fmaf(cam.fx * pc3[0], izc, cam.cx) * scale;
+        const float v = __builtin_fmaf(cam.fy * pc3[1], izc, cam.cy) * scale;
+        const int ui = (int)floorf(u), vi = (int)floorf(v);
+        if (ui < 0 || vi < 0 || ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H) {
+            out_now = true;
+        } else {
+            const float su = u - ui, sv = v - vi;
+            const float wtl = wmulf(1.f - su, 1.f - sv), wtr = wmulf(su, 1.f - sv);
+            const float wbl = wmulf(1.f - su, sv), wbr = wmulf(su, sv);
+            float Sx = 0.f, Sy = 0.f, chi2 = 0.f;
+            const uint8_t *base = cimg + (size_t)(vi - 2) * W + (ui - 2);
+            float r0[5];
+            load_row<5>(base, r0);
+#pragma unroll
+            for (int py = 0; py < 4; py++) {
+                float r1[5];
+                load_row<5>(base + (size_t)(py + 1) * W, r1);
+#pragma unroll
+                for (int px = 0; px < 4; px++) {
+                    const int pi = py * 4 + px;
+                    const float ic = __builtin_fmaf(
+                        wbr, r1[px + 1], __builtin_fmaf(wbl, r1[px], __builtin_fmaf(wtr, r0[px + 1], wtl * r0[px])));
+                    const float res = ic - s_patch[pi][f];
+                    Sx = __builtin_fmaf(F.gx[pi], res, Sx);
+                    Sy = __builtin_fmaf(F.gy[pi], res, Sy);
+                    chi2 = __builtin_fmaf(res, res, chi2);
+                }
+#pragma unroll
+                for (int c = 0; c < 5; c++) r0[c] = r1[c];
+            }
+            float fj[12];
+            jacob_xyz2cam_ff(F.X, F.Y, F.Z, fj);
+#pragma unroll
+            for (int r = 0; r < 6; r++) acc[r] = -(fj[r] * Sx + fj[6 + r] * Sy) * fs;
+            acc[6] = chi2;
+            acc[7] = 16.f;
+        }
+    }
+    {
+        const float t = wave_reduce8(acc, lane);
+        if ((lane & 7) == 0) part[wave][lane >> 3] = t;
+    }
+    // H_f of the features projected out of bounds, summed per wave (usually none)
+    if (__ballot(out_now)) {
+        float fj[12];
+        jacob_xyz2cam_fresh(F.X, F.Y, F.Z, fj);
+        const float fs2 = fs * fs;
+        float hv[32];
+        int m = 0;
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = r; c < 6; c++) {
+                const float hrc = fj[r] * fj[c] * F.Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * F.Sxy +
+                                  fj[6 + r] * fj[6 + c] * F.Syy;
+                hv[m++] = out_now ? hrc * fs2 : 0.f;
+            }
+#pragma unroll
+        for (int k = 21; k < 32; k++) hv[k] = 0.f;
+        const float t = wave_reduce32(hv, lane);
+        if ((lane & 1) == 0 && (lane >> 1) < 21) opart[wave][lane >> 1] = t;
+    } else if (lane < 21) {
+        opart[wave][lane] = 0.f;
+    }
+}
+
+// One frame pair per workgroup: wave 0 solves, waves 1..NW-1 own one feature per lane.
+// (Two pairs per workgroup, ping-ponging the solver wave, was measured at 0.62 ms per
+// 1023 pairs against 0.39: the second pair's 40 feature registers spill at 1024
+// threads -- profiles/r04_align_pingpong.txt.)
 template <int NT>
 __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_camera cam,
                                                          const AlignJob *__restrict__ jobs,
@@ -695,301 +1012,50 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
         sparse_align_generic<NT>(lv, cam, jobs[blockIdx.x], scratch + blockIdx.x * scratch_per_job, out + blockIdx.x);
         return;
     }
-    __shared__ float s_part[NW][32];
+    __shared__ AlignPairLds<NW> P;
     __shared__ float s_patch[16][NF];  // ref_patch_cache_ of the owned features (column = feature)
-    __shared__ float s_Hvis[21];       // the level's H over its visible features
-    __shared__ float s_opart[NW][24];  // per-wave H of the features projected out of bounds this iteration
-    __shared__ SE3 s_T, s_old;
-    __shared__ float s_chi2, s_Hpk[21];  // H of the last iteration, upper triangle row-major
-    __shared__ int s_stop, s_break, s_nmeas;
     const AlignJob &job = jobs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int border = 3;
-    if (tid == 0) {
-        for (int i = 0; i < 4; i++) s_T.q[i] = job.T_init.q[i];
-        for (int i = 0; i < 3; i++) s_T.t[i] = job.T_init.t[i];
-        s_chi2 = 1e10f;
-        s_stop = 0;
-        s_nmeas = 0;
-        s_break = 0;
-        for (int i = 0; i < 21; i++) s_Hpk[i] = 0.f;
-    }
+    if (tid == 0) align_pair_init(P, job);
     __syncthreads();
     YGZ_STAMP(9);
     if (wave == 0) {
-        // ---------------- solver wave: reduce partials, LDLT, T <- T exp(-x) (NLSSolver_impl.hpp:18-91)
         for (int level = job.max_level; level >= job.min_level; level--) {
-            if (tid == 0) s_old = s_T;
-            __syncthreads();  // L0: level start, s_part = per-wave sums of the features' H
+            if (tid == 0) P.old = P.T;
+            __syncthreads();  // L0: level start, part = per-wave sums of the features' H
             YGZ_STAMP(1);
-            if (lane < 21) {
-                float r = 0.f;
-                for (int w = 1; w < NW; w++) r += s_part[w][lane];
-                s_Hvis[lane] = r;
-            }
-            __syncthreads();  // L0b: s_part free again
+            align_sum_hvis(P, lane);
+            __syncthreads();  // L0b: part free again
             YGZ_STAMP(2);
             for (int it = 0; it < 10; it++) {
                 __syncthreads();  // A: partials written
-            YGZ_STAMP(3);
-                // Jres[6], chi2, n_meas over waves 1..NW-1: lane 8g + k adds waves
-                // 2g+1, 2g+2 of value k, then the 8 groups are folded by cross-lane adds
-                float pk8;
-                {
-                    const int k8 = lane & 7, w1 = 2 * (lane >> 3) + 1, w2 = w1 + 1;
-                    pk8 = (w1 < NW ? s_part[w1][k8] : 0.f) + (w2 < NW ? s_part[w2][k8] : 0.f);
-                    pk8 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(pk8), 0x128, 0xF, 0xF, false));
-                    pk8 += __shfl_xor(pk8, 16, 64);
-                    pk8 += __shfl_xor(pk8, 32, 64);
-                }
-                float r = 0.f;
-                if (lane < 29) {
-                    if (lane < 8) {
-                        r = pk8;
-                    } else {  // H = H_vis - sum of the out-of-bounds features' H_f (per-wave sums)
-                        const int k = lane - 8;
-                        float o = 0.f;
-#pragma unroll
-                        for (int w = 1; w < NW; w++) o += s_opart[w][k];
-                        r = s_Hvis[k] - o;
-                        s_Hpk[k] = r;  // H of this iteration (the result's Fisher information)
-                    }
-                }
-                YGZ_STAMP(6);
-                {
-                    float x[6];
-                    const int nmeas = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 7));
-                    const float new_chi2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 6)) / (float)nmeas;
-                    if (lane == 0) s_nmeas = nmeas;
-                    YGZ_STAMP(7);
-                    ldlt_solve6_nopiv(r, x);
-                    YGZ_STAMP(8);
-                    const bool stop = s_stop || isnan(x[0]);
-                    const bool rollback = (it > 0 && (double)new_chi2 > 1.2 * (double)s_chi2) || stop;
-                    if (rollback) {
-                        if (lane == 0) {
-                            s_stop = stop ? 1 : 0;
-                            s_T = s_old;
-                            s_break = 1;
-                        }
-                    } else {
-                        float mx[6];
-#pragma unroll
-                        for (int k = 0; k < 6; k++) mx[k] = -x[k];
-                        SE3 E, Tn;
-                        se3_exp_wave(mx, E);
-                        const SE3 Tc = s_T;
-                        se3_mul_fast(Tc, E, Tn);
-                        YGZ_STAMP(10);
-                        float nm = -1.f;
-#pragma unroll
-                        for (int k = 0; k < 6; k++) nm = fabsf(x[k]) > nm ? fabsf(x[k]) : nm;
-                        if (lane == 0) {
-                            s_old = Tc;
-                            s_T = Tn;
-                            s_chi2 = new_chi2;
-                            s_break = nm <= 0.000001f ? 1 : 0;
-                        }
-                    }
-                }
+                YGZ_STAMP(3);
+                align_solver_step(P, it, lane);
                 __syncthreads();  // B: pose / decision published
-            YGZ_STAMP(4);
-                if (s_break) break;
+                YGZ_STAMP(4);
+                if (P.brk) break;
             }
             __syncthreads();  // L1: level end
             YGZ_STAMP(5);
         }
-        if (tid == 0) {
-            ygzfe_align_result res;
-            for (int i = 0; i < 4; i++) res.T_cur_ref.q[i] = s_T.q[i];
-            for (int i = 0; i < 3; i++) res.T_cur_ref.t[i] = s_T.t[i];
-            res.n_visible = s_nmeas / kPA;
-            res.chi2 = s_chi2;
-            for (int rr = 0, m = 0; rr < 6; rr++)
-                for (int c = rr; c < 6; c++, m++) { res.H[rr * 6 + c] = s_Hpk[m]; res.H[c * 6 + rr] = s_Hpk[m]; }
-            out[blockIdx.x] = res;
-        }
+        if (tid == 0) align_pair_result(P, out + blockIdx.x);
         return;
     }
-    // ---------------- feature waves: one thread per reference feature
     const int f = tid - 64;
-    const int n = job.n;
-    const bool own = f < n;
-    float X = 0.f, Y = 0.f, Z = 1.f, kx = 0.f, ky = 0.f;
-    bool usable = false, vis = false;
-    if (own) {
-        X = job.xyz[3 * f]; Y = job.xyz[3 * f + 1]; Z = job.xyz[3 * f + 2];
-        usable = job.usable[f] != 0;
-        kx = job.kps[f].x; ky = job.kps[f].y;
-    }
-    float gx[16], gy[16];
+    AlignFeat F;
+    align_feat_load(F, job, f);
 #pragma unroll
-    for (int p = 0; p < 16; p++) { gx[p] = 0.f; gy[p] = 0.f; s_patch[p][f] = 0.f; }
-    float Sxx = 0.f, Sxy = 0.f, Syy = 0.f;  // the level's gradient moments (H_f of an out-of-bounds feature)
+    for (int p = 0; p < 16; p++) s_patch[p][f] = 0.f;
     for (int level = job.max_level; level >= job.min_level; level--) {
-        const int W = lv.w[level], H = lv.h[level];
-        const float scale = lv.inv_scale[level];
-        const float fs = cam.fx * scale;
-        const uint8_t *rimg = job.ref_pyr + lv.off[level];
-        const uint8_t *cimg = job.cur_pyr + lv.off[level];
-        // precomputeReferencePatches (SparseImageAlign.cc:57-128) for the owned feature
-        bool here = false;
-        if (own && usable) {
-            const float u_ref = kx * scale, v_ref = ky * scale;
-            const int ui = (int)floorf(u_ref), vi = (int)floorf(v_ref);
-            here = !(ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H);
-            if (here) {
-                vis = true;  // visible_fts_ is never reset between levels (SparseImageAlign.cc:34,81)
-                const float su = u_ref - ui, sv = v_ref - vi;
-                const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
-                const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
-                // 7x7 window: rows vi-3..vi+3, cols ui-3..ui+3; R[y][x] = ref(vi-3+y, ui-3+x),
-                // kept as packed bytes (all 7 rows in flight at once)
-                const uint8_t *base = rimg + (size_t)(vi - 3) * W + (ui - 3);
-                uint32_t R[7][2];
-#pragma unroll
-                for (int y = 0; y < 7; y++) load_row_packed<7>(base + (size_t)y * W, R[y]);
-                auto rpx = [&](int y, int x) -> float { return (float)((R[y][x >> 2] >> (8 * (x & 3))) & 0xFFu); };
-                // J[y][x]: the bilinear sample at (x + su, y + sv) of the window; the
-                // reference's patch and central differences are entries of J:
-                // patch = J[py+1][px+1], gx = (J[py+1][px+2] - J[py+1][px]) / 2,
-                // gy = (J[py+2][px+1] - J[py][px+1]) / 2 -- the same expressions
-                // as SparseImageAlign.cc:98-125, each evaluated once
-                float J0[6], J1[6], J2[6];
-                auto jrow = [&](int y, float (&o)[6]) {
-#pragma unroll
-                    for (int x = 0; x < 6; x++)
-                        o[x] = wtl * rpx(y, x) + wtr * rpx(y, x + 1) + wbl * rpx(y + 1, x) + wbr * rpx(y + 1, x + 1);
-                };
-                jrow(0, J0);
-                jrow(1, J1);
-#pragma unroll
-                for (int py = 0; py < 4; py++) {
-                    jrow(py + 2, J2);  // rows py, py+1, py+2 in J0, J1, J2
-#pragma unroll
-                    for (int px = 0; px < 4; px++) {
-                        const int pi = py * 4 + px;
-                        s_patch[pi][f] = J1[px + 1];
-                        gx[pi] = 0.5f * (J1[px + 2] - J1[px]);
-                        gy[pi] = 0.5f * (J2[px + 1] - J0[px + 1]);
-                    }
-#pragma unroll
-                    for (int x = 0; x < 6; x++) { J0[x] = J1[x]; J1[x] = J2[x]; }
-                }
-            }
-        }
-        if (!here) {  // jacobian_cache_.setZero() per level; the stale ref patch stays
-#pragma unroll
-            for (int p = 0; p < 16; p++) { gx[p] = 0.f; gy[p] = 0.f; }
-        }
-        {
-            Sxx = 0.f, Sxy = 0.f, Syy = 0.f;
-#pragma unroll
-            for (int p = 0; p < 16; p++) { Sxx += gx[p] * gx[p]; Sxy += gx[p] * gy[p]; Syy += gy[p] * gy[p]; }
-            const float fs2 = fs * fs;
-            float fj[12];
-            jacob_xyz2cam_fresh(X, Y, Z, fj);
-            float hv[32];
-            int m = 0;
-#pragma unroll
-            for (int r = 0; r < 6; r++)
-#pragma unroll
-                for (int c = r; c < 6; c++) {
-                    const float hrc = fj[r] * fj[c] * Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * Sxy +
-                                      fj[6 + r] * fj[6 + c] * Syy;
-                    hv[m] = (own && vis) ? hrc * fs2 : 0.f;
-                    m++;
-                }
-#pragma unroll
-            for (int k = 21; k < 32; k++) hv[k] = 0.f;
-            const float t = wave_reduce32(hv, lane);
-            if ((lane & 1) == 0 && (lane >> 1) < 21) s_part[wave][lane >> 1] = t;
-        }
+        align_feat_precompute<NF, NW>(F, lv, cam, job.ref_pyr, level, s_patch, f, P.part, wave, lane);
         __syncthreads();  // L0
         __syncthreads();  // L0b
         for (int it = 0; it < 10; it++) {
-            float acc[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) acc[k] = 0.f;
-            bool out_now = false;
-            if (own && vis) {
-                // The residual loop runs in fused multiply-adds and projects with
-                // one reciprocal of z: rounding-level differences from the
-                // reference's separate products, inside the 1e-4 pose parity of
-                // SparseImgAlign (the Jacobian and the bilinear weights keep the
-                // reference's values: jacob_xyz2cam_ff, wmulf)
-                const SE3 T = s_T;
-                const float P3[3] = {X, Y, Z};
-                float pc3[3];
-                se3_act(T, P3, pc3);
-                const float izc = 1.0f / pc3[2];
-                const float u = __builtin_fmaf(cam.fx * pc3[0], izc, cam.cx) * scale;
-                const float v = __builtin_fmaf(cam.fy * pc3[1], izc, cam.cy) * scale;
-                const int ui = (int)floorf(u), vi = (int)floorf(v);
-                if (ui < 0 || vi < 0 || ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H) {
-                    out_now = true;
-                } else {
-                    const float su = u - ui, sv = v - vi;
-                    const float wtl = wmulf(1.f - su, 1.f - sv), wtr = wmulf(su, 1.f - sv);
-                    const float wbl = wmulf(1.f - su, sv), wbr = wmulf(su, sv);
-                    float Sx = 0.f, Sy = 0.f, chi2 = 0.f;
-                    const uint8_t *base = cimg + (size_t)(vi - 2) * W + (ui - 2);
-                    float r0[5];
-                    load_row<5>(base, r0);
-#pragma unroll
-                    for (int py = 0; py < 4; py++) {
-                        float r1[5];
-                        load_row<5>(base + (size_t)(py + 1) * W, r1);
-#pragma unroll
-                        for (int px = 0; px < 4; px++) {
-                            const int pi = py * 4 + px;
-                            const float ic = __builtin_fmaf(
-                                wbr, r1[px + 1], __builtin_fmaf(wbl, r1[px], __builtin_fmaf(wtr, r0[px + 1], wtl * r0[px])));
-                            const float res = ic - s_patch[pi][f];
-                            Sx = __builtin_fmaf(gx[pi], res, Sx);
-                            Sy = __builtin_fmaf(gy[pi], res, Sy);
-                            chi2 = __builtin_fmaf(res, res, chi2);
-                        }
-#pragma unroll
-                        for (int c = 0; c < 5; c++) r0[c] = r1[c];
-                    }
-                    float fj[12];
-                    jacob_xyz2cam_ff(X, Y, Z, fj);
-#pragma unroll
-                    for (int r = 0; r < 6; r++) acc[r] = -(fj[r] * Sx + fj[6 + r] * Sy) * fs;
-                    acc[6] = chi2;
-                    acc[7] = 16.f;
-                }
-            }
-            {
-                const float t = wave_reduce8(acc, lane);
-                if ((lane & 7) == 0) s_part[wave][lane >> 3] = t;
-            }
-            // H_f of the features projected out of bounds, summed per wave (usually none)
-            if (__ballot(out_now)) {
-                float fj[12];
-                jacob_xyz2cam_fresh(X, Y, Z, fj);
-                const float fs2 = fs * fs;
-                float hv[32];
-                int m = 0;
-#pragma unroll
-                for (int r = 0; r < 6; r++)
-#pragma unroll
-                    for (int c = r; c < 6; c++) {
-                        const float hrc = fj[r] * fj[c] * Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * Sxy +
-                                          fj[6 + r] * fj[6 + c] * Syy;
-                        hv[m++] = out_now ? hrc * fs2 : 0.f;
-                    }
-#pragma unroll
-                for (int k = 21; k < 32; k++) hv[k] = 0.f;
-                const float t = wave_reduce32(hv, lane);
-                if ((lane & 1) == 0 && (lane >> 1) < 21) s_opart[wave][lane >> 1] = t;
-            } else if (lane < 21) {
-                s_opart[wave][lane] = 0.f;
-            }
+            const SE3 T = P.T;
+            align_feat_residual<NF, NW>(F, T, lv, cam, job.cur_pyr, level, s_patch, f, P.part, P.opart, wave, lane);
             __syncthreads();  // A
             __syncthreads();  // B
-            if (s_break) break;
+            if (P.brk) break;
         }
         __syncthreads();  // L1
     }
@@ -1199,11 +1265,23 @@ hipError_t launch_align2d(const uint8_t *img, int w, int h, int n, const uint8_t
 
 // ------------------------------------------------------------------ FindDirectProjection
 // One (map point, keyframe) item: GetWarpAffineMatrix + GetBestSearchLevel +
-// WarpAffine 10x10 + Align2D at the search level.  px (level-0 px) in/out.
-__device__ int find_direct_one(const uint8_t *__restrict__ ref_pyr, const AlignLevels &rlv,
-                               const uint8_t *__restrict__ cur_pyr, const AlignLevels &clv, int nlevels,
-                               const float *__restrict__ scale, float inv_sigma2_1, const ygzfe_camera &cam,
-                               const ygzfe_kp &kp, const float pt[3], const ygzfe_se3 &Tcr, float px[2], int *level) {
+// WarpAffine 10x10 + Align2D at the search level, by ONE wave: the wave-uniform
+// warp set-up, lanes own the 100 warped pixels (2 per lane) and then pixel
+// `lane` of the 8x8 patch (gradient, bilinear sample, residual, products), and
+// every lane folds the 64 products of an iteration in the reference's pixel order
+// (LDS broadcast reads), so H, Jres and the update are Align.cc:8-105's
+// sequential float sums bit for bit.  px (level-0 px) in/out, wave-uniform.
+struct DirectLds {
+    uint8_t pb[112];    // the warped 10x10 patch with its 1-px border (Align.cc:37-64)
+    float j[2][64];     // reference gradients in pixel order
+    float4 prod[64];    // res * J0, res * J1, res of one iteration, in pixel order
+};
+
+__device__ int find_direct_wave(const uint8_t *__restrict__ ref_pyr, const AlignLevels &rlv,
+                                const uint8_t *__restrict__ cur_pyr, const AlignLevels &clv, int nlevels,
+                                const float *__restrict__ scale, float inv_sigma2_1, const ygzfe_camera &cam,
+                                const ygzfe_kp &kp, const float pt[3], const ygzfe_se3 &Tcr, float px[2], int *level,
+                                int lane, DirectLds &S) {
     SE3 T;
     for (int k = 0; k < 4; k++) T.q[k] = Tcr.q[k];
     for (int k = 0; k < 3; k++) T.t[k] = Tcr.t[k];
@@ -1227,58 +1305,115 @@ __device__ int find_direct_one(const uint8_t *__restrict__ ref_pyr, const AlignL
     float D = A0 * A3 - A2 * A1;
     while (D > 3.0f && sl < nlevels - 1) { sl += 1; D *= inv_sigma2_1; }
     *level = sl;
-    // WarpAffine 10x10 (ORBmatcher.cc:1549-1571)
+    // WarpAffine 10x10 (ORBmatcher.cc:1549-1571): pixels lane and lane + 64
     const uint8_t *rimg = ref_pyr + rlv.off[oc];
     const int rw = rlv.w[oc], rh = rlv.h[oc];
     const float det = A0 * A3 - A2 * A1;
     const float inv = 1.f / det;
     const float R00 = A3 * inv, R01 = -A1 * inv, R10 = -A2 * inv, R11 = A0 * inv;
     const float prx = kp.x / scale[oc], pry = kp.y / scale[oc];
-    uint8_t pb[100], pp[64];
-    for (int y = 0; y < 10; y++)
-        for (int x = 0; x < 10; x++) {
-            const float ppx = (float)(x - 5) * scale[sl], ppy = (float)(y - 5) * scale[sl];
-            const float qx = (R00 * ppx + R01 * ppy) + prx;
-            const float qy = (R10 * ppx + R11 * ppy) + pry;
-            uint8_t val = 0;
-            if (!(qx < 0 || qy < 0 || qx >= rw - 1 || qy >= rh - 1)) {
-                const double X = qx, Y = qy;
-                const double xx = X - floor(X), yy = Y - floor(Y);
-                const uint8_t *d = rimg + (size_t)(int)Y * rw + (int)X;
-                val = (uint8_t)((1 - xx) * (1 - yy) * d[0] + xx * (1 - yy) * d[1] + (1 - xx) * yy * d[rw] +
-                                xx * yy * d[rw + 1]);
-            }
-            pb[y * 10 + x] = val;
+    for (int k = lane; k < 100; k += 64) {
+        const int y = k / 10, x = k - 10 * (k / 10);
+        const float ppx = (float)(x - 5) * scale[sl], ppy = (float)(y - 5) * scale[sl];
+        const float qx = (R00 * ppx + R01 * ppy) + prx;
+        const float qy = (R10 * ppx + R11 * ppy) + pry;
+        uint8_t val = 0;
+        if (!(qx < 0 || qy < 0 || qx >= rw - 1 || qy >= rh - 1)) {
+            const double X = qx, Y = qy;
+            const double xx = X - floor(X), yy = Y - floor(Y);
+            const uint8_t *d = rimg + (size_t)(int)Y * rw + (int)X;
+            val = (uint8_t)((1 - xx) * (1 - yy) * d[0] + xx * (1 - yy) * d[1] + (1 - xx) * yy * d[rw] +
+                            xx * yy * d[rw + 1]);
         }
-    for (int y = 1; y < 9; ++y)
-        for (int x = 0; x < 8; ++x) pp[(y - 1) * 8 + x] = pb[y * 10 + 1 + x];
-    float q[2] = {px[0] * clv.inv_scale[sl], px[1] * clv.inv_scale[sl]};
-    const int ok = align2d_lane(cur_pyr + clv.off[sl], clv.w[sl], clv.w[sl], clv.h[sl], 0, 0, clv.w[sl], clv.h[sl], pb,
-                                pp, 10, q);
-    px[0] = q[0] * scale[sl];
-    px[1] = q[1] * scale[sl];
-    return ok;
+        S.pb[k] = val;
+    }
+    wave_lds_order();
+    // Align2D (Align.cc:8-105) at the search level; pixel (y, x) = lane; the patch
+    // without border is pb[(y + 1) * 10 + 1 + x] (ORBmatcher.cc:1590-1594)
+    const int hp = 4, step = 10, y = lane >> 3, x = lane & 7;
+    const uint8_t *it = S.pb + (y + 1) * step + 1 + x;
+    const float J0 = (float)(0.5 * (it[1] - it[-1]));
+    const float J1 = (float)(0.5 * (it[step] - it[-step]));
+    const float refp = (float)it[0];
+    S.j[0][lane] = J0;
+    S.j[1][lane] = J1;
+    wave_lds_order();
+    float H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 64; i++) {  // H += J J^T in pixel order (Align.cc:58-63)
+        const float J[3] = {S.j[0][i], S.j[1][i], 1.f};
+        for (int r = 0; r < 3; r++)
+            for (int cc = 0; cc < 3; cc++) H[r * 3 + cc] += J[r] * J[cc];
+    }
+    float Hi[9];
+    inverse3(H, Hi);
+    const uint8_t *img = cur_pyr + clv.off[sl];
+    const int w = clv.w[sl], h = clv.h[sl];
+    const float q0 = px[0] * clv.inv_scale[sl], q1 = px[1] * clv.inv_scale[sl];
+    float mean_diff = 0.f, u = q0, v = q1;
+    const float min_upd2 = (float)(0.03 * 0.03);
+    int converged = 0;
+    bool nan_stop = false;
+    for (int iter = 0; iter < 10; ++iter) {
+        const int ur = (int)floorf(u), vr = (int)floorf(v);
+        if (ur < hp || vr < hp || ur >= w - hp || vr >= h - hp) break;
+        if (isnan(u) || isnan(v)) { nan_stop = true; break; }  // Align.cc: returns false, estimate untouched
+        const float sx = u - ur, sy = v - vr;
+        const float wTL = wmul(1.0 - sx, 1.0 - sy), wTR = wmul(sx, 1.0 - sy);
+        const float wBL = wmul(1.0 - sx, sy), wBR = wmul(sx, sy);
+        const uint8_t *q = img + (size_t)(vr + y - hp) * w + (ur - hp) + x;
+        const float spx = wTL * q[0] + wTR * q[1] + wBL * q[w] + wBR * q[w + 1];
+        const float res = spx - refp + mean_diff;
+        S.prod[lane] = make_float4(res * J0, res * J1, res, 0.f);
+        wave_lds_order();
+        float Jr0 = 0.f, Jr1 = 0.f, Jr2 = 0.f;
+        for (int i = 0; i < 64; i++) {
+            const float4 p4 = S.prod[i];
+            Jr0 -= p4.x;
+            Jr1 -= p4.y;
+            Jr2 -= p4.z;
+        }
+        wave_lds_order();
+        const float u0 = Hi[0] * Jr0 + Hi[1] * Jr1 + Hi[2] * Jr2;
+        const float u1 = Hi[3] * Jr0 + Hi[4] * Jr1 + Hi[5] * Jr2;
+        const float u2 = Hi[6] * Jr0 + Hi[7] * Jr1 + Hi[8] * Jr2;
+        u += u0;
+        v += u1;
+        mean_diff += u2;
+        if (u0 * u0 + u1 * u1 < min_upd2) { converged = 1; break; }
+    }
+    if (nan_stop) {
+        u = q0;
+        v = q1;
+        converged = 0;
+    }
+    px[0] = u * scale[sl];
+    px[1] = v * scale[sl];
+    return converged;
 }
 
-__global__ __launch_bounds__(256) void k_find_direct(const uint8_t *const *__restrict__ ref_pyrs, AlignLevels rlv,
-                                                     const uint8_t *__restrict__ cur_pyr, AlignLevels clv,
-                                                     int nlevels, const float *__restrict__ scale,
-                                                     float inv_sigma2_1, ygzfe_camera cam, int n,
-                                                     const int32_t *__restrict__ ref_index,
-                                                     const ygzfe_kp *__restrict__ kps, const float *__restrict__ pts,
-                                                     const ygzfe_se3 *__restrict__ Tcr, float *__restrict__ px_io,
-                                                     int32_t *__restrict__ level_out, uint8_t *__restrict__ ok_out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// one wave per item, four per workgroup
+constexpr int kDirectWaves = 4;
+__global__ __launch_bounds__(64 * kDirectWaves) void k_find_direct(
+    const uint8_t *const *__restrict__ ref_pyrs, AlignLevels rlv, const uint8_t *__restrict__ cur_pyr,
+    AlignLevels clv, int nlevels, const float *__restrict__ scale, float inv_sigma2_1, ygzfe_camera cam, int n,
+    const int32_t *__restrict__ ref_index, const ygzfe_kp *__restrict__ kps, const float *__restrict__ pts,
+    const ygzfe_se3 *__restrict__ Tcr, float *__restrict__ px_io, int32_t *__restrict__ level_out,
+    uint8_t *__restrict__ ok_out) {
+    __shared__ DirectLds s[kDirectWaves];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int i = blockIdx.x * kDirectWaves + wave;
     if (i >= n) return;
     const float pt[3] = {pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
     float px[2] = {px_io[2 * i], px_io[2 * i + 1]};
     int sl;
-    const int ok = find_direct_one(ref_pyrs[ref_index[i]], rlv, cur_pyr, clv, nlevels, scale, inv_sigma2_1, cam,
-                                   kps[i], pt, Tcr[i], px, &sl);
-    level_out[i] = sl;
-    px_io[2 * i] = px[0];
-    px_io[2 * i + 1] = px[1];
-    ok_out[i] = (uint8_t)ok;
+    const int ok = find_direct_wave(ref_pyrs[ref_index[i]], rlv, cur_pyr, clv, nlevels, scale, inv_sigma2_1, cam,
+                                    kps[i], pt, Tcr[i], px, &sl, lane, s[wave]);
+    if (lane == 0) {
+        level_out[i] = sl;
+        px_io[2 * i] = px[0];
+        px_io[2 * i + 1] = px[1];
+        ok_out[i] = (uint8_t)ok;
+    }
 }
 
 hipError_t launch_find_direct(const uint8_t *const *ref_pyrs, const AlignLevels &ref_lv, const uint8_t *cur_pyr,
@@ -1287,8 +1422,9 @@ hipError_t launch_find_direct(const uint8_t *const *ref_pyrs, const AlignLevels 
                               const float *pt_ref, const ygzfe_se3 *T_cr, float *px, int32_t *level, uint8_t *ok,
                               hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_find_direct, dim3((n + 255) / 256), dim3(256), 0, st, ref_pyrs, ref_lv, cur_pyr, cur_lv,
-                       nlevels, scale, inv_sigma2_1, cam, n, ref_index, kp_ref, pt_ref, T_cr, px, level, ok);
+    hipLaunchKernelGGL(k_find_direct, dim3((n + kDirectWaves - 1) / kDirectWaves), dim3(64 * kDirectWaves), 0, st,
+                       ref_pyrs, ref_lv, cur_pyr, cur_lv, nlevels, scale, inv_sigma2_1, cam, n, ref_index, kp_ref,
+                       pt_ref, T_cr, px, level, ok);
     return hipGetLastError();
 }
 
@@ -1301,29 +1437,32 @@ hipError_t launch_find_direct(const uint8_t *const *ref_pyrs, const AlignLevels 
 // inside the 20 px border (Tracking.cc:2287-2296 / 2356-2364): the same answer
 // the reference's sequential loop with its `break` gives.
 
-__global__ __launch_bounds__(256) void k_direct_items(const uint8_t *const *__restrict__ ref_pyrs, AlignLevels lv,
-                                                      const uint8_t *__restrict__ cur_pyr, int nlevels,
-                                                      const float *__restrict__ scale, float inv_sigma2_1,
-                                                      ygzfe_camera cam, int n, const DirectItem *__restrict__ items,
-                                                      const float *__restrict__ px_proj, float *__restrict__ px_out,
-                                                      uint8_t *__restrict__ ok_out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(64 * kDirectWaves) void k_direct_items(
+    const uint8_t *const *__restrict__ ref_pyrs, AlignLevels lv, const uint8_t *__restrict__ cur_pyr, int nlevels,
+    const float *__restrict__ scale, float inv_sigma2_1, ygzfe_camera cam, int n,
+    const DirectItem *__restrict__ items, const float *__restrict__ px_proj, float *__restrict__ px_out,
+    uint8_t *__restrict__ ok_out) {
+    __shared__ DirectLds s[kDirectWaves];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int i = blockIdx.x * kDirectWaves + wave;
     if (i >= n) return;
-    const DirectItem it = items[i];
+    const DirectItem it = scalar_load(items + i);
     float px[2] = {px_proj[2 * it.point], px_proj[2 * it.point + 1]};  // (mTrackProjX, mTrackProjY)
     int sl;
-    const int ok = find_direct_one(ref_pyrs[it.ref], lv, cur_pyr, lv, nlevels, scale, inv_sigma2_1, cam, it.kp,
-                                   it.pt, it.Tcr, px, &sl);
-    px_out[2 * i] = px[0];
-    px_out[2 * i + 1] = px[1];
-    ok_out[i] = (uint8_t)ok;
+    const int ok = find_direct_wave(ref_pyrs[it.ref], lv, cur_pyr, lv, nlevels, scale, inv_sigma2_1, cam, it.kp,
+                                    it.pt, it.Tcr, px, &sl, lane, s[wave]);
+    if (lane == 0) {
+        px_out[2 * i] = px[0];
+        px_out[2 * i + 1] = px[1];
+        ok_out[i] = (uint8_t)ok;
+    }
 }
 
 // Tracking::SearchLocalPointsDirect's sequential part (Tracking.cc:2258-2410) in one
-// workgroup: wave 0 replays the cache points in the reference's order against the
-// 5-px coverage grid (an LDS bitmap), 64 points per step: each lane finds its
-// point's first converged in-border item and the two grid cells in parallel, then
-// the wave walks the 64 lanes in order with uniform control flow (readlane + one
+// workgroup: all 16 waves find every cache point's first converged in-border item
+// and its two grid cells (into LDS, 2,048 points per chunk); wave 0 then replays
+// the points in the reference's order against the 5-px coverage grid (an LDS
+// bitmap), 64 per step: the wave walks the 64 lanes in order with uniform control flow (readlane + one
 // ballot per point resolves "cell already taken by an earlier success of this
 // step"; earlier steps' marks are already in the bitmap).  The success count
 // decides mnCacheHitTh (:2334-2340); then all 16 waves take the local-map points,
@@ -1364,61 +1503,84 @@ __global__ __launch_bounds__(1024) void k_direct_replay(int n_cache, int n_local
                                                         int32_t *__restrict__ hdr) {
     extern __shared__ uint32_t grid[];
     __shared__ int s_cnt;
+    // the cache points' first in-border success and grid cells, found by the whole
+    // workgroup per chunk; wave 0 then replays the chunk in order from LDS
+    constexpr int kChunk = 2048;
+    __shared__ int s_m[kChunk], s_c[kChunk], s_mk[kChunk];
+    __shared__ float s_u[kChunk], s_v[kChunk];
     const int tid = threadIdx.x, lane = tid & 63;
     const int nwords = (ncell + 31) >> 5;
     for (int w = tid; w < nwords; w += blockDim.x) grid[w] = 0u;
-    __syncthreads();
     const float fc = (float)cols, fr = (float)rows;
-    if (tid < 64) {
-        int cnt = 0;
-        for (int base = 0; base < n_cache; base += 64) {
-            const int i = base + lane;
-            const bool valid = i < n_cache;
-            float u = 0.f, v = 0.f;
-            int m = -1, c = -2, mk = -1;
-            bool pre = false;
-            if (valid) {
-                m = direct_first_item(i, item_ptr, px_item, ok_item, border, fc, fr, u, v);
-                c = direct_cell(px_proj[2 * i], px_proj[2 * i + 1], grid_size, grid_cols, ncell);
-                if (m >= 0) {
-                    mk = direct_cell(u, v, grid_size, grid_cols, ncell);
-                    if (mk < 0) mk = -1;  // the reference writes outside its grid; never read back here
-                }
-                pre = c >= 0 && ((grid[c >> 5] >> (c & 31)) & 1u);
+    int cnt = 0;
+    for (int c0 = 0; c0 < n_cache; c0 += kChunk) {
+        const int nc = min(kChunk, n_cache - c0);
+        for (int k = tid; k < nc; k += blockDim.x) {
+            const int i = c0 + k;
+            float u, v;
+            const int m = direct_first_item(i, item_ptr, px_item, ok_item, border, fc, fr, u, v);
+            int mk = -1;
+            if (m >= 0) {
+                mk = direct_cell(u, v, grid_size, grid_cols, ncell);
+                if (mk < 0) mk = -1;  // the reference writes outside its grid; never read back here
             }
-            const int nb = min(64, n_cache - base);
-            bool marked = false;
-            int st = 0;
-            for (int j = 0; j < nb; j++) {
-                const int cj = __builtin_amdgcn_readlane(c, j);
-                const int mj = __builtin_amdgcn_readlane(m, j);
-                const int prej = __builtin_amdgcn_readlane((int)pre, j);
-                const uint64_t hit = __ballot(marked && mk == cj);
-                const bool skip = prej || hit != 0;
-                const int sj = skip ? 2 : (mj >= 0 ? 1 : 0);
-                if (lane == j) {
-                    st = sj;
-                    marked = sj == 1 && mk >= 0;
+            s_m[k] = m;
+            s_u[k] = u;
+            s_v[k] = v;
+            s_c[k] = direct_cell(px_proj[2 * i], px_proj[2 * i + 1], grid_size, grid_cols, ncell);
+            s_mk[k] = mk;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            for (int base = 0; base < nc; base += 64) {
+                const int k = base + lane, i = c0 + k;
+                const bool valid = k < nc;
+                float u = 0.f, v = 0.f;
+                int m = -1, c = -2, mk = -1;
+                bool pre = false;
+                if (valid) {
+                    m = s_m[k];
+                    u = s_u[k];
+                    v = s_v[k];
+                    c = s_c[k];
+                    mk = s_mk[k];
+                    pre = c >= 0 && ((grid[c >> 5] >> (c & 31)) & 1u);
                 }
-                cnt += sj == 1;
-            }
-            if (marked) atomicOr(&grid[mk >> 5], 1u << (mk & 31));
-            wave_lds_order();
-            if (valid) {
-                const bool ok = st == 1;
-                status[i] = st;
-                matched[i] = ok ? m : -1;
-                px_out[2 * i] = ok ? u : 0.f;
-                px_out[2 * i + 1] = ok ? v : 0.f;
+                const int nb = min(64, nc - base);
+                bool marked = false;
+                int st = 0;
+                for (int j = 0; j < nb; j++) {
+                    const int cj = __builtin_amdgcn_readlane(c, j);
+                    const int mj = __builtin_amdgcn_readlane(m, j);
+                    const int prej = __builtin_amdgcn_readlane((int)pre, j);
+                    const uint64_t hit = __ballot(marked && mk == cj);
+                    const bool skip = prej || hit != 0;
+                    const int sj = skip ? 2 : (mj >= 0 ? 1 : 0);
+                    if (lane == j) {
+                        st = sj;
+                        marked = sj == 1 && mk >= 0;
+                    }
+                    cnt += sj == 1;
+                }
+                if (marked) atomicOr(&grid[mk >> 5], 1u << (mk & 31));
+                wave_lds_order();
+                if (valid) {
+                    const bool ok = st == 1;
+                    status[i] = st;
+                    matched[i] = ok ? m : -1;
+                    px_out[2 * i] = ok ? u : 0.f;
+                    px_out[2 * i + 1] = ok ? v : 0.f;
+                }
             }
         }
-        if (lane == 0) s_cnt = cnt;
+        __syncthreads();  // the chunk's LDS arrays are free again
     }
+    if (tid == 0) s_cnt = cnt;
     __syncthreads();
-    const int cnt = s_cnt;
-    const bool local_ran = !(cnt > cache_hit_th);
+    const int n_success = s_cnt;
+    const bool local_ran = !(n_success > cache_hit_th);
     if (tid == 0) {
-        hdr[0] = cnt;
+        hdr[0] = n_success;
         hdr[1] = local_ran ? 1 : 0;
     }
     for (int i = n_cache + tid; i < n_cache + n_local; i += blockDim.x) {
@@ -1439,7 +1601,8 @@ hipError_t launch_search_direct(const uint8_t *const *ref_pyrs, const AlignLevel
                                 hipStream_t st) {
     const int n_points = n_cache + n_local;
     if (n_items > 0)
-        hipLaunchKernelGGL(k_direct_items, dim3((n_items + 255) / 256), dim3(256), 0, st, ref_pyrs, lv, cur_pyr,
+        hipLaunchKernelGGL(k_direct_items, dim3((n_items + kDirectWaves - 1) / kDirectWaves), dim3(64 * kDirectWaves), 0,
+                           st, ref_pyrs, lv, cur_pyr,
                            nlevels, scale, inv_sigma2_1, cam, n_items, (const DirectItem *)items, px_proj, px_item,
                            ok_item);
     const int grid_cols = lv.w[0] / grid_size, ncell = (lv.h[0] / grid_size) * grid_cols;

@@ -327,8 +327,10 @@ static void frame_rows() {
             std::printf("TIMING compute_stereo_matches dropin_ms %.4f oracle_ms %.4f\n", gm, cm);
         }
 
-        // ---------------- ComputeBoW: a k = 10, L = 3 vocabulary bound to the Frame's ORBVocabulary
-        const int k = 10, Lv = 3;
+        // ---------------- ComputeBoW: vocabularies bound to the Frame's ORBVocabulary: k = 10, L = 3,
+        // and ORBvoc.txt's shape k = 10, L = 6 (1,111,111 nodes; the timed one)
+        for (const int Lv : {3, 6}) {
+        const int k = 10;
         std::vector<int32_t> parent(1, -1);
         std::vector<uint8_t> leaf(1, 0);
         int lvl_begin = 0, lvl_end = 1;
@@ -363,9 +365,10 @@ static void frame_rows() {
         const int rc = ygzfe_vocab_create(dropin::device(), k, Lv, 0, 0, nn, parent.data(), leaf.data(), vdesc.data(),
                                           wgt.data(), &gv);
         ygzo_vocab *ov = ygzo_vocab_create(k, Lv, 0, 0, nn, parent.data(), leaf.data(), vdesc.data(), wgt.data());
-        static int voc_token;  // stands for the System's ORBVocabulary object
-        gpu::BindVocabulary(&voc_token, gv);
-        S.mpORBvocabulary = reinterpret_cast<ORBVocabulary *>(&voc_token);
+        static int voc_token[2];  // stand for the System's ORBVocabulary objects
+        gpu::BindVocabulary(&voc_token[Lv == 6], gv);
+        S.mpORBvocabulary = reinterpret_cast<ORBVocabulary *>(&voc_token[Lv == 6]);
+        S.mBowVec.clear();
         S.ComputeBoW();
         std::vector<int32_t> ow(S.N), ofn(S.N), off(S.N);
         std::vector<double> oval(S.N);
@@ -385,8 +388,8 @@ static void frame_rows() {
             }
         b_ok = b_ok && j == onf;
         CHECK(b_ok, "Frame::ComputeBoW(): BowVector %d words, FeatureVector %d entries == oracle (bound vocabulary, "
-              "%d nodes)", (int)S.mBowVec.size(), j, nn);
-        if (g_timing) {
+              "k %d, L %d, %d nodes)", (int)S.mBowVec.size(), j, k, Lv, nn);
+        if (g_timing && Lv == 6) {
             const double gm = median_ms(20, [&] {
                 S.mBowVec.clear();
                 S.ComputeBoW();
@@ -398,6 +401,7 @@ static void frame_rows() {
             std::printf("TIMING compute_bow dropin_ms %.4f oracle_ms %.4f\n", gm, cm);
         }
         ygzo_vocab_destroy(ov);
+        }
     }
 }
 
@@ -946,9 +950,14 @@ int main(int argc, char **argv) {
                     T.TrackLocalMapDirect();
                 };
                 const double g = median_ms(30, run);
+                gpu::direct_stats() = gpu::DirectStats();
+                for (int r = 0; r < 30; r++) run();
+                const gpu::DirectStats ds = gpu::direct_stats();
                 const double c = median_ms(5, [&] { (void)expected(cache0, local, th); });
-                std::printf("TIMING search_local_points_direct dropin_ms %.4f oracle_ms %.4f points %zu\n", g, c,
-                            local.size() + cache0.size());
+                // split (means over 30 runs): C-ABI calls (H2D + kernels + D2H), pyramid-pool lookups
+                std::printf("TIMING search_local_points_direct dropin_ms %.4f oracle_ms %.4f points %zu c_abi_ms %.4f "
+                            "pool_ms %.4f calls_per_run %.1f\n", g, c, local.size() + cache0.size(), ds.call_ms / 30,
+                            ds.pool_ms / 30, ds.calls / 30.0);
             }
         }
         if (NK == 3) {
