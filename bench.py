@@ -266,6 +266,7 @@ def main():
     dom_ms = stage_ms[dom]
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
     traffic = valu_frac = None
+    pmc = {}
     # the newest round's PMC pass (profiles/rNN_traffic.json)
     tcands = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_traffic.json"))
     tpath = os.path.join(ROOT, "profiles", tcands[-1]) if tcands else ""
@@ -275,10 +276,15 @@ def main():
         if per is not None:  # scaled to this launch's frame count
             traffic = int(per["traffic_bytes"] * F)
             valu_frac = per.get("valu_frac")
+            pmc = {k: per[k] for k in ("wait_inst_frac", "wait_any_frac", "lds_conflict_per_inst") if k in per}
+            pmc["source"] = os.path.basename(tpath)
         elif dom in tj.get("per_step", {}):
             traffic = tj["per_step"][dom]["traffic_bytes"]
     roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic, "valu_frac": valu_frac,
+            # what binds the dominant kernel below its HBM roofline: for FAST, VALU issue
+            # and LDS / load latency, not HBM bandwidth (the PMC figures of the same kernel beside it)
+            "binding": BINDING.get(dom, "see DESIGN.md section 4"), "pmc": pmc or None,
             "avg_launch_ms": round(dom_ms, 4), "alg_bytes_per_launch": int(alg[dom]), "frames_per_launch": F_ext,
             "stages_ms": {k: round(v, 4) for k, v in stage_ms.items()},
             "stages_gbps": {k: round(alg[k] / (stage_ms[k] * 1e-3) / 1e9, 1) for k in alg if stage_ms.get(k, 0) > 0}}
@@ -421,6 +427,16 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# the resource that binds each stage below its HBM roofline (measured: DESIGN.md §4)
+BINDING = {
+    "fast9_cells": "VALU issue + LDS/load latency (segment test on survivors, per-cell ROI staging)",
+    "orient_rbrief": "LDS gather latency at 5 waves/SIMD",
+    "sparse_align": "the serial Gauss-Newton chain (one pair per CU)",
+    "blur7": "texture/load path",
+    "octree": "LDS / barrier latency",
+}
 
 
 def dropin_leg():

@@ -20,7 +20,7 @@ import os
 import re
 import sys
 
-STAGES = [("pyramid", r"k_resize_|k_pyramid"), ("blur7", r"k_blur7"), ("fast9_cells", r"k_fast_cells"),
+STAGES = [("pyramid", r"k_resize_|k_pyramid"), ("blur7", r"k_blur7"), ("fast9_cells", r"k_fast_cells|k_fast_screen"),
           ("octree", r"k_octree"), ("orient_rbrief", r"k_orient_desc"), ("hamming_best2", r"k_hamming_best2"),
           ("sparse_align", r"k_sparse_align|k_build_align_jobs")]
 
@@ -40,7 +40,9 @@ def main(pmc_dir, steps, frames=None, bench=None):
     for path in glob.glob(os.path.join(pmc_dir, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
             st = stage_of(r["Kernel_Name"])
-            if st and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"):
+            if st and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_WAVE_CYCLES",
+                                            "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_INSTS_LDS",
+                                            "SQ_LDS_BANK_CONFLICT"):
                 tot[st][r["Counter_Name"]] += float(r["Counter_Value"])
     out = {}
     for st, c in tot.items():
@@ -48,6 +50,11 @@ def main(pmc_dir, steps, frames=None, bench=None):
         write = c["WRITE_SIZE"] * 1024 / steps
         out[st] = {"fetch_bytes": int(fetch), "write_bytes": int(write), "traffic_bytes": int(fetch + write),
                    "valu_insts": int(c["SQ_INSTS_VALU"] / steps)}
+        if c["SQ_WAVE_CYCLES"] > 0:  # the p1 / p2 passes: latency and LDS figures of the stage
+            out[st]["wait_inst_frac"] = round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+            out[st]["wait_any_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+        if c["SQ_INSTS_LDS"] > 0:
+            out[st]["lds_conflict_per_inst"] = round(c["SQ_LDS_BANK_CONFLICT"] / c["SQ_INSTS_LDS"], 3)
     res = {"source": pmc_dir, "steps_per_pass": steps,
            "correction": "FETCH_SIZE x2 (gfx950), KiB -> B", "per_step": out}
     if frames:
@@ -56,6 +63,9 @@ def main(pmc_dir, steps, frames=None, bench=None):
         pf = {}
         for st, v in out.items():
             d = {"traffic_bytes": v["traffic_bytes"] / frames, "valu_insts": v["valu_insts"] / frames}
+            for k in ("wait_inst_frac", "wait_any_frac", "lds_conflict_per_inst"):
+                if k in v:
+                    d[k] = v[k]
             if stage_ms.get(st):
                 d["valu_frac"] = round(d["valu_insts"] * fb / (VALU_ISSUE_PER_S * stage_ms[st] * 1e-3), 4)
             pf[st] = d
