@@ -811,6 +811,7 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
         const void *key[15] = {pyr,          ws.blur.p,  ws.cellbuf.p, ws.sel.p,       ws.candA.p,
                                ws.candB.p,   ex->res.p,  ex->hout.p,   ws.ojobs.p,     ws.cellcnt.p,
                                ws.selcnt.p,  pd.cells.p, pd.plan.p,    pd.tabs.p,      ws.octq.p};
+        static_assert(sizeof(key) == sizeof(f->gkey), "graph key size");
         static const bool no_graph = getenv("YGZFE_NO_GRAPH") != nullptr;
         bool launched = false;
         if (n_existing == 0 && !no_graph && !ex->graph_broken) {

@@ -3,7 +3,7 @@
 # (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950; no trace domains mixed in).
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/pmc_${1:-x}
+OUT=gpurun_out/${1:-x}/pmc
 mkdir -p $OUT
 B="python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --latency-frames 0 --no-direct --no-stereo --no-bow --no-undistort --no-c4 --no-a11"
 R="rocprofv3 --output-format csv"
