@@ -800,33 +800,40 @@ __device__ __forceinline__ void align_solver_step(AlignPairLds<NW> &P, int it, i
 // one reference feature owned by a thread of the feature waves
 struct AlignFeat {
     float X, Y, Z, kx, ky;
-    bool own, usable, vis;
+    bool own, usable;
+};
+// its data at one level: reference gradients, their moments, visibility so far
+struct AlignLevelData {
     float gx[16], gy[16];
     float Sxx, Sxy, Syy;  // the level's gradient moments (H_f of an out-of-bounds feature)
+    bool vis;             // visible_fts_ after this level's set-up (never reset between levels)
 };
 
-__device__ __forceinline__ void align_feat_load(AlignFeat &F, const AlignJob &job, int f) {
+__device__ __forceinline__ void align_feat_load(AlignFeat &F, AlignLevelData &D, const AlignJob &job, int f) {
     F.own = f < job.n;
     F.X = 0.f; F.Y = 0.f; F.Z = 1.f; F.kx = 0.f; F.ky = 0.f;
     F.usable = false;
-    F.vis = false;
     if (F.own) {
         F.X = job.xyz[3 * f]; F.Y = job.xyz[3 * f + 1]; F.Z = job.xyz[3 * f + 2];
         F.usable = job.usable[f] != 0;
         F.kx = job.kps[f].x; F.ky = job.kps[f].y;
     }
 #pragma unroll
-    for (int p = 0; p < 16; p++) { F.gx[p] = 0.f; F.gy[p] = 0.f; }
-    F.Sxx = F.Sxy = F.Syy = 0.f;
+    for (int p = 0; p < 16; p++) { D.gx[p] = 0.f; D.gy[p] = 0.f; }
+    D.Sxx = D.Sxy = D.Syy = 0.f;
+    D.vis = false;
 }
 
 // precomputeReferencePatches (SparseImageAlign.cc:57-128) for the thread's feature at
-// `level`: its patch column of s_patch, gradients and moments; the wave's partial
-// sums of the visible features' H into part[wave]
+// `level` into D and its patch column of s_patch (a feature not inside the level keeps
+// its previous patch: copied from prev_patch when that is another buffer); the wave's
+// partial sums of the visible features' H into part[wave]
 template <int NF, int NW>
-__device__ __forceinline__ void align_feat_precompute(AlignFeat &F, const AlignLevels &lv, const ygzfe_camera &cam,
-                                                      const uint8_t *ref_pyr, int level, float (*s_patch)[NF], int f,
-                                                      float (*part)[32], int wave, int lane) {
+__device__ __forceinline__ void align_feat_precompute(const AlignFeat &F, bool vis_in, AlignLevelData &D,
+                                                      const AlignLevels &lv, const ygzfe_camera &cam,
+                                                      const uint8_t *ref_pyr, int level, float (*s_patch)[NF],
+                                                      const float (*prev_patch)[NF], int f, float (*part)[32],
+                                                      int wave, int lane) {
     const int border = 3;
     const int W = lv.w[level], H = lv.h[level];
     const float scale = lv.inv_scale[level];
@@ -838,7 +845,6 @@ __device__ __forceinline__ void align_feat_precompute(AlignFeat &F, const AlignL
         const int ui = (int)floorf(u_ref), vi = (int)floorf(v_ref);
         here = !(ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H);
         if (here) {
-            F.vis = true;  // visible_fts_ is never reset between levels (SparseImageAlign.cc:34,81)
             const float su = u_ref - ui, sv = v_ref - vi;
             const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
             const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
@@ -869,21 +875,26 @@ __device__ __forceinline__ void align_feat_precompute(AlignFeat &F, const AlignL
                 for (int px = 0; px < 4; px++) {
                     const int pi = py * 4 + px;
                     s_patch[pi][f] = J1[px + 1];
-                    F.gx[pi] = 0.5f * (J1[px + 2] - J1[px]);
-                    F.gy[pi] = 0.5f * (J2[px + 1] - J0[px + 1]);
+                    D.gx[pi] = 0.5f * (J1[px + 2] - J1[px]);
+                    D.gy[pi] = 0.5f * (J2[px + 1] - J0[px + 1]);
                 }
 #pragma unroll
                 for (int x = 0; x < 6; x++) { J0[x] = J1[x]; J1[x] = J2[x]; }
             }
         }
     }
+    D.vis = vis_in || here;  // visible_fts_ is never reset between levels (SparseImageAlign.cc:34,81)
     if (!here) {  // jacobian_cache_.setZero() per level; the stale ref patch stays
 #pragma unroll
-        for (int p = 0; p < 16; p++) { F.gx[p] = 0.f; F.gy[p] = 0.f; }
-    }
-    F.Sxx = 0.f, F.Sxy = 0.f, F.Syy = 0.f;
+        for (int p = 0; p < 16; p++) { D.gx[p] = 0.f; D.gy[p] = 0.f; }
+        if (prev_patch != s_patch) {
 #pragma unroll
-    for (int p = 0; p < 16; p++) { F.Sxx += F.gx[p] * F.gx[p]; F.Sxy += F.gx[p] * F.gy[p]; F.Syy += F.gy[p] * F.gy[p]; }
+            for (int p = 0; p < 16; p++) s_patch[p][f] = prev_patch[p][f];
+        }
+    }
+    D.Sxx = 0.f, D.Sxy = 0.f, D.Syy = 0.f;
+#pragma unroll
+    for (int p = 0; p < 16; p++) { D.Sxx += D.gx[p] * D.gx[p]; D.Sxy += D.gx[p] * D.gy[p]; D.Syy += D.gy[p] * D.gy[p]; }
     const float fs2 = fs * fs;
     float fj[12];
     jacob_xyz2cam_fresh(F.X, F.Y, F.Z, fj);
@@ -893,9 +904,9 @@ __device__ __forceinline__ void align_feat_precompute(AlignFeat &F, const AlignL
     for (int r = 0; r < 6; r++)
 #pragma unroll
         for (int c = r; c < 6; c++) {
-            const float hrc = fj[r] * fj[c] * F.Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * F.Sxy +
-                              fj[6 + r] * fj[6 + c] * F.Syy;
-            hv[m] = (F.own && F.vis) ? hrc * fs2 : 0.f;
+            const float hrc = fj[r] * fj[c] * D.Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * D.Sxy +
+                              fj[6 + r] * fj[6 + c] * D.Syy;
+            hv[m] = (F.own && D.vis) ? hrc * fs2 : 0.f;
             m++;
         }
 #pragma unroll
@@ -908,7 +919,8 @@ __device__ __forceinline__ void align_feat_precompute(AlignFeat &F, const AlignL
 // the wave's partial Jres / chi2 / count into part[wave], and the per-wave H of the
 // features projected out of bounds (usually none) into opart[wave]
 template <int NF, int NW>
-__device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const SE3 &T, const AlignLevels &lv,
+__device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const AlignLevelData &D, const SE3 &T,
+                                                    const AlignLevels &lv,
                                                     const ygzfe_camera &cam, const uint8_t *cur_pyr, int level,
                                                     const float (*s_patch)[NF], int f, float (*part)[32],
                                                     float (*opart)[24], int wave, int lane) {
@@ -921,7 +933,7 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const SE
 #pragma unroll
     for (int k = 0; k < 8; k++) acc[k] = 0.f;
     bool out_now = false;
-    if (F.own && F.vis) {
+    if (F.own && D.vis) {
         // The residual loop runs in fused multiply-adds and projects with
         // one reciprocal of z: rounding-level differences from the
         // reference's separate products, inside the 1e-4 pose parity of
@@ -954,8 +966,8 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const SE
                     const float ic = __builtin_fmaf(
                         wbr, r1[px + 1], __builtin_fmaf(wbl, r1[px], __builtin_fmaf(wtr, r0[px + 1], wtl * r0[px])));
                     const float res = ic - s_patch[pi][f];
-                    Sx = __builtin_fmaf(F.gx[pi], res, Sx);
-                    Sy = __builtin_fmaf(F.gy[pi], res, Sy);
+                    Sx = __builtin_fmaf(D.gx[pi], res, Sx);
+                    Sy = __builtin_fmaf(D.gy[pi], res, Sy);
                     chi2 = __builtin_fmaf(res, res, chi2);
                 }
 #pragma unroll
@@ -984,8 +996,8 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const SE
         for (int r = 0; r < 6; r++)
 #pragma unroll
             for (int c = r; c < 6; c++) {
-                const float hrc = fj[r] * fj[c] * F.Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * F.Sxy +
-                                  fj[6 + r] * fj[6 + c] * F.Syy;
+                const float hrc = fj[r] * fj[c] * D.Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * D.Sxy +
+                                  fj[6 + r] * fj[6 + c] * D.Syy;
                 hv[m++] = out_now ? hrc * fs2 : 0.f;
             }
 #pragma unroll
@@ -998,6 +1010,10 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const SE
 }
 
 // One frame pair per workgroup: wave 0 solves, waves 1..NW-1 own one feature per lane.
+// The next level's reference patches, gradients and H are set up by the feature waves
+// in the first iteration's solver window (between barriers A and B: they depend on the
+// reference frame only), into the other half of a double-buffered patch cache, so only
+// the first level waits for its set-up.
 // (Two pairs per workgroup, ping-ponging the solver wave, was measured at 0.62 ms per
 // 1023 pairs against 0.39: the second pair's 40 feature registers spill at 1024
 // threads -- profiles/r04_align_pingpong.txt.)
@@ -1013,7 +1029,8 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
         return;
     }
     __shared__ AlignPairLds<NW> P;
-    __shared__ float s_patch[16][NF];  // ref_patch_cache_ of the owned features (column = feature)
+    __shared__ float s_part_next[NW][32];  // the next level's H partials
+    __shared__ float s_patch[2][16][NF];   // ref_patch_cache_ of the owned features, this level / the next
     const AlignJob &job = jobs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) align_pair_init(P, job);
@@ -1022,9 +1039,15 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
     if (wave == 0) {
         for (int level = job.max_level; level >= job.min_level; level--) {
             if (tid == 0) P.old = P.T;
-            __syncthreads();  // L0: level start, part = per-wave sums of the features' H
+            __syncthreads();  // L0: level start, the level's H partials are in
             YGZ_STAMP(1);
-            align_sum_hvis(P, lane);
+            if (level == job.max_level) {
+                align_sum_hvis(P, lane);
+            } else if (lane < 21) {
+                float r = 0.f;
+                for (int w = 1; w < NW; w++) r += s_part_next[w][lane];
+                P.Hvis[lane] = r;
+            }
             __syncthreads();  // L0b: part free again
             YGZ_STAMP(2);
             for (int it = 0; it < 10; it++) {
@@ -1043,17 +1066,29 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
     }
     const int f = tid - 64;
     AlignFeat F;
-    align_feat_load(F, job, f);
+    AlignLevelData D, Dn;
+    align_feat_load(F, D, job, f);
 #pragma unroll
-    for (int p = 0; p < 16; p++) s_patch[p][f] = 0.f;
+    for (int p = 0; p < 16; p++) { s_patch[0][p][f] = 0.f; s_patch[1][p][f] = 0.f; }
+    int cb = 0;  // the level's half of the patch cache
     for (int level = job.max_level; level >= job.min_level; level--) {
-        align_feat_precompute<NF, NW>(F, lv, cam, job.ref_pyr, level, s_patch, f, P.part, wave, lane);
+        if (level == job.max_level) {
+            align_feat_precompute<NF, NW>(F, false, D, lv, cam, job.ref_pyr, level, s_patch[cb], s_patch[cb], f,
+                                          P.part, wave, lane);
+        } else {  // set up during the previous level
+            D = Dn;
+            cb ^= 1;
+        }
         __syncthreads();  // L0
         __syncthreads();  // L0b
         for (int it = 0; it < 10; it++) {
             const SE3 T = P.T;
-            align_feat_residual<NF, NW>(F, T, lv, cam, job.cur_pyr, level, s_patch, f, P.part, P.opart, wave, lane);
+            align_feat_residual<NF, NW>(F, D, T, lv, cam, job.cur_pyr, level, s_patch[cb], f, P.part, P.opart, wave,
+                                        lane);
             __syncthreads();  // A
+            if (it == 0 && level > job.min_level)  // the next level, beside the solver's step
+                align_feat_precompute<NF, NW>(F, D.vis, Dn, lv, cam, job.ref_pyr, level - 1, s_patch[cb ^ 1],
+                                              s_patch[cb], f, s_part_next, wave, lane);
             __syncthreads();  // B
             if (P.brk) break;
         }
