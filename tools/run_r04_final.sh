@@ -11,3 +11,6 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --steps 5 --warmup 2 > $O/prof_bench.json 2> $O/prof_bench.err
 python tools/prof_summary.py $(find $O/prof -name '*kernel_stats.csv') > $O/kernel_summary.txt 2>&1 || true
 bash tools/run_pmc.sh ${1:-r04final}
+# diagnostics: SparseImgAlign solver-wave stamps, octree block timeline (diag builds)
+timeout -k 10 200 python tools/mb_align.py --diag --reps 3 > $O/mb_align_diag.txt 2>&1
+STAMPK=3 YGZ_DIAG_LIB=$PWD/orb-ygz-slam_amd/lib/libygzfe_diag3.so timeout -k 10 200 python tools/diag_blocks.py 1024 > $O/diag_oct.txt 2>&1
