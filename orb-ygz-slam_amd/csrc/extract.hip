@@ -1438,8 +1438,22 @@ __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const L
         for (int i = tid; i < size; i += NT) {
             const uint32_t r = nd[i];
             const int st = (int)(r & 0xFFFFu), ln = (int)(r >> 16);
+            // the (score, -index) values are distinct, so the maximum does not depend on
+            // the visiting order: four keys' loads in flight at a time
             uint32_t best = 0u, bkey = 0u;
-            for (int k = st; k < st + ln; k++) {
+            int k = st;
+            for (; k + 4 <= st + ln; k += 4) {
+                uint32_t kv[4], ix[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) key_at(k + u, kv[u], ix[u]);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t v = ((uint32_t)key_score(kv[u]) << 24) | (0xFFFFFFu - ix[u]);
+                    bkey = v > best ? kv[u] : bkey;
+                    best = v > best ? v : best;
+                }
+            }
+            for (; k < st + ln; k++) {
                 uint32_t kv, ix;
                 key_at(k, kv, ix);
                 const uint32_t v = ((uint32_t)key_score(kv) << 24) | (0xFFFFFFu - ix);
