@@ -1342,7 +1342,6 @@ __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const L
                 if (tid + u * NT < nc) ck[rk[u]] = mine[u];
             __syncthreads();
         }
-        if (l == 0 && guard == 0) YGZ_BSTAMP_K(3, 2);
         // children per candidate: 1 + #{k in the run : L_k == depth}, four L bytes per
         // LDS read (exact zero-byte test on L ^ depth)
         if (tid == 0) Sc.s[0] = nc;

@@ -51,12 +51,11 @@ names = ({3: "entry->before loads", 4: "window loads landed (+LDS store)", 5: "I
          {3: "ROI staged", 4: "A: 4-point test", 5: "B: segment test", 6: "C: scores",
           7: "D: NMS (+retry)", 1: "end"} if kern == "2" else
          {3: "gather keys", 4: "codes + radix sort", 7: "(until the list kernel starts)",
-          5: "L, histograms, list", 2: "final round 1: candidates + rank sort",
-          6: "final rounds: the rest", 1: "retain + end"} if kern == "3" else
+          5: "L, histograms, list", 6: "final rounds", 1: "retain + end"} if kern == "3" else
          {3: "entry .. before the passes", 4: "pass 1", 5: "pass 2", 6: "pass 3", 7: "pass 4",
           1: "later passes + retain + end"})
 prev = st[:, 0]
-for k in ((3, 4, 7, 5, 2, 6, 1) if kern == "3" else (3, 4, 5, 6, 7, 1)):
+for k in ((3, 4, 7, 5, 6, 1) if kern == "3" else (3, 4, 5, 6, 7, 1)):
     if k not in names:
         continue
     ok = st[:, k] > 0
