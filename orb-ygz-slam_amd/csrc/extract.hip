@@ -20,10 +20,6 @@
 namespace ygzfe {
 
 __constant__ __attribute__((aligned(16))) int8_t c_pattern[1024];
-// IC_Angle row weights for k_orient_desc, lane s = |row offset| - 1 (lane 15: the
-// centre row): byte b of dword k is column u = 4k + b - 15 of the window row;
-// [s][k] = 1 where |u| <= umax[|v|] (else 0), [s][8 + k] = u + 15 there (else 0)
-__constant__ __attribute__((aligned(16))) uint32_t c_icw[16][16];
 
 #ifdef YGZ_STAMPS
 __device__ unsigned long long g_bstamps[1 << 20];
@@ -1725,6 +1721,10 @@ constexpr uint32_t kMagicBits = 0x4B000000u;  // bits of 2^23 (ulp 1 in [2^23, 2
 // 37 bytes at any 16-B misalignment (o + 37 <= 52).  An odd dword stride puts
 // 32 consecutive rows on 32 different banks (a 64-B stride folds every row onto
 // two bank offsets); rows are 4-B aligned, so they are written as dwords.
+// (A 44-B stride with each row stored from the dword holding the window's first
+// byte fits 6 workgroups per CU: bit-exact, but 0.468 ms / 1024 frames at 5 waves
+// / SIMD and 0.96 with the 6th wave's register spills, against 0.448 --
+// profiles/r04_orient_patch44.txt.)
 constexpr int kPatchStride = 52;
 // slot per keypoint row: 37 rows, padded to 496 dwords (= 16 mod 32) so that the
 // two keypoints of a 32-lane group read complementary bank sets in the IC pass
@@ -1863,9 +1863,6 @@ struct IcWindow {
 // address) & 15 of LDS row r); every tap is an LDS byte read.  Octree
 // keypoints sit >= 19 px inside the level, so the 31x31 IC window and the
 // 37x37 rotated-pattern window never leave it.
-#ifndef YGZ_ORIENT_V2
-#define YGZ_ORIENT_V2 1
-#endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_orient_desc(const uint8_t *__restrict__ pyr,
                                                      const uint8_t *__restrict__ blur, uint32_t pitch,
                                                      const Plan *__restrict__ plan, const uint2 *__restrict__ ojobs,
@@ -1873,28 +1870,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                                                      ygzfe_kp *__restrict__ kps, uint8_t *__restrict__ desc,
                                                      int row_cap) {
     __shared__ uint8_t s_patch[16][kPatchBytes];  // one 37x37 window per keypoint row
-#if YGZ_ORIENT_V2
     // the pattern (c_pattern, 1 KB) staged once per workgroup; the IC row weights are
     // formed in registers from umax, so the workgroup's LDS is 32 KB (5 per CU)
     __shared__ uint4 s_const[64];
-#else
-    // the IC row weights (c_icw, 1 KB) and the pattern (c_pattern, 1 KB), staged
-    // once per workgroup instead of 8 vector loads per lane: the stage is bound by
-    // the vector-memory address path, and 16 rows share them
-    __shared__ uint4 s_const[128];
-#endif
     int bx, f;
     swizzled_block_2d(bx, f);  // one frame's keypoints on one XCD: window lines shared in its L2
     const int lane = threadIdx.x & 63, s = lane & 15;
     const int idx = bx * 16 + (threadIdx.x >> 4);
     uint4 cst = make_uint4(0u, 0u, 0u, 0u);
-#if YGZ_ORIENT_V2
     if (threadIdx.x < 64) cst = reinterpret_cast<const uint4 *>(c_pattern)[threadIdx.x];
-#else
-    if (threadIdx.x < 128)
-        cst = threadIdx.x < 64 ? reinterpret_cast<const uint4 *>(c_icw)[threadIdx.x]
-                               : reinterpret_cast<const uint4 *>(c_pattern)[threadIdx.x - 64];
-#endif
     const int sel_total = plan->sel_total;
     uint2 job = make_uint2(kOrientNone, 0u);
     if (idx < sel_total) job = ojobs[(size_t)f * sel_total + idx];
@@ -1908,7 +1892,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     uint8_t *P = s_patch[threadIdx.x >> 4];
     IcWindow wic;
     Window<18, 37> wdesc;
-#if YGZ_ORIENT_V2
     wic.load(fimg, w, c, s);  // the rBRIEF window follows once the IC window is in LDS
     if (threadIdx.x < 64) s_const[threadIdx.x] = cst;
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
@@ -1916,7 +1899,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     wave_lds_order();
     if (!active) return;  // whole rows leave together
     // IC row weights of lane s's rows (|v| = s + 1; lane 15 the centre row): byte b of
-    // the 32 is 1 / b where |b - 15| <= umax[|v|] (the disc), else 0 -- c_icw's values
+    // the 32 is 1 / b where |b - 15| <= umax[|v|] (the disc), else 0
     uint32_t W0[8], W1[8];
     {
         const int um = plan->umax[s == 15 ? 0 : s + 1];
@@ -1932,32 +1915,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     {
         wic.store(P, s);
         wdesc.load(fblur, w, c, s);  // in flight during the IC sums
-#else
-    wic.load(fimg, w, c, s);  // both windows in flight before the first wait
-    wdesc.load(fblur, w, c, s);
-    // publish the constants: LDS writes retired, then a bare s_barrier (a
-    // __syncthreads would also wait for the window loads in flight)
-    if (threadIdx.x < 128) s_const[threadIdx.x] = cst;
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-    wave_lds_order();
-    if (!active) return;  // whole rows leave together
-    uint4 wq[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) wq[q] = s_const[s * 4 + q];
-    int4 pat[4];  // 16 pairs x (x0, y0, x1, y1) int8
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const uint4 u = s_const[64 + s * 4 + q];
-        pat[q] = make_int4((int)u.x, (int)u.y, (int)u.z, (int)u.w);
-    }
-    const int ne = n_existing ? n_existing[f] : 0;
-    float angle;
-    {
-        wic.store(P, s);
-        const uint32_t W0[8] = {wq[0].x, wq[0].y, wq[0].z, wq[0].w, wq[1].x, wq[1].y, wq[1].z, wq[1].w};
-        const uint32_t W1[8] = {wq[2].x, wq[2].y, wq[2].z, wq[2].w, wq[3].x, wq[3].y, wq[3].z, wq[3].w};
-#endif
         // IC_Angle (ORBextractor.cc:77-101): lane s takes the window rows 15 +- (s+1)
         // (lane 15 the centre row).  Per row, with I the 31 row bytes (32nd
         // weighted 0): S0 = sum of I over the disc (dot4 with the 0/1 weights),
@@ -1991,14 +1948,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         angle = fast_atan2_deg((float)m01, (float)m10);
     }
     // computeOrbDescriptor (ORBextractor.cc:105-149) on the blurred level
-#if YGZ_ORIENT_V2
     int4 pat[4];  // 16 pairs x (x0, y0, x1, y1) int8 (read after the IC pass: fewer live registers there)
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const uint4 u = s_const[s * 4 + q];
         pat[q] = make_int4((int)u.x, (int)u.y, (int)u.z, (int)u.w);
     }
-#endif
     wave_lds_order();  // IC taps read before the window is replaced
     wdesc.store(P, s);
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
@@ -2120,21 +2075,7 @@ hipError_t run_arith_guard(uint32_t host_fails[2]) {
 hipError_t upload_pattern(const int *pat) {
     int8_t p8[1024];
     for (int i = 0; i < 1024; i++) p8[i] = (int8_t)pat[i];
-    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), p8, sizeof(p8));
-    if (e != hipSuccess) return e;
-    int umax[16];
-    ic_umax(umax);
-    uint32_t w[16][16] = {};
-    for (int s = 0; s < 16; s++) {
-        const int um = umax[s == 15 ? 0 : s + 1];
-        for (int b = 0; b < 31; b++) {
-            const int u = b - 15;
-            if (u < -um || u > um) continue;
-            w[s][b >> 2] |= 1u << (8 * (b & 3));
-            w[s][8 + (b >> 2)] |= (uint32_t)b << (8 * (b & 3));
-        }
-    }
-    return hipMemcpyToSymbol(HIP_SYMBOL(c_icw), w, sizeof(w));
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), p8, sizeof(p8));
 }
 
 hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const int *dtabs,
