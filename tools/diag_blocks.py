@@ -55,7 +55,12 @@ names = ({3: "entry->before loads", 4: "window loads landed (+LDS store)", 5: "I
          {3: "entry .. before the passes", 4: "pass 1", 5: "pass 2", 6: "pass 3", 7: "pass 4",
           1: "later passes + retain + end"})
 prev = st[:, 0]
-for k in ((3, 4, 7, 5, 6, 1) if kern == "3" else (3, 4, 5, 6, 7, 1)):
+order = (3, 4, 7, 5, 6, 1) if kern == "3" else (3, 4, 5, 6, 7, 1)
+if os.environ.get("YGZ_DIAG_ORDER"):  # a build whose stamps sit elsewhere: "slot:name,slot:name,..."
+    pairs = [x.split(":", 1) for x in os.environ["YGZ_DIAG_ORDER"].split(",")]
+    order = tuple(int(a) for a, _ in pairs)
+    names = {int(a): b for a, b in pairs}
+for k in order:
     if k not in names:
         continue
     ok = st[:, k] > 0
