@@ -1155,7 +1155,6 @@ __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const L
         a = Lc[k];
         b = Lc[k + 1];
     };
-#pragma unroll
     for (int i = 0; i < nch; i++) {
         const int k = s0 + 64 * i + lane;
         const bool v = k < s1;
@@ -1209,7 +1208,6 @@ __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const L
     __syncthreads();
     {
         int wh = 0;
-#pragma unroll
         for (int i = 0; i < nch; i++) {
             const int sec = chunk_sec(i, s0 + 64 * i + lane);
             const uint64_t hb = __ballot(sec >= 0);
@@ -1257,7 +1255,6 @@ __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const L
     int overflow = bad || nheads > NC;
     if (!overflow) {
         int hr = hbase;
-#pragma unroll
         for (int i = 0; i < nch; i++) {
             const int k = s0 + 64 * i + lane;
             const int sec = chunk_sec(i, k);
@@ -1326,7 +1323,6 @@ __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const L
 #pragma unroll
             for (int u = 0; u < kPer; u++) {
                 if (u * NT + w * 64 >= nc) break;  // wave-uniform: slots past the candidates skip
-#pragma unroll 2
                 for (int j = 0; j < nc; j += 4) {
                     const uint4 v = *reinterpret_cast<const uint4 *>(ck + j);
                     rk[u] += (v.x < mine[u]) + (v.y < mine[u]) + (v.z < mine[u]) + (v.w < mine[u]);
