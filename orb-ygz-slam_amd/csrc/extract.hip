@@ -147,6 +147,11 @@ __device__ __forceinline__ uint32_t pair_at(uint32_t d0, uint32_t d1, uint32_t d
     return __builtin_amdgcn_alignbyte(hi, lo, o & 3u) & 0xFFFFu;
 }
 
+#ifndef YGZ_PYR_BATCH
+#define YGZ_PYR_BATCH 4
+#endif
+constexpr int kPyrBatch = YGZ_PYR_BATCH;
+
 __global__ __launch_bounds__(1024) void k_pyramid_linear_chain(uint8_t *__restrict__ pyr, uint32_t pitch,
                                                                const Plan *__restrict__ plan,
                                                                const int *__restrict__ tabs, int l0) {
@@ -164,45 +169,65 @@ __global__ __launch_bounds__(1024) void k_pyramid_linear_chain(uint8_t *__restri
         const int gw = (D.w + 3) >> 2, ng = gw * D.h;
         const uint8_t *src = fr + S.off;
         uint8_t *dst = fr + D.off;
-#pragma unroll 2  // (4 and 8 measured the same: 0.284-0.285 ms / 256 frames, profiles/r04_c4_pyramid_unroll.txt)
-        for (int g = threadIdx.x; g < ng; g += 1024) {
-            const int y = g / gw, x0 = (g - y * gw) * 4;
-            const int ya = s_yt[3 * y], yb = s_yt[3 * y + 1], bw = s_yt[3 * y + 2];
-            const int b0 = (int)(int16_t)(bw & 0xFFFF), b1 = (int)(int16_t)(bw >> 16);
-            const int sx0 = s_xt[x0].x;
-            const uint32_t base = (uint32_t)sx0 & ~3u;
-            const uint32_t sa = (uint32_t)((size_t)ya * S.w & 3), sb = (uint32_t)((size_t)yb * S.w & 3);
-            const uint32_t *ra = reinterpret_cast<const uint32_t *>(src + (size_t)ya * S.w + base - sa);
-            const uint32_t *rb = reinterpret_cast<const uint32_t *>(src + (size_t)yb * S.w + base - sb);
-            const uint4 wa = make_uint4(ra[0], ra[1], ra[2], ra[3]);
-            const uint4 wb = make_uint4(rb[0], rb[1], rb[2], rb[3]);
-            uint32_t out = 0u;
+        // kPyrBatch groups per thread per step: every source window of the step is loaded
+        // before any of its stores (the compiler cannot hoist loads above stores that may
+        // alias them).  Batches of 1, 4 and 8 measured equal, 0.285-0.288 ms / 256 frames
+        // (profiles/r04_c4_pyramid_batch.txt): the load -> store round trip does not bind.
+        for (int g0 = threadIdx.x; g0 < ng; g0 += 1024 * kPyrBatch) {
+            uint4 wa[kPyrBatch], wb[kPyrBatch];
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int x = x0 + i;
-                const int2 xt = s_xt[x < D.w ? x : x0];
-                const int sx = xt.x;
-                const int a0 = (int)(int16_t)(xt.y & 0xFFFF), a1 = (int)(int16_t)(xt.y >> 16);
-                // byte offsets of sx inside the dword windows of the two rows
-                const uint32_t oa = (uint32_t)(sx - (int)base) + sa, ob = (uint32_t)(sx - (int)base) + sb;
-                const uint32_t pa = oa < 8 ? pair_at(wa.x, wa.y, wa.z, oa) : pair_at(wa.y, wa.z, wa.w, oa - 4);
-                const uint32_t pb = ob < 8 ? pair_at(wb.x, wb.y, wb.z, ob) : pair_at(wb.y, wb.z, wb.w, ob - 4);
-                int r0, r1;
-                if (x < D.xmax) {
-                    r0 = (int)(pa & 0xFF) * a0 + (int)(pa >> 8) * a1;
-                    r1 = (int)(pb & 0xFF) * a0 + (int)(pb >> 8) * a1;
-                } else {
-                    r0 = (int)(pa & 0xFF) * 2048;
-                    r1 = (int)(pb & 0xFF) * 2048;
+            for (int u = 0; u < kPyrBatch; u++) {
+                const int g = g0 + 1024 * u;
+                wa[u] = wb[u] = make_uint4(0u, 0u, 0u, 0u);
+                if (g < ng) {
+                    const int y = g / gw, x0 = (g - y * gw) * 4;
+                    const int ya = s_yt[3 * y], yb = s_yt[3 * y + 1];
+                    const uint32_t base = (uint32_t)s_xt[x0].x & ~3u;
+                    const uint32_t sa = (uint32_t)((size_t)ya * S.w & 3), sb = (uint32_t)((size_t)yb * S.w & 3);
+                    const uint32_t *ra = reinterpret_cast<const uint32_t *>(src + (size_t)ya * S.w + base - sa);
+                    const uint32_t *rb = reinterpret_cast<const uint32_t *>(src + (size_t)yb * S.w + base - sb);
+                    wa[u] = make_uint4(ra[0], ra[1], ra[2], ra[3]);
+                    wb[u] = make_uint4(rb[0], rb[1], rb[2], rb[3]);
                 }
-                const int v = (b0 * r0 + b1 * r1 + (1 << 21)) >> 22;
-                out |= (uint32_t)clampi(v, 0, 255) << (8 * i);
             }
-            uint8_t *o = dst + (size_t)y * D.w + x0;
-            if (x0 + 4 <= D.w && (((uintptr_t)o & 3) == 0)) {
-                *reinterpret_cast<uint32_t *>(o) = out;
-            } else {
-                for (int i = 0; i < 4 && x0 + i < D.w; i++) o[i] = (uint8_t)(out >> (8 * i));
+#pragma unroll
+            for (int u = 0; u < kPyrBatch; u++) {
+                const int g = g0 + 1024 * u;
+                if (g >= ng) break;
+                const int y = g / gw, x0 = (g - y * gw) * 4;
+                const int ya = s_yt[3 * y], yb = s_yt[3 * y + 1], bw = s_yt[3 * y + 2];
+                const int b0 = (int)(int16_t)(bw & 0xFFFF), b1 = (int)(int16_t)(bw >> 16);
+                const int sx0 = s_xt[x0].x;
+                const uint32_t base = (uint32_t)sx0 & ~3u;
+                const uint32_t sa = (uint32_t)((size_t)ya * S.w & 3), sb = (uint32_t)((size_t)yb * S.w & 3);
+                uint32_t out = 0u;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int x = x0 + i;
+                    const int2 xt = s_xt[x < D.w ? x : x0];
+                    const int sx = xt.x;
+                    const int a0 = (int)(int16_t)(xt.y & 0xFFFF), a1 = (int)(int16_t)(xt.y >> 16);
+                    // byte offsets of sx inside the dword windows of the two rows
+                    const uint32_t oa = (uint32_t)(sx - (int)base) + sa, ob = (uint32_t)(sx - (int)base) + sb;
+                    const uint32_t pa = oa < 8 ? pair_at(wa[u].x, wa[u].y, wa[u].z, oa) : pair_at(wa[u].y, wa[u].z, wa[u].w, oa - 4);
+                    const uint32_t pb = ob < 8 ? pair_at(wb[u].x, wb[u].y, wb[u].z, ob) : pair_at(wb[u].y, wb[u].z, wb[u].w, ob - 4);
+                    int r0, r1;
+                    if (x < D.xmax) {
+                        r0 = (int)(pa & 0xFF) * a0 + (int)(pa >> 8) * a1;
+                        r1 = (int)(pb & 0xFF) * a0 + (int)(pb >> 8) * a1;
+                    } else {
+                        r0 = (int)(pa & 0xFF) * 2048;
+                        r1 = (int)(pb & 0xFF) * 2048;
+                    }
+                    const int v = (b0 * r0 + b1 * r1 + (1 << 21)) >> 22;
+                    out |= (uint32_t)clampi(v, 0, 255) << (8 * i);
+                }
+                uint8_t *o = dst + (size_t)y * D.w + x0;
+                if (x0 + 4 <= D.w && (((uintptr_t)o & 3) == 0)) {
+                    *reinterpret_cast<uint32_t *>(o) = out;
+                } else {
+                    for (int i = 0; i < 4 && x0 + i < D.w; i++) o[i] = (uint8_t)(out >> (8 * i));
+                }
             }
         }
         __syncthreads();  // level l complete and the tables free before the next level
