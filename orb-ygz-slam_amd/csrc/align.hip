@@ -1494,14 +1494,20 @@ __global__ __launch_bounds__(64 * kDirectWaves) void k_direct_items(
 }
 
 // Tracking::SearchLocalPointsDirect's sequential part (Tracking.cc:2258-2410) in one
-// workgroup: all 16 waves find every cache point's first converged in-border item
-// and its two grid cells (into LDS, 2,048 points per chunk); wave 0 then replays
-// the points in the reference's order against the 5-px coverage grid (an LDS
-// bitmap), 64 per step: the wave walks the 64 lanes in order with uniform control flow (readlane + one
-// ballot per point resolves "cell already taken by an earlier success of this
-// step"; earlier steps' marks are already in the bitmap).  The success count
-// decides mnCacheHitTh (:2334-2340); then all 16 waves take the local-map points,
-// which have no grid (:2348-2405).
+// workgroup, per chunk of 2,048 cache points:
+//   A  every point's first converged in-border item, its matched cell mk and its
+//      projected cell c (LDS); "pre" = c already marked by an earlier chunk.  A point
+//      that could mark a cell (m >= 0, mk >= 0, not pre) enters a per-chunk LDS hash
+//      cell -> its earliest such point W(cell);
+//   B  a point j is skipped by the reference's loop iff an earlier success marked c_j.
+//      W(c_j) >= j: nothing earlier can, j is final.  W(c_j) = i0 < j with i0 itself
+//      final (nothing earlier can mark c_{i0}): i0 is a success, j skipped, final.
+//      Otherwise j is pending;
+//   C  wave 0 resolves the pending points in order (rare: a chain of points in shared
+//      cells), each by one ballot scan of [i0, j) for a success that marked c_j;
+//   D  statuses out, the chunk's successes marked in the grid bitmap for later chunks.
+// The success count decides mnCacheHitTh (:2334-2340); then all 16 waves take the
+// local-map points, which have no grid (:2348-2405).
 __device__ __forceinline__ int direct_first_item(int i, const int32_t *__restrict__ item_ptr,
                                                  const float *__restrict__ px_item,
                                                  const uint8_t *__restrict__ ok_item, float border, float cols,
@@ -1528,6 +1534,33 @@ __device__ __forceinline__ int direct_cell(float x, float y, int grid_size, int 
     return (k >= 0 && k < ncell) ? (int)k : -2;
 }
 
+constexpr int kReplayHashSlots = 4096;  // >= 2 x the chunk's points: load factor <= 1/2
+
+__device__ __forceinline__ uint32_t replay_hash(int cell) { return ((uint32_t)cell * 2654435761u) >> 20; }
+
+// W(cell) = min(W(cell), k): open addressing, keys claimed by CAS (-1 = free)
+__device__ __forceinline__ void replay_hash_min(int *hk, int *hv, int cell, int k) {
+    uint32_t h = replay_hash(cell);
+    while (true) {
+        const int prev = atomicCAS(&hk[h], -1, cell);
+        if (prev == -1 || prev == cell) {
+            atomicMin(&hv[h], k);
+            return;
+        }
+        h = (h + 1) & (kReplayHashSlots - 1);
+    }
+}
+
+__device__ __forceinline__ int replay_hash_find(const int *hk, const int *hv, int cell) {
+    uint32_t h = replay_hash(cell);
+    while (true) {
+        const int key = hk[h];
+        if (key == cell) return hv[h];
+        if (key == -1) return 0x7fffffff;
+        h = (h + 1) & (kReplayHashSlots - 1);
+    }
+}
+
 __global__ __launch_bounds__(1024) void k_direct_replay(int n_cache, int n_local, const int32_t *__restrict__ item_ptr,
                                                         const float *__restrict__ px_item,
                                                         const uint8_t *__restrict__ ok_item,
@@ -1538,18 +1571,23 @@ __global__ __launch_bounds__(1024) void k_direct_replay(int n_cache, int n_local
                                                         int32_t *__restrict__ hdr) {
     extern __shared__ uint32_t grid[];
     __shared__ int s_cnt;
-    // the cache points' first in-border success and grid cells, found by the whole
-    // workgroup per chunk; wave 0 then replays the chunk in order from LDS
-    constexpr int kChunk = 2048;
-    __shared__ int s_m[kChunk], s_c[kChunk], s_mk[kChunk];
+    constexpr int kChunk = kReplayHashSlots / 2;
+    __shared__ int s_m[kChunk], s_c[kChunk], s_mk[kChunk], s_st[kChunk];
     __shared__ float s_u[kChunk], s_v[kChunk];
+    __shared__ int s_hk[kReplayHashSlots], s_hv[kReplayHashSlots];
     const int tid = threadIdx.x, lane = tid & 63;
     const int nwords = (ncell + 31) >> 5;
     for (int w = tid; w < nwords; w += blockDim.x) grid[w] = 0u;
+    if (tid == 0) s_cnt = 0;
     const float fc = (float)cols, fr = (float)rows;
-    int cnt = 0;
     for (int c0 = 0; c0 < n_cache; c0 += kChunk) {
         const int nc = min(kChunk, n_cache - c0);
+        for (int h = tid; h < kReplayHashSlots; h += blockDim.x) {
+            s_hk[h] = -1;
+            s_hv[h] = 0x7fffffff;
+        }
+        __syncthreads();  // the hash clear; the grid (cleared / the last chunk's marks)
+        // A
         for (int k = tid; k < nc; k += blockDim.x) {
             const int i = c0 + k;
             float u, v;
@@ -1559,58 +1597,67 @@ __global__ __launch_bounds__(1024) void k_direct_replay(int n_cache, int n_local
                 mk = direct_cell(u, v, grid_size, grid_cols, ncell);
                 if (mk < 0) mk = -1;  // the reference writes outside its grid; never read back here
             }
+            const int c = direct_cell(px_proj[2 * i], px_proj[2 * i + 1], grid_size, grid_cols, ncell);
+            const bool pre = c >= 0 && ((grid[c >> 5] >> (c & 31)) & 1u);
             s_m[k] = m;
             s_u[k] = u;
             s_v[k] = v;
-            s_c[k] = direct_cell(px_proj[2 * i], px_proj[2 * i + 1], grid_size, grid_cols, ncell);
+            s_c[k] = c;
             s_mk[k] = mk;
+            s_st[k] = pre ? 2 : -1;
+            if (!pre && m >= 0 && mk >= 0) replay_hash_min(s_hk, s_hv, mk, k);
         }
         __syncthreads();
+        // B
+        for (int k = tid; k < nc; k += blockDim.x) {
+            if (s_st[k] == 2) continue;  // pre-marked: skipped
+            const int c = s_c[k];
+            int st = s_m[k] >= 0 ? 1 : 0;
+            if (c >= 0) {
+                const int i0 = replay_hash_find(s_hk, s_hv, c);
+                if (i0 < k) {  // i0: not pre, m >= 0, final unless an earlier point can mark c_{i0}
+                    const int ci0 = s_c[i0];
+                    st = (ci0 >= 0 && replay_hash_find(s_hk, s_hv, ci0) < i0) ? -1 : 2;
+                }
+            }
+            s_st[k] = st;
+        }
+        __syncthreads();
+        // C
         if (tid < 64) {
             for (int base = 0; base < nc; base += 64) {
-                const int k = base + lane, i = c0 + k;
-                const bool valid = k < nc;
-                float u = 0.f, v = 0.f;
-                int m = -1, c = -2, mk = -1;
-                bool pre = false;
-                if (valid) {
-                    m = s_m[k];
-                    u = s_u[k];
-                    v = s_v[k];
-                    c = s_c[k];
-                    mk = s_mk[k];
-                    pre = c >= 0 && ((grid[c >> 5] >> (c & 31)) & 1u);
-                }
-                const int nb = min(64, nc - base);
-                bool marked = false;
-                int st = 0;
-                for (int j = 0; j < nb; j++) {
-                    const int cj = __builtin_amdgcn_readlane(c, j);
-                    const int mj = __builtin_amdgcn_readlane(m, j);
-                    const int prej = __builtin_amdgcn_readlane((int)pre, j);
-                    const uint64_t hit = __ballot(marked && mk == cj);
-                    const bool skip = prej || hit != 0;
-                    const int sj = skip ? 2 : (mj >= 0 ? 1 : 0);
-                    if (lane == j) {
-                        st = sj;
-                        marked = sj == 1 && mk >= 0;
+                uint64_t pend = __ballot(base + lane < nc && s_st[base + lane] == -1);
+                while (pend) {
+                    const int j = base + (int)__builtin_ctzll(pend);
+                    pend &= pend - 1;
+                    const int cj = s_c[j];
+                    const int i0 = replay_hash_find(s_hk, s_hv, cj);
+                    bool hit = false;
+                    for (int b = i0; b < j && !hit; b += 64) {
+                        const int i = b + lane;
+                        hit = __ballot(i < j && s_mk[i] == cj && s_st[i] == 1) != 0;
                     }
-                    cnt += sj == 1;
-                }
-                if (marked) atomicOr(&grid[mk >> 5], 1u << (mk & 31));
-                wave_lds_order();
-                if (valid) {
-                    const bool ok = st == 1;
-                    status[i] = st;
-                    matched[i] = ok ? m : -1;
-                    px_out[2 * i] = ok ? u : 0.f;
-                    px_out[2 * i + 1] = ok ? v : 0.f;
+                    if (lane == 0) s_st[j] = hit ? 2 : (s_m[j] >= 0 ? 1 : 0);
+                    wave_lds_order();
                 }
             }
         }
+        __syncthreads();
+        // D
+        int mine = 0;
+        for (int k = tid; k < nc; k += blockDim.x) {
+            const int i = c0 + k, st = s_st[k], mk = s_mk[k];
+            const bool ok = st == 1;
+            status[i] = st;
+            matched[i] = ok ? s_m[k] : -1;
+            px_out[2 * i] = ok ? s_u[k] : 0.f;
+            px_out[2 * i + 1] = ok ? s_v[k] : 0.f;
+            if (ok && mk >= 0) atomicOr(&grid[mk >> 5], 1u << (mk & 31));
+            mine += ok;
+        }
+        if (mine) atomicAdd(&s_cnt, mine);
         __syncthreads();  // the chunk's LDS arrays are free again
     }
-    if (tid == 0) s_cnt = cnt;
     __syncthreads();
     const int n_success = s_cnt;
     const bool local_ran = !(n_success > cache_hit_th);

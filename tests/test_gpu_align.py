@@ -248,3 +248,53 @@ def test_search_local_points_direct_grid_bitexact(gpu, seed):
     px, m = gpu.search_direct_batch(kf_fr, cur_fr, cam, *args)
     opx, om, ost, _, _ = O.search_local_points_direct(orc, kl, cl, O.Cam(*d["scene"].cam), 0, *args)
     assert np.array_equal(m, om) and np.array_equal(px, opx)
+
+
+def test_search_local_points_direct_dense_chunks(gpu):
+    """SearchLocalPointsDirect with > 2,048 cache points (two replay chunks: the grid marks
+    of the first reach the second) and 5-point clusters, so that some points' earliest
+    possible marker of their cell is itself undecided until the ordered pass over the
+    chunk (checked below from the local-only form's matches).  Statuses, matches, pixels
+    and counts bit-exact with the oracle's sequential loop (Tracking.cc:2258-2410)."""
+    d = S.direct_scene(4, n_kf=3, max_obs=3, cluster=4)
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    ex = gpu.ORBextractor(nf, sf, nl, ini, mn)
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    kf_fr = [ex.ComputePyramid(im) for im in d["kf_images"]]
+    cur_fr = ex.ComputePyramid(d["cur_image"])
+    kl = [orc.pyramid(im) for im in d["kf_images"]]
+    cl = orc.pyramid(d["cur_image"])
+    cam = d["scene"].camera()
+    args = (d["item_ptr"], d["ref_index"], d["kps"], d["pt_ref"], d["T_cr"], d["px_proj"])
+    n = len(d["item_ptr"]) - 1
+    n_cache = (3 * n) // 5
+    assert n_cache > 2048
+    # every point's first in-border match (no grid) -> its matched cell; the first chunk's
+    # earliest possible marker per cell and the points that wait on an undecided one
+    px_all, m_all = gpu.search_direct_batch(kf_fr, cur_fr, cam, *args)
+    gs, gcols = 5, W // 5
+    ncell = (H // 5) * gcols
+
+    def cell(p):
+        k = int(np.float32(p[1]) / np.float32(gs)) * gcols + int(np.float32(p[0]) / np.float32(gs))
+        return k if 0 <= k < ncell else -2
+
+    c = [cell(d["px_proj"][i]) for i in range(2048)]
+    first = {}
+    for k in range(2048):
+        if m_all[k] >= 0:
+            mk = cell(px_all[k])
+            if mk >= 0:
+                first.setdefault(mk, k)
+    waits = [k for k in range(2048) if c[k] >= 0 and first.get(c[k], 1 << 30) < k
+             and c[first[c[k]]] >= 0 and first.get(c[first[c[k]]], 1 << 30) < first[c[k]]]
+    assert len(waits) >= 5, len(waits)
+    for th in (10 ** 6, 150):
+        px, m, st, cs, ran = gpu.search_local_points_direct(kf_fr, cur_fr, cam, n_cache, *args, cache_hit_th=th)
+        opx, om, ost, ocs, oran = O.search_local_points_direct(orc, kl, cl, O.Cam(*d["scene"].cam), n_cache, *args,
+                                                               cache_hit_th=th)
+        assert np.array_equal(st, ost), th
+        assert np.array_equal(m, om) and np.array_equal(px, opx), th
+        assert (cs, ran) == (ocs, oran), th
+        assert (st[:n_cache] == gpu.DIRECT_GRID_SKIP).mean() >= 0.2
+        assert (st[2048:n_cache] == gpu.DIRECT_GRID_SKIP).any()
