@@ -1306,10 +1306,8 @@ hipError_t launch_align2d(const uint8_t *img, int w, int h, int n, const uint8_t
 // every lane folds the 64 products of an iteration in the reference's pixel order
 // (LDS broadcast reads), so H, Jres and the update are Align.cc:8-105's
 // sequential float sums bit for bit.  px (level-0 px) in/out, wave-uniform.
-constexpr int kDirectWin = 20;  // Align2D's search-level window staged in LDS: 20 x 20 bytes
 struct DirectLds {
     uint8_t pb[112];    // the warped 10x10 patch with its 1-px border (Align.cc:37-64)
-    uint8_t win[kDirectWin * kDirectWin];  // the current level around the start estimate
     float j[2][64];     // reference gradients in pixel order
     float4 prod[64];    // res * J0, res * J1, res of one iteration, in pixel order
 };
@@ -1342,33 +1340,6 @@ __device__ int find_direct_wave(const uint8_t *__restrict__ ref_pyr, const Align
     float D = A0 * A3 - A2 * A1;
     while (D > 3.0f && sl < nlevels - 1) { sl += 1; D *= inv_sigma2_1; }
     *level = sl;
-    // the search level's 20 x 20 bytes around the start estimate (the patch's 8 x 8 + 1
-    // bilinear column / row for ur, vr within [-6, +5] of the start) in flight during the
-    // warp and H; bytes outside the level read 0 and are never sampled (the iteration's
-    // bound check keeps the sampled 9 x 9 inside the image)
-    const uint8_t *img = cur_pyr + clv.off[sl];
-    const int w = clv.w[sl], h = clv.h[sl];
-    const float q0 = px[0] * clv.inv_scale[sl], q1 = px[1] * clv.inv_scale[sl];
-    const bool q_finite = q0 == q0 && q1 == q1 && fabsf(q0) < 1e6f && fabsf(q1) < 1e6f;
-    const int wx0 = q_finite ? (int)floorf(q0) - 10 : 0, wy0 = q_finite ? (int)floorf(q1) - 10 : 0;
-    {
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void *)img, 0, (int)((uint32_t)w * (uint32_t)h), 0x00020000);
-        uint8_t wv[7];
-#pragma unroll
-        for (int k = 0; k < 7; k++) {
-            const int t = lane + 64 * k, r = t / kDirectWin, cc = t - kDirectWin * r;
-            const int gy = wy0 + r, gx = wx0 + cc;
-            // outside the level: an offset past num_records (the load returns 0)
-            const uint32_t off = (gy >= 0 && gy < h && gx >= 0 && gx < w) ? (uint32_t)(gy * w + gx) : 0xFFFFFFF0u;
-            wv[k] = t < kDirectWin * kDirectWin ? __builtin_amdgcn_raw_buffer_load_b8(rs, off, 0, 0) : (uint8_t)0;
-        }
-#pragma unroll
-        for (int k = 0; k < 7; k++) {
-            const int t = lane + 64 * k;
-            if (t < kDirectWin * kDirectWin) S.win[t] = wv[k];
-        }
-    }
     // WarpAffine 10x10 (ORBmatcher.cc:1549-1571): pixels lane and lane + 64
     const uint8_t *rimg = ref_pyr + rlv.off[oc];
     const int rw = rlv.w[oc], rh = rlv.h[oc];
@@ -1410,6 +1381,9 @@ __device__ int find_direct_wave(const uint8_t *__restrict__ ref_pyr, const Align
     }
     float Hi[9];
     inverse3(H, Hi);
+    const uint8_t *img = cur_pyr + clv.off[sl];
+    const int w = clv.w[sl], h = clv.h[sl];
+    const float q0 = px[0] * clv.inv_scale[sl], q1 = px[1] * clv.inv_scale[sl];
     float mean_diff = 0.f, u = q0, v = q1;
     const float min_upd2 = (float)(0.03 * 0.03);
     int converged = 0;
@@ -1421,18 +1395,8 @@ __device__ int find_direct_wave(const uint8_t *__restrict__ ref_pyr, const Align
         const float sx = u - ur, sy = v - vr;
         const float wTL = wmul(1.0 - sx, 1.0 - sy), wTR = wmul(sx, 1.0 - sy);
         const float wBL = wmul(1.0 - sx, sy), wBR = wmul(sx, sy);
-        // the same bytes from the LDS window while the 9 x 9 stays inside it (wave-uniform)
-        const int lx = ur - hp - wx0, ly = vr - hp - wy0;
-        const bool in_win = lx >= 0 && ly >= 0 && lx + 8 < kDirectWin && ly + 8 < kDirectWin;
-        uint32_t b00, b01, b10, b11;
-        if (in_win) {
-            const uint8_t *q = S.win + (ly + y) * kDirectWin + lx + x;
-            b00 = q[0], b01 = q[1], b10 = q[kDirectWin], b11 = q[kDirectWin + 1];
-        } else {
-            const uint8_t *q = img + (size_t)(vr + y - hp) * w + (ur - hp) + x;
-            b00 = q[0], b01 = q[1], b10 = q[w], b11 = q[w + 1];
-        }
-        const float spx = wTL * b00 + wTR * b01 + wBL * b10 + wBR * b11;
+        const uint8_t *q = img + (size_t)(vr + y - hp) * w + (ur - hp) + x;
+        const float spx = wTL * q[0] + wTR * q[1] + wBL * q[w] + wBR * q[w + 1];
         const float res = spx - refp + mean_diff;
         S.prod[lane] = make_float4(res * J0, res * J1, res, 0.f);
         wave_lds_order();
