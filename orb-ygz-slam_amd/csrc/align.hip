@@ -1475,17 +1475,18 @@ hipError_t launch_find_direct(const uint8_t *const *ref_pyrs, const AlignLevels 
 __global__ __launch_bounds__(64 * kDirectWaves) void k_direct_items(
     const uint8_t *const *__restrict__ ref_pyrs, AlignLevels lv, const uint8_t *__restrict__ cur_pyr, int nlevels,
     const float *__restrict__ scale, float inv_sigma2_1, ygzfe_camera cam, int n,
-    const DirectItem *__restrict__ items, const float *__restrict__ px_proj, float *__restrict__ px_out,
-    uint8_t *__restrict__ ok_out) {
+    const DirectItem *__restrict__ items, const ygzfe_se3 *__restrict__ tcr_tab, const float *__restrict__ px_proj,
+    float *__restrict__ px_out, uint8_t *__restrict__ ok_out) {
     __shared__ DirectLds s[kDirectWaves];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int i = blockIdx.x * kDirectWaves + wave;
     if (i >= n) return;
     const DirectItem it = scalar_load(items + i);
+    const ygzfe_se3 Tcr = scalar_load(tcr_tab + it.tcr);
     float px[2] = {px_proj[2 * it.point], px_proj[2 * it.point + 1]};  // (mTrackProjX, mTrackProjY)
     int sl;
     const int ok = find_direct_wave(ref_pyrs[it.ref], lv, cur_pyr, lv, nlevels, scale, inv_sigma2_1, cam, it.kp,
-                                    it.pt, it.Tcr, px, &sl, lane, s[wave]);
+                                    it.pt, Tcr, px, &sl, lane, s[wave]);
     if (lane == 0) {
         px_out[2 * i] = px[0];
         px_out[2 * i + 1] = px[1];
@@ -1678,14 +1679,14 @@ __global__ __launch_bounds__(1024) void k_direct_replay(int n_cache, int n_local
 hipError_t launch_search_direct(const uint8_t *const *ref_pyrs, const AlignLevels &lv, const uint8_t *cur_pyr,
                                 int nlevels, const float *scale, float inv_sigma2_1, const ygzfe_camera &cam,
                                 int n_cache, int n_local, int n_items, const int32_t *item_ptr, const void *items,
-                                const float *px_proj, float *px_item, uint8_t *ok_item, float border, int grid_size,
+                                const ygzfe_se3 *tcr_tab, const float *px_proj, float *px_item, uint8_t *ok_item, float border, int grid_size,
                                 int cache_hit_th, float *px_out, int32_t *matched, int32_t *status, int32_t *hdr,
                                 hipStream_t st) {
     const int n_points = n_cache + n_local;
     if (n_items > 0)
         hipLaunchKernelGGL(k_direct_items, dim3((n_items + kDirectWaves - 1) / kDirectWaves), dim3(64 * kDirectWaves), 0,
                            st, ref_pyrs, lv, cur_pyr,
-                           nlevels, scale, inv_sigma2_1, cam, n_items, (const DirectItem *)items, px_proj, px_item,
+                           nlevels, scale, inv_sigma2_1, cam, n_items, (const DirectItem *)items, tcr_tab, px_proj, px_item,
                            ok_item);
     const int grid_cols = lv.w[0] / grid_size, ncell = (lv.h[0] / grid_size) * grid_cols;
     const size_t lds = (size_t)((ncell + 31) / 32) * 4 + 4;

@@ -1761,11 +1761,29 @@ static int search_direct_impl(const ygzfe_frame *const *ref, int n_ref, const yg
     YGZ_TRY(ensure_device(ex->device));
     std::lock_guard<std::mutex> lk(ex->mu);
     hipStream_t st = ex->stream;
-    // in: [ref ptrs][scale][item_ptr][px_proj][items]   out: [hdr][px_out][matched][status] | [px_item][ok_item]
+    // in: [ref ptrs][scale][item_ptr][px_proj][items][T table]   out: [hdr][px_out][matched][status] | [px_item][ok_item]
+    // T table: one T_cr per keyframe slot while its items agree (Tracking's TCR is per
+    // keyframe), else one per differing item
+    std::vector<int32_t> slot_tcr((size_t)std::max(1, n_ref), -1);
+    std::vector<ygzfe_se3> tab;
+    tab.reserve(std::max(1, n_ref));
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_ptr = 0, o_sc = al(o_ptr + sizeof(void *) * std::max(1, n_ref));
     const size_t o_ip = al(o_sc + 4 * kMaxLevels), o_pp = al(o_ip + 4 * ((size_t)n_points + 1));
-    const size_t o_it = al(o_pp + 8 * (size_t)n_points), in_bytes = al(o_it + sizeof(DirectItem) * (size_t)n_items);
+    const size_t o_it = al(o_pp + 8 * (size_t)n_points), o_tab = al(o_it + sizeof(DirectItem) * (size_t)n_items);
+    std::vector<int32_t> tcr_of((size_t)n_items);
+    for (int k = 0; k < n_items; k++) {
+        int &e = slot_tcr[ref_index[k]];
+        if (e < 0 || memcmp(&tab[e], &T_cr[k], sizeof(ygzfe_se3)) != 0) {
+            const int t = (int)tab.size();
+            tab.push_back(T_cr[k]);
+            if (e < 0) e = t;
+            tcr_of[k] = t;
+        } else {
+            tcr_of[k] = e;
+        }
+    }
+    const size_t in_bytes = al(o_tab + sizeof(ygzfe_se3) * std::max<size_t>(1, tab.size()));
     const size_t o_hdr = 0, o_pxo = 16, o_m = o_pxo + 8 * (size_t)n_points, o_st = o_m + 4 * (size_t)n_points;
     const size_t back_bytes = o_st + 4 * (size_t)n_points;
     const size_t o_pxi = al(back_bytes), o_ok = al(o_pxi + 8 * (size_t)n_items), out_bytes = al(o_ok + (size_t)n_items);
@@ -1783,18 +1801,18 @@ static int search_direct_impl(const ygzfe_frame *const *ref, int n_ref, const yg
         for (int k = item_ptr[i]; k < item_ptr[i + 1]; k++) {
             it[k].kp = kp_ref[k];
             memcpy(it[k].pt, pt_ref + 3 * (size_t)k, 12);
-            it[k].Tcr = T_cr[k];
             it[k].ref = ref_index[k];
             it[k].point = i;
-            it[k].pad = 0;
+            it[k].tcr = tcr_of[k];
         }
+    if (!tab.empty()) memcpy(h + o_tab, tab.data(), sizeof(ygzfe_se3) * tab.size());
     YGZ_TRY(ex->direct_dev.ensure(in_bytes + out_bytes));
     uint8_t *d = ex->direct_dev.as<uint8_t>(), *dout = d + in_bytes;
     YGZ_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st));
     YGZ_HIP(launch_search_direct((const uint8_t *const *)(d + o_ptr), levels_of(P), cur->pyr.as<uint8_t>(),
                                  P.nlevels, (const float *)(d + o_sc), ex->scales.inv_sigma2[1 < P.nlevels ? 1 : 0],
                                  *cam, n_cache, n_local, n_items, (const int32_t *)(d + o_ip), d + o_it,
-                                 (const float *)(d + o_pp), (float *)(dout + o_pxi), dout + o_ok, border, grid_size,
+                                 (const ygzfe_se3 *)(d + o_tab), (const float *)(d + o_pp), (float *)(dout + o_pxi), dout + o_ok, border, grid_size,
                                  cache_hit_th, (float *)(dout + o_pxo), (int32_t *)(dout + o_m),
                                  (int32_t *)(dout + o_st), (int32_t *)(dout + o_hdr), st));
     uint8_t *hb = ex->direct_hout.as<uint8_t>();

@@ -170,19 +170,19 @@ hipError_t launch_bow_vectors(const int *counts, int n_static, int n_frames, con
 struct DirectItem {
     ygzfe_kp kp;        // ref->mvKeys[index] (28 B)
     float pt[3];        // T_ref * P_w
-    ygzfe_se3 Tcr;      // T_cur * T_ref^-1
     int32_t ref;        // keyframe slot
     int32_t point;      // owning map point
-    int32_t pad;
+    int32_t tcr;        // T_cur * T_ref^-1 in the call's T table (one entry per keyframe when
+                        // the items of a keyframe agree, as Tracking's do)
 };
-static_assert(sizeof(DirectItem) == 80, "DirectItem layout");
+static_assert(sizeof(DirectItem) == 52, "DirectItem layout");
 // n_cache cache points (5-px coverage grid of grid_size, replayed in order) then
 // n_local local-map points (run only if the cache successes <= cache_hit_th);
 // hdr[0] = cache successes, hdr[1] = local phase ran
 hipError_t launch_search_direct(const uint8_t *const *ref_pyrs, const AlignLevels &lv, const uint8_t *cur_pyr,
                                 int nlevels, const float *scale, float inv_sigma2_1, const ygzfe_camera &cam,
                                 int n_cache, int n_local, int n_items, const int32_t *item_ptr, const void *items,
-                                const float *px_proj, float *px_item, uint8_t *ok_item, float border, int grid_size,
+                                const ygzfe_se3 *tcr_tab, const float *px_proj, float *px_item, uint8_t *ok_item, float border, int grid_size,
                                 int cache_hit_th, float *px_out, int32_t *matched, int32_t *status, int32_t *hdr,
                                 hipStream_t st);
 constexpr int kDirectMaxGridCells = 65536 * 8 - 64;  // LDS bitmap of k_direct_replay (<= 64 KB)

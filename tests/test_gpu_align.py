@@ -298,3 +298,24 @@ def test_search_local_points_direct_dense_chunks(gpu):
         assert (cs, ran) == (ocs, oran), th
         assert (st[:n_cache] == gpu.DIRECT_GRID_SKIP).mean() >= 0.2
         assert (st[2048:n_cache] == gpu.DIRECT_GRID_SKIP).any()
+
+
+def test_search_direct_items_own_tcr(gpu):
+    """Items of one keyframe whose T_cr differ (the C ABI takes a T_cr per item; the call
+    packs one per keyframe only while they agree): bit-exact with the oracle."""
+    d = S.direct_scene(1, n_kf=4, max_obs=5)
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    ex = gpu.ORBextractor(nf, sf, nl, ini, mn)
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    kf_fr = [ex.ComputePyramid(im) for im in d["kf_images"]]
+    cur_fr = ex.ComputePyramid(d["cur_image"])
+    T = d["T_cr"].copy()
+    T["t"][::3, 0] += np.float32(2e-3)
+    T["t"][1::7, 1] -= np.float32(1e-3)
+    args = (d["item_ptr"], d["ref_index"], d["kps"], d["pt_ref"], T, d["px_proj"])
+    px, m = gpu.search_direct_batch(kf_fr, cur_fr, cam := d["scene"].camera(), *args)
+    opx, om = O.search_direct(orc, [orc.pyramid(im) for im in d["kf_images"]], orc.pyramid(d["cur_image"]),
+                              O.Cam(*d["scene"].cam), *args)
+    assert np.array_equal(m, om) and np.array_equal(px, opx)
+    base, bm = gpu.search_direct_batch(kf_fr, cur_fr, cam, *(args[:4] + (d["T_cr"], args[5])))
+    assert not np.array_equal(base, px)  # the per-item poses were used
