@@ -1373,12 +1373,18 @@ __device__ int find_direct_wave(const uint8_t *__restrict__ ref_pyr, const Align
     S.j[0][lane] = J0;
     S.j[1][lane] = J1;
     wave_lds_order();
-    float H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < 64; i++) {  // H += J J^T in pixel order (Align.cc:58-63)
-        const float J[3] = {S.j[0][i], S.j[1][i], 1.f};
-        for (int r = 0; r < 3; r++)
-            for (int cc = 0; cc < 3; cc++) H[r * 3 + cc] += J[r] * J[cc];
+    // H += J J^T in pixel order (Align.cc:58-63) with J = (J0, J1, 1): the five distinct
+    // sums (H is symmetric term by term, J * 1 is exact, and 64 ones sum to 64 exactly)
+    float h00 = 0.f, h01 = 0.f, h02 = 0.f, h11 = 0.f, h12 = 0.f;
+    for (int i = 0; i < 64; i++) {
+        const float a = S.j[0][i], b = S.j[1][i];
+        h00 += a * a;
+        h01 += a * b;
+        h02 += a;
+        h11 += b * b;
+        h12 += b;
     }
+    const float H[9] = {h00, h01, h02, h01, h11, h12, h02, h12, 64.f};
     float Hi[9];
     inverse3(H, Hi);
     const uint8_t *img = cur_pyr + clv.off[sl];
