@@ -180,17 +180,22 @@ __global__ __launch_bounds__(1024) void k_bow_vectors(const int *__restrict__ co
     }
     __threadfence_block();
     __syncthreads();
+    // the values into LDS (over the sorted keys, no longer read): the norm's ordered sum
+    // (one thread, the reference's order) then reads LDS instead of global memory
+    double *s_val = reinterpret_cast<double *>(s_key);
+    for (int j = threadIdx.x; j < nw_total; j += blockDim.x) s_val[j] = bv[j];
+    __syncthreads();
     if (tf && !must) {
         const double nd = (double)nw_total;
-        for (int j = threadIdx.x; j < nw_total; j += blockDim.x) bv[j] /= nd;
+        for (int j = threadIdx.x; j < nw_total; j += blockDim.x) bv[j] = s_val[j] / nd;
     }
     if (must) {
         if (threadIdx.x == 0) {
             double norm = 0.0;
             if (!l2) {
-                for (int j = 0; j < nw_total; j++) norm += fabs(bv[j]);
+                for (int j = 0; j < nw_total; j++) norm += fabs(s_val[j]);
             } else {
-                for (int j = 0; j < nw_total; j++) norm += bv[j] * bv[j];
+                for (int j = 0; j < nw_total; j++) norm += s_val[j] * s_val[j];
                 norm = sqrt(norm);
             }
             s_norm = norm;
@@ -198,7 +203,7 @@ __global__ __launch_bounds__(1024) void k_bow_vectors(const int *__restrict__ co
         __syncthreads();
         const double norm = s_norm;
         if (norm > 0.0)
-            for (int j = threadIdx.x; j < nw_total; j += blockDim.x) bv[j] /= norm;
+            for (int j = threadIdx.x; j < nw_total; j += blockDim.x) bv[j] = s_val[j] / norm;
     }
     __syncthreads();
     // FeatureVector: (node, feature) in map order
