@@ -111,11 +111,23 @@ inline void ComputeImagePyramid(FrameT &F) {
             }
         }
     }
-    // Frame.cc:807-813
+    // Frame.cc:807-813.  The reference clones the extractor's levels because its
+    // extractor resizes into them again for the next image; the drop-in extractor
+    // hands out fresh buffers per ComputePyramid that nothing writes afterwards, so the
+    // Frame shares them: the same pixels without a copy, and the device pyramid is
+    // found by their level-0 pointer
     F.mpORBextractorLeft->ComputePyramid(F.mImGray);
-    F.mvImagePyramid.resize(F.mpORBextractorLeft->GetLevels());
-    for (int l = 0; l < F.mpORBextractorLeft->GetLevels(); l++)
-        F.mvImagePyramid[l] = F.mpORBextractorLeft->mvImagePyramid[l].clone();
+    F.mvImagePyramid = F.mpORBextractorLeft->mvImagePyramid;
+}
+
+// Frame.cc:186-188, the copy constructor's pyramid copy (Tracking's
+// mLastFrame = Frame(mCurrentFrame), Tracking.cc:718): the same deep copy, and the
+// copy's level 0 indexed to the device pyramid of the original (no compare, no upload
+// when the next SparseImgAlign::run reads mLastFrame)
+template <class MatVec>
+inline void CopyImagePyramid(MatVec &dst, const MatVec &src) {
+    for (const auto &mat : src) dst.push_back(mat.clone());
+    dropin::PyramidPool::instance().alias(dst, src);
 }
 
 // Frame.cc:509-682: row-band Hamming search + SAD sub-pixel refinement + median cut,

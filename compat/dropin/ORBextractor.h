@@ -109,25 +109,34 @@ public:
     std::vector<cv::Mat> mvImagePyramid;
 
     // ORBextractor.cc:1129-1150: the pyramid on the GPU; mvImagePyramid gets host
-    // copies of the levels (the reference's Frame clones them, Frame.cc:810-813)
+    // copies of the levels in fresh buffers that nothing writes afterwards (the
+    // reference resizes into its own, ORBextractor.cc:1135-1146; a Frame shares them,
+    // FrameGPU.h).  Level 0 is the image (:1135), copied here while the GPU builds the
+    // levels above it, which come back in one DMA.
     void ComputePyramid(cv::Mat image) {
-        if (image.empty()) {
-            last_ = nullptr;
+        last_ = nullptr;
+        mvImagePyramid.assign(nlevels, cv::Mat());
+        if (image.empty() || !ex_) return;
+        dropin::PyramidPool &pool = dropin::PyramidPool::instance();
+        ygzfe_frame *f = pool.compute(ex_, nlevels, image.data, image.cols, image.rows, image.step[0]);
+        if (!f) return;
+        std::vector<uint8_t *> dst(nlevels);
+        std::vector<int> ds(nlevels);
+        for (int l = 0; l < nlevels; l++) {
+            int w = 0, h = 0;
+            if (ygzfe_frame_level(f, l, &w, &h, nullptr, 0) != YGZFE_OK) return;  // sizes only, no device work
+            mvImagePyramid[l].create(h, w, CV_8U);
+            dst[l] = mvImagePyramid[l].data;
+            ds[l] = (int)mvImagePyramid[l].step[0];
+        }
+        for (int y = 0; y < image.rows; y++)
+            std::memcpy(dst[0] + (size_t)y * ds[0], image.data + (size_t)y * image.step[0], (size_t)image.cols);
+        if (nlevels > 1 && ygzfe_frame_levels(f, 1, nlevels - 1, &dst[1], &ds[1]) != YGZFE_OK) {
             mvImagePyramid.assign(nlevels, cv::Mat());
             return;
         }
-        last_ = ex_ ? dropin::PyramidPool::instance().compute(ex_, nlevels, image.data, image.cols, image.rows,
-                                                              image.step[0])
-                    : nullptr;
-        mvImagePyramid.assign(nlevels, cv::Mat());
-        if (!last_) return;
-        for (int l = 0; l < nlevels; l++) {
-            int w = 0, h = 0;
-            if (ygzfe_frame_level(last_, l, &w, &h, nullptr, 0) != YGZFE_OK) return;
-            cv::Mat m(h, w, CV_8U);
-            ygzfe_frame_level(last_, l, nullptr, nullptr, m.data, (int)m.step[0]);
-            mvImagePyramid[l] = m;
-        }
+        pool.bind(f, mvImagePyramid[0]);
+        last_ = f;
     }
 
     ygzfe_extractor *handle() const { return ex_; }

@@ -12,12 +12,14 @@
 // member names, so this header needs none of their definitions.
 //
 // Device pyramids: Frame::ComputeImagePyramid computes the pyramid through the
-// extractor (ComputePyramid, then clones mvImagePyramid, Frame.cc:807-813).
-// The extractor leaves the device copy in a process-wide pool; a later call that
-// receives the Frame's (cloned) host pyramid finds it by its level-0 pointer and
-// a content fingerprint (one full compare of level 0 the first time a pointer is
-// seen), and uploads the host levels only when the pool has no copy (a Frame
-// built some other way).
+// extractor (ComputePyramid, Frame.cc:807-813).  The extractor leaves the device copy
+// in a process-wide pool, indexed by the host level-0 buffer it was computed from; a
+// later call that receives a Frame's host pyramid finds the device copy by that
+// pointer.  The pool holds every host buffer it indexes (a copy of its cv::Mat
+// header, i.e. a reference count), so an indexed buffer is never freed and handed to
+// another image: a pointer hit is exact.  A buffer seen for the first time (a Frame
+// deep-copied elsewhere, Frame.cc:186-188) is matched by one full compare of level 0,
+// or uploaded.
 #ifndef YGZFE_DROPIN_H_
 #define YGZFE_DROPIN_H_
 
@@ -25,8 +27,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <iterator>
 #include <list>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <string>
@@ -66,31 +70,45 @@ public:
         return *p;
     }
 
-    // The device pyramid of `img` (level 0, w x h, row stride) computed by `ex`;
-    // the returned frame stays valid until soft_capacity() newer pyramids have been made
-    // (unless pinned).
+    // ORBextractor::ComputePyramid: the device pyramid of `img` (level 0, w x h, row
+    // stride) computed by `ex` into a free entry.  The entry is found by pointer only
+    // after bind() names the host level-0 buffer holding these pixels; until then it
+    // can be found by content (its fingerprint, then a full compare).  The returned
+    // frame stays valid until soft_capacity() newer pyramids have been made (unless pinned).
     ygzfe_frame *compute(ygzfe_extractor *ex, int nlevels, const uint8_t *img, int w, int h, size_t stride) {
         std::lock_guard<std::mutex> lk(mu_);
         Entry *e = slot(ex, nlevels, w, h);
-        if (!e || !e->f) return nullptr;
-        e->level0.resize((size_t)w * h);
-        for (int y = 0; y < h; y++) std::memcpy(&e->level0[(size_t)y * w], img + (size_t)y * stride, (size_t)w);
-        if (ygzfe_compute_pyramid(ex, e->f, e->level0.data(), w) != YGZFE_OK) {
-            e->level0.clear();
-            return nullptr;
-        }
-        set_fp(e, fingerprint(e->level0.data(), w, h, (size_t)w));
+        if (!e || !e->f) return failed(last_error());
+        if (ygzfe_compute_pyramid(ex, e->f, img, (int)stride) != YGZFE_OK) return failed(last_error());
+        set_fp(e, fingerprint(img, w, h, stride));
         return e->f;
     }
 
+    // `level0` (a cv::Mat) holds the pixels `f`'s pyramid was computed from, and nothing
+    // writes into it afterwards: held and indexed by its pointer
+    template <class Mat>
+    void bind(const ygzfe_frame *f, const Mat &level0) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = by_frame_.find(f);
+        if (it != by_frame_.end() && level0.data) hold(it->second, level0);
+    }
+
+    // `dst` is a deep copy of `src` (Frame.cc:186-188, gpu::CopyImagePyramid): when
+    // src's level 0 is indexed, dst's is indexed to the same device pyramid
+    template <class MatVec>
+    void alias(const MatVec &dst, const MatVec &src) {
+        if (dst.empty() || src.empty() || !dst[0].data || !src[0].data) return;
+        std::lock_guard<std::mutex> lk(mu_);
+        auto ip = by_ptr_.find(src[0].data);
+        if (ip == by_ptr_.end()) return;
+        Entry *e = ip->second;
+        if (dst[0].cols == e->w && dst[0].rows == e->h && (int)dst.size() == e->nlevels) hold(e, dst[0]);
+    }
+
     // The device copy of a host pyramid (levels[l]: .data / .cols / .rows / .step).
-    // Lookup by the host level-0 pointer, guarded by a content fingerprint (8 whole
-    // rows and 512 bytes spread over level 0, hashed), so a hit costs no full
-    // compare.  A pointer seen for the first time is matched to an entry with the same
-    // fingerprint by one full compare of level 0 (once per host pyramid: a Frame clones
-    // the extractor's levels, Frame.cc:812; a KeyFrame shares its Frame's, KeyFrame.cc:
-    // 257-260), so a reused host buffer never returns a stale pyramid unless new
-    // content matched every sampled byte of the old.
+    // An indexed level-0 pointer is a hit (exact: the pool holds the buffer); a buffer
+    // seen for the first time is matched to an entry with the same fingerprint by one
+    // full compare of level 0 against that entry's held pixels, else uploaded (one DMA).
     template <class MatVec>
     ygzfe_frame *find_or_upload(const MatVec &levels) {
         if (levels.empty() || !levels[0].data) {
@@ -100,20 +118,18 @@ public:
         const int w = levels[0].cols, h = levels[0].rows, nl = (int)levels.size();
         const uint8_t *key = levels[0].data;
         const size_t stride = (size_t)levels[0].step[0];
-        const uint64_t fp = fingerprint(key, w, h, stride);
         std::lock_guard<std::mutex> lk(mu_);
         auto ip = by_ptr_.find(key);
         if (ip != by_ptr_.end()) {
             Entry *e = ip->second;
-            if (e->fp == fp && e->w == w && e->h == h && e->nlevels == nl) return touch(e)->f;
-            by_ptr_.erase(ip);  // the buffer holds other content now
-            e->host_ptr = nullptr;
+            if (e->w == w && e->h == h && e->nlevels == nl) return touch(e)->f;
         }
+        const uint64_t fp = fingerprint(key, w, h, stride);
         auto range = by_fp_.equal_range(fp);
         for (auto it = range.first; it != range.second; ++it) {
             Entry *e = it->second;
             if (e->w == w && e->h == h && e->nlevels == nl && same_level0(*e, key, stride)) {
-                bind_ptr(e, key);
+                hold(e, levels[0]);
                 return touch(e)->f;
             }
         }
@@ -123,23 +139,27 @@ public:
         if (!ex) return failed("no live ORBextractor with this pyramid's level count defines the level geometry");
         Entry *e = slot(ex, nl, w, h);
         if (!e || !e->f) return failed(last_error());
-        for (int l = 0; l < nl; l++)
-            if (ygzfe_frame_set_level(e->f, l, levels[l].data, (int)levels[l].step[0]) != YGZFE_OK)
-                return failed(last_error());
-        e->level0.resize((size_t)w * h);
-        for (int y = 0; y < h; y++) std::memcpy(&e->level0[(size_t)y * w], key + (size_t)y * stride, (size_t)w);
+        std::vector<const uint8_t *> src(nl);
+        std::vector<int> ss(nl);
+        for (int l = 0; l < nl; l++) {
+            src[l] = levels[l].data;
+            ss[l] = (int)levels[l].step[0];
+        }
+        if (ygzfe_frame_set_levels(e->f, 0, nl, src.data(), ss.data()) != YGZFE_OK) return failed(last_error());
         set_fp(e, fp);
-        bind_ptr(e, key);
+        hold(e, levels[0]);
         return e->f;
     }
 
     // Entries a caller needs together (a SearchLocalPointsDirect phase's keyframes)
     // are pinned: they are never recycled, and the pool grows past its soft capacity
-    // rather than fail when every entry is pinned.
+    // rather than fail when every entry is pinned; it shrinks back once they are unpinned.
     void pin(const ygzfe_frame *f, int delta) {
         std::lock_guard<std::mutex> lk(mu_);
         auto it = by_frame_.find(f);
-        if (it != by_frame_.end()) it->second->pins += delta;
+        if (it == by_frame_.end()) return;
+        it->second->pins += delta;
+        if (delta < 0 && it->second->pins == 0) trim();
     }
 
     // why the last lookup returned no pyramid
@@ -154,6 +174,16 @@ public:
         std::lock_guard<std::mutex> lk(mu_);
         return (int)lru_.size();
     }
+    // the most entries the pool has had at once (pinned growth past the soft capacity)
+    int peak() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return peak_;
+    }
+    // host level-0 buffers the pool holds (tests: the pool's host memory stays bounded)
+    int held() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return (int)by_ptr_.size();
+    }
 
     // the extractors whose level geometry uploads use: the latest live one with the
     // pyramid's level count (a destroyed extractor -- e.g. Tracking's mpIniORBextractor
@@ -166,10 +196,7 @@ public:
         std::lock_guard<std::mutex> lk(mu_);
         for (auto it = lru_.begin(); it != lru_.end();)
             if (it->ex == ex) {
-                unindex(&*it);
-                by_frame_.erase(it->f);
-                ygzfe_frame_destroy(it->f);
-                it = lru_.erase(it);
+                it = destroy(it);
             } else {
                 ++it;
             }
@@ -181,20 +208,28 @@ private:
     // a local map's keyframes plus the frames in flight: 96 pyramids of 752 x 480 are
     // ~46 MB of HBM; pinned entries may take the pool past it
     static constexpr int kCapacity = 96;
+    // host buffers held per entry (the extractor's level 0, which the Frame shares, and
+    // the copies Tracking makes, mLastFrame = Frame(mCurrentFrame), Tracking.cc:718); an
+    // older one is released and, if met again, matched by content
+    static constexpr int kHeld = 3;
+    struct Held {
+        const uint8_t *ptr;
+        std::shared_ptr<const void> mat;  // the cv::Mat header copy that keeps the buffer alive
+    };
     struct Entry {
         ygzfe_extractor *ex = nullptr;
         ygzfe_frame *f = nullptr;
         int w = 0, h = 0, nlevels = 0, pins = 0;
-        const uint8_t *host_ptr = nullptr;  // the host level 0 this content was last seen at
         uint64_t fp = 0;
         bool has_fp = false;
-        std::vector<uint8_t> level0;
+        std::vector<Held> held;  // host level-0 buffers with these pixels, oldest first
         std::list<Entry>::iterator self;  // its own position in lru_ (list iterators are stable)
     };
     static uint64_t mix(uint64_t h, uint64_t v) {
         h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
         return h * 0xBF58476D1CE4E5B9ull;
     }
+    // the content index for first-seen buffers (a hit is confirmed by a full compare):
     // 8 whole rows (first, last, 6 spread) + 512 bytes on a stride coprime to the width
     static uint64_t fingerprint(const uint8_t *p, int w, int h, size_t stride) {
         uint64_t f = mix((uint64_t)w, (uint64_t)h);
@@ -217,22 +252,47 @@ private:
         for (int k = 0; k < 512; k++, i = (i + step * 2 + 1) % n) f = mix(f, p[(i / w) * stride + i % w]);
         return f;
     }
+    // level 0 at p equals the entry's pixels (any held buffer: they are all equal)
     bool same_level0(const Entry &e, const uint8_t *p, size_t stride) const {
-        if (e.level0.size() != (size_t)e.w * e.h) return false;
+        if (e.held.empty()) return false;
+        const Held &hb = e.held.back();
+        const size_t hs = held_stride_.at(hb.ptr);
         for (int y = 0; y < e.h; y++)
-            if (std::memcmp(&e.level0[(size_t)y * e.w], p + (size_t)y * stride, (size_t)e.w) != 0) return false;
+            if (std::memcmp(hb.ptr + (size_t)y * hs, p + (size_t)y * stride, (size_t)e.w) != 0) return false;
         return true;
     }
     Entry *touch(Entry *e) {
         lru_.splice(lru_.begin(), lru_, e->self);
         return e;
     }
-    void unindex(Entry *e) {
-        if (e->host_ptr) {
-            auto ip = by_ptr_.find(e->host_ptr);
-            if (ip != by_ptr_.end() && ip->second == e) by_ptr_.erase(ip);
-            e->host_ptr = nullptr;
+    template <class Mat>
+    void hold(Entry *e, const Mat &m) {
+        const uint8_t *p = m.data;
+        auto ip = by_ptr_.find(p);
+        if (ip != by_ptr_.end()) {
+            if (ip->second == e) return;
+            release(ip->second, p);  // a buffer the pool holds has one content: it moved entries
         }
+        if ((int)e->held.size() >= kHeld) release(e, e->held.front().ptr);
+        std::shared_ptr<const void> keep(new Mat(m), [](const void *q) { delete static_cast<const Mat *>(q); });
+        e->held.push_back(Held{p, keep});
+        by_ptr_[p] = e;
+        held_stride_[p] = (size_t)m.step[0];
+    }
+    void release(Entry *e, const uint8_t *p) {
+        for (auto it = e->held.begin(); it != e->held.end(); ++it)
+            if (it->ptr == p) {
+                e->held.erase(it);
+                break;
+            }
+        auto ip = by_ptr_.find(p);
+        if (ip != by_ptr_.end() && ip->second == e) {
+            by_ptr_.erase(ip);
+            held_stride_.erase(p);
+        }
+    }
+    void unindex(Entry *e) {
+        while (!e->held.empty()) release(e, e->held.back().ptr);
         if (e->has_fp) {
             auto range = by_fp_.equal_range(e->fp);
             for (auto it = range.first; it != range.second; ++it)
@@ -248,15 +308,19 @@ private:
         e->has_fp = true;
         by_fp_.insert(std::make_pair(fp, e));
     }
-    void bind_ptr(Entry *e, const uint8_t *key) {
-        if (e->host_ptr && e->host_ptr != key) {
-            auto ip = by_ptr_.find(e->host_ptr);
-            if (ip != by_ptr_.end() && ip->second == e) by_ptr_.erase(ip);
+    std::list<Entry>::iterator destroy(std::list<Entry>::iterator it) {
+        unindex(&*it);
+        by_frame_.erase(it->f);
+        ygzfe_frame_destroy(it->f);
+        return lru_.erase(it);
+    }
+    // pinned entries made the pool grow: the unpinned least recently used ones beyond
+    // the soft capacity are freed (device pyramid and held host buffers)
+    void trim() {
+        for (auto it = lru_.end(); (int)lru_.size() > kCapacity && it != lru_.begin();) {
+            --it;
+            if (it->pins == 0) it = destroy(it);
         }
-        auto ip = by_ptr_.find(key);
-        if (ip != by_ptr_.end() && ip->second != e) ip->second->host_ptr = nullptr;
-        by_ptr_[key] = e;
-        e->host_ptr = key;
     }
     // a free (least recently used, unpinned) entry for a w x h pyramid of `ex`, at the front:
     // the least recently used one of the same geometry if there is one (its device
@@ -280,6 +344,7 @@ private:
             lru_.splice(lru_.begin(), lru_, victim);
         } else {
             lru_.emplace_front();
+            peak_ = std::max(peak_, (int)lru_.size());
         }
         Entry &e = lru_.front();
         e.self = lru_.begin();
@@ -296,7 +361,6 @@ private:
         e.h = h;
         e.nlevels = nlevels;
         e.pins = 0;
-        e.level0.clear();
         return &e;
     }
     ygzfe_frame *failed(const char *why) {
@@ -305,10 +369,12 @@ private:
     }
     std::mutex mu_;
     std::string why_;
+    int peak_ = 0;
     std::list<Entry> lru_;
-    std::unordered_map<const uint8_t *, Entry *> by_ptr_;
+    std::unordered_map<const uint8_t *, Entry *> by_ptr_;  // held host level-0 buffers
+    std::unordered_map<const uint8_t *, size_t> held_stride_;
     std::unordered_multimap<uint64_t, Entry *> by_fp_;
-    std::unordered_map<const ygzfe_frame *, Entry *> by_frame_;  // pin() lookups
+    std::unordered_map<const ygzfe_frame *, Entry *> by_frame_;  // pin() / bind() lookups
     std::vector<std::pair<ygzfe_extractor *, int>> live_;  // (extractor, nlevels), construction order
 };
 

@@ -110,6 +110,14 @@ int ygzfe_compute_pyramid_device(ygzfe_extractor *ex, ygzfe_frame *f, const uint
 int ygzfe_frame_level(const ygzfe_frame *f, int level, int *w, int *h, uint8_t *dst, int dst_stride);
 /* Upload a whole host pyramid (e.g. a Frame deep-copied from elsewhere). */
 int ygzfe_frame_set_level(ygzfe_frame *f, int level, const uint8_t *src, int src_stride);
+/* Host mirror of levels [first, first + count) in one DMA and one synchronisation:
+ * ORBextractor::ComputePyramid's public mvImagePyramid (ORBextractor.cc:1129-1150,
+ * ORBextractor.h:114), which Frame::ComputeImagePyramid hands to the Frame
+ * (Frame.cc:807-813).  dst[i] / dst_stride[i] receive level first + i. */
+int ygzfe_frame_levels(const ygzfe_frame *f, int first, int count, uint8_t *const *dst, const int *dst_stride);
+/* Upload levels [first, first + count) of a host pyramid in one DMA (a Frame whose
+ * pyramid the device has not seen, e.g. one deep-copied elsewhere, Frame.cc:186-188). */
+int ygzfe_frame_set_levels(ygzfe_frame *f, int first, int count, const uint8_t *const *src, const int *src_stride);
 
 /* ORBextractor::operator()(Frame*, keypoints, descriptors, method, leftEye=true)
  * (ORBextractor.cc:1031-1127, called from Frame::ExtractORB Frame.cc:332-348).

@@ -5,8 +5,11 @@
 //    Gauss-Newton loop of NLSSolver_impl.hpp:18-91, LDLT solve (:233-238) and
 //    T <- T * exp(-x) (:240-244).  One 1024-thread workgroup per frame pair runs
 //    every level and iteration (wave 0 solves, waves 1..15 own one feature per
-//    lane); H / Jres / chi2 are reduced with DPP wave steps + one LDS pass.  The reduction order differs from the reference's sequential sum,
-//    so poses agree within 1e-4, not bitwise.
+//    lane); H / Jres / chi2 are reduced with DPP / permlane wave steps + one LDS
+//    pass, and while no feature leaves the level a step is x = H_vis^-1 Jres with
+//    the inverse formed once per level.  The reduction order differs from the
+//    reference's sequential sum, so poses agree within 1e-4, not bitwise
+//    (SURVEY.md §8a row a12).
 //  * k_align2d: Align2D (Align.cc:8-105), one lane per patch, sequential float
 //    order as the reference -> bit-exact with oracle/.
 //  * k_find_direct: FindDirectProjection (ORBmatcher.cc:1573-1602) =
@@ -240,6 +243,59 @@ __device__ __forceinline__ void ldlt_solve6_nopiv(float r, float x[6]) {
     }
 #pragma unroll
     for (int i = 0; i < 6; i++) x[i] = y[i];
+}
+
+// The level's fixed H_vis (no feature out of bounds: H = H_vis exactly) solved once
+// per level for the six unit vectors: lane c (< 6) runs ldlt_solve6_nopiv's
+// factorization and substitutions on H_vis with y = e_c and keeps column c of
+// M = H_vis^-1 (the same zero rules, so x = M b is the LDLT solve of b up to
+// rounding); every iteration then costs a 6x6 matrix-vector product.  `hv` holds
+// H_vis in lanes 8 + hpack6(i, j) (ldlt_solve6_nopiv's layout).  Column c goes to
+// Mw[r * 6 + c].
+__device__ __forceinline__ void ldlt6_inverse_cols(float hv, int lane, float *Mw) {
+#pragma clang fp contract(fast)  // solver: fused products (rounding-level, pose parity 1e-4)
+    const int ri = __float_as_int(hv);
+    float A[36], y[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        y[i] = lane == i ? 1.f : 0.f;
+#pragma unroll
+        for (int j = i; j < 6; j++) {
+            const float v = __int_as_float(__builtin_amdgcn_readlane(ri, 8 + hpack6(i, j)));
+            A[i * 6 + j] = v;
+            A[j * 6 + i] = v;
+        }
+    }
+    if (ldlt6_step_nopiv<0>(A)) {
+        ldlt6_step_nopiv<1>(A);
+        ldlt6_step_nopiv<2>(A);
+        ldlt6_step_nopiv<3>(A);
+        ldlt6_step_nopiv<4>(A);
+        ldlt6_step_nopiv<5>(A);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        float t = y[i];
+#pragma unroll
+        for (int j = 0; j < i; j++) t -= A[i * 6 + j] * y[j];
+        y[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        const float dd = A[i * 6 + i];
+        y[i] = fabsf(dd) > 1.17549435e-38f ? y[i] * __builtin_amdgcn_rcpf(dd) : 0.f;
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+        float t = y[i];
+#pragma unroll
+        for (int j = i + 1; j < 6; j++) t -= A[j * 6 + i] * y[j];
+        y[i] = t;
+    }
+    if (lane < 6) {
+#pragma unroll
+        for (int r = 0; r < 6; r++) Mw[r * 6 + lane] = y[r];
+    }
 }
 
 // Eigen's diagonally pivoted LDLT (lower-triangle transpositions; |D_i| <=
@@ -694,9 +750,11 @@ struct AlignPairLds {
     float part[NW][32];
     float Hvis[21];
     float opart[NW][24];
+    float M[36];  // H_vis^-1 of the level, row-major (ldlt6_inverse_cols)
     SE3 T, old;
     float chi2, Hpk[21];  // H of the last iteration, upper triangle row-major
     int stop, brk, nmeas;
+    int out_it;  // the iteration (level * 16 + it) whose residual pass saw a feature out of bounds
 };
 
 template <int NW>
@@ -707,6 +765,7 @@ __device__ __forceinline__ void align_pair_init(AlignPairLds<NW> &P, const Align
     P.stop = 0;
     P.nmeas = 0;
     P.brk = 0;
+    P.out_it = -1;
     for (int i = 0; i < 21; i++) P.Hpk[i] = 0.f;
 }
 
@@ -732,41 +791,59 @@ __device__ __forceinline__ void align_sum_hvis(AlignPairLds<NW> &P, int lane) {
     }
 }
 
+// level start, solver wave (beside the first residual pass): M = H_vis^-1
+template <int NW>
+__device__ __forceinline__ void align_level_inverse(AlignPairLds<NW> &P, int lane) {
+    const float hv = (lane >= 8 && lane < 29) ? P.Hvis[lane - 8] : 0.f;
+    ldlt6_inverse_cols(hv, lane, P.M);
+}
+
 // one Gauss-Newton step, solver wave (NLSSolver_impl.hpp:18-91): reduce the
 // partials, H = H_vis - sum of the out-of-bounds features' H_f, LDLT, rollback or
 // T <- T exp(-x); P.brk set when the level's loop ends
 template <int NW>
-__device__ __forceinline__ void align_solver_step(AlignPairLds<NW> &P, int it, int lane) {
-    // Jres[6], chi2, n_meas over waves 1..NW-1: lane 8g + k adds waves
-    // 2g+1, 2g+2 of value k, then the 8 groups are folded by cross-lane adds
+__device__ __forceinline__ void align_solver_step(AlignPairLds<NW> &P, int it, int gi, int lane) {
+    // Jres[6], chi2, n_meas over waves 1..NW-1: lane 8g + k adds waves 2g+1, 2g+2 of
+    // value k, then the 8 groups fold (bit 3: DPP row_ror 8; bits 4, 5: permlane16 /
+    // permlane32 swaps, no LDS round trip), so every lane holds the total of value k
     float pk8;
     {
         const int k8 = lane & 7, w1 = 2 * (lane >> 3) + 1, w2 = w1 + 1;
         pk8 = (w1 < NW ? P.part[w1][k8] : 0.f) + (w2 < NW ? P.part[w2][k8] : 0.f);
         pk8 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(pk8), 0x128, 0xF, 0xF, false));
-        pk8 += __shfl_xor(pk8, 16, 64);
-        pk8 += __shfl_xor(pk8, 32, 64);
+        pk8 = pair_pl16(pk8, pk8);
+        pk8 = pair_pl32(pk8, pk8);
     }
-    float r = 0.f;
-    if (lane < 29) {
-        if (lane < 8) {
-            r = pk8;
-        } else {  // per-wave sums of the out-of-bounds features' H_f
+    YGZ_STAMP(6);
+    float x[6];
+    const int pi = __float_as_int(pk8);
+    const int nmeas = (int)__int_as_float(__builtin_amdgcn_readlane(pi, 7));
+    const float new_chi2 = __int_as_float(__builtin_amdgcn_readlane(pi, 6)) / (float)nmeas;
+    if (lane == 0) P.nmeas = nmeas;
+    YGZ_STAMP(7);
+    if (P.out_it != gi) {  // every feature inside the level: H = H_vis, x = H_vis^-1 Jres (lane r: row r)
+#pragma clang fp contract(fast)  // solver wave: fused products (rounding-level, pose parity 1e-4)
+        const float *Mr = &P.M[(lane < 6 ? lane : 0) * 6];
+        float xr = 0.f;
+#pragma unroll
+        for (int c = 0; c < 6; c++) xr += Mr[c] * __int_as_float(__builtin_amdgcn_readlane(pi, c));
+#pragma unroll
+        for (int k = 0; k < 6; k++) x[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xr), k));
+        if (lane < 21) P.Hpk[lane] = P.Hvis[lane];  // H of this iteration (the result's Fisher information)
+    } else {  // a feature left the level: H = H_vis - the per-wave sums of its H_f, factored afresh
+        float r = pk8;
+        if (lane >= 8 && lane < 29) {
             const int k = lane - 8;
             float o = 0.f;
 #pragma unroll
             for (int w = 1; w < NW; w++) o += P.opart[w][k];
             r = P.Hvis[k] - o;
-            P.Hpk[k] = r;  // H of this iteration (the result's Fisher information)
+            P.Hpk[k] = r;
+        } else if (lane >= 29) {
+            r = 0.f;
         }
+        ldlt_solve6_nopiv(r, x);
     }
-    YGZ_STAMP(6);
-    float x[6];
-    const int nmeas = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 7));
-    const float new_chi2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), 6)) / (float)nmeas;
-    if (lane == 0) P.nmeas = nmeas;
-    YGZ_STAMP(7);
-    ldlt_solve6_nopiv(r, x);
     YGZ_STAMP(8);
     const bool stop = P.stop || isnan(x[0]);
     const bool rollback = (it > 0 && (double)new_chi2 > 1.2 * (double)P.chi2) || stop;
@@ -923,7 +1000,7 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const Al
                                                     const AlignLevels &lv,
                                                     const ygzfe_camera &cam, const uint8_t *cur_pyr, int level,
                                                     const float (*s_patch)[NF], int f, float (*part)[32],
-                                                    float (*opart)[24], int wave, int lane) {
+                                                    float (*opart)[24], int *out_it, int gi, int wave, int lane) {
     const int border = 3;
     const int W = lv.w[level], H = lv.h[level];
     const float scale = lv.inv_scale[level];
@@ -1004,6 +1081,7 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const Al
         for (int k = 21; k < 32; k++) hv[k] = 0.f;
         const float t = wave_reduce32(hv, lane);
         if ((lane & 1) == 0 && (lane >> 1) < 21) opart[wave][lane >> 1] = t;
+        if (lane == 0) *out_it = gi;  // every wave that saw one writes the same value
     } else if (lane < 21) {
         opart[wave][lane] = 0.f;
     }
@@ -1049,11 +1127,12 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                 P.Hvis[lane] = r;
             }
             __syncthreads();  // L0b: part free again
+            align_level_inverse(P, lane);  // beside the first residual pass
             YGZ_STAMP(2);
             for (int it = 0; it < 10; it++) {
                 __syncthreads();  // A: partials written
                 YGZ_STAMP(3);
-                align_solver_step(P, it, lane);
+                align_solver_step(P, it, level * 16 + it, lane);
                 __syncthreads();  // B: pose / decision published
                 YGZ_STAMP(4);
                 if (P.brk) break;
@@ -1083,8 +1162,8 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
         __syncthreads();  // L0b
         for (int it = 0; it < 10; it++) {
             const SE3 T = P.T;
-            align_feat_residual<NF, NW>(F, D, T, lv, cam, job.cur_pyr, level, s_patch[cb], f, P.part, P.opart, wave,
-                                        lane);
+            align_feat_residual<NF, NW>(F, D, T, lv, cam, job.cur_pyr, level, s_patch[cb], f, P.part, P.opart,
+                                        &P.out_it, level * 16 + it, wave, lane);
             __syncthreads();  // A
             if (it == 0 && level > job.min_level)  // the next level, beside the solver's step
                 align_feat_precompute<NF, NW>(F, D.vis, Dn, lv, cam, job.ref_pyr, level - 1, s_patch[cb ^ 1],
@@ -1096,7 +1175,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
     }
 }
 
-int sparse_align_reg_capacity() { return 1024; }
+int sparse_align_reg_capacity() { return 1024 - 64; }  // one feature per thread of waves 1..15
 
 hipError_t launch_sparse_align(const AlignLevels &lv, const ygzfe_camera &cam, const AlignJob *jobs, int njobs,
                                float *scratch, size_t scratch_per_job, ygzfe_align_result *out, hipStream_t st,

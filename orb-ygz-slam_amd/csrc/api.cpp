@@ -175,6 +175,9 @@ struct StagingLease {
     StagingLease &operator=(const StagingLease &) = delete;
     ~StagingLease() {
         if (!s) return;
+        // an early error return may leave DMAs into / out of the pinned buffers queued:
+        // the next lessee (possibly another thread) writes them at once
+        if (hipStreamQuery(s->stream) != hipSuccess) (void)hipStreamSynchronize(s->stream);
         std::lock_guard<std::mutex> lk(staging_mutex());
         staging_free()[device].push_back(s);
     }
@@ -718,6 +721,75 @@ int ygzfe_frame_set_level(ygzfe_frame *f, int level, const uint8_t *src, int src
     }
     YGZ_HIP(hipMemcpyAsync(f->pyr.as<uint8_t>() + L.off, hs, n, hipMemcpyHostToDevice, ex->stream));
     YGZ_HIP(hipStreamSynchronize(ex->stream));  // the level is in place when the call returns, as before
+    return YGZFE_OK;
+}
+
+// levels [first, first + count) of the plan: checked range, and the device span
+// [lv[first].off, lv[last].off + w * h) that holds them (one DMA for all)
+static int level_span(const ygzfe_frame *f, int first, int count, size_t *off, size_t *bytes) {
+    const Plan &P = f->plan->hp();
+    if (first < 0 || count < 1 || first + count > P.nlevels) {
+        set_error("levels [%d, %d) out of range (%d levels)", first, first + count, P.nlevels);
+        return YGZFE_EINVAL;
+    }
+    const LevelDesc &a = P.lv[first], &b = P.lv[first + count - 1];
+    *off = a.off;
+    *bytes = (size_t)b.off + (size_t)b.w * b.h - a.off;
+    return YGZFE_OK;
+}
+
+int ygzfe_frame_levels(const ygzfe_frame *f, int first, int count, uint8_t *const *dst, const int *dst_stride) {
+    if (!f || !dst || !dst_stride) { set_error("null argument"); return YGZFE_EINVAL; }
+    size_t off = 0, bytes = 0;
+    YGZ_TRY(level_span(f, first, count, &off, &bytes));
+    const Plan &P = f->plan->hp();
+    for (int i = 0; i < count; i++)
+        if (!dst[i] || dst_stride[i] < P.lv[first + i].w) { set_error("level %d: no buffer or stride < width", first + i); return YGZFE_EINVAL; }
+    ygzfe_extractor *ex = f->ex;
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    // every level in one DMA into page-locked staging, ordered after the pyramid's writers on
+    // ex->stream; one synchronisation, then the row copies on the host
+    // (every user of the staging synchronises before it returns, under ex->mu)
+    YGZ_TRY(ex->hlvl.ensure(bytes));
+    YGZ_HIP(hipMemcpyAsync(ex->hlvl.p, f->pyr.as<uint8_t>() + off, bytes, hipMemcpyDeviceToHost, ex->stream));
+    YGZ_HIP(hipStreamSynchronize(ex->stream));
+    for (int i = 0; i < count; i++) {
+        const LevelDesc &L = P.lv[first + i];
+        const uint8_t *hs = ex->hlvl.as<uint8_t>() + (L.off - off);
+        if (dst_stride[i] == L.w) {
+            memcpy(dst[i], hs, (size_t)L.w * L.h);
+        } else {
+            for (int y = 0; y < L.h; y++) memcpy(dst[i] + (size_t)y * dst_stride[i], hs + (size_t)y * L.w, (size_t)L.w);
+        }
+    }
+    return YGZFE_OK;
+}
+
+int ygzfe_frame_set_levels(ygzfe_frame *f, int first, int count, const uint8_t *const *src, const int *src_stride) {
+    if (!f || !src || !src_stride) { set_error("null argument"); return YGZFE_EINVAL; }
+    size_t off = 0, bytes = 0;
+    YGZ_TRY(level_span(f, first, count, &off, &bytes));
+    const Plan &P = f->plan->hp();
+    for (int i = 0; i < count; i++)
+        if (!src[i] || src_stride[i] < P.lv[first + i].w) { set_error("level %d: no buffer or stride < width", first + i); return YGZFE_EINVAL; }
+    ygzfe_extractor *ex = f->ex;
+    YGZ_TRY(ensure_device(ex->device));
+    std::lock_guard<std::mutex> lk(ex->mu);
+    if (ex->align_pending) YGZ_HIP(hipEventSynchronize(ex->ev_align_done));  // an alignment reading this pyramid
+    YGZ_TRY(ex->hlvl.ensure(bytes));
+    for (int i = 0; i < count; i++) {
+        const LevelDesc &L = P.lv[first + i];
+        uint8_t *hs = ex->hlvl.as<uint8_t>() + (L.off - off);
+        if (src_stride[i] == L.w) {
+            memcpy(hs, src[i], (size_t)L.w * L.h);
+        } else {
+            for (int y = 0; y < L.h; y++) memcpy(hs + (size_t)y * L.w, src[i] + (size_t)y * src_stride[i], (size_t)L.w);
+        }
+    }
+    // the gaps between levels carry staging bytes: no kernel reads them as pixels
+    YGZ_HIP(hipMemcpyAsync(f->pyr.as<uint8_t>() + off, ex->hlvl.p, bytes, hipMemcpyHostToDevice, ex->stream));
+    YGZ_HIP(hipStreamSynchronize(ex->stream));  // the levels are in place when the call returns
     return YGZFE_OK;
 }
 
@@ -1394,6 +1466,18 @@ int ygzfe_sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, con
     // after everything queued so far on the extractor stream (the two pyramids)
     YGZ_HIP(hipEventRecord(ex->ev_align_fork, ex->stream));
     YGZ_HIP(hipStreamWaitEvent(st, ex->ev_align_fork, 0));
+    // A feature without a usable map point adds nothing to H, Jres, chi2 or the count
+    // (SparseImageAlign.cc:67-75), so a reference frame with more keypoints than the
+    // register kernel's threads (a keyframe after its DSO extraction, Frame.cc:717-771:
+    // ~2,400 rows, only the tracked ones with map points) sends only its usable
+    // features, in order, and stays on the register kernel
+    const int n_all = n;
+    int n_use = n;
+    if (n > sparse_align_reg_capacity()) {
+        n_use = 0;
+        for (int i = 0; i < n; i++) n_use += usable[i] != 0;
+    }
+    n = n_use;
     // one packed H2D from pinned staging: [job][keypoints][xyz][usable] (16-B aligned
     // pieces), cached device buffers, one D2H of the result
     const size_t o_k = align16(sizeof(AlignJob)), o_x = o_k + align16(sizeof(ygzfe_kp) * (size_t)n);
@@ -1415,9 +1499,21 @@ int ygzfe_sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, con
     job.min_level = min_level;
     job.T_init = *T_init;
     memcpy(hin, &job, sizeof(job));
-    memcpy(hin + o_k, kps, sizeof(ygzfe_kp) * (size_t)n);
-    memcpy(hin + o_x, xyz_ref, sizeof(float) * 3 * (size_t)n);
-    memcpy(hin + o_u, usable, (size_t)n);
+    if (n == n_all) {
+        memcpy(hin + o_k, kps, sizeof(ygzfe_kp) * (size_t)n);
+        memcpy(hin + o_x, xyz_ref, sizeof(float) * 3 * (size_t)n);
+        memcpy(hin + o_u, usable, (size_t)n);
+    } else {
+        ygzfe_kp *hk = reinterpret_cast<ygzfe_kp *>(hin + o_k);
+        float *hx = reinterpret_cast<float *>(hin + o_x);
+        for (int i = 0, j = 0; i < n_all; i++)
+            if (usable[i]) {
+                hk[j] = kps[i];
+                memcpy(hx + 3 * (size_t)j, xyz_ref + 3 * (size_t)i, 3 * sizeof(float));
+                j++;
+            }
+        memset(hin + o_u, 1, (size_t)n);
+    }
     YGZ_HIP(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, st));
     YGZ_HIP(launch_sparse_align(levels_of(P), *cam, reinterpret_cast<const AlignJob *>(din), 1,
                                 ex->align_scratch.as<float>(), spj, ex->align_out.as<ygzfe_align_result>(), st, n));
@@ -1580,7 +1676,8 @@ extern "C" int ygzfe_fast10_detect(int device, const uint8_t *img, int width, in
     YGZ_TRY(S->hout.ensure(out_bytes));
     YGZ_TRY(S->dev.ensure(in_bytes + out_bytes));
     uint8_t *h = S->hin.as<uint8_t>(), *d = S->dev.as<uint8_t>();
-    memcpy(h, img, img_b);
+    // the caller's last row may hold only `width` bytes (a cv::Mat ROI view)
+    memcpy(h, img, (size_t)(height - 1) * stride + width);
     memcpy(h + o_r, rois, (size_t)n_roi * 16);
     YGZ_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, S->stream));
     int32_t *dc = reinterpret_cast<int32_t *>(d + in_bytes);
@@ -1985,7 +2082,7 @@ extern "C" int ygzfe_stereo_from_rgbd(int device, const float *im_depth, int wid
     YGZ_TRY(S->hout.ensure(out_bytes));
     YGZ_TRY(S->dev.ensure(in_bytes + out_bytes));
     uint8_t *h = S->hin.as<uint8_t>(), *d = S->dev.as<uint8_t>();
-    memcpy(h, im_depth, img);
+    memcpy(h, im_depth, 4 * ((size_t)(height - 1) * stride + width));  // the last row may end at `width`
     memcpy(h + o_k, kps, sizeof(ygzfe_kp) * (size_t)n);
     YGZ_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, S->stream));
     float *du = reinterpret_cast<float *>(d + in_bytes), *dd = du + n;

@@ -109,6 +109,7 @@ hipError_t launch_sparse_align(const AlignLevels &lv, const ygzfe_camera &cam, c
                                int njobs, float *scratch, size_t scratch_per_job, ygzfe_align_result *out,
                                hipStream_t st, int max_n);
 size_t sparse_align_scratch_floats(int n);
+int sparse_align_reg_capacity();  // features the register kernel holds (one per feature-wave thread)
 // stream placement probe (ensure_align_stream): a kernel that holds its stream for
 // `us` microseconds of wall clock, and an empty one
 hipError_t launch_hold_us(int us, hipStream_t st);

@@ -241,14 +241,17 @@ class ORBextractor:
         return self.extract(frame, ORBSLAM_KEYPOINT)
 
 
-def fast10_detect(img, barrier, rois, sse=True, cap=1 << 16, device=0):
+def fast10_detect(img, barrier, rois, sse=True, cap=None, device=0):
     """Thirdparty/fast FAST-10 on the GPU (ygzfe_fast10_detect): fast_corner_detect_10_sse2 (sse) or
     fast_corner_detect_10 over each ROI (x0, y0, w, h) of `img` -> list of int16[n, 2] (x, y) corner
-    arrays, ROI-relative and in the reference's raster order."""
+    arrays, ROI-relative and in the reference's raster order.  `cap` (corners per ROI) defaults to
+    the largest ROI's pixel count, which no ROI can exceed."""
     img = np.ascontiguousarray(img, np.uint8)
     H, W = img.shape
     rois = np.ascontiguousarray(rois, np.int32).reshape(-1, 4)
     n = len(rois)
+    if cap is None:
+        cap = max(1, int((rois[:, 2].clip(0) * rois[:, 3].clip(0)).max())) if n else 1
     xy = np.zeros((max(n, 1), cap, 2), np.int16)
     counts = np.zeros(max(n, 1), np.int32)
     _check(lib().ygzfe_fast10_detect(device, _p(img), W, H, W, _p(rois), n, int(barrier), int(bool(sse)), _p(xy), cap,

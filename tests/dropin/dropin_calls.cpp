@@ -450,6 +450,40 @@ int main(int argc, char **argv) {
                     "+ descriptors == oracle", fi, F.N);
     }
 
+    // The pyramid pool's lookups are exact.  A Frame's pyramid is found by its
+    // level-0 pointer (the pool holds that buffer, so the address cannot be handed to another
+    // image).  A host pyramid in a fresh buffer whose level 0 differs from a pooled one only in
+    // pixels the content index does not sample gets its own device pyramid; an identical deep
+    // copy is matched by one full compare.
+    {
+        dropin::PyramidPool &pool = dropin::PyramidPool::instance();
+        Frame A(im1, T.mpORBextractorLeft);
+        std::vector<cv::Mat> B, Cc;
+        for (const cv::Mat &m : A.mvImagePyramid) {
+            B.push_back(m.clone());  // plain deep copies: not aliased to A's device pyramid
+            Cc.push_back(m.clone());
+        }
+        std::vector<uint8_t> sampled((size_t)W * H, 0);  // the fingerprint's 512 spread samples
+        {
+            const size_t n = (size_t)W * H, step = n / 512 + 1;
+            size_t i = 7 % n;
+            for (int k = 0; k < 512; k++, i = (i + step * 2 + 1) % n) sampled[i] = 1;
+        }
+        int x = 8;
+        while (sampled[(size_t)W + x]) x++;  // row 1 is none of the 8 whole sampled rows
+        B[0].data[(size_t)W + x] ^= 0x40;
+        ygzfe_frame *fa = pool.find_or_upload(A.mvImagePyramid);
+        ygzfe_frame *fb = pool.find_or_upload(B);
+        ygzfe_frame *fc = pool.find_or_upload(Cc);
+        std::vector<uint8_t> back((size_t)W * H);
+        const bool read = fb && ygzfe_frame_level(fb, 0, nullptr, nullptr, back.data(), W) == YGZFE_OK;
+        const bool b_ok = read && fb != fa && std::memcmp(back.data(), B[0].data, back.size()) == 0;
+        CHECK(fa && b_ok && fc == fa && pool.held() <= 3 * pool.size(),
+              "pyramid pool: an unsampled one-pixel change gets its own device pyramid (%s), an identical copy is "
+              "matched (%s), %d held host buffers for %d entries", b_ok ? "yes" : "NO", fc == fa ? "yes" : "NO",
+              pool.held(), pool.size());
+    }
+
     // DSO path: a frame with direct-tracked keypoints and no features yet (Frame.cc:335-337)
     {
         ORBextractor dso_ex(1000, 2.0f, nl, 20, 7);
@@ -607,6 +641,69 @@ int main(int argc, char **argv) {
             });
             std::printf("TIMING search_by_projection_last_frame dropin_ms %.4f oracle_ms %.4f queries %zu\n", g, c,
                         q.size());
+        }
+
+        // ---------------- a whole fallback frame in Tracking's call order: Frame(im) (Tracking.cc:390)
+        // -> TrackWithMotionModel: ExtractFeatures, ORB mode (:1154), the pose from the last frame
+        // (:1160), the map points cleared (:1162), SearchByProjection(mCurrentFrame, mLastFrame, 15,
+        // MONOCULAR) (:1171) -> mLastFrame = Frame(mCurrentFrame) (:718; the copy is kept aside so
+        // the last frame stays the one with map points)
+        std::vector<double> f_ctor, f_extract, f_search, f_copy;
+        auto fallback = [&](bool record) {
+            auto t0 = std::chrono::steady_clock::now();
+            auto lap = [&t0]() {
+                const auto t1 = std::chrono::steady_clock::now();
+                const double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+                t0 = t1;
+                return ms;
+            };
+            T.mCurrentFrame = Frame(im1, T.mpORBextractorLeft);
+            const double a = lap();
+            T.mCurrentFrame.ExtractFeatures();
+            const double b = lap();
+            T.mCurrentFrame.SetPose(TCR * T.mLastFrame.mTcw);
+            std::fill(C.mvpMapPoints.begin(), C.mvpMapPoints.end(), static_cast<MapPoint *>(nullptr));
+            const int nm = T.MotionModel(15);
+            const double c = lap();
+            { Frame copy(T.mCurrentFrame); }
+            const double d = lap();
+            if (record) {
+                f_ctor.push_back(a);
+                f_extract.push_back(b);
+                f_search.push_back(c);
+                f_copy.push_back(d);
+            }
+            return nm;
+        };
+        {
+            const int nm = fallback(false);
+            int same = nm == wn && nm > 100;
+            for (int i2 = 0; i2 < C.N && same; i2++) {
+                MapPoint *exp = want[i2] >= 0 ? L.mvpMapPoints[src[want[i2]]] : nullptr;
+                same = C.mvpMapPoints[i2] == exp;
+            }
+            CHECK(same, "whole fallback frame (Frame(im) -> ExtractFeatures -> SearchByProjection(mCurrentFrame, "
+                        "mLastFrame, 15, MONOCULAR) -> Frame(mCurrentFrame)): %d matches (oracle %d)", nm, wn);
+        }
+        if (g_timing) {
+            for (int i = 0; i < 4; i++) fallback(false);
+            const double g = median_ms(30, [&] { fallback(true); });
+            auto med = [](std::vector<double> v) {
+                std::sort(v.begin(), v.end());
+                return v[v.size() / 2];
+            };
+            std::vector<ygzo_kp> okf(4096);
+            std::vector<uint8_t> odf(4096 * 32);
+            const ygzo_mframe mfc = mframe(C, true);  // the frame the fallback left
+            const double c = median_ms(10, [&] {
+                ygzo_compute_pyramid(&o, im1.data, W, H, W, lp);
+                ygzo_extract_orbslam(&o, lp, lw, lh, nullptr, 0, okf.data(), odf.data(), 4096);
+                ygzo_search_projection_best(&mfc, q.data(), qd.data(), (int)q.size(), blocked.data(), 100, 1,
+                                            want.data());
+            });
+            std::printf("TIMING fallback_frame dropin_ms %.4f oracle_ms %.4f frame_ctor_ms %.4f extract_ms %.4f "
+                        "search_by_projection_ms %.4f last_frame_copy_ms %.4f\n",
+                        g, c, med(f_ctor), med(f_extract), med(f_search), med(f_copy));
         }
     }
 
@@ -931,8 +1028,10 @@ int main(int argc, char **argv) {
                   "map %s, cache %zu -> %zu", NK, th, C.mvKeys.size(), w.keys.size(),
                   w.local_runs ? "searched" : "skipped", cache0.size(), T.mvpDirectMapPointsCache.size());
             if (NK > dropin::PyramidPool::soft_capacity() && th == 150)
-                CHECK(dropin::PyramidPool::instance().size() > dropin::PyramidPool::soft_capacity(),
-                      "  the pyramid pool grew past its soft capacity for the pinned keyframes: %d entries",
+                CHECK(dropin::PyramidPool::instance().peak() > dropin::PyramidPool::soft_capacity() &&
+                          dropin::PyramidPool::instance().size() <= dropin::PyramidPool::soft_capacity(),
+                      "  the pyramid pool grew past its soft capacity for the pinned keyframes (%d entries) and "
+                      "shrank back once they were unpinned (%d)", dropin::PyramidPool::instance().peak(),
                       dropin::PyramidPool::instance().size());
             if (g_timing && th == 150 && NK == 3) {
                 auto run = [&] {
@@ -994,6 +1093,182 @@ int main(int argc, char **argv) {
               "matcher.FindDirectProjection(ob.first, &mCurrentFrame, mp, px_curr, level): %d / %d bit-exact, "
               "%d converged", same, tried, conv);
         (void)cur_level0;
+
+        // ------------------------------------------------ whole direct frames in Tracking's call order
+        // GrabImageMonocular's Frame(im) (Tracking.cc:390) -> TrackWithSparseAlignment: the pose from
+        // the last frame (mVelocity = I, :2151), mpAlign->run (:2170-2171), SetPose(TCR *
+        // mLastFrame.mTcw) (:2179) -> TrackLocalMapDirect's SearchLocalPointsDirect (:2191-2201) ->
+        // for a keyframe, CreateNewKeyFrame's ExtractFeatures, DSO mode (:1535, Frame.cc:717-771:
+        // N tracked points, no features yet) -> mLastFrame = Frame(mCurrentFrame) (:718).  The
+        // frames alternate im1 / im0 and chain as in Tracking: each run() aligns against the copy
+        // the previous frame left, whose points are the previous SearchLocalPointsDirect's.
+        // The first frames are checked against the oracle step by step; then each kind is timed
+        // beside the oracle's work on the same inputs (pyramid, SparseImgAlign, the search
+        // restated above, ygzo_extract_dso).
+        {
+            const Frame saved_last = T.mLastFrame;
+            const cv::Mat ims[2] = {im1, im0};
+            ygzo_orb odso;
+            ygzo_orb_init(&odso, 1000, 2.0f, nl, 20, 7, 0);
+            auto reset_direct = [&] {
+                T.mvpDirectMapPointsCache = cache0;
+                T.mvpLocalMapPoints.clear();
+                T.mvpNextLocalMapPoints = local;
+                T.mnCacheHitTh = 150;
+                T.nUpdateLocalMap = 0;
+            };
+            // SparseImageAlign.cc:57-128's inputs of the oracle, from the Frames' own members
+            auto oracle_align = [&](const Frame &ref, const Frame &cur, ygzo_align_out &ao) {
+                std::vector<float> xyz(3 * (size_t)ref.N, 0.f);
+                std::vector<uint8_t> us(ref.N, 0);
+                for (int i = 0; i < ref.N; i++) {
+                    MapPoint *mp = ref.mvpMapPoints[i];
+                    if (!mp || mp->isBad() || ref.mvbOutlier[i]) continue;
+                    us[i] = 1;
+                    const Vector3f p = ref.mTcw * mp->GetWorldPos();
+                    for (int q = 0; q < 3; q++) xyz[3 * i + q] = p[q];
+                }
+                uint8_t *rpp[YGZO_MAX_LEVELS], *cpp[YGZO_MAX_LEVELS];
+                for (int l = 0; l < nl; l++) {
+                    rpp[l] = ref.mvImagePyramid[l].data;
+                    cpp[l] = cur.mvImagePyramid[l].data;
+                }
+                const SE3f T0s = cur.mTcw * ref.mTcw.inverse();
+                const ygzo_se3 T0{{T0s.unit_quaternion().x(), T0s.unit_quaternion().y(), T0s.unit_quaternion().z(),
+                                   T0s.unit_quaternion().w()},
+                                  {T0s.translation()[0], T0s.translation()[1], T0s.translation()[2]}};
+                ygzo_sparse_align(rpp, cpp, lw, lh, o.inv_scale, &ocam,
+                                  reinterpret_cast<const ygzo_kp *>(ref.mvKeys.data()), xyz.data(), us.data(), ref.N,
+                                  nl - 1, 1, &T0, &ao);
+            };
+            std::vector<double> t_ctor, t_align, t_direct, t_kf, t_copy;
+            std::vector<ygzo_kp> kf_exist;  // the last keyframe's tracked rows before its extraction
+            int32_t kf_grid = -1;           // and the DSO grid state it started from
+            auto stamp = [](std::chrono::steady_clock::time_point &t0) {
+                const auto t1 = std::chrono::steady_clock::now();
+                const double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+                t0 = t1;
+                return ms;
+            };
+            // one frame; check >= 0: compare every step with the oracle (frame number `check`)
+            int bad = 0, steps = 0;
+            size_t last_visible = 0;
+            auto direct_frame = [&](int k, bool keyframe, bool check) {
+                auto t0 = std::chrono::steady_clock::now();
+                T.mCurrentFrame = Frame(ims[k & 1], T.mpORBextractorLeft);  // Tracking.cc:390
+                const double a = stamp(t0);
+                T.mCurrentFrame.SetPose(T.mLastFrame.mTcw);  // mVelocity * mLastFrame.mTcw, :2151
+                ygzo_align_out ao;
+                if (check) oracle_align(T.mLastFrame, T.mCurrentFrame, ao);
+                t0 = std::chrono::steady_clock::now();
+                SE3f TCRk;
+                const size_t vis = T.SparseAlign(TCRk);  // :2170-2171
+                const double b = stamp(t0);
+                last_visible = vis;
+                if (check) {
+                    float err = 0.f;
+                    const float gq[4] = {TCRk.unit_quaternion().x(), TCRk.unit_quaternion().y(),
+                                         TCRk.unit_quaternion().z(), TCRk.unit_quaternion().w()};
+                    for (int q = 0; q < 4; q++) err = std::fmax(err, std::fabs(gq[q] - ao.T.q[q]));
+                    for (int q = 0; q < 3; q++) err = std::fmax(err, std::fabs(TCRk.translation()[q] - ao.T.t[q]));
+                    bad += !(err <= 1e-4f && (int)vis == ao.n_visible && vis > 100);
+                    steps++;
+                }
+                T.mCurrentFrame.SetPose(TCRk * T.mLastFrame.mTcw);  // :2179
+                reset_direct();
+                Want w;
+                if (check) {
+                    for (int l = 0; l < nl; l++) cp[l] = C.mvImagePyramid[l].data;
+                    w = expected(cache0, local, 150);
+                }
+                t0 = std::chrono::steady_clock::now();
+                T.TrackLocalMapDirect();  // :2201
+                const double c = stamp(t0);
+                if (check) {
+                    bool same = C.mvKeys.size() == w.keys.size() && C.mvpMapPoints == w.mps && w.keys.size() > 100;
+                    for (size_t i = 0; same && i < w.keys.size(); i++)
+                        same = C.mvKeys[i].pt.x == w.keys[i].pt.x && C.mvKeys[i].pt.y == w.keys[i].pt.y;
+                    bad += !same;
+                    steps++;
+                }
+                double d = 0;
+                if (keyframe) {
+                    std::vector<ygzo_kp> ex(C.N), ok_(8192);
+                    std::vector<uint8_t> odesc(8192 * 32);
+                    std::memcpy(ex.data(), C.mvKeys.data(), sizeof(ygzo_kp) * C.N);
+                    int32_t g0 = 0;
+                    ygzfe_extractor_dso_grid(T.mpORBextractorLeft->handle(), &g0, nullptr);
+                    kf_exist = ex;
+                    kf_grid = g0;
+                    t0 = std::chrono::steady_clock::now();
+                    T.mCurrentFrame.ExtractFeatures();  // CreateNewKeyFrame, :1535 (DSO: N > 0, not extracted)
+                    d = stamp(t0);
+                    if (check) {
+                        uint8_t *lpc[YGZO_MAX_LEVELS];
+                        for (int l = 0; l < nl; l++) lpc[l] = C.mvImagePyramid[l].data;
+                        odso.dso_grid = g0;
+                        const int n = ygzo_extract_dso(&odso, lpc, lw, lh, ex.data(), (int)ex.size(), ok_.data(),
+                                                       odesc.data(), 8192);
+                        bad += !(n == C.N && n > (int)ex.size() &&
+                                 std::memcmp(ok_.data(), C.mvKeys.data(), sizeof(ygzo_kp) * n) == 0 &&
+                                 std::memcmp(odesc.data(), C.mDescriptors.data, (size_t)32 * n) == 0);
+                        steps++;
+                    }
+                }
+                t0 = std::chrono::steady_clock::now();
+                T.mLastFrame = Frame(T.mCurrentFrame);  // :718
+                const double e = stamp(t0);
+                if (!check) {
+                    t_ctor.push_back(a);
+                    t_align.push_back(b);
+                    t_direct.push_back(c);
+                    t_kf.push_back(d);
+                    t_copy.push_back(e);
+                }
+            };
+            for (int k = 0; k < 4; k++) direct_frame(k, k == 3, true);
+            CHECK(bad == 0, "whole direct frames (Frame(im) -> mpAlign->run -> SearchLocalPointsDirect [-> DSO "
+                  "ExtractFeatures] -> mLastFrame = Frame(mCurrentFrame)), 4 chained frames: %d / %d steps == oracle "
+                  "(last run() visible %zu)", steps - bad, steps, last_visible);
+            if (g_timing) {
+                auto med = [](std::vector<double> v) {
+                    std::sort(v.begin(), v.end());
+                    return v.empty() ? 0.0 : v[v.size() / 2];
+                };
+                for (int kind = 0; kind < 2; kind++) {
+                    const bool kf = kind == 1;
+                    t_ctor.clear(), t_align.clear(), t_direct.clear(), t_kf.clear(), t_copy.clear();
+                    int k = 0;
+                    for (int i = 0; i < 6; i++) direct_frame(k++, kf, false);  // warm
+                    t_ctor.clear(), t_align.clear(), t_direct.clear(), t_kf.clear(), t_copy.clear();
+                    const double g = median_ms(30, [&] { direct_frame(k++, kf, false); });
+                    // the oracle's work on the same inputs: the pyramid, SparseImgAlign from the last
+                    // frame the chain left, the search, and for a keyframe ygzo_extract_dso
+                    std::vector<ygzo_kp> okk(8192);
+                    std::vector<uint8_t> odk(8192 * 32);
+                    for (int l = 0; l < nl; l++) cp[l] = C.mvImagePyramid[l].data;
+                    const Frame last = T.mLastFrame;
+                    const double c = median_ms(5, [&] {
+                        ygzo_compute_pyramid(&o, ims[k & 1].data, W, H, W, lp);
+                        ygzo_align_out ao;
+                        oracle_align(last, T.mCurrentFrame, ao);
+                        (void)expected(cache0, local, 150);
+                        if (kf) {
+                            odso.dso_grid = kf_grid;
+                            ygzo_extract_dso(&odso, cp, lw, lh, kf_exist.data(), (int)kf_exist.size(), okk.data(),
+                                             odk.data(), 8192);
+                        }
+                    });
+                    std::printf("TIMING %s dropin_ms %.4f oracle_ms %.4f frame_ctor_ms %.4f run_ms %.4f "
+                                "search_local_points_direct_ms %.4f extract_dso_ms %.4f last_frame_copy_ms %.4f\n",
+                                kf ? "keyframe_frame" : "direct_frame", g, c, med(t_ctor), med(t_align), med(t_direct),
+                                med(t_kf), med(t_copy));
+                }
+            }
+            T.mLastFrame = saved_last;
+            T.mCurrentFrame = Frame(im1, T.mpORBextractorLeft);
+            T.mCurrentFrame.SetPose(TCR);
+        }
         }
     }
 

@@ -49,6 +49,25 @@ public:
         ComputeImagePyramid();
     }
 
+    // Frame.cc:156-189 for the members this stub has (deep copies of the images and
+    // descriptors, mbFeatureExtracted false), the pyramid copy of :186-188 through the
+    // drop-in (gpu::CopyImagePyramid: the one-line edit INTEGRATION.md §1 lists)
+    Frame(const Frame &frame)
+        : mbf(frame.mbf), mb(frame.mb), N(frame.N), mvKeys(frame.mvKeys), mvKeysRight(frame.mvKeysRight),
+          mvuRight(frame.mvuRight), mvDepth(frame.mvDepth), mDescriptors(frame.mDescriptors.clone()),
+          mDescriptorsRight(frame.mDescriptorsRight.clone()), mvpMapPoints(frame.mvpMapPoints),
+          mvbOutlier(frame.mvbOutlier), mvMatchedFrom(frame.mvMatchedFrom), mFeatVec(frame.mFeatVec),
+          mBowVec(frame.mBowVec), mpORBvocabulary(frame.mpORBvocabulary), mK(frame.mK),
+          mDistCoef(frame.mDistCoef.clone()), mSensor(frame.mSensor), mImDepth(frame.mImDepth.clone()),
+          mTcw(frame.mTcw), mnScaleLevels(frame.mnScaleLevels), mvScaleFactors(frame.mvScaleFactors),
+          mvInvScaleFactors(frame.mvInvScaleFactors), mvLevelSigma2(frame.mvLevelSigma2),
+          mvInvLevelSigma2(frame.mvInvLevelSigma2), mpORBextractorLeft(frame.mpORBextractorLeft),
+          mpORBextractorRight(frame.mpORBextractorRight), mImGray(frame.mImGray.clone()),
+          mImRight(frame.mImRight.clone()), mbFeatureExtracted(false), mnId(frame.mnId) {
+        gpu::CopyImagePyramid(mvImagePyramid, frame.mvImagePyramid);
+    }
+    Frame &operator=(const Frame &) = default;  // the reference's implicit member-wise assignment
+
     void ExtractORB(int flag, const cv::Mat &im);
     void ComputeImagePyramid();
     void ComputeStereoMatches();
