@@ -47,7 +47,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-from ygzfe.sequence import C5_FRAMES, XI, C5Shard, sweep_index  # noqa: E402
+from ygzfe.sequence import C2, C5_FRAMES, XI, C5Shard, sweep_index  # noqa: E402
 
 
 def parse():
@@ -65,11 +65,12 @@ def parse():
     ap.add_argument("--no-align", action="store_true")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture one step into a HIP graph and replay it (measured: same throughput as eager launches)")
-    ap.add_argument("--schedule", choices=["split", "overlap", "tail", "serial"], default="serial",
-                    help="split: blur + descriptors + Hamming on a side stream beside FAST / octree, "
-                         "SparseImgAlign after them; overlap: SparseImgAlign beside orient + Hamming too; "
-                         "tail: the extraction on one stream, then Hamming on a side stream beside "
-                         "SparseImgAlign; serial: every stage on one stream")
+    ap.add_argument("--schedule", choices=["split", "overlap", "tail", "serial"], default="overlap",
+                    help="the timed steps' schedule. split: blur + descriptors + Hamming on a side stream "
+                         "beside FAST / octree, SparseImgAlign after them; overlap: SparseImgAlign beside "
+                         "orient + Hamming too; tail: the extraction on one stream, then Hamming on a side "
+                         "stream beside SparseImgAlign; serial: every stage on one stream.  The per-stage "
+                         "roofline pass always runs serial (one kernel on the GPU at a time)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="process each rank's shard in this many chunks (each its own batch), gathering a "
                          "chunk's result slots on a communication stream while the next chunk computes "
@@ -141,13 +142,12 @@ def main():
         if int(one.item()) != args.gpus:
             sys.exit(f"bench.py: all_reduce over RCCL counted {int(one.item())} ranks, expected {args.gpus}")
 
-    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    W, H, nf, sf, nl, ini, mn = C2
     n_seq = (args.frames or C5_FRAMES) if args.workload == "c5" else world * args.batch
     n_chunks = args.chunks if args.chunks > 0 else (4 if world > 1 else 1)
     t_r = time.time()
     # the rank's whole C5 job (ygzfe/sequence.py; tests/test_gpu_c5.py runs the same object)
-    shard = C5Shard(n_seq, rank, world, dev, chunks=n_chunks, schedule=args.schedule, align=not args.no_align,
-                    scenes=S)
+    shard = C5Shard(n_seq, rank, world, dev, chunks=n_chunks, schedule=args.schedule, align=not args.no_align)
     render_s = time.time() - t_r
     torch.cuda.set_stream(shard.stream)
     stream, sptr = shard.stream, shard.sptr
@@ -205,12 +205,16 @@ def main():
     # stay out of the throughput run)
     stage_ms = {}
     if not args.no_stage_timing:
+        # serial: each stage's events bracket one kernel that has the GPU to itself (under
+        # overlap a stage's time would include its neighbour's share of the GPU)
+        shard.schedule = "serial"
         timing_all(True)
         torch.cuda.synchronize(dev)
         for _ in range(args.steps):
             step(timed_gather=True)
         torch.cuda.synchronize(dev)
         stage_ms = timing_all(False)
+        shard.schedule = args.schedule
         check_all()
         if gather_ms:
             stage_ms["rccl_gather"] = float(np.mean([a.elapsed_time(b) for a, b in gather_ms]))
@@ -411,7 +415,13 @@ def main():
                        "collective": (f"RCCL gather of result slots to rank 0 (torch.distributed.gather), "
                                       f"{n_chunks} chunk(s), each gathered on a communication stream while the "
                                       f"next chunk computes") if world > 1 else "none (N=1: rank 0 is the root)",
-                       "schedule": args.schedule, "hip_graph": graph_ok},
+                       "schedule": ("chunked (each chunk serial)" if shard.chunks else args.schedule),
+                       "schedule_stage_timing": "serial",
+                       "schedule_note": ("value times the steps under `schedule`; roofline.stages_ms comes from "
+                                         "a separate pass of the same steps in the serial schedule (one kernel "
+                                         "on the GPU at a time), so the stage times sum to that pass's step, "
+                                         "not to ms_per_step"),
+                       "hip_graph": graph_ok},
             "roofline": roof,
             "pipeline_gbps_model": round(pipeline_gbps, 2),
             "render_s": round(render_s, 2),

@@ -351,6 +351,13 @@ int ygzfe_batch_sparse_align(ygzfe_batch *b, int n_pairs, const int32_t *d_ref_i
  * counts[r] = corners found (ECAP if any exceeds cap; the first cap are written). */
 int ygzfe_fast10_detect(int device, const uint8_t *img, int width, int height, int stride, const int32_t *rois,
                         int n_roi, int barrier, int variant, int16_t *xy, int cap, int32_t *counts);
+/* Debug view of the DSO_KEYPOINT cell kernel itself (ComputeKeyPointsDSOSingleLevel's
+ * per-cell FAST-10, ORBextractor.cc:1317-1345): one pass over every g x g cell of the
+ * grid of a width x height image (tight rows) at `barrier`, with the cell kernel's own
+ * scan region (the whole cell for g < 22, else [3, g-3)).  flags[cell][g * g] = 1 at
+ * each corner (cell-relative raster order); border cells, which the kernel skips, are
+ * all 0.  (h / g) * (w / g) cells, row-major. */
+int ygzfe_debug_dso_cells(int device, const uint8_t *img, int width, int height, int g, int barrier, uint8_t *flags);
 
 /* ------------------------------------------------------------------------ */
 /* Align2D / FindDirectProjection (Align.h:20-26, ORBmatcher.cc:1573-1602)   */

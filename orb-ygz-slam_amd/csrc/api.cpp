@@ -1696,6 +1696,31 @@ extern "C" int ygzfe_fast10_detect(int device, const uint8_t *img, int width, in
     return YGZFE_OK;
 }
 
+extern "C" int ygzfe_debug_dso_cells(int device, const uint8_t *img, int width, int height, int g, int barrier,
+                                     uint8_t *flags) {
+    if (!img || !flags || width <= 0 || height <= 0 || g < 7 || g > kDsoMaxGridHost) {
+        set_error("invalid argument (g in [7, %d])", kDsoMaxGridHost);
+        return YGZFE_EINVAL;
+    }
+    const size_t ncells = (size_t)(height / g) * (width / g), img_b = (size_t)width * height;
+    const size_t o_f = align16(img_b), fb = ncells * g * g;
+    if (ncells == 0) return YGZFE_OK;
+    YGZ_TRY(ensure_device(device));
+    StagingLease S;
+    YGZ_TRY(S.acquire(device));
+    YGZ_TRY(S->hin.ensure(img_b));
+    YGZ_TRY(S->hout.ensure(fb));
+    YGZ_TRY(S->dev.ensure(o_f + fb));
+    uint8_t *d = S->dev.as<uint8_t>();
+    memcpy(S->hin.p, img, img_b);
+    YGZ_HIP(hipMemcpyAsync(d, S->hin.p, img_b, hipMemcpyHostToDevice, S->stream));
+    YGZ_HIP(launch_dso_cells_debug(d, width, height, g, barrier, d + o_f, S->stream));
+    YGZ_HIP(hipMemcpyAsync(S->hout.p, d + o_f, fb, hipMemcpyDeviceToHost, S->stream));
+    YGZ_HIP(hipStreamSynchronize(S->stream));
+    memcpy(flags, S->hout.p, fb);
+    return YGZFE_OK;
+}
+
 // Align2D(const cv::Mat& cur_img, ...) on a host image: the 48 x 48 window around
 // the estimate goes up (the whole image only when the iterations walk out of it).
 extern "C" int ygzfe_align2d_image(int device, const uint8_t *img, int w, int h, int stride,

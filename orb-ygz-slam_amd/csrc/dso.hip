@@ -60,9 +60,14 @@ __device__ __forceinline__ float shi_tomasi(const uint8_t *p, int S) {
 
 // cell k of the grid; writes up to 3 keys (x | y << 16, level-0 px) sorted by
 // descending score (NaN last, ties by scan order) and the count.
+// Debug form (dbg_flags != null, ygzfe_debug_dso_cells): one pass of the cell's scan at
+// `dbg_barrier` only, its corner flags written to dbg_flags[k][g * g] (cell-relative
+// raster order, 0 outside the scanned region), no scoring -- the cell path's own
+// segment-test output, compared with the reference's per-cell corner lists.
 __global__ __launch_bounds__(256) void k_dso_cells(const uint8_t *__restrict__ img, int w, int h, int g,
                                                    const uint8_t *__restrict__ occ,
-                                                   uint32_t *__restrict__ out_keys, int *__restrict__ out_cnt) {
+                                                   uint32_t *__restrict__ out_keys, int *__restrict__ out_cnt,
+                                                   int dbg_barrier, uint8_t *__restrict__ dbg_flags) {
     __shared__ uint8_t s_img[kDsoS * kDsoS];
     __shared__ float s_sc[kDsoMaxGrid * kDsoMaxGrid];
     __shared__ int s_any;
@@ -70,7 +75,11 @@ __global__ __launch_bounds__(256) void k_dso_cells(const uint8_t *__restrict__ i
     const int rows = h / g, cols = w / g;
     const int k = blockIdx.x;
     const int nn = k / cols;
-    if (threadIdx.x == 0) out_cnt[k] = 0;
+    if (dbg_flags) {
+        for (int i = threadIdx.x; i < g * g; i += 256) dbg_flags[(size_t)k * g * g + i] = 0;
+    } else if (threadIdx.x == 0) {
+        out_cnt[k] = 0;
+    }
     if (nn == 0 || nn == rows - 1 || (k % cols) == 0 || (k + 1) % cols == 0) return;
     const int x_start = (k - nn * cols) * g, y_start = nn * g;
     const int S = g + 2 * kDsoHalo;
@@ -83,6 +92,14 @@ __global__ __launch_bounds__(256) void k_dso_cells(const uint8_t *__restrict__ i
     const int lo = g < 22 ? 0 : 3, hi = g < 22 ? g : g - 3;
     const int span = hi > lo ? hi - lo : 0;
     __syncthreads();
+    if (dbg_flags) {
+        for (int i = threadIdx.x; i < span * span; i += 256) {
+            const int cy = lo + i / span, cx = lo + i % span;
+            dbg_flags[(size_t)k * g * g + cy * g + cx] =
+                fast10_corner(s_img + (cy + kDsoHalo) * S + cx + kDsoHalo, S, dbg_barrier) ? 1 : 0;
+        }
+        return;
+    }
     int barrier = 20;
     for (int pass = 0; pass < 2; pass++) {
         if (threadIdx.x == 0) s_any = 0;
@@ -207,7 +224,17 @@ hipError_t launch_dso_pass(const uint8_t *img, int w, int h, int g, const uint8_
                            hipStream_t st) {
     const int ncells = (h / g) * (w / g);
     if (ncells <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_dso_cells, dim3(ncells), dim3(256), 0, st, img, w, h, g, occ, keys, cnt);
+    hipLaunchKernelGGL(k_dso_cells, dim3(ncells), dim3(256), 0, st, img, w, h, g, occ, keys, cnt, 0,
+                       (uint8_t *)nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_dso_cells_debug(const uint8_t *img, int w, int h, int g, int barrier, uint8_t *flags,
+                                  hipStream_t st) {
+    const int ncells = (h / g) * (w / g);
+    if (ncells <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dso_cells, dim3(ncells), dim3(256), 0, st, img, w, h, g, (const uint8_t *)nullptr,
+                       (uint32_t *)nullptr, (int *)nullptr, barrier, flags);
     return hipGetLastError();
 }
 

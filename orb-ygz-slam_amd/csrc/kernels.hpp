@@ -42,6 +42,8 @@ hipError_t launch_dso_pass(const uint8_t *img, int w, int h, int g, const uint8_
                            hipStream_t st);
 hipError_t launch_dso_finish2(const uint32_t *keys, const int *cnt, int ncells, ygzfe_kp *kps, int row0,
                               int *total, hipStream_t st);
+hipError_t launch_dso_cells_debug(const uint8_t *img, int w, int h, int g, int barrier, uint8_t *flags,
+                                  hipStream_t st);
 constexpr int kDsoMaxGridHost = 96;
 
 // hamming.hip

@@ -241,6 +241,22 @@ class ORBextractor:
         return self.extract(frame, ORBSLAM_KEYPOINT)
 
 
+def debug_dso_cells(img, g, barrier, device=0):
+    """The DSO_KEYPOINT cell kernel's own FAST-10 pass (ygzfe_debug_dso_cells): for each g x g
+    cell of the grid, row-major, the cell-relative corners in raster order (int16[n, 2] (x, y)),
+    from one pass at `barrier` over the kernel's scan region; border cells are empty."""
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape
+    ncells = (H // g) * (W // g)
+    flags = np.zeros((max(ncells, 1), g, g), np.uint8)
+    _check(lib().ygzfe_debug_dso_cells(device, _p(img), W, H, int(g), int(barrier), _p(flags)), "debug_dso_cells")
+    out = []
+    for k in range(ncells):
+        ys, xs = np.nonzero(flags[k])  # raster order (row-major nonzero)
+        out.append(np.stack([xs, ys], 1).astype(np.int16))
+    return out
+
+
 def fast10_detect(img, barrier, rois, sse=True, cap=None, device=0):
     """Thirdparty/fast FAST-10 on the GPU (ygzfe_fast10_detect): fast_corner_detect_10_sse2 (sse) or
     fast_corner_detect_10 over each ROI (x0, y0, w, h) of `img` -> list of int16[n, 2] (x, y) corner

@@ -41,7 +41,7 @@ class C5Shard:
         import torch
         import ygzfe
         if scenes is None:
-            import _scenes as scenes  # tests/_scenes.py: the textured plane and its constants
+            from . import scene as scenes  # the textured plane, its constants and pose algebra
         self.S = S = scenes
         self.torch = torch
         self.n_seq, self.rank, self.world, self.dev = n_seq, rank, world, dev

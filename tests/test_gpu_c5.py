@@ -9,6 +9,9 @@ the object bench.py times) over the whole 13,728-frame EuRoC MH01..05-length seq
 * the frames either side of every shard boundary (1715/1716, 3431/3432, ..., 13727) against
   the oracle (ORBextractor C2, bit-exact), and every halo align pair (b-1 -> b) against the
   oracle's SparseImgAlign (pose within 1e-4, same visible count);
+* every 16th frame against the oracle's extraction and every 64th align pair against its
+  SparseImgAlign (858 frames, 215 pairs);
+* the overlap / split / tail stream schedules (bench.py times `overlap`) equal serial;
 * a world-size-1 RCCL process group ("nccl" = RCCL, device_id bound): the device-packed
   slots gathered to rank 0 with torch.distributed.gather (one batch and chunked) equal the
   local slots.
@@ -132,6 +135,64 @@ def test_c5_shard_boundaries_vs_oracle(c5_full):
         assert err <= POSE_TOL, f"halo pair ({b - 1}, {b}): pose differs by {err}"
         assert cur["n_visible"] == o.n_visible, f"halo pair ({b - 1}, {b}): n_visible {cur['n_visible']} vs " \
                                                 f"{o.n_visible}"
+
+
+def test_c5_sampled_frames_and_pairs_vs_oracle(c5_full):
+    """Beyond the shard boundaries: every 16th frame's keypoints and descriptors (858 frames)
+    against the oracle's extraction (ORBextractor C2, bit-exact) and every 64th align pair
+    (215 pairs) against the oracle's SparseImgAlign (pose within 1e-4, same visible count)."""
+    sh = c5_full
+    W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    slots = sh.local_slots().cpu().numpy()
+    cap = sh.cap
+    pyr = {}
+
+    def pyramid(g):
+        if g not in pyr:
+            pyr[g] = orc.pyramid(sh.batch.read_level(g, 0))
+        return pyr[g]
+
+    frames = list(range(0, C5_FRAMES, 16))
+    bad = []
+    for g in frames:
+        got = D.unpack_slot(slots[g], cap, ygzfe.KP_DTYPE)
+        rk, rd = orc.extract(pyramid(g))
+        same = got["frame"] == g and got["n"] == len(rk) and np.array_equal(got["desc"], rd) and \
+            all(np.array_equal(got["kps"][f], rk[f]) for f in rk.dtype.names)
+        if not same:
+            bad.append(g)
+    assert not bad, f"{len(bad)} of {len(frames)} sampled frames differ from the oracle, first {bad[:8]}"
+    xyz = sh.xyz
+    ocam = O.Cam(*sh.cam)
+    T0 = O.se3_from((0, 0, 0, 1), (0, 0, 0))
+    pairs = list(range(1, C5_FRAMES, 64))
+    worst = 0.0
+    for b in pairs:
+        ref = D.unpack_slot(slots[b - 1], cap, ygzfe.KP_DTYPE)
+        cur = D.unpack_slot(slots[b], cap, ygzfe.KP_DTYPE)
+        n = ref["n"]
+        x = xyz[b - 1, :n].cpu().numpy()
+        o = O.sparse_align(pyramid(b - 1), pyramid(b), orc.inv_scale, ocam, ref["kps"], x, np.ones(n, np.uint8), 3, 1,
+                           T0)
+        assert cur["has_align"]
+        err = S.se3_log_inf(cur["q"], cur["t"], np.array(o.T.q[:]), np.array(o.T.t[:]))
+        worst = max(worst, err)
+        assert err <= POSE_TOL, f"pair ({b - 1}, {b}): pose differs by {err}"
+        assert cur["n_visible"] == o.n_visible, f"pair ({b - 1}, {b}): n_visible {cur['n_visible']} vs {o.n_visible}"
+        pyr.pop(b - 1, None)
+    print(f"C5 sample: {len(frames)} frames bit-exact, {len(pairs)} align pairs, worst |dT| {worst:.2e}")
+
+
+@pytest.mark.parametrize("schedule", ["overlap", "split", "tail"])
+def test_c5_schedules_equal_serial(c5_full, schedule):
+    """The stream schedules bench.py can time (the default `overlap` included) give the serial
+    schedule's slots byte for byte: they reorder launches across streams, never the results."""
+    dev = torch.device("cuda", 0)
+    sh = _run(C5Shard(C5_FRAMES, 0, 1, dev, schedule=schedule))
+    assert torch.equal(sh.local_slots(), c5_full.local_slots())
+    del sh
+    torch.cuda.empty_cache()
 
 
 def test_c5_rccl_gather_world1(c5_full):

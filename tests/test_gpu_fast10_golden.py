@@ -11,7 +11,7 @@ oracle in between).
   faster_corner_10_sse.cpp:192-194), thresholds 20 and 5.
 
 The GPU runs the same segment test as k_dso_cells (csrc/dso.hip fast10_corner) through the C ABI
-(ygzfe_fast10_detect)."""
+(ygzfe_fast10_detect), and k_dso_cells itself through its debug pass (ygzfe_debug_dso_cells)."""
 import os
 
 import numpy as np
@@ -60,6 +60,28 @@ def test_fast10_dso_cells_match_reference(gpu, g, th):
         want = xy[offs[k]:offs[k + 1]]
         assert np.array_equal(got[k], want), f"g {g} th {th} cell {tuple(cells[k])}: {got[k].tolist()} vs " \
                                              f"{want.tolist()}"
+
+
+@pytest.mark.parametrize("g", [18, 19, 22, 30])
+@pytest.mark.parametrize("th", [20, 5])
+def test_dso_cell_kernel_matches_reference(gpu, g, th):
+    """k_dso_cells itself (its debug pass: the cell kernel's LDS tile, scan region and segment
+    test, ORBextractor.cc:1317-1345) against the reference's fast_corner_detect_10_sse2 corner
+    lists of the same cells."""
+    img = _image("test1")
+    H, W = img.shape
+    got = gpu.debug_dso_cells(img, g, th)
+    cols = W // g
+    cells = FIX[f"dso/g{g}/cells"].astype(np.int32)
+    xy, offs = FIX[f"dso/g{g}/t{th}/xy"], FIX[f"dso/g{g}/t{th}/offs"]
+    n_corners = 0
+    for k, (x0, y0) in enumerate(cells):
+        assert x0 % g == 0 and y0 % g == 0
+        want = xy[offs[k]:offs[k + 1]]
+        mine = got[(y0 // g) * cols + x0 // g]
+        assert np.array_equal(mine, want), f"g {g} th {th} cell ({x0}, {y0}): {mine.tolist()} vs {want.tolist()}"
+        n_corners += len(want)
+    assert n_corners > 0
 
 
 def test_fast10_rejects_out_of_bounds_roi(gpu):
