@@ -16,11 +16,9 @@
 // 255 * 255) (:51-55).
 //
 // Method: NLLSSolver::optimize dispatches on method_ (NLSSolver_impl.hpp:8-13) to
-// Gauss-Newton or Levenberg-Marquardt (:95 ff).  The GPU kernel implements the
-// Gauss-Newton path Tracking uses (Tracking.cc:284 keeps the default).  An instance
-// constructed with LevenbergMarquardt refuses to run: run() logs once to stderr and
-// returns 0 (the reference's "no alignment" result, SparseImageAlign.cc:24-27)
-// instead of silently computing a different estimate.
+// optimizeGaussNewton (:18-91, what Tracking.cc:284 constructs) or
+// optimizeLevenbergMarquardt (:95-212); both run on the GPU
+// (ygzfe_sparse_align_method).
 #ifndef YGZ_SPARSE_IMAGE_ALIGN_
 #define YGZ_SPARSE_IMAGE_ALIGN_
 
@@ -48,15 +46,6 @@ public:
 
     template <class FrameT, class SE3T>
     size_t run(FrameT *ref_frame, FrameT *cur_frame, SE3T &TCR) {
-        if (method_ != GaussNewton) {  // NLSSolver_impl.hpp:8-13: only the GN path is on the GPU
-            static bool logged = false;
-            if (!logged) {
-                logged = true;
-                fprintf(stderr, "ygzfe SparseImgAlign: Method LevenbergMarquardt is not implemented on the GPU; "
-                                "run() returns 0 (construct with GaussNewton, as Tracking.cc:284 does)\n");
-            }
-            return 0;
-        }
         if (ref_frame->mvKeys.empty()) return 0;  // SparseImageAlign.cc:24-27
         const SE3T T_cur_from_ref = cur_frame->mTcw * ref_frame->mTcw.inverse();
         const int n = ref_frame->N;
@@ -91,9 +80,12 @@ public:
         T0.t[1] = t[1];
         T0.t[2] = t[2];
         ygzfe_align_result r;
-        if (ygzfe_sparse_align(ref, cur, &cam, dropin::as_kp(ref_frame->mvKeys.data()), xyz.data(), usable.data(), n,
-                               max_level_, min_level_, &T0, &r) != YGZFE_OK)
+        const int method = method_ == LevenbergMarquardt ? YGZFE_ALIGN_LEVENBERG_MARQUARDT : YGZFE_ALIGN_GAUSS_NEWTON;
+        if (ygzfe_sparse_align_method(ref, cur, &cam, dropin::as_kp(ref_frame->mvKeys.data()), xyz.data(),
+                                      usable.data(), n, max_level_, min_level_, &T0, method, &r) != YGZFE_OK) {
+            dropin::log_once("SparseImgAlign::run", dropin::last_error());
             return 0;
+        }
         typedef typename std::decay<decltype(T_cur_from_ref.unit_quaternion())>::type Quat;
         typedef typename std::decay<decltype(T_cur_from_ref.translation())>::type Vec;
         Vec tr;

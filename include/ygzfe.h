@@ -326,6 +326,16 @@ int ygzfe_sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, con
                              const ygzfe_kp *kps, const float *xyz_ref, const uint8_t *usable, int n,
                              int max_level, int min_level, const ygzfe_se3 *T_init);
 int ygzfe_sparse_align_end(const ygzfe_frame *cur, ygzfe_align_result *result);
+/* NLLSSolver's method (NLSSolver_impl.hpp:8-13): SparseImgAlign(.., n_iter, method).  */
+enum ygzfe_align_method { YGZFE_ALIGN_GAUSS_NEWTON = 0, YGZFE_ALIGN_LEVENBERG_MARQUARDT = 1 };
+/* ygzfe_sparse_align with the method: Gauss-Newton (optimizeGaussNewton, :18-91, what
+ * Tracking.cc:284 constructs) or Levenberg-Marquardt (optimizeLevenbergMarquardt,
+ * :95-212: damped H_ii (1 + mu), a trial per chi2 evaluation, mu_ 0.1 per level,
+ * SparseImageAlign.cc:40).  For LM, result->H is H_ as the last trial left it (damped). */
+int ygzfe_sparse_align_method(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam,
+                              const ygzfe_kp *kps, const float *xyz_ref, const uint8_t *usable, int n,
+                              int max_level, int min_level, const ygzfe_se3 *T_init, int method,
+                              ygzfe_align_result *result);
 /* The align stream's hardware-queue placement probe, for audit: streams
  * the probe created (0 before the first alignment) and whether the chosen one passed
  * the probe (1), was taken unprobed (0: probe off, 4 rejections or its 150 ms spent),

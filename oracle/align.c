@@ -193,10 +193,65 @@ static inline float wmul(double a, double b) { return (float)(a * b); }
 
 enum { PS = 4, PH = 2, PA = 16 };
 
-int ygzo_sparse_align(uint8_t **ref_levels, uint8_t **cur_levels, const int *lw, const int *lh,
-                      const float *inv_scale, const ygzo_cam *cam, const ygzo_kp *kps,
-                      const float *xyz_ref, const uint8_t *usable, int n, int max_level,
-                      int min_level, const ygzo_se3 *T_init, ygzo_align_out *out) {
+/* computeResiduals (SparseImageAlign.cc:130-231) at T over the visible features: returns
+ * chi2 (the sum; the caller divides by n_meas_), adds the measurement count to *n_meas,
+ * and with linearize the H / Jres terms (unit weights: the robust cost is never enabled) */
+static float align_residuals(const uint8_t *cimg, int cw, int chh, float scale, const ygzo_cam *cam,
+                             const float *xyz_ref, const uint8_t *vis, const float *patch, const float *jac, int n,
+                             const ygzo_se3 *T, int linearize, size_t *n_meas, float H[36], float Jres[6]) {
+    const int border = PH + 1, cs = cw;
+    float chi2 = 0.f;
+    for (int i = 0; i < n; i++) {
+        if (!vis[i]) continue;
+        float pc3[3];
+        ygzo_se3_act(T, xyz_ref + 3 * (size_t)i, pc3);
+        const float u = (cam->fx * pc3[0] / pc3[2] + cam->cx) * scale;
+        const float v = (cam->fy * pc3[1] / pc3[2] + cam->cy) * scale;
+        const int ui = (int)floorf(u), vi = (int)floorf(v);
+        if (ui < 0 || vi < 0 || ui - border < 0 || vi - border < 0 || ui + border >= cw || vi + border >= chh)
+            continue;
+        const float su = u - ui, sv = v - vi;
+        const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
+        const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
+        int pcn = 0;
+        for (int y = 0; y < PS; ++y) {
+            const uint8_t *p = cimg + (size_t)(vi + y - PH) * cs + (ui - PH);
+            for (int xx = 0; xx < PS; ++xx, ++p, ++pcn) {
+                const float ic = wtl * p[0] + wtr * p[1] + wbl * p[cs] + wbr * p[cs + 1];
+                const float res = ic - patch[(size_t)i * PA + pcn];
+                chi2 += res * res * 1.0f;
+                (*n_meas)++;
+                if (!linearize) continue;
+                const float *J = jac + ((size_t)i * PA + pcn) * 6;
+                for (int r = 0; r < 6; r++) {
+                    for (int c = 0; c < 6; c++) H[r * 6 + c] += J[r] * J[c] * 1.0f;
+                    Jres[r] -= J[r] * res * 1.0f;
+                }
+            }
+        }
+    }
+    return chi2;
+}
+
+static float norm_max6(const float x[6]) {
+    float nm = -1.f;
+    for (int k = 0; k < 6; k++) if (fabsf(x[k]) > nm) nm = fabsf(x[k]);
+    return nm;
+}
+
+/* update (SparseImageAlign.cc:240-244): T_new = T * exp(-x) */
+static void align_update(const ygzo_se3 *T, const float x[6], ygzo_se3 *Tn) {
+    float mx[6];
+    for (int k = 0; k < 6; k++) mx[k] = -x[k];
+    ygzo_se3 E;
+    ygzo_se3_exp(mx, &E);
+    ygzo_se3_mul(T, &E, Tn);
+}
+
+int ygzo_sparse_align_method(uint8_t **ref_levels, uint8_t **cur_levels, const int *lw, const int *lh,
+                             const float *inv_scale, const ygzo_cam *cam, const ygzo_kp *kps,
+                             const float *xyz_ref, const uint8_t *usable, int n, int max_level,
+                             int min_level, const ygzo_se3 *T_init, int method, ygzo_align_out *out) {
     memset(out, 0, sizeof(*out));
     out->T = *T_init;
     if (n <= 0) return 0; /* SparseImageAlign.cc:24-27 */
@@ -204,10 +259,12 @@ int ygzo_sparse_align(uint8_t **ref_levels, uint8_t **cur_levels, const int *lw,
     float *jac = (float *)calloc((size_t)n * PA * 6, sizeof(float));
     uint8_t *vis = (uint8_t *)calloc((size_t)n, 1);
     ygzo_se3 T = *T_init;
-    float chi2_ = 1e10f;
+    /* NLLSSolver::reset (NLSSolver_impl.hpp:289-298): once per run */
+    float chi2_ = 1e10f, mu = 0.01f, nu = 2.0f; /* mu_init_ 0.01, nu_init_ 2 (NLSSolver.h:126-129) */
     int stop = 0;
     size_t n_meas = 0;
     float H[36], Jres[6], x[6];
+    memset(H, 0, sizeof(H));
     const int border = PH + 1;
     for (int level = max_level; level >= min_level; level--) {
         const int n_iter = 10; /* iterations[] = {10,...}; levels >= 6 read past it (UB) */
@@ -243,65 +300,84 @@ int ygzo_sparse_align(uint8_t **ref_levels, uint8_t **cur_levels, const int *lw,
                 }
             }
         }
-        /* optimizeGaussNewton (NLSSolver_impl.hpp:18-91) */
-        ygzo_se3 old = T;
-        int it;
-        for (it = 0; it < n_iter; ++it) {
-            memset(H, 0, sizeof(H));
-            memset(Jres, 0, sizeof(Jres));
-            n_meas = 0;
-            /* computeResiduals (SparseImageAlign.cc:130-231) */
-            const uint8_t *cimg = cur_levels[level];
-            const int cw = lw[level], chh = lh[level], cs = cw;
-            float chi2 = 0.f;
-            for (int i = 0; i < n; i++) {
-                if (!vis[i]) continue;
-                float pc3[3];
-                ygzo_se3_act(&T, xyz_ref + 3 * (size_t)i, pc3);
-                const float u = (cam->fx * pc3[0] / pc3[2] + cam->cx) * scale;
-                const float v = (cam->fy * pc3[1] / pc3[2] + cam->cy) * scale;
-                const int ui = (int)floorf(u), vi = (int)floorf(v);
-                if (ui < 0 || vi < 0 || ui - border < 0 || vi - border < 0 || ui + border >= cw || vi + border >= chh)
-                    continue;
-                const float su = u - ui, sv = v - vi;
-                const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
-                const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
-                int pcn = 0;
-                for (int y = 0; y < PS; ++y) {
-                    const uint8_t *p = cimg + (size_t)(vi + y - PH) * cs + (ui - PH);
-                    for (int xx = 0; xx < PS; ++xx, ++p, ++pcn) {
-                        const float ic = wtl * p[0] + wtr * p[1] + wbl * p[cs] + wbr * p[cs + 1];
-                        const float res = ic - patch[(size_t)i * PA + pcn];
-                        chi2 += res * res * 1.0f;
-                        n_meas++;
-                        const float *J = jac + ((size_t)i * PA + pcn) * 6;
-                        for (int r = 0; r < 6; r++) {
-                            for (int c = 0; c < 6; c++) H[r * 6 + c] += J[r] * J[c] * 1.0f;
-                            Jres[r] -= J[r] * res * 1.0f;
-                        }
-                    }
+        const uint8_t *cimg = cur_levels[level];
+        const int cw = lw[level], chh = lh[level];
+        int it = 0;
+        if (method == YGZO_ALIGN_GN) {
+            /* optimizeGaussNewton (NLSSolver_impl.hpp:18-91) */
+            ygzo_se3 old = T;
+            for (it = 0; it < n_iter; ++it) {
+                memset(H, 0, sizeof(H));
+                memset(Jres, 0, sizeof(Jres));
+                n_meas = 0;
+                const float chi2 = align_residuals(cimg, cw, chh, scale, cam, xyz_ref, vis, patch, jac, n, &T, 1,
+                                                   &n_meas, H, Jres);
+                const float new_chi2 = chi2 / (float)n_meas;
+                /* solve (SparseImageAlign.cc:233-238) */
+                ldlt_solve6(H, Jres, x);
+                if (isnan(x[0])) stop = 1;
+                if ((it > 0 && new_chi2 > 1.2 * chi2_) || stop) {
+                    T = old; /* rollback */
+                    break;
                 }
+                ygzo_se3 Tn;
+                align_update(&T, x, &Tn);
+                old = T;
+                T = Tn;
+                chi2_ = new_chi2;
+                if (norm_max6(x) <= 0.000001f) { it++; break; }
             }
-            const float new_chi2 = chi2 / (float)n_meas;
-            /* solve (SparseImageAlign.cc:233-238) */
-            ldlt_solve6(H, Jres, x);
-            if (isnan(x[0])) stop = 1;
-            if ((it > 0 && new_chi2 > 1.2 * chi2_) || stop) {
-                T = old; /* rollback */
-                break;
+        } else {
+            /* optimizeLevenbergMarquardt (NLSSolver_impl.hpp:95-212); SparseImgAlign::run sets
+             * mu_ = 0.1 per level (SparseImageAlign.cc:40), eps_ = 1e-6 (:17).  The level's first
+             * computeResiduals neither clears H_ nor n_meas_: chi2_ divides by the count carried
+             * over from the previous call plus this one. */
+            mu = 0.1f;
+            float Hacc[36], Jacc[6];
+            memcpy(Hacc, H, sizeof(H));
+            memset(Jacc, 0, sizeof(Jacc));
+            chi2_ = align_residuals(cimg, cw, chh, scale, cam, xyz_ref, vis, patch, jac, n, &T, 1, &n_meas, Hacc,
+                                    Jacc) / (float)n_meas;
+            for (it = 0; it < n_iter; ++it) {
+                float rho = 0.f;
+                int n_trials = 0;
+                do {
+                    ygzo_se3 Tn = T;
+                    float new_chi2 = -1.f;
+                    memset(H, 0, sizeof(H));
+                    memset(Jres, 0, sizeof(Jres));
+                    n_meas = 0;
+                    (void)align_residuals(cimg, cw, chh, scale, cam, xyz_ref, vis, patch, jac, n, &T, 1, &n_meas, H,
+                                          Jres);
+                    for (int k = 0; k < 6; k++) H[k * 6 + k] += H[k * 6 + k] * mu; /* damping (:146) */
+                    ldlt_solve6(H, Jres, x);
+                    if (!isnan(x[0])) {
+                        align_update(&T, x, &Tn);
+                        n_meas = 0;
+                        float Hd[36], Jd[6];
+                        new_chi2 = align_residuals(cimg, cw, chh, scale, cam, xyz_ref, vis, patch, jac, n, &Tn, 0,
+                                                   &n_meas, Hd, Jd) / (float)n_meas;
+                        rho = chi2_ - new_chi2;
+                    } else {
+                        rho = -1.f; /* singular */
+                    }
+                    if (rho > 0) {
+                        T = Tn;
+                        chi2_ = new_chi2;
+                        stop = norm_max6(x) <= 0.000001f;
+                        const double r3 = pow(2 * rho - 1, 3);
+                        const double f = fmax(1. / 3., fmin(1. - r3, 2. / 3.));
+                        mu = (float)((double)mu * f);
+                        nu = 2.f;
+                    } else {
+                        mu *= nu;
+                        nu *= 2.f;
+                        ++n_trials;
+                        if (n_trials >= 5) stop = 1; /* n_trials_max_ (NLSSolver.h:133) */
+                    }
+                } while (!(rho > 0 || stop));
+                if (stop) { it++; break; }
             }
-            /* update (SparseImageAlign.cc:240-244): T <- T * exp(-x) */
-            float mx[6];
-            for (int k = 0; k < 6; k++) mx[k] = -x[k];
-            ygzo_se3 E, Tn;
-            ygzo_se3_exp(mx, &E);
-            ygzo_se3_mul(&T, &E, &Tn);
-            old = T;
-            T = Tn;
-            chi2_ = new_chi2;
-            float nm = -1.f;
-            for (int k = 0; k < 6; k++) if (fabsf(x[k]) > nm) nm = fabsf(x[k]);
-            if (nm <= 0.000001f) { it++; break; }
         }
         if (level < YGZO_MAX_LEVELS) out->iters[level] = it;
     }
@@ -311,6 +387,14 @@ int ygzo_sparse_align(uint8_t **ref_levels, uint8_t **cur_levels, const int *lw,
     memcpy(out->H, H, sizeof(H));
     free(patch); free(jac); free(vis);
     return out->n_visible;
+}
+
+int ygzo_sparse_align(uint8_t **ref_levels, uint8_t **cur_levels, const int *lw, const int *lh,
+                      const float *inv_scale, const ygzo_cam *cam, const ygzo_kp *kps,
+                      const float *xyz_ref, const uint8_t *usable, int n, int max_level,
+                      int min_level, const ygzo_se3 *T_init, ygzo_align_out *out) {
+    return ygzo_sparse_align_method(ref_levels, cur_levels, lw, lh, inv_scale, cam, kps, xyz_ref, usable, n,
+                                    max_level, min_level, T_init, YGZO_ALIGN_GN, out);
 }
 
 /* ---------------- Align2D (Align.cc:8-105) ---------------- */

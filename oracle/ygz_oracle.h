@@ -187,7 +187,7 @@ typedef struct ygzo_align_out {
     int n_visible;         /* n_meas_/16 of the last computeResiduals */
     float chi2;            /* chi2_ at exit */
     int iters[YGZO_MAX_LEVELS];
-    float H[36];           /* H_ of the last linearisation */
+    float H[36];           /* H_ of the last linearisation (LM: damped, as the last trial left it) */
 } ygzo_align_out;
 /* SparseImgAlign::run (SparseImageAlign.cc:20-49).  Features i = 0..n-1 are the
  * reference frame's keypoints (level-0 px) with usable[i] != 0 when the
@@ -196,6 +196,13 @@ int ygzo_sparse_align(uint8_t **ref_levels, uint8_t **cur_levels, const int *lw,
                       const float *inv_scale, const ygzo_cam *cam, const ygzo_kp *kps,
                       const float *xyz_ref, const uint8_t *usable, int n, int max_level,
                       int min_level, const ygzo_se3 *T_init, ygzo_align_out *out);
+/* The same with NLLSSolver's method (NLSSolver_impl.hpp:8-13): YGZO_ALIGN_GN =
+ * optimizeGaussNewton (:18-91), YGZO_ALIGN_LM = optimizeLevenbergMarquardt (:95-212). */
+enum { YGZO_ALIGN_GN = 0, YGZO_ALIGN_LM = 1 };
+int ygzo_sparse_align_method(uint8_t **ref_levels, uint8_t **cur_levels, const int *lw, const int *lh,
+                             const float *inv_scale, const ygzo_cam *cam, const ygzo_kp *kps,
+                             const float *xyz_ref, const uint8_t *usable, int n, int max_level,
+                             int min_level, const ygzo_se3 *T_init, int method, ygzo_align_out *out);
 void ygzo_se3_mul(const ygzo_se3 *a, const ygzo_se3 *b, ygzo_se3 *out);
 void ygzo_se3_exp(const float x[6], ygzo_se3 *out);
 void ygzo_se3_act(const ygzo_se3 *T, const float p[3], float out[3]);

@@ -474,6 +474,131 @@ __device__ __forceinline__ void jacob_xyz2cam_ff(float X, float Y, float Z, floa
     fj[10] = -fj[3]; fj[11] = -X * z_inv;
 }
 
+// ---- Levenberg-Marquardt (NLLSSolver::optimizeLevenbergMarquardt,
+// NLSSolver_impl.hpp:95-212), the method a SparseImgAlign constructed with
+// LevenbergMarquardt runs.  Every residual pass (all features at one pose) feeds
+// lm_round, which plays the reference's loop forward to the next pose whose chi2 it
+// needs:
+//  * the level's first pass is the reference's chi2_ = computeResiduals(model, true)
+//    (:104-105; n_meas_ not cleared, so chi2_ divides by the previous count plus this
+//    one) and, at the same pose, the first trial's linearisation (:137-141);
+//  * a trial damps H (H_ii += H_ii mu, :146), solves (the pivoted LDLT), and asks for
+//    the chi2 at T exp(-x) (:154-156); a singular H fails the trial without a pass;
+//  * an evaluation pass decides the trial (rho = chi2_ - new_chi2, :157): success
+//    updates T, chi2_, stop = |x|max <= eps, mu, nu (:166-170) and ends the iteration;
+//    the next iteration's linearisation is at the same pose, so it is this pass; a
+//    failure raises mu (mu *= nu, nu *= 2, :184-190) and retries on the cached
+//    linearisation, or stops after 5 trials.
+// The level ends when stop is set or after 10 iterations (SparseImageAlign.cc:38-44;
+// stop_ persists across levels: a later level then runs one trial).  mu_ starts at
+// 0.01 per run (reset(), NLSSolver.h:126) and is set to 0.1 per level (:40).
+struct LmState {
+    SE3 T, Te;           // the model; the pose of the next residual pass
+    float mu, nu, chi2;  // mu_, nu_, chi2_
+    float x[6];
+    float Hc[21], Jc[6];  // the linearisation at T (upper H row-major, Jres)
+    int ncl;              // its measurement count
+    float H[36];          // H_ as the last trial left it (damped): getFisherInformation
+    int nmeas;            // n_meas_ of the last computeResiduals
+    int stop, iter, n_trials, brk, rounds;
+};
+constexpr int kLmMaxRounds = 64;  // a level needs <= 1 + 10 x 5 passes
+
+__device__ __forceinline__ void lm_init(LmState &L, const ygzfe_se3 &T0) {
+    for (int i = 0; i < 4; i++) L.T.q[i] = T0.q[i];
+    for (int i = 0; i < 3; i++) L.T.t[i] = T0.t[i];
+    L.Te = L.T;
+    L.mu = 0.01f;
+    L.nu = 2.f;
+    L.chi2 = 1e10f;
+    L.stop = 0;
+    L.nmeas = 0;
+    for (int i = 0; i < 36; i++) L.H[i] = 0.f;
+}
+
+__device__ __forceinline__ void lm_level_start(LmState &L) {
+    L.mu = 0.1f;
+    L.iter = 0;
+    L.brk = 0;
+    L.rounds = 0;
+    L.Te = L.T;
+}
+
+// trials on the cached linearisation until one needs an evaluation pass (L.Te) or the
+// level's loop ends (L.brk)
+__device__ void lm_trials(LmState &L) {
+    for (;;) {
+        L.nmeas = L.ncl;  // the trial's computeResiduals(model, true)
+        float Hd[36], b[6], x[6];
+        for (int r = 0, m = 0; r < 6; r++)
+            for (int c = r; c < 6; c++, m++) { Hd[r * 6 + c] = L.Hc[m]; Hd[c * 6 + r] = L.Hc[m]; }
+        for (int k = 0; k < 6; k++) Hd[k * 6 + k] += Hd[k * 6 + k] * L.mu;
+        for (int k = 0; k < 6; k++) b[k] = L.Jc[k];
+        for (int i = 0; i < 36; i++) L.H[i] = Hd[i];
+        ldlt_solve6_reg(Hd, b, x);
+        if (!isnan(x[0])) {
+            for (int k = 0; k < 6; k++) L.x[k] = x[k];
+            float mx[6];
+            for (int k = 0; k < 6; k++) mx[k] = -x[k];
+            SE3 E;
+            se3_exp(mx, E);
+            se3_mul(L.T, E, L.Te);
+            return;
+        }
+        // singular: rho = -1, a failed trial
+        L.mu *= L.nu;
+        L.nu *= 2.f;
+        if (++L.n_trials >= 5) L.stop = 1;
+        if (L.stop) { L.brk = 1; return; }
+    }
+}
+
+// one residual pass at L.Te: H (upper, 21), Jres, chi2 sum and count
+__device__ void lm_round(LmState &L, const float H[21], const float b[6], float chi2sum, int cnt, bool level_first) {
+    if (++L.rounds >= kLmMaxRounds) { L.brk = 1; return; }
+    if (level_first) {
+        L.chi2 = chi2sum / (float)(L.nmeas + cnt);
+    } else {
+        L.nmeas = cnt;
+        const float new_chi2 = chi2sum / (float)cnt;
+        const float rho = L.chi2 - new_chi2;
+        if (rho > 0) {
+            L.T = L.Te;
+            L.chi2 = new_chi2;
+            float nm = -1.f;
+            for (int k = 0; k < 6; k++) nm = fabsf(L.x[k]) > nm ? fabsf(L.x[k]) : nm;
+            L.stop = nm <= 0.000001f;
+            const double t = 2.0 * (double)rho - 1.0;  // (2 rho - 1)^3 in double (pow(.., 3))
+            L.mu = (float)((double)L.mu * fmax(1. / 3., fmin(1. - t * t * t, 2. / 3.)));
+            L.nu = 2.f;
+            if (L.stop || ++L.iter >= 10) { L.brk = 1; return; }
+        } else {
+            L.mu *= L.nu;
+            L.nu *= 2.f;
+            if (++L.n_trials >= 5) L.stop = 1;
+            if (L.stop) { L.brk = 1; return; }
+            lm_trials(L);  // retry on the cached linearisation
+            return;
+        }
+    }
+    // a new iteration: linearised at T (= the pose of this pass)
+    for (int k = 0; k < 21; k++) L.Hc[k] = H[k];
+    for (int k = 0; k < 6; k++) L.Jc[k] = b[k];
+    L.ncl = cnt;
+    L.n_trials = 0;
+    lm_trials(L);
+}
+
+__device__ __forceinline__ void lm_result(const LmState &L, ygzfe_align_result *out) {
+    ygzfe_align_result r;
+    for (int i = 0; i < 4; i++) r.T_cur_ref.q[i] = L.T.q[i];
+    for (int i = 0; i < 3; i++) r.T_cur_ref.t[i] = L.T.t[i];
+    r.n_visible = L.nmeas / kPA;
+    r.chi2 = L.chi2;
+    for (int i = 0; i < 36; i++) r.H[i] = L.H[i];
+    *out = r;
+}
+
 // Generic path (any n): (feature, pixel) terms strided over the workgroup,
 // ref patches and Jacobians cached in a global scratch slab per job.
 template <int NT>
@@ -512,11 +637,51 @@ __device__ __attribute__((noinline)) void sparse_align_generic(const AlignLevels
         return;
     }
     const int border = 3;
+    __shared__ LmState s_lm_store;
+    LmState *s_lm = &s_lm_store;
+    if (job.method == 1 && tid == 0) lm_init(*s_lm, job.T_init);
     for (int level = job.max_level; level >= job.min_level; level--) {
         const int W = lv.w[level], H = lv.h[level];
         const float scale = lv.inv_scale[level];
         const uint8_t *rimg = job.ref_pyr + lv.off[level];
         const uint8_t *cimg = job.cur_pyr + lv.off[level];
+        // computeResiduals (SparseImageAlign.cc:130-231) at T: the wave sums of the 21 H
+        // terms, Jres, chi2 and the count into s_red (then a barrier)
+        auto generic_pass = [&](const SE3 T) {
+            float acc[kRed];
+            for (int k = 0; k < kRed; k++) acc[k] = 0.f;
+            for (int e = tid; e < n * kPA; e += NT) {
+                const int i = e >> 4, pc = e & 15;
+                if (vis[i] == 0.f) continue;
+                float pc3[3];
+                se3_act(T, job.xyz + 3 * i, pc3);
+                const float u = (cam.fx * pc3[0] / pc3[2] + cam.cx) * scale;
+                const float v = (cam.fy * pc3[1] / pc3[2] + cam.cy) * scale;
+                const int ui = (int)floorf(u), vi = (int)floorf(v);
+                if (ui < 0 || vi < 0 || ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H)
+                    continue;
+                const float su = u - ui, sv = v - vi;
+                const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
+                const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
+                const int py = pc >> 2, px = pc & 3;
+                const uint8_t *p = cimg + (size_t)(vi + py - 2) * W + (ui + px - 2);
+                const float ic = wtl * p[0] + wtr * p[1] + wbl * p[W] + wbr * p[W + 1];
+                const float res = ic - patch[e];
+                const float *J = jac + (size_t)e * 6;
+                float j[6];
+                for (int k = 0; k < 6; k++) j[k] = J[k];
+                int m = 0;
+                for (int r = 0; r < 6; r++)
+                    for (int c = r; c < 6; c++) acc[m++] += j[r] * j[c];
+                for (int r = 0; r < 6; r++) acc[21 + r] -= j[r] * res;
+                acc[27] += res * res;
+                acc[28] += 1.f;
+            }
+            for (int k = 0; k < kRed; k++) acc[k] = wave_sum_f(acc[k]);
+            if (lane == 0)
+                for (int k = 0; k < kRed; k++) s_red[wave][k] = acc[k];
+            __syncthreads();
+        };
         // precomputeReferencePatches: (feature, pixel) per thread
         for (int e = tid; e < n * kPA; e += NT) {
             const int i = e >> 4, pc = e & 15;
@@ -552,43 +717,30 @@ __device__ __attribute__((noinline)) void sparse_align_generic(const AlignLevels
             const float fs = cam.fx * scale;
             for (int k = 0; k < 6; k++) J[k] = (dx * fj[k] + dy * fj[6 + k]) * fs;
         }
+        if (job.method == 1) {  // Levenberg-Marquardt (lm_round): a residual pass per round
+            if (tid == 0) lm_level_start(*s_lm);
+            __syncthreads();
+            for (int round = 0;; round++) {
+                generic_pass(s_lm->Te);
+                if (tid == 0) {
+                    float r[kRed];
+                    for (int k = 0; k < kRed; k++) {
+                        float a = 0.f;
+                        for (int w = 0; w < NW; w++) a += s_red[w][k];
+                        r[k] = a;
+                    }
+                    lm_round(*s_lm, r, r + 21, r[27], (int)r[28], round == 0);
+                }
+                __syncthreads();
+                if (s_lm->brk) break;
+            }
+            __syncthreads();
+            continue;
+        }
         if (tid == 0) s_old = s_T;
         __syncthreads();
         for (int it = 0; it < 10; it++) {
-            const SE3 T = s_T;
-            float acc[kRed];
-            for (int k = 0; k < kRed; k++) acc[k] = 0.f;
-            for (int e = tid; e < n * kPA; e += NT) {
-                const int i = e >> 4, pc = e & 15;
-                if (vis[i] == 0.f) continue;
-                float pc3[3];
-                se3_act(T, job.xyz + 3 * i, pc3);
-                const float u = (cam.fx * pc3[0] / pc3[2] + cam.cx) * scale;
-                const float v = (cam.fy * pc3[1] / pc3[2] + cam.cy) * scale;
-                const int ui = (int)floorf(u), vi = (int)floorf(v);
-                if (ui < 0 || vi < 0 || ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H)
-                    continue;
-                const float su = u - ui, sv = v - vi;
-                const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
-                const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
-                const int py = pc >> 2, px = pc & 3;
-                const uint8_t *p = cimg + (size_t)(vi + py - 2) * W + (ui + px - 2);
-                const float ic = wtl * p[0] + wtr * p[1] + wbl * p[W] + wbr * p[W + 1];
-                const float res = ic - patch[e];
-                const float *J = jac + (size_t)e * 6;
-                float j[6];
-                for (int k = 0; k < 6; k++) j[k] = J[k];
-                int m = 0;
-                for (int r = 0; r < 6; r++)
-                    for (int c = r; c < 6; c++) acc[m++] += j[r] * j[c];
-                for (int r = 0; r < 6; r++) acc[21 + r] -= j[r] * res;
-                acc[27] += res * res;
-                acc[28] += 1.f;
-            }
-            for (int k = 0; k < kRed; k++) acc[k] = wave_sum_f(acc[k]);
-            if (lane == 0)
-                for (int k = 0; k < kRed; k++) s_red[wave][k] = acc[k];
-            __syncthreads();
+            generic_pass(s_T);
             if (tid == 0) {
                 float r[kRed];
                 for (int k = 0; k < kRed; k++) {
@@ -631,6 +783,10 @@ __device__ __attribute__((noinline)) void sparse_align_generic(const AlignLevels
         __syncthreads();
     }
     if (tid == 0) {
+        if (job.method == 1) {
+            lm_result(*s_lm, outp);
+            return;
+        }
         ygzfe_align_result r;
         for (int i = 0; i < 4; i++) r.T_cur_ref.q[i] = s_T.q[i];
         for (int i = 0; i < 3; i++) r.T_cur_ref.t[i] = s_T.t[i];
@@ -796,6 +952,30 @@ template <int NW>
 __device__ __forceinline__ void align_level_inverse(AlignPairLds<NW> &P, int lane) {
     const float hv = (lane >= 8 && lane < 29) ? P.Hvis[lane - 8] : 0.f;
     ldlt6_inverse_cols(hv, lane, P.M);
+}
+
+// the solver wave's view of a residual pass: lane k (< 8) of *pk8 holds value k's
+// total (Jres[6], chi2, count); lanes 8 + hpack6(i, j) of *hr hold H(i, j) = H_vis less
+// the out-of-bounds features' H_f when the pass saw any (tag gi)
+template <int NW>
+__device__ __forceinline__ void align_solver_reduce(AlignPairLds<NW> &P, int gi, int lane, float &pk8, float &hr) {
+    {
+        const int k8 = lane & 7, w1 = 2 * (lane >> 3) + 1, w2 = w1 + 1;
+        pk8 = (w1 < NW ? P.part[w1][k8] : 0.f) + (w2 < NW ? P.part[w2][k8] : 0.f);
+        pk8 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(pk8), 0x128, 0xF, 0xF, false));
+        pk8 = pair_pl16(pk8, pk8);
+        pk8 = pair_pl32(pk8, pk8);
+    }
+    hr = 0.f;
+    if (lane >= 8 && lane < 29) {
+        const int k = lane - 8;
+        float o = 0.f;
+        if (P.out_it == gi) {
+#pragma unroll
+            for (int w = 1; w < NW; w++) o += P.opart[w][k];
+        }
+        hr = P.Hvis[k] - o;
+    }
 }
 
 // one Gauss-Newton step, solver wave (NLSSolver_impl.hpp:18-91): reduce the
@@ -1095,7 +1275,7 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const Al
 // (Two pairs per workgroup, ping-ponging the solver wave, was measured at 0.62 ms per
 // 1023 pairs against 0.39: the second pair's 40 feature registers spill at 1024
 // threads -- profiles/r04_align_pingpong.txt.)
-template <int NT>
+template <int NT, int METHOD>
 __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_camera cam,
                                                          const AlignJob *__restrict__ jobs,
                                                          float *__restrict__ scratch, size_t scratch_per_job,
@@ -1107,6 +1287,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
         return;
     }
     __shared__ AlignPairLds<NW> P;
+    __shared__ LmState s_lm[METHOD == 1 ? 1 : 1];  // read by METHOD 1 (Levenberg-Marquardt) only
     __shared__ float s_part_next[NW][32];  // the next level's H partials
     __shared__ float s_patch[2][16][NF];   // ref_patch_cache_ of the owned features, this level / the next
     const AlignJob &job = jobs[blockIdx.x];
@@ -1114,6 +1295,48 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
     if (tid == 0) align_pair_init(P, job);
     __syncthreads();
     YGZ_STAMP(9);
+    if (METHOD == 1 && wave == 0) {  // Levenberg-Marquardt: lm_round decides each pass's pose
+        if (lane == 0) lm_init(s_lm[0], job.T_init);
+        int gi = 0;
+        for (int level = job.max_level; level >= job.min_level; level--, gi += kLmMaxRounds) {
+            __syncthreads();  // L0: the level's H partials are in
+            if (level == job.max_level) {
+                align_sum_hvis(P, lane);
+            } else if (lane < 21) {
+                float r = 0.f;
+                for (int w = 1; w < NW; w++) r += s_part_next[w][lane];
+                P.Hvis[lane] = r;
+            }
+            if (lane == 0) {
+                lm_level_start(s_lm[0]);
+                P.T = s_lm[0].T;  // the level's first pass is at the model
+                P.brk = 0;
+            }
+            __syncthreads();  // L0b
+            for (int round = 0;; round++) {
+                __syncthreads();  // A
+                float pk8, hr;
+                align_solver_reduce(P, gi + round, lane, pk8, hr);
+                float Hu[21], b[6];
+#pragma unroll
+                for (int k = 0; k < 21; k++) Hu[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hr), 8 + k));
+#pragma unroll
+                for (int k = 0; k < 6; k++) b[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pk8), k));
+                const float chi2sum = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pk8), 6));
+                const int cnt = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(pk8), 7));
+                if (lane == 0) {
+                    lm_round(s_lm[0], Hu, b, chi2sum, cnt, round == 0);
+                    P.T = s_lm[0].Te;
+                    P.brk = s_lm[0].brk;
+                }
+                __syncthreads();  // B
+                if (P.brk) break;
+            }
+            __syncthreads();  // L1
+        }
+        if (tid == 0) lm_result(s_lm[0], out + blockIdx.x);
+        return;
+    }
     if (wave == 0) {
         for (int level = job.max_level; level >= job.min_level; level--) {
             if (tid == 0) P.old = P.T;
@@ -1150,6 +1373,33 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
 #pragma unroll
     for (int p = 0; p < 16; p++) { s_patch[0][p][f] = 0.f; s_patch[1][p][f] = 0.f; }
     int cb = 0;  // the level's half of the patch cache
+    if (METHOD == 1) {  // Levenberg-Marquardt: a residual pass per round at the published pose
+        int gi = 0;
+        for (int level = job.max_level; level >= job.min_level; level--, gi += kLmMaxRounds) {
+            if (level == job.max_level) {
+                align_feat_precompute<NF, NW>(F, false, D, lv, cam, job.ref_pyr, level, s_patch[cb], s_patch[cb], f,
+                                              P.part, wave, lane);
+            } else {
+                D = Dn;
+                cb ^= 1;
+            }
+            __syncthreads();  // L0
+            __syncthreads();  // L0b
+            for (int round = 0;; round++) {
+                const SE3 T = P.T;
+                align_feat_residual<NF, NW>(F, D, T, lv, cam, job.cur_pyr, level, s_patch[cb], f, P.part, P.opart,
+                                            &P.out_it, gi + round, wave, lane);
+                __syncthreads();  // A
+                if (round == 0 && level > job.min_level)
+                    align_feat_precompute<NF, NW>(F, D.vis, Dn, lv, cam, job.ref_pyr, level - 1, s_patch[cb ^ 1],
+                                                  s_patch[cb], f, s_part_next, wave, lane);
+                __syncthreads();  // B
+                if (P.brk) break;
+            }
+            __syncthreads();  // L1
+        }
+        return;
+    }
     for (int level = job.max_level; level >= job.min_level; level--) {
         if (level == job.max_level) {
             align_feat_precompute<NF, NW>(F, false, D, lv, cam, job.ref_pyr, level, s_patch[cb], s_patch[cb], f,
@@ -1179,11 +1429,15 @@ int sparse_align_reg_capacity() { return 1024 - 64; }  // one feature per thread
 
 hipError_t launch_sparse_align(const AlignLevels &lv, const ygzfe_camera &cam, const AlignJob *jobs, int njobs,
                                float *scratch, size_t scratch_per_job, ygzfe_align_result *out, hipStream_t st,
-                               int max_n) {
+                               int max_n, int method) {
     if (njobs <= 0) return hipSuccess;
     (void)max_n;
-    hipLaunchKernelGGL(k_sparse_align_reg<1024>, dim3(njobs), dim3(1024), 0, st, lv, cam, jobs, scratch,
-                       scratch_per_job, out);
+    if (method == 1)
+        hipLaunchKernelGGL((k_sparse_align_reg<1024, 1>), dim3(njobs), dim3(1024), 0, st, lv, cam, jobs, scratch,
+                           scratch_per_job, out);
+    else
+        hipLaunchKernelGGL((k_sparse_align_reg<1024, 0>), dim3(njobs), dim3(1024), 0, st, lv, cam, jobs, scratch,
+                           scratch_per_job, out);
     return hipGetLastError();
 }
 

@@ -1434,9 +1434,13 @@ static AlignLevels levels_of(const Plan &P) {
     return lv;
 }
 
-int ygzfe_sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam,
-                             const ygzfe_kp *kps, const float *xyz_ref, const uint8_t *usable, int n, int max_level,
-                             int min_level, const ygzfe_se3 *T_init) {
+static int sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam,
+                              const ygzfe_kp *kps, const float *xyz_ref, const uint8_t *usable, int n, int max_level,
+                              int min_level, const ygzfe_se3 *T_init, int method) {
+    if (method != YGZFE_ALIGN_GAUSS_NEWTON && method != YGZFE_ALIGN_LEVENBERG_MARQUARDT) {
+        set_error("unknown SparseImgAlign method %d", method);
+        return YGZFE_EINVAL;
+    }
     if (!ref || !cur || !cam || !T_init || n < 0 || (n > 0 && (!kps || !xyz_ref || !usable))) {
         set_error("invalid argument");
         return YGZFE_EINVAL;
@@ -1497,6 +1501,7 @@ int ygzfe_sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, con
     job.n = n;
     job.max_level = max_level;
     job.min_level = min_level;
+    job.method = method;
     job.T_init = *T_init;
     memcpy(hin, &job, sizeof(job));
     if (n == n_all) {
@@ -1516,7 +1521,8 @@ int ygzfe_sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, con
     }
     YGZ_HIP(hipMemcpyAsync(din, hin, in_bytes, hipMemcpyHostToDevice, st));
     YGZ_HIP(launch_sparse_align(levels_of(P), *cam, reinterpret_cast<const AlignJob *>(din), 1,
-                                ex->align_scratch.as<float>(), spj, ex->align_out.as<ygzfe_align_result>(), st, n));
+                                ex->align_scratch.as<float>(), spj, ex->align_out.as<ygzfe_align_result>(), st, n,
+                                method));
     YGZ_HIP(hipMemcpyAsync(ex->ahout.p, ex->align_out.p, sizeof(ygzfe_align_result), hipMemcpyDeviceToHost, st));
     YGZ_HIP(hipEventRecord(ex->ev_align_done, st));
     ex->align_pending = true;
@@ -1543,11 +1549,25 @@ int ygzfe_sparse_align_end(const ygzfe_frame *cur, ygzfe_align_result *result) {
     return YGZFE_OK;
 }
 
+int ygzfe_sparse_align_begin(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam,
+                             const ygzfe_kp *kps, const float *xyz_ref, const uint8_t *usable, int n, int max_level,
+                             int min_level, const ygzfe_se3 *T_init) {
+    return sparse_align_begin(ref, cur, cam, kps, xyz_ref, usable, n, max_level, min_level, T_init,
+                              YGZFE_ALIGN_GAUSS_NEWTON);
+}
+
 int ygzfe_sparse_align(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam, const ygzfe_kp *kps,
                        const float *xyz_ref, const uint8_t *usable, int n, int max_level, int min_level,
                        const ygzfe_se3 *T_init, ygzfe_align_result *result) {
+    return ygzfe_sparse_align_method(ref, cur, cam, kps, xyz_ref, usable, n, max_level, min_level, T_init,
+                                     YGZFE_ALIGN_GAUSS_NEWTON, result);
+}
+
+int ygzfe_sparse_align_method(const ygzfe_frame *ref, const ygzfe_frame *cur, const ygzfe_camera *cam,
+                              const ygzfe_kp *kps, const float *xyz_ref, const uint8_t *usable, int n, int max_level,
+                              int min_level, const ygzfe_se3 *T_init, int method, ygzfe_align_result *result) {
     if (!result) { set_error("invalid argument"); return YGZFE_EINVAL; }
-    YGZ_TRY(ygzfe_sparse_align_begin(ref, cur, cam, kps, xyz_ref, usable, n, max_level, min_level, T_init));
+    YGZ_TRY(sparse_align_begin(ref, cur, cam, kps, xyz_ref, usable, n, max_level, min_level, T_init, method));
     return ygzfe_sparse_align_end(cur, result);
 }
 
@@ -1570,6 +1590,7 @@ __global__ void k_build_align_jobs(AlignJob *jobs, int n_pairs, const int32_t *r
     j.n = counts[r];
     j.max_level = max_level;
     j.min_level = min_level;
+    j.method = 0;
     j.T_init = T_init[p];
     jobs[p] = j;
 }

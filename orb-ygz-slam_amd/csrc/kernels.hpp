@@ -105,11 +105,13 @@ struct AlignJob {
     const uint8_t *usable;
     int n;
     int max_level, min_level;
+    int method;  // NLLSSolver's method (NLSSolver_impl.hpp:8-13): 0 Gauss-Newton, 1 Levenberg-Marquardt
     ygzfe_se3 T_init;
 };
+// method: 0 Gauss-Newton (every job's method must be 0), 1 Levenberg-Marquardt (every job's 1)
 hipError_t launch_sparse_align(const AlignLevels &lv, const ygzfe_camera &cam, const AlignJob *jobs,
                                int njobs, float *scratch, size_t scratch_per_job, ygzfe_align_result *out,
-                               hipStream_t st, int max_n);
+                               hipStream_t st, int max_n, int method = 0);
 size_t sparse_align_scratch_floats(int n);
 int sparse_align_reg_capacity();  // features the register kernel holds (one per feature-wave thread)
 // stream placement probe (ensure_align_stream): a kernel that holds its stream for

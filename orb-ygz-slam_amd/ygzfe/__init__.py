@@ -473,18 +473,20 @@ def search_by_bow(kf, F, kf_usable, fv_kf, fv_f, nnratio=0.7, check_ori=False):
 
 
 class SparseImgAlign:
-    """SparseImgAlign(n_levels, min_level, n_iter=10) (SparseImageAlign.h:37-60)."""
+    """SparseImgAlign(n_levels, min_level, n_iter=10, method=GaussNewton) (SparseImageAlign.h:37-60)."""
+    GaussNewton, LevenbergMarquardt = 0, 1  # NLLSSolver's methods (NLSSolver.h:40-43)
 
-    def __init__(self, max_level, min_level, n_iter=10):
-        self.max_level, self.min_level = max_level, min_level
+    def __init__(self, max_level, min_level, n_iter=10, method=0):
+        self.max_level, self.min_level, self.method = max_level, min_level, int(method)
 
     def run(self, ref_frame, cur_frame, cam, kps, xyz_ref, usable, T_init):
         kps = np.ascontiguousarray(kps, KP_DTYPE)
         xyz = np.ascontiguousarray(xyz_ref, np.float32).reshape(-1, 3)
         us = np.ascontiguousarray(usable, np.uint8)
         res = AlignResult()
-        _check(lib().ygzfe_sparse_align(ref_frame.h, cur_frame.h, C.byref(cam), _p(kps), _p(xyz), _p(us), len(kps),
-                                        self.max_level, self.min_level, C.byref(T_init), C.byref(res)),
+        _check(lib().ygzfe_sparse_align_method(ref_frame.h, cur_frame.h, C.byref(cam), _p(kps), _p(xyz), _p(us),
+                                               len(kps), self.max_level, self.min_level, C.byref(T_init),
+                                               self.method, C.byref(res)),
                "sparse_align")
         return res
 

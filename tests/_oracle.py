@@ -284,8 +284,11 @@ def hamming_best2(q, t):
     return bi, bd, sd
 
 
+ALIGN_GN, ALIGN_LM = 0, 1  # NLLSSolver's methods (NLSSolver_impl.hpp:8-13)
+
+
 def sparse_align(ref_levels, cur_levels, inv_scale, cam, kps, xyz_ref, usable, max_level,
-                 min_level, T_init):
+                 min_level, T_init, method=ALIGN_GN):
     rp = (C.c_void_p * MAXL)(*[l.ctypes.data for l in ref_levels])
     cp = (C.c_void_p * MAXL)(*[l.ctypes.data for l in cur_levels])
     lw = (C.c_int * MAXL)(*[l.shape[1] for l in ref_levels])
@@ -295,8 +298,8 @@ def sparse_align(ref_levels, cur_levels, inv_scale, cam, kps, xyz_ref, usable, m
     xyz = np.ascontiguousarray(xyz_ref, np.float32)
     us = np.ascontiguousarray(usable, np.uint8)
     out = AlignOut()
-    lib().ygzo_sparse_align(rp, cp, lw, lh, inv, C.byref(cam), _p(kps), _p(xyz), _p(us), len(kps),
-                            max_level, min_level, C.byref(T_init), C.byref(out))
+    lib().ygzo_sparse_align_method(rp, cp, lw, lh, inv, C.byref(cam), _p(kps), _p(xyz), _p(us), len(kps),
+                                   max_level, min_level, C.byref(T_init), int(method), C.byref(out))
     return out
 
 

@@ -549,11 +549,22 @@ int main(int argc, char **argv) {
         CHECK(ret == (size_t)ao.n_visible && err <= 1e-4f && ret > 100,
               "mpAlign->run(&mLastFrame, &mCurrentFrame, TCR): visible %zu (oracle %d), |dT| %.2e, t (%.4f %.4f) "
               "expected ~(%.4f %.4f)", ret, ao.n_visible, err, TCR.translation()[0], TCR.translation()[1], tx, ty);
-        {  // NLSSolver_impl.hpp:8-13: the GPU runs only Gauss-Newton; LM is refused (returns 0)
+        {  // NLSSolver_impl.hpp:8-13: SparseImgAlign(.., LevenbergMarquardt) -> optimizeLevenbergMarquardt
             ygz::SparseImgAlign lm(nl - 1, 1, 10, ygz::SparseImgAlign::LevenbergMarquardt);
             SE3f Tlm;
-            CHECK(lm.run(&T.mLastFrame, &T.mCurrentFrame, Tlm) == 0,
-                  "SparseImgAlign(.., LevenbergMarquardt).run() refused (returns 0, logs once)");
+            const size_t vlm = lm.run(&T.mLastFrame, &T.mCurrentFrame, Tlm);
+            ygzo_align_out lo;
+            ygzo_sparse_align_method(rp, cp, lw, lh, o.inv_scale, &cam,
+                                     reinterpret_cast<const ygzo_kp *>(T.mLastFrame.mvKeys.data()), xyz.data(),
+                                     us.data(), T.mLastFrame.N, nl - 1, 1, &T0, YGZO_ALIGN_LM, &lo);
+            float el = 0.f;
+            const float lq[4] = {Tlm.unit_quaternion().x(), Tlm.unit_quaternion().y(), Tlm.unit_quaternion().z(),
+                                 Tlm.unit_quaternion().w()};
+            for (int k = 0; k < 4; k++) el = std::fmax(el, std::fabs(lq[k] - lo.T.q[k]));
+            for (int k = 0; k < 3; k++) el = std::fmax(el, std::fabs(Tlm.translation()[k] - lo.T.t[k]));
+            CHECK(vlm == (size_t)lo.n_visible && el <= 1e-4f && vlm > 100,
+                  "SparseImgAlign(.., LevenbergMarquardt).run(): visible %zu (oracle %d), |dT| %.2e", vlm,
+                  lo.n_visible, el);
         }
         const auto I = T.mpAlign->getFisherInformation();
         CHECK(std::fabs(I(0, 0) - ao.H[0] / (float)(5e-4 * 255 * 255)) <= 1e-3f * std::fabs(I(0, 0)) + 1e-3f,

@@ -13,9 +13,10 @@ pytestmark = pytest.mark.gpu
 POSE_TOL = 1e-4
 
 
-def align_case(gpu, seed, n_usable_frac=1.0, max_level=3, min_level=1, motion_scale=1.0):
+def align_case(gpu, seed, n_usable_frac=1.0, max_level=3, min_level=1, motion_scale=1.0, method=0, nfeatures=None):
     sc = S.PlaneScene(seed)
     W, H, nf, sf, nl, ini, mn = S.CONFIGS["C2"]
+    nf = nfeatures or nf
     ex = gpu.ORBextractor(nf, sf, nl, ini, mn)
     orc = O.OrbOracle(nf, sf, nl, ini, mn)
     # reference camera at a generic pose, current = ref moved by the true motion
@@ -34,11 +35,11 @@ def align_case(gpu, seed, n_usable_frac=1.0, max_level=3, min_level=1, motion_sc
     usable = (ok.astype(bool) & (rng.random(len(kps)) < n_usable_frac)).astype(np.uint8)
     T0 = gpu.SE3.make()
     cam = sc.camera()
-    res = gpu.SparseImgAlign(max_level, min_level).run(fr_ref, fr_cur, cam, kps, xyz, usable, T0)
+    res = gpu.SparseImgAlign(max_level, min_level, method=method).run(fr_ref, fr_cur, cam, kps, xyz, usable, T0)
     ocam = O.Cam(*sc.cam)
     oT0 = O.se3_from((0, 0, 0, 1), (0, 0, 0))
     ores = O.sparse_align(orc.pyramid(f_ref), orc.pyramid(f_cur), orc.inv_scale, ocam, kps, xyz, usable, max_level,
-                          min_level, oT0)
+                          min_level, oT0, method=method)
     true_q, true_t = q_d, v
     return res, ores, (true_q, true_t)
 
