@@ -464,24 +464,26 @@ int ygzo_extract_dso(ygzo_orb *o, uint8_t **levels, const int *lw, const int *lh
     int nn = ygzo_dso_single_level(o, levels, lw, lh, existing, n_existing, nk, capn);
     int total = n_existing + nn;
     if (total > cap) { free(nk); return -1; }
+    /* GaussianBlur of every level once (ORBextractor.cc:1079-1084), then the existing rows'
+     * descriptors on their octave's blurred level (:1088-1099) and the new ones' on level 0 */
+    uint8_t *blur[YGZO_MAX_LEVELS];
+    for (int l = 0; l < o->nlevels; l++) {
+        blur[l] = (uint8_t *)malloc((size_t)lw[l] * lh[l]);
+        ygzo_gaussian_blur7(levels[l], lw[l], lh[l], lw[l], blur[l], lw[l], o->blur_variant);
+    }
     for (int i = 0; i < n_existing; i++) {
         ygzo_kp t = existing[i];
         int oc = t.octave;
-        uint8_t *blur = (uint8_t *)malloc((size_t)lw[oc] * lh[oc]);
-        ygzo_gaussian_blur7(levels[oc], lw[oc], lh[oc], lw[oc], blur, lw[oc], o->blur_variant);
         t.x *= o->inv_scale[oc];
         t.y *= o->inv_scale[oc];
-        ygzo_orb_descriptor(blur, lw[oc], lh[oc], lw[oc], &t, out_desc + 32 * (size_t)i);
+        ygzo_orb_descriptor(blur[oc], lw[oc], lh[oc], lw[oc], &t, out_desc + 32 * (size_t)i);
         out_kps[i] = existing[i];
-        free(blur);
     }
-    uint8_t *blur0 = (uint8_t *)malloc((size_t)lw[0] * lh[0]);
-    ygzo_gaussian_blur7(levels[0], lw[0], lh[0], lw[0], blur0, lw[0], o->blur_variant);
     for (int i = 0; i < nn; i++) {
-        ygzo_orb_descriptor(blur0, lw[0], lh[0], lw[0], &nk[i], out_desc + 32 * (size_t)(n_existing + i));
+        ygzo_orb_descriptor(blur[0], lw[0], lh[0], lw[0], &nk[i], out_desc + 32 * (size_t)(n_existing + i));
         out_kps[n_existing + i] = nk[i];
     }
-    free(blur0);
+    for (int l = 0; l < o->nlevels; l++) free(blur[l]);
     free(nk);
     return total;
 }

@@ -2160,7 +2160,10 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
         // level 0 on the caller's stream, the others spread over the given side streams
         const hipStream_t st = (l == 0 || !lvl_streams || n_lvl_streams <= 0) ? st0
                                                                                 : lvl_streams[(l - 1) % n_lvl_streams];
-        const size_t lds = kFastWaves * (size_t)fast_slice_bytes(S, R);
+#ifndef YGZ_FAST_LDS_MIN
+#define YGZ_FAST_LDS_MIN 0  // experiment: workgroup LDS floor (caps FAST's occupancy, leaving slots to a concurrent stage)
+#endif
+        const size_t lds = std::max<size_t>(kFastWaves * (size_t)fast_slice_bytes(S, R), YGZ_FAST_LDS_MIN);
         const dim3 grid((L.ncells + kFastWaves - 1) / kFastWaves, nframes);
 #define YGZ_FAST(SS, RR)                                                                                        \
     if (S == SS && R == RR)                                                                                     \
