@@ -466,11 +466,7 @@ __device__ __forceinline__ float wmulf(float a, float b) { return a * b; }
 
 __device__ __forceinline__ void jacob_xyz2cam_ff(float X, float Y, float Z, float fj[12]) {
     asm volatile("" : "+v"(X), "+v"(Y), "+v"(Z));  // recomputed where used (see jacob_xyz2cam_fresh)
-#ifdef YGZ_ALIGN_RCP
-    const float z_inv = __builtin_amdgcn_rcpf(Z);
-#else
-    const float z_inv = 1.0f / Z;
-#endif
+    const float z_inv = __builtin_amdgcn_rcpf(Z);  // 1 ulp; pose parity is 1e-4 (tests/test_gpu_align.py)
     const float z_inv_2 = z_inv * z_inv;
     fj[0] = -z_inv; fj[1] = 0.f; fj[2] = X * z_inv_2; fj[3] = Y * fj[2];
     fj[4] = -(1.0f + X * fj[2]); fj[5] = Y * z_inv;
@@ -1203,11 +1199,7 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const Al
         const float P3[3] = {F.X, F.Y, F.Z};
         float pc3[3];
         se3_act(T, P3, pc3);
-#ifdef YGZ_ALIGN_RCP
         const float izc = __builtin_amdgcn_rcpf(pc3[2]);  // 1 ulp instead of the IEEE division's ~10 VALU
-#else
-        const float izc = 1.0f / pc3[2];
-#endif
         const float u = __builtin_fmaf(cam.fx * pc3[0], izc, cam.cx) * scale;
         const float v = __builtin_fmaf(cam.fy * pc3[1], izc, cam.cy) * scale;
         const int ui = (int)floorf(u), vi = (int)floorf(v);
