@@ -416,6 +416,27 @@ __device__ __forceinline__ void load_row(const uint8_t *p, float (&out)[N]) {
     }
 }
 
+// five bytes at byte offset `off` of a buffer as floats: one 8-byte buffer load from
+// the enclosing dword boundary (32-bit offsets: no 64-bit address arithmetic per row)
+__device__ __forceinline__ void load_row5_buf(__amdgpu_buffer_rsrc_t rs, uint32_t off, float (&out)[5]) {
+    const uint32_t sh = off & 3u;
+    const auto d = __builtin_amdgcn_raw_buffer_load_b64(rs, off - sh, 0, 0);
+    const uint32_t v0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+    const uint32_t v1 = __builtin_amdgcn_alignbyte(0u, d[1], sh);
+#pragma unroll
+    for (int b = 0; b < 4; b++) out[b] = (float)((v0 >> (8 * b)) & 0xFFu);
+    out[4] = (float)(v1 & 0xFFu);
+}
+
+// seven bytes at byte offset `off` of a buffer, packed: one 12-byte buffer load from the
+// enclosing dword boundary, realigned
+__device__ __forceinline__ void load_row7_packed_buf(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t (&out)[2]) {
+    const uint32_t sh = off & 3u;
+    const auto d = __builtin_amdgcn_raw_buffer_load_b96(rs, off - sh, 0, 0);
+    out[0] = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+    out[1] = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+}
+
 template <int N>
 __device__ __forceinline__ void load_row_packed(const uint8_t *p, uint32_t (&out)[(N + 3) / 4]) {
     const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
@@ -435,24 +456,6 @@ constexpr int kRed = 29;   // 21 (upper H) + 6 (Jres) + chi2 + count
 
 size_t sparse_align_scratch_floats(int n) { return (size_t)n * kPA * 7 + (size_t)n; }
 
-// JacobXYZ2Cam (SparseImageAlign.h:95-116): translation first, pre-negated.
-__device__ __forceinline__ void jacob_xyz2cam_f(float X, float Y, float Z, float fj[12]) {
-    const float z_inv = (float)(1. / (double)Z);
-    const float z_inv_2 = z_inv * z_inv;
-    fj[0] = -z_inv; fj[1] = 0.f; fj[2] = X * z_inv_2; fj[3] = Y * fj[2];
-    fj[4] = (float)(-(1.0 + (double)(X * fj[2]))); fj[5] = Y * z_inv;
-    fj[6] = 0.f; fj[7] = -z_inv; fj[8] = Y * z_inv_2; fj[9] = (float)(1.0 + (double)(Y * fj[8]));
-    fj[10] = -fj[3]; fj[11] = -X * z_inv;
-}
-
-// The Jacobian recomputed where it is used: without the opaque copy the
-// compiler hoists the 12 (loop-invariant) entries and their products out of
-// every level and iteration loop and spills them across the whole kernel.
-__device__ __forceinline__ void jacob_xyz2cam_fresh(float X, float Y, float Z, float fj[12]) {
-    asm volatile("" : "+v"(X), "+v"(Y), "+v"(Z));
-    jacob_xyz2cam_f(X, Y, Z, fj);
-}
-
 // Single-precision forms of the reference's mixed float/double expressions,
 // with identical results:
 //  * bilinear weights (1.0 - su) * (1.0 - sv) (SparseImageAlign.cc:84-87,
@@ -464,14 +467,49 @@ __device__ __forceinline__ void jacob_xyz2cam_fresh(float X, float Y, float Z, f
 //    or sum of floats equals the correctly rounded float operation.
 __device__ __forceinline__ float wmulf(float a, float b) { return a * b; }
 
+// JacobXYZ2Cam (SparseImageAlign.h:95-116): translation first, pre-negated.  Recomputed
+// where it is used: without the opaque copy the compiler hoists the 12 loop-invariant
+// entries and their products out of every level and iteration loop and spills them.
 __device__ __forceinline__ void jacob_xyz2cam_ff(float X, float Y, float Z, float fj[12]) {
-    asm volatile("" : "+v"(X), "+v"(Y), "+v"(Z));  // recomputed where used (see jacob_xyz2cam_fresh)
+    asm volatile("" : "+v"(X), "+v"(Y), "+v"(Z));
     const float z_inv = __builtin_amdgcn_rcpf(Z);  // 1 ulp; pose parity is 1e-4 (tests/test_gpu_align.py)
     const float z_inv_2 = z_inv * z_inv;
     fj[0] = -z_inv; fj[1] = 0.f; fj[2] = X * z_inv_2; fj[3] = Y * fj[2];
     fj[4] = -(1.0f + X * fj[2]); fj[5] = Y * z_inv;
     fj[6] = 0.f; fj[7] = -z_inv; fj[8] = Y * z_inv_2; fj[9] = 1.0f + Y * fj[8];
     fj[10] = -fj[3]; fj[11] = -X * z_inv;
+}
+
+// One feature's H_f = fs^2 J^T [Sxx Sxy; Sxy Syy] J for its 2x6 frame Jacobian J
+// (jacob_xyz2cam_ff: J[0][1] = J[1][0] = 0) as 21 upper-triangle entries, row-major:
+// A = fs^2 G J first, then H = J^T A, the structural zeros of J skipped (the sums of
+// SparseImageAlign.cc:121-125 regrouped: rounding-level, pose parity 1e-4)
+__device__ __forceinline__ void feat_hessian(float X, float Y, float Z, float Sxx, float Sxy, float Syy, float fs2,
+                                             float hv[21]) {
+#pragma clang fp contract(fast)
+    float fj[12];
+    jacob_xyz2cam_ff(X, Y, Z, fj);
+    const float gxx = Sxx * fs2, gxy = Sxy * fs2, gyy = Syy * fs2;
+    float A0[6], A1[6];
+    A0[0] = gxx * fj[0];
+    A1[0] = gxy * fj[0];
+    A0[1] = gxy * fj[7];
+    A1[1] = gyy * fj[7];
+#pragma unroll
+    for (int c = 2; c < 6; c++) {
+        A0[c] = gxx * fj[c] + gxy * fj[6 + c];
+        A1[c] = gxy * fj[c] + gyy * fj[6 + c];
+    }
+    int m = 0;
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int c = r; c < 6; c++) {
+            if (r == 0) hv[m] = fj[0] * A0[c];
+            else if (r == 1) hv[m] = fj[7] * A1[c];
+            else hv[m] = fj[r] * A0[c] + fj[6 + r] * A1[c];
+            m++;
+        }
 }
 
 // ---- Levenberg-Marquardt (NLLSSolver::optimizeLevenbergMarquardt,
@@ -812,15 +850,29 @@ __device__ __attribute__((noinline)) void sparse_align_generic(const AlignLevels
 // the level's moments Sxx, Sxy, Syy kept in registers and summed per wave, so LDS
 // holds only the reference patches (61 KB).
 #ifdef YGZ_STAMPS
-// diagnostic build only (lib/libygzfe_diag.so): solver-wave timestamps of block 0
+// diagnostic build only (lib/libygzfe_diag.so): block 0's timestamps, gathered in LDS
+// (an LDS atomic slot + s_memtime: ~100 cycles a stamp, against ~700 for a global
+// counter) and copied out by YGZ_STAMP_FLUSH at the solver wave's end
 __device__ unsigned long long g_stamps[4096];
 __device__ int g_nstamps;
-#define YGZ_STAMP(tag)                                                                   \
+__shared__ unsigned long long s_stamps[1536];
+__shared__ unsigned s_nstamps;
+#define YGZ_STAMP_AT(tag, who)                                                           \
     do {                                                                                 \
-        if (blockIdx.x == 0 && threadIdx.x == 0 && g_nstamps < 2047) {                   \
-            g_stamps[2 * g_nstamps] = (unsigned long long)(tag);                         \
-            g_stamps[2 * g_nstamps + 1] = __builtin_amdgcn_s_memtime();                  \
-            g_nstamps++;                                                                 \
+        if (blockIdx.x == 0 && (who)) {                                                  \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
+            const unsigned k_ = atomicAdd(&s_nstamps, 1u);                               \
+            if (k_ < 768) { s_stamps[2 * k_] = (unsigned long long)(tag); s_stamps[2 * k_ + 1] = t_; } \
+        }                                                                                \
+    } while (0)
+#define YGZ_STAMP(tag) YGZ_STAMP_AT(tag, threadIdx.x == 0)
+#define YGZ_STAMP_INIT() do { if (threadIdx.x == 0) s_nstamps = 0; } while (0)
+#define YGZ_STAMP_FLUSH()                                                                \
+    do {                                                                                 \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                                       \
+            const unsigned n_ = s_nstamps < 768 ? s_nstamps : 768;                       \
+            for (unsigned i_ = 0; i_ < 2 * n_; i_++) g_stamps[i_] = s_stamps[i_];        \
+            g_nstamps = (int)n_;                                                         \
         }                                                                                \
     } while (0)
 extern "C" int ygzfe_diag_stamps(unsigned long long *out, int cap) {
@@ -834,6 +886,9 @@ extern "C" int ygzfe_diag_stamps(unsigned long long *out, int cap) {
 }
 #else
 #define YGZ_STAMP(tag) do {} while (0)
+#define YGZ_STAMP_AT(tag, who) do {} while (0)
+#define YGZ_STAMP_INIT() do {} while (0)
+#define YGZ_STAMP_FLUSH() do {} while (0)
 #endif
 
 // Wave sum with DPP row operations (no LDS traffic, one temporary per value):
@@ -908,8 +963,9 @@ struct AlignPairLds {
     float opart[NW][24];
     float M[36];  // H_vis^-1 of the level, row-major (ldlt6_inverse_cols)
     SE3 T, old;
-    float chi2, Hpk[21];  // H of the last iteration, upper triangle row-major
+    float chi2, Hpk[21];  // H of the last iteration, upper triangle row-major (when hsrc)
     int stop, brk, nmeas;
+    int hsrc;    // the last iteration's H: 1 Hpk, 0 Hvis (no feature out of bounds)
     int out_it;  // the iteration (level * 16 + it) whose residual pass saw a feature out of bounds
 };
 
@@ -922,6 +978,7 @@ __device__ __forceinline__ void align_pair_init(AlignPairLds<NW> &P, const Align
     P.nmeas = 0;
     P.brk = 0;
     P.out_it = -1;
+    P.hsrc = 1;
     for (int i = 0; i < 21; i++) P.Hpk[i] = 0.f;
 }
 
@@ -932,8 +989,9 @@ __device__ __forceinline__ void align_pair_result(const AlignPairLds<NW> &P, ygz
     for (int i = 0; i < 3; i++) res.T_cur_ref.t[i] = P.T.t[i];
     res.n_visible = P.nmeas / kPA;
     res.chi2 = P.chi2;
+    const float *Hl = P.hsrc ? P.Hpk : P.Hvis;
     for (int rr = 0, m = 0; rr < 6; rr++)
-        for (int c = rr; c < 6; c++, m++) { res.H[rr * 6 + c] = P.Hpk[m]; res.H[c * 6 + rr] = P.Hpk[m]; }
+        for (int c = rr; c < 6; c++, m++) { res.H[rr * 6 + c] = Hl[m]; res.H[c * 6 + rr] = Hl[m]; }
     *out = res;
 }
 
@@ -947,11 +1005,65 @@ __device__ __forceinline__ void align_sum_hvis(AlignPairLds<NW> &P, int lane) {
     }
 }
 
-// level start, solver wave (beside the first residual pass): M = H_vis^-1
+// level start, solver wave (beside the first residual pass): M = H_vis^-1; returns
+// the lane's entry for align_solver_step's product: M[r][c] in lane 8r + c (r, c < 6),
+// 0 elsewhere
 template <int NW>
-__device__ __forceinline__ void align_level_inverse(AlignPairLds<NW> &P, int lane) {
+__device__ __forceinline__ float align_level_inverse(AlignPairLds<NW> &P, int lane) {
     const float hv = (lane >= 8 && lane < 29) ? P.Hvis[lane - 8] : 0.f;
     ldlt6_inverse_cols(hv, lane, P.M);
+    __builtin_amdgcn_wave_barrier();  // one wave: its LDS writes land before its reads
+    const int r = lane >> 3, c = lane & 7;
+    return (r < 6 && c < 6) ? P.M[r * 6 + c] : 0.f;
+}
+
+// the solver wave's copy of the pair's pose state (the same in every lane)
+struct SolverRegs {
+    SE3 T, old;
+    float chi2;
+    bool stop;
+    float mreg;  // align_level_inverse's entry of M = H_vis^-1
+};
+
+// Sophus SE3::exp of a (se3_exp) for the solver wave: the four transcendentals in
+// every lane (hardware v_sin/v_cos, no broadcasts) and V a = a_t + c1 (w x a_t) +
+// c2 (w (w . a_t) - theta^2 a_t), the closed form of (I + c1 O + c2 O^2) a_t without
+// O's zero products (rounding-level, pose parity 1e-4)
+__device__ __forceinline__ void se3_exp_solver(const float a[6], SE3 &out) {
+#pragma clang fp contract(fast)
+    const float eps = 1e-5f;
+    const float w0 = a[3], w1 = a[4], w2 = a[5];
+    const float theta_sq = w0 * w0 + w1 * w1 + w2 * w2;
+    const float theta = __builtin_amdgcn_sqrtf(theta_sq);
+    if (theta < eps) {  // wave-uniform: se3_exp's small-angle branch
+        const float theta_po4 = theta_sq * theta_sq;
+        const float im = 0.5f - (float)(1.0 / 48.0) * theta_sq + (float)(1.0 / 3840.0) * theta_po4;
+        const float q[4] = {im * w0, im * w1, im * w2,
+                            1.f - 0.5f * theta_sq + (float)(1.0 / 384.0) * theta_po4};
+        float V[9];
+        quat_to_mat(q, V);
+        for (int i = 0; i < 3; i++) out.t[i] = V[i * 3 + 0] * a[0] + V[i * 3 + 1] * a[1] + V[i * 3 + 2] * a[2];
+        for (int i = 0; i < 4; i++) out.q[i] = q[i];
+        return;
+    }
+    const float half_theta = 0.5f * theta;
+    const float s_half = __sinf(half_theta), c_half = __cosf(half_theta);
+    const float s_th = __sinf(theta), c_th = __cosf(theta);
+    const float inv_theta = __builtin_amdgcn_rcpf(theta);
+    const float imag = s_half * inv_theta;
+    const float inv_sq = inv_theta * inv_theta;
+    const float c1 = (1.f - c_th) * inv_sq;
+    const float c2 = (theta - s_th) * (inv_sq * inv_theta);
+    const float v0 = a[0], v1 = a[1], v2 = a[2];
+    const float x0 = w1 * v2 - w2 * v1, x1 = w2 * v0 - w0 * v2, x2 = w0 * v1 - w1 * v0;  // w x v
+    const float d = w0 * v0 + w1 * v1 + w2 * v2;
+    out.t[0] = v0 + c1 * x0 + c2 * (w0 * d - theta_sq * v0);
+    out.t[1] = v1 + c1 * x1 + c2 * (w1 * d - theta_sq * v1);
+    out.t[2] = v2 + c1 * x2 + c2 * (w2 * d - theta_sq * v2);
+    out.q[0] = imag * w0;
+    out.q[1] = imag * w1;
+    out.q[2] = imag * w2;
+    out.q[3] = c_half;
 }
 
 // the solver wave's view of a residual pass: lane k (< 8) of *pk8 holds value k's
@@ -979,10 +1091,13 @@ __device__ __forceinline__ void align_solver_reduce(AlignPairLds<NW> &P, int gi,
 }
 
 // one Gauss-Newton step, solver wave (NLSSolver_impl.hpp:18-91): reduce the
-// partials, H = H_vis - sum of the out-of-bounds features' H_f, LDLT, rollback or
-// T <- T exp(-x); P.brk set when the level's loop ends
+// partials, x = M Jres when every feature stayed inside the level (H = H_vis), else
+// H = H_vis - the out-of-bounds features' H_f and a fresh LDLT; rollback or
+// T <- T exp(-x).  The pose state lives in the wave's registers (S); lane 0 publishes
+// the pose and the loop decision.  Returns true when the level's loop ends.
 template <int NW>
-__device__ __forceinline__ void align_solver_step(AlignPairLds<NW> &P, int it, int gi, int lane) {
+__device__ __forceinline__ bool align_solver_step(AlignPairLds<NW> &P, SolverRegs &S, int it, int gi, int lane) {
+    const bool fast = P.out_it != gi;
     // Jres[6], chi2, n_meas over waves 1..NW-1: lane 8g + k adds waves 2g+1, 2g+2 of
     // value k, then the 8 groups fold (bit 3: DPP row_ror 8; bits 4, 5: permlane16 /
     // permlane32 swaps, no LDS round trip), so every lane holds the total of value k
@@ -998,18 +1113,19 @@ __device__ __forceinline__ void align_solver_step(AlignPairLds<NW> &P, int it, i
     float x[6];
     const int pi = __float_as_int(pk8);
     const int nmeas = (int)__int_as_float(__builtin_amdgcn_readlane(pi, 7));
-    const float new_chi2 = __int_as_float(__builtin_amdgcn_readlane(pi, 6)) / (float)nmeas;
+    const float chi2sum = __int_as_float(__builtin_amdgcn_readlane(pi, 6));
     if (lane == 0) P.nmeas = nmeas;
     YGZ_STAMP(7);
-    if (P.out_it != gi) {  // every feature inside the level: H = H_vis, x = H_vis^-1 Jres (lane r: row r)
+    if (fast) {  // every feature inside the level: H = H_vis, x = H_vis^-1 Jres
 #pragma clang fp contract(fast)  // solver wave: fused products (rounding-level, pose parity 1e-4)
-        const float *Mr = &P.M[(lane < 6 ? lane : 0) * 6];
-        float xr = 0.f;
+        // lane 8r + c: M[r][c] Jres[c], summed over the 8 lanes of row r by DPP
+        float pr = (lane & 7) < 6 ? S.mreg * pk8 : 0.f;
+        pr += YGZ_DPP(pr, 0xB1, 0xF);   // quad_perm [1,0,3,2]
+        pr += YGZ_DPP(pr, 0x4E, 0xF);   // quad_perm [2,3,0,1]
+        pr += YGZ_DPP(pr, 0x141, 0xF);  // row_half_mirror
 #pragma unroll
-        for (int c = 0; c < 6; c++) xr += Mr[c] * __int_as_float(__builtin_amdgcn_readlane(pi, c));
-#pragma unroll
-        for (int k = 0; k < 6; k++) x[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xr), k));
-        if (lane < 21) P.Hpk[lane] = P.Hvis[lane];  // H of this iteration (the result's Fisher information)
+        for (int k = 0; k < 6; k++) x[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pr), 8 * k));
+        if (lane == 0) P.hsrc = 0;  // H of this iteration (the result's Fisher information) = H_vis
     } else {  // a feature left the level: H = H_vis - the per-wave sums of its H_f, factored afresh
         float r = pk8;
         if (lane >= 8 && lane < 29) {
@@ -1022,36 +1138,40 @@ __device__ __forceinline__ void align_solver_step(AlignPairLds<NW> &P, int it, i
         } else if (lane >= 29) {
             r = 0.f;
         }
+        if (lane == 0) P.hsrc = 1;
         ldlt_solve6_nopiv(r, x);
     }
     YGZ_STAMP(8);
-    const bool stop = P.stop || isnan(x[0]);
-    const bool rollback = (it > 0 && (double)new_chi2 > 1.2 * (double)P.chi2) || stop;
+    const float new_chi2 = chi2sum / (float)nmeas;
+    const bool stop = S.stop || isnan(x[0]);
+    const bool rollback = (it > 0 && (double)new_chi2 > 1.2 * (double)S.chi2) || stop;
     if (rollback) {
+        S.stop = stop;
+        S.T = S.old;
         if (lane == 0) {
-            P.stop = stop ? 1 : 0;
-            P.T = P.old;
+            P.T = S.T;
             P.brk = 1;
         }
-    } else {
-        float mx[6];
-#pragma unroll
-        for (int k = 0; k < 6; k++) mx[k] = -x[k];
-        SE3 E, Tn;
-        se3_exp_wave(mx, E);
-        const SE3 Tc = P.T;
-        se3_mul_fast(Tc, E, Tn);
-        YGZ_STAMP(10);
-        float nm = -1.f;
-#pragma unroll
-        for (int k = 0; k < 6; k++) nm = fabsf(x[k]) > nm ? fabsf(x[k]) : nm;
-        if (lane == 0) {
-            P.old = Tc;
-            P.T = Tn;
-            P.chi2 = new_chi2;
-            P.brk = nm <= 0.000001f ? 1 : 0;
-        }
+        return true;
     }
+    float mx[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) mx[k] = -x[k];
+    SE3 E, Tn;
+    se3_exp_solver(mx, E);
+    se3_mul_fast(S.T, E, Tn);
+    YGZ_STAMP(10);
+    const float nm = fmaxf(fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))),
+                           fmaxf(fabsf(x[4]), fabsf(x[5])));
+    const bool brk = nm <= 0.000001f;
+    S.old = S.T;
+    S.T = Tn;
+    S.chi2 = new_chi2;
+    if (lane == 0) {
+        P.T = Tn;
+        P.brk = brk ? 1 : 0;
+    }
+    return brk;
 }
 
 // one reference feature owned by a thread of the feature waves
@@ -1095,7 +1215,8 @@ __device__ __forceinline__ void align_feat_precompute(const AlignFeat &F, bool v
     const int W = lv.w[level], H = lv.h[level];
     const float scale = lv.inv_scale[level];
     const float fs = cam.fx * scale;
-    const uint8_t *rimg = ref_pyr + lv.off[level];
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(ref_pyr + lv.off[level]), 0, (int)((uint32_t)W * (uint32_t)H + 64u), 0x00020000);
     bool here = false;
     if (F.own && F.usable) {
         const float u_ref = F.kx * scale, v_ref = F.ky * scale;
@@ -1103,25 +1224,28 @@ __device__ __forceinline__ void align_feat_precompute(const AlignFeat &F, bool v
         here = !(ui - border < 0 || vi - border < 0 || ui + border >= W || vi + border >= H);
         if (here) {
             const float su = u_ref - ui, sv = v_ref - vi;
-            const float wtl = wmul(1.0 - su, 1.0 - sv), wtr = wmul(su, 1.0 - sv);
-            const float wbl = wmul(1.0 - su, sv), wbr = wmul(su, sv);
+            const float wtl = wmulf(1.f - su, 1.f - sv), wtr = wmulf(su, 1.f - sv);
+            const float wbl = wmulf(1.f - su, sv), wbr = wmulf(su, sv);
             // 7x7 window: rows vi-3..vi+3, cols ui-3..ui+3; R[y][x] = ref(vi-3+y, ui-3+x),
             // kept as packed bytes (all 7 rows in flight at once)
-            const uint8_t *base = rimg + (size_t)(vi - 3) * W + (ui - 3);
+            const uint32_t base = (uint32_t)(vi - 3) * (uint32_t)W + (uint32_t)(ui - 3);
             uint32_t R[7][2];
 #pragma unroll
-            for (int y = 0; y < 7; y++) load_row_packed<7>(base + (size_t)y * W, R[y]);
+            for (int y = 0; y < 7; y++) load_row7_packed_buf(rs, base + (uint32_t)y * (uint32_t)W, R[y]);
             auto rpx = [&](int y, int x) -> float { return (float)((R[y][x >> 2] >> (8 * (x & 3))) & 0xFFu); };
             // J[y][x]: the bilinear sample at (x + su, y + sv) of the window; the
             // reference's patch and central differences are entries of J:
             // patch = J[py+1][px+1], gx = (J[py+1][px+2] - J[py+1][px]) / 2,
-            // gy = (J[py+2][px+1] - J[py][px+1]) / 2 -- the same expressions
-            // as SparseImageAlign.cc:98-125, each evaluated once
+            // gy = (J[py+2][px+1] - J[py][px+1]) / 2 -- the expressions of
+            // SparseImageAlign.cc:98-125, each evaluated once (the bilinear sums fused:
+            // rounding-level, pose parity 1e-4)
             float J0[6], J1[6], J2[6];
             auto jrow = [&](int y, float (&o)[6]) {
 #pragma unroll
                 for (int x = 0; x < 6; x++)
-                    o[x] = wtl * rpx(y, x) + wtr * rpx(y, x + 1) + wbl * rpx(y + 1, x) + wbr * rpx(y + 1, x + 1);
+                    o[x] = __builtin_fmaf(wbr, rpx(y + 1, x + 1),
+                                          __builtin_fmaf(wbl, rpx(y + 1, x),
+                                                         __builtin_fmaf(wtr, rpx(y, x + 1), wtl * rpx(y, x))));
             };
             jrow(0, J0);
             jrow(1, J1);
@@ -1151,21 +1275,16 @@ __device__ __forceinline__ void align_feat_precompute(const AlignFeat &F, bool v
     }
     D.Sxx = 0.f, D.Sxy = 0.f, D.Syy = 0.f;
 #pragma unroll
-    for (int p = 0; p < 16; p++) { D.Sxx += D.gx[p] * D.gx[p]; D.Sxy += D.gx[p] * D.gy[p]; D.Syy += D.gy[p] * D.gy[p]; }
-    const float fs2 = fs * fs;
-    float fj[12];
-    jacob_xyz2cam_fresh(F.X, F.Y, F.Z, fj);
+    for (int p = 0; p < 16; p++) {
+        D.Sxx = __builtin_fmaf(D.gx[p], D.gx[p], D.Sxx);
+        D.Sxy = __builtin_fmaf(D.gx[p], D.gy[p], D.Sxy);
+        D.Syy = __builtin_fmaf(D.gy[p], D.gy[p], D.Syy);
+    }
     float hv[32];
-    int m = 0;
+    feat_hessian(F.X, F.Y, F.Z, D.Sxx, D.Sxy, D.Syy, fs * fs, hv);
+    const bool counted = F.own && D.vis;
 #pragma unroll
-    for (int r = 0; r < 6; r++)
-#pragma unroll
-        for (int c = r; c < 6; c++) {
-            const float hrc = fj[r] * fj[c] * D.Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * D.Sxy +
-                              fj[6 + r] * fj[6 + c] * D.Syy;
-            hv[m] = (F.own && D.vis) ? hrc * fs2 : 0.f;
-            m++;
-        }
+    for (int k = 0; k < 21; k++) hv[k] = counted ? hv[k] : 0.f;
 #pragma unroll
     for (int k = 21; k < 32; k++) hv[k] = 0.f;
     const float t = wave_reduce32(hv, lane);
@@ -1185,7 +1304,9 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const Al
     const int W = lv.w[level], H = lv.h[level];
     const float scale = lv.inv_scale[level];
     const float fs = cam.fx * scale;
-    const uint8_t *cimg = cur_pyr + lv.off[level];
+    // the level as a buffer (the pyramid's tail padding covers the 8-byte row reads)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(cur_pyr + lv.off[level]), 0, (int)((uint32_t)W * (uint32_t)H + 64u), 0x00020000);
     float acc[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) acc[k] = 0.f;
@@ -1210,13 +1331,13 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const Al
             const float wtl = wmulf(1.f - su, 1.f - sv), wtr = wmulf(su, 1.f - sv);
             const float wbl = wmulf(1.f - su, sv), wbr = wmulf(su, sv);
             float Sx = 0.f, Sy = 0.f, chi2 = 0.f;
-            const uint8_t *base = cimg + (size_t)(vi - 2) * W + (ui - 2);
+            const uint32_t base = (uint32_t)(vi - 2) * (uint32_t)W + (uint32_t)(ui - 2);
             float r0[5];
-            load_row<5>(base, r0);
+            load_row5_buf(rs, base, r0);
 #pragma unroll
             for (int py = 0; py < 4; py++) {
                 float r1[5];
-                load_row<5>(base + (size_t)(py + 1) * W, r1);
+                load_row5_buf(rs, base + (uint32_t)(py + 1) * (uint32_t)W, r1);
 #pragma unroll
                 for (int px = 0; px < 4; px++) {
                     const int pi = py * 4 + px;
@@ -1230,10 +1351,19 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const Al
 #pragma unroll
                 for (int c = 0; c < 5; c++) r0[c] = r1[c];
             }
-            float fj[12];
-            jacob_xyz2cam_ff(F.X, F.Y, F.Z, fj);
-#pragma unroll
-            for (int r = 0; r < 6; r++) acc[r] = -(fj[r] * Sx + fj[6 + r] * Sy) * fs;
+            // -(J_xyz2cam^T [Sx Sy]) fs (SparseImageAlign.h:95-116 with x = X/Z, y = Y/Z):
+            // the twelve products of jacob_xyz2cam_ff collapsed (rounding-level)
+            float X = F.X, Y = F.Y, Z = F.Z;
+            asm volatile("" : "+v"(X), "+v"(Y), "+v"(Z));  // recomputed here, not hoisted (register pressure)
+            const float zi = __builtin_amdgcn_rcpf(Z);
+            const float xh = X * zi, yh = Y * zi, xy = xh * yh;
+            const float sx = Sx * fs, sy = Sy * fs;
+            acc[0] = zi * sx;
+            acc[1] = zi * sy;
+            acc[2] = -zi * __builtin_fmaf(xh, sx, yh * sy);
+            acc[3] = -__builtin_fmaf(xy, sx, __builtin_fmaf(yh * yh, sy, sy));
+            acc[4] = __builtin_fmaf(xy, sy, __builtin_fmaf(xh * xh, sx, sx));
+            acc[5] = __builtin_fmaf(xh, sy, -(yh * sx));
             acc[6] = chi2;
             acc[7] = 16.f;
         }
@@ -1244,19 +1374,10 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const Al
     }
     // H_f of the features projected out of bounds, summed per wave (usually none)
     if (__ballot(out_now)) {
-        float fj[12];
-        jacob_xyz2cam_fresh(F.X, F.Y, F.Z, fj);
-        const float fs2 = fs * fs;
         float hv[32];
-        int m = 0;
+        feat_hessian(F.X, F.Y, F.Z, D.Sxx, D.Sxy, D.Syy, fs * fs, hv);
 #pragma unroll
-        for (int r = 0; r < 6; r++)
-#pragma unroll
-            for (int c = r; c < 6; c++) {
-                const float hrc = fj[r] * fj[c] * D.Sxx + (fj[r] * fj[6 + c] + fj[6 + r] * fj[c]) * D.Sxy +
-                                  fj[6 + r] * fj[6 + c] * D.Syy;
-                hv[m++] = out_now ? hrc * fs2 : 0.f;
-            }
+        for (int k = 0; k < 21; k++) hv[k] = out_now ? hv[k] : 0.f;
 #pragma unroll
         for (int k = 21; k < 32; k++) hv[k] = 0.f;
         const float t = wave_reduce32(hv, lane);
@@ -1293,6 +1414,7 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
     const AlignJob &job = jobs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) align_pair_init(P, job);
+    YGZ_STAMP_INIT();
     __syncthreads();
     YGZ_STAMP(9);
     if (METHOD == 1 && wave == 0) {  // Levenberg-Marquardt: lm_round decides each pass's pose
@@ -1338,8 +1460,13 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
         return;
     }
     if (wave == 0) {
+        SolverRegs S;
+        for (int i = 0; i < 4; i++) S.T.q[i] = job.T_init.q[i];
+        for (int i = 0; i < 3; i++) S.T.t[i] = job.T_init.t[i];
+        S.chi2 = 1e10f;
+        S.stop = false;
         for (int level = job.max_level; level >= job.min_level; level--) {
-            if (tid == 0) P.old = P.T;
+            S.old = S.T;
             __syncthreads();  // L0: level start, the level's H partials are in
             YGZ_STAMP(1);
             if (level == job.max_level) {
@@ -1350,20 +1477,24 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
                 P.Hvis[lane] = r;
             }
             __syncthreads();  // L0b: part free again
-            align_level_inverse(P, lane);  // beside the first residual pass
+            S.mreg = align_level_inverse(P, lane);  // beside the first residual pass
             YGZ_STAMP(2);
             for (int it = 0; it < 10; it++) {
                 __syncthreads();  // A: partials written
                 YGZ_STAMP(3);
-                align_solver_step(P, it, level * 16 + it, lane);
+                const bool brk = align_solver_step(P, S, it, level * 16 + it, lane);
                 __syncthreads();  // B: pose / decision published
                 YGZ_STAMP(4);
-                if (P.brk) break;
+                if (brk) break;
             }
             __syncthreads();  // L1: level end
             YGZ_STAMP(5);
         }
-        if (tid == 0) align_pair_result(P, out + blockIdx.x);
+        YGZ_STAMP_FLUSH();
+        if (tid == 0) {
+            P.chi2 = S.chi2;
+            align_pair_result(P, out + blockIdx.x);
+        }
         return;
     }
     const int f = tid - 64;
@@ -1411,9 +1542,12 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
         __syncthreads();  // L0
         __syncthreads();  // L0b
         for (int it = 0; it < 10; it++) {
+            YGZ_STAMP_AT(11, tid == 64);
             const SE3 T = P.T;
             align_feat_residual<NF, NW>(F, D, T, lv, cam, job.cur_pyr, level, s_patch[cb], f, P.part, P.opart,
                                         &P.out_it, level * 16 + it, wave, lane);
+            YGZ_STAMP_AT(12, tid == 64);
+            YGZ_STAMP_AT(13, tid == 1023);
             __syncthreads();  // A
             if (it == 0 && level > job.min_level)  // the next level, beside the solver's step
                 align_feat_precompute<NF, NW>(F, D.vis, Dn, lv, cam, job.ref_pyr, level - 1, s_patch[cb ^ 1],

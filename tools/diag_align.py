@@ -30,16 +30,15 @@ for rep in range(3):
     ygzfe.lib().ygzfe_diag_stamps(buf, 4096)
     res = al.run(fr, fc, sc.camera(), kps, xyz, ok, ygzfe.SE3.make())
     n = ygzfe.lib().ygzfe_diag_stamps(buf, 4096)
-st = [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
-t0 = st[0][1]
-names = {9: "start", 1: "L0 (precompute done)", 2: "L0b (H_vis)", 3: "A (features done)", 4: "B (published)",
-         5: "L1", 6: "partials reduced", 7: "H/b unpacked", 8: "LDLT done", 10: "exp+mul done"}
-prev = t0
-tot = {}
-for tag, t in st:
-    d = t - prev
-    tot[tag] = tot.get(tag, 0) + d
-    prev = t
-print("n_features", len(kps), "n_visible", res.n_visible, "stamps", n, "total cycles", st[-1][1] - t0)
-for k, vv in sorted(tot.items()):
-    print(f"  phase ending at {names.get(k, k):24s}: {vv:8d} cycles  ({st.count if False else sum(1 for a, b in st if a == k)} times)")
+st = sorted([(buf[2 * i], buf[2 * i + 1]) for i in range(n)], key=lambda x: x[1])
+names = {9: "start", 1: "L0 (level H in)", 2: "L0b + inverse", 3: "A passed (solver)", 4: "B passed",
+         5: "L1", 6: "partials reduced", 7: "chi2 read", 8: "x solved", 10: "exp+mul done",
+         11: "w1 residual start", 12: "w1 residual done", 13: "w15 residual done"}
+print("n_features", len(kps), "n_visible", res.n_visible, "stamps", n, "total cycles", st[-1][1] - st[0][1])
+tot, cnt = {}, {}
+for (a, ta), (b, tb) in zip(st, st[1:]):
+    k = (a, b)
+    tot[k] = tot.get(k, 0) + (tb - ta)
+    cnt[k] = cnt.get(k, 0) + 1
+for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
+    print(f"  {names.get(k[0], k[0]):20s} -> {names.get(k[1], k[1]):20s}: {v:8d} cycles over {cnt[k]:3d}  ({v / cnt[k]:.0f} each)")
