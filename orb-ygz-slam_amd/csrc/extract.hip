@@ -721,6 +721,10 @@ __device__ __forceinline__ s16x2 fast_arcmax2(const uint8_t *img, uint32_t e0, u
 //   BC survivors: segment test + score, corners compacted in place, scores into the map
 //   D  corners: strict 3x3 non-max suppression, survivors -> the cell's list
 // and the retry at minThFAST when no corner survives (ORBextractor.cc:765-770).
+#ifndef YGZ_FAST_KO
+#define YGZ_FAST_KO 0  // diagnostic knock-outs (tools/run_fast_phases.sh): 1 ROI staging only, 2 + A,
+                       // 3 + BC, 4 + D (2-4: the first pass only, no retry); 0 the product
+#endif
 template <int S>
 __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, const CellDesc &cd, uint8_t *img,
                                                uint8_t *sc, uint16_t *list, uint32_t *__restrict__ out,
@@ -728,7 +732,7 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
     const int rw = cd.rw, rh = cd.rh;
     const int iw = rw - 6, ih = rh - 6;
     int total = 0;
-    for (int pass = pass0; pass < 2; pass++) {
+    for (int pass = pass0; pass < (YGZ_FAST_KO ? pass0 + 1 : 2); pass++) {
         const int th = pass == 0 ? plan->ini_th : plan->min_th;
         {
             uint4 *z = reinterpret_cast<uint4 *>(sc);
@@ -767,6 +771,10 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                     if ((m >> k) & 1u) list[pos++] = (uint16_t)(ey | (uint32_t)(4 * j + k + 3));
             }
         }
+        if (YGZ_FAST_KO == 2) {
+            total = na;
+            break;
+        }
         // BC: two survivors per lane (low half list[i], high half list[i+1]); corners
         // compacted in place in raster order (writes never pass the read front)
         int nc = 0;
@@ -786,6 +794,10 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             nc += __popcll(M0) + __popcll(M1);
         }
         wave_lds_order();
+        if (YGZ_FAST_KO == 3) {
+            total = nc;
+            break;
+        }
         // D: strict 3x3 NMS over the corner list
         for (int i0 = 0; i0 < nc; i0 += 64) {
             const int i = i0 + lane;
@@ -856,6 +868,12 @@ __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu
         RoiStage<S, R> st;
         st.issue(rs, off0, L.w, cd.rw, cd.rh, lane);
         st.commit(img, off0, L.w, cd.rw, cd.rh, lane);
+    }
+    if (YGZ_FAST_KO == 1) {  // staging only: one byte of the tile out, so the staging stays
+        wave_lds_order();
+        const uint32_t probe = (uint32_t)img[lane] + img[S * 8 + lane] + img[S * 20 + lane];  // < 2^10
+        if (lane == 0) cellcnt[(size_t)f * plan->ncells + c] = (int)(probe >> 30);
+        return;
     }
     fast_cell_item<S>(plan, cd, img, sc, list, cellbuf + ((size_t)f * plan->ncells + c) * plan->cell_cap,
                       cellcnt + (size_t)f * plan->ncells + c, lane, 0);
@@ -1884,13 +1902,24 @@ struct IcWindow {
 // address) & 15 of LDS row r); every tap is an LDS byte read.  Octree
 // keypoints sit >= 19 px inside the level, so the 31x31 IC window and the
 // 37x37 rotated-pattern window never leave it.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_orient_desc(const uint8_t *__restrict__ pyr,
+#ifndef YGZ_ORIENT_GATHER
+#define YGZ_ORIENT_GATHER 0  // experiment: rBRIEF taps gathered from the blurred level (L1/L2), only the IC
+                             // window in LDS (6 workgroups / CU) -- VERDICT r04 #5
+#endif
+#if YGZ_ORIENT_GATHER
+#define YGZ_ORIENT_WPE 6
+#define YGZ_ORIENT_SLOT 1616
+#else
+#define YGZ_ORIENT_WPE 5
+#define YGZ_ORIENT_SLOT kPatchBytes
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YGZ_ORIENT_WPE))) void k_orient_desc(const uint8_t *__restrict__ pyr,
                                                      const uint8_t *__restrict__ blur, uint32_t pitch,
                                                      const Plan *__restrict__ plan, const uint2 *__restrict__ ojobs,
                                                      const int *__restrict__ n_existing,
                                                      ygzfe_kp *__restrict__ kps, uint8_t *__restrict__ desc,
                                                      int row_cap) {
-    __shared__ uint8_t s_patch[16][kPatchBytes];  // one 37x37 window per keypoint row
+    __shared__ uint8_t s_patch[16][YGZ_ORIENT_SLOT];  // one 37x37 window per keypoint row
     // the pattern (c_pattern, 1 KB) staged once per workgroup; the IC row weights are
     // formed in registers from umax, so the workgroup's LDS is 32 KB (5 per CU)
     __shared__ uint4 s_const[64];
@@ -1912,7 +1941,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const uint8_t *fblur = blur + (size_t)f * pitch;
     uint8_t *P = s_patch[threadIdx.x >> 4];
     IcWindow wic;
+#if !YGZ_ORIENT_GATHER
     Window<18, 37> wdesc;
+#endif
     wic.load(fimg, w, c, s);  // the rBRIEF window follows once the IC window is in LDS
     if (threadIdx.x < 64) s_const[threadIdx.x] = cst;
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
@@ -1935,7 +1966,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     float angle;
     {
         wic.store(P, s);
+#if !YGZ_ORIENT_GATHER
         wdesc.load(fblur, w, c, s);  // in flight during the IC sums
+#endif
         // IC_Angle (ORBextractor.cc:77-101): lane s takes the window rows 15 +- (s+1)
         // (lane 15 the centre row).  Per row, with I the 31 row bytes (32nd
         // weighted 0): S0 = sum of I over the disc (dot4 with the 0/1 weights),
@@ -1976,7 +2009,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         pat[q] = make_int4((int)u.x, (int)u.y, (int)u.z, (int)u.w);
     }
     wave_lds_order();  // IC taps read before the window is replaced
+#if !YGZ_ORIENT_GATHER
     wdesc.store(P, s);
+#endif
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float ca, sb;
     glibc_sincosf(angle * factorPI, sb, ca);  // the reference's std::cos(float) / std::sin(float) = glibc cosf / sinf
@@ -1997,6 +2032,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const f32x2 magic = {__uint_as_float(kMagicBits + 64u), __uint_as_float(kMagicBits + Pa + 64u)};
     constexpr uint32_t kFix = kMagicBits + 46u * (uint32_t)kPatchStride + 64u - 18u;
     const f32x2 rot_a = {sb, ca}, rot_b = {ca, -sb};
+#if YGZ_ORIENT_GATHER
+    (void)Pa; (void)c0; (void)w16;
+    const f32x2 magic_g = {__uint_as_float(kMagicBits + 64u), __uint_as_float(kMagicBits + 64u)};
+    const gptr_t<uint8_t> gb = as_global(fblur + c);
+    auto tap = [&](float px, float py) -> uint32_t {
+        const f32x2 m = (f32x2){py, py} * rot_b;
+        const f32x2 yx = __builtin_elementwise_fma((f32x2){px, px}, rot_a, m) + magic_g;
+        const int ry = (int)(__float_as_uint(yx.x) - kMagicBits) - 64, rx = (int)(__float_as_uint(yx.y) - kMagicBits) - 64;
+        return (uint32_t)gb[ry * (int)w + rx];
+    };
+#else
     auto tap = [&](float px, float py) -> uint32_t {
         const f32x2 m = (f32x2){py, py} * rot_b;
         const f32x2 yx = __builtin_elementwise_fma((f32x2){px, px}, rot_a, m) + magic;
@@ -2004,6 +2050,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         const uint32_t a = mad24(yb, (uint32_t)kPatchStride, xb), o = (yb & 15u) * w16 + c0;
         return (uint32_t)*(const lds_u8 *)(uintptr_t)(a + (o & 15u) - kFix);
     };
+#endif
     uint32_t bits = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
