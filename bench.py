@@ -65,11 +65,13 @@ def parse():
     ap.add_argument("--no-align", action="store_true")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture one step into a HIP graph and replay it (measured: same throughput as eager launches)")
-    ap.add_argument("--schedule", choices=["split", "overlap", "tail", "serial"], default="overlap",
+    ap.add_argument("--schedule", choices=["split", "overlap", "tail", "serial", "pipe"], default="overlap",
                     help="the timed steps' schedule. split: blur + descriptors + Hamming on a side stream "
                          "beside FAST / octree, SparseImgAlign after them; overlap: SparseImgAlign beside "
                          "orient + Hamming too; tail: the extraction on one stream, then Hamming on a side "
-                         "stream beside SparseImgAlign; serial: every stage on one stream.  The per-stage "
+                         "stream beside SparseImgAlign; serial: every stage on one stream; pipe: the shard in chunks "
+                         "(default 2), chunk c + 1's pyramid / FAST / octree beside chunk c's descriptors, "
+                         "Hamming and SparseImgAlign.  The per-stage "
                          "roofline pass always runs serial (one kernel on the GPU at a time)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="process each rank's shard in this many chunks (each its own batch), gathering a "
@@ -144,7 +146,7 @@ def main():
 
     W, H, nf, sf, nl, ini, mn = C2
     n_seq = (args.frames or C5_FRAMES) if args.workload == "c5" else world * args.batch
-    n_chunks = args.chunks if args.chunks > 0 else (4 if world > 1 else 1)
+    n_chunks = args.chunks if args.chunks > 0 else (4 if world > 1 else (2 if args.schedule == "pipe" else 1))
     t_r = time.time()
     # the rank's whole C5 job (ygzfe/sequence.py; tests/test_gpu_c5.py runs the same object)
     shard = C5Shard(n_seq, rank, world, dev, chunks=n_chunks, schedule=args.schedule, align=not args.no_align)
@@ -236,7 +238,7 @@ def main():
                      "slot_bytes": S_b}
 
     # ------------------------------------------------ roofline (dominant stage)
-    counts = counts_t[:F].cpu().numpy()
+    counts = shard.counts().cpu().numpy()
     nvis = out[:max(P, 1), 7].contiguous().view(torch.int32).cpu().numpy() if P > 0 else np.zeros(1, np.int32)
     plan = ygzfe.orb_plan(nf, sf, nl, ini, mn, W, H)
     areas = [w * hh for w, hh in plan["sizes"]]
@@ -415,7 +417,8 @@ def main():
                        "collective": (f"RCCL gather of result slots to rank 0 (torch.distributed.gather), "
                                       f"{n_chunks} chunk(s), each gathered on a communication stream while the "
                                       f"next chunk computes") if world > 1 else "none (N=1: rank 0 is the root)",
-                       "schedule": ("chunked (each chunk serial)" if shard.chunks else args.schedule),
+                       "schedule": (args.schedule if (args.schedule == "pipe" or not shard.chunks)
+                                    else "chunked (each chunk serial)"),
                        "schedule_stage_timing": "serial",
                        "schedule_note": ("value times the steps under `schedule`; roofline.stages_ms comes from "
                                          "a separate pass of the same steps in the serial schedule (one kernel "

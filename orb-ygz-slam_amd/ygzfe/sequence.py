@@ -46,6 +46,7 @@ class C5Shard:
         self.torch = torch
         self.n_seq, self.rank, self.world, self.dev = n_seq, rank, world, dev
         self.schedule, self.align = schedule, align
+        self.schedule_buffers = schedule  # the chunk buffers follow the constructor's schedule
         self.gather = (world > 1) if gather is None else bool(gather)
         W, H, nf, sf, nl, ini, mn = C2
         self.W, self.H = W, H
@@ -132,13 +133,31 @@ class C5Shard:
             maxlen_c, Rc = D.chunk_rows(n_seq, world, n_chunks)
             self.slots = torch.zeros((n_chunks * Rc, S_b), dtype=torch.uint8, device=dev)
             self.comm = torch.cuda.Stream(dev)
+            # schedule "pipe": two stream pairs, chunks alternating between them
+            self.pipe_streams = [(self.stream, self.side), (torch.cuda.Stream(dev), torch.cuda.Stream(dev))]
+            # "pipe" runs chunk c + 1's extraction beside chunk c's descriptors and alignment, so
+            # the frame they share (chunk c + 1's lead frame) must not be rewritten under chunk
+            # c's readers: every chunk gets its own pyramids / rows (level 0 copied once here)
+            self.chunk_kps = []
             for c in range(n_chunks):
                 s_c, e_c, hc, nc = D.chunk_frames(n_own, h, c, Rc)
                 bt = None
                 if nc > 0:
                     bt = ygzfe.Batch(self.params, dev_i, W, H, max(e_c - s_c, 2))
-                    bt.bind(pyramids=self.pyr_t.data_ptr() + s_c * batch.frame_pitch,
-                            kps=self.kps_t[s_c:].data_ptr(), counts=self.counts_t[s_c:].data_ptr())
+                    if schedule == "pipe":
+                        Lc = e_c - s_c
+                        pyr_c = self.pyr_t[s_c * batch.frame_pitch:e_c * batch.frame_pitch].clone()
+                        kps_c = torch.empty((max(Lc, 2), cap, 7), dtype=torch.float32, device=dev)
+                        cnt_c = torch.zeros(max(Lc, 2), dtype=torch.int32, device=dev)
+                        bt.bind(pyramids=pyr_c.data_ptr(), kps=kps_c.data_ptr(), counts=cnt_c.data_ptr())
+                        bt._own = (pyr_c, kps_c, cnt_c)  # kept alive with the batch
+                        self.chunk_kps.append(kps_c)
+                    else:
+                        bt.bind(pyramids=self.pyr_t.data_ptr() + s_c * batch.frame_pitch,
+                                kps=self.kps_t[s_c:].data_ptr(), counts=self.counts_t[s_c:].data_ptr())
+                        self.chunk_kps.append(self.kps_t[s_c:])
+                else:
+                    self.chunk_kps.append(None)
                 bufs = [torch.empty((Rc, S_b), dtype=torch.uint8, device=dev) for _ in range(world)] \
                     if (rank == 0 and self.gather) else None
                 self.chunks.append((s_c, e_c - s_c, hc, nc, bt, bufs, c * Rc))
@@ -146,15 +165,17 @@ class C5Shard:
         self.F_ext = sum(ch[1] for ch in self.chunks if ch[3] > 0) if self.chunks else F
 
     # ------------------------------------------------------------------ steps
-    def _plane_points(self, off, n):
+    def _plane_points(self, off, n, stream=None, kps=None):
         import ygzfe
-        ygzfe.plane_points_device(self.kps_t[off:].data_ptr(), self.cap, n, self.cam, self.r3_t[off:].data_ptr(),
-                                  self.cz_t[off:].data_ptr(), self.S.PLANE_Z, self.xyz[off:].data_ptr(), self.sptr)
+        kp = self.kps_t[off:] if kps is None else kps
+        ygzfe.plane_points_device(kp.data_ptr(), self.cap, n, self.cam, self.r3_t[off:].data_ptr(),
+                                  self.cz_t[off:].data_ptr(), self.S.PLANE_Z, self.xyz[off:].data_ptr(),
+                                  self.sptr if stream is None else stream)
 
-    def _align(self, bt, off, n):
+    def _align(self, bt, off, n, stream=None):
         bt.sparse_align(n, self.ref_idx.data_ptr(), self.cur_idx.data_ptr(), self.xyz[off:].data_ptr(),
                         self.usable[off:].data_ptr(), self.camera, 3, 1, self.T_init[off:].data_ptr(),
-                        self.out[off:].data_ptr(), self.sptr)
+                        self.out[off:].data_ptr(), self.sptr if stream is None else stream)
 
     def _match(self, bt, off, n, stream):
         bt.match(n, self.cur_idx.data_ptr(), self.ref_idx.data_ptr(), self.bi[off:].data_ptr(),
@@ -218,6 +239,43 @@ class C5Shard:
         self.stream.wait_stream(self.side)  # the slots need the descriptors
         self._pack_and_gather(timed_gather)
 
+    def _step_pipe(self, timed_gather=False):
+        # software pipeline over the chunks: chunk c on its own stream pair (keypoint rows on
+        # `st`, blur + descriptors + Hamming on `sd`, as in the overlap schedule), its start
+        # held back until chunk c - 1's keypoint rows are out, so chunk c's pyramid / FAST /
+        # octree run beside chunk c - 1's orientation, Hamming and SparseImgAlign
+        import torch.distributed as dist
+        torch = self.torch
+        prev = torch.cuda.Event()
+        prev.record(self.stream)  # the previous step's work
+        for c, (s_c, L_c, hc, nc, bt, bufs, row0) in enumerate(self.chunks):
+            st, sd = self.pipe_streams[c & 1]
+            if nc == 0:
+                continue
+            st.wait_event(prev)
+            sd.wait_stream(st)
+            Pc = L_c - 1
+            bt.extract_split(L_c, st.cuda_stream, sd.cuda_stream)
+            prev = torch.cuda.Event()
+            prev.record(st)  # chunk c's keypoint rows: the next chunk starts here
+            if Pc > 0:
+                self._match(bt, s_c, Pc, sd.cuda_stream)
+                if self.align:
+                    self._plane_points(s_c, Pc, st.cuda_stream, self.chunk_kps[c])
+                    self._align(bt, s_c, Pc, st.cuda_stream)
+            st.wait_stream(sd)  # the slots need the descriptors
+            bt.pack_slots(hc, nc, self.out[s_c:].data_ptr() if (Pc > 0 and self.align) else 0, self.b0 + row0,
+                          self.slots[row0:].data_ptr(), self.slot_bytes, st.cuda_stream)
+            if self.gather:
+                self.comm.wait_stream(st)
+                with torch.cuda.stream(self.comm):
+                    dist.gather(self.slots[row0:row0 + (self.slots.shape[0] // self.n_chunks)], bufs, dst=0)
+        for st, sd in self.pipe_streams:
+            self.stream.wait_stream(st)
+            self.stream.wait_stream(sd)
+        if self.gather:
+            self.stream.wait_stream(self.comm)
+
     def _step_chunked(self, timed_gather=False):
         import torch.distributed as dist
         torch = self.torch
@@ -228,7 +286,7 @@ class C5Shard:
                 if Pc > 0:
                     self._match(bt, s_c, Pc, self.sptr)
                     if self.align:
-                        self._plane_points(s_c, Pc)
+                        self._plane_points(s_c, Pc, None, self.chunk_kps[c])
                         self._align(bt, s_c, Pc)
                 bt.pack_slots(hc, nc, self.out[s_c:].data_ptr() if (Pc > 0 and self.align) else 0, self.b0 + row0,
                               self.slots[row0:].data_ptr(), self.slot_bytes, self.sptr)
@@ -248,6 +306,8 @@ class C5Shard:
             self.stream.wait_stream(self.comm)
 
     def step(self, timed_gather=False):
+        if self.chunks and self.schedule == "pipe":
+            return self._step_pipe(timed_gather)
         if self.chunks:
             return self._step_chunked(timed_gather)
         if self.schedule == "serial" or self.P == 0:
@@ -257,6 +317,16 @@ class C5Shard:
         return self._step_split(timed_gather)
 
     # ------------------------------------------------------------------ results
+    def counts(self):
+        """Keypoints per extracted frame of the shard (F), whichever buffers the schedule used."""
+        if self.chunks and self.schedule_buffers == "pipe":
+            out = self.torch.zeros(self.F, dtype=self.torch.int32, device=self.dev)
+            for (s_c, L_c, hc, nc, bt, bufs, row0) in self.chunks:
+                if nc > 0:
+                    out[s_c:s_c + L_c] = bt._own[2][:L_c]
+            return out
+        return self.counts_t[:self.F]
+
     def check(self):
         for bt in self.batches:
             bt.check()

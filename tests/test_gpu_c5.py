@@ -184,13 +184,21 @@ def test_c5_sampled_frames_and_pairs_vs_oracle(c5_full):
     print(f"C5 sample: {len(frames)} frames bit-exact, {len(pairs)} align pairs, worst |dT| {worst:.2e}")
 
 
-@pytest.mark.parametrize("schedule", ["overlap", "split", "tail"])
-def test_c5_schedules_equal_serial(c5_full, schedule):
+@pytest.mark.parametrize("schedule,chunks", [("overlap", 1), ("split", 1), ("tail", 1), ("pipe", 2), ("pipe", 4)])
+def test_c5_schedules_equal_serial(c5_full, schedule, chunks):
     """The stream schedules bench.py can time (the default `overlap` included) give the serial
-    schedule's slots byte for byte: they reorder launches across streams, never the results."""
+    schedule's slots byte for byte: they reorder launches across streams, never the results.
+    `pipe` runs chunk c + 1's extraction beside chunk c's descriptors and alignment (private
+    per-chunk buffers); its align records must equal the unchunked run's too."""
     dev = torch.device("cuda", 0)
-    sh = _run(C5Shard(C5_FRAMES, 0, 1, dev, schedule=schedule))
+    sh = _run(C5Shard(C5_FRAMES, 0, 1, dev, chunks=chunks, schedule=schedule))
     assert torch.equal(sh.local_slots(), c5_full.local_slots())
+    if schedule == "pipe":
+        assert torch.equal(sh.counts(), c5_full.counts())
+        sh.step()  # a second step reuses the chunk batches (the write-after-read edges)
+        torch.cuda.synchronize()
+        sh.check()
+        assert torch.equal(sh.local_slots(), c5_full.local_slots())
     del sh
     torch.cuda.empty_cache()
 
