@@ -65,18 +65,18 @@ def parse():
     ap.add_argument("--no-align", action="store_true")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture one step into a HIP graph and replay it (measured: same throughput as eager launches)")
-    ap.add_argument("--schedule", choices=["split", "overlap", "tail", "serial", "pipe"], default="overlap",
+    ap.add_argument("--schedule", choices=["split", "overlap", "tail", "serial", "pipe"], default="pipe",
                     help="the timed steps' schedule. split: blur + descriptors + Hamming on a side stream "
                          "beside FAST / octree, SparseImgAlign after them; overlap: SparseImgAlign beside "
                          "orient + Hamming too; tail: the extraction on one stream, then Hamming on a side "
                          "stream beside SparseImgAlign; serial: every stage on one stream; pipe: the shard in chunks "
-                         "(default 2), chunk c + 1's pyramid / FAST / octree beside chunk c's descriptors, "
+                         "(default 4), chunk c + 1's pyramid / FAST / octree beside chunk c's descriptors, "
                          "Hamming and SparseImgAlign.  The per-stage "
                          "roofline pass always runs serial (one kernel on the GPU at a time)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="process each rank's shard in this many chunks (each its own batch), gathering a "
                          "chunk's result slots on a communication stream while the next chunk computes "
-                         "(default: 4 when N > 1, else 1 = one batch)")
+                         "(default: 4 under the pipe schedule or when N > 1, else 1 = one batch)")
     ap.add_argument("--no-undistort", action="store_true", help="skip the undistort-remap side measurement")
     ap.add_argument("--no-stage-timing", action="store_true", help="no per-stage hipEvents in the timed region")
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2-transform side measurement")
@@ -146,7 +146,7 @@ def main():
 
     W, H, nf, sf, nl, ini, mn = C2
     n_seq = (args.frames or C5_FRAMES) if args.workload == "c5" else world * args.batch
-    n_chunks = args.chunks if args.chunks > 0 else (4 if world > 1 else (2 if args.schedule == "pipe" else 1))
+    n_chunks = args.chunks if args.chunks > 0 else (4 if (world > 1 or args.schedule == "pipe") else 1)
     t_r = time.time()
     # the rank's whole C5 job (ygzfe/sequence.py; tests/test_gpu_c5.py runs the same object)
     shard = C5Shard(n_seq, rank, world, dev, chunks=n_chunks, schedule=args.schedule, align=not args.no_align)
@@ -269,6 +269,7 @@ def main():
     if not any(v > 0 for k, v in stage_ms.items() if k in alg):  # --no-stage-timing
         stage_ms = {k: 1e-9 for k in alg}
     dom = max((k for k in stage_ms if k in alg and stage_ms[k] > 0), key=lambda k: stage_ms[k])
+    n_batches = max(1, len(batches))
     dom_ms = stage_ms[dom]
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
     traffic = valu_frac = None
@@ -280,7 +281,7 @@ def main():
         tj = json.load(open(tpath))
         per = tj.get("per_frame", {}).get(dom)
         if per is not None:  # scaled to this launch's frame count
-            traffic = int(per["traffic_bytes"] * F)
+            traffic = int(per["traffic_bytes"] * F / n_batches)
             valu_frac = per.get("valu_frac")
             pmc = {k: per[k] for k in ("wait_inst_frac", "wait_any_frac", "lds_conflict_per_inst") if k in per}
             pmc["source"] = os.path.basename(tpath)
@@ -291,7 +292,10 @@ def main():
             # what binds the dominant kernel below its HBM roofline: for FAST, VALU issue
             # and LDS / load latency, not HBM bandwidth (the PMC figures of the same kernel beside it)
             "binding": BINDING.get(dom, "see DESIGN.md section 4"), "pmc": pmc or None,
-            "avg_launch_ms": round(dom_ms, 4), "alg_bytes_per_launch": int(alg[dom]), "frames_per_launch": F_ext,
+            # one "launch" = the stage over one batch: with chunks, each chunk's batch (its FAST = one
+            # kernel per pyramid level), n_batches of them per step; stages_ms are per-step sums
+            "avg_launch_ms": round(dom_ms / n_batches, 4), "alg_bytes_per_launch": int(alg[dom] / n_batches),
+            "frames_per_launch": round(F_ext / n_batches, 1), "launches_per_step": n_batches,
             "stages_ms": {k: round(v, 4) for k, v in stage_ms.items()},
             "stages_gbps": {k: round(alg[k] / (stage_ms[k] * 1e-3) / 1e9, 1) for k in alg if stage_ms.get(k, 0) > 0}}
     # whole pipeline, SURVEY §8d model: (B_extract + B_align) per frame x fps
@@ -421,9 +425,9 @@ def main():
                                     else "chunked (each chunk serial)"),
                        "schedule_stage_timing": "serial",
                        "schedule_note": ("value times the steps under `schedule`; roofline.stages_ms comes from "
-                                         "a separate pass of the same steps in the serial schedule (one kernel "
-                                         "on the GPU at a time), so the stage times sum to that pass's step, "
-                                         "not to ms_per_step"),
+                                         "a separate pass of the same steps (same chunk batches) in the serial "
+                                         "schedule (one kernel on the GPU at a time), so the stage times sum to "
+                                         "that pass's step, not to ms_per_step"),
                        "hip_graph": graph_ok},
             "roofline": roof,
             "pipeline_gbps_model": round(pipeline_gbps, 2),

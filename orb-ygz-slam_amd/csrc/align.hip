@@ -1095,13 +1095,9 @@ __device__ __forceinline__ void align_solver_reduce(AlignPairLds<NW> &P, int gi,
 // H = H_vis - the out-of-bounds features' H_f and a fresh LDLT; rollback or
 // T <- T exp(-x).  The pose state lives in the wave's registers (S); lane 0 publishes
 // the pose and the loop decision.  Returns true when the level's loop ends.
-// ALL: every wave of the workgroup runs the step on its own copy (identical inputs,
-// identical instructions: identical results), reading double-buffered partials, so no
-// wave waits for a publish; `writer` (wave 0) keeps the result's fields in P.
-__device__ __forceinline__ float uniform_f(float v) {
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
-template <int NW, bool ALL>
+// (Every wave running the step on its own copy, with double-buffered partials and no
+// publish barrier, was measured at 0.49 against 0.34 ms per 1,023 pairs: profiles/r05/align.)
+template <int NW>
 __device__ __forceinline__ bool align_solver_step(AlignPairLds<NW> &P, SolverRegs &S, int it, int gi, int lane,
                                                   const float (*part)[32], const float (*opart)[24],
                                                   const int *out_it, bool writer) {
@@ -1156,7 +1152,7 @@ __device__ __forceinline__ bool align_solver_step(AlignPairLds<NW> &P, SolverReg
     if (rollback) {
         S.stop = stop;
         S.T = S.old;
-        if (!ALL && lane == 0) {
+        if (lane == 0) {
             P.T = S.T;
             P.brk = 1;
         }
@@ -1175,14 +1171,7 @@ __device__ __forceinline__ bool align_solver_step(AlignPairLds<NW> &P, SolverReg
     S.old = S.T;
     S.T = Tn;
     S.chi2 = new_chi2;
-    if (ALL) {  // wave-uniform: SGPRs, off the feature waves' VGPR budget
-#pragma unroll
-        for (int i = 0; i < 4; i++) S.T.q[i] = uniform_f(S.T.q[i]);
-#pragma unroll
-        for (int i = 0; i < 3; i++) S.T.t[i] = uniform_f(S.T.t[i]);
-        S.chi2 = uniform_f(S.chi2);
-    }
-    if (!ALL && lane == 0) {
+    if (lane == 0) {
         P.T = Tn;
         P.brk = brk ? 1 : 0;
     }
@@ -1403,9 +1392,6 @@ __device__ __forceinline__ void align_feat_residual(const AlignFeat &F, const Al
     }
 }
 
-#ifndef YGZ_ALIGN_ALLSOLVE
-#define YGZ_ALIGN_ALLSOLVE 0  // experiment: every wave runs the Gauss-Newton step (no publish barrier)
-#endif
 // One frame pair per workgroup: wave 0 solves, waves 1..NW-1 own one feature per lane.
 // The next level's reference patches, gradients and H are set up by the feature waves
 // in the first iteration's solver window (between barriers A and B: they depend on the
@@ -1429,19 +1415,9 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
     __shared__ LmState s_lm[METHOD == 1 ? 1 : 1];  // read by METHOD 1 (Levenberg-Marquardt) only
     __shared__ float s_part_next[NW][32];  // the next level's H partials
     __shared__ float s_patch[2][16][NF];   // ref_patch_cache_ of the owned features, this level / the next
-#if YGZ_ALIGN_ALLSOLVE
-    // every wave solves (align_solver_step<NW, true>): residual partials, out-of-bounds
-    // H_f partials and tags double-buffered by iteration parity
-    __shared__ float s_rpart[2][NW][32];
-    __shared__ float s_opart[2][NW][24];
-    __shared__ int s_outit[2];
-#endif
     const AlignJob &job = jobs[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) align_pair_init(P, job);
-#if YGZ_ALIGN_ALLSOLVE
-    if (tid == 0) s_outit[0] = s_outit[1] = -1;
-#endif
     YGZ_STAMP_INIT();
     __syncthreads();
     YGZ_STAMP(9);
@@ -1487,91 +1463,6 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
         if (tid == 0) lm_result(s_lm[0], out + blockIdx.x);
         return;
     }
-#if YGZ_ALIGN_ALLSOLVE
-    if (METHOD == 0) {
-        SolverRegs S;
-        for (int i = 0; i < 4; i++) S.T.q[i] = job.T_init.q[i];
-        for (int i = 0; i < 3; i++) S.T.t[i] = job.T_init.t[i];
-        S.chi2 = 1e10f;
-        S.stop = false;
-        S.mreg = 0.f;
-        if (wave == 0) {
-            for (int level = job.max_level; level >= job.min_level; level--) {
-                S.old = S.T;
-                __syncthreads();  // L0: level start, the level's H partials are in
-                YGZ_STAMP(1);
-                if (level == job.max_level) {
-                    align_sum_hvis(P, lane);
-                } else if (lane < 21) {
-                    float r = 0.f;
-                    for (int w = 1; w < NW; w++) r += s_part_next[w][lane];
-                    P.Hvis[lane] = r;
-                }
-                __syncthreads();  // L0b: part free again
-                S.mreg = align_level_inverse(P, lane);  // beside the first residual pass
-                YGZ_STAMP(2);
-                for (int it = 0; it < 10; it++) {
-                    const int gi = level * 16 + it, b = gi & 1;
-                    __syncthreads();  // A: partials written
-                    YGZ_STAMP(3);
-                    const bool brk = align_solver_step<NW, true>(P, S, it, gi, lane, s_rpart[b], s_opart[b],
-                                                                 &s_outit[b], true);
-                    YGZ_STAMP(4);
-                    if (brk) break;
-                }
-                __syncthreads();  // L1: level end
-                YGZ_STAMP(5);
-            }
-            YGZ_STAMP_FLUSH();
-            if (tid == 0) {
-                P.T = S.T;
-                P.chi2 = S.chi2;
-                align_pair_result(P, out + blockIdx.x);
-            }
-            return;
-        }
-        const int f = tid - 64;
-        AlignFeat F;
-        AlignLevelData D, Dn;
-        align_feat_load(F, D, job, f);
-#pragma unroll
-        for (int p = 0; p < 16; p++) { s_patch[0][p][f] = 0.f; s_patch[1][p][f] = 0.f; }
-        int cb = 0;
-        for (int level = job.max_level; level >= job.min_level; level--) {
-            if (level == job.max_level) {
-                align_feat_precompute<NF, NW>(F, false, D, lv, cam, job.ref_pyr, level, s_patch[cb], s_patch[cb], f,
-                                              P.part, wave, lane);
-            } else {
-                D = Dn;
-                cb ^= 1;
-            }
-            S.old = S.T;
-            __syncthreads();  // L0
-            __syncthreads();  // L0b
-            for (int it = 0; it < 10; it++) {
-                const int gi = level * 16 + it, b = gi & 1;
-                YGZ_STAMP_AT(11, tid == 64);
-                align_feat_residual<NF, NW>(F, D, S.T, lv, cam, job.cur_pyr, level, s_patch[cb], f, s_rpart[b],
-                                            s_opart[b], &s_outit[b], gi, wave, lane);
-                YGZ_STAMP_AT(12, tid == 64);
-                YGZ_STAMP_AT(13, tid == 1023);
-                __syncthreads();  // A
-                if (it == 0) {
-                    const int r = lane >> 3, c = lane & 7;
-                    S.mreg = (r < 6 && c < 6) ? P.M[r * 6 + c] : 0.f;
-                }
-                const bool brk = align_solver_step<NW, true>(P, S, it, gi, lane, s_rpart[b], s_opart[b],
-                                                             &s_outit[b], false);
-                if (it == 0 && level > job.min_level)  // the next level, after this step
-                    align_feat_precompute<NF, NW>(F, D.vis, Dn, lv, cam, job.ref_pyr, level - 1, s_patch[cb ^ 1],
-                                                  s_patch[cb], f, s_part_next, wave, lane);
-                if (brk) break;
-            }
-            __syncthreads();  // L1
-        }
-        return;
-    }
-#endif
     if (wave == 0) {
         SolverRegs S;
         for (int i = 0; i < 4; i++) S.T.q[i] = job.T_init.q[i];
@@ -1595,8 +1486,8 @@ __global__ __launch_bounds__(NT) void k_sparse_align_reg(AlignLevels lv, ygzfe_c
             for (int it = 0; it < 10; it++) {
                 __syncthreads();  // A: partials written
                 YGZ_STAMP(3);
-                const bool brk = align_solver_step<NW, false>(P, S, it, level * 16 + it, lane, P.part, P.opart,
-                                                              &P.out_it, true);
+                const bool brk = align_solver_step<NW>(P, S, it, level * 16 + it, lane, P.part, P.opart, &P.out_it,
+                                                      true);
                 __syncthreads();  // B: pose / decision published
                 YGZ_STAMP(4);
                 if (brk) break;

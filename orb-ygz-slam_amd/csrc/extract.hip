@@ -1019,6 +1019,58 @@ __device__ __forceinline__ void radix_pass(CP src_c, IP src_i, CP dst_c, IP dst_
     __syncthreads();
 }
 
+// radix_pass without the index array: one stable LSD pass of 32-bit codes
+template <int NT>
+__device__ __forceinline__ void radix_pass_codes(const uint32_t *src, uint32_t *dst, int s0, int s1, int sh, int db,
+                                                 uint32_t *hist, Scal &Sc) {
+    constexpr int NW = nwaves<NT>();
+    const int lane = lane_id(), w = threadIdx.x >> 6, nb = 1 << db;
+    uint32_t *hw = hist + w * 256;
+    for (int d = lane; d < nb; d += 64) hw[d] = 0u;
+    for (int k0 = s0; k0 < s1; k0 += 64) {
+        const int k = k0 + lane;
+        const bool v = k < s1;
+        const uint32_t dg = v ? (src[k] >> sh) & (uint32_t)(nb - 1) : 0u;
+        const uint64_t peers = match_bits(dg, db, __ballot(v));
+        if (v && (peers & lanes_below()) == 0) hw[dg] += (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    {
+        const int d = threadIdx.x;
+        int sum = 0;
+        if (d < nb)
+            for (int ww = 0; ww < NW; ww++) sum += (int)hist[ww * 256 + d];
+        int tot;
+        const int base = block_excl_scan<NT>(d < nb ? sum : 0, Sc.red, &tot);
+        if (d < nb) {
+            int run = base;
+            for (int ww = 0; ww < NW; ww++) {
+                const int c = (int)hist[ww * 256 + d];
+                hist[ww * 256 + d] = (uint32_t)run;
+                run += c;
+            }
+        }
+    }
+    __syncthreads();
+    for (int k0 = s0; k0 < s1; k0 += 64) {
+        const int k = k0 + lane;
+        const bool v = k < s1;
+        uint32_t c = 0u, dg = 0u;
+        if (v) {
+            c = src[k];
+            dg = (c >> sh) & (uint32_t)(nb - 1);
+        }
+        const uint64_t peers = match_bits(dg, db, __ballot(v));
+        const uint32_t base = v ? hw[dg] : 0u;
+        if (v) {
+            const uint64_t below = peers & lanes_below();
+            dst[base + (uint32_t)__popcll(below)] = c;
+            if (below == 0) hw[dg] = base + (uint32_t)__popcll(peers);
+        }
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ int lcp_depth(uint32_t a, uint32_t b, int rb) {
     const uint32_t x = a ^ b;
     if (x == 0u) return 14;  // equal codes: not separated (Dn <= 14: flagged by the caller)
@@ -1175,6 +1227,9 @@ __device__ __forceinline__ void body_sort(const Plan *__restrict__ plan, const L
 // list from the histograms of L, the final rounds, the retained keys.  Lc: L of the
 // sorted keys (i8 [n + 1]); key_at(k) -> {key, candidate index} of sorted key k;
 // lsm: ListLayout<NC> (L not in it).
+#ifndef YGZ_OCT_CAND_RADIX
+#define YGZ_OCT_CAND_RADIX 1  // the final rounds' candidate order by radix passes (0: the rank sort)
+#endif
 template <int NC, int NT, typename LP, typename KF>
 __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const LevelDesc &L, int l, int f,
                                           uint8_t *lsm, Scal &Sc, LP Lc, int n, int bad, KF key_at,
@@ -1192,6 +1247,7 @@ __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const L
         Sc.hL[tid] = 0;
         Sc.hM[tid] = 0;
     }
+    if (YGZ_OCT_CAND_RADIX && tid == 0) Sc.s[2] = 0;
     __syncthreads();
     auto chunk_ab = [&](int i, int k, int &a, int &b) {
         (void)i;
@@ -1350,10 +1406,31 @@ __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const L
             int tot;
             const int ex = block_excl_scan<NT>(cand ? 1 : 0, Sc.red, &tot);
             if (cand) ck[nc + ex] = ((0xFFFFu - (r >> 16)) << 16) | (uint32_t)p;
+            if (YGZ_OCT_CAND_RADIX && cand && (r >> 16) >= 256u) Sc.s[2] = 1;  // a node of >= 256 keys
             nc += tot;
         }
         if (tid < 4) ck[nc + tid] = 0xFFFFFFFFu;  // pad to a multiple of 4 (never smaller)
         __syncthreads();
+#if YGZ_OCT_CAND_RADIX
+        if constexpr (NW * 1024 <= 4 * NC) {
+            // the candidates are in list-position order already, so (count desc, position asc)
+            // is a stable sort on 0xFFFF - count: one 8-bit LSD pass (bits 16-23), a second
+            // (bits 24-31) only when a node holds >= 256 keys
+            uint32_t *tmp = reinterpret_cast<uint32_t *>(lsm + Lay::kCe);   // cev + cin: written after
+            uint32_t *hist = reinterpret_cast<uint32_t *>(lsm + Lay::kHs);  // hs + ngr: free after step 5
+            const int cseg = (((nc + NW - 1) / NW) + 63) & ~63;
+            const int c0 = min(nc, w * cseg), c1 = min(nc, c0 + cseg);
+            const bool big = Sc.s[2] != 0;
+            radix_pass_codes<NT>(ck, tmp, c0, c1, 16, 8, hist, Sc);
+            if (big) {
+                radix_pass_codes<NT>(tmp, ck, c0, c1, 24, 8, hist, Sc);
+            } else {
+                for (int c = tid; c < nc; c += NT) ck[c] = tmp[c];
+                __syncthreads();
+            }
+            if (tid == 0) Sc.s[2] = 0;
+        } else
+#endif
         {   // ascending by rank (distinct keys): one barrier, broadcast 16-B reads
             constexpr int kPer = (NC + NT - 1) / NT;
             uint32_t mine[kPer];
@@ -1902,24 +1979,16 @@ struct IcWindow {
 // address) & 15 of LDS row r); every tap is an LDS byte read.  Octree
 // keypoints sit >= 19 px inside the level, so the 31x31 IC window and the
 // 37x37 rotated-pattern window never leave it.
-#ifndef YGZ_ORIENT_GATHER
-#define YGZ_ORIENT_GATHER 0  // experiment: rBRIEF taps gathered from the blurred level (L1/L2), only the IC
-                             // window in LDS (6 workgroups / CU) -- VERDICT r04 #5
-#endif
-#if YGZ_ORIENT_GATHER
-#define YGZ_ORIENT_WPE 6
-#define YGZ_ORIENT_SLOT 1616
-#else
-#define YGZ_ORIENT_WPE 5
-#define YGZ_ORIENT_SLOT kPatchBytes
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YGZ_ORIENT_WPE))) void k_orient_desc(const uint8_t *__restrict__ pyr,
+// (The rBRIEF taps gathered from the L1/L2-resident blurred level with only the IC window
+// in LDS, six workgroups per CU, was bit-exact but 0.84 against 0.45 ms per 1,024 frames:
+// 2.6x the TA busy cycles of the LDS form -- profiles/r05_orient_gather.txt.)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_orient_desc(const uint8_t *__restrict__ pyr,
                                                      const uint8_t *__restrict__ blur, uint32_t pitch,
                                                      const Plan *__restrict__ plan, const uint2 *__restrict__ ojobs,
                                                      const int *__restrict__ n_existing,
                                                      ygzfe_kp *__restrict__ kps, uint8_t *__restrict__ desc,
                                                      int row_cap) {
-    __shared__ uint8_t s_patch[16][YGZ_ORIENT_SLOT];  // one 37x37 window per keypoint row
+    __shared__ uint8_t s_patch[16][kPatchBytes];  // one 37x37 window per keypoint row
     // the pattern (c_pattern, 1 KB) staged once per workgroup; the IC row weights are
     // formed in registers from umax, so the workgroup's LDS is 32 KB (5 per CU)
     __shared__ uint4 s_const[64];
@@ -1941,9 +2010,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YGZ_ORIENT_
     const uint8_t *fblur = blur + (size_t)f * pitch;
     uint8_t *P = s_patch[threadIdx.x >> 4];
     IcWindow wic;
-#if !YGZ_ORIENT_GATHER
     Window<18, 37> wdesc;
-#endif
     wic.load(fimg, w, c, s);  // the rBRIEF window follows once the IC window is in LDS
     if (threadIdx.x < 64) s_const[threadIdx.x] = cst;
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
@@ -1966,9 +2033,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YGZ_ORIENT_
     float angle;
     {
         wic.store(P, s);
-#if !YGZ_ORIENT_GATHER
         wdesc.load(fblur, w, c, s);  // in flight during the IC sums
-#endif
         // IC_Angle (ORBextractor.cc:77-101): lane s takes the window rows 15 +- (s+1)
         // (lane 15 the centre row).  Per row, with I the 31 row bytes (32nd
         // weighted 0): S0 = sum of I over the disc (dot4 with the 0/1 weights),
@@ -2009,9 +2074,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YGZ_ORIENT_
         pat[q] = make_int4((int)u.x, (int)u.y, (int)u.z, (int)u.w);
     }
     wave_lds_order();  // IC taps read before the window is replaced
-#if !YGZ_ORIENT_GATHER
     wdesc.store(P, s);
-#endif
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     float ca, sb;
     glibc_sincosf(angle * factorPI, sb, ca);  // the reference's std::cos(float) / std::sin(float) = glibc cosf / sinf
@@ -2032,17 +2095,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YGZ_ORIENT_
     const f32x2 magic = {__uint_as_float(kMagicBits + 64u), __uint_as_float(kMagicBits + Pa + 64u)};
     constexpr uint32_t kFix = kMagicBits + 46u * (uint32_t)kPatchStride + 64u - 18u;
     const f32x2 rot_a = {sb, ca}, rot_b = {ca, -sb};
-#if YGZ_ORIENT_GATHER
-    (void)Pa; (void)c0; (void)w16;
-    const f32x2 magic_g = {__uint_as_float(kMagicBits + 64u), __uint_as_float(kMagicBits + 64u)};
-    const gptr_t<uint8_t> gb = as_global(fblur + c);
-    auto tap = [&](float px, float py) -> uint32_t {
-        const f32x2 m = (f32x2){py, py} * rot_b;
-        const f32x2 yx = __builtin_elementwise_fma((f32x2){px, px}, rot_a, m) + magic_g;
-        const int ry = (int)(__float_as_uint(yx.x) - kMagicBits) - 64, rx = (int)(__float_as_uint(yx.y) - kMagicBits) - 64;
-        return (uint32_t)gb[ry * (int)w + rx];
-    };
-#else
     auto tap = [&](float px, float py) -> uint32_t {
         const f32x2 m = (f32x2){py, py} * rot_b;
         const f32x2 yx = __builtin_elementwise_fma((f32x2){px, px}, rot_a, m) + magic;
@@ -2050,7 +2102,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YGZ_ORIENT_
         const uint32_t a = mad24(yb, (uint32_t)kPatchStride, xb), o = (yb & 15u) * w16 + c0;
         return (uint32_t)*(const lds_u8 *)(uintptr_t)(a + (o & 15u) - kFix);
     };
-#endif
     uint32_t bits = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {

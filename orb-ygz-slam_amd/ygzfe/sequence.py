@@ -269,7 +269,13 @@ class C5Shard:
             if self.gather:
                 self.comm.wait_stream(st)
                 with torch.cuda.stream(self.comm):
+                    if timed_gather:
+                        e0_, e1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0_.record(self.comm)
                     dist.gather(self.slots[row0:row0 + (self.slots.shape[0] // self.n_chunks)], bufs, dst=0)
+                    if timed_gather:
+                        e1_.record(self.comm)
+                        self.gather_ms.append((e0_, e1_))
         for st, sd in self.pipe_streams:
             self.stream.wait_stream(st)
             self.stream.wait_stream(sd)

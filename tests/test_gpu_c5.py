@@ -205,7 +205,8 @@ def test_c5_schedules_equal_serial(c5_full, schedule, chunks):
 
 def test_c5_rccl_gather_world1(c5_full):
     """torch.distributed over RCCL at world size 1 (the bench's N > 1 init, device_id bound):
-    the device-packed slots gathered to rank 0 equal the local slots, one batch and chunked."""
+    the device-packed slots gathered to rank 0 equal the local slots, one batch, chunked and
+    under the pipe schedule (a chunk's gather beside the next chunks' work)."""
     import torch.distributed as dist
     if dist.is_initialized():
         pytest.skip("a process group is already initialised in this process")
@@ -215,8 +216,8 @@ def test_c5_rccl_gather_world1(c5_full):
     try:
         assert dist.get_backend() == "nccl"
         full = c5_full.local_slots()
-        for chunks in (1, 4):
-            sh = C5Shard(C5_FRAMES, 0, 1, dev, chunks=chunks, gather=True)
+        for chunks, schedule in ((1, "serial"), (4, "serial"), (4, "pipe")):
+            sh = C5Shard(C5_FRAMES, 0, 1, dev, chunks=chunks, schedule=schedule, gather=True)
             sh.step(timed_gather=True)
             torch.cuda.synchronize()
             sh.check()
