@@ -79,6 +79,8 @@ typedef struct ygzfe_frame ygzfe_frame;
 
 /* ORBextractor::ORBextractor (ORBextractor.cc:412-470). */
 int ygzfe_extractor_create(const ygzfe_orb_params *p, int device, ygzfe_extractor **out);
+/* Frames borrow their extractor: destroying it while frames are alive releases it when the
+ * last of them is destroyed (any destroy order is safe, e.g. a garbage collector's). */
 void ygzfe_extractor_destroy(ygzfe_extractor *ex);
 /* GetLevels / GetScaleFactor / GetScaleFactors / GetInverseScaleFactors /
  * GetScaleSigmaSquares / GetInverseScaleSigmaSquares (ORBextractor.h:87-109).

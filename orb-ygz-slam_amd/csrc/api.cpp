@@ -274,6 +274,10 @@ using namespace ygzfe;
 struct ygzfe_extractor {
     ygzfe_orb_params p;
     int device = 0;
+    // frames borrow the extractor (its stream, mutex, plans): a destroy while frames are
+    // alive is deferred to the last frame's destroy (under graph_mutex())
+    int live_frames = 0;
+    bool dead = false;
     hipStream_t stream = nullptr;
     ScaleInfo scales;
     std::map<std::pair<int, int>, std::unique_ptr<PlanDev>> plans;
@@ -519,9 +523,7 @@ int ygzfe_extractor_create(const ygzfe_orb_params *p, int device, ygzfe_extracto
     return YGZFE_OK;
 }
 
-void ygzfe_extractor_destroy(ygzfe_extractor *ex) {
-    if (!ex) return;
-    std::lock_guard<std::recursive_mutex> lk(graph_mutex());
+static void extractor_release(ygzfe_extractor *ex) {
     (void)hipSetDevice(ex->device);
     if (ex->stream) (void)hipStreamSynchronize(ex->stream);
     for (int i = 0; i < 3; i++) {
@@ -542,6 +544,16 @@ void ygzfe_extractor_destroy(ygzfe_extractor *ex) {
     ex->plans.clear();
     if (ex->stream) (void)hipStreamDestroy(ex->stream);
     delete ex;
+}
+
+void ygzfe_extractor_destroy(ygzfe_extractor *ex) {
+    if (!ex) return;
+    std::lock_guard<std::recursive_mutex> lk(graph_mutex());
+    if (ex->live_frames > 0) {  // released by the last frame (a finalizer order we do not control)
+        ex->dead = true;
+        return;
+    }
+    extractor_release(ex);
 }
 
 int ygzfe_orb_plan(const ygzfe_orb_params *p, int width, int height, int32_t *level_w, int32_t *level_h,
@@ -610,6 +622,10 @@ int ygzfe_frame_create(ygzfe_extractor *ex, int width, int height, ygzfe_frame *
     f->H = height;
     YGZ_TRY(extractor_plan(ex, width, height, &f->plan));
     YGZ_TRY(f->pyr.ensure(f->plan->hp().pyr_bytes));
+    {
+        std::lock_guard<std::recursive_mutex> g(graph_mutex());
+        ex->live_frames++;
+    }
     *out = f.release();
     return YGZFE_OK;
 }
@@ -625,7 +641,9 @@ void ygzfe_frame_destroy(ygzfe_frame *f) {
         (void)hipStreamSynchronize(f->ex->stream);
     }
     std::lock_guard<std::recursive_mutex> lk(graph_mutex());
+    ygzfe_extractor *ex = f->ex;
     delete f;
+    if (--ex->live_frames == 0 && ex->dead) extractor_release(ex);
 }
 
 static int pyramid_from_level0(ygzfe_frame *f, hipStream_t st) {
