@@ -104,6 +104,10 @@ struct DevBuf {
             return YGZFE_ENOMEM;
         }
         n = bytes;
+        // YGZFE_POISON=1 (debugging): fresh buffers start as 0xA5 bytes instead of whatever
+        // the allocator hands back, so a read-before-write shows on every run
+        static const bool poison = getenv("YGZFE_POISON") != nullptr;
+        if (poison) (void)hipMemset(p, 0xA5, bytes);
         return YGZFE_OK;
     }
     void bind(void *ext, size_t bytes) {
@@ -816,8 +820,18 @@ static int dso_max_rows(const Plan &P) {
     return 3 * (P.lv[0].w / g) * (P.lv[0].h / g);
 }
 
+// YGZFE_TRACE=1 (debugging): ygzfe_extract's steps on stderr
+static void trace_step(const char *what, long a = 0, long b = 0) {
+    static const bool on = getenv("YGZFE_TRACE") != nullptr;
+    if (on) {
+        fprintf(stderr, "[ygzfe_extract] %s %ld %ld\n", what, a, b);
+        fflush(stderr);
+    }
+}
+
 int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps_io, int n_existing, int cap,
                   uint8_t *desc, int *n_out) {
+    trace_step("enter", method, cap);
     if (!ex || !f || !n_out || n_existing < 0 || (n_existing > 0 && !kps_io)) {
         set_error("invalid argument");
         return YGZFE_EINVAL;
@@ -838,6 +852,7 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
     const int rows = n_existing + (method == YGZFE_DSO_KEYPOINT ? std::max(P.kp_cap, dso_max_rows(P)) : P.kp_cap);
     Workspace &ws = ex->ws;
     YGZ_TRY(ws.ensure(P, 1, rows));
+    trace_step("workspace", rows, P.kp_cap);
     const uint8_t *pyr = f->pyr.as<uint8_t>();
     int total = 0;
     if (method == YGZFE_ORBSLAM_KEYPOINT) {
@@ -881,10 +896,13 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
             YGZ_HIP(hipEventRecord(ex->ev_join[0], sd[0]));
             YGZ_HIP(launch_fast_merged(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(),
                                        ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), 1, st, d_err));
+            // the node-pool classes (nfeatures > ~1000 puts level 0 in a larger class than the
+            // rest) in sequence on st: a captured graph with this second fork beside the blur's
+            // crashed inside hipGraphLaunch after a long run of other work in the process
+            // (profiles/r05_graph_fork.txt); the classes' concurrency saved little
             YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
                                   ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_err,
-                                  ws.octq.as<int>(), 1, st,
-                                  &sd[1], 2, ex->ev_oct_fork, ex->ev_oct_join, true));
+                                  ws.octq.as<int>(), 1, st, nullptr, 0, nullptr, nullptr, true));
             YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_nexist, d_kps, d_count,
                                     rows, ws.ojobs.as<uint2>(), 1, st));
             YGZ_HIP(hipStreamWaitEvent(st, ex->ev_join[0], 0));  // the blurred levels
@@ -904,8 +922,10 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
         static_assert(sizeof(key) == sizeof(f->gkey), "graph key size");
         static const bool no_graph = getenv("YGZFE_NO_GRAPH") != nullptr;
         bool launched = false;
+        trace_step("staged", (long)rbytes, (long)copy);
         if (n_existing == 0 && !no_graph && !ex->graph_broken) {
             if (!f->gexec || memcmp(f->gkey, key, sizeof(key)) != 0 || f->grows != rows || f->gcopy != copy) {
+                trace_step("capture", (long)(f->gexec != nullptr), 0);
                 std::lock_guard<std::recursive_mutex> lk(graph_mutex());
                 f->drop_graph();
                 bool ok = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess;
@@ -929,9 +949,11 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
                 launched = true;
             }
         }
+        trace_step("launched", launched, 0);
         if (!launched) YGZ_TRY(enqueue());
         YGZ_HIP(hipStreamSynchronize(st));
         total = ex->hout.as<int>()[0];
+        trace_step("synced", total, ex->hout.as<int>()[1]);
         if (ex->hout.as<int>()[1]) {
             set_error("octree node pool overflow");
             return YGZFE_EINVAL;

@@ -20,6 +20,20 @@ def gpu_available():
         return False
 
 
+def _segv_trace():
+    """YGZFE_SEGV_TRACE=path/to/libsegv_trace.so (tools/segv): native backtrace on a segfault."""
+    path = os.environ.get("YGZFE_SEGV_TRACE")
+    if path:
+        import ctypes
+        ctypes.CDLL(path).segv_trace_install()
+
+
+@pytest.fixture(autouse=True)
+def _segv_trace_each():
+    _segv_trace()  # re-installed per test: a runtime may have replaced the handler
+    yield
+
+
 @pytest.fixture(scope="session")
 def gpu():
     import ygzfe
