@@ -59,7 +59,7 @@ def main(pmc_dir, steps, frames=None, bench=None):
            "correction": "FETCH_SIZE x2 (gfx950), KiB -> B", "per_step": out}
     if frames:
         stage_ms = json.load(open(bench))["roofline"]["stages_ms"] if bench else {}
-        fb = json.load(open(bench))["roofline"]["frames_per_launch"] if bench else frames
+        fb = frames  # stages_ms are per step (the sum over a step's chunk launches): frames per step
         pf = {}
         for st, v in out.items():
             d = {"traffic_bytes": v["traffic_bytes"] / frames, "valu_insts": v["valu_insts"] / frames}
