@@ -115,52 +115,6 @@ __device__ void se3_exp(const float a[6], SE3 &out) {
     for (int i = 0; i < 4; i++) out.q[i] = q[i];
 }
 
-// se3_exp with the four transcendentals evaluated in parallel lanes (lane 0:
-// sincos(theta/2), lane 1: sincos(theta), hardware sin/cos) and broadcast by
-// readlane; every lane of the calling wave must be active and pass the same argument.
-__device__ void se3_exp_wave(const float a[6], SE3 &out) {
-#pragma clang fp contract(fast)  // solver wave: fused products (rounding-level, pose parity 1e-4)
-    const float eps = 1e-5f;
-    const float w0 = a[3], w1 = a[4], w2 = a[5];
-    const float theta_sq = w0 * w0 + w1 * w1 + w2 * w2;
-    const float theta = sqrtf(theta_sq);
-    const float half_theta = 0.5f * theta;
-    // hardware v_sin/v_cos (GN increments are small angles; the pose parity is 1e-4)
-    const float arg = (threadIdx.x & 1) ? theta : half_theta;
-    const float sn = __sinf(arg), cs = __cosf(arg);
-    const float s_half = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sn), 0));
-    const float c_half = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cs), 0));
-    const float s_th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sn), 1));
-    const float c_th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cs), 1));
-    float imag, real;
-    const float inv_theta = __builtin_amdgcn_rcpf(theta);  // 1 ulp: pose parity is 1e-4
-    if (theta < eps) {
-        const float theta_po4 = theta_sq * theta_sq;
-        imag = 0.5f - (float)(1.0 / 48.0) * theta_sq + (float)(1.0 / 3840.0) * theta_po4;
-        real = 1.f - 0.5f * theta_sq + (float)(1.0 / 384.0) * theta_po4;
-    } else {
-        imag = s_half * inv_theta;
-        real = c_half;
-    }
-    const float q[4] = {imag * w0, imag * w1, imag * w2, real};
-    const float O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
-    float V[9];
-    if (theta < eps) {
-        quat_to_mat(q, V);
-    } else {
-        float O2[9];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++)
-                O2[i * 3 + j] = O[i * 3 + 0] * O[0 * 3 + j] + O[i * 3 + 1] * O[1 * 3 + j] + O[i * 3 + 2] * O[2 * 3 + j];
-        const float inv_sq = inv_theta * inv_theta;
-        const float c1 = (1.f - c_th) * inv_sq;
-        const float c2 = (theta - s_th) * (inv_sq * inv_theta);
-        for (int i = 0; i < 9; i++) V[i] = ((i % 4 == 0) ? 1.f : 0.f) + c1 * O[i] + c2 * O2[i];
-    }
-    for (int i = 0; i < 3; i++) out.t[i] = V[i * 3 + 0] * a[0] + V[i * 3 + 1] * a[1] + V[i * 3 + 2] * a[2];
-    for (int i = 0; i < 4; i++) out.q[i] = q[i];
-}
-
 // Row-major upper-triangle index of (i, j): the lane order of the H components
 // (lane 8 + hpack6) in the solver wave.
 __device__ __forceinline__ int hpack6(int i, int j) {
@@ -393,29 +347,11 @@ __device__ __forceinline__ void ldlt_solve6_reg(const float Hin[36], const float
 
 __device__ __forceinline__ float wmul(double a, double b) { return (float)(a * b); }
 
-// Row gathers for the 7x7 reference / 5x5 current windows: a feature window
-// sits at an arbitrary byte offset, so a lane reads whole dwords from the
-// enclosing 4-byte boundary and realigns them with v_alignbyte: one
-// dwordx3 / dwordx2 load per row instead of 7 / 5 scattered byte loads
-// (each byte load of a wave touches up to 64 distinct cache lines).
-// Frame pyramids carry >= 64 bytes of tail padding for the over-read.
-template <int N>
-__device__ __forceinline__ void load_row(const uint8_t *p, float (&out)[N]) {
-    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
-    const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(p - sh));
-    constexpr int ND = (N + 3 + 3) / 4;  // dwords covering [p, p+N) for any sh <= 3
-    uint32_t d[ND + 1];
-#pragma unroll
-    for (int i = 0; i < ND; i++) d[i] = q[i];
-    d[ND] = 0;
-#pragma unroll
-    for (int w = 0; w * 4 < N; w++) {
-        const uint32_t v = __builtin_amdgcn_alignbyte(d[w + 1], d[w], sh);
-#pragma unroll
-        for (int b = 0; b < 4 && w * 4 + b < N; b++) out[w * 4 + b] = (float)((v >> (8 * b)) & 0xFFu);
-    }
-}
-
+// Row gathers for the 7x7 reference / 5x5 current windows: a feature window sits at an
+// arbitrary byte offset, so a lane reads whole dwords from the enclosing 4-byte boundary
+// and realigns them with v_alignbyte (one 12- / 8-byte buffer load per row instead of
+// 7 / 5 scattered byte loads).  Frame pyramids carry >= 64 bytes of tail padding for the
+// over-read.
 // five bytes at byte offset `off` of a buffer as floats: one 8-byte buffer load from
 // the enclosing dword boundary (32-bit offsets: no 64-bit address arithmetic per row)
 __device__ __forceinline__ void load_row5_buf(__amdgpu_buffer_rsrc_t rs, uint32_t off, float (&out)[5]) {
@@ -435,19 +371,6 @@ __device__ __forceinline__ void load_row7_packed_buf(__amdgpu_buffer_rsrc_t rs, 
     const auto d = __builtin_amdgcn_raw_buffer_load_b96(rs, off - sh, 0, 0);
     out[0] = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
     out[1] = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
-}
-
-template <int N>
-__device__ __forceinline__ void load_row_packed(const uint8_t *p, uint32_t (&out)[(N + 3) / 4]) {
-    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
-    const gptr_t<uint32_t> q = as_global(reinterpret_cast<const uint32_t *>(p - sh));
-    constexpr int ND = (N + 3 + 3) / 4;
-    uint32_t d[ND + 1];
-#pragma unroll
-    for (int i = 0; i < ND; i++) d[i] = q[i];
-    d[ND] = 0;
-#pragma unroll
-    for (int w = 0; w < (N + 3) / 4; w++) out[w] = __builtin_amdgcn_alignbyte(d[w + 1], d[w], sh);
 }
 
 // ------------------------------------------------------------------ sparse align
@@ -891,20 +814,9 @@ extern "C" int ygzfe_diag_stamps(unsigned long long *out, int cap) {
 #define YGZ_STAMP_FLUSH() do {} while (0)
 #endif
 
-// Wave sum with DPP row operations (no LDS traffic, one temporary per value):
-// quad swaps, half-row / row mirrors, then row_bcast15 / row_bcast31.  The
-// total lands in lane 63.
+// DPP lane permutation of a float (update_dpp with the old value 0)
 #define YGZ_DPP(v, ctrl, rmask) \
     __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, rmask, 0xF, false))
-__device__ __forceinline__ float wave_sum_dpp(float v) {
-    v += YGZ_DPP(v, 0xB1, 0xF);   // quad_perm [1,0,3,2]
-    v += YGZ_DPP(v, 0x4E, 0xF);   // quad_perm [2,3,0,1]
-    v += YGZ_DPP(v, 0x141, 0xF);  // row_half_mirror
-    v += YGZ_DPP(v, 0x140, 0xF);  // row_mirror
-    v += YGZ_DPP(v, 0x142, 0xA);  // row_bcast:15 -> rows 1,3
-    v += YGZ_DPP(v, 0x143, 0xC);  // row_bcast:31 -> rows 2,3
-    return v;
-}
 
 // Transposing wave reductions (every lane active).  A step pairs two values
 // and two lane sets: the lanes of one set keep the sum of value x over both
