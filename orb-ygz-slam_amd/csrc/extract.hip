@@ -1227,6 +1227,9 @@ __device__ __forceinline__ void body_sort(const Plan *__restrict__ plan, const L
 // list from the histograms of L, the final rounds, the retained keys.  Lc: L of the
 // sorted keys (i8 [n + 1]); key_at(k) -> {key, candidate index} of sorted key k;
 // lsm: ListLayout<NC> (L not in it).
+#ifndef YGZ_OCT_SEGSCAN
+#define YGZ_OCT_SEGSCAN 1  // the final rounds' scans over a contiguous run of items per thread (0: strided)
+#endif
 #ifndef YGZ_OCT_CAND_RADIX
 #define YGZ_OCT_CAND_RADIX 1  // the final rounds' candidate order by radix passes (0: the rank sort)
 #endif
@@ -1399,6 +1402,25 @@ __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const L
         uint8_t *dd = ndep + cur * NC, *dn = ndep + (cur ^ 1) * NC;
         // candidates: front nodes with > 1 key, key (count desc, position asc)
         int nc = 0;
+#if YGZ_OCT_SEGSCAN
+        {   // a contiguous run of nodes per thread: one block scan for the whole front
+            const int per = (front + NT - 1) / NT;
+            const int b0 = min(front, tid * per), b1 = min(front, b0 + per);
+            int cnt = 0;
+            for (int p = b0; p < b1; p++) cnt += (nd[p] >> 16) > 1u ? 1 : 0;
+            int tot;
+            int o = block_excl_scan<NT>(cnt, Sc.red, &tot);
+            for (int p = b0; p < b1; p++) {
+                const uint32_t r = nd[p];
+                if ((r >> 16) > 1u) {
+                    ck[o++] = ((0xFFFFu - (r >> 16)) << 16) | (uint32_t)p;
+                    if (YGZ_OCT_CAND_RADIX && (r >> 16) >= 256u) Sc.s[2] = 1;
+                }
+            }
+            nc = tot;
+        }
+        if (false)
+#endif
         for (int p0 = 0; p0 < front; p0 += NT) {
             const int p = p0 + tid;
             const uint32_t r = p < front ? nd[p] : 0u;
@@ -1478,6 +1500,33 @@ __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const L
         }
         __syncthreads();
         // cut: first c with size + sum_{c' <= c} (e - 1) >= N; one scan carries both sums
+#if YGZ_OCT_SEGSCAN
+        {
+            const int per = (nc + NT - 1) / NT;
+            const int b0 = min(nc, tid * per), b1 = min(nc, b0 + per);
+            int sE = 0, sD = 0;
+            for (int c = b0; c < b1; c++) {
+                const int e = (int)cev[c];
+                sE += e;
+                sD += e - 1;
+            }
+            int tot;
+            const int ex = block_excl_scan<NT>((sE << 16) | sD, Sc.red, &tot);
+            int runE = ex >> 16, runD = ex & 0xFFFF;
+            bool hit = false;
+            for (int c = b0; c < b1; c++) {
+                const int e = (int)cev[c];
+                runE += e;
+                cin[c] = (uint16_t)runE;
+                if (!hit && size + runD + (e - 1) >= N) {
+                    atomicMin(&Sc.s[0], c);
+                    hit = true;
+                }
+                runD += e - 1;
+            }
+        }
+        if (false)
+#endif
         {
             int carryE = 0, carryD = 0;
             for (int c0 = 0; c0 < nc; c0 += NT) {
@@ -1522,6 +1571,24 @@ __device__ __forceinline__ void body_list(const Plan *__restrict__ plan, const L
         }
         __syncthreads();
         // the other nodes keep their order behind the new front
+#if YGZ_OCT_SEGSCAN
+        {
+            const int per = (size + NT - 1) / NT;
+            const int b0 = min(size, tid * per), b1 = min(size, b0 + per);
+            int cnt = 0;
+            for (int p = b0; p < b1; p++) cnt += (dd[p] & 0x80) ? 0 : 1;
+            int tot;
+            int o = ctot + block_excl_scan<NT>(cnt, Sc.red, &tot);
+            for (int p = b0; p < b1; p++) {
+                if (!(dd[p] & 0x80)) {
+                    nn[o] = nd[p];
+                    dn[o] = dd[p];
+                    o++;
+                }
+            }
+        }
+        if (false)
+#endif
         {
             int carry = 0;
             for (int p0 = 0; p0 < size; p0 += NT) {
