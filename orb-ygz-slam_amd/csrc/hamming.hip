@@ -21,7 +21,7 @@ namespace ygzfe {
 // inside an operand is free as long as A and B agree: k-step s, lane half h
 // carries descriptor bits [32 s + 16 h, 32 s + 16 h + 16).
 //
-// A workgroup serves kHamWaves x 32 queries and streams the train set in
+// A workgroup serves kHamWaves x kHamGroups x 32 queries and streams the train set in
 // 32-row tiles; each tile is expanded to bytes once into LDS (double buffered,
 // by the first 256 threads) and read by all waves.  Per lane the running best /
 // second best are keys
@@ -33,11 +33,23 @@ namespace ygzfe {
 // and a wave-uniform (SGPR) index base: inside the loop the index omits the
 // lane half's row offset 4h, which is added once before the two halves merge
 // (a constant per lane, so it keeps each lane's order).
+// Each wave carries kHamGroups query groups of 32 (its B operands in registers), so
+// every A operand read from LDS feeds kHamGroups MFMAs: with one group per wave the
+// LDS reads of the train tiles (1 KB per wave per MFMA) matched the matrix cores'
+// time per CU.  Two groups x 4 waves (121 VGPRs, 4 waves / SIMD): 1,023 pairs of 936
+// rows 0.258 -> 0.245 ms, C5 stage 2.86 -> 2.69 ms (profiles/r05/hamming_groups/);
+// 2 x 8 and 4 x 4 measured slower.  The kernel stays ~2.5x its MFMA floor: ~10 VALU
+// per MFMA (keys + tile expansion) and 42 % of wave cycles waiting on LDS / loads.
 #ifndef YGZ_HAM_WAVES
-#define YGZ_HAM_WAVES 8
+#define YGZ_HAM_WAVES 4
+#endif
+#ifndef YGZ_HAM_GROUPS
+#define YGZ_HAM_GROUPS 2
 #endif
 constexpr int kHamWaves = YGZ_HAM_WAVES;     // query waves per workgroup
-constexpr int kHamQPB = 32 * kHamWaves;      // queries per workgroup
+constexpr int kHamGroups = YGZ_HAM_GROUPS;   // 32-query groups per wave
+constexpr int kHamQPB = 32 * kHamGroups * kHamWaves;  // queries per workgroup
+static_assert(kHamWaves >= 4, "the 256 staging threads of a train tile");
 constexpr int kHamRowBytes = 256 + 16;       // expanded train row + pad (conflict-free b128 reads)
 constexpr int kHamTileBytes = 32 * kHamRowBytes;
 constexpr uint32_t kHamNone = 0xFFFFFFFFu;
@@ -84,13 +96,16 @@ __device__ __forceinline__ void ham_expand_store(uint8_t *s_tile, int row, int s
 __device__ __forceinline__ void hamming_block_mfma(const uint8_t *__restrict__ q, int nq, const uint8_t *__restrict__ t, int nt,
                                    int32_t *__restrict__ bi_out, int32_t *__restrict__ bd_out,
                                    int32_t *__restrict__ sd_out, int qblock) {
+    constexpr int G = kHamGroups;
     __shared__ __attribute__((aligned(16))) uint8_t s_tile[2][kHamTileBytes];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-    const int qi = qblock * kHamQPB + wave * 32 + (lane & 31);
+    // group g of this lane: query qi0 + 32 g
+    const int qw = qblock * kHamQPB + wave * 32 * G, qi0 = qw + (lane & 31);
     // query operands: +1 / -1 bytes of this lane's half of each descriptor dword
-    ham_v4i bq[8];
-    int pq = 0;
-    {
+    ham_v4i bq[G][8];
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        const int qi = qi0 + 32 * g;
         uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (qi < nq) {
             const uint4 *qp = reinterpret_cast<const uint4 *>(q + (size_t)qi * 32);
@@ -100,71 +115,94 @@ __device__ __forceinline__ void hamming_block_mfma(const uint8_t *__restrict__ q
         }
 #pragma unroll
         for (int s = 0; s < 8; s++) {
-            pq += __popc(w[s]);
             const uint32_t half = (w[s] >> (16 * h)) & 0xFFFFu;
 #pragma unroll
             for (int m = 0; m < 4; m++) {
-                const uint32_t e = nib_bytes(half, m);         // 0 / 1 per byte
-                bq[s][m] = (int)(((e << 8) - e) | 0x01010101u);  // 0 -> +1, 1 -> -1 (0xFF)
+                const uint32_t e = nib_bytes(half, m);            // 0 / 1 per byte
+                bq[g][s][m] = (int)(((e << 8) - e) | 0x01010101u);  // 0 -> +1, 1 -> -1 (0xFF)
             }
         }
     }
-    uint32_t k1 = kHamNone, k2 = kHamNone;
-    // waves whose 32 queries all lie past nq only stage tiles
-    const bool active = qblock * kHamQPB + wave * 32 < nq;
+    uint32_t k1[G], k2[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) k1[g] = k2[g] = kHamNone;
+    // waves whose queries all lie past nq only stage tiles
+    const bool active = qw < nq;
     const int ntiles = (nt + 31) >> 5;
     // staging (threads < 256): thread -> (row tid >> 3, dword tid & 7) of a 32-row tile
     const int srow = tid >> 3, sdw = tid & 7;
     const bool stager = tid < 256;
+    // branch-free buffer loads: rows past nt (and tiles past the last) read 0, and no
+    // load sits under an exec branch, so the wait counts before each expansion stay exact
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void *)t, 0, nt * 32, 0x00020000);
     auto fetch = [&](int tile) -> uint32_t {
-        const int row = tile * 32 + srow;
-        return stager && row < nt ? reinterpret_cast<const uint32_t *>(t + (size_t)row * 32)[sdw] : 0u;
+        return __builtin_amdgcn_raw_buffer_load_b32(rt, (uint32_t)(tile * 32 + srow) * 32u + 4u * (uint32_t)sdw, 0, 0);
     };
-    if (ntiles > 0 && stager) ham_expand_store(s_tile[0], srow, sdw, fetch(0));
-    __syncthreads();
-    for (int tile = 0; tile < ntiles; tile++) {
+    // tile t: MFMAs on buffer t & 1, then the next tile's dwords (fetched earlier)
+    // expanded into the other buffer, then one barrier
+    auto tile_step = [&](int tile, uint32_t nxt) {
         const uint8_t *L = s_tile[tile & 1];
-        const bool more = tile + 1 < ntiles;
-        const uint32_t nxt = more ? fetch(tile + 1) : 0u;  // in flight during the MFMAs
         if (active) {
-            ham_v16i acc = {};
+            ham_v16i acc[G];
+#pragma unroll
+            for (int g = 0; g < G; g++) acc[g] = (ham_v16i){};
             const uint8_t *arow = L + (lane & 31) * kHamRowBytes + h * 16;
 #pragma unroll
             for (int s = 0; s < 8; s++) {
                 const ham_v4i a = *(const ham_v4i *)(arow + s * 32);
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[s], acc, 0, 0, 0);
+#pragma unroll
+                for (int g = 0; g < G; g++) acc[g] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[g][s], acc[g], 0, 0, 0);
             }
             const uint32_t tb = (uint32_t)tile * 32, tu = (256u << 22) + tb;
             if (tb + 32 <= (uint32_t)nt) {
 #pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const uint32_t key = ham_key(acc[r], tu, (uint32_t)((r & 3) + 8 * (r >> 2)));
-                    k2 = ham_med3(k1, key, k2);
-                    k1 = min(k1, key);
-                }
+                for (int g = 0; g < G; g++)
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+                        const uint32_t key = ham_key(acc[g][r], tu, (uint32_t)((r & 3) + 8 * (r >> 2)));
+                        k2[g] = ham_med3(k1[g], key, k2[g]);
+                        k1[g] = min(k1[g], key);
+                    }
             } else {  // partial last tile: rows past nt never win
 #pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const uint32_t row = tb + (uint32_t)((r & 3) + 8 * (r >> 2) + 4 * h);
-                    const uint32_t key =
-                        row < (uint32_t)nt ? ham_key(acc[r], tu, (uint32_t)((r & 3) + 8 * (r >> 2))) : kHamNone;
-                    k2 = ham_med3(k1, key, k2);
-                    k1 = min(k1, key);
-                }
+                for (int g = 0; g < G; g++)
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+                        const uint32_t row = tb + (uint32_t)((r & 3) + 8 * (r >> 2) + 4 * h);
+                        const uint32_t key =
+                            row < (uint32_t)nt ? ham_key(acc[g][r], tu, (uint32_t)((r & 3) + 8 * (r >> 2))) : kHamNone;
+                        k2[g] = ham_med3(k1[g], key, k2[g]);
+                        k1[g] = min(k1[g], key);
+                    }
             }
         }
-        if (more && stager) ham_expand_store(s_tile[(tile + 1) & 1], srow, sdw, nxt);
+        if (tile + 1 < ntiles && stager) ham_expand_store(s_tile[(tile + 1) & 1], srow, sdw, nxt);
         __syncthreads();  // tile + 1 staged; tile's buffer free for tile + 2
-    }
-    // the lane half's row offset, then merge the two halves (same query, disjoint rows)
-    if (k1 != kHamNone) k1 += 4u * (uint32_t)h;
-    if (k2 != kHamNone) k2 += 4u * (uint32_t)h;
-    const uint32_t o1 = (uint32_t)__shfl_xor((int)k1, 32, 64), o2 = (uint32_t)__shfl_xor((int)k2, 32, 64);
-    const uint32_t K1 = min(k1, o1), K2 = min(max(k1, o1), min(k2, o2));
-    if (h == 0 && qi < nq) {
-        bi_out[qi] = K1 == kHamNone ? -1 : (int)(K1 & (kHamMaxTrain - 1));
-        bd_out[qi] = K1 == kHamNone ? 257 : (int)(K1 >> 22) - 256 + pq;
-        sd_out[qi] = K2 == kHamNone ? 257 : (int)(K2 >> 22) - 256 + pq;
+    };
+    if (ntiles > 0 && stager) ham_expand_store(s_tile[0], srow, sdw, fetch(0));
+    __syncthreads();
+    // one tile ahead is enough: fetching two ahead (the loop unrolled by two, so the
+    // fetch registers alternate without a copy) measured the same
+    for (int tile = 0; tile < ntiles; tile++) tile_step(tile, fetch(tile + 1));
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        // the lane half's row offset, then merge the two halves (same query, disjoint rows)
+        uint32_t a1 = k1[g], a2 = k2[g];
+        if (a1 != kHamNone) a1 += 4u * (uint32_t)h;
+        if (a2 != kHamNone) a2 += 4u * (uint32_t)h;
+        const uint32_t o1 = (uint32_t)__shfl_xor((int)a1, 32, 64), o2 = (uint32_t)__shfl_xor((int)a2, 32, 64);
+        const uint32_t K1 = min(a1, o1), K2 = min(max(a1, o1), min(a2, o2));
+        const int qi = qi0 + 32 * g;
+        if (h == 0 && qi < nq) {
+            // popc(q) read again here: not held in registers through the tile loop
+            const uint4 *qp = reinterpret_cast<const uint4 *>(q + (size_t)qi * 32);
+            const uint4 u0 = qp[0], u1 = qp[1];
+            const int pq = __popc(u0.x) + __popc(u0.y) + __popc(u0.z) + __popc(u0.w) + __popc(u1.x) + __popc(u1.y) +
+                           __popc(u1.z) + __popc(u1.w);
+            bi_out[qi] = K1 == kHamNone ? -1 : (int)(K1 & (kHamMaxTrain - 1));
+            bd_out[qi] = K1 == kHamNone ? 257 : (int)(K1 >> 22) - 256 + pq;
+            sd_out[qi] = K2 == kHamNone ? 257 : (int)(K2 >> 22) - 256 + pq;
+        }
     }
 }
 
