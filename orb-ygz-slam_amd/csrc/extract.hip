@@ -669,6 +669,32 @@ __device__ __forceinline__ uint32_t fast_screen4(uint32_t T, uint32_t B, uint32_
            (((sg[1] >> 31) & 1u) << 3);
 }
 
+// The same test with per-lane packed thresholds (t01: pixels 0 / 2, t23: 1 / 3; a pixel
+// outside the cell interior gets kFastNoTh, which no |m| <= 255 passes) and the two
+// packed results returned as they are: pixel k survives iff its half of sg[k & 1] is
+// negative (pixels 0 / 1: the low halves, 2 / 3: the high halves, so the 32-bit sign).
+#ifndef YGZ_FAST_SG
+#define YGZ_FAST_SG 1  // phase A: ballots straight from the packed signs (0: the 4-bit mask form)
+#endif
+constexpr uint32_t kFastNoTh = 0x3FFFu;
+__device__ __forceinline__ void fast_screen4_sg(uint32_t T, uint32_t B, uint32_t Lw, uint32_t Rw, uint32_t C,
+                                                uint32_t t01, uint32_t t23, uint32_t sg[2]) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int hlf = 0; hlf < 2; hlf++) {
+        const uint32_t sel = hlf ? 0x0C030C01u : 0x0C020C00u;
+        const u16x2 dT = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(T, T, sel));
+        const u16x2 dB = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(B, B, sel));
+        const u16x2 dL = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Lw, Lw, sel));
+        const u16x2 dR = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Rw, Rw, sel));
+        const u16x2 bv = __builtin_elementwise_min(__builtin_elementwise_max(dT, dB), __builtin_elementwise_max(dL, dR));
+        const u16x2 dv = __builtin_elementwise_max(__builtin_elementwise_min(dT, dB), __builtin_elementwise_min(dL, dR));
+        const s16x2 v = as_s16x2(__builtin_amdgcn_perm(C, C, sel));
+        const s16x2 m = __builtin_elementwise_max(__builtin_bit_cast(s16x2, bv) - v, v - __builtin_bit_cast(s16x2, dv));
+        sg[hlf] = as_u32(as_s16x2(hlf ? t23 : t01) - m);
+    }
+}
+
 // Segment test and score of two survivors at once (entries e = row << 8 | col on a
 // tile of row stride S), as packed pairs: with e[k] = r_k - v,
 //   arcmax = max(max_k min(e[k..k+8]), max_k min(-e[k..k+8]))
@@ -747,6 +773,46 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             const int lpr = iw <= 32 ? 8 : (iw <= 64 ? 16 : 32);  // lanes per row (4 px each)
             const int rpc = 64 / lpr;                                  // rows per chunk
             const int j = lane & (lpr - 1), rr = lane / lpr;
+#if YGZ_FAST_SG
+            // per-lane packed thresholds: pixels past the interior's columns never pass
+            const uint32_t thv = (uint32_t)th;
+            const uint32_t tc01 = (4 * j + 0 < iw ? thv : kFastNoTh) | ((4 * j + 2 < iw ? thv : kFastNoTh) << 16);
+            const uint32_t tc23 = (4 * j + 1 < iw ? thv : kFastNoTh) | ((4 * j + 3 < iw ? thv : kFastNoTh) << 16);
+            for (int y0 = 0; y0 < ih; y0 += rpc) {
+                const int y = y0 + rr;
+                const uint32_t *rt = reinterpret_cast<const uint32_t *>(img + y * S) + j;
+                const uint32_t *rc = reinterpret_cast<const uint32_t *>(img + (y + 3) * S) + j;
+                const uint32_t *rb = reinterpret_cast<const uint32_t *>(img + (y + 6) * S) + j;
+                const uint32_t D0 = rc[0], D1 = rc[1], D2 = rc[2];
+                const uint32_t C = __builtin_amdgcn_alignbyte(D1, D0, 3);   // x .. x+3
+                const uint32_t Rw = __builtin_amdgcn_alignbyte(D2, D1, 2);  // x+3 .. x+6
+                const uint32_t Tw = __builtin_amdgcn_alignbyte(rt[1], rt[0], 3);
+                const uint32_t Bw = __builtin_amdgcn_alignbyte(rb[1], rb[0], 3);
+                const bool yin = y < ih;
+                uint32_t sg[2];
+                fast_screen4_sg(Tw, Bw, D0, Rw, C, yin ? tc01 : (kFastNoTh * 0x10001u), yin ? tc23 : (kFastNoTh * 0x10001u),
+                                sg);
+                const bool b0 = (short)sg[0] < 0, b1 = (short)sg[1] < 0;
+                const bool b2 = (int)sg[0] < 0, b3 = (int)sg[1] < 0;
+                const uint64_t M0 = __ballot(b0), M1 = __ballot(b1), M2 = __ballot(b2), M3 = __ballot(b3);
+                // survivors in lanes below: one mbcnt chain (each step adds to the last)
+                uint32_t pc = __builtin_amdgcn_mbcnt_lo((uint32_t)M0, (uint32_t)na);
+                pc = __builtin_amdgcn_mbcnt_hi((uint32_t)(M0 >> 32), pc);
+                pc = __builtin_amdgcn_mbcnt_lo((uint32_t)M1, pc);
+                pc = __builtin_amdgcn_mbcnt_hi((uint32_t)(M1 >> 32), pc);
+                pc = __builtin_amdgcn_mbcnt_lo((uint32_t)M2, pc);
+                pc = __builtin_amdgcn_mbcnt_hi((uint32_t)(M2 >> 32), pc);
+                pc = __builtin_amdgcn_mbcnt_lo((uint32_t)M3, pc);
+                pc = __builtin_amdgcn_mbcnt_hi((uint32_t)(M3 >> 32), pc);
+                int pos = (int)pc;
+                na += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
+                const uint32_t e = ((uint32_t)(y + 3) << 8) | (uint32_t)(4 * j + 3);
+                if (b0) list[pos++] = (uint16_t)e;
+                if (b1) list[pos++] = (uint16_t)(e + 1u);
+                if (b2) list[pos++] = (uint16_t)(e + 2u);
+                if (b3) list[pos] = (uint16_t)(e + 3u);
+            }
+#else
             uint32_t colmask = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) colmask |= (uint32_t)(4 * j + k < iw) << k;
@@ -770,6 +836,7 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                 for (int k = 0; k < 4; k++)
                     if ((m >> k) & 1u) list[pos++] = (uint16_t)(ey | (uint32_t)(4 * j + k + 3));
             }
+#endif
         }
         if (YGZ_FAST_KO == 2) {
             total = na;
