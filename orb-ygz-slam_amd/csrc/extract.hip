@@ -695,7 +695,20 @@ __device__ __forceinline__ void fast_screen4_sg(uint32_t T, uint32_t B, uint32_t
     }
 }
 
-// Segment test and score of two survivors at once (entries e = row << 8 | col on a
+// Survivor / corner list entries: the pixel's byte offset row * S + col in the ROI tile
+// (ring taps and score-map writes take it as it is; measured the same as row << 8 | col
+// with a multiply per use, profiles/r05/fast_entry_offsets).
+template <int S>
+__device__ __forceinline__ uint32_t fast_entry(uint32_t row, uint32_t col) {
+    return row * S + col;
+}
+template <int S>
+__device__ __forceinline__ void fast_entry_xy(uint32_t e, int &x, int &y) {
+    y = (int)(e / S);
+    x = (int)e - y * S;
+}
+
+// Segment test and score of two survivors at once (list entries e, fast_entry, on a
 // tile of row stride S), as packed pairs: with e[k] = r_k - v,
 //   arcmax = max(max_k min(e[k..k+8]), max_k min(-e[k..k+8]))
 // corner (FAST_t<16>: 9 contiguous ring pixels all > v+t or all < v-t) <=> arcmax > t,
@@ -706,7 +719,7 @@ __device__ __forceinline__ void fast_screen4_sg(uint32_t T, uint32_t B, uint32_t
 template <int S>
 __device__ __forceinline__ s16x2 fast_arcmax2(const uint8_t *img, uint32_t e0, uint32_t e1) {
     // ring bases q = centre - 3S - 3: every tap an immediate, non-negative ds_read offset
-    uint32_t b0 = ((e0 >> 8) - 3) * S + (e0 & 0xFFu) - 3, b1 = ((e1 >> 8) - 3) * S + (e1 & 0xFFu) - 3;
+    uint32_t b0 = e0 - (3 * S + 3), b1 = e1 - (3 * S + 3);
     asm("" : "+v"(b0), "+v"(b1));  // taps off q (not off the centre): immediate offsets only
     const uint8_t *q0 = img + b0, *q1 = img + b1;
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -806,7 +819,7 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                 pc = __builtin_amdgcn_mbcnt_hi((uint32_t)(M3 >> 32), pc);
                 int pos = (int)pc;
                 na += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
-                const uint32_t e = ((uint32_t)(y + 3) << 8) | (uint32_t)(4 * j + 3);
+                const uint32_t e = fast_entry<S>((uint32_t)(y + 3), (uint32_t)(4 * j + 3));
                 if (b0) list[pos++] = (uint16_t)e;
                 if (b1) list[pos++] = (uint16_t)(e + 1u);
                 if (b2) list[pos++] = (uint16_t)(e + 2u);
@@ -831,10 +844,9 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                 const uint64_t M0 = __ballot(m & 1u), M1 = __ballot(m & 2u), M2 = __ballot(m & 4u), M3 = __ballot(m & 8u);
                 int pos = na + popc_below(M0) + popc_below(M1) + popc_below(M2) + popc_below(M3);
                 na += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
-                const uint32_t ey = (uint32_t)(y + 3) << 8;
 #pragma unroll
                 for (int k = 0; k < 4; k++)
-                    if ((m >> k) & 1u) list[pos++] = (uint16_t)(ey | (uint32_t)(4 * j + k + 3));
+                    if ((m >> k) & 1u) list[pos++] = (uint16_t)fast_entry<S>((uint32_t)(y + 3), (uint32_t)(4 * j + k + 3));
             }
 #endif
         }
@@ -849,11 +861,11 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             const int i = i0 + 2 * lane;
             const uint32_t pr = reinterpret_cast<const uint32_t *>(list)[i >> 1];  // list[i], list[i+1]
             const bool v0 = i < na, v1 = i + 1 < na;
-            const uint32_t e0 = v0 ? (pr & 0xFFFFu) : 0x0303u, e1 = v1 ? (pr >> 16) : 0x0303u;
+            const uint32_t e0 = v0 ? (pr & 0xFFFFu) : fast_entry<S>(3u, 3u), e1 = v1 ? (pr >> 16) : fast_entry<S>(3u, 3u);
             const s16x2 am = fast_arcmax2<S>(img, e0, e1);
             const bool c0 = v0 && am.x > th, c1 = v1 && am.y > th;
-            if (c0) sc[(e0 >> 8) * S + (e0 & 0xFFu)] = (uint8_t)(am.x - 1);
-            if (c1) sc[(e1 >> 8) * S + (e1 & 0xFFu)] = (uint8_t)(am.y - 1);
+            if (c0) sc[e0] = (uint8_t)(am.x - 1);
+            if (c1) sc[e1] = (uint8_t)(am.y - 1);
             const uint64_t M0 = __ballot(c0), M1 = __ballot(c1);
             const int pos = nc + popc_below(M0) + popc_below(M1);
             if (c0) list[pos] = (uint16_t)e0;
@@ -871,9 +883,7 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             bool keep = false;
             int s = 0, x = 0, y = 0;
             if (i < nc) {
-                const uint16_t e = list[i];
-                x = e & 0xFF;
-                y = e >> 8;
+                fast_entry_xy<S>(list[i], x, y);
                 const uint8_t *r = sc + (y - 1) * S + (x - 1);
                 s = r[S + 1];
                 // all nine reads in flight together (a short-circuit chain here
