@@ -609,28 +609,35 @@ template <int S, int R>
 struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI height)
     static constexpr int DW = S / 4, RPI = 64 / DW, NI = (R + RPI - 1) / RPI;
     uint32_t lo[NI], hi[NI];
+    // Every lane loads its dword pair of rows rlane + k RPI unconditionally (rows past the
+    // ROI, and columns past its width, land in tile bytes nothing reads; rows past the
+    // level read 0 from the buffer); row k's offset is the lane's row-0 offset plus the
+    // wave-uniform k RPI w, and its tile address an immediate offset.  Only the spare
+    // lane (rlane == RPI) and rows past the tile's R are not stored.
     __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, uint32_t off0, int w, int rw, int rh, int lane) {
-        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + 3) / 4;
+        const int rlane = lane / DW, dw = lane - rlane * DW;
+        const uint32_t f0 = mad24((uint32_t)rlane, (uint32_t)w, off0) + 4u * (uint32_t)dw;
 #pragma unroll
         for (int k = 0; k < NI; k++) {
-            const int r = k * RPI + rlane;
+            const uint32_t o = (f0 + (uint32_t)(k * RPI) * (uint32_t)w) & ~3u;
             lo[k] = hi[k] = 0u;
-            if (rlane < RPI && r < rh && dw < ndw) {
-                const uint32_t o = (mad24((uint32_t)r, (uint32_t)w, off0) & ~3u) + 4u * (uint32_t)dw;
+            if (stored(k, rlane)) {  // (a load used only under the store's condition is sunk past the others' waits)
                 lo[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0);
                 hi[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4u, 0, 0);
             }
         }
     }
+    static __device__ __forceinline__ bool stored(int k, int rlane) {
+        return rlane < RPI && (k + 1 < NI || k * RPI + RPI <= R || k * RPI + rlane < R);
+    }
     __device__ __forceinline__ void commit(uint8_t *img, uint32_t off0, int w, int rw, int rh, int lane) const {
-        const int rlane = lane / DW, dw = lane - rlane * DW, ndw = (rw + 3) / 4;
+        const int rlane = lane / DW, dw = lane - rlane * DW;
+        const uint32_t f0 = mad24((uint32_t)rlane, (uint32_t)w, off0) + 4u * (uint32_t)dw;
+        uint32_t *d = reinterpret_cast<uint32_t *>(img + rlane * S) + dw;
 #pragma unroll
         for (int k = 0; k < NI; k++) {
-            const int r = k * RPI + rlane;
-            if (rlane < RPI && r < rh && dw < ndw) {
-                const uint32_t sh = mad24((uint32_t)r, (uint32_t)w, off0) & 3u;
-                reinterpret_cast<uint32_t *>(img + r * S)[dw] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh);
-            }
+            const uint32_t sh = (f0 + (uint32_t)(k * RPI) * (uint32_t)w) & 3u;
+            if (stored(k, rlane)) d[k * RPI * DW] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh);
         }
         wave_lds_order();
     }
