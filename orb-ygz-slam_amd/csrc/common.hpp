@@ -274,25 +274,26 @@ __device__ __forceinline__ void glibc_sincosf(float y, float &sinv, float &cosv)
         cosv = glibc_sinf_poly(x * s, x * x, (n & 1) == 0, neg);
         return;
     }
-    if (top < ((__float_as_uint((float)0x1.921FB54442D18p-1) >> 20) & 0x7ffu)) {
-        if (top < ((__float_as_uint(0x1p-12f) >> 20) & 0x7ffu)) {
-            sinv = y;
-            cosv = 1.0f;
-            return;
-        }
-        const double x2 = x * x;
-        sinv = glibc_sinf_poly(x, x2, false, false);
-        cosv = glibc_sinf_poly(x, x2, true, false);
+    if (top < ((__float_as_uint(0x1p-12f) >> 20) & 0x7ffu)) {
+        sinv = y;
+        cosv = 1.0f;
         return;
     }
+    // |y| < pi/4 (glibc's first branch) is the n = 0 case of the reduction below: x * 2/pi
+    // < 0.5 gives n = 0, x - 0 * pi/2 = x, sign +1 and table 0, so one path serves both.
+    // Each polynomial is evaluated once, unsigned: the sine one is odd and the negated
+    // cosine table (table 1) negates every coefficient, so sign and table come out as
+    // exact float negations, and (n & 1) only swaps the two results.  (glibc_sinf_poly's
+    // lane-dependent branches would otherwise run both polynomials twice per wave.)
     const double r = x * 0x1.45F306DC9C883p+23;  // reduce_fast: 2/pi * 2^24, truncating conversion
     const int n = ((int32_t)r + 0x800000) >> 24;
     x = x - n * 0x1.921FB54442D18p0;
-    const double s = ((n + 1) & 2) ? -1.0 : 1.0;  // sign[n & 3] = {1, -1, -1, 1}
-    const bool neg = (n & 2) != 0;
-    const double xs = x * s, x2 = x * x;
-    sinv = glibc_sinf_poly(xs, x2, (n & 1) != 0, neg);
-    cosv = glibc_sinf_poly(xs, x2, (n & 1) == 0, neg);
+    const double x2 = x * x;
+    const float sp = glibc_sinf_poly(x, x2, false, false), cp = glibc_sinf_poly(x, x2, true, false);
+    const float ss = ((n + 1) & 2) ? -sp : sp;  // sign[n & 3] = {1, -1, -1, 1}
+    const float cs = (n & 2) ? -cp : cp;        // table 1: the cosine coefficients negated
+    sinv = (n & 1) ? cs : ss;
+    cosv = (n & 1) ? ss : cs;
 }
 
 }  // namespace ygzfe

@@ -14,6 +14,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <type_traits>
 
 #include "plan.hpp"
 
@@ -2248,26 +2249,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const f32x2 magic = {__uint_as_float(kMagicBits + 64u), __uint_as_float(kMagicBits + Pa + 64u)};
     constexpr uint32_t kFix = kMagicBits + 46u * (uint32_t)kPatchStride + 64u - 18u;
     const f32x2 rot_a = {sb, ca}, rot_b = {ca, -sb};
-    auto tap = [&](float px, float py) -> uint32_t {
-        const f32x2 m = (f32x2){py, py} * rot_b;
-        const f32x2 yx = __builtin_elementwise_fma((f32x2){px, px}, rot_a, m) + magic;
-        const uint32_t yb = __float_as_uint(yx.x), xb = __float_as_uint(yx.y);
-        const uint32_t a = mad24(yb, (uint32_t)kPatchStride, xb), o = (yb & 15u) * w16 + c0;
-        return (uint32_t)*(const lds_u8 *)(uintptr_t)(a + (o & 15u) - kFix);
-    };
-    uint32_t bits = 0;
+    // rows whose width is a multiple of 16 (C2 level 0) start at the same offset o(r) = c0
+    // in every LDS row: the tap address is then one mad24 and one add (a wave-uniform choice)
+    const uint32_t cfix = c0 - kFix;
+    auto descriptor = [&](auto aligned_rows) -> uint32_t {
+        auto tap = [&](float px, float py) -> uint32_t {
+            const f32x2 m = (f32x2){py, py} * rot_b;
+            const f32x2 yx = __builtin_elementwise_fma((f32x2){px, px}, rot_a, m) + magic;
+            const uint32_t yb = __float_as_uint(yx.x), xb = __float_as_uint(yx.y);
+            const uint32_t a = mad24(yb, (uint32_t)kPatchStride, xb);
+            if constexpr (decltype(aligned_rows)::value) {
+                return (uint32_t)*(const lds_u8 *)(uintptr_t)(a + cfix);
+            } else {
+                const uint32_t o = (yb & 15u) * w16 + c0;
+                return (uint32_t)*(const lds_u8 *)(uintptr_t)(a + (o & 15u) - kFix);
+            }
+        };
+        uint32_t b = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int4 Pq = pat[q];
-        const uint32_t wd[4] = {(uint32_t)Pq.x, (uint32_t)Pq.y, (uint32_t)Pq.z, (uint32_t)Pq.w};
+        for (int q = 0; q < 4; q++) {
+            const int4 Pq = pat[q];
+            uint32_t wd[4] = {(uint32_t)Pq.x, (uint32_t)Pq.y, (uint32_t)Pq.z, (uint32_t)Pq.w};
+            // opaque per path: the pattern's conversions are not hoisted above the path choice
+            // (both paths' 64 converted coordinates would be live there and spill)
+            asm volatile("" : "+v"(wd[0]), "+v"(wd[1]), "+v"(wd[2]), "+v"(wd[3]));
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const float px0 = (float)(int8_t)(wd[k] & 0xFF), py0 = (float)(int8_t)((wd[k] >> 8) & 0xFF);
-            const float px1 = (float)(int8_t)((wd[k] >> 16) & 0xFF), py1 = (float)(int8_t)(wd[k] >> 24);
-            const uint32_t t0 = tap(px0, py0), t1 = tap(px1, py1);
-            bits |= (uint32_t)(t0 < t1) << (q * 4 + k);
+            for (int k = 0; k < 4; k++) {
+                const float px0 = (float)(int8_t)(wd[k] & 0xFF), py0 = (float)(int8_t)((wd[k] >> 8) & 0xFF);
+                const float px1 = (float)(int8_t)((wd[k] >> 16) & 0xFF), py1 = (float)(int8_t)(wd[k] >> 24);
+                const uint32_t t0 = tap(px0, py0), t1 = tap(px1, py1);
+                b |= (uint32_t)(t0 < t1) << (q * 4 + k);
+            }
         }
-    }
+        return b;
+    };
+    // (orientation stage 0.441 -> 0.435 ms / 1,024 frames, profiles/r05/orient_sincos_taps)
+    const uint32_t bits = __ballot(w16 != 0u) == 0ull ? descriptor(std::true_type{}) : descriptor(std::false_type{});
     const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bits, 0xB1, 0xF, 0xF, false);
     const int row = ne + idx;
     if ((s & 1) == 0)
