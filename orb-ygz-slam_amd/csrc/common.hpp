@@ -21,7 +21,10 @@
 namespace ygzfe {
 
 constexpr int kMaxLevels = YGZFE_MAX_LEVELS;
-constexpr int kBlurRows = 32;  // k_blur7 strip height (plan.cpp tiles the levels with it)
+#ifndef YGZ_BLUR_ROWS
+#define YGZ_BLUR_ROWS 32
+#endif
+constexpr int kBlurRows = YGZ_BLUR_ROWS;  // k_blur7 strip height (plan.cpp tiles the levels with it)
 constexpr int kEdgeThreshold = 19;  // ORBextractor.cc:75
 constexpr int kMinBorder = kEdgeThreshold - 3;
 constexpr int kPatchSize = 31, kHalfPatch = 15;

@@ -425,11 +425,18 @@ __device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ s
 __global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(const uint8_t *__restrict__ pyr,
                                                uint8_t *__restrict__ blur, uint32_t pitch,
                                                const Plan *__restrict__ plan) {
-    const int f = blockIdx.y;
+#ifndef YGZ_BLUR_SWZ
+#define YGZ_BLUR_SWZ 1
+#endif
+    // one frame's strips on one XCD (swizzled_block_2d): the 6 halo rows a strip shares with
+    // the band below are then read again from that XCD's L2, not from HBM (blur stage 3.29 ->
+    // 3.21 ms per step; 48- and 64-row strips measured slower: profiles/r05/blur_xcd_strips)
+    int bx = blockIdx.x, f = blockIdx.y;
+    if (YGZ_BLUR_SWZ) swizzled_block_2d(bx, f);
     const int lane = threadIdx.x & 63;
     // wave-uniform strip index (readfirstlane: row indices, reflections and row
     // base addresses then live in SGPRs)
-    int task = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)), l = 0;
+    int task = __builtin_amdgcn_readfirstlane(bx * 4 + (threadIdx.x >> 6)), l = 0;
     if (task >= plan->blur_tiles) return;
     while (l + 1 < plan->nlevels && task >= plan->lv[l + 1].blur_tile_begin) l++;
     const LevelDesc &L = plan->lv[l];

@@ -1,3 +1,6 @@
+// Host-side check that glibc_sincosf (csrc/common.hpp) in its one-path form equals the
+// two-branch form it replaced, for every float |y| < 120:  gcc -O2 -fopenmp -ffp-contract=off
+// tools/sincosf_onepath_check.c -o /tmp/chk && /tmp/chk  (test infrastructure only)
 #include <stdio.h>
 #include <stdint.h>
 #include <string.h>
