@@ -1,5 +1,6 @@
 #!/bin/bash
 # pipe schedule: SparseImgAlign on its own stream at high / low priority vs on the chunk's stream
+# (record of a measured-negative experiment: the YGZFE_PIPE_ALIGN_PRIO knob was removed after it)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-r05_prio}
