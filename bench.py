@@ -897,6 +897,9 @@ def cpu_baseline(frames, r3, cz, S, args, sc):
             "ms_per_frame": round(wall1 * 1e3 / max(1, st1.frames), 3),
             "ms_pyramid": round(st1.t_pyr * per, 3), "ms_extract": round(st1.t_extract * per, 3),
             "ms_hamming": round(st1.t_hamming * perp, 3), "ms_align": round(st1.t_align * perp, 3),
+            # BENCH_r04's figure for the same leg: round 5's oracle refactor made it 3.861 ms
+            # (accumulators through aliasing pointers); oracle/align.c keeps them in locals again
+            "ms_align_r04": 1.675,
             "threads_frames_per_s": round(stt.frames / wallt, 2)}
     # FAST sanity (the CPU FAST stage must be no slower than the reference's
     # SSE2 FAST-10).  Like for like: the same FAST-10 pipeline -- detect (SSE2 variant) +

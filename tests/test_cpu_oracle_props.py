@@ -330,3 +330,25 @@ def test_search_local_points_direct_replays_the_grid():
         assert (m[~ok] == -1).all() and (px[~ok] == 0).all()
     assert (want[:n_cache] == 2).mean() >= 0.1
     assert ((want[:n_cache] == 1).sum() > 3) and (want[n_cache:] == 3).all()
+
+
+def test_align_gn_matches_round4_oracle():
+    """The GN SparseImgAlign oracle reproduces round 4's restatement bit for bit on a fixed
+    scene (tests/golden/align_gn_r04.json, made by tests/golden/make_align_gn_r04.py from
+    oracle/align.c at 651410b): round 5's refactor into align_residuals() changed the speed
+    of the CPU baseline (2.3x slower, fixed) and must not change its outputs."""
+    import json
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_align_gn_r04 as G
+    with open(G.FIXTURE) as f:
+        want = json.load(f)["outputs"]
+    got, _ = G.run(None, G.scene_inputs())
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        assert g["n_visible"] == w["n_visible"] > 100
+        assert g["iters"] == w["iters"]
+        for k in ("q", "t", "H"):
+            assert np.array_equal(np.float32(g[k]), np.float32(w[k])), k
+        assert np.float32(g["chi2"]) == np.float32(w["chi2"])
