@@ -106,7 +106,7 @@ public:
     }
 
     // The device copy of a host pyramid (levels[l]: .data / .cols / .rows / .step).
-    // An indexed level-0 pointer is a hit (exact: the pool holds the buffer); a buffer
+    // An indexed level-0 pointer whose fingerprint still agrees is a hit; a buffer
     // seen for the first time is matched to an entry with the same fingerprint by one
     // full compare of level 0 against that entry's held pixels, else uploaded (one DMA).
     template <class MatVec>
@@ -119,12 +119,15 @@ public:
         const uint8_t *key = levels[0].data;
         const size_t stride = (size_t)levels[0].step[0];
         std::lock_guard<std::mutex> lk(mu_);
+        const uint64_t fp = fingerprint(key, w, h, stride);
         auto ip = by_ptr_.find(key);
         if (ip != by_ptr_.end()) {
+            // a held buffer cannot be freed, but cv::Mat::create / copyTo of the same size
+            // rewrites it in place: the pointer hit stands only while the fingerprint agrees
             Entry *e = ip->second;
-            if (e->w == w && e->h == h && e->nlevels == nl) return touch(e)->f;
+            if (e->w == w && e->h == h && e->nlevels == nl && (!e->has_fp || e->fp == fp)) return touch(e)->f;
+            release(e, key);  // rewritten: no longer this entry's pixels
         }
-        const uint64_t fp = fingerprint(key, w, h, stride);
         auto range = by_fp_.equal_range(fp);
         for (auto it = range.first; it != range.second; ++it) {
             Entry *e = it->second;

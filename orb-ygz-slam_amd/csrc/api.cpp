@@ -290,8 +290,8 @@ struct ygzfe_extractor {
     // SearchLocalPointsDirect staging: one packed H2D, one packed D2H per call
     DevBuf direct_dev;
     HostBuf direct_hin, direct_hout;
-    // single-frame latency path: side streams (blur, FAST levels >= 1, octree
-    // classes after the first) forked from / joined to `stream`, pinned staging,
+    // single-frame latency path: side streams (side[0] the blur, side[1] the octree
+    // classes after the first under YGZFE_OCT_FORK) forked from / joined to `stream`, pinned staging,
     // the packed extraction result (one D2H) and the SparseImgAlign buffers
     hipStream_t side[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
@@ -308,6 +308,17 @@ struct ygzfe_extractor {
     bool align_pending = false;
     bool graph_broken = false;  // stream capture failed once: plain launches
     std::mutex mu;
+    // -1 when neither `stream` nor a side stream is in a capture, else the first that is
+    // (0: stream, 1..3: side[0..2])
+    int capture_left_open() const {
+        const hipStream_t all[4] = {stream, side[0], side[1], side[2]};
+        for (int i = 0; i < 4; i++) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            if (all[i] && (hipStreamIsCapturing(all[i], &cs) != hipSuccess || cs != hipStreamCaptureStatusNone))
+                return i;
+        }
+        return -1;
+    }
     int ensure_side() {
         if (side[0]) return YGZFE_OK;
         for (int i = 0; i < 3; i++) {
@@ -799,6 +810,9 @@ int ygzfe_frame_set_levels(ygzfe_frame *f, int first, int count, const uint8_t *
     YGZ_TRY(ensure_device(ex->device));
     std::lock_guard<std::mutex> lk(ex->mu);
     if (ex->align_pending) YGZ_HIP(hipEventSynchronize(ex->ev_align_done));  // an alignment reading this pyramid
+    // no DMA may still target the staging (an earlier call that returned on an error
+    // between its async copy and its synchronisation), as in ygzfe_frame_set_level
+    YGZ_HIP(hipStreamSynchronize(ex->stream));
     YGZ_TRY(ex->hlvl.ensure(bytes));
     for (int i = 0; i < count; i++) {
         const LevelDesc &L = P.lv[first + i];
@@ -856,11 +870,12 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
     const uint8_t *pyr = f->pyr.as<uint8_t>();
     int total = 0;
     if (method == YGZFE_ORBSLAM_KEYPOINT) {
-        // The single-frame DAG (one Tracking thread's latency): blur on side[0]
-        // beside FAST level 0 (st) and FAST levels >= 1 (side[1], side[2]); the
-        // octree's node-pool classes concurrent (side[1..2]); keypoint rows,
-        // angle + rBRIEF after the join; one packing kernel, one D2H into pinned
-        // memory, one synchronisation.
+        // The single-frame DAG (one Tracking thread's latency): the blur on side[0]
+        // beside FAST (st); the octree on st (its node-pool classes in sequence, or with
+        // YGZFE_OCT_FORK the classes after the first on side[1]); keypoint rows, angle +
+        // rBRIEF after the blur's join; one packing kernel, one D2H into pinned memory,
+        // one synchronisation.  Every stream forked here is joined back into st before
+        // the capture ends (checked after every capture).
         YGZ_TRY(ex->ensure_side());
         // The rows, descriptors, count and octree-overflow flag are written straight
         // into one result buffer -- [count, flag, 0, 0][rows x 28 B keypoints]
@@ -887,22 +902,25 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
         const size_t copy = desc ? 16 + kbytes + (size_t)32 * cap_rows : 16 + sizeof(ygzfe_kp) * (size_t)cap_rows;
         hipStream_t *sd = ex->side;
         // the DAG: blur on side[0] beside FAST (every level in one launch; its first
-        // lane also clears the overflow flag) on st; the octree's node-pool classes on st / side[1] / side[2];
-        // rows + jobs, then angle + rBRIEF after the blur joins; the D2H
+        // lane also clears the overflow flag) on st; the octree; rows + jobs, then
+        // angle + rBRIEF after the blur joins; the D2H.  Only side[0] waits on ev_fork:
+        // round 5 forked all three side streams here and joined only side[0], and a
+        // capture of that crashed inside hipGraphLaunch (profiles/r05_graph_fork.txt).
+        static const bool oct_fork = getenv("YGZFE_OCT_FORK") != nullptr;
         auto enqueue = [&]() -> int {
             YGZ_HIP(hipEventRecord(ex->ev_fork, st));
-            for (int i = 0; i < 3; i++) YGZ_HIP(hipStreamWaitEvent(sd[i], ex->ev_fork, 0));
+            YGZ_HIP(hipStreamWaitEvent(sd[0], ex->ev_fork, 0));
             YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), 1, sd[0]));
             YGZ_HIP(hipEventRecord(ex->ev_join[0], sd[0]));
             YGZ_HIP(launch_fast_merged(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(),
                                        ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), 1, st, d_err));
-            // the node-pool classes (nfeatures > ~1000 puts level 0 in a larger class than the
-            // rest) in sequence on st: a captured graph with this second fork beside the blur's
-            // crashed inside hipGraphLaunch after a long run of other work in the process
-            // (profiles/r05_graph_fork.txt); the classes' concurrency saved little
+            // the node-pool classes (nfeatures > ~1000 puts level 0 in a larger class than
+            // the rest): in sequence on st, or forked onto side[1] (launch_octree records
+            // its own fork event after FAST and joins side[1] back before it returns)
             YGZ_HIP(launch_octree(P, pd.dp(), ws.cellbuf.as<uint32_t>(), ws.cellcnt.as<int>(), ws.candA.as<uint32_t>(),
                                   ws.candB.as<uint32_t>(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_err,
-                                  ws.octq.as<int>(), 1, st, nullptr, 0, nullptr, nullptr, true));
+                                  ws.octq.as<int>(), 1, st, oct_fork ? &sd[1] : nullptr, oct_fork ? 1 : 0,
+                                  ex->ev_oct_fork, ex->ev_oct_join, true));
             YGZ_HIP(launch_emit_kps(P, pd.dp(), ws.sel.as<uint32_t>(), ws.selcnt.as<int>(), d_nexist, d_kps, d_count,
                                     rows, ws.ojobs.as<uint2>(), 1, st));
             YGZ_HIP(hipStreamWaitEvent(st, ex->ev_join[0], 0));  // the blurred levels
@@ -932,8 +950,18 @@ int ygzfe_extract(ygzfe_extractor *ex, ygzfe_frame *f, int method, ygzfe_kp *kps
                 const int rc = ok ? enqueue() : YGZFE_EHIP;
                 hipGraph_t g = nullptr;
                 if (ok) ok = hipStreamEndCapture(st, &g) == hipSuccess && rc == YGZFE_OK && g;
-                if (ok) ok = hipGraphInstantiate(&f->gexec, g, nullptr, nullptr, 0) == hipSuccess;
                 f->graph = g;
+                // a stream still capturing after the origin's EndCapture is an unjoined fork:
+                // its next launch would land in this graph, freed by the next drop_graph()
+                const int bad = ex->capture_left_open();
+                if (bad >= 0) {
+                    f->drop_graph();
+                    ex->graph_broken = true;
+                    (void)hipGetLastError();
+                    set_error("stream %d still capturing after ygzfe_extract's capture ended", bad);
+                    return YGZFE_EHIP;
+                }
+                if (ok) ok = hipGraphInstantiate(&f->gexec, g, nullptr, nullptr, 0) == hipSuccess;
                 if (ok) {
                     memcpy(f->gkey, key, sizeof(key));
                     f->grows = rows;

@@ -261,17 +261,26 @@ def fast10_detect(img, barrier, rois, sse=True, cap=None, device=0):
     """Thirdparty/fast FAST-10 on the GPU (ygzfe_fast10_detect): fast_corner_detect_10_sse2 (sse) or
     fast_corner_detect_10 over each ROI (x0, y0, w, h) of `img` -> list of int16[n, 2] (x, y) corner
     arrays, ROI-relative and in the reference's raster order.  `cap` (corners per ROI) defaults to
-    the largest ROI's pixel count, which no ROI can exceed."""
+    1 << 16 bounded by the largest ROI's pixel count; when a ROI holds more, the call is repeated
+    once with the cap the first call's counts report (ygzfe.h: ECAP, counts = corners found)."""
     img = np.ascontiguousarray(img, np.uint8)
     H, W = img.shape
     rois = np.ascontiguousarray(rois, np.int32).reshape(-1, 4)
     n = len(rois)
-    if cap is None:
-        cap = max(1, int((rois[:, 2].clip(0) * rois[:, 3].clip(0)).max())) if n else 1
-    xy = np.zeros((max(n, 1), cap, 2), np.int16)
-    counts = np.zeros(max(n, 1), np.int32)
-    _check(lib().ygzfe_fast10_detect(device, _p(img), W, H, W, _p(rois), n, int(barrier), int(bool(sse)), _p(xy), cap,
-                                     _p(counts)), "fast10_detect")
+    area = max(1, int((rois[:, 2].clip(0) * rois[:, 3].clip(0)).max())) if n else 1
+    retry = cap is None
+    cap = min(area, 1 << 16) if cap is None else cap
+    while True:
+        xy = np.zeros((max(n, 1), cap, 2), np.int16)
+        counts = np.zeros(max(n, 1), np.int32)
+        rc = lib().ygzfe_fast10_detect(device, _p(img), W, H, W, _p(rois), n, int(barrier), int(bool(sse)), _p(xy),
+                                       cap, _p(counts))
+        if rc == ECAP and retry:
+            retry = False
+            cap = int(counts.max())
+            continue
+        _check(rc, "fast10_detect")
+        break
     return [xy[r, :counts[r]].copy() for r in range(n)]
 
 

@@ -482,6 +482,16 @@ int main(int argc, char **argv) {
               "pyramid pool: an unsampled one-pixel change gets its own device pyramid (%s), an identical copy is "
               "matched (%s), %d held host buffers for %d entries", b_ok ? "yes" : "NO", fc == fa ? "yes" : "NO",
               pool.held(), pool.size());
+        // A held level-0 buffer rewritten in place (cv::Mat::create / copyTo of the same size
+        // reuse it): the pointer is indexed, its fingerprint no longer agrees, so the new pixels
+        // are uploaded instead of the old device pyramid being returned.
+        for (int xx = 0; xx < W; xx++) A.mvImagePyramid[0].data[xx] ^= 0x5a;  // row 0: a sampled row
+        ygzfe_frame *fr = pool.find_or_upload(A.mvImagePyramid);
+        const bool rread = fr && ygzfe_frame_level(fr, 0, nullptr, nullptr, back.data(), W) == YGZFE_OK;
+        const bool r_ok = rread && std::memcmp(back.data(), A.mvImagePyramid[0].data, back.size()) == 0;
+        ygzfe_frame *fr2 = pool.find_or_upload(A.mvImagePyramid);
+        CHECK(r_ok && fr2 == fr, "pyramid pool: a held buffer rewritten in place gets the new pixels (%s), then hits "
+              "by pointer again (%s)", r_ok ? "yes" : "NO", fr2 == fr ? "yes" : "NO");
     }
 
     // DSO path: a frame with direct-tracked keypoints and no features yet (Frame.cc:335-337)

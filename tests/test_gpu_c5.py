@@ -11,7 +11,8 @@ the object bench.py times) over the whole 13,728-frame EuRoC MH01..05-length seq
   oracle's SparseImgAlign (pose within 1e-4, same visible count);
 * every 16th frame against the oracle's extraction and every 64th align pair against its
   SparseImgAlign (858 frames, 215 pairs);
-* the overlap / split / tail stream schedules (bench.py times `overlap`) equal serial;
+* the overlap / split / tail / pipe stream schedules (bench.py times `pipe` with 4 chunks by default;
+  its roofline stage times come from a separate serial pass) equal serial;
 * a world-size-1 RCCL process group ("nccl" = RCCL, device_id bound): the device-packed
   slots gathered to rank 0 with torch.distributed.gather (one batch and chunked) equal the
   local slots.
@@ -186,7 +187,7 @@ def test_c5_sampled_frames_and_pairs_vs_oracle(c5_full):
 
 @pytest.mark.parametrize("schedule,chunks", [("overlap", 1), ("split", 1), ("tail", 1), ("pipe", 2), ("pipe", 4)])
 def test_c5_schedules_equal_serial(c5_full, schedule, chunks):
-    """The stream schedules bench.py can time (the default `overlap` included) give the serial
+    """The stream schedules bench.py can time (the default `pipe` / 4 included) give the serial
     schedule's slots byte for byte: they reorder launches across streams, never the results.
     `pipe` runs chunk c + 1's extraction beside chunk c's descriptors and alignment (private
     per-chunk buffers); its align records must equal the unchunked run's too."""
