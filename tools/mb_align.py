@@ -15,6 +15,7 @@ ap.add_argument("--batch", type=int, default=1024)
 ap.add_argument("--pairs", type=int, default=0, help="pairs per launch (0 = B-1)")
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--diag", action="store_true")
+ap.add_argument("--save", default="", help="np.save the result records here")
 args = ap.parse_args()
 import ygzfe  # noqa: E402
 if args.diag:
@@ -72,6 +73,8 @@ for r in range(args.reps):
 nvis = out[:, 7].contiguous().view(torch.int32).cpu().numpy()
 print(f"pairs {P}  mean kps {counts_t.float().mean().item():.1f}  mean visible {nvis.mean():.1f}  "
       f"align ms: median {np.median(ts):.4f} min {min(ts):.4f}  ({P / np.median(ts) * 1e3:.0f} pairs/s)")
+if args.save:
+    np.save(args.save, out.cpu().numpy())
 if args.diag:
     import ctypes as C
     buf = (C.c_ulonglong * 4096)()
