@@ -84,6 +84,23 @@ def test_best2_tile_edges_and_ties(gpu, nt):
     assert np.array_equal(bi, ri) and np.array_equal(bd, rd) and np.array_equal(sd, rs)
 
 
+@pytest.mark.parametrize("nt", [8191, 8192, 8193, 9000])
+def test_best2_fused_key_boundary(gpu, nt):
+    """hamming.hip's FP4 form keeps the key in the accumulators for train sets of <= 8,192
+    rows (tile index < 256) and builds it per element above that: both sides of the switch,
+    with duplicates of a query planted at the first and last rows and across tile 255."""
+    rng = np.random.default_rng(nt)
+    q, t = rand_desc(rng, 70), rand_desc(rng, nt)
+    for r in (0, 8160, 8191 % nt, nt - 1):
+        t[r] = q[1]
+    t[8190 % nt] = q[2]
+    t[nt - 2] = q[2]
+    bi, bd, sd = gpu.ORBmatcher().best2(q, t)
+    ri, rd, rs = O.hamming_best2(q, t)
+    assert np.array_equal(bi, ri) and np.array_equal(bd, rd) and np.array_equal(sd, rs)
+    assert bi[1] == 0 and bd[1] == 0 and sd[1] == 0
+
+
 def test_best2_extreme_distances(gpu):
     """All-zero vs all-one descriptors: distances 0 and 256 (the key's full range)."""
     z, o = np.zeros((1, 32), np.uint8), np.full((1, 32), 255, np.uint8)

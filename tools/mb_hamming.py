@@ -1,7 +1,8 @@
 """Microbenchmark: batched dense Hamming best-2 (ygzfe_batch_match) alone, on synthetic descriptors.
 B frames of `--n` random 256-bit descriptors each (bound into the batch's descriptor/count buffers),
 B-1 pairs k vs k-1 per launch, timed with HIP events over `--reps` launches.  The MFMA floor printed
-beside it is 8 v_mfma_i32_32x32x32_i8 (32 cycles each) per (32 queries x 32 train rows) tile per wave."""
+beside it is 8 v_mfma_i32_32x32x32_i8 (32 cycles each) per (32 queries x 32 train rows) tile per wave
+(the i8 form's; the FP4 form issues half as many MFMAs of the same cycles, so its floor is half the printed one)."""
 import argparse
 import os
 import sys
