@@ -1168,8 +1168,17 @@ int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, voi
     YGZ_HIP(hipStreamIsCapturing(st, &cap));
     if (b->desc_pending && cap == hipStreamCaptureStatusNone) YGZ_HIP(hipStreamWaitEvent(st, b->ev_desc_done, 0));
     YGZ_HIP(hipMemsetAsync(ws.err.p, 0, 16, st));
+    // An all-area pyramid (C2: levels 1..3 exact x2 INTER_AREA) is formed by the level-0
+    // blur strips as they stream level 0 (k_blur7's fused mode: level 0 read once for both),
+    // on st before FAST; the other levels' blur then goes beside FAST.  (Timed as the
+    // pyramid stage; YGZFE_PYR_UNFUSED=1 keeps the separate pyramid pass, for A/B.)
+    static const bool unfused = getenv("YGZFE_PYR_UNFUSED") != nullptr;
+    const bool fused = !unfused && pyramid_fusable(P) > 0;
     hipEvent_t t0 = b->begin(st);
-    YGZ_HIP(launch_pyramid(pyr, P.pyr_bytes, P, pd.dp(), pd.tabs.as<int>(), n_frames, st));
+    if (fused)
+        YGZ_HIP(launch_pyramid_blur0(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), n_frames, st));
+    else
+        YGZ_HIP(launch_pyramid(pyr, P.pyr_bytes, P, pd.dp(), pd.tabs.as<int>(), n_frames, st));
     b->end(ST_PYR, t0, st);
     // the blur feeds only the descriptors: on desc_stream, beside FAST.  (Both
     // are VALU-bound; beside the octree instead, the blur slows the octree's
@@ -1181,7 +1190,10 @@ int ygzfe_batch_extract_split(ygzfe_batch *b, int n_frames, void *kp_stream, voi
         YGZ_HIP(hipStreamWaitEvent(ds, b->ev_fork, 0));
     }
     t0 = b->begin(bs);
-    YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), n_frames, bs));
+    if (fused)
+        YGZ_HIP(launch_blur_rest(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), n_frames, bs));
+    else
+        YGZ_HIP(launch_blur(pyr, ws.blur.as<uint8_t>(), P.pyr_bytes, P, pd.dp(), n_frames, bs));
     b->end(ST_BLUR, t0, bs);
     t0 = b->begin(st);
     YGZ_HIP(launch_fast(pyr, P.pyr_bytes, P, pd.dp(), pd.cells.as<CellDesc>(), ws.cellbuf.as<uint32_t>(),

@@ -327,9 +327,54 @@ struct BlurRow {
 // per 4 pixels.  Vertical taps: the row sums (<= 255 * 256, 16 bits) of
 // consecutive rows packed in pairs, three v_dot2_u32_u16 + one 24-bit
 // multiply-add per pixel.
-template <bool CV3>
+// The exact x2 INTER_AREA levels 1..K (K <= 3) of a level-0 strip, formed from the
+// strip's own rows as the blur streams them (k_blur7's fused mode, the batch path of
+// an all-area pyramid): lane l's dword holds columns x..x+3 of a row, so a row pair
+// gives its two level-1 pixels, two row pairs its level-2 pixel and four the level-3
+// pixel of the lane pair (l, l ^ 1) -- the (a + b + c + d + 2) >> 2 chain of
+// k_pyramid_area_chain, level from level.  Strips are 256 columns x kBlurRows rows
+// (multiples of 8), so every block lies inside one strip.
+struct PyrFused {
+    uint8_t *frame;   // the frame's pyramid (level 0 read by the blur, levels 1..K written here)
+    int K;            // levels to form (0: none)
+    uint32_t off[4];  // level offsets in the frame
+    uint32_t w[4];    // level widths
+    uint32_t prev;    // the previous (even) row's dword
+    uint32_t l1;      // the lane's level-1 pair of the previous odd row (low: cols 0-1, high: 2-3)
+    uint32_t l2;      // the lane's level-2 pixel of the previous level-2 row
+};
+#define YGZ_PYR_FUSED_ROW(P, raw, yy, x, store_lane, rs)                                                          \
+    do {                                                                                                          \
+        if ((yy) & 1) {                                                                                           \
+            const uint32_t a_ = __builtin_amdgcn_udot4((raw), 0x00000101u, __builtin_amdgcn_udot4((P).prev, 0x00000101u, 2u, false), false) >> 2; \
+            const uint32_t b_ = __builtin_amdgcn_udot4((raw), 0x01010000u, __builtin_amdgcn_udot4((P).prev, 0x01010000u, 2u, false), false) >> 2; \
+            if (store_lane)                                                                                       \
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(a_ | (b_ << 8)), (rs),                            \
+                    (P).off[1] + ((uint32_t)(yy) >> 1) * (P).w[1] + ((uint32_t)(x) >> 1), 0, 0);                   \
+            if ((P).K >= 2 && ((yy) & 3) == 3) {                                                                  \
+                const uint32_t l2_ = ((P).l1 & 0xFFu) + ((P).l1 >> 8) + a_ + b_ + 2u;                             \
+                const uint32_t v2_ = l2_ >> 2;                                                                    \
+                if (store_lane)                                                                                   \
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v2_, (rs),                                       \
+                        (P).off[2] + ((uint32_t)(yy) >> 2) * (P).w[2] + ((uint32_t)(x) >> 2), 0, 0);               \
+                if ((P).K >= 3 && ((yy) & 7) == 7) {                                                              \
+                    const uint32_t t_ = (P).l2 + v2_;                                                             \
+                    const uint32_t n_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t_, 0xB1, 0xF, 0xF, false); \
+                    if ((store_lane) && ((x) & 7) == 0)                                                           \
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((t_ + n_ + 2u) >> 2), (rs),                 \
+                            (P).off[3] + ((uint32_t)(yy) >> 3) * (P).w[3] + ((uint32_t)(x) >> 3), 0, 0);           \
+                }                                                                                                 \
+                (P).l2 = v2_;                                                                                     \
+            }                                                                                                     \
+            (P).l1 = a_ | (b_ << 8);                                                                              \
+        } else {                                                                                                  \
+            (P).prev = (raw);                                                                                     \
+        }                                                                                                         \
+    } while (0)
+
+template <bool CV3, bool PYR>
 __device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, int w,
-                                                   int hgt, int sx, int y0, int lane) {
+                                                   int hgt, int sx, int y0, int lane, PyrFused &pf) {
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     constexpr uint32_t k0 = 18, k1 = 34, k2 = CV3 ? 49 : 48, k3 = CV3 ? 55 : 56;
     const int x = sx + 4 * lane;
@@ -365,10 +410,18 @@ __device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ s
     const bool store_lane = x < w;
     uint32_t prv[4] = {0u, 0u, 0u, 0u};  // row sums of the previous row
     uint32_t pr[5][4];                   // pr[m]: (row n-5+m-1, row n-5+m) packed, m = 0..4
+    // the pyramid levels 1..K of this strip are written through the frame's buffer
+    const __amdgpu_buffer_rsrc_t rpyr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)pf.frame, 0, PYR ? (int)(pf.off[pf.K] + pf.w[pf.K] * (uint32_t)(hgt >> pf.K)) : 0,
+                                          0x00020000);
 #pragma unroll
     for (int r = 0; r < kBlurRows + 6; r++) {
         Row cur = buf[r % kBlurAhead];
         if (r + kBlurAhead < kBlurRows + 6) fetch(r + kBlurAhead, buf[r % kBlurAhead]);
+        if (PYR && r >= 3 && r < kBlurRows + 3 && y0 + r - 3 < hgt) {  // the strip's own rows (no reflection)
+            const int yy = y0 + r - 3;
+            YGZ_PYR_FUSED_ROW(pf, cur.a, yy, x, store_lane, rpyr);
+        }
         uint32_t am1 = (uint32_t)__builtin_amdgcn_update_dpp((int)cur.halo, (int)cur.a, 0x138, 0xF, 0xF, false);
         if (right_edge) {
             if (fix_r) cur.a = __builtin_amdgcn_perm(cur.a, am1, 0x03000102u);
@@ -422,9 +475,13 @@ __device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ s
 #else
 #define YGZ_BLUR_ATTR
 #endif
-__global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(const uint8_t *__restrict__ pyr,
+// Strips [task_begin, task_end) of the blur tiles (level order).  pyr_k > 0 (the batch
+// path of an all-area pyramid, level-0 strips only): the strips also form pyramid
+// levels 1..pyr_k (PyrFused), so the pyramid's own pass is not run.
+__global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(uint8_t *__restrict__ pyr,
                                                uint8_t *__restrict__ blur, uint32_t pitch,
-                                               const Plan *__restrict__ plan) {
+                                               const Plan *__restrict__ plan, int task_begin, int task_end,
+                                               int pyr_k) {
 #ifndef YGZ_BLUR_SWZ
 #define YGZ_BLUR_SWZ 1
 #endif
@@ -436,8 +493,8 @@ __global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(const uint8_t *__re
     const int lane = threadIdx.x & 63;
     // wave-uniform strip index (readfirstlane: row indices, reflections and row
     // base addresses then live in SGPRs)
-    int task = __builtin_amdgcn_readfirstlane(bx * 4 + (threadIdx.x >> 6)), l = 0;
-    if (task >= plan->blur_tiles) return;
+    int task = __builtin_amdgcn_readfirstlane(task_begin + bx * 4 + (threadIdx.x >> 6)), l = 0;
+    if (task >= task_end) return;
     while (l + 1 < plan->nlevels && task >= plan->lv[l + 1].blur_tile_begin) l++;
     const LevelDesc &L = plan->lv[l];
     task -= L.blur_tile_begin;
@@ -450,10 +507,21 @@ __global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(const uint8_t *__re
     const uint32_t k0 = 18, k1 = 34, k2 = cv3 ? 49 : 48, k3 = cv3 ? 55 : 56;
     const int kk[7] = {(int)k0, (int)k1, (int)k2, (int)k3, (int)k2, (int)k1, (int)k0};
     if (w >= 16 && (w & 3) == 0) {
-        if (cv3)
-            blur_strip_aligned<true>(src, dst, w, hgt, sx, y0, lane);
-        else
-            blur_strip_aligned<false>(src, dst, w, hgt, sx, y0, lane);
+        PyrFused pf;
+        pf.frame = pyr + (size_t)f * pitch;
+        pf.K = l == 0 ? pyr_k : 0;
+        pf.prev = pf.l1 = pf.l2 = 0u;
+        for (int k = 0; k < 4; k++) {
+            pf.off[k] = k <= pf.K ? plan->lv[k].off : 0u;
+            pf.w[k] = k <= pf.K ? (uint32_t)plan->lv[k].w : 0u;
+        }
+        if (pf.K > 0) {
+            if (cv3) blur_strip_aligned<true, true>(src, dst, w, hgt, sx, y0, lane, pf);
+            else blur_strip_aligned<false, true>(src, dst, w, hgt, sx, y0, lane, pf);
+        } else {
+            if (cv3) blur_strip_aligned<true, false>(src, dst, w, hgt, sx, y0, lane, pf);
+            else blur_strip_aligned<false, false>(src, dst, w, hgt, sx, y0, lane, pf);
+        }
         return;
     }
     if (w >= 16) {
@@ -2410,7 +2478,35 @@ hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Pl
 
 hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
                        int nframes, hipStream_t st) {
-    hipLaunchKernelGGL(k_blur7, dim3((hp.blur_tiles + 3) / 4, nframes), dim3(256), 0, st, pyr, blur, pitch, dp);
+    hipLaunchKernelGGL(k_blur7, dim3((hp.blur_tiles + 3) / 4, nframes), dim3(256), 0, st, const_cast<uint8_t *>(pyr),
+                       blur, pitch, dp, 0, hp.blur_tiles, 0);
+    return hipGetLastError();
+}
+
+// Levels 1..K of an all-area pyramid (every level >= 1 an exact x2 INTER_AREA, K <= 3)
+// whose level 0 takes the aligned blur path: 0 when the plan does not qualify.
+int pyramid_fusable(const Plan &hp) {
+    const int K = hp.nlevels - 1;
+    if (K < 1 || K > 3 || hp.lv[0].w < 16 || (hp.lv[0].w & 3) || kBlurRows % 8) return 0;
+    for (int l = 1; l <= K; l++)
+        if (hp.lv[l].resize_mode != 1) return 0;
+    return K;
+}
+
+// The batch path's pyramid + level-0 blur in one pass (k_blur7 fused mode), then the
+// blur of levels >= 1 on `st_rest` after it (caller orders st_rest after st_l0)
+hipError_t launch_pyramid_blur0(uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
+                                int nframes, hipStream_t st_l0) {
+    const int K = pyramid_fusable(hp), n0 = hp.lv[0].blur_tiles_x * hp.lv[0].blur_tiles_y;
+    hipLaunchKernelGGL(k_blur7, dim3((n0 + 3) / 4, nframes), dim3(256), 0, st_l0, pyr, blur, pitch, dp, 0, n0, K);
+    return hipGetLastError();
+}
+hipError_t launch_blur_rest(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
+                            int nframes, hipStream_t st) {
+    const int n0 = hp.lv[0].blur_tiles_x * hp.lv[0].blur_tiles_y, n = hp.blur_tiles - n0;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_blur7, dim3((n + 3) / 4, nframes), dim3(256), 0, st, const_cast<uint8_t *>(pyr), blur, pitch,
+                       dp, n0, hp.blur_tiles, 0);
     return hipGetLastError();
 }
 

@@ -9,6 +9,12 @@ hipError_t upload_pattern(const int *pat);
 hipError_t run_arith_guard(uint32_t host_fails[2]);  // extract.hip k_arith_guard
 hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const int *dtabs,
                           int nframes, hipStream_t st);
+// the batch path of an all-area pyramid: levels 1..K formed by the level-0 blur strips
+int pyramid_fusable(const Plan &hp);
+hipError_t launch_pyramid_blur0(uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
+                                int nframes, hipStream_t st_l0);
+hipError_t launch_blur_rest(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
+                            int nframes, hipStream_t st);
 hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
                        int nframes, hipStream_t st);
 hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const CellDesc *dcells,

@@ -188,6 +188,33 @@ def test_batch_blur_every_pixel(gpu, size, cfg, blur):
                 raise AssertionError(f"frame {i} level {l} {lv.shape}: {len(bad)} px differ, first {bad[:5].tolist()}")
 
 
+@pytest.mark.parametrize("W,H,nl", [(752, 480, 4), (1280, 720, 4), (776, 488, 4), (752, 480, 3), (752, 480, 2)])
+def test_batch_fused_area_pyramid(gpu, W, H, nl):
+    """An all-area pyramid (scale 2.0: every level an exact x2 INTER_AREA) is formed in the
+    batch path by the level-0 blur strips (k_blur7's fused mode, K = nl - 1 levels), the
+    separate pyramid pass skipped: every level and every blurred level of every frame equal
+    the oracle's (ORBextractor.cc:1129-1150, 1079-1084), widths whose last strip is short
+    (776: 8 columns) and heights whose last strip is (720, 488) included; keypoints and
+    descriptors too."""
+    frames = np.stack([S.frame(s, W, H) for s in (21, 22, 23)])
+    b = gpu.Batch((1000, 2.0, nl, 20, 7, 0), 0, W, H, 4)
+    b.upload(frames)
+    b.extract(len(frames))
+    b.check()
+    orc = O.OrbOracle(1000, 2.0, nl, 20, 7)
+    for i in range(len(frames)):
+        lv = orc.pyramid(frames[i])
+        for l in range(nl):
+            got = b.read_level(i, l)
+            assert np.array_equal(got, lv[l]), f"frame {i} level {l}: {np.count_nonzero(got != lv[l])} px differ"
+            bl = b.read_level(i, l, blurred=True)
+            assert np.array_equal(bl, O.blur7(lv[l], 0)), f"frame {i} blurred level {l}"
+        kg, dg = b.result(i)
+        kr, dr = orc.extract(lv)
+        assert_kps_equal(kg, kr, f"frame {i}")
+        assert np.array_equal(dg, dr)
+
+
 @pytest.mark.parametrize("cfg", ["C2", "C4"])
 @pytest.mark.parametrize("kind", ["uniform", "checker"])
 def test_dense_noise_frames_capacity(gpu, cfg, kind):
