@@ -255,9 +255,14 @@ def main():
     ncells_tot = int(sum(plan["ncells"]))
     # algorithmic bytes per launch (per step, F frames): each intermediate crosses
     # HBM once written and once read
+    # With the all-area pyramid of C2 the batch path forms levels 1..3 in the level-0 blur
+    # strips (extract.hip k_blur7 fused mode): its "pyramid" stage reads level 0 once and
+    # writes levels 1..3 and the blurred level 0; "blur7" is the other levels' blur.
+    fused = os.environ.get("YGZFE_PYR_UNFUSED") is None and sf == 2.0 and nl <= 4 and W % 4 == 0
     alg = {
-        "pyramid": F_ext * sum(areas[l - 1] + areas[l] for l in range(1, nl)),
-        "blur7": F_ext * 2 * sum(areas),
+        "pyramid": F_ext * (2 * areas[0] + sum(areas[1:])) if fused else
+        F_ext * sum(areas[l - 1] + areas[l] for l in range(1, nl)),
+        "blur7": F_ext * 2 * sum(areas[1:] if fused else areas),
         "fast9_cells": F_ext * sum(a for a, c in zip(areas, plan["ncells"]) if c > 0) + 4 * int(cand.sum())
         + 4 * F_ext * ncells_tot,
         "octree": 4 * int(cand.sum()) + 4 * F_ext * ncells_tot + 4 * int(selk.sum()),
