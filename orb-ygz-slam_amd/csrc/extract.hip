@@ -681,6 +681,14 @@ __device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
 __host__ __device__ constexpr int fast_slice_bytes(int S, int R) {
     return (S * R + S * R + 2 * (S - 6) * (R - 6) + 15) / 16 * 16;
 }
+// The loads of the last YGZ_FAST_ROWS_ROI row groups are predicated on the ROI's rows (rh):
+// rows past the ROI but inside the tile's R were fetched for nothing (level 0: 40-row tiles
+// for 38-row ROIs).  FAST alone, counter traffic / algorithmic bytes: 1.46x with none, 1.38x
+// with the last group, 1.36x with the last two, 1.35x with every group (+1.5 % time; the
+// others within noise): profiles/r06/fast_rows_roi.txt
+#ifndef YGZ_FAST_ROWS_ROI
+#define YGZ_FAST_ROWS_ROI 2
+#endif
 template <int S, int R>
 struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI height)
     static constexpr int DW = S / 4, RPI = 64 / DW, NI = (R + RPI - 1) / RPI;
@@ -697,7 +705,7 @@ struct RoiStage {  // S: LDS row stride (>= ROI width), R: row capacity (>= ROI 
         for (int k = 0; k < NI; k++) {
             const uint32_t o = (f0 + (uint32_t)(k * RPI) * (uint32_t)w) & ~3u;
             lo[k] = hi[k] = 0u;
-            if (stored(k, rlane)) {  // (a load used only under the store's condition is sunk past the others' waits)
+            if (stored(k, rlane) && (k + YGZ_FAST_ROWS_ROI < NI || k * RPI + rlane < rh)) {  // (a load used only under the store's condition is sunk past the others' waits)
                 lo[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0);
                 hi[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4u, 0, 0);
             }

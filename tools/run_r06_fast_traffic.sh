@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-r06_fast_traffic}
 mkdir -p $O
 R="rocprofv3 --output-format csv --kernel-include-regex k_fast_"
-for lib in libygzfe.so libygzfe_f0.so; do
+for lib in libygzfe.so ${LIBS:-libygzfe_f0.so}; do
 B="python3 tools/mb_fast.py --child 1024 $PWD/orb-ygz-slam_amd/lib/$lib"
 YGZ_MB_STAGES=0 timeout -s KILL 120 $R --pmc FETCH_SIZE -d $O/$lib/fetch -o run -- $B > $O/$lib.fetch.log 2>&1
 YGZ_MB_STAGES=0 timeout -s KILL 120 $R --pmc WRITE_SIZE -d $O/$lib/write -o run -- $B > $O/$lib.write.log 2>&1
