@@ -478,6 +478,7 @@ __device__ __forceinline__ void blur_strip_aligned(const uint8_t *__restrict__ s
 // Strips [task_begin, task_end) of the blur tiles (level order).  pyr_k > 0 (the batch
 // path of an all-area pyramid, level-0 strips only): the strips also form pyramid
 // levels 1..pyr_k (PyrFused), so the pyramid's own pass is not run.
+template <bool PYR>  // PYR: the fused mode's launch (a separate kernel name for the profiles' stage split)
 __global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(uint8_t *__restrict__ pyr,
                                                uint8_t *__restrict__ blur, uint32_t pitch,
                                                const Plan *__restrict__ plan, int task_begin, int task_end,
@@ -509,7 +510,7 @@ __global__ __launch_bounds__(256) YGZ_BLUR_ATTR void k_blur7(uint8_t *__restrict
     if (w >= 16 && (w & 3) == 0) {
         PyrFused pf;
         pf.frame = pyr + (size_t)f * pitch;
-        pf.K = l == 0 ? pyr_k : 0;
+        pf.K = PYR && l == 0 ? pyr_k : 0;
         pf.prev = pf.l1 = pf.l2 = 0u;
         for (int k = 0; k < 4; k++) {
             pf.off[k] = k <= pf.K ? plan->lv[k].off : 0u;
@@ -2486,8 +2487,8 @@ hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Pl
 
 hipError_t launch_blur(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
                        int nframes, hipStream_t st) {
-    hipLaunchKernelGGL(k_blur7, dim3((hp.blur_tiles + 3) / 4, nframes), dim3(256), 0, st, const_cast<uint8_t *>(pyr),
-                       blur, pitch, dp, 0, hp.blur_tiles, 0);
+    hipLaunchKernelGGL(k_blur7<false>, dim3((hp.blur_tiles + 3) / 4, nframes), dim3(256), 0, st,
+                       const_cast<uint8_t *>(pyr), blur, pitch, dp, 0, hp.blur_tiles, 0);
     return hipGetLastError();
 }
 
@@ -2506,15 +2507,15 @@ int pyramid_fusable(const Plan &hp) {
 hipError_t launch_pyramid_blur0(uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
                                 int nframes, hipStream_t st_l0) {
     const int K = pyramid_fusable(hp), n0 = hp.lv[0].blur_tiles_x * hp.lv[0].blur_tiles_y;
-    hipLaunchKernelGGL(k_blur7, dim3((n0 + 3) / 4, nframes), dim3(256), 0, st_l0, pyr, blur, pitch, dp, 0, n0, K);
+    hipLaunchKernelGGL(k_blur7<true>, dim3((n0 + 3) / 4, nframes), dim3(256), 0, st_l0, pyr, blur, pitch, dp, 0, n0, K);
     return hipGetLastError();
 }
 hipError_t launch_blur_rest(const uint8_t *pyr, uint8_t *blur, uint32_t pitch, const Plan &hp, const Plan *dp,
                             int nframes, hipStream_t st) {
     const int n0 = hp.lv[0].blur_tiles_x * hp.lv[0].blur_tiles_y, n = hp.blur_tiles - n0;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_blur7, dim3((n + 3) / 4, nframes), dim3(256), 0, st, const_cast<uint8_t *>(pyr), blur, pitch,
-                       dp, n0, hp.blur_tiles, 0);
+    hipLaunchKernelGGL(k_blur7<false>, dim3((n + 3) / 4, nframes), dim3(256), 0, st, const_cast<uint8_t *>(pyr), blur,
+                       pitch, dp, n0, hp.blur_tiles, 0);
     return hipGetLastError();
 }
 

@@ -20,7 +20,7 @@ import os
 import re
 import sys
 
-STAGES = [("pyramid", r"k_resize_|k_pyramid"), ("blur7", r"k_blur7"), ("fast9_cells", r"k_fast_cells"),
+STAGES = [("pyramid", r"k_resize_|k_pyramid|k_blur7<true>"), ("blur7", r"k_blur7"), ("fast9_cells", r"k_fast_cells"),
           ("octree", r"k_octree"), ("orient_rbrief", r"k_orient_desc"), ("hamming_best2", r"k_hamming_best2"),
           ("sparse_align", r"k_sparse_align|k_build_align_jobs")]
 
