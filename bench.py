@@ -369,7 +369,11 @@ def main():
     # ------------------------------------------------ §8(f) rank 4: DBoW2 transform (Frame::ComputeBoW)
     bow_line = None
     if rank == 0 and world == 1 and not args.no_bow:
-        bow_line = bow_leg(S, batch, min(F, 1024), dev, stream, args.cpu_sample > 0)
+        # the descriptors of an extracted batch: with chunks that is a chunk's batch (the
+        # shard-wide `batch` then only owns the rendered level 0 and the slot packing)
+        ext = [ch for ch in chunks if ch[3] > 0] if chunks else None
+        bow_b, bow_F = (ext[0][4], ext[0][1]) if ext else (batch, F)
+        bow_line = bow_leg(S, bow_b, min(bow_F, 1024), dev, stream, args.cpu_sample > 0)
 
     # ------------------------------------------------ C4 throughput (TUM1.yaml, batched 256 frames)
     c4_line = None
@@ -666,6 +670,8 @@ def bow_leg(S, batch, B, dev, stream, with_cpu, reps=10):
     e1.record(stream)
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / reps
+    if int(nw.min().item()) <= 0:
+        raise RuntimeError("bow_leg: a frame of the batch has no BoW words (batch not extracted?)")
     _, d0 = batch.result(0)
     for _ in range(3):
         voc.transform(d0, 4)

@@ -130,3 +130,52 @@ def test_round5_repro_order_with_graphs(gpu):
     _check(ex, orc, S.frame(300, *INI[:2]), "after the repro order")
     del sh
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("cfg", ["INI", "C2"])
+def test_batch_extract_captured_in_a_graph(gpu, cfg):
+    """the batch path forks the octree's node-pool classes after the
+    first onto the batch's aux streams (api.cpp ygzfe_batch_extract_split -> launch_octree),
+    and `bench.py --graph 1` captures that path into a HIP graph.  The initialiser's 2048-node
+    level-0 class makes two launch groups, so a fork and join happen inside the capture.
+    Captured on a torch stream, replayed twice, then new frames uploaded into the same
+    buffers and replayed again; every result bit-exact against the oracle, and an eager
+    extract afterwards (it would fail on an aux stream left capturing) equal too."""
+    W, H, nf, sf, nl, ini, mn = INI if cfg == "INI" else S.CONFIGS["C2"]
+    F = 3
+    b = gpu.Batch((nf, sf, nl, ini, mn, 0), 0, W, H, F)
+    orc = O.OrbOracle(nf, sf, nl, ini, mn)
+    fa = np.stack([S.frame(400 + i, W, H) for i in range(F)])
+    fb = np.stack([S.frame(500 + i, W, H) for i in range(F)])
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    b.upload(fa)
+    torch.cuda.synchronize()
+    b.extract(F, st.cuda_stream)  # warm: plans, workspaces, lazily created streams
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    b.upload(fa)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=st):
+        b.extract(F, st.cuda_stream)
+    for frames, tag in ((fa, "a"), (fa, "a again"), (fb, "b")):
+        b.upload(frames)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        b.check()
+        for i in range(F):
+            kg, dg = b.result(i)
+            kr, dr = orc.extract(orc.pyramid(frames[i]))
+            assert_kps_equal(kg, kr, f"{cfg} replay {tag} frame {i}")
+            assert np.array_equal(dg, dr), f"{cfg} replay {tag} frame {i}"
+    b.upload(fa)
+    b.extract(F)
+    torch.cuda.synchronize()
+    b.check()
+    for i in range(F):
+        kg, dg = b.result(i)
+        kr, dr = orc.extract(orc.pyramid(fa[i]))
+        assert_kps_equal(kg, kr, f"{cfg} eager after the graph frame {i}")
+        assert np.array_equal(dg, dr)
+    del g
