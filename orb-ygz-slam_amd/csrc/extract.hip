@@ -21,6 +21,11 @@
 namespace ygzfe {
 
 __constant__ __attribute__((aligned(16))) int8_t c_pattern[1024];
+// The same pattern as FP8 (OCP E4M3, gfx950's format): every coordinate is an integer with
+// |v| <= 13, exact in E4M3 (3 mantissa bits hold every integer up to 16), so one
+// v_cvt_pk_f32_fp8 turns a point's two bytes into its (x, y) floats: half the
+// conversions of the int8 form (k_orient_desc)
+__constant__ __attribute__((aligned(16))) uint8_t c_pattern_f8[1024];
 
 #ifdef YGZ_STAMPS
 __device__ unsigned long long g_bstamps[1 << 20];
@@ -2233,7 +2238,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const int lane = threadIdx.x & 63, s = lane & 15;
     const int idx = bx * 16 + (threadIdx.x >> 4);
     uint4 cst = make_uint4(0u, 0u, 0u, 0u);
-    if (threadIdx.x < 64) cst = reinterpret_cast<const uint4 *>(c_pattern)[threadIdx.x];
+    if (threadIdx.x < 64) cst = reinterpret_cast<const uint4 *>(c_pattern_f8)[threadIdx.x];
     const int sel_total = plan->sel_total;
     uint2 job = make_uint2(kOrientNone, 0u);
     if (idx < sel_total) job = ojobs[(size_t)f * sel_total + idx];
@@ -2305,7 +2310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         angle = fast_atan2_deg((float)m01, (float)m10);
     }
     // computeOrbDescriptor (ORBextractor.cc:105-149) on the blurred level
-    int4 pat[4];  // 16 pairs x (x0, y0, x1, y1) int8 (read after the IC pass: fewer live registers there)
+    int4 pat[4];  // 16 pairs x (x0, y0, x1, y1) FP8 (read after the IC pass: fewer live registers there)
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const uint4 u = s_const[s * 4 + q];
@@ -2359,9 +2364,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             asm volatile("" : "+v"(wd[0]), "+v"(wd[1]), "+v"(wd[2]), "+v"(wd[3]));
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const float px0 = (float)(int8_t)(wd[k] & 0xFF), py0 = (float)(int8_t)((wd[k] >> 8) & 0xFF);
-                const float px1 = (float)(int8_t)((wd[k] >> 16) & 0xFF), py1 = (float)(int8_t)(wd[k] >> 24);
-                const uint32_t t0 = tap(px0, py0), t1 = tap(px1, py1);
+                const f32x2 p0 = __builtin_amdgcn_cvt_pk_f32_fp8((int)wd[k], false);  // (x0, y0)
+                const f32x2 p1 = __builtin_amdgcn_cvt_pk_f32_fp8((int)wd[k], true);   // (x1, y1)
+                const uint32_t t0 = tap(p0.x, p0.y), t1 = tap(p1.x, p1.y);
                 b |= (uint32_t)(t0 < t1) << (q * 4 + k);
             }
         }
@@ -2447,8 +2452,19 @@ hipError_t run_arith_guard(uint32_t host_fails[2]) {
 
 hipError_t upload_pattern(const int *pat) {
     int8_t p8[1024];
-    for (int i = 0; i < 1024; i++) p8[i] = (int8_t)pat[i];
-    return hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), p8, sizeof(p8));
+    uint8_t f8[1024];
+    for (int i = 0; i < 1024; i++) {
+        p8[i] = (int8_t)pat[i];
+        // OCP E4M3: sign, 4 exponent bits (bias 7), 3 mantissa bits; exact for |v| <= 16
+        const int v = pat[i], a = v < 0 ? -v : v;
+        if (a > 16) return hipErrorInvalidValue;
+        int e = 0;
+        while ((2 << e) <= a) e++;
+        f8[i] = a == 0 ? 0 : (uint8_t)((v < 0 ? 0x80 : 0) | ((e + 7) << 3) | (((a << 3) >> e) & 7));
+    }
+    hipError_t err = hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), p8, sizeof(p8));
+    if (err != hipSuccess) return err;
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_pattern_f8), f8, sizeof(f8));
 }
 
 hipError_t launch_pyramid(uint8_t *pyr, uint32_t pitch, const Plan &hp, const Plan *dp, const int *dtabs,
