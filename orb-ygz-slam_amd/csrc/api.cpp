@@ -2246,6 +2246,7 @@ struct ygzfe_vocab {
     int k = 0, L = 0, scoring = 0, weighting = 0, n_nodes = 0, n_words = 0;
     DevBuf child_ptr, slot_node, slot_desc, word_id, weight;
     DevBuf scratch;
+    HostBuf hin, hout;  // pinned staging of the single-frame calls (one DMA each way)
     hipStream_t stream = nullptr;
     std::mutex mu;
     VocabDev dev() const {
@@ -2433,7 +2434,8 @@ extern "C" int ygzfe_vocab_info(const ygzfe_vocab *v, int *k, int *L, int *scori
     return YGZFE_OK;
 }
 
-// one frame: host descriptors -> device -> transform (+ vectors) -> host
+// one frame: host descriptors -> pinned staging -> device (one DMA) -> transform (+ vectors)
+// -> one DMA of the whole result block back into pinned memory -> one synchronisation
 static int bow_one(ygzfe_vocab *v, const uint8_t *desc, int n, int levelsup, bool vectors, int32_t *word,
                    double *weight, int32_t *nid, int32_t *bow_words, double *bow_values, int *n_words,
                    int32_t *fv_nodes, int32_t *fv_features, int *n_fv) {
@@ -2443,42 +2445,50 @@ static int bow_one(ygzfe_vocab *v, const uint8_t *desc, int n, int levelsup, boo
     hipStream_t st = v->stream;
     const size_t N = (size_t)std::max(n, 1);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    // device block: descriptors | word, weight, node (transform) | BowVector words, values,
+    // FeatureVector nodes, features, the two counts (vectors); each part 256-B aligned
     const size_t o_d = 0, o_w = al(32 * N), o_v = al(o_w + 4 * N), o_n = al(o_v + 8 * N);
     const size_t o_bw = al(o_n + 4 * N), o_bv = al(o_bw + 4 * N), o_fn = al(o_bv + 8 * N), o_ff = al(o_fn + 4 * N);
     const size_t o_c = al(o_ff + 4 * N), total = al(o_c + 16);
     YGZ_TRY(v->scratch.ensure(total));
     uint8_t *d = v->scratch.as<uint8_t>();
     int *cnt = (int *)(d + o_c);
-    if (n > 0) YGZ_HIP(hipMemcpyAsync(d + o_d, desc, 32 * (size_t)n, hipMemcpyHostToDevice, st));
+    const size_t r0 = vectors ? o_bw : o_w, r1 = vectors ? o_c + 16 : o_n + 4 * N;  // the result block
+    YGZ_TRY(v->hin.ensure(32 * N));
+    YGZ_TRY(v->hout.ensure(r1 - r0));
+    if (n > 0) {
+        memcpy(v->hin.p, desc, 32 * (size_t)n);
+        YGZ_HIP(hipMemcpyAsync(d + o_d, v->hin.p, 32 * (size_t)n, hipMemcpyHostToDevice, st));
+    }
     const int nn = v->n_words > 0 ? n : 0;  // transform() returns early on an empty vocabulary
     YGZ_HIP(launch_bow_transform(v->dev(), d + o_d, 0, nullptr, nn, 1, levelsup, (int32_t *)(d + o_w),
                                  (double *)(d + o_v), (int32_t *)(d + o_n), 0, st));
+    if (vectors)
+        YGZ_HIP(launch_bow_vectors(nullptr, nn, 1, (int32_t *)(d + o_w), (double *)(d + o_v), (int32_t *)(d + o_n), 0,
+                                   v->weighting, v->scoring, (int32_t *)(d + o_bw), (double *)(d + o_bv), cnt,
+                                   (int32_t *)(d + o_fn), (int32_t *)(d + o_ff), cnt + 1, 0, st));
+    if (vectors || nn > 0) YGZ_HIP(hipMemcpyAsync(v->hout.p, d + r0, r1 - r0, hipMemcpyDeviceToHost, st));
+    YGZ_HIP(hipStreamSynchronize(st));
+    const uint8_t *h = v->hout.as<uint8_t>() - r0;  // h + o_x: part o_x of the block
     if (!vectors) {
         if (nn > 0) {
-            YGZ_HIP(hipMemcpyAsync(word, d + o_w, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
-            YGZ_HIP(hipMemcpyAsync(weight, d + o_v, 8 * (size_t)n, hipMemcpyDeviceToHost, st));
-            YGZ_HIP(hipMemcpyAsync(nid, d + o_n, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+            memcpy(word, h + o_w, 4 * (size_t)n);
+            memcpy(weight, h + o_v, 8 * (size_t)n);
+            memcpy(nid, h + o_n, 4 * (size_t)n);
         }
-        YGZ_HIP(hipStreamSynchronize(st));
         return YGZFE_OK;
     }
-    YGZ_HIP(launch_bow_vectors(nullptr, nn, 1, (int32_t *)(d + o_w), (double *)(d + o_v), (int32_t *)(d + o_n), 0,
-                               v->weighting, v->scoring, (int32_t *)(d + o_bw), (double *)(d + o_bv), cnt,
-                               (int32_t *)(d + o_fn), (int32_t *)(d + o_ff), cnt + 1, 0, st));
-    int hc[2] = {0, 0};
-    YGZ_HIP(hipMemcpyAsync(hc, cnt, 8, hipMemcpyDeviceToHost, st));
-    YGZ_HIP(hipStreamSynchronize(st));
+    const int *hc = (const int *)(h + o_c);
     *n_words = hc[0];
     *n_fv = hc[1];
     if (hc[0] > 0) {
-        YGZ_HIP(hipMemcpyAsync(bow_words, d + o_bw, 4 * (size_t)hc[0], hipMemcpyDeviceToHost, st));
-        YGZ_HIP(hipMemcpyAsync(bow_values, d + o_bv, 8 * (size_t)hc[0], hipMemcpyDeviceToHost, st));
+        memcpy(bow_words, h + o_bw, 4 * (size_t)hc[0]);
+        memcpy(bow_values, h + o_bv, 8 * (size_t)hc[0]);
     }
     if (hc[1] > 0) {
-        YGZ_HIP(hipMemcpyAsync(fv_nodes, d + o_fn, 4 * (size_t)hc[1], hipMemcpyDeviceToHost, st));
-        YGZ_HIP(hipMemcpyAsync(fv_features, d + o_ff, 4 * (size_t)hc[1], hipMemcpyDeviceToHost, st));
+        memcpy(fv_nodes, h + o_fn, 4 * (size_t)hc[1]);
+        memcpy(fv_features, h + o_ff, 4 * (size_t)hc[1]);
     }
-    YGZ_HIP(hipStreamSynchronize(st));
     return YGZFE_OK;
 }
 

@@ -191,13 +191,19 @@ __global__ __launch_bounds__(1024) void k_bow_vectors(const int *__restrict__ co
     }
     if (must) {
         if (threadIdx.x == 0) {
+            // the sum in word order, as std::map iteration does; the LDS reads of 16 values
+            // are issued together ahead of their adds (one LDS latency per 16, not per value)
             double norm = 0.0;
-            if (!l2) {
-                for (int j = 0; j < nw_total; j++) norm += fabs(s_val[j]);
-            } else {
-                for (int j = 0; j < nw_total; j++) norm += s_val[j] * s_val[j];
-                norm = sqrt(norm);
+            int j = 0;
+            for (; j + 16 <= nw_total; j += 16) {
+                double t[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) t[u] = s_val[j + u];
+#pragma unroll
+                for (int u = 0; u < 16; u++) norm += l2 ? t[u] * t[u] : fabs(t[u]);
             }
+            for (; j < nw_total; j++) norm += l2 ? s_val[j] * s_val[j] : fabs(s_val[j]);
+            if (l2) norm = sqrt(norm);
             s_norm = norm;
         }
         __syncthreads();
