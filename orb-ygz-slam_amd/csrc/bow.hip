@@ -100,6 +100,34 @@ __device__ void bow_bitonic(uint64_t *s, int P) {
         }
 }
 
+// The same sort for P <= blockDim.x (one key per thread, the usual frame): the key stays in
+// a register; stages whose partner lies in the same wave (j < 64) exchange by lane
+// shuffles with no barrier, the others through LDS (two barriers).  Same network, same
+// result as bow_bitonic.
+__device__ void bow_bitonic_reg(uint64_t *s, int P) {
+    const int t = threadIdx.x;
+    uint64_t key = t < P ? s[t] : ~0ull;
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            uint64_t b;
+            if (j >= 64) {
+                __syncthreads();  // the previous LDS stage's reads are done
+                if (t < P) s[t] = key;
+                __syncthreads();
+                b = t < P ? s[t ^ j] : ~0ull;
+            } else {
+                const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)key, j, 64);
+                const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), j, 64);
+                b = ((uint64_t)hi << 32) | lo;
+            }
+            const bool up = (t & k) == 0, lower = t < (t ^ j);
+            key = (lower == up) ? (key < b ? key : b) : (key < b ? b : key);
+        }
+    __syncthreads();
+    if (t < P) s[t] = key;
+    __syncthreads();
+}
+
 // exclusive scan of one int per thread over the workgroup (1024 threads)
 __device__ int bow_block_scan(int v, int *s_tmp, int *total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -127,6 +155,9 @@ __device__ int bow_block_scan(int v, int *s_tmp, int *total) {
     return r;
 }
 
+// Two workgroups per frame: even blocks the BowVector, odd blocks the FeatureVector (they
+// share nothing but the inputs, so the FeatureVector's sort runs beside the BowVector's
+// sort, fold and ordered norm instead of after them).
 __global__ __launch_bounds__(1024) void k_bow_vectors(const int *__restrict__ counts, int n_static,
                                                       const int32_t *__restrict__ word_in,
                                                       const double *__restrict__ weight_in,
@@ -138,26 +169,49 @@ __global__ __launch_bounds__(1024) void k_bow_vectors(const int *__restrict__ co
     __shared__ uint64_t s_key[kBowSortMax];
     __shared__ int s_tmp[17];
     __shared__ double s_norm;
-    const int f = blockIdx.x;
+    const int f = blockIdx.x >> 1;
+    const bool feature_vector = blockIdx.x & 1;
     const int n = counts ? counts[f] : n_static;
     const int32_t *wi = word_in + (size_t)f * in_pitch;
     const double *wv = weight_in + (size_t)f * in_pitch;
     const int32_t *ni = nid_in + (size_t)f * in_pitch;
-    int32_t *bw = bow_words + (size_t)f * out_pitch;
-    double *bv = bow_values + (size_t)f * out_pitch;
-    int32_t *fn = fv_nodes + (size_t)f * out_pitch;
-    int32_t *ff = fv_feats + (size_t)f * out_pitch;
     int P = 1;
     while (P < n) P <<= 1;
+    if (feature_vector) {
+        // FeatureVector: (node, feature) in map order, of the features that are not stopped
+        int32_t *fn = fv_nodes + (size_t)f * out_pitch;
+        int32_t *ff = fv_feats + (size_t)f * out_pitch;
+        int m = 0;
+        for (int t = threadIdx.x; t < P; t += blockDim.x) {
+            const bool ok = t < n && wv[t] > 0;
+            m += ok;
+            s_key[t] = ok ? (((uint64_t)(uint32_t)ni[t] << 32) | (uint32_t)t) : ~0ull;
+        }
+        int m_total;
+        (void)bow_block_scan(m, s_tmp, &m_total);
+        if (P <= (int)blockDim.x) bow_bitonic_reg(s_key, P);
+        else bow_bitonic(s_key, P);
+        for (int j = threadIdx.x; j < m_total; j += blockDim.x) {
+            fn[j] = (int32_t)(s_key[j] >> 32);
+            ff[j] = (int32_t)(uint32_t)s_key[j];
+        }
+        if (threadIdx.x == 0) n_fv[f] = m_total;
+        return;
+    }
+    int32_t *bw = bow_words + (size_t)f * out_pitch;
+    double *bv = bow_values + (size_t)f * out_pitch;
     // (word, feature) keys of the features that are not stopped (weight > 0)
     for (int t = threadIdx.x; t < P; t += blockDim.x)
         s_key[t] = (t < n && wv[t] > 0) ? (((uint64_t)(uint32_t)wi[t] << 32) | (uint32_t)t) : ~0ull;
     __syncthreads();
-    bow_bitonic(s_key, P);
+    if (P <= (int)blockDim.x) bow_bitonic_reg(s_key, P);
+    else bow_bitonic(s_key, P);
     const bool tf = weighting == 0 || weighting == 1;  // TF_IDF, TF
     const bool must = scoring != 5;                     // all but DOT_PRODUCT
     const bool l2 = scoring == 1;
-    // run heads -> output positions (each thread owns a contiguous chunk)
+    // run heads -> output positions (each thread owns a contiguous chunk of at most
+    // kBowSortMax / 1024 keys; their folded values are kept in registers)
+    constexpr int kMaxChunk = (kBowSortMax + 1023) / 1024;
     const int chunk = (P + blockDim.x - 1) / blockDim.x;
     const int t0 = threadIdx.x * chunk;
     int heads = 0;
@@ -166,7 +220,9 @@ __global__ __launch_bounds__(1024) void k_bow_vectors(const int *__restrict__ co
         if (k != ~0ull && (j == 0 || (s_key[j - 1] >> 32) != (k >> 32))) heads++;
     }
     int nw_total;
-    int pos = bow_block_scan(heads, s_tmp, &nw_total);
+    const int pos0 = bow_block_scan(heads, s_tmp, &nw_total);
+    double vals[kMaxChunk];
+    int pos = pos0, h = 0;
     for (int j = t0; j < t0 + chunk && j < P; j++) {
         const uint64_t k = s_key[j];
         if (k == ~0ull || (j > 0 && (s_key[j - 1] >> 32) == (k >> 32))) continue;
@@ -175,20 +231,20 @@ __global__ __launch_bounds__(1024) void k_bow_vectors(const int *__restrict__ co
         if (tf)
             for (int r = j + 1; r < P && s_key[r] != ~0ull && (s_key[r] >> 32) == (k >> 32); r++) v += w;
         bw[pos] = (int32_t)(k >> 32);
-        bv[pos] = v;
+#pragma unroll
+        for (int u = 0; u < kMaxChunk; u++)
+            if (u == h) vals[u] = v;
+        h++;
         pos++;
     }
-    __threadfence_block();
-    __syncthreads();
-    // the values into LDS (over the sorted keys, no longer read): the norm's ordered sum
-    // (one thread, the reference's order) then reads LDS instead of global memory
+    __syncthreads();  // every key read: the values go into the sorted keys' LDS
+    // the values in LDS (over the keys, no longer read): the norm's ordered sum (one thread,
+    // the reference's order) and the scaling read LDS, not global memory
     double *s_val = reinterpret_cast<double *>(s_key);
-    for (int j = threadIdx.x; j < nw_total; j += blockDim.x) s_val[j] = bv[j];
+#pragma unroll
+    for (int u = 0; u < kMaxChunk; u++)
+        if (u < h) s_val[pos0 + u] = vals[u];
     __syncthreads();
-    if (tf && !must) {
-        const double nd = (double)nw_total;
-        for (int j = threadIdx.x; j < nw_total; j += blockDim.x) bv[j] = s_val[j] / nd;
-    }
     if (must) {
         if (threadIdx.x == 0) {
             // the sum in word order, as std::map iteration does; the LDS reads of 16 values
@@ -208,28 +264,12 @@ __global__ __launch_bounds__(1024) void k_bow_vectors(const int *__restrict__ co
         }
         __syncthreads();
         const double norm = s_norm;
-        if (norm > 0.0)
-            for (int j = threadIdx.x; j < nw_total; j += blockDim.x) bv[j] = s_val[j] / norm;
+        for (int j = threadIdx.x; j < nw_total; j += blockDim.x) bv[j] = norm > 0.0 ? s_val[j] / norm : s_val[j];
+    } else {
+        const double nd = (double)nw_total;  // DOT_PRODUCT: TF / TF_IDF values divided by v.size()
+        for (int j = threadIdx.x; j < nw_total; j += blockDim.x) bv[j] = tf ? s_val[j] / nd : s_val[j];
     }
-    __syncthreads();
-    // FeatureVector: (node, feature) in map order
-    int m = 0;
-    for (int t = threadIdx.x; t < P; t += blockDim.x) {
-        const bool ok = t < n && wv[t] > 0;
-        m += ok;
-        s_key[t] = ok ? (((uint64_t)(uint32_t)ni[t] << 32) | (uint32_t)t) : ~0ull;
-    }
-    int m_total;
-    (void)bow_block_scan(m, s_tmp, &m_total);
-    bow_bitonic(s_key, P);
-    for (int j = threadIdx.x; j < m_total; j += blockDim.x) {
-        fn[j] = (int32_t)(s_key[j] >> 32);
-        ff[j] = (int32_t)(uint32_t)s_key[j];
-    }
-    if (threadIdx.x == 0) {
-        n_words[f] = nw_total;
-        n_fv[f] = m_total;
-    }
+    if (threadIdx.x == 0) n_words[f] = nw_total;
 }
 
 hipError_t launch_bow_vectors(const int *counts, int n_static, int n_frames, const int32_t *word, const double *weight,
@@ -237,7 +277,7 @@ hipError_t launch_bow_vectors(const int *counts, int n_static, int n_frames, con
                               double *bow_values, int *n_words, int32_t *fv_nodes, int32_t *fv_feats, int *n_fv,
                               size_t out_pitch, hipStream_t st) {
     if (n_frames <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_bow_vectors, dim3(n_frames), dim3(1024), 0, st, counts, n_static, word, weight, nid, in_pitch,
+    hipLaunchKernelGGL(k_bow_vectors, dim3(2 * n_frames), dim3(1024), 0, st, counts, n_static, word, weight, nid, in_pitch,
                        weighting, scoring, bow_words, bow_values, n_words, fv_nodes, fv_feats, n_fv, out_pitch);
     return hipGetLastError();
 }

@@ -623,21 +623,29 @@ int main(int argc, char **argv) {
         std::vector<ygzo_mquery> q;
         std::vector<uint8_t> qd;
         std::vector<int> src;
-        for (int i = 0; i < L.N; i++) {
-            MapPoint *pMP = L.mvpMapPoints[i];
-            if (!pMP || L.mvbOutlier[i]) continue;
-            const Vector3f x3Dc = Rcw * pMP->GetWorldPos() + tcw;
-            const float invzc = 1.0 / x3Dc[2];
-            if (invzc < 0) continue;
-            const float u = C.fx * x3Dc[0] * invzc + C.cx, v = C.fy * x3Dc[1] * invzc + C.cy;
-            if (u < C.mnMinX || u > C.mnMaxX || v < C.mnMinY || v > C.mnMaxY) continue;
-            const int oc = L.mvKeys[i].octave;
-            ygzo_mquery Q{u, v, 15 * C.mvScaleFactors[oc], u - C.mbf * invzc, oc - 1, oc + 1, L.mvKeys[i].angle,
-                          YGZO_MQ_VALID | YGZO_MQ_STEREO | (pMP->Observations() > 0 ? YGZO_MQ_BLOCKS : 0)};
-            q.push_back(Q);
-            qd.insert(qd.end(), pMP->mDescriptor.data, pMP->mDescriptor.data + 32);
-            src.push_back(i);
-        }
+        // the reference's per-point projection and window set-up (ORBmatcher.cc:1241-1280),
+        // timed with the oracle's search below as the reference runs them, in one loop
+        auto build_last = [&] {
+            q.clear();
+            qd.clear();
+            src.clear();
+            for (int i = 0; i < L.N; i++) {
+                MapPoint *pMP = L.mvpMapPoints[i];
+                if (!pMP || L.mvbOutlier[i]) continue;
+                const Vector3f x3Dc = Rcw * pMP->GetWorldPos() + tcw;
+                const float invzc = 1.0 / x3Dc[2];
+                if (invzc < 0) continue;
+                const float u = C.fx * x3Dc[0] * invzc + C.cx, v = C.fy * x3Dc[1] * invzc + C.cy;
+                if (u < C.mnMinX || u > C.mnMaxX || v < C.mnMinY || v > C.mnMaxY) continue;
+                const int oc = L.mvKeys[i].octave;
+                ygzo_mquery Q{u, v, 15 * C.mvScaleFactors[oc], u - C.mbf * invzc, oc - 1, oc + 1, L.mvKeys[i].angle,
+                              YGZO_MQ_VALID | YGZO_MQ_STEREO | (pMP->Observations() > 0 ? YGZO_MQ_BLOCKS : 0)};
+                q.push_back(Q);
+                qd.insert(qd.end(), pMP->mDescriptor.data, pMP->mDescriptor.data + 32);
+                src.push_back(i);
+            }
+        };
+        build_last();
         std::vector<int32_t> want(C.N);
         std::vector<uint8_t> blocked(C.N, 0);
         const ygzo_mframe mf = mframe(C, true);
@@ -657,6 +665,7 @@ int main(int argc, char **argv) {
                 T.MotionModel(15);
             });
             const double c = median_ms(50, [&] {
+                build_last();
                 ygzo_search_projection_best(&mf, q.data(), qd.data(), (int)q.size(), blocked.data(), 100, 1,
                                             want.data());
             });
@@ -719,6 +728,7 @@ int main(int argc, char **argv) {
             const double c = median_ms(10, [&] {
                 ygzo_compute_pyramid(&o, im1.data, W, H, W, lp);
                 ygzo_extract_orbslam(&o, lp, lw, lh, nullptr, 0, okf.data(), odf.data(), 4096);
+                build_last();
                 ygzo_search_projection_best(&mfc, q.data(), qd.data(), (int)q.size(), blocked.data(), 100, 1,
                                             want.data());
             });
@@ -746,15 +756,21 @@ int main(int argc, char **argv) {
         }
         std::vector<ygzo_mquery> q;
         std::vector<uint8_t> qd;
-        for (MapPoint *pMP : T.mvpLocalMapPoints) {
-            const float r = (pMP->mTrackViewCos > 0.998 ? 2.5f : 4.0f) * 3.0f;
-            const int lvl = pMP->mnTrackScaleLevel;
-            ygzo_mquery Q{pMP->mTrackProjX, pMP->mTrackProjY, r * C.mvScaleFactors[lvl], pMP->mTrackProjXR, -1, -1,
-                          0.f, (pMP->mbTrackInView && !pMP->isBad() ? YGZO_MQ_VALID : 0) | YGZO_MQ_STEREO |
-                                   (pMP->Observations() > 0 ? YGZO_MQ_BLOCKS : 0)};
-            q.push_back(Q);
-            qd.insert(qd.end(), pMP->mDescriptor.data, pMP->mDescriptor.data + 32);
-        }
+        // the reference's per-point window set-up (ORBmatcher.cc:55-80), timed with the search
+        auto build_local = [&] {
+            q.clear();
+            qd.clear();
+            for (MapPoint *pMP : T.mvpLocalMapPoints) {
+                const float r = (pMP->mTrackViewCos > 0.998 ? 2.5f : 4.0f) * 3.0f;
+                const int lvl = pMP->mnTrackScaleLevel;
+                ygzo_mquery Q{pMP->mTrackProjX, pMP->mTrackProjY, r * C.mvScaleFactors[lvl], pMP->mTrackProjXR, -1, -1,
+                              0.f, (pMP->mbTrackInView && !pMP->isBad() ? YGZO_MQ_VALID : 0) | YGZO_MQ_STEREO |
+                                       (pMP->Observations() > 0 ? YGZO_MQ_BLOCKS : 0)};
+                q.push_back(Q);
+                qd.insert(qd.end(), pMP->mDescriptor.data, pMP->mDescriptor.data + 32);
+            }
+        };
+        build_local();
         std::vector<int32_t> want(C.N);
         const ygzo_mframe mf = mframe(C, true);
         const int wn = ygzo_search_projection_ratio(&mf, q.data(), qd.data(), (int)q.size(), nullptr, 0.8f, want.data());
@@ -769,6 +785,7 @@ int main(int argc, char **argv) {
                 T.LocalPoints(3);
             });
             const double c = median_ms(50, [&] {
+                build_local();
                 ygzo_search_projection_ratio(&mf, q.data(), qd.data(), (int)q.size(), nullptr, 0.8f, want.data());
             });
             std::printf("TIMING search_by_projection_local_map dropin_ms %.4f oracle_ms %.4f queries %zu\n", g, c,
