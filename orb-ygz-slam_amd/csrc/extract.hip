@@ -902,7 +902,12 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                 uint32_t sg[2];
                 fast_screen4_sg(Tw, Bw, D0, Rw, C, yin ? tc01 : (kFastNoTh * 0x10001u), yin ? tc23 : (kFastNoTh * 0x10001u),
                                 sg);
-                const bool b0 = (short)sg[0] < 0, b1 = (short)sg[1] < 0;
+                // the low halves' signs as 32-bit signs: one v_cmp each, shared by the ballot and
+                // the list write's exec mask (a 16-bit sign test compiles to two compares, one per
+                // use; the opaque shift keeps it a 32-bit compare)
+                uint32_t lo0 = sg[0] << 16, lo1 = sg[1] << 16;
+                asm("" : "+v"(lo0), "+v"(lo1));
+                const bool b0 = (int)lo0 < 0, b1 = (int)lo1 < 0;
                 const bool b2 = (int)sg[0] < 0, b3 = (int)sg[1] < 0;
                 const uint64_t M0 = __ballot(b0), M1 = __ballot(b1), M2 = __ballot(b2), M3 = __ballot(b3);
                 // survivors in lanes below: one mbcnt chain (each step adds to the last)
@@ -914,13 +919,13 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                 pc = __builtin_amdgcn_mbcnt_hi((uint32_t)(M2 >> 32), pc);
                 pc = __builtin_amdgcn_mbcnt_lo((uint32_t)M3, pc);
                 pc = __builtin_amdgcn_mbcnt_hi((uint32_t)(M3 >> 32), pc);
-                int pos = (int)pc;
                 na += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
                 const uint32_t e = fast_entry<S>((uint32_t)(y + 3), (uint32_t)(4 * j + 3));
-                if (b0) list[pos++] = (uint16_t)e;
-                if (b1) list[pos++] = (uint16_t)(e + 1u);
-                if (b2) list[pos++] = (uint16_t)(e + 2u);
-                if (b3) list[pos] = (uint16_t)(e + 3u);
+                uint16_t *lp = list + pc;  // this lane's next list slot
+                if (b0) *lp++ = (uint16_t)e;
+                if (b1) *lp++ = (uint16_t)(e + 1u);
+                if (b2) *lp++ = (uint16_t)(e + 2u);
+                if (b3) *lp = (uint16_t)(e + 3u);
             }
 #else
             uint32_t colmask = 0;
