@@ -888,17 +888,22 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
             const uint32_t thv = (uint32_t)th;
             const uint32_t tc01 = (4 * j + 0 < iw ? thv : kFastNoTh) | ((4 * j + 2 < iw ? thv : kFastNoTh) << 16);
             const uint32_t tc23 = (4 * j + 1 < iw ? thv : kFastNoTh) | ((4 * j + 3 < iw ? thv : kFastNoTh) << 16);
-            for (int y0 = 0; y0 < ih; y0 += rpc) {
+            // a row chunk of the interior; `full`: every row of the chunk is inside it (all but
+            // the last chunk when rpc does not divide ih), so no per-row threshold select
+            const uint32_t lane_off = (uint32_t)(rr * S + 4 * j);  // the lane's dword in a chunk's first row
+            auto chunk = [&](int y0, bool full) {
                 const int y = y0 + rr;
-                const uint32_t *rt = reinterpret_cast<const uint32_t *>(img + y * S) + j;
-                const uint32_t *rc = reinterpret_cast<const uint32_t *>(img + (y + 3) * S) + j;
-                const uint32_t *rb = reinterpret_cast<const uint32_t *>(img + (y + 6) * S) + j;
+                // row addresses: the wave-uniform y0 S (SALU) plus the lane's offset
+                const uint32_t o = (uint32_t)(y0 * S) + lane_off;
+                const uint32_t *rt = reinterpret_cast<const uint32_t *>(img + o);
+                const uint32_t *rc = reinterpret_cast<const uint32_t *>(img + o + 3 * S);
+                const uint32_t *rb = reinterpret_cast<const uint32_t *>(img + o + 6 * S);
                 const uint32_t D0 = rc[0], D1 = rc[1], D2 = rc[2];
                 const uint32_t C = __builtin_amdgcn_alignbyte(D1, D0, 3);   // x .. x+3
                 const uint32_t Rw = __builtin_amdgcn_alignbyte(D2, D1, 2);  // x+3 .. x+6
                 const uint32_t Tw = __builtin_amdgcn_alignbyte(rt[1], rt[0], 3);
                 const uint32_t Bw = __builtin_amdgcn_alignbyte(rb[1], rb[0], 3);
-                const bool yin = y < ih;
+                const bool yin = full || y < ih;
                 uint32_t sg[2];
                 fast_screen4_sg(Tw, Bw, D0, Rw, C, yin ? tc01 : (kFastNoTh * 0x10001u), yin ? tc23 : (kFastNoTh * 0x10001u),
                                 sg);
@@ -920,13 +925,16 @@ __device__ __forceinline__ void fast_cell_item(const Plan *__restrict__ plan, co
                 pc = __builtin_amdgcn_mbcnt_lo((uint32_t)M3, pc);
                 pc = __builtin_amdgcn_mbcnt_hi((uint32_t)(M3 >> 32), pc);
                 na += __popcll(M0) + __popcll(M1) + __popcll(M2) + __popcll(M3);
-                const uint32_t e = fast_entry<S>((uint32_t)(y + 3), (uint32_t)(4 * j + 3));
+                const uint32_t e = o + (uint32_t)(3 * S + 3);  // fast_entry<S>(y + 3, 4 j + 3)
                 uint16_t *lp = list + pc;  // this lane's next list slot
                 if (b0) *lp++ = (uint16_t)e;
                 if (b1) *lp++ = (uint16_t)(e + 1u);
                 if (b2) *lp++ = (uint16_t)(e + 2u);
                 if (b3) *lp = (uint16_t)(e + 3u);
-            }
+            };
+            int y0 = 0;
+            for (; y0 + rpc <= ih; y0 += rpc) chunk(y0, true);
+            if (y0 < ih) chunk(y0, false);
 #else
             uint32_t colmask = 0;
 #pragma unroll

@@ -1,6 +1,6 @@
 #!/bin/bash
-# FAST phase A: the low halves' signs as one shared 32-bit compare each, list writes through a
-# lane pointer (libygzfe.so) against the previous build (libygzfe_base.so): parity, stage alone, bench A/B
+# FAST phase A A/B: libygzfe.so (working tree) against libygzfe_base.so (HEAD): parity, stage alone, bench A/B
+# (r06_fast_cmp: shared sign compares + lane-pointer list writes; r06_fast_chunk: full chunks without the row test, incremental row addresses)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-r06_fast_cmp}
