@@ -53,6 +53,23 @@ def test_compute_bow_bitexact(gpu, scoring, weighting):
         assert abs((np.abs(bv).sum() if scoring != 1 else np.sqrt((bv ** 2).sum())) - 1.0) < 1e-12
 
 
+@pytest.mark.parametrize("n_random,scoring", [(0, 0), (73, 1), (74, 0), (3000, 0), (3000, 1), (7000, 5)])
+def test_compute_bow_sizes(gpu, n_random, scoring):
+    """k_bow_vectors across its sort paths: <= 1,024 features (one key per thread, the
+    register bitonic network), 1,025 and more (the LDS network, several keys and folded
+    values per thread, up to 8 per thread at 8,192 slots); L1, L2 and DOT_PRODUCT.  The
+    frame has 934 keypoints + 17 repeats, so n_random 73 / 74 make 1,024 / 1,025 features."""
+    k, L = 10, 4
+    parent, is_leaf, desc, weight = V.synth_vocab(9, k, L)
+    voc = gpu.Vocabulary.from_arrays(k, L, scoring, 0, parent, is_leaf, desc, weight)
+    ovoc = O.Vocab(k, L, scoring, 0, parent, is_leaf, desc, weight)
+    f = _features(gpu, 5, n_random)
+    (bw, bv), (fn, ff) = voc.transform(f, 4)
+    (obw, obv), (ofn, off) = ovoc.transform(f, 4)
+    assert np.array_equal(bw, obw) and np.array_equal(bv, obv), len(f)
+    assert np.array_equal(fn, ofn) and np.array_equal(ff, off), len(f)
+
+
 def test_vocab_file_loaders(gpu, tmp_path):
     k, L = 10, 3
     parent, is_leaf, desc, weight = V.synth_vocab(11, k, L)
