@@ -2569,11 +2569,14 @@ hipError_t launch_fast(const uint8_t *pyr, uint32_t pitch, const Plan &hp, const
         // level 0 on the caller's stream, the others spread over the given side streams
         const hipStream_t st = (l == 0 || !lvl_streams || n_lvl_streams <= 0) ? st0
                                                                                 : lvl_streams[(l - 1) % n_lvl_streams];
-        // LDS floor per workgroup: caps the small-ROI levels at 7 workgroups/CU (7 waves/SIMD)
-        // instead of 8, leaving slots to the other chunk's stages under the overlap schedule.
-        // Measured (r05 A/B, C5 overlap): floor 0 471k fps, 23000 485k, 26800 482k, 32000 463k.
+        // Optional LDS floor per workgroup (a floor of 23,000 B caps the small-ROI levels at 7
+        // workgroups/CU instead of 8, leaving slots to the other chunk's stages).  Round 5 under
+        // the overlap schedule: floor 0 471k fps, 23000 485k, 26800 482k, 32000 463k.  Round 6
+        // under the pipe schedule with this round's FAST: floor 0 runs FAST 1.5 % faster (7.00-7.09
+        // vs 7.12-7.20 ms per step) and the headline within noise (+0.35 %), so no floor
+        // (profiles/r06/lds_floor/).
 #ifndef YGZ_FAST_LDS_MIN
-#define YGZ_FAST_LDS_MIN 23000
+#define YGZ_FAST_LDS_MIN 0
 #endif
         const size_t lds = std::max<size_t>(kFastWaves * (size_t)fast_slice_bytes(S, R), YGZ_FAST_LDS_MIN);
         const dim3 grid((L.ncells + kFastWaves - 1) / kFastWaves, nframes);
