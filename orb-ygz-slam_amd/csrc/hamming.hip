@@ -174,7 +174,9 @@ __device__ __forceinline__ void hamming_block_mfma(const uint8_t *__restrict__ q
 #if YGZ_HAM_FP4
 #pragma unroll
         for (int s = 0; s < 4; s++) {
-            const uint32_t d = h ? w[2 * s + 1] : w[2 * s];  // bits 64 s + 32 h .. + 31
+            // bits 64 s + 32 h .. + 31, selected arithmetically (a select on h compiled to an
+            // indexed access of w through scratch)
+            const uint32_t d = w[2 * s] ^ ((w[2 * s] ^ w[2 * s + 1]) & (0u - (uint32_t)h));
 #pragma unroll
             for (int m = 0; m < 4; m++) bq[g][s][m] = (int)((spread8(d >> (8 * m)) << 3) | 0x22222222u);  // +1 / -1
         }
