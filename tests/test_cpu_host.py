@@ -112,3 +112,34 @@ def test_compat_adapter_builds_and_fails_loudly_without_gpu(ygzfe):
         pytest.skip("a GPU is visible: tests/test_gpu_compat.py runs the demo")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "no HIP device" in r.stdout
+
+
+def _e4m3_encode(v):
+    """extract.hip upload_pattern's OCP E4M3 encoding of an integer |v| <= 16."""
+    a = abs(v)
+    if a == 0:
+        return 0
+    e = 0
+    while (2 << e) <= a:
+        e += 1
+    return (0x80 if v < 0 else 0) | ((e + 7) << 3) | (((a << 3) >> e) & 7)
+
+
+def _e4m3_decode(b):
+    if b & 0x7F == 0:
+        return 0.0
+    s = -1.0 if b & 0x80 else 1.0
+    return s * (1 + (b & 7) / 8) * 2.0 ** (((b >> 3) & 15) - 7)
+
+
+def test_pattern_fp8_exact():
+    """k_orient_desc reads the rBRIEF pattern as FP8 (E4M3) point pairs and converts them with
+    v_cvt_pk_f32_fp8: every coordinate of the ORB pattern (ORBextractor.cc:152-410,
+    include/ygzfe_pattern.inc) must be an integer that E4M3 holds exactly."""
+    txt = open(os.path.join(ROOT, "include", "ygzfe_pattern.inc")).read()
+    body = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    vals = [int(x) for x in re.findall(r"-?\d+", body)]
+    assert len(vals) == 1024
+    assert max(abs(v) for v in vals) <= 16
+    for v in set(vals):
+        assert _e4m3_decode(_e4m3_encode(v)) == float(v), v
