@@ -1020,9 +1020,15 @@ static void fast_slice_shape(int rw, int rh, int &S, int &R) {
     R = std::max(40, ((rh + 7) / 8) * 8);
 }
 
-// One wave per (cell, frame), four per workgroup: the cell's ROI staged into the
+// One wave per (cell, frame), kFastWaves per workgroup: the cell's ROI staged into the
 // wave's LDS slice, then fast_cell_item.
-constexpr int kFastWaves = 4;
+// Waves (cells) per workgroup: 2.  Under the pipe schedule the smaller workgroups interleave
+// with the other chunk's stages: headline +1.2 % over 4 waves in six alternating pass pairs (FAST
+// alone ~0.7 % slower); 8 waves measured 6 % slower (profiles/r06/fast_waves/)
+#ifndef YGZ_FAST_WAVES
+#define YGZ_FAST_WAVES 2
+#endif
+constexpr int kFastWaves = YGZ_FAST_WAVES;
 template <int S, int R>
 __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu(6))) void k_fast_cells(
     const uint8_t *__restrict__ pyr, uint32_t pitch, const Plan *__restrict__ plan,
@@ -1032,7 +1038,7 @@ __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu
     constexpr int slice = fast_slice_bytes(S, R);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     // Block order (a traffic / speed choice; results never depend on it): runs of 4
-    // consecutive blocks (16 neighbouring cells) per XCD (block b runs on XCD b % 8), so
+    // consecutive blocks (4 kFastWaves neighbouring cells) per XCD (block b runs on XCD b % 8), so
     // neighbouring cells' ROI halos come from one L2: HBM reads 1.29x the levels' bytes
     // instead of 2.07x in plain order, for +1 % time; whole frames per XCD read 0.87x but
     // ran 13 % slower (round 3)
