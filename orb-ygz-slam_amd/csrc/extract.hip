@@ -1037,14 +1037,22 @@ __global__ __launch_bounds__(64 * kFastWaves) __attribute__((amdgpu_waves_per_eu
     extern __shared__ uint8_t s_dyn[];
     constexpr int slice = fast_slice_bytes(S, R);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    // Block order (a traffic / speed choice; results never depend on it): runs of 4
-    // consecutive blocks (4 kFastWaves neighbouring cells) per XCD (block b runs on XCD b % 8), so
+    // Block order (a traffic / speed choice; results never depend on it): runs of kRun
+    // consecutive blocks (16 neighbouring cells) per XCD (block b runs on XCD b % 8), so
     // neighbouring cells' ROI halos come from one L2: HBM reads 1.29x the levels' bytes
     // instead of 2.07x in plain order, for +1 % time; whole frames per XCD read 0.87x but
     // ran 13 % slower (round 3)
+    // Runs of kRun blocks = YGZ_FAST_RUN_CELLS cells whatever the workgroup size.  FAST alone
+    // (1,024 C2 frames, 2-wave workgroups), counter traffic / algorithmic bytes and time: 8-cell
+    // runs 1.59x / 0.548 ms, 16 cells 1.36x / 0.554 ms, 32 cells 1.16x / 0.534 ms; the headline
+    // the same within noise (profiles/r06/fast_runs/)
+#ifndef YGZ_FAST_RUN_CELLS
+#define YGZ_FAST_RUN_CELLS 32
+#endif
+    constexpr int kRun = YGZ_FAST_RUN_CELLS / kFastWaves, kGroup = 8 * kRun;
     const int orig = blockIdx.x + gridDim.x * blockIdx.y, nwg = gridDim.x * gridDim.y;
-    int lid = ((orig >> 5) << 5) + ((orig & 7) << 2) + ((orig >> 3) & 3);
-    if ((orig | 31) >= nwg) lid = orig;  // the ragged tail keeps the plain order
+    int lid = (orig / kGroup) * kGroup + (orig % 8) * kRun + (orig / 8) % kRun;
+    if ((orig | (kGroup - 1)) >= nwg) lid = orig;  // the ragged tail keeps the plain order
     const int bx = lid % gridDim.x, f = lid / gridDim.x;
     const int c = cell_begin + bx * kFastWaves + wave;
     if (clear_flag && c == cell_begin && f == 0 && lane == 0) *clear_flag = 0;
